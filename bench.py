@@ -1,0 +1,326 @@
+#!/usr/bin/env python3
+"""bench.py -- quorum commit decisions/s (+ LogEntry CRC64 GB/s) on 1..8 MI355X.
+
+Driver contract: `python bench.py --gpus N --steps K --warmup W`; N>1 is launched by
+torch.distributed.run (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from env).
+Rank 0 prints ONE JSON line.
+
+Headline (`value`): quorum commit decisions/s, whole job.  Workload per GPU = 1M Raft
+groups x 5 peers with joint-consensus masks (BASELINE config C3 at N=1; at N>1 config
+C4: 8M groups sharded by contiguous groupId blocks, 1M per GPU, weak scaling).  One
+step = one quorum epoch kernel over the GPU's groups; at N>1 the step also publishes
+the node-wide committed-index snapshot with an RCCL all-gather over xGMI.  Inputs are
+device-resident; the step cycles through several distinct epochs (> the 256 MiB
+Infinity Cache) so every launch reads its inputs from HBM.
+
+Also measured in the same run (extra fields): LogEntry CRC64 verify GB/s on C5
+(64k x 16 KiB entries per GPU), the C2 config (10k groups x 3 peers), HIP-event
+kernel times -> `roofline`, and the oracle (Java-faithful C restatement) timed on
+this host -> `cpu_baseline`.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sofa-jraft_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+QUORUM_EPOCH_BUFFERS = 6
+
+
+def quorum_bytes_per_group(P: int) -> int:
+    # reads: match 8P, pendingIndex 8, lastAppended 8, lastCommitted 8, conf 8;
+    # writes: committed 8, status 1  
+    return 8 * P + 41
+
+
+def crc_bytes(n_entries: int, payload_bytes: int, verify: bool = True) -> int:
+    # payload + offsets (N+1)*8 + per entry type 1, index 8, term 8, out 8 (+ expected 8, corrupt 1)
+    b = payload_bytes + 8 * (n_entries + 1) + n_entries * (1 + 8 + 8 + 8)
+    if verify:
+        b += n_entries * (8 + 1)
+    return b
+
+
+def to_dev(arr, dev):
+    import torch
+    if arr is None:
+        return None
+    a = arr.view(np.int64) if arr.dtype == np.uint64 else arr
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def timed_launches(fn, steps, warmup, stream, sync):
+    """warmup untimed, then `steps` launches each bracketed by HIP events on `stream`."""
+    import torch
+    for _ in range(warmup):
+        fn()
+    sync()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        evs[i][0].record(stream)
+        fn(i)
+        evs[i][1].record(stream)
+    sync()
+    wall = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    return wall, kern_ms
+
+
+def cpu_quorum_baseline(budget_s: float):
+    """Oracle (Java-faithful BallotBox replay, oracle/jraft_oracle.c) on C3 groups, 1 thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import jraft_oracle as O
+    from jraft_amd import workloads as W
+    done, t_used, grants = 0, 0.0, 0
+    chunk_groups = 256
+    off = 0
+    while t_used < budget_s and done < (1 << 20):
+        b = W.quorum_batch("C3", groups=chunk_groups, group_offset=off)
+        t0 = time.perf_counter()
+        _, _, g = O.quorum_epoch_replay(b["match"], b["pending_index"], b["last_appended"],
+                                        b["last_committed"], b["conf"], chunk=1024)
+        t_used += time.perf_counter() - t0
+        grants += g
+        done += chunk_groups
+        off += chunk_groups
+    return dict(value=done / t_used, unit="decisions/s", cores=1, kind="port",
+                sample=f"{done} C3 groups (1k pending, 5 peers, joint) replayed through the "
+                       f"Java-faithful BallotBox restatement, {grants} Ballot.grant calls, "
+                       f"{t_used:.1f} s, 1 thread")
+
+
+def cpu_crc_baseline(budget_s: float):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import jraft_oracle as O
+    from jraft_amd import workloads as W
+    n = 2048  # 32 MiB of C5 entries per round
+    b = W.entry_batch(n, 16 << 10, seed=5)
+    t_used, rounds = 0.0, 0
+    while t_used < budget_s:
+        t0 = time.perf_counter()
+        O.logentry_checksum_batch(b["etype"], b["index"], b["term"], None, b["payload"],
+                                  b["offsets"])
+        t_used += time.perf_counter() - t0
+        rounds += 1
+    gb = rounds * n * (16 << 10) / 1e9
+    return dict(value=gb / t_used, unit="GB/s", cores=1, kind="port",
+                sample=f"{rounds * n} C5 LogEntries x 16 KiB ({gb:.2f} GB) through the byte-at-a-time "
+                       f"CRC64.update restatement, {t_used:.1f} s, 1 thread")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--groups-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU baseline leg")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-crc", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from jraft_amd import Engine
+    from jraft_amd import workloads as W
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    eng = Engine(local)
+    stream = torch.cuda.current_stream(dev)
+    eng.use_stream(stream.cuda_stream)
+
+    def sync():
+        torch.cuda.synchronize(dev)
+
+    # ------------------------------------------------ quorum (headline) -----
+    G = args.groups_per_gpu
+    cfg = "C3" if world == 1 else "C4"
+    P = W.CONFIGS[cfg]["peers"]
+    epochs = []
+    for e in range(QUORUM_EPOCH_BUFFERS):
+        b = W.quorum_batch(cfg, groups=G, group_offset=rank * G,
+                           seed=(W.SEED_BASE ^ int(cfg[1])) + 7919 * e)
+        epochs.append({k: to_dev(v, dev) for k, v in b.items()})
+    committed = torch.empty(G, dtype=torch.int64, device=dev)
+    status = torch.empty(G, dtype=torch.uint8, device=dev)
+    snapshot = torch.empty(G * world, dtype=torch.int64, device=dev) if world > 1 else None
+    if world > 1:
+        uid = [Engine.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.rccl_init(world, rank, uid[0])
+
+    state = {"i": 0}
+
+    def quorum_step(i=None):
+        t = epochs[state["i"] % QUORUM_EPOCH_BUFFERS]
+        state["i"] += 1
+        eng.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
+                             t["last_committed"], t["conf"], committed, status)
+
+    def full_step(i=None):
+        quorum_step(i)
+        if world > 1:
+            eng.publish_committed_dev(committed, snapshot)
+
+    # kernel-only timing (HIP events around each launch)
+    _, kern_ms = timed_launches(quorum_step, args.steps, args.warmup, stream, sync)
+    # the contract's timed region: K steps between barrier+sync on both sides
+    for _ in range(args.warmup):
+        full_step()
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        full_step()
+    sync()
+    barrier()
+    sync()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    decisions = G * world * args.steps
+    value = decisions / elapsed
+    k_avg_ms = float(np.mean(kern_ms))
+    q_bytes = quorum_bytes_per_group(P) * G
+    achieved = q_bytes / (k_avg_ms * 1e-3) / 1e9
+
+    # ------------------------------------------------ C2 (configs[1]) -------
+    c2 = W.quorum_batch("C2")
+    c2d = {k: to_dev(v, dev) for k, v in c2.items()}
+    G2 = c2["pending_index"].shape[0]
+    c2c = torch.empty(G2, dtype=torch.int64, device=dev)
+    c2s = torch.empty(G2, dtype=torch.uint8, device=dev)
+
+    def c2_step(i=None):
+        eng.quorum_epoch_dev(c2d["match"], c2d["pending_index"], c2d["last_appended"],
+                             c2d["last_committed"], c2d["conf"], c2c, c2s)
+
+    c2_wall, c2_ms = timed_launches(c2_step, args.steps, args.warmup, stream, sync)
+
+    # ------------------------------------------------ CRC64 (C5) ------------
+    crc = None
+    if not args.no_crc:
+        c5 = W.CONFIGS["C5"]
+        n = c5["groups"]
+        eb = W.entry_batch(n, c5["entry_bytes"], seed=W.SEED_BASE ^ 5 ^ rank)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        expected = None
+        if rank == 0 and not args.no_cpu:
+            import jraft_oracle as O
+            expected = O.logentry_checksum_batch(eb["etype"], eb["index"], eb["term"], None,
+                                                 eb["payload"], eb["offsets"])
+        if expected is None:
+            expected = np.zeros(n, np.uint64)
+        flip = np.zeros(n, bool)
+        flip[::1024] = True  # 1/1024 entries corrupted
+        expected_c = expected ^ flip.astype(np.uint64)
+        d = {k: to_dev(v, dev) for k, v in eb.items() if isinstance(v, np.ndarray)}
+        d_exp = to_dev(expected_c, dev)
+        out = torch.empty(n, dtype=torch.int64, device=dev)
+        corrupt = torch.empty(n, dtype=torch.uint8, device=dev)
+
+        def crc_step(i=None):
+            eng.logentry_checksum_batch_dev(d["etype"], d["index"], d["term"], None, d["payload"],
+                                            d["offsets"], out, expected=d_exp, corrupt=corrupt)
+
+        _, crc_ms = timed_launches(crc_step, max(5, args.steps // 5), 2, stream, sync)
+        barrier()
+        crc_avg = float(np.mean(crc_ms))
+        crc_ms_max = max_over_ranks(crc_avg)
+        pay = n * c5["entry_bytes"]
+        ok = None
+        if rank == 0 and not args.no_cpu:
+            got = out.cpu().numpy().view(np.uint64)
+            ok = bool(np.array_equal(got, expected)) and \
+                bool(np.array_equal(corrupt.cpu().numpy().astype(bool), flip))
+        alg = crc_bytes(n, pay, verify=True)
+        crc = {
+            "metric": "LogEntry CRC64 verify GB/s",
+            "value": pay * world / (crc_ms_max * 1e-3) / 1e9, "unit": "GB/s (payload)",
+            "workload": "C5: 64k x 16 KiB DATA LogEntries per GPU, checksum + isCorrupted verify",
+            "ms_per_launch": crc_avg,
+            "bit_exact_vs_oracle": ok,
+            "roofline": {"bound": "hbm", "achieved": alg / (crc_avg * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": alg / (crc_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None},
+        }
+
+    # ------------------------------------------------ CPU baselines ---------
+    cpu_q = cpu_c = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu_q = cpu_quorum_baseline(args.cpu_budget)
+        if not args.no_crc:
+            cpu_c = cpu_crc_baseline(args.cpu_budget)
+        if crc is not None and cpu_c is not None:
+            crc["cpu_baseline"] = cpu_c
+
+    if rank == 0:
+        line = {
+            "metric": "quorum commit decisions/sec",
+            "value": value,
+            "unit": "decisions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (seeded splitmix64, SURVEY.md §8d)",
+            "config": {
+                "workload": ("C3: 1M Raft groups x 5 peers, joint consensus (old 3 + new 5), "
+                             "1k pending/group" if world == 1 else
+                             f"C4: {G * world} Raft groups x 5 peers sharded by groupId, "
+                             f"{G} per GPU, + RCCL all-gather of committed[]"),
+                "groups_per_gpu": G, "peers": P, "epoch_buffers": QUORUM_EPOCH_BUFFERS,
+                "parallelism": f"groupId shards x{world}",
+            },
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                         "kernel": "quorum_epoch_kernel<5>", "kernel_ms": k_avg_ms,
+                         "bytes_per_launch": q_bytes},
+            "cpu_baseline": cpu_q,
+            "crc64": crc,
+            "C2": {"workload": "C2: 10k groups x 3 peers x 1k pending (configs[1])",
+                   "decisions_per_s": G2 * args.steps / c2_wall,
+                   "kernel_ms": float(np.mean(c2_ms))},
+        }
+        print(json.dumps(line))
+    eng.use_stream(None)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,185 @@
+/*
+ * jrq.h -- C ABI of libjrq.so, the MI355X-native batched quorum + CRC64 engine
+ * that takes over SOFAJRaft's data-parallel hot path.
+ *
+ * The reference has no plug-in point for this path: BallotBox is
+ * instantiated directly (NodeImpl.java:829-836) and CrcUtil is a static utility.
+ * The drop-in surface is therefore the Java class API, and this header is what a
+ * JDK 8 JNI shim behind those classes binds.  Every entry
+ * point below names the reference interface it replaces.
+ *   JC = jraft-core/src/main/java/com/alipay/sofa/jraft
+ *
+ * Conventions
+ *   - extern "C", plain pointers and sizes, no C++ or torch types.
+ *   - Return value: 0 = OK, negative = jrq_error.  Per-group outcomes go to
+ *     status_out (jrq_group_status bit flags); no exceptions cross the ABI.  The
+ *     Java shim re-throws ArrayIndexOutOfBoundsException / IllegalArgumentException
+ *     itself (its synchronous checks), so the reference's error
+ *     behaviour is preserved.
+ *   - Ownership: the caller owns every buffer; the engine never frees them.
+ *   - *_dev functions take DEVICE pointers and are asynchronous on the engine's
+ *     stream (jrq_get_stream / jrq_set_stream); the other variants take HOST
+ *     pointers, stage through device memory and return after synchronising.
+ *   - Threading: one engine per host thread; calls on one handle are not
+ *     re-entrant.  Different handles may run concurrently.
+ */
+#ifndef JRQ_H
+#define JRQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JRQ_ABI_VERSION 1
+#define JRQ_MAX_PEERS 16 /* peer slots per group (16-bit masks) */
+
+typedef struct jrq_engine jrq_engine;
+
+typedef enum {
+    JRQ_OK = 0,
+    JRQ_E_INVALID = -1,     /* bad argument (null pointer, size, peer count ...) */
+    JRQ_E_NOMEM = -2,       /* device or host allocation failed */
+    JRQ_E_HIP = -3,         /* a HIP runtime call failed (jrq_last_error for text) */
+    JRQ_E_RCCL = -4,        /* an RCCL call failed */
+    JRQ_E_NODEV = -5,       /* no usable gfx950 device */
+    JRQ_E_STATE = -6        /* call not valid in the engine's state (e.g. no communicator) */
+} jrq_error;
+
+/* Per-group status flags (uint8 per group).  Mirrors the reference outcomes:
+ *   NOT_LEADER   pendingIndex == 0: BallotBox.commitAt returns false (JC/core/BallotBox.java:101-103)
+ *   OUT_OF_RANGE a peer's match exceeds lastAppended: that ack would throw
+ *                ArrayIndexOutOfBoundsException (:107-109) and is ignored
+ *   EMPTY_CONF   a pending run has an empty conf: its ballots can never be granted
+ *                (Ballot.init with an empty Configuration, JC/entity/Ballot.java:63-85) */
+typedef enum {
+    JRQ_ST_OK = 0,
+    JRQ_ST_NOT_LEADER = 1,
+    JRQ_ST_OUT_OF_RANGE = 2,
+    JRQ_ST_EMPTY_CONF = 4
+} jrq_group_status;
+
+/* Packed per-run configuration word (uint64):
+ *   bits  0-15  new-conf peer mask over the group's peer slots   (Ballot.peers)
+ *   bits 16-31  old-conf peer mask                               (Ballot.oldPeers)
+ *   bits 32-39  new quorum  = |conf|/2+1                          (Ballot.quorum)
+ *   bits 40-47  old quorum  = |oldConf|/2+1, or 0 if oldConf==null (Ballot.oldQuorum)
+ * Learners are never in a mask (Configuration.iterator yields peers only,
+ * JC/conf/Configuration.java:184-186).  Explicit quorums keep Ballot.init's
+ * size-based arithmetic (JC/entity/Ballot.java:77-83) for any conf list. */
+#define JRQ_CONF(newMask, oldMask, newQ, oldQ)                                                 \
+    ((uint64_t)(uint16_t)(newMask) | ((uint64_t)(uint16_t)(oldMask) << 16) |                    \
+     ((uint64_t)(uint8_t)(newQ) << 32) | ((uint64_t)(uint8_t)(oldQ) << 40))
+
+/* One epoch of a group batch, structure-of-arrays (all arrays length G unless noted).
+ * Replaces the per-call state of JC/core/BallotBox.java:50-55 for G groups at once:
+ *   match[p*match_ld + g]  highest log index peer slot p has acknowledged for group g
+ *                          (the `last` of its BallotBox.commitAt(first,last,peer) calls;
+ *                          Replicator acks are contiguous from pendingIndex, Replicator.java:
+ *                          1387-1392,1401, so one index per peer is the whole ack set)
+ *   pending_index[g]       BallotBox.pendingIndex (0 = not leader)
+ *   last_appended[g]       pendingIndex + pendingMetaQueue.size() - 1
+ *   last_committed[g]      BallotBox.lastCommittedIndex before the epoch
+ *   conf[g]                packed conf of every pending entry (used when run_off == NULL)
+ *   run_off[G+1]           optional CSR of conf runs (joint consensus, conf changes):
+ *                          runs of group g are [run_off[g], run_off[g+1]); run r covers log
+ *                          indices [run_start[r], run_start[r+1]) (the group's last run ends at
+ *                          last_appended; the first run's start is treated as <= pendingIndex);
+ *                          run_conf[r] is its packed conf.
+ */
+typedef struct {
+    const int64_t *match;
+    const int64_t *pending_index;
+    const int64_t *last_appended;
+    const int64_t *last_committed;
+    const uint64_t *conf;
+    const uint32_t *run_off;   /* nullable */
+    const int64_t *run_start;  /* [num_runs], nullable iff run_off is */
+    const uint64_t *run_conf;  /* [num_runs], nullable iff run_off is */
+    uint32_t num_peers;        /* P, 1..JRQ_MAX_PEERS */
+    uint32_t num_runs;         /* R (host variant: bytes to stage) */
+    uint64_t match_ld;         /* row stride of match in elements, >= G */
+} jrq_group_batch;
+
+/* ---------------------------------------------------------------- engine -- */
+
+/* Create an engine on HIP device `device` sized for up to max_groups groups per
+ * epoch and max_peers peer slots (host-variant staging; device variants take any G).
+ * Replaces: `new BallotBox()` per group (JC/core/NodeImpl.java:829-836) and the
+ * ThreadLocal CRC64 of CrcUtil (JC/util/CrcUtil.java:28). */
+jrq_engine *jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int *err);
+/* Replaces BallotBox.shutdown (JC/core/BallotBox.java:250-253) for the whole batch. */
+void jrq_destroy(jrq_engine *e);
+
+int jrq_abi_version(void);
+/* Text of the last error on this engine (or of jrq_create's last failure when e==NULL). */
+const char *jrq_last_error(const jrq_engine *e);
+/* hipStream_t the engine launches on (as void*); jrq_set_stream adopts an external
+ * stream (not owned).  NULL restores the engine's own stream. */
+void *jrq_get_stream(jrq_engine *e);
+int jrq_set_stream(jrq_engine *e, void *hip_stream);
+int jrq_synchronize(jrq_engine *e);
+/* Page-lock a host buffer (e.g. a DirectByteBuffer's address) for fast staging. */
+int jrq_host_register(void *ptr, size_t bytes);
+int jrq_host_unregister(void *ptr);
+
+/* ---------------------------------------------------------------- quorum -- */
+
+/* One quorum epoch for G groups: committed_out[g] = the lastCommittedIndex that
+ * BallotBox.commitAt (JC/core/BallotBox.java:96-139, Ballot.grant/isGranted
+ * JC/entity/Ballot.java:100-140) reaches after all of group g's acks of the epoch,
+ * in any order; status_out[g] = jrq_group_status flags.  committed_out may alias
+ * in->last_committed.  pendingIndex after the epoch is committed_out[g]+1 when it
+ * advanced (BallotBox.java:130-132). */
+int jrq_quorum_epoch_dev(jrq_engine *e, const jrq_group_batch *in_dev, int64_t *committed_out_dev,
+                         uint8_t *status_out_dev, uint32_t G);
+int jrq_quorum_epoch(jrq_engine *e, const jrq_group_batch *in_host, int64_t *committed_out,
+                     uint8_t *status_out, uint32_t G);
+
+/* --------------------------------------------------------------- checksum -- */
+
+/* crc_out[i] = CrcUtil.crc64(payload[offsets[i] .. offsets[i+1]))
+ * (JC/util/CrcUtil.java:36-80 -> CRC64.update JC/util/CRC64.java:100-110):
+ * CRC-64/ECMA-182, MSB first, init 0, xorout 0.  offsets has N+1 monotone entries
+ * (byte positions into payload; offsets[0] need not be 0).  Zero-length ranges give 0. */
+int jrq_crc64_batch_dev(jrq_engine *e, const uint8_t *payload_dev, const uint64_t *offsets_dev,
+                        uint32_t N, uint64_t *crc_out_dev);
+int jrq_crc64_batch(jrq_engine *e, const uint8_t *payload, const uint64_t *offsets, uint32_t N,
+                    uint64_t *crc_out);
+
+/* out[i] = LogEntry.checksum() of entry i (JC/entity/LogEntry.java:88-108):
+ *   (uint64)type[i] ^ LogId(index[i],term[i]).checksum() ^ peer_xor[i] ^ crc64(data_i)
+ * with LogId.checksum = crc64(BE64(index) || BE64(term)) (JC/entity/LogId.java:45-50) and
+ * peer_xor[i] = XOR of PeerId.checksum() over peers/oldPeers/learners/oldLearners
+ * (precomputed per conf on the host; NULL = 0 for data entries, NodeImpl.java:1201-1203).
+ * Verify mode (expected != NULL): corrupt_out[i] = LogEntry.isCorrupted()
+ * = has[i] && expected[i] != out[i] (:156-158); has == NULL means every entry has one. */
+int jrq_logentry_checksum_batch_dev(jrq_engine *e, const uint8_t *type_dev, const int64_t *index_dev,
+                                    const int64_t *term_dev, const uint64_t *peer_xor_dev,
+                                    const uint8_t *payload_dev, const uint64_t *offsets_dev,
+                                    uint32_t N, uint64_t *out_dev, const uint64_t *expected_dev,
+                                    const uint8_t *has_dev, uint8_t *corrupt_out_dev);
+int jrq_logentry_checksum_batch(jrq_engine *e, const uint8_t *type, const int64_t *index,
+                                const int64_t *term, const uint64_t *peer_xor,
+                                const uint8_t *payload, const uint64_t *offsets, uint32_t N,
+                                uint64_t *out, const uint64_t *expected, const uint8_t *has,
+                                uint8_t *corrupt_out);
+
+/* --------------------------------------------------- node-wide publication -- */
+
+/* Multi-GPU (one process per GPU): groups are sharded by contiguous groupId blocks.
+ * jrq_publish_committed_dev all-gathers each rank's int64 committed[count_per_rank]
+ * into global_dev[nranks*count_per_rank] over RCCL/xGMI, the node-wide snapshot read
+ * by getLastCommittedIndex consumers (JC/core/BallotBox.java:67-79, Replicator.java:1433).
+ * The unique id is 128 opaque bytes produced on rank 0 and shared out of band. */
+int jrq_rccl_get_unique_id(uint8_t id_out[128]);
+int jrq_rccl_init(jrq_engine *e, int nranks, int rank, const uint8_t id[128]);
+int jrq_publish_committed_dev(jrq_engine *e, const int64_t *local_dev, int64_t *global_dev,
+                              uint64_t count_per_rank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JRQ_H */

@@ -1,0 +1,379 @@
+/*
+ * jraft_oracle.c -- CPU restatement of SOFAJRaft's quorum + checksum hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see jraft_oracle.h).  Never linked into libjrq.so.
+ * Loop structure deliberately follows the Java reference (JC = jraft-core/src/
+ * main/java/com/alipay/sofa/jraft): it is both the parity oracle and the "port"
+ * CPU baseline that bench.py times.
+ */
+#include "jraft_oracle.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ======================= CRC64 (JC/util/CRC64.java) ======================= */
+
+/* CRC-64/ECMA-182, MSB first: poly=0x42f0e1eba9ea3693 init=0 refin=false
+ * refout=false xorout=0 (JC/util/CRC64.java:27-40).  Entry i is the register
+ * after shifting i<<56 through 8 polynomial steps; tests/golden pins every entry
+ * against the literal table at JC/util/CRC64.java:41-92. */
+#define JO_POLY 0x42F0E1EBA9EA3693ULL
+static uint64_t g_table[256];
+static int g_table_ready = 0;
+
+static void build_table(void) {
+    for (int i = 0; i < 256; ++i) {
+        uint64_t c = (uint64_t)i << 56;
+        for (int k = 0; k < 8; ++k) c = (c & 0x8000000000000000ULL) ? (c << 1) ^ JO_POLY : (c << 1);
+        g_table[i] = c;
+    }
+    g_table_ready = 1;
+}
+
+const uint64_t *jo_crc64_table(void) {
+    if (!g_table_ready) build_table();
+    return g_table;
+}
+
+/* CRC64.update(byte): tab_index = ((int)(crc >> 56) ^ b) & 0xFF;
+ * crc = CRC_TABLE[tab_index] ^ (crc << 8)  (JC/util/CRC64.java:100-103).
+ * Java's arithmetic >> is masked by & 0xFF, so a logical shift is equivalent. */
+uint64_t jo_crc64_update(uint64_t crc, const uint8_t *p, size_t n) {
+    const uint64_t *t = jo_crc64_table();
+    for (size_t i = 0; i < n; ++i) crc = t[((crc >> 56) ^ p[i]) & 0xFF] ^ (crc << 8);
+    return crc;
+}
+
+/* CrcUtil.crc64(byte[],off,len): ThreadLocal CRC64 -> update -> getValue -> reset
+ * (JC/util/CrcUtil.java:51-57).  A zero-length range returns 0. */
+uint64_t jo_crc64(const uint8_t *p, size_t n) { return jo_crc64_update(0, p, n); }
+
+void jo_crc64_batch(const uint8_t *payload, const uint64_t *offsets, uint32_t n, uint64_t *out) {
+    for (uint32_t i = 0; i < n; ++i)
+        out[i] = jo_crc64(payload + offsets[i], (size_t)(offsets[i + 1] - offsets[i]));
+}
+
+/* ======================= checksums (JC/entity) ============================ */
+
+/* Bits.putLong big-endian (JC/util/Bits.java:71-80). */
+static void put_long_be(uint8_t *b, int64_t v) {
+    uint64_t u = (uint64_t)v;
+    for (int k = 7; k >= 0; --k) { b[k] = (uint8_t)u; u >>= 8; }
+}
+
+/* LogId.checksum (JC/entity/LogId.java:45-50). */
+uint64_t jo_logid_checksum(int64_t index, int64_t term) {
+    uint8_t bs[16];
+    put_long_be(bs, index);
+    put_long_be(bs + 8, term);
+    return jo_crc64(bs, 16);
+}
+
+/* PeerId.checksum over AsciiStringUtil.unsafeEncode(toString()) (JC/entity/PeerId.java:60-65,
+ * 135-144; Endpoint.toString JC/util/Endpoint.java:60-65).  Characters are truncated to a byte
+ * ((byte) in.charAt(i), JC/util/AsciiStringUtil.java:27-34); C strings are already bytes. */
+uint64_t jo_peerid_checksum(const char *ip, int32_t port, int32_t idx) {
+    char s[512];
+    int n = (idx != 0) ? snprintf(s, sizeof s, "%s:%d:%d", ip, port, idx)
+                       : snprintf(s, sizeof s, "%s:%d", ip, port);
+    if (n < 0) return 0;
+    if ((size_t)n >= sizeof s) n = (int)sizeof s - 1;
+    return jo_crc64((const uint8_t *)s, (size_t)n);
+}
+
+/* LogEntry.checksum (JC/entity/LogEntry.java:88-99):
+ *   c = type.getNumber() ^ id.checksum();  c ^= peer.checksum() for each peer list;
+ *   if (data != null && data.hasRemaining()) c ^= CrcUtil.crc64(data).
+ * An empty data buffer is skipped by the reference and contributes crc64("") = 0 here:
+ * identical result. */
+uint64_t jo_logentry_checksum(int32_t type, int64_t index, int64_t term, uint64_t peer_xor,
+                              const uint8_t *data, size_t len) {
+    uint64_t c = (uint64_t)(int64_t)type ^ jo_logid_checksum(index, term);
+    c ^= peer_xor;
+    if (data != NULL && len > 0) c ^= jo_crc64(data, len);
+    return c;
+}
+
+void jo_logentry_checksum_batch(const uint8_t *type, const int64_t *index, const int64_t *term,
+                                const uint64_t *peer_xor, const uint8_t *payload,
+                                const uint64_t *offsets, uint32_t n, uint64_t *out,
+                                const uint64_t *expected, const uint8_t *has, uint8_t *corrupt) {
+    for (uint32_t i = 0; i < n; ++i) {
+        uint64_t c = jo_logentry_checksum(type[i], index[i], term[i], peer_xor ? peer_xor[i] : 0,
+                                          payload + offsets[i], (size_t)(offsets[i + 1] - offsets[i]));
+        out[i] = c;
+        /* LogEntry.isCorrupted: hasChecksum && checksum != checksum() (:156-158). */
+        if (expected && corrupt) corrupt[i] = (uint8_t)(((has == NULL) || has[i]) && expected[i] != c);
+    }
+}
+
+/* ======================= Ballot (JC/entity/Ballot.java) ==================== */
+
+static void list_init(jo_peer_list *l, const int32_t *ids, int32_t n) {
+    l->n = 0;
+    if (n > JO_MAX_CONF) {
+        fprintf(stderr, "jraft_oracle: conf larger than JO_MAX_CONF\n");
+        abort();
+    }
+    for (int32_t i = 0; i < n; ++i) {
+        l->peer[i] = ids[i];
+        l->found[i] = 0;
+    }
+    l->n = n > 0 ? n : 0;
+}
+
+/* Ballot.init (:63-85): peers from conf (learners never iterate, JC/conf/Configuration.java:184-186),
+ * quorum = size/2+1; oldQuorum = 0 when oldConf == null, else oldSize/2+1. */
+int jo_ballot_init(jo_ballot *b, const int32_t *conf, int32_t nconf, const int32_t *old, int32_t nold) {
+    list_init(&b->peers, conf, nconf);
+    list_init(&b->old_peers, old, 0);
+    b->quorum = b->old_quorum = 0;
+    b->quorum = b->peers.n / 2 + 1;
+    if (nold < 0) return 1;
+    list_init(&b->old_peers, old, nold);
+    b->old_quorum = b->old_peers.n / 2 + 1;
+    return 1;
+}
+
+/* Ballot.findPeer (:87-98): the hint slot if it holds the peer, else the first equal slot. */
+static int find_peer(const jo_peer_list *l, int32_t peer, int32_t hint) {
+    if (hint < 0 || hint >= l->n || l->peer[hint] != peer) {
+        for (int32_t i = 0; i < l->n; ++i)
+            if (l->peer[i] == peer) return i;
+        return -1;
+    }
+    return hint;
+}
+
+/* Ballot.grant(peerId, hint) (:100-127). */
+jo_pos_hint jo_ballot_grant_hint(jo_ballot *b, int32_t peer, jo_pos_hint hint) {
+    int i = find_peer(&b->peers, peer, hint.pos0);
+    if (i >= 0) {
+        if (!b->peers.found[i]) {
+            b->peers.found[i] = 1;
+            b->quorum--;
+        }
+        hint.pos0 = i;
+    } else {
+        hint.pos0 = -1;
+    }
+    if (b->old_peers.n == 0) {
+        hint.pos1 = -1;
+        return hint;
+    }
+    i = find_peer(&b->old_peers, peer, hint.pos1);
+    if (i >= 0) {
+        if (!b->old_peers.found[i]) {
+            b->old_peers.found[i] = 1;
+            b->old_quorum--;
+        }
+        hint.pos1 = i;
+    } else {
+        hint.pos1 = -1;
+    }
+    return hint;
+}
+
+void jo_ballot_grant(jo_ballot *b, int32_t peer) {
+    jo_pos_hint h = {-1, -1};
+    (void)jo_ballot_grant_hint(b, peer, h);
+}
+
+int jo_ballot_is_granted(const jo_ballot *b) { return b->quorum <= 0 && b->old_quorum <= 0; }
+
+/* ======================= BallotBox (JC/core/BallotBox.java) ================ */
+
+struct jo_ballot_box {
+    int64_t last_committed_index; /* :53 */
+    int64_t pending_index;        /* :54 */
+    /* pendingMetaQueue (:55): util.ArrayDeque is an ArrayList whose removeRange(0,k)
+     * drops the head (JC/util/ArrayDeque.java:106-109); kept here as array + head. */
+    jo_ballot *q;
+    int64_t head, tail, cap;
+    int64_t on_committed_calls, on_committed_last; /* the FSMCaller waiter */
+    int64_t grants;                                /* Ballot.grant calls executed */
+};
+
+jo_ballot_box *jo_bb_new(void) {
+    jo_ballot_box *bb = (jo_ballot_box *)calloc(1, sizeof *bb);
+    return bb;
+}
+
+void jo_bb_free(jo_ballot_box *bb) {
+    if (!bb) return;
+    free(bb->q);
+    free(bb);
+}
+
+int64_t jo_bb_last_committed_index(const jo_ballot_box *bb) { return bb->last_committed_index; }
+int64_t jo_bb_pending_index(const jo_ballot_box *bb) { return bb->pending_index; }
+int64_t jo_bb_queue_size(const jo_ballot_box *bb) { return bb->tail - bb->head; }
+int64_t jo_bb_on_committed_calls(const jo_ballot_box *bb) { return bb->on_committed_calls; }
+int64_t jo_bb_on_committed_last(const jo_ballot_box *bb) { return bb->on_committed_last; }
+
+static void on_committed(jo_ballot_box *bb, int64_t idx) {
+    bb->on_committed_calls++;
+    bb->on_committed_last = idx;
+}
+
+/* BallotBox.commitAt (:96-139). */
+int jo_bb_commit_at(jo_ballot_box *bb, int64_t first, int64_t last, int32_t peer) {
+    int64_t last_committed = 0;
+    if (bb->pending_index == 0) return JO_FALSE;
+    if (last < bb->pending_index) return JO_TRUE;
+    if (last >= bb->pending_index + (bb->tail - bb->head)) return JO_AIOOBE;
+    int64_t start_at = first > bb->pending_index ? first : bb->pending_index;
+    jo_pos_hint hint = {-1, -1};
+    for (int64_t log_index = start_at; log_index <= last; ++log_index) {
+        jo_ballot *bl = &bb->q[bb->head + (log_index - bb->pending_index)];
+        hint = jo_ballot_grant_hint(bl, peer, hint);
+        bb->grants++;
+        if (jo_ballot_is_granted(bl)) last_committed = log_index;
+    }
+    if (last_committed == 0) return JO_TRUE;
+    bb->head += (last_committed - bb->pending_index) + 1; /* removeRange(0, lc - pending + 1) */
+    bb->pending_index = last_committed + 1;
+    bb->last_committed_index = last_committed;
+    on_committed(bb, last_committed); /* after unlock in the reference */
+    return JO_TRUE;
+}
+
+/* BallotBox.clearPendingTasks (:147-156). */
+void jo_bb_clear_pending_tasks(jo_ballot_box *bb) {
+    bb->head = bb->tail = 0;
+    bb->pending_index = 0;
+}
+
+/* BallotBox.resetPendingIndex (:167-186). */
+int jo_bb_reset_pending_index(jo_ballot_box *bb, int64_t n) {
+    if (!(bb->pending_index == 0 && bb->tail == bb->head)) return JO_FALSE;
+    if (n <= bb->last_committed_index) return JO_FALSE;
+    bb->pending_index = n;
+    bb->head = bb->tail = 0;
+    return JO_TRUE;
+}
+
+/* BallotBox.appendPendingTask (:197-215). */
+int jo_bb_append_pending_task(jo_ballot_box *bb, const int32_t *conf, int32_t nconf,
+                              const int32_t *old, int32_t nold) {
+    jo_ballot bl;
+    if (!jo_ballot_init(&bl, conf, nconf, old, nold)) return JO_FALSE;
+    if (bb->pending_index <= 0) return JO_FALSE;
+    if (bb->tail == bb->cap) {
+        if (bb->head > 0) { /* compact, keeps queue order */
+            memmove(bb->q, bb->q + bb->head, (size_t)(bb->tail - bb->head) * sizeof(jo_ballot));
+            bb->tail -= bb->head;
+            bb->head = 0;
+        }
+        if (bb->tail == bb->cap) {
+            int64_t nc = bb->cap ? bb->cap * 2 : 64;
+            jo_ballot *nq = (jo_ballot *)realloc(bb->q, (size_t)nc * sizeof(jo_ballot));
+            if (!nq) abort();
+            bb->q = nq;
+            bb->cap = nc;
+        }
+    }
+    bb->q[bb->tail++] = bl;
+    return JO_TRUE;
+}
+
+/* BallotBox.setLastCommittedIndex (:223-248). */
+int jo_bb_set_last_committed_index(jo_ballot_box *bb, int64_t idx) {
+    if (bb->pending_index != 0 || bb->tail != bb->head) {
+        if (!(idx < bb->pending_index)) return JO_IAE; /* Requires.requireTrue */
+        return JO_FALSE;
+    }
+    if (idx < bb->last_committed_index) return JO_FALSE;
+    if (idx > bb->last_committed_index) {
+        bb->last_committed_index = idx;
+        on_committed(bb, idx);
+    }
+    return JO_TRUE;
+}
+
+/* ======================= epoch replay ===================================== */
+
+static int32_t mask_to_ids(uint32_t mask, int32_t *ids) {
+    int32_t n = 0;
+    for (int32_t s = 0; s < 16; ++s)
+        if (mask & (1u << s)) ids[n++] = s;
+    return n;
+}
+
+int64_t jo_quorum_epoch_replay(uint32_t G, uint32_t P, const int64_t *match, const int64_t *pending_index,
+                               const int64_t *last_appended, const int64_t *last_committed,
+                               const uint64_t *conf, const uint32_t *run_off, const int64_t *run_start,
+                               const uint64_t *run_conf, int64_t chunk, int64_t *committed_out,
+                               uint8_t *status_out) {
+    int64_t grants = 0;
+    if (chunk <= 0) chunk = 1;
+    jo_ballot_box *bb = jo_bb_new();
+    int64_t *next = (int64_t *)malloc(sizeof(int64_t) * (P ? P : 1));
+    for (uint32_t g = 0; g < G; ++g) {
+        /* fresh box seeded to the group's state: follower path sets lastCommitted,
+         * then the leader's resetPendingIndex (NodeImpl.becomeLeader). */
+        bb->head = bb->tail = 0;
+        bb->pending_index = 0;
+        bb->last_committed_index = 0;
+        bb->on_committed_calls = 0;
+        bb->grants = 0;
+        const int64_t lc0 = last_committed[g], pi = pending_index[g], la = last_appended[g];
+        uint8_t st = JO_ST_OK;
+        jo_bb_set_last_committed_index(bb, lc0);
+        if (pi == 0) {
+            committed_out[g] = lc0;
+            status_out[g] = JO_ST_NOT_LEADER;
+            continue;
+        }
+        if (jo_bb_reset_pending_index(bb, pi) != JO_TRUE) {
+            fprintf(stderr, "jraft_oracle: group %u violates pendingIndex > lastCommitted\n", g);
+            abort();
+        }
+        /* appendPendingTask for each pending index with the conf of its run. */
+        uint32_t r0 = run_off ? run_off[g] : 0, r1 = run_off ? run_off[g + 1] : 1;
+        uint32_t r = r0;
+        for (int64_t i = pi; i <= la; ++i) {
+            uint64_t cw;
+            if (run_off) {
+                while (r + 1 < r1 && run_start[r + 1] <= i) ++r;
+                cw = run_conf[r];
+            } else {
+                cw = conf[g];
+            }
+            int32_t nids[16], oids[16];
+            int32_t nn = mask_to_ids((uint32_t)(cw & 0xFFFF), nids);
+            int32_t no = ((cw >> 40) & 0xFF) ? mask_to_ids((uint32_t)((cw >> 16) & 0xFFFF), oids) : -1;
+            if (nn == 0) st |= JO_ST_EMPTY_CONF;
+            jo_bb_append_pending_task(bb, nids, nn, oids, no);
+        }
+        /* acks, Replicator-style: contiguous chunks, round-robin over peers. */
+        for (uint32_t p = 0; p < P; ++p) next[p] = pi;
+        for (uint32_t p = 0; p < P; ++p) {
+            if (match[(size_t)p * G + g] > la) {
+                int rc = jo_bb_commit_at(bb, pi, match[(size_t)p * G + g], (int32_t)p);
+                if (rc == JO_AIOOBE) st |= JO_ST_OUT_OF_RANGE;
+                next[p] = INT64_MAX; /* this peer's ack threw: no grants from it */
+            }
+        }
+        for (;;) {
+            int any = 0;
+            for (uint32_t p = 0; p < P; ++p) {
+                const int64_t m = match[(size_t)p * G + g];
+                if (next[p] == INT64_MAX || next[p] > m) continue;
+                int64_t last = next[p] + chunk - 1;
+                if (last > m) last = m;
+                jo_bb_commit_at(bb, next[p], last, (int32_t)p);
+                next[p] = last + 1;
+                any = 1;
+            }
+            if (!any) break;
+        }
+        committed_out[g] = bb->last_committed_index;
+        status_out[g] = st;
+        grants += bb->grants;
+    }
+    free(next);
+    jo_bb_free(bb);
+    return grants;
+}

@@ -1,0 +1,140 @@
+/*
+ * jraft_oracle.h -- CPU restatement of SOFAJRaft's quorum + checksum hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity oracle: only tests/, the smoke()
+ * entry of __graft_entry__.py and bench.py's cpu_baseline leg may load it, and
+ * only as the checker / the timed CPU baseline.  The product path (libjrq.so)
+ * never links or calls it.
+ *
+ * Everything here restates the reference Java loop structure one-for-one
+ * (byte-at-a-time CRC table walk, per-entry Ballot objects, per-(entry, ack)
+ * grant loop) so that it doubles as the "port" CPU baseline.
+ * Citations: JC = jraft-core/src/main/java/com/alipay/sofa/jraft in the
+ * reference tree.
+ */
+#ifndef JRAFT_ORACLE_H
+#define JRAFT_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- CRC-64/ECMA-182 (JC/util/CRC64.java) ------------------- */
+
+/* The 256-entry table, generated from the polynomial (JC/util/CRC64.java:41-92). */
+const uint64_t *jo_crc64_table(void);
+/* CRC64.update(byte[],off,len) continuing from `crc` (JC/util/CRC64.java:100-110). */
+uint64_t jo_crc64_update(uint64_t crc, const uint8_t *p, size_t n);
+/* CrcUtil.crc64(byte[],off,len): fresh state, update, getValue (JC/util/CrcUtil.java:51-57). */
+uint64_t jo_crc64(const uint8_t *p, size_t n);
+/* Batch of ragged payloads: out[i] = crc64(payload[off[i] .. off[i+1])). */
+void jo_crc64_batch(const uint8_t *payload, const uint64_t *offsets, uint32_t n, uint64_t *out);
+
+/* ---------------- checksums (JC/entity) ---------------------------- */
+
+/* LogId.checksum: crc64(BE64(index) || BE64(term)) (JC/entity/LogId.java:45-50, JC/util/Bits.java:71-80). */
+uint64_t jo_logid_checksum(int64_t index, int64_t term);
+/* PeerId.checksum: crc64(latin1(ip ":" port [":" idx if idx != 0]))
+ * (JC/entity/PeerId.java:60-65,135-144; JC/util/Endpoint.java:60-65; JC/util/AsciiStringUtil.java:27-34). */
+uint64_t jo_peerid_checksum(const char *ip, int32_t port, int32_t idx);
+/* LogEntry.checksum (JC/entity/LogEntry.java:88-108): type ^ LogId ^ (xor of peer checksums) ^ crc64(data).
+ * peer_xor is the XOR of every PeerId.checksum() of peers, oldPeers, learners, oldLearners
+ * (XOR is order independent: JC/entity/Checksum.java:40-42). */
+uint64_t jo_logentry_checksum(int32_t type, int64_t index, int64_t term, uint64_t peer_xor,
+                              const uint8_t *data, size_t len);
+/* Batch form with optional verify (LogEntry.isCorrupted, JC/entity/LogEntry.java:156-158).
+ * expected/has/corrupt may be NULL (then no verify).  has==NULL means "every entry has a checksum". */
+void jo_logentry_checksum_batch(const uint8_t *type, const int64_t *index, const int64_t *term,
+                                const uint64_t *peer_xor, const uint8_t *payload,
+                                const uint64_t *offsets, uint32_t n, uint64_t *out,
+                                const uint64_t *expected, const uint8_t *has, uint8_t *corrupt);
+
+/* ---------------- Ballot (JC/entity/Ballot.java) --------------------------- */
+
+#define JO_MAX_CONF 32 /* peers per Configuration list kept by the oracle */
+
+typedef struct {
+    int32_t peer[JO_MAX_CONF];
+    uint8_t found[JO_MAX_CONF];
+    int32_t n;
+} jo_peer_list;
+
+typedef struct {
+    jo_peer_list peers;
+    int32_t quorum;
+    jo_peer_list old_peers;
+    int32_t old_quorum;
+} jo_ballot;
+
+typedef struct {
+    int32_t pos0, pos1;
+} jo_pos_hint;
+
+/* Ballot.init(conf, oldConf) (JC/entity/Ballot.java:63-85).  Peers are small integer ids:
+ * PeerId.equals == id equality.  nconf < 0 means conf == null, nold < 0 means oldConf == null. */
+int jo_ballot_init(jo_ballot *b, const int32_t *conf, int32_t nconf, const int32_t *old, int32_t nold);
+/* Ballot.grant(peer, hint) including the PosHint search (JC/entity/Ballot.java:87-127). */
+jo_pos_hint jo_ballot_grant_hint(jo_ballot *b, int32_t peer, jo_pos_hint hint);
+void jo_ballot_grant(jo_ballot *b, int32_t peer);
+/* Ballot.isGranted (JC/entity/Ballot.java:138-140). */
+int jo_ballot_is_granted(const jo_ballot *b);
+
+/* ---------------- BallotBox (JC/core/BallotBox.java) ----------------------- */
+
+enum { JO_FALSE = 0, JO_TRUE = 1, JO_AIOOBE = -1 /* ArrayIndexOutOfBoundsException */,
+       JO_IAE = -2 /* IllegalArgumentException */ };
+
+typedef struct jo_ballot_box jo_ballot_box;
+
+jo_ballot_box *jo_bb_new(void);
+void jo_bb_free(jo_ballot_box *bb);
+int64_t jo_bb_last_committed_index(const jo_ballot_box *bb); /* :67-79 */
+int64_t jo_bb_pending_index(const jo_ballot_box *bb);
+int64_t jo_bb_queue_size(const jo_ballot_box *bb);
+/* FSMCaller.onCommitted(idx) calls observed so far (the Mockito waiter of BallotBoxTest). */
+int64_t jo_bb_on_committed_calls(const jo_ballot_box *bb);
+int64_t jo_bb_on_committed_last(const jo_ballot_box *bb);
+int jo_bb_commit_at(jo_ballot_box *bb, int64_t first, int64_t last, int32_t peer); /* :96-139 */
+void jo_bb_clear_pending_tasks(jo_ballot_box *bb);                                 /* :147-156 */
+int jo_bb_reset_pending_index(jo_ballot_box *bb, int64_t new_pending_index);       /* :167-186 */
+int jo_bb_append_pending_task(jo_ballot_box *bb, const int32_t *conf, int32_t nconf,
+                              const int32_t *old, int32_t nold);                   /* :197-215 */
+int jo_bb_set_last_committed_index(jo_ballot_box *bb, int64_t idx);                /* :223-248 */
+
+/* ---------------- one quorum epoch, replayed as calls ---------------------- */
+
+/* Per-group status codes shared with the engine (include/jrq.h). */
+enum { JO_ST_OK = 0, JO_ST_NOT_LEADER = 1, JO_ST_OUT_OF_RANGE = 2, JO_ST_EMPTY_CONF = 4 };
+
+/*
+ * Replays one epoch of a group batch through real jo_ballot_box objects:
+ *   for each group g: resetPendingIndex(pendingIndex), appendPendingTask for every
+ *   index in [pendingIndex, lastAppended] with the conf of the run that covers it,
+ *   then, per peer p, the acks a Replicator would send for match[p][g]: contiguous
+ *   commitAt(first, last, p) calls of at most `chunk` entries from pendingIndex up to
+ *   match (interleaved round-robin across peers, leader first); a peer whose match
+ *   exceeds lastAppended sends commitAt(pendingIndex, match) which throws AIOOBE.
+ * Runs: run_off[G+1] (NULL => one run per group from conf[]), run_start[R] (first
+ * index of the run), run_conf[R] in the same packing as conf[].
+ * conf packing (uint64, shared with include/jrq.h): bits 0-15 new-peer mask over
+ *   the group's peer slots, 16-31 old-peer mask, 32-39 new quorum, 40-47 old quorum.
+ *   The oracle builds Ballots from the masks exactly as Ballot.init does (quorum =
+ *   n/2+1, computed here, not read); old quorum byte 0 means oldConf == null, any
+ *   other value means an old conf is present (possibly empty).
+ * lastCommitted[g] is the state before the epoch.  Outputs committed[g] and status[g].
+ * Returns the number of Ballot.grant calls executed (the work the reference does).
+ */
+int64_t jo_quorum_epoch_replay(uint32_t G, uint32_t P, const int64_t *match /* [P][G] */,
+                               const int64_t *pending_index, const int64_t *last_appended,
+                               const int64_t *last_committed, const uint64_t *conf,
+                               const uint32_t *run_off, const int64_t *run_start,
+                               const uint64_t *run_conf, int64_t chunk,
+                               int64_t *committed_out, uint8_t *status_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

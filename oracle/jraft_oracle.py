@@ -1,0 +1,279 @@
+"""Python face of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may
+import this module, and only as the checker or the timed CPU baseline.  The
+product path (``libjrq.so`` + ``jraft_amd``) never imports it.
+
+Two layers:
+  * ctypes bindings to ``oracle/_build/libjraft_oracle.so`` (jraft_oracle.c), the
+    Java-faithful restatement used for parity and as the "port" CPU baseline;
+  * tiny pure-Python restatements (``py_crc64`` ...) used only on small inputs to
+    cross-check the C restatement itself.
+Reference citations use JC = jraft-core/src/main/java/com/alipay/sofa/jraft.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libjraft_oracle.so")
+_lib = None
+
+POLY = 0x42F0E1EBA9EA3693  # JC/util/CRC64.java:27-40
+M64 = (1 << 64) - 1
+
+# status codes (shared with include/jrq.h)
+ST_OK, ST_NOT_LEADER, ST_OUT_OF_RANGE, ST_EMPTY_CONF = 0, 1, 2, 4
+FALSE, TRUE, AIOOBE, IAE = 0, 1, -1, -2
+
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+_u64p = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
+_u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+
+
+def build() -> str:
+    """Compile the C oracle with make (gcc only)."""
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        L.jo_crc64.restype = C.c_uint64
+        L.jo_crc64.argtypes = [C.c_void_p, C.c_size_t]
+        L.jo_crc64_update.restype = C.c_uint64
+        L.jo_crc64_update.argtypes = [C.c_uint64, C.c_void_p, C.c_size_t]
+        L.jo_crc64_table.restype = C.POINTER(C.c_uint64)
+        L.jo_crc64_batch.restype = None
+        L.jo_crc64_batch.argtypes = [_u8p, _u64p, C.c_uint32, _u64p]
+        L.jo_logid_checksum.restype = C.c_uint64
+        L.jo_logid_checksum.argtypes = [C.c_int64, C.c_int64]
+        L.jo_peerid_checksum.restype = C.c_uint64
+        L.jo_peerid_checksum.argtypes = [C.c_char_p, C.c_int32, C.c_int32]
+        L.jo_logentry_checksum.restype = C.c_uint64
+        L.jo_logentry_checksum.argtypes = [C.c_int32, C.c_int64, C.c_int64, C.c_uint64, C.c_void_p,
+                                           C.c_size_t]
+        L.jo_logentry_checksum_batch.restype = None
+        L.jo_logentry_checksum_batch.argtypes = [_u8p, _i64p, _i64p, C.c_void_p, _u8p, _u64p,
+                                                 C.c_uint32, _u64p, C.c_void_p, C.c_void_p,
+                                                 C.c_void_p]
+        L.jo_bb_new.restype = C.c_void_p
+        L.jo_bb_free.argtypes = [C.c_void_p]
+        for name in ("jo_bb_last_committed_index", "jo_bb_pending_index", "jo_bb_queue_size",
+                     "jo_bb_on_committed_calls", "jo_bb_on_committed_last"):
+            getattr(L, name).restype = C.c_int64
+            getattr(L, name).argtypes = [C.c_void_p]
+        L.jo_bb_commit_at.restype = C.c_int
+        L.jo_bb_commit_at.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int32]
+        L.jo_bb_clear_pending_tasks.argtypes = [C.c_void_p]
+        L.jo_bb_reset_pending_index.restype = C.c_int
+        L.jo_bb_reset_pending_index.argtypes = [C.c_void_p, C.c_int64]
+        L.jo_bb_append_pending_task.restype = C.c_int
+        L.jo_bb_append_pending_task.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
+                                                C.c_int32]
+        L.jo_bb_set_last_committed_index.restype = C.c_int
+        L.jo_bb_set_last_committed_index.argtypes = [C.c_void_p, C.c_int64]
+        L.jo_quorum_epoch_replay.restype = C.c_int64
+        L.jo_quorum_epoch_replay.argtypes = [C.c_uint32, C.c_uint32, _i64p, _i64p, _i64p, _i64p,
+                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_int64, _i64p, _u8p]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+# ------------------------------------------------------------------ CRC64 --
+
+def table() -> np.ndarray:
+    t = lib().jo_crc64_table()
+    return np.array([t[i] for i in range(256)], dtype=np.uint64)
+
+
+def crc64(data: bytes) -> int:
+    """CrcUtil.crc64(byte[]) (JC/util/CrcUtil.java:36-41); None -> 0 as in the reference."""
+    if data is None:
+        return 0
+    b = bytes(data)
+    return int(lib().jo_crc64(C.c_char_p(b), len(b)))
+
+
+def crc64_batch(payload: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    out = np.zeros(max(n, 0), dtype=np.uint64)
+    if n > 0:
+        if payload.size == 0:
+            payload = np.zeros(1, dtype=np.uint8)
+        lib().jo_crc64_batch(payload, offsets, n, out)
+    return out
+
+
+def logid_checksum(index: int, term: int) -> int:
+    return int(lib().jo_logid_checksum(index, term))
+
+
+def peerid_checksum(ip: str, port: int, idx: int = 0) -> int:
+    return int(lib().jo_peerid_checksum(ip.encode("latin-1"), port, idx))
+
+
+def logentry_checksum(etype: int, index: int, term: int, peer_xor: int, data: bytes | None) -> int:
+    b = b"" if data is None else bytes(data)
+    return int(lib().jo_logentry_checksum(etype, index, term, peer_xor, C.c_char_p(b), len(b)))
+
+
+def logentry_checksum_batch(etype, index, term, peer_xor, payload, offsets, expected=None,
+                            has=None):
+    etype = np.ascontiguousarray(etype, dtype=np.uint8)
+    index = np.ascontiguousarray(index, dtype=np.int64)
+    term = np.ascontiguousarray(term, dtype=np.int64)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    if payload.size == 0:
+        payload = np.zeros(1, dtype=np.uint8)
+    n = len(offsets) - 1
+    px = None if peer_xor is None else np.ascontiguousarray(peer_xor, dtype=np.uint64)
+    ex = None if expected is None else np.ascontiguousarray(expected, dtype=np.uint64)
+    hs = None if has is None else np.ascontiguousarray(has, dtype=np.uint8)
+    out = np.zeros(n, dtype=np.uint64)
+    corrupt = np.zeros(n, dtype=np.uint8) if ex is not None else None
+    lib().jo_logentry_checksum_batch(etype, index, term, _ptr(px), payload, offsets, n, out,
+                                     _ptr(ex), _ptr(hs), _ptr(corrupt))
+    return out if corrupt is None else (out, corrupt)
+
+
+# ------------------------------------------------- pure-Python cross-checks --
+
+def py_table() -> list[int]:
+    """Table entries as the doc comment of JC/util/CRC64.java:27-40 defines them."""
+    t = []
+    for i in range(256):
+        c = i << 56
+        for _ in range(8):
+            c = ((c << 1) ^ POLY) & M64 if c >> 63 else (c << 1) & M64
+        t.append(c)
+    return t
+
+
+_PY_T = None
+
+
+def py_crc64(data: bytes, crc: int = 0) -> int:
+    """CRC64.update(byte) loop (JC/util/CRC64.java:100-110), pure Python, small inputs only."""
+    global _PY_T
+    if _PY_T is None:
+        _PY_T = py_table()
+    for b in bytes(data):
+        crc = _PY_T[((crc >> 56) ^ b) & 0xFF] ^ ((crc << 8) & M64)
+    return crc
+
+
+def py_logid_checksum(index: int, term: int) -> int:
+    return py_crc64((index & M64).to_bytes(8, "big") + (term & M64).to_bytes(8, "big"))
+
+
+def py_peer_string(ip: str, port: int, idx: int = 0) -> str:
+    """PeerId.toString (JC/entity/PeerId.java:135-144)."""
+    s = f"{ip}:{port}"
+    return s + f":{idx}" if idx != 0 else s
+
+
+def py_peerid_checksum(ip: str, port: int, idx: int = 0) -> int:
+    return py_crc64(py_peer_string(ip, port, idx).encode("latin-1"))
+
+
+# --------------------------------------------------------------- BallotBox --
+
+class BallotBox:
+    """ctypes handle on the C restatement of JC/core/BallotBox.java.
+
+    Peers are small integer ids (PeerId.equals == id equality).  Return codes
+    follow the reference: bool, or the exception it would throw.
+    """
+
+    def __init__(self):
+        self._h = lib().jo_bb_new()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().jo_bb_free(self._h)
+            self._h = None
+
+    @property
+    def last_committed_index(self):
+        return lib().jo_bb_last_committed_index(self._h)
+
+    @property
+    def pending_index(self):
+        return lib().jo_bb_pending_index(self._h)
+
+    @property
+    def queue_size(self):
+        return lib().jo_bb_queue_size(self._h)
+
+    @property
+    def on_committed_calls(self):
+        return lib().jo_bb_on_committed_calls(self._h)
+
+    @property
+    def on_committed_last(self):
+        return lib().jo_bb_on_committed_last(self._h)
+
+    def commit_at(self, first, last, peer):
+        rc = lib().jo_bb_commit_at(self._h, first, last, peer)
+        if rc == AIOOBE:
+            raise IndexError("ArrayIndexOutOfBoundsException")
+        return bool(rc)
+
+    def clear_pending_tasks(self):
+        lib().jo_bb_clear_pending_tasks(self._h)
+
+    def reset_pending_index(self, n):
+        return bool(lib().jo_bb_reset_pending_index(self._h, n))
+
+    def append_pending_task(self, conf, old_conf=None):
+        c = None if conf is None else np.ascontiguousarray(conf, dtype=np.int32)
+        o = None if old_conf is None else np.ascontiguousarray(old_conf, dtype=np.int32)
+        return bool(lib().jo_bb_append_pending_task(
+            self._h, _ptr(c), -1 if c is None else len(c), _ptr(o), -1 if o is None else len(o)))
+
+    def set_last_committed_index(self, idx):
+        rc = lib().jo_bb_set_last_committed_index(self._h, idx)
+        if rc == IAE:
+            raise ValueError("IllegalArgumentException")
+        return bool(rc)
+
+
+def quorum_epoch_replay(match, pending_index, last_appended, last_committed, conf,
+                        run_off=None, run_start=None, run_conf=None, chunk=1024):
+    """Replay one epoch of a group batch through real BallotBoxes (see jraft_oracle.h).
+
+    Returns (committed[G] int64, status[G] uint8, grants executed)."""
+    match = np.ascontiguousarray(match, dtype=np.int64)
+    P, G = match.shape
+    pending_index = np.ascontiguousarray(pending_index, dtype=np.int64)
+    last_appended = np.ascontiguousarray(last_appended, dtype=np.int64)
+    last_committed = np.ascontiguousarray(last_committed, dtype=np.int64)
+    conf_a = None if conf is None else np.ascontiguousarray(conf, dtype=np.uint64)
+    ro = None if run_off is None else np.ascontiguousarray(run_off, dtype=np.uint32)
+    rs = None if run_start is None else np.ascontiguousarray(run_start, dtype=np.int64)
+    rc = None if run_conf is None else np.ascontiguousarray(run_conf, dtype=np.uint64)
+    committed = np.zeros(G, dtype=np.int64)
+    status = np.zeros(G, dtype=np.uint8)
+    grants = lib().jo_quorum_epoch_replay(G, P, match, pending_index, last_appended,
+                                          last_committed, _ptr(conf_a), _ptr(ro), _ptr(rs),
+                                          _ptr(rc), chunk, committed, status)
+    return committed, status, int(grants)

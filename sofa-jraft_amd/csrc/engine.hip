@@ -1,0 +1,490 @@
+// engine.hip -- the C ABI of libjrq.so (include/jrq.h): engine lifetime, constant
+// tables, staging for host-pointer calls, kernel dispatch and RCCL publication.
+//
+// Host-side code only; the kernels live in crc64.hip and quorum.hip.  Nothing here
+// computes a result on the CPU: every jrq_* entry point runs its work on the GPU
+// and fails (negative return) when no gfx950 device is usable.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/jrq.h"
+#include "jrq_device.h"
+
+extern "C" hipError_t jrq_launch_crc64(const JrqCrcArgs* args, int log_entry, int grid,
+                                       hipStream_t stream);
+extern "C" hipError_t jrq_launch_quorum(const JrqQuorumArgs* args, int grid, hipStream_t stream);
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+}  // namespace
+
+struct jrq_engine {
+  int device = -1;
+  int num_cus = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  uint64_t* slice = nullptr;  // [2][256]
+  uint64_t* shift = nullptr;  // [kShiftTables][8][256]
+  uint64_t* acc = nullptr;    // straddler accumulators
+  uint32_t* cnt = nullptr;    // straddler counters
+  uint32_t scratch_len = 0;
+  int crc_grid = 0;
+  uint32_t max_groups = 0;
+  uint8_t max_peers = 0;
+  DevBuf stage[16];
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = -1;
+  std::string err;
+};
+
+namespace {
+
+// --------------------------------------------------------------- helpers ---
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int fail(jrq_engine* e, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (e) e->err = buf;
+  else g_create_error = buf;
+  return code;
+}
+
+#define JRQ_HIP(e, call)                                                                    \
+  do {                                                                                      \
+    hipError_t _s = (call);                                                                 \
+    if (_s != hipSuccess)                                                                   \
+      return fail((e), JRQ_E_HIP, "%s failed: %s", #call, hipGetErrorString(_s));          \
+  } while (0)
+
+// GF(2)[x] / (x^64 + poly): a * b mod G, MSB-first representation as in CRC64.java.
+uint64_t mulmod(uint64_t a, uint64_t b) {
+  uint64_t r = 0;
+  for (int i = 63; i >= 0; --i) {
+    r = (r & 0x8000000000000000ULL) ? (r << 1) ^ jrq::kCrcPoly : (r << 1);
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r;
+}
+
+// Constant tables (see crc64.hip):
+//   T0[i]  = CRC64 table entry (jraft-core/.../util/CRC64.java:41-92, generated from the poly)
+//   T1[i]  = T0[i] advanced by one zero byte
+//   slice  = { bswap(T0), bswap(T1) }  (reversed-domain slice-by-2)
+//   shift[t][k][i] = (i * x^(8k)) * x^(8 * 2^t) mod G
+void build_tables(std::vector<uint64_t>& slice, std::vector<uint64_t>& shift) {
+  uint64_t t0[256], t1[256];
+  for (int i = 0; i < 256; ++i) {
+    uint64_t c = static_cast<uint64_t>(i) << 56;
+    for (int k = 0; k < 8; ++k) c = (c & 0x8000000000000000ULL) ? (c << 1) ^ jrq::kCrcPoly : (c << 1);
+    t0[i] = c;
+  }
+  for (int i = 0; i < 256; ++i) t1[i] = t0[t0[i] >> 56] ^ (t0[i] << 8);
+  slice.resize(512);
+  for (int i = 0; i < 256; ++i) {
+    slice[i] = __builtin_bswap64(t0[i]);
+    slice[256 + i] = __builtin_bswap64(t1[i]);
+  }
+  shift.resize(static_cast<size_t>(jrq::kShiftTables) * 8 * 256);
+  uint64_t K = 0x100;  // x^8
+  for (int t = 0; t < jrq::kShiftTables; ++t) {
+    for (int k = 0; k < 8; ++k)
+      for (int i = 0; i < 256; ++i)
+        shift[(static_cast<size_t>(t) * 8 + k) * 256 + i] = mulmod(static_cast<uint64_t>(i) << (8 * k), K);
+    K = mulmod(K, K);  // x^(8 * 2^(t+1))
+  }
+}
+
+int ensure_stage(jrq_engine* e, int slot, size_t bytes, void** out) {
+  DevBuf& b = e->stage[slot];
+  if (bytes == 0) bytes = 16;
+  if (b.cap < bytes) {
+    if (b.p) {
+      JRQ_HIP(e, hipStreamSynchronize(e->stream));
+      JRQ_HIP(e, hipFree(b.p));
+      b.p = nullptr;
+      b.cap = 0;
+    }
+    size_t cap = bytes + bytes / 4;
+    JRQ_HIP(e, hipMalloc(&b.p, cap));
+    b.cap = cap;
+  }
+  *out = b.p;
+  return JRQ_OK;
+}
+
+template <typename T>
+int stage_in(jrq_engine* e, int slot, const T* host, size_t count, const T** dev) {
+  if (host == nullptr) {
+    *dev = nullptr;
+    return JRQ_OK;
+  }
+  void* p = nullptr;
+  int rc = ensure_stage(e, slot, count * sizeof(T), &p);
+  if (rc) return rc;
+  if (count) JRQ_HIP(e, hipMemcpyAsync(p, host, count * sizeof(T), hipMemcpyHostToDevice, e->stream));
+  *dev = static_cast<const T*>(p);
+  return JRQ_OK;
+}
+
+int crc_dispatch(jrq_engine* e, JrqCrcArgs& a, int log_entry) {
+  if (a.n == 0) return JRQ_OK;
+  a.slice = e->slice;
+  a.shift = e->shift;
+  a.acc = e->acc;
+  a.cnt = e->cnt;
+  a.scratch_len = e->scratch_len;
+  a.min_seg_log2 = 8;
+  JRQ_HIP(e, jrq_launch_crc64(&a, log_entry, e->crc_grid, e->stream));
+  return JRQ_OK;
+}
+
+}  // namespace
+
+// ================================================================ C ABI ====
+
+extern "C" {
+
+int jrq_abi_version(void) { return JRQ_ABI_VERSION; }
+
+const char* jrq_last_error(const jrq_engine* e) {
+  return e ? e->err.c_str() : g_create_error.c_str();
+}
+
+jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* err) {
+  auto set = [&](int c) {
+    if (err) *err = c;
+  };
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    fail(nullptr, JRQ_E_NODEV, "no HIP device visible");
+    set(JRQ_E_NODEV);
+    return nullptr;
+  }
+  if (device < 0 || device >= ndev || max_peers == 0 || max_peers > JRQ_MAX_PEERS) {
+    fail(nullptr, JRQ_E_INVALID, "bad device %d or max_peers %u", device, max_peers);
+    set(JRQ_E_INVALID);
+    return nullptr;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess ||
+      std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    fail(nullptr, JRQ_E_NODEV, "device %d is not gfx950 (%s)", device, prop.gcnArchName);
+    set(JRQ_E_NODEV);
+    return nullptr;
+  }
+  DeviceGuard guard(device);
+  auto* e = new jrq_engine();
+  e->device = device;
+  e->num_cus = prop.multiProcessorCount;
+  e->max_groups = max_groups;
+  e->max_peers = max_peers;
+  e->crc_grid = e->num_cus;  // persistent: one 1024-thread workgroup per CU (128 KiB LDS)
+  e->scratch_len = static_cast<uint32_t>(2ull * e->crc_grid * jrq::kCrcBlock + 2);
+  int rc = JRQ_OK;
+  std::vector<uint64_t> slice, shift;
+  build_tables(slice, shift);
+  auto try_hip = [&](hipError_t s, const char* what) {
+    if (s != hipSuccess && rc == JRQ_OK) rc = fail(nullptr, JRQ_E_HIP, "%s: %s", what, hipGetErrorString(s));
+  };
+  try_hip(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking), "hipStreamCreate");
+  e->stream = e->own_stream;
+  try_hip(hipMalloc(&e->slice, slice.size() * 8), "hipMalloc(slice)");
+  try_hip(hipMalloc(&e->shift, shift.size() * 8), "hipMalloc(shift)");
+  try_hip(hipMalloc(&e->acc, static_cast<size_t>(e->scratch_len) * 8), "hipMalloc(acc)");
+  try_hip(hipMalloc(&e->cnt, static_cast<size_t>(e->scratch_len) * 4), "hipMalloc(cnt)");
+  if (rc == JRQ_OK) {
+    try_hip(hipMemcpy(e->slice, slice.data(), slice.size() * 8, hipMemcpyHostToDevice), "upload slice");
+    try_hip(hipMemcpy(e->shift, shift.data(), shift.size() * 8, hipMemcpyHostToDevice), "upload shift");
+    try_hip(hipMemset(e->acc, 0, static_cast<size_t>(e->scratch_len) * 8), "zero acc");
+    try_hip(hipMemset(e->cnt, 0, static_cast<size_t>(e->scratch_len) * 4), "zero cnt");
+  }
+  if (rc != JRQ_OK) {
+    set(rc);
+    jrq_destroy(e);
+    return nullptr;
+  }
+  set(JRQ_OK);
+  return e;
+}
+
+void jrq_destroy(jrq_engine* e) {
+  if (!e) return;
+  DeviceGuard guard(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->comm) (void)ncclCommDestroy(e->comm);
+  for (auto& b : e->stage)
+    if (b.p) (void)hipFree(b.p);
+  if (e->slice) (void)hipFree(e->slice);
+  if (e->shift) (void)hipFree(e->shift);
+  if (e->acc) (void)hipFree(e->acc);
+  if (e->cnt) (void)hipFree(e->cnt);
+  if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+  delete e;
+}
+
+void* jrq_get_stream(jrq_engine* e) { return e ? static_cast<void*>(e->stream) : nullptr; }
+
+int jrq_set_stream(jrq_engine* e, void* s) {
+  if (!e) return JRQ_E_INVALID;
+  e->stream = s ? static_cast<hipStream_t>(s) : e->own_stream;
+  return JRQ_OK;
+}
+
+int jrq_synchronize(jrq_engine* e) {
+  if (!e) return JRQ_E_INVALID;
+  DeviceGuard guard(e->device);
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
+int jrq_host_register(void* ptr, size_t bytes) {
+  if (!ptr || !bytes) return JRQ_E_INVALID;
+  return hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess ? JRQ_OK : JRQ_E_HIP;
+}
+
+int jrq_host_unregister(void* ptr) {
+  if (!ptr) return JRQ_E_INVALID;
+  return hipHostUnregister(ptr) == hipSuccess ? JRQ_OK : JRQ_E_HIP;
+}
+
+// ----------------------------------------------------------------- quorum ---
+
+int jrq_quorum_epoch_dev(jrq_engine* e, const jrq_group_batch* in, int64_t* committed_out,
+                         uint8_t* status_out, uint32_t G) {
+  if (!e || !in) return e ? fail(e, JRQ_E_INVALID, "null batch") : JRQ_E_INVALID;
+  if (G == 0) return JRQ_OK;
+  if (in->num_peers == 0 || in->num_peers > JRQ_MAX_PEERS)
+    return fail(e, JRQ_E_INVALID, "num_peers %u outside 1..%d", in->num_peers, JRQ_MAX_PEERS);
+  if (!in->match || !in->pending_index || !in->last_appended || !in->last_committed ||
+      !committed_out || !status_out || (!in->run_off && !in->conf) ||
+      (in->run_off && (!in->run_start || !in->run_conf)) || in->match_ld < G)
+    return fail(e, JRQ_E_INVALID, "missing array or match_ld < G");
+  DeviceGuard guard(e->device);
+  JrqQuorumArgs a;
+  a.match = in->match;
+  a.pending_index = in->pending_index;
+  a.last_appended = in->last_appended;
+  a.last_committed = in->last_committed;
+  a.conf = in->conf;
+  a.run_off = in->run_off;
+  a.run_start = in->run_start;
+  a.run_conf = in->run_conf;
+  a.num_peers = in->num_peers;
+  a.match_ld = in->match_ld;
+  a.committed = committed_out;
+  a.status = status_out;
+  a.G = G;
+  // enough 256-thread blocks for ~8 per CU, grid-stride beyond
+  const uint64_t need = (static_cast<uint64_t>(G) + 255) / 256;
+  const uint64_t cap = static_cast<uint64_t>(e->num_cus) * 8;
+  const int grid = static_cast<int>(need < cap ? need : cap);
+  JRQ_HIP(e, jrq_launch_quorum(&a, grid, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_quorum_epoch(jrq_engine* e, const jrq_group_batch* in, int64_t* committed_out,
+                     uint8_t* status_out, uint32_t G) {
+  if (!e || !in) return e ? fail(e, JRQ_E_INVALID, "null batch") : JRQ_E_INVALID;
+  if (G == 0) return JRQ_OK;
+  if (!committed_out || !status_out) return fail(e, JRQ_E_INVALID, "null output");
+  if (in->num_peers == 0 || in->num_peers > JRQ_MAX_PEERS || in->match_ld < G || !in->match)
+    return fail(e, JRQ_E_INVALID, "bad num_peers / match_ld");
+  DeviceGuard guard(e->device);
+  jrq_group_batch d = *in;
+  int rc;
+  const size_t P = in->num_peers;
+  if ((rc = stage_in(e, 0, in->match, (P - 1) * in->match_ld + G, &d.match))) return rc;
+  if ((rc = stage_in(e, 1, in->pending_index, G, &d.pending_index))) return rc;
+  if ((rc = stage_in(e, 2, in->last_appended, G, &d.last_appended))) return rc;
+  if ((rc = stage_in(e, 3, in->last_committed, G, &d.last_committed))) return rc;
+  if ((rc = stage_in(e, 4, in->conf, G, &d.conf))) return rc;
+  if (in->run_off) {
+    if ((rc = stage_in(e, 5, in->run_off, static_cast<size_t>(G) + 1, &d.run_off))) return rc;
+    if ((rc = stage_in(e, 6, in->run_start, in->num_runs, &d.run_start))) return rc;
+    if ((rc = stage_in(e, 7, in->run_conf, in->num_runs, &d.run_conf))) return rc;
+  }
+  void *dc = nullptr, *ds = nullptr;
+  if ((rc = ensure_stage(e, 8, static_cast<size_t>(G) * 8, &dc))) return rc;
+  if ((rc = ensure_stage(e, 9, G, &ds))) return rc;
+  if ((rc = jrq_quorum_epoch_dev(e, &d, static_cast<int64_t*>(dc), static_cast<uint8_t*>(ds), G)))
+    return rc;
+  JRQ_HIP(e, hipMemcpyAsync(committed_out, dc, static_cast<size_t>(G) * 8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(status_out, ds, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
+// --------------------------------------------------------------- checksum ---
+
+int jrq_crc64_batch_dev(jrq_engine* e, const uint8_t* payload, const uint64_t* offsets, uint32_t N,
+                        uint64_t* crc_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (N == 0) return JRQ_OK;
+  if (!payload || !offsets || !crc_out) return fail(e, JRQ_E_INVALID, "null pointer");
+  DeviceGuard guard(e->device);
+  JrqCrcArgs a{};
+  a.payload = payload;
+  a.offsets = offsets;
+  a.n = N;
+  a.out = crc_out;
+  return crc_dispatch(e, a, 0);
+}
+
+int jrq_crc64_batch(jrq_engine* e, const uint8_t* payload, const uint64_t* offsets, uint32_t N,
+                    uint64_t* crc_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (N == 0) return JRQ_OK;
+  if (!payload || !offsets || !crc_out) return fail(e, JRQ_E_INVALID, "null pointer");
+  DeviceGuard guard(e->device);
+  int rc;
+  const uint64_t lo = offsets[0], hi = offsets[N];
+  if (hi < lo) return fail(e, JRQ_E_INVALID, "offsets not monotone");
+  // stage only the referenced payload window and rebase the offsets onto it
+  const uint8_t* dp;
+  const uint64_t* doff;
+  if ((rc = stage_in(e, 10, payload + lo, hi - lo, &dp))) return rc;
+  std::vector<uint64_t> rebased(offsets, offsets + N + 1);
+  for (auto& o : rebased) o -= lo;
+  if ((rc = stage_in(e, 11, rebased.data(), rebased.size(), &doff))) return rc;
+  void* dout = nullptr;
+  if ((rc = ensure_stage(e, 12, static_cast<size_t>(N) * 8, &dout))) return rc;
+  if ((rc = jrq_crc64_batch_dev(e, dp, doff, N, static_cast<uint64_t*>(dout)))) return rc;
+  JRQ_HIP(e, hipMemcpyAsync(crc_out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
+int jrq_logentry_checksum_batch_dev(jrq_engine* e, const uint8_t* type, const int64_t* index,
+                                    const int64_t* term, const uint64_t* peer_xor,
+                                    const uint8_t* payload, const uint64_t* offsets, uint32_t N,
+                                    uint64_t* out, const uint64_t* expected, const uint8_t* has,
+                                    uint8_t* corrupt_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (N == 0) return JRQ_OK;
+  if (!type || !index || !term || !payload || !offsets || !out)
+    return fail(e, JRQ_E_INVALID, "null pointer");
+  if ((expected == nullptr) != (corrupt_out == nullptr))
+    return fail(e, JRQ_E_INVALID, "expected and corrupt_out go together");
+  DeviceGuard guard(e->device);
+  JrqCrcArgs a{};
+  a.payload = payload;
+  a.offsets = offsets;
+  a.n = N;
+  a.out = out;
+  a.type = type;
+  a.index = index;
+  a.term = term;
+  a.peer_xor = peer_xor;
+  a.expected = expected;
+  a.has = has;
+  a.corrupt = corrupt_out;
+  return crc_dispatch(e, a, 1);
+}
+
+int jrq_logentry_checksum_batch(jrq_engine* e, const uint8_t* type, const int64_t* index,
+                                const int64_t* term, const uint64_t* peer_xor,
+                                const uint8_t* payload, const uint64_t* offsets, uint32_t N,
+                                uint64_t* out, const uint64_t* expected, const uint8_t* has,
+                                uint8_t* corrupt_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (N == 0) return JRQ_OK;
+  if (!type || !index || !term || !payload || !offsets || !out)
+    return fail(e, JRQ_E_INVALID, "null pointer");
+  if ((expected == nullptr) != (corrupt_out == nullptr))
+    return fail(e, JRQ_E_INVALID, "expected and corrupt_out go together");
+  DeviceGuard guard(e->device);
+  int rc;
+  const uint64_t lo = offsets[0], hi = offsets[N];
+  if (hi < lo) return fail(e, JRQ_E_INVALID, "offsets not monotone");
+  const uint8_t *dp, *dt, *dh;
+  const uint64_t *doff, *dpx, *dex;
+  const int64_t *di, *dtm;
+  if ((rc = stage_in(e, 10, payload + lo, hi - lo, &dp))) return rc;
+  std::vector<uint64_t> rebased(offsets, offsets + N + 1);
+  for (auto& o : rebased) o -= lo;
+  if ((rc = stage_in(e, 11, rebased.data(), rebased.size(), &doff))) return rc;
+  if ((rc = stage_in(e, 1, type, N, &dt))) return rc;
+  if ((rc = stage_in(e, 2, index, N, &di))) return rc;
+  if ((rc = stage_in(e, 3, term, N, &dtm))) return rc;
+  if ((rc = stage_in(e, 4, peer_xor, N, &dpx))) return rc;
+  if ((rc = stage_in(e, 5, expected, N, &dex))) return rc;
+  if ((rc = stage_in(e, 6, has, N, &dh))) return rc;
+  void *dout = nullptr, *dcor = nullptr;
+  if ((rc = ensure_stage(e, 12, static_cast<size_t>(N) * 8, &dout))) return rc;
+  if (corrupt_out && (rc = ensure_stage(e, 13, N, &dcor))) return rc;
+  if ((rc = jrq_logentry_checksum_batch_dev(e, dt, di, dtm, dpx, dp, doff, N, static_cast<uint64_t*>(dout),
+                                            dex, dh, static_cast<uint8_t*>(dcor))))
+    return rc;
+  JRQ_HIP(e, hipMemcpyAsync(out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
+  if (corrupt_out) JRQ_HIP(e, hipMemcpyAsync(corrupt_out, dcor, N, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
+// ---------------------------------------------------------------- RCCL -----
+
+int jrq_rccl_get_unique_id(uint8_t id_out[128]) {
+  if (!id_out) return JRQ_E_INVALID;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return JRQ_E_RCCL;
+  static_assert(sizeof(id.internal) == 128, "ncclUniqueId is 128 bytes");
+  std::memcpy(id_out, id.internal, 128);
+  return JRQ_OK;
+}
+
+int jrq_rccl_init(jrq_engine* e, int nranks, int rank, const uint8_t id_in[128]) {
+  if (!e || !id_in || nranks <= 0 || rank < 0 || rank >= nranks) return JRQ_E_INVALID;
+  DeviceGuard guard(e->device);
+  ncclUniqueId id;
+  std::memcpy(id.internal, id_in, 128);
+  if (e->comm) {
+    (void)ncclCommDestroy(e->comm);
+    e->comm = nullptr;
+  }
+  ncclResult_t r = ncclCommInitRank(&e->comm, nranks, id, rank);
+  if (r != ncclSuccess) return fail(e, JRQ_E_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  e->nranks = nranks;
+  e->rank = rank;
+  return JRQ_OK;
+}
+
+int jrq_publish_committed_dev(jrq_engine* e, const int64_t* local, int64_t* global,
+                              uint64_t count_per_rank) {
+  if (!e || !local || !global) return JRQ_E_INVALID;
+  if (!e->comm) return fail(e, JRQ_E_STATE, "jrq_rccl_init not called");
+  DeviceGuard guard(e->device);
+  ncclResult_t r = ncclAllGather(local, global, count_per_rank, ncclInt64, e->comm, e->stream);
+  if (r != ncclSuccess) return fail(e, JRQ_E_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
+  return JRQ_OK;
+}
+
+}  // extern "C"

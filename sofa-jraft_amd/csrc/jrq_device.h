@@ -1,0 +1,72 @@
+// jrq_device.h -- shared device-side definitions for the libjrq kernels (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace jrq {
+
+// ----------------------------------------------------------------- CRC64 ---
+// CRC-64/ECMA-182, MSB first, poly 0x42F0E1EBA9EA3693, init 0, xorout 0
+// (reference: jraft-core/.../util/CRC64.java:27-40).
+constexpr uint64_t kCrcPoly = 0x42F0E1EBA9EA3693ULL;
+
+// Device copies of the constant tables (written once by jrq_create):
+//   slice[2][256]  "reversed-domain" slice-by-2 tables, see crc64.hip
+//   shift[kShiftTables][8][256]  multiply-by-x^(8*2^t) mod P byte tables
+constexpr int kShiftTables = 48;  // shifts up to 2^48 - 1 bytes
+
+// LDS image of the two slice tables, replicated so that lane l only ever touches
+// bank slot (l & 31): byte address = table<<16 | index<<8 | (l&31)<<3 (128 KiB).
+constexpr int kCrcLdsBytes = 2 * 256 * 32 * 8;
+constexpr int kCrcBlock = 1024;  // threads per workgroup (16 waves, 1 workgroup / CU)
+
+// Status flags, identical to include/jrq.h jrq_group_status.
+constexpr uint8_t kStNotLeader = 1, kStOutOfRange = 2, kStEmptyConf = 4;
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint64_t bswap64(uint64_t v) { return __builtin_bswap64(v); }
+
+}  // namespace jrq
+
+// Host-visible launch parameter blocks (plain structs, passed by value).
+struct JrqCrcArgs {
+  const uint8_t* payload;
+  const uint64_t* offsets;  // N+1
+  uint32_t n;
+  uint64_t* out;
+  // LogEntry fields (all null for the plain crc64 batch)
+  const uint8_t* type;
+  const int64_t* index;
+  const int64_t* term;
+  const uint64_t* peer_xor;
+  const uint64_t* expected;
+  const uint8_t* has;
+  uint8_t* corrupt;
+  // engine constants / scratch
+  const uint64_t* slice;   // [2][256]
+  const uint64_t* shift;   // [kShiftTables][8][256]
+  uint64_t* acc;           // straddler accumulators, zero between launches
+  uint32_t* cnt;           // straddler arrival counters, zero between launches
+  uint32_t scratch_len;    // entries in acc/cnt
+  uint32_t min_seg_log2;   // smallest segment size (log2 bytes)
+};
+
+struct JrqQuorumArgs {
+  const int64_t* match;
+  const int64_t* pending_index;
+  const int64_t* last_appended;
+  const int64_t* last_committed;
+  const uint64_t* conf;
+  const uint32_t* run_off;
+  const int64_t* run_start;
+  const uint64_t* run_conf;
+  uint32_t num_peers;
+  uint64_t match_ld;
+  int64_t* committed;
+  uint8_t* status;
+  uint32_t G;
+};

@@ -1,0 +1,106 @@
+"""ctypes binding of libjrq.so (include/jrq.h).
+
+This is the same C ABI a JDK 8 JNI shim binds; Python uses it
+for tests and bench.py.  There is no CPU fallback: if libjrq.so is missing or no
+gfx950 device is visible, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libjrq.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_PKG)), "include", "jrq.h")
+
+JRQ_OK = 0
+ERRORS = {-1: "JRQ_E_INVALID", -2: "JRQ_E_NOMEM", -3: "JRQ_E_HIP", -4: "JRQ_E_RCCL",
+          -5: "JRQ_E_NODEV", -6: "JRQ_E_STATE"}
+ST_OK, ST_NOT_LEADER, ST_OUT_OF_RANGE, ST_EMPTY_CONF = 0, 1, 2, 4
+MAX_PEERS = 16
+
+
+class JrqError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class GroupBatch(C.Structure):
+    """jrq_group_batch (include/jrq.h)."""
+    _fields_ = [
+        ("match", C.c_void_p),
+        ("pending_index", C.c_void_p),
+        ("last_appended", C.c_void_p),
+        ("last_committed", C.c_void_p),
+        ("conf", C.c_void_p),
+        ("run_off", C.c_void_p),
+        ("run_start", C.c_void_p),
+        ("run_conf", C.c_void_p),
+        ("num_peers", C.c_uint32),
+        ("num_runs", C.c_uint32),
+        ("match_ld", C.c_uint64),
+    ]
+
+
+# (name, restype, argtypes) for every function declared in include/jrq.h
+_V = C.c_void_p
+SIGNATURES = [
+    ("jrq_abi_version", C.c_int, []),
+    ("jrq_last_error", C.c_char_p, [_V]),
+    ("jrq_create", _V, [C.c_int, C.c_uint32, C.c_uint8, C.POINTER(C.c_int)]),
+    ("jrq_destroy", None, [_V]),
+    ("jrq_get_stream", _V, [_V]),
+    ("jrq_set_stream", C.c_int, [_V, _V]),
+    ("jrq_synchronize", C.c_int, [_V]),
+    ("jrq_host_register", C.c_int, [_V, C.c_size_t]),
+    ("jrq_host_unregister", C.c_int, [_V]),
+    ("jrq_quorum_epoch_dev", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
+    ("jrq_quorum_epoch", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
+    ("jrq_crc64_batch_dev", C.c_int, [_V, _V, _V, C.c_uint32, _V]),
+    ("jrq_crc64_batch", C.c_int, [_V, _V, _V, C.c_uint32, _V]),
+    ("jrq_logentry_checksum_batch_dev", C.c_int,
+     [_V, _V, _V, _V, _V, _V, _V, C.c_uint32, _V, _V, _V, _V]),
+    ("jrq_logentry_checksum_batch", C.c_int,
+     [_V, _V, _V, _V, _V, _V, _V, C.c_uint32, _V, _V, _V, _V]),
+    ("jrq_rccl_get_unique_id", C.c_int, [_V]),
+    ("jrq_rccl_init", C.c_int, [_V, C.c_int, C.c_int, _V]),
+    ("jrq_publish_committed_dev", C.c_int, [_V, _V, _V, C.c_uint64]),
+]
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libjrq.so (raises if it was not built: no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FileNotFoundError(
+                f"{LIB_PATH} missing: run `make -C sofa-jraft_amd` (or __graft_entry__.build())")
+        lib = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, engine_handle=None) -> None:
+    if rc != JRQ_OK:
+        msg = load().jrq_last_error(engine_handle)
+        raise JrqError(rc, msg.decode() if msg else "")
+
+
+def conf_word(new_mask: int, old_mask: int = 0, new_q: int | None = None,
+              old_q: int | None = None, old_present: bool | None = None) -> int:
+    """JRQ_CONF(): quorums default to Ballot.init's |conf|/2+1 (Ballot.java:77-83)."""
+    if new_q is None:
+        new_q = bin(new_mask).count("1") // 2 + 1
+    if old_present is None:
+        old_present = old_mask != 0 or (old_q is not None and old_q > 0)
+    if old_q is None:
+        old_q = (bin(old_mask).count("1") // 2 + 1) if old_present else 0
+    return (new_mask & 0xFFFF) | ((old_mask & 0xFFFF) << 16) | ((new_q & 0xFF) << 32) | \
+        ((old_q & 0xFF) << 40)

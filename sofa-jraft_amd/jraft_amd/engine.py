@@ -1,0 +1,182 @@
+"""Engine: Python handle on a libjrq.so engine (one per GPU / host thread).
+
+Host-pointer methods take numpy arrays and return numpy arrays (the path a Java
+host takes with DirectByteBuffers).  ``*_dev`` methods take device buffers that
+expose ``data_ptr()`` (torch tensors on ``cuda:N``) and run asynchronously on the
+engine's stream; ``use_stream`` makes the engine launch on a caller's stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import GroupBatch, check
+
+
+def _np_ptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def _dev_ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _c(a, dtype):
+    return None if a is None else np.ascontiguousarray(a, dtype=dtype)
+
+
+class Engine:
+    def __init__(self, device: int = 0, max_groups: int = 1 << 20, max_peers: int = 16):
+        self._L = _lib.load()
+        err = C.c_int(0)
+        h = self._L.jrq_create(device, max_groups, max_peers, C.byref(err))
+        if not h:
+            raise _lib.JrqError(err.value, (self._L.jrq_last_error(None) or b"").decode())
+        self._h = C.c_void_p(h)
+        self.device = device
+
+    # ------------------------------------------------------------ lifetime --
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.jrq_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def stream(self) -> int:
+        return int(self._L.jrq_get_stream(self._h) or 0)
+
+    def use_stream(self, stream_handle: int | None):
+        """Launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""
+        check(self._L.jrq_set_stream(self._h, C.c_void_p(stream_handle) if stream_handle else None),
+              self._h)
+
+    def synchronize(self):
+        check(self._L.jrq_synchronize(self._h), self._h)
+
+    # -------------------------------------------------------------- quorum --
+    @staticmethod
+    def _batch(ptr, match, pending_index, last_appended, last_committed, conf, run_off, run_start,
+               run_conf, num_peers, match_ld, num_runs):
+        b = GroupBatch()
+        b.match = ptr(match)
+        b.pending_index = ptr(pending_index)
+        b.last_appended = ptr(last_appended)
+        b.last_committed = ptr(last_committed)
+        b.conf = ptr(conf)
+        b.run_off = ptr(run_off)
+        b.run_start = ptr(run_start)
+        b.run_conf = ptr(run_conf)
+        b.num_peers = num_peers
+        b.num_runs = num_runs
+        b.match_ld = match_ld
+        return b
+
+    def quorum_epoch(self, match, pending_index, last_appended, last_committed, conf=None,
+                     run_off=None, run_start=None, run_conf=None):
+        """Host variant: numpy in, (committed int64[G], status uint8[G]) out."""
+        match = _c(match, np.int64)
+        P, G = match.shape
+        arrs = dict(match=match, pending_index=_c(pending_index, np.int64),
+                    last_appended=_c(last_appended, np.int64),
+                    last_committed=_c(last_committed, np.int64), conf=_c(conf, np.uint64),
+                    run_off=_c(run_off, np.uint32), run_start=_c(run_start, np.int64),
+                    run_conf=_c(run_conf, np.uint64))
+        nr = 0 if arrs["run_start"] is None else len(arrs["run_start"])
+        b = self._batch(_np_ptr, num_peers=P, match_ld=G, num_runs=nr, **arrs)
+        committed = np.zeros(G, dtype=np.int64)
+        status = np.zeros(G, dtype=np.uint8)
+        check(self._L.jrq_quorum_epoch(self._h, C.byref(b), _np_ptr(committed), _np_ptr(status), G),
+              self._h)
+        return committed, status
+
+    def quorum_epoch_dev(self, match, pending_index, last_appended, last_committed, conf,
+                         committed_out, status_out, run_off=None, run_start=None, run_conf=None):
+        """Device variant: torch tensors (match shape [P, ld]); asynchronous on the engine stream."""
+        P = match.shape[0]
+        G = pending_index.shape[0]
+        b = self._batch(_dev_ptr, match, pending_index, last_appended, last_committed, conf,
+                        run_off, run_start, run_conf, num_peers=P, match_ld=match.stride(0),
+                        num_runs=0 if run_start is None else run_start.shape[0])
+        check(self._L.jrq_quorum_epoch_dev(self._h, C.byref(b), _dev_ptr(committed_out),
+                                           _dev_ptr(status_out), G), self._h)
+
+    # ------------------------------------------------------------ checksum --
+    def crc64_batch(self, payload, offsets):
+        payload = _c(payload, np.uint8)
+        offsets = _c(offsets, np.uint64)
+        n = len(offsets) - 1
+        out = np.zeros(max(n, 0), dtype=np.uint64)
+        if n > 0:
+            if payload.size == 0:
+                payload = np.zeros(1, np.uint8)
+            check(self._L.jrq_crc64_batch(self._h, _np_ptr(payload), _np_ptr(offsets), n,
+                                          _np_ptr(out)), self._h)
+        return out
+
+    def crc64_batch_dev(self, payload, offsets, out, n=None):
+        n = offsets.shape[0] - 1 if n is None else n
+        check(self._L.jrq_crc64_batch_dev(self._h, _dev_ptr(payload), _dev_ptr(offsets), n,
+                                          _dev_ptr(out)), self._h)
+
+    def logentry_checksum_batch(self, etype, index, term, peer_xor, payload, offsets,
+                                expected=None, has=None):
+        etype = _c(etype, np.uint8)
+        index = _c(index, np.int64)
+        term = _c(term, np.int64)
+        peer_xor = _c(peer_xor, np.uint64)
+        payload = _c(payload, np.uint8)
+        if payload.size == 0:
+            payload = np.zeros(1, np.uint8)
+        offsets = _c(offsets, np.uint64)
+        expected = _c(expected, np.uint64)
+        has = _c(has, np.uint8)
+        n = len(offsets) - 1
+        out = np.zeros(n, dtype=np.uint64)
+        corrupt = np.zeros(n, dtype=np.uint8) if expected is not None else None
+        if n > 0:
+            check(self._L.jrq_logentry_checksum_batch(
+                self._h, _np_ptr(etype), _np_ptr(index), _np_ptr(term), _np_ptr(peer_xor),
+                _np_ptr(payload), _np_ptr(offsets), n, _np_ptr(out), _np_ptr(expected),
+                _np_ptr(has), _np_ptr(corrupt)), self._h)
+        return out if corrupt is None else (out, corrupt)
+
+    def logentry_checksum_batch_dev(self, etype, index, term, peer_xor, payload, offsets, out,
+                                    expected=None, has=None, corrupt=None, n=None):
+        n = offsets.shape[0] - 1 if n is None else n
+        check(self._L.jrq_logentry_checksum_batch_dev(
+            self._h, _dev_ptr(etype), _dev_ptr(index), _dev_ptr(term), _dev_ptr(peer_xor),
+            _dev_ptr(payload), _dev_ptr(offsets), n, _dev_ptr(out), _dev_ptr(expected),
+            _dev_ptr(has), _dev_ptr(corrupt)), self._h)
+
+    # ---------------------------------------------------------------- RCCL --
+    @staticmethod
+    def rccl_unique_id() -> bytes:
+        L = _lib.load()
+        buf = (C.c_uint8 * 128)()
+        check(L.jrq_rccl_get_unique_id(buf))
+        return bytes(buf)
+
+    def rccl_init(self, nranks: int, rank: int, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        check(self._L.jrq_rccl_init(self._h, nranks, rank, buf), self._h)
+
+    def publish_committed_dev(self, local, global_out):
+        check(self._L.jrq_publish_committed_dev(self._h, _dev_ptr(local), _dev_ptr(global_out),
+                                                local.shape[0]), self._h)

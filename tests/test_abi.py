@@ -1,0 +1,66 @@
+"""CPU: libjrq.so loads and exports exactly the C ABI of include/jrq.h; no compute here.
+
+Without a GPU the engine must refuse to start (no silent CPU fallback)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from jraft_amd import _lib
+
+
+def declared_functions():
+    text = open(_lib.HEADER_PATH).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(jrq_[a-z0-9_]+)\s*\(", text)))
+
+
+def exported_functions():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    return sorted(set(m.group(1) for m in re.finditer(r" T (jrq_[a-z0-9_]+)$", out, re.M)))
+
+
+def test_library_built():
+    assert os.path.exists(_lib.LIB_PATH), "run __graft_entry__.build()"
+
+
+def test_every_declared_symbol_is_exported():
+    decl = declared_functions()
+    assert len(decl) >= 18
+    exp = exported_functions()
+    missing = [f for f in decl if f not in exp]
+    assert not missing, missing
+    extra = [f for f in exp if f not in decl]
+    assert not extra, f"exported but not in include/jrq.h: {extra}"
+
+
+def test_ctypes_signatures_cover_header():
+    names = {s[0] for s in _lib.SIGNATURES}
+    assert names == set(declared_functions())
+    L = _lib.load()
+    assert L.jrq_abi_version() == 1
+
+
+def test_group_batch_layout_matches_header():
+    # 8 pointers + 2 uint32 + uint64 = 80 bytes on LP64
+    assert ctypes.sizeof(_lib.GroupBatch) == 80
+
+
+def test_conf_word_packing():
+    w = _lib.conf_word(0b11111, 0b00111)
+    assert w & 0xFFFF == 0b11111 and (w >> 16) & 0xFFFF == 0b111
+    assert (w >> 32) & 0xFF == 3 and (w >> 40) & 0xFF == 2
+    assert (_lib.conf_word(0b111) >> 40) & 0xFF == 0  # oldConf == null
+    assert (_lib.conf_word(0b111, 0, old_present=True) >> 40) & 0xFF == 1  # empty oldConf
+
+
+def test_create_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from jraft_amd import Engine, JrqError
+    with pytest.raises(JrqError):
+        Engine(0)

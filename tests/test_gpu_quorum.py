@@ -1,0 +1,117 @@
+"""GPU parity: libjrq quorum epoch kernel vs replaying the same acks through the
+oracle's Java-faithful BallotBox (jraft-core/.../core/BallotBox.java:96-139,
+entity/Ballot.java:63-140).  Bit-exact on committed index and status flags.
+"""
+import numpy as np
+import pytest
+
+from jraft_amd import ST_NOT_LEADER, conf_word
+from jraft_amd import workloads as W
+from quorum_cases import even_removal_batch, random_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _replay(oracle, b, runs=True, chunk=7):
+    kw = dict(run_off=b["run_off"], run_start=b["run_start"], run_conf=b["run_conf"]) if runs else {}
+    c, s, _ = oracle.quorum_epoch_replay(b["match"], b["pending_index"], b["last_appended"],
+                                         b["last_committed"], b["conf"], chunk=chunk, **kw)
+    return c, s
+
+
+def _gpu(engine, b, runs=True):
+    kw = dict(run_off=b["run_off"], run_start=b["run_start"], run_conf=b["run_conf"]) if runs else {}
+    return engine.quorum_epoch(b["match"], b["pending_index"], b["last_appended"],
+                               b["last_committed"], b["conf"], **kw)
+
+
+def test_ballot_box_test_scenario(engine):
+    """BallotBoxTest.testCommitAt: conf {8081,8082,8083}, oldConf {8081}; acks from 8081 then
+    8082 on entry 1 commit index 1 (jraft-core/src/test/.../core/BallotBoxTest.java:109-137)."""
+    b = dict(match=np.array([[1], [1], [0]], np.int64), pending_index=np.array([1], np.int64),
+             last_appended=np.array([1], np.int64), last_committed=np.array([0], np.int64),
+             conf=np.array([conf_word(0b111, 0b001)], np.uint64))
+    c, s = _gpu(engine, b, runs=False)
+    assert c[0] == 1 and s[0] == 0
+    b["match"] = np.array([[1], [0], [0]], np.int64)  # only 8081: new quorum 2 not reached
+    c, s = _gpu(engine, b, runs=False)
+    assert c[0] == 0
+
+
+def test_not_leader_returns_state(engine):
+    b = dict(match=np.array([[5], [5], [5]], np.int64), pending_index=np.array([0], np.int64),
+             last_appended=np.array([5], np.int64), last_committed=np.array([3], np.int64),
+             conf=np.array([conf_word(0b111)], np.uint64))
+    c, s = _gpu(engine, b, runs=False)
+    assert c[0] == 3 and s[0] == ST_NOT_LEADER
+
+
+def test_even_size_removal(engine, oracle):
+    b = even_removal_batch()
+    c, s = _gpu(engine, b)
+    ce, se = _replay(oracle, b)
+    assert c[0] == ce[0] == 15
+    assert s[0] == se[0]
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 7, 8, 16])
+def test_random_batches(engine, oracle, P):
+    b = random_batch(100 + P, 3000, P)
+    c, s = _gpu(engine, b)
+    ce, se = _replay(oracle, b)
+    np.testing.assert_array_equal(c, ce)
+    np.testing.assert_array_equal(s, se)
+
+
+@pytest.mark.parametrize("P", [3, 5])
+def test_random_batches_single_run(engine, oracle, P):
+    b = random_batch(200 + P, 3000, P, run_prob=0.0)
+    c, s = _gpu(engine, b, runs=False)
+    ce, se = _replay(oracle, b, runs=False)
+    np.testing.assert_array_equal(c, ce)
+    np.testing.assert_array_equal(s, se)
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_config_shapes_vs_replay(engine, oracle, cfg):
+    """C2 / C3 shaped groups (1k pending each, 1024-entry ack chunks as the Replicator sends,
+    RaftOptions.maxEntriesSize = 1024) replayed through real BallotBoxes."""
+    b = W.quorum_batch(cfg, groups=2000)
+    c, s = _gpu(engine, b, runs=False)
+    ce, se = _replay(oracle, b, runs=False, chunk=1024)
+    np.testing.assert_array_equal(c, ce)
+    np.testing.assert_array_equal(s, se)
+
+
+def test_full_c3_sampled_and_properties(engine, oracle):
+    """Full C3 (1M groups x 5 peers, joint): device-resident path; 4096 random groups are
+    replayed through the oracle; every group satisfies lc <= committed <= lastAppended and
+    a second epoch on the committed state is idempotent."""
+    import torch
+    b = W.quorum_batch("C3")
+    G = b["pending_index"].shape[0]
+    dev = torch.device("cuda:0")
+    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v).to(dev)
+         for k, v in b.items()}
+    committed = torch.empty(G, dtype=torch.int64, device=dev)
+    status = torch.empty(G, dtype=torch.uint8, device=dev)
+    engine.use_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        engine.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
+                                t["last_committed"], t["conf"], committed, status)
+        again = torch.empty_like(committed)
+        st2 = torch.empty_like(status)
+        engine.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"], committed,
+                                t["conf"], again, st2)
+        torch.cuda.synchronize()
+    finally:
+        engine.use_stream(None)
+    c = committed.cpu().numpy()
+    assert (c >= b["last_committed"]).all() and (c <= b["last_appended"]).all()
+    np.testing.assert_array_equal(again.cpu().numpy(), c)
+    rng = np.random.default_rng(3)
+    idx = rng.choice(G, 4096, replace=False)
+    sub = {k: (v[:, idx] if k == "match" else v[idx]) for k, v in b.items()}
+    ce, se = _replay(oracle, sub, runs=False, chunk=1024)
+    np.testing.assert_array_equal(c[idx], ce)
+    np.testing.assert_array_equal(status.cpu().numpy()[idx], se)

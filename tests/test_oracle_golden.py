@@ -1,0 +1,187 @@
+"""CPU: the oracle against the golden fixtures and the reference's own tests, restated.
+
+Reference tests re-expressed (jraft-core/src/test/java/com/alipay/sofa/jraft/...):
+  entity/BallotTest.java:37-50, core/BallotBoxTest.java:62-154, util/CrcUtilTest.java:27-42,
+  entity/LogEntryTest.java:95-125, entity/LogIdTest.java:42-50, entity/PeerIdTest.java:72-78.
+"""
+import hashlib
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+# ------------------------------------------------------------------ CRC64 ---
+
+def test_table_matches_reference_pin(oracle):
+    """The generated table equals the literal CRC_TABLE of CRC64.java:41-92 (pinned digest)."""
+    pin = load("crc64_table_pin.json")
+    t = oracle.table()
+    assert hashlib.sha256(t.astype("<u8").tobytes()).hexdigest() == pin["sha256_le_u64"]
+    for i, v in pin["spot"].items():
+        assert int(t[int(i)]) == int(v, 16)
+    assert [int(x) for x in t] == oracle.py_table()
+
+
+def test_catalogue_check_value(oracle):
+    assert oracle.crc64(b"123456789") == 0x6C40DF5F0B497347
+    assert oracle.crc64(b"") == 0
+    assert oracle.crc64(None) == 0  # CrcUtil.crc64(null) -> 0 (CrcUtil.java:37-39)
+
+
+def test_golden_crc_vectors(oracle):
+    g = load("crc64_vectors.json")
+    payload = np.frombuffer(bytes.fromhex(g["payload_hex"]), dtype=np.uint8)
+    offs = np.array(g["offsets"], dtype=np.uint64)
+    got = oracle.crc64_batch(payload, offs)
+    assert [f"0x{int(x):016X}" for x in got] == g["crc64"]
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.binary(max_size=300))
+def test_c_oracle_equals_python_restatement(oracle, data):
+    assert oracle.crc64(data) == oracle.py_crc64(data)
+
+
+def test_crc_util_heap_direct_array_consistency(oracle):
+    """CrcUtilTest: byte[] / heap buffer / direct buffer give the same value; with an
+    array offset the value is that of the sub-range."""
+    rng = random.Random(5)
+    b = bytes(rng.getrandbits(8) for _ in range(1000))
+    whole = oracle.crc64(b)
+    assert oracle.crc64(memoryview(b)) == whole
+    assert oracle.crc64(b[10:500]) == oracle.py_crc64(b[10:500])
+
+
+def test_continuation_equals_concatenation(oracle):
+    a, b = b"raft-", b"group-log"
+    assert oracle.py_crc64(b, oracle.py_crc64(a)) == oracle.crc64(a + b)
+
+
+# ------------------------------------------------------------ entities ---
+
+def test_entity_vectors(oracle):
+    g = load("entity_vectors.json")
+    assert int(g["crc64_check_123456789"], 16) == 0x6C40DF5F0B497347
+    for v in g["logid"]:
+        assert oracle.logid_checksum(v["index"], v["term"]) == int(v["checksum"], 16)
+        assert oracle.py_logid_checksum(v["index"], v["term"]) == int(v["checksum"], 16)
+    for v in g["peerid"]:
+        assert oracle.peerid_checksum(v["ip"], v["port"], v["idx"]) == int(v["checksum"], 16)
+        assert oracle.py_peerid_checksum(v["ip"], v["port"], v["idx"]) == int(v["checksum"], 16)
+    for v in g["logentry"]:
+        assert oracle.logentry_checksum(v["type"], v["index"], v["term"], int(v["peer_xor"], 16),
+                                        v["data"].encode()) == int(v["checksum"], 16)
+
+
+def test_logentry_test_semantics(oracle):
+    """LogEntryTest.testChecksum: non-zero, stable, index or data change -> isCorrupted."""
+    px = oracle.peerid_checksum("localhost", 99, 1) ^ oracle.peerid_checksum("localhost", 100, 2)
+    c = oracle.logentry_checksum(1, 100, 3, px, b"hello")
+    assert c != 0 and c == oracle.logentry_checksum(1, 100, 3, px, b"hello")
+    assert oracle.logentry_checksum(1, 1, 3, px, b"hello") != c
+    assert oracle.logentry_checksum(1, 100, 3, px, b"hEllo") != c
+    # isCorrupted through the batch form with expected/has
+    payload = np.frombuffer(b"hellohEllo", np.uint8).copy()
+    offs = np.array([0, 5, 10], np.uint64)
+    out, corrupt = oracle.logentry_checksum_batch([1, 1], [100, 100], [3, 3], [px, px], payload,
+                                                  offs, expected=[c, c], has=[1, 1])
+    assert list(corrupt) == [0, 1]
+    _, corrupt = oracle.logentry_checksum_batch([1, 1], [100, 100], [3, 3], [px, px], payload,
+                                                offs, expected=[c, c], has=[1, 0])
+    assert list(corrupt) == [0, 0]  # no checksum -> never corrupted (hasChecksum false)
+
+
+def test_logid_checksum_stable_nonzero(oracle):
+    """LogIdTest.testChecksum: LogId(1,2) checksum non-zero and stable."""
+    assert oracle.logid_checksum(1, 2) != 0
+    assert oracle.logid_checksum(1, 2) == oracle.logid_checksum(1, 2)
+
+
+def test_peerid_checksum(oracle):
+    """PeerIdTest.testChecksum: 192.168.1.1:8081:1."""
+    c = oracle.peerid_checksum("192.168.1.1", 8081, 1)
+    assert c != 0 and c == oracle.py_crc64(b"192.168.1.1:8081:1")
+
+
+# -------------------------------------------------------------- Ballot ---
+
+def test_ballot_test_grant(oracle):
+    """BallotTest.testGrant: conf {8081,8082,8083}; unknown 8084 never counts."""
+    bb = oracle.BallotBox()
+    assert bb.reset_pending_index(1)
+    assert bb.append_pending_task([0, 1, 2])
+    assert bb.commit_at(1, 1, 0) and bb.last_committed_index == 0
+    assert bb.commit_at(1, 1, 3) and bb.last_committed_index == 0
+    assert bb.commit_at(1, 1, 1) and bb.last_committed_index == 1
+
+
+def test_ballot_box_test(oracle):
+    """BallotBoxTest.testCommitAt / testSetLastCommittedIndex* / testResetPendingIndex."""
+    bb = oracle.BallotBox()
+    assert not bb.commit_at(1, 3, 0)
+    assert bb.reset_pending_index(1)
+    assert bb.append_pending_task([0, 1, 2], [0])
+    assert bb.last_committed_index == 0
+    with pytest.raises(IndexError):
+        bb.commit_at(1, 3, 0)
+    assert bb.commit_at(1, 1, 0)
+    assert bb.last_committed_index == 0 and bb.pending_index == 1
+    assert bb.commit_at(1, 1, 1)
+    assert bb.last_committed_index == 1 and bb.pending_index == 2
+    assert bb.on_committed_calls == 1 and bb.on_committed_last == 1  # verify(waiter, only())
+    bb2 = oracle.BallotBox()
+    assert bb2.reset_pending_index(1)
+    with pytest.raises(ValueError):
+        bb2.set_last_committed_index(1)
+    bb3 = oracle.BallotBox()
+    assert not bb3.set_last_committed_index(-1)
+    bb4 = oracle.BallotBox()
+    assert bb4.set_last_committed_index(1) and bb4.last_committed_index == 1
+    assert bb4.on_committed_calls == 1
+    bb5 = oracle.BallotBox()
+    assert not bb5.append_pending_task([0, 1, 2], [0])  # pendingIndex 0
+    assert bb5.reset_pending_index(1) and bb5.append_pending_task([0, 1, 2], [0])
+    assert bb5.queue_size == 1
+    bb5.clear_pending_tasks()
+    assert bb5.queue_size == 0 and bb5.pending_index == 0
+
+
+def test_golden_ballot_box_traces(oracle):
+    """Every recorded call result and post-state of tests/golden/ballot_box_traces.json."""
+    for tr in load("ballot_box_traces.json")["traces"]:
+        bb = oracle.BallotBox()
+        for s in tr["steps"]:
+            c = s["call"]
+            try:
+                if c[0] == "reset":
+                    r = bb.reset_pending_index(c[1])
+                elif c[0] == "append":
+                    r = bb.append_pending_task(c[1], c[2])
+                elif c[0] == "commit":
+                    r = bb.commit_at(c[1], c[2], c[3])
+                elif c[0] == "setlc":
+                    r = bb.set_last_committed_index(c[1])
+                else:
+                    bb.clear_pending_tasks()
+                    r = None
+            except IndexError:
+                r = "AIOOBE"
+            except ValueError:
+                r = "IAE"
+            assert r == s["result"], (tr["name"], c)
+            assert bb.last_committed_index == s["last_committed"], (tr["name"], c)
+            assert bb.pending_index == s["pending_index"]
+            assert bb.queue_size == s["queue_size"]
+            assert bb.on_committed_calls == s["on_committed_calls"]

@@ -1,0 +1,24 @@
+#!/bin/bash
+# GPU session driver: each GPU step under its own time limit; stop at the first
+# crash / abort / timeout (exit >= 124), continue past ordinary test failures (exit 1).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+mkdir -p gpurun_out
+run() {  # run <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-"tests smoke bench"}
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 ;;
+    smoke) run smoke 300 python __graft_entry__.py smoke ;;
+    bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
+    prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu ;;
+  esac
+done
