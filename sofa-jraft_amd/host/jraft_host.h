@@ -1,0 +1,193 @@
+// jraft_host.h -- C++ host-side mirror of SOFAJRaft's hot-path API over libjrq.so.
+//
+// The reference host is Java (JDK absent in this image, SURVEY.md env probes), so the
+// host side above the C ABI is written in C++ with the reference's class and method
+// names, argument meaning and error behaviour:
+//   jraft::BallotBox  <- jraft-core/.../core/BallotBox.java (commitAt, appendPendingTask,
+//                        resetPendingIndex, setLastCommittedIndex, clearPendingTasks,
+//                        getLastCommittedIndex, describe, shutdown)
+//   jraft::LogEntry   <- jraft-core/.../entity/LogEntry.java (checksum, isCorrupted, setChecksum)
+//   jraft::CrcUtil    <- jraft-core/.../util/CrcUtil.java (crc64 of byte ranges)
+//   jraft::PeerId / Configuration (peers only; learners never vote, Configuration.java:184-186)
+// Exceptions mirror the Java ones: std::out_of_range for ArrayIndexOutOfBoundsException,
+// std::invalid_argument for IllegalArgumentException (Requires.requireTrue).
+//
+// Every checksum and every quorum decision is computed by libjrq.so on the GPU.  The
+// BallotBox objects of many groups share one GroupBatch; acks are recorded at call time
+// (with the reference's synchronous checks) and decided in batched epochs by flush(),
+// after which the FSMCaller waiter sees onCommitted(index) exactly as the reference calls it.
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/jrq.h"
+
+namespace jraft {
+
+// ------------------------------------------------------------------ entities
+
+struct PeerId {
+  std::string ip;
+  int32_t port = 0;
+  int32_t idx = 0;
+  PeerId() = default;
+  PeerId(std::string ip_, int32_t port_, int32_t idx_ = 0) : ip(std::move(ip_)), port(port_), idx(idx_) {}
+  // PeerId.toString (PeerId.java:135-144): ip:port[:idx]
+  std::string toString() const;
+  // PeerId.parse (PeerId.java:150-170): "ip:port" or "ip:port:idx"
+  static bool parse(const std::string& s, PeerId* out);
+  bool operator==(const PeerId& o) const { return ip == o.ip && port == o.port && idx == o.idx; }
+  bool operator<(const PeerId& o) const {
+    return ip != o.ip ? ip < o.ip : (port != o.port ? port < o.port : idx < o.idx);
+  }
+};
+
+struct Configuration {
+  std::vector<PeerId> peers;     // voting members, in order (duplicates kept, as ArrayList)
+  std::vector<PeerId> learners;  // never vote
+  // Configuration.parse (Configuration.java:285-311): "a:1,b:2,c:3/learner"
+  static Configuration parse(const std::string& s);
+  bool isEmpty() const { return peers.empty(); }
+  bool operator==(const Configuration& o) const { return peers == o.peers && learners == o.learners; }
+};
+
+enum class EntryType : int32_t { UNKNOWN = 0, NO_OP = 1, DATA = 2, CONFIGURATION = 3 };
+
+struct LogId {
+  int64_t index = 0;
+  int64_t term = 0;
+};
+
+class Engine;  // owns one jrq_engine
+
+// LogEntry (LogEntry.java): checksum fields; data is a byte range owned by the entry.
+struct LogEntry {
+  EntryType type = EntryType::UNKNOWN;
+  LogId id;
+  std::vector<PeerId> peers, oldPeers, learners, oldLearners;
+  std::vector<uint8_t> data;
+  bool hasChecksum_ = false;
+  uint64_t checksum_ = 0;
+
+  uint64_t checksum(Engine& eng) const;          // LogEntry.checksum (:88-99), on the GPU
+  bool isCorrupted(Engine& eng) const;           // :156-158
+  void setChecksum(uint64_t c) { checksum_ = c; hasChecksum_ = true; }  // :169-172
+  bool hasChecksum() const { return hasChecksum_; }                    // :147-149
+  uint64_t getChecksum() const { return checksum_; }
+};
+
+// ------------------------------------------------------------------- engine
+
+class Engine {
+ public:
+  explicit Engine(int device = 0, uint32_t max_groups = 1u << 20, uint8_t max_peers = 16);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+  jrq_engine* raw() { return e_; }
+
+  // CrcUtil.crc64 over many byte ranges at once (CrcUtil.java:36-80): one GPU batch.
+  std::vector<uint64_t> crc64(const std::vector<std::vector<uint8_t>>& items);
+  // LogEntry.checksum for a batch (LogEntry.java:88-108); PeerId checksums of every
+  // distinct peer are computed in the same style (GPU CRC batch of the peer strings).
+  std::vector<uint64_t> checksum(const std::vector<const LogEntry*>& entries);
+  // isCorrupted for a batch: hasChecksum && stored != checksum() (:156-158).
+  std::vector<uint8_t> verify(const std::vector<const LogEntry*>& entries);
+
+ private:
+  uint64_t peerXor(const LogEntry& e, std::map<std::string, uint64_t>& cache);
+  jrq_engine* e_ = nullptr;
+};
+
+class CrcUtil {
+ public:
+  // CrcUtil.crc64(byte[]) / (byte[], off, len) (CrcUtil.java:36-57); null -> 0.
+  static uint64_t crc64(Engine& eng, const uint8_t* array, size_t offset, size_t length);
+  static uint64_t crc64(Engine& eng, const std::vector<uint8_t>& array) {
+    return crc64(eng, array.data(), 0, array.size());
+  }
+};
+
+// --------------------------------------------------------------- ballot box
+
+// FSMCaller.onCommitted (FSMCallerImpl.java:239-244) as seen by BallotBox.
+using CommitWaiter = std::function<void(int64_t lastCommittedIndex)>;
+
+struct BallotBoxOptions {
+  CommitWaiter waiter;  // BallotBoxOptions.getWaiter (must be set, BallotBox.java:82-90)
+  bool closureQueue = true;  // stands for the non-null ClosureQueue requirement
+};
+
+class GroupBatch;
+
+// One Raft group's BallotBox (BallotBox.java), backed by a shared GroupBatch.
+class BallotBox {
+ public:
+  BallotBox(std::shared_ptr<GroupBatch> batch, uint32_t group);
+  bool init(const BallotBoxOptions& opts);                                     // :82-90
+  // :96-139 -- false if not leader; true if last < pendingIndex (stale); throws
+  // std::out_of_range when last >= pendingIndex + queue size; otherwise records the ack,
+  // decided at the next GroupBatch::flush().  Acks of one peer must be contiguous from
+  // pendingIndex (the Replicator invariant, Replicator.java:1387-1401): a gap throws
+  // std::logic_error.
+  bool commitAt(int64_t firstLogIndex, int64_t lastLogIndex, const PeerId& peer);
+  void clearPendingTasks();                                                    // :147-156
+  bool resetPendingIndex(int64_t newPendingIndex);                             // :167-186
+  // :197-215 -- oldConf == nullptr means a stable configuration
+  bool appendPendingTask(const Configuration& conf, const Configuration* oldConf,
+                         std::function<void(bool)> done = {});
+  bool setLastCommittedIndex(int64_t lastCommittedIndex);                      // :223-248
+  int64_t getLastCommittedIndex() const;                                       // :67-79
+  int64_t getPendingIndex() const;
+  int64_t getPendingMetaQueueSize() const;
+  std::string describe() const;                                                // :256-281
+  void shutdown() { clearPendingTasks(); }
+
+ private:
+  std::shared_ptr<GroupBatch> batch_;
+  uint32_t g_;
+};
+
+// Engine-backed state of G groups (SoA, include/jrq.h jrq_group_batch layout).
+class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
+ public:
+  // eng may be null until the first flush() (host-only state checks need no GPU)
+  GroupBatch(Engine* eng, uint32_t groups, uint32_t peers);
+  uint32_t groups() const { return G_; }
+  uint32_t peers() const { return P_; }
+  // One epoch: evaluate every group with a pending queue on the GPU, advance
+  // pendingIndex / lastCommittedIndex, drop committed ballots, call waiters.
+  // Returns the number of groups whose commit index advanced.
+  uint32_t flush();
+
+ private:
+  friend class BallotBox;
+  struct Run {
+    int64_t start;
+    uint64_t conf;
+  };
+  struct Group {
+    CommitWaiter waiter;
+    bool inited = false;
+    int64_t pendingIndex = 0;
+    int64_t lastCommitted = 0;
+    int64_t lastAppended = -1;  // pendingIndex + queue size - 1
+    std::vector<Run> runs;
+    std::map<PeerId, int> slot;  // PeerId -> peer slot (<= P)
+    std::vector<int64_t> match;  // per slot, highest contiguous ack
+    std::vector<std::function<void(bool)>> closures;
+  };
+  int slotOf(Group& g, const PeerId& p, bool create);
+  uint64_t confWord(Group& g, const Configuration& conf, const Configuration* old);
+  Engine* eng_;
+  uint32_t G_, P_;
+  std::vector<Group> grp_;
+};
+
+}  // namespace jraft
