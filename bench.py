@@ -157,8 +157,12 @@ def main():
         return float(t.item())
 
     eng = Engine(local)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-default) stream: the kernels and the HIP events bracketing them
+    # must be on the same stream (the default stream's handle is 0 = "engine's own")
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     eng.use_stream(stream.cuda_stream)
+    assert eng.stream() == stream.cuda_stream != 0
 
     def sync():
         torch.cuda.synchronize(dev)

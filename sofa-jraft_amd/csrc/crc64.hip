@@ -82,7 +82,7 @@ __device__ __forceinline__ uint64_t crc_value(const RState& r) {
 }
 
 // CRC of payload[a, b) from a zero register.
-__device__ uint64_t crc_range(const uint8_t* __restrict__ payload, uint64_t a, uint64_t b,
+__device__ __forceinline__ uint64_t crc_range(const uint8_t* __restrict__ payload, uint64_t a, uint64_t b,
                               const char* lds, uint32_t lc) {
   RState r{0u, 0u};
   uint64_t p = a;
@@ -91,31 +91,51 @@ __device__ uint64_t crc_range(const uint8_t* __restrict__ payload, uint64_t a, u
     step1(r, payload[p], lds, lc);
     ++p;
   }
-  if (p + 64 <= b) {  // 64-byte blocks, next block's loads in flight while hashing this one
+  const uint64_t nblk = (b - p) >> 6;
+  if (nblk != 0) {
+    // 64-byte blocks through a 3-deep register ring: the loads of block i+2 are issued
+    // before block i is hashed, unconditionally (the address is clamped to the last
+    // block), so the compiler's wait before block i is a counted vmcnt(8), not vmcnt(0).
+    // Unrolled by three with fixed buffer roles: a loaded register is never copied
+    // (a copy would force the wait early).  The empty asm after each load group is a
+    // compiler memory barrier: the loads may not be re-issued (rematerialised) at
+    // their use two blocks later; it implies no hardware wait.
     const uint4* q = reinterpret_cast<const uint4*>(payload + p);
-    uint4 c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3];
-    for (;;) {
-      const uint64_t pn = p + 64;
-      const bool more = pn + 64 <= b;
-      uint4 n0, n1, n2, n3;
-      if (more) {
-        const uint4* qn = reinterpret_cast<const uint4*>(payload + pn);
-        n0 = qn[0];
-        n1 = qn[1];
-        n2 = qn[2];
-        n3 = qn[3];
-      }
-      step16(r, c0, lds, lc);
-      step16(r, c1, lds, lc);
-      step16(r, c2, lds, lc);
-      step16(r, c3, lds, lc);
-      p = pn;
-      if (!more) break;
-      c0 = n0;
-      c1 = n1;
-      c2 = n2;
-      c3 = n3;
+    const uint64_t last = nblk - 1;
+    uint4 A0, A1, A2, A3, B0, B1, B2, B3, C0, C1, C2, C3;
+#define JRQ_LOAD(X, blk)                                               \
+  do {                                                                 \
+    const uint64_t bb = (blk) < last ? (blk) : last;                   \
+    const uint4* qq = q + 4 * bb;                                      \
+    X##0 = qq[0];                                                      \
+    X##1 = qq[1];                                                      \
+    X##2 = qq[2];                                                      \
+    X##3 = qq[3];                                                      \
+    asm volatile("" ::: "memory");                                     \
+  } while (0)
+#define JRQ_HASH(X)            \
+  do {                         \
+    step16(r, X##0, lds, lc);  \
+    step16(r, X##1, lds, lc);  \
+    step16(r, X##2, lds, lc);  \
+    step16(r, X##3, lds, lc);  \
+  } while (0)
+    JRQ_LOAD(A, 0);
+    JRQ_LOAD(B, 1);
+    for (uint64_t i = 0;;) {
+      JRQ_LOAD(C, i + 2);
+      JRQ_HASH(A);
+      if (++i == nblk) break;
+      JRQ_LOAD(A, i + 2);
+      JRQ_HASH(B);
+      if (++i == nblk) break;
+      JRQ_LOAD(B, i + 2);
+      JRQ_HASH(C);
+      if (++i == nblk) break;
     }
+#undef JRQ_LOAD
+#undef JRQ_HASH
+    p += nblk << 6;
   }
   while (p + 16 <= b) {
     const uint4 v = *reinterpret_cast<const uint4*>(payload + p);

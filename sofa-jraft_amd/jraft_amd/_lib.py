@@ -75,6 +75,15 @@ def load() -> C.CDLL:
     """Load libjrq.so (raises if it was not built: no silent fallback)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7 /
+        # libhsa-runtime64.so.1 / librccl.so.1 (same SONAMEs as /opt/rocm's).  Whichever
+        # is loaded first is the one every later library binds to; if libjrq pulled in
+        # /opt/rocm's first, torch would then find no GPU.  So load torch's first when
+        # torch is installed (tensors, streams and libjrq then share one runtime).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise FileNotFoundError(
                 f"{LIB_PATH} missing: run `make -C sofa-jraft_amd` (or __graft_entry__.build())")

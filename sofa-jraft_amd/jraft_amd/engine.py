@@ -63,7 +63,9 @@ class Engine:
         return int(self._L.jrq_get_stream(self._h) or 0)
 
     def use_stream(self, stream_handle: int | None):
-        """Launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""
+        """Launch on an external hipStream_t (e.g. a torch.cuda.Stream().cuda_stream).
+
+        None (or 0, the default stream's handle) selects the engine's own stream."""
         check(self._L.jrq_set_stream(self._h, C.c_void_p(stream_handle) if stream_handle else None),
               self._h)
 

@@ -17,8 +17,14 @@ STEPS=${STEPS:-"tests smoke bench"}
 for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 ;;
+    crc)   run crc_tests 600 python -m pytest tests/test_gpu_crc.py -q -x -p no:cacheprovider --timeout 300 ;;
+    quorum) run quorum_tests 600 python -m pytest tests/test_gpu_quorum.py -q -x -p no:cacheprovider --timeout 300 ;;
+    quick) run bench_quick 600 python bench.py --steps 20 --warmup 3 --no-cpu ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu ;;
+    pmcf)  run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
+    pmcw)  run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
+    host)  run host_test 300 ./sofa-jraft_amd/lib/host_test gpu ;;
   esac
 done
