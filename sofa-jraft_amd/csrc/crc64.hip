@@ -82,8 +82,9 @@ __device__ __forceinline__ uint64_t crc_value(const RState& r) {
 }
 
 // CRC of payload[a, b) from a zero register.
-__device__ __forceinline__ uint64_t crc_range(const uint8_t* __restrict__ payload, uint64_t a, uint64_t b,
-                              const char* lds, uint32_t lc) {
+template <int BV>
+__device__ __forceinline__ uint64_t crc_range(const uint8_t* __restrict__ payload, uint64_t a,
+                                              uint64_t b, const char* lds, uint32_t lc) {
   RState r{0u, 0u};
   uint64_t p = a;
   const uint64_t mis = reinterpret_cast<uintptr_t>(payload) & 15u;
@@ -91,51 +92,42 @@ __device__ __forceinline__ uint64_t crc_range(const uint8_t* __restrict__ payloa
     step1(r, payload[p], lds, lc);
     ++p;
   }
-  const uint64_t nblk = (b - p) >> 6;
+  // Blocks of 16*BV bytes through a 2-deep register ring: block i+1's loads are issued
+  // before block i is hashed, unconditionally (address clamped to the last block), so
+  // the compiler's wait before block i is a counted vmcnt(BV), not vmcnt(0).  Unrolled
+  // by two with fixed buffer roles: a loaded register is never copied (a copy would
+  // force the wait early).  The empty asm after each load group is a compiler memory
+  // barrier: the loads may not be re-issued (rematerialised) at their use a block
+  // later; it implies no hardware wait.  BV = 8 reads whole 128-B lines per lane.
+  constexpr uint32_t kBlkBytes = 16u * BV;
+  const uint64_t nblk = (b - p) / kBlkBytes;
   if (nblk != 0) {
-    // 64-byte blocks through a 3-deep register ring: the loads of block i+2 are issued
-    // before block i is hashed, unconditionally (the address is clamped to the last
-    // block), so the compiler's wait before block i is a counted vmcnt(8), not vmcnt(0).
-    // Unrolled by three with fixed buffer roles: a loaded register is never copied
-    // (a copy would force the wait early).  The empty asm after each load group is a
-    // compiler memory barrier: the loads may not be re-issued (rematerialised) at
-    // their use two blocks later; it implies no hardware wait.
     const uint4* q = reinterpret_cast<const uint4*>(payload + p);
     const uint64_t last = nblk - 1;
-    uint4 A0, A1, A2, A3, B0, B1, B2, B3, C0, C1, C2, C3;
-#define JRQ_LOAD(X, blk)                                               \
-  do {                                                                 \
-    const uint64_t bb = (blk) < last ? (blk) : last;                   \
-    const uint4* qq = q + 4 * bb;                                      \
-    X##0 = qq[0];                                                      \
-    X##1 = qq[1];                                                      \
-    X##2 = qq[2];                                                      \
-    X##3 = qq[3];                                                      \
-    asm volatile("" ::: "memory");                                     \
+    uint4 A[BV], B[BV];
+#define JRQ_LOAD(X, blk)                                 \
+  do {                                                   \
+    const uint64_t bb = (blk) < last ? (blk) : last;     \
+    const uint4* qq = q + BV * bb;                       \
+    _Pragma("unroll") for (int v = 0; v < BV; ++v) X[v] = qq[v]; \
+    asm volatile("" ::: "memory");                       \
   } while (0)
-#define JRQ_HASH(X)            \
-  do {                         \
-    step16(r, X##0, lds, lc);  \
-    step16(r, X##1, lds, lc);  \
-    step16(r, X##2, lds, lc);  \
-    step16(r, X##3, lds, lc);  \
+#define JRQ_HASH(X)                                                          \
+  do {                                                                       \
+    _Pragma("unroll") for (int v = 0; v < BV; ++v) step16(r, X[v], lds, lc); \
   } while (0)
     JRQ_LOAD(A, 0);
-    JRQ_LOAD(B, 1);
     for (uint64_t i = 0;;) {
-      JRQ_LOAD(C, i + 2);
+      JRQ_LOAD(B, i + 1);
       JRQ_HASH(A);
       if (++i == nblk) break;
-      JRQ_LOAD(A, i + 2);
+      JRQ_LOAD(A, i + 1);
       JRQ_HASH(B);
-      if (++i == nblk) break;
-      JRQ_LOAD(B, i + 2);
-      JRQ_HASH(C);
       if (++i == nblk) break;
     }
 #undef JRQ_LOAD
 #undef JRQ_HASH
-    p += nblk << 6;
+    p += nblk * kBlkBytes;
   }
   while (p + 16 <= b) {
     const uint4 v = *reinterpret_cast<const uint4*>(payload + p);
@@ -196,6 +188,28 @@ __device__ __forceinline__ void emit(const JrqCrcArgs& a, uint32_t e, uint64_t v
   }
 }
 
+// One piece of an entry that spans `parts` segments: XOR its (already shifted) CRC into
+// the entry's scratch slot; the last of the `parts` arrivals publishes and re-zeroes it.
+// Hand-off = 8-byte agent-scope atomics on both sides (MI355X_MICROARCH.md, visibility
+// "valid forms"): the XOR is drained (s_waitcnt vmcnt(0)) before the arrival add, the last
+// arriver reads the slot with an atomic after its add returned.  No release/acquire
+// fences: those would write back the XCD's L2 / invalidate L1 on every piece.
+template <bool kLogEntry>
+__device__ __forceinline__ void straddle_piece(const JrqCrcArgs& a, uint32_t e, uint32_t slot,
+                                               uint32_t parts, uint64_t c) {
+  __hip_atomic_fetch_xor(&a.acc[slot], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint32_t arrived =
+      __hip_atomic_fetch_add(&a.cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (arrived + 1 == parts) {
+    // read-and-zero in one memory-side RMW (an xor-with-0 would be folded into a load)
+    const uint64_t v =
+        __hip_atomic_exchange(&a.acc[slot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    emit<kLogEntry>(a, e, v);
+    __hip_atomic_store(&a.cnt[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // First e in [0, n] with offsets[e] >= x (offsets[n] >= x is guaranteed by the caller).
 __device__ __forceinline__ uint32_t lower_bound_off(const uint64_t* __restrict__ off, uint32_t n,
                                                     uint64_t x) {
@@ -208,7 +222,7 @@ __device__ __forceinline__ uint32_t lower_bound_off(const uint64_t* __restrict__
   return lo;
 }
 
-template <bool kLogEntry>
+template <bool kLogEntry, int BV>
 __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
   const char* lds = reinterpret_cast<const char*>(lds_tab);
@@ -226,16 +240,32 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a)
   const uint64_t base = a.offsets[0];
   const uint64_t total = a.offsets[a.n] - base;
   const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  // segment size: power of two, ~total/lanes, at least 2^min_seg_log2
-  uint32_t s = a.min_seg_log2;
-  while (s < 40 && (total >> (s + 1)) >= lanes) ++s;
-  const uint64_t S = 1ull << s;
-  uint64_t nseg = (total + S - 1) >> s;
+  // Segment size S ~ total/lanes (>= 2^min_seg_log2).  All lanes walk their segments in
+  // lockstep, so lane l reads near l*S at any moment: S is an ODD multiple of 64 B so
+  // that those addresses spread over the memory channels (a power-of-two stride piles
+  // a whole wave onto a few of them).  seg_mode 0 keeps the power-of-two size (A/B).
+  uint64_t S;
+  if (a.seg_bytes != 0) {
+    S = a.seg_bytes;
+  } else if (a.seg_mode == 0) {
+    uint32_t s = a.min_seg_log2;
+    while (s < 40 && (total >> (s + 1)) >= lanes) ++s;
+    S = 1ull << s;
+  } else {
+    uint64_t t = (total + lanes - 1) / lanes;
+    const uint64_t floor_bytes = 1ull << a.min_seg_log2;
+    if (t < floor_bytes) t = floor_bytes;
+    S = (((t + 63) >> 6) | 1u) << 6;
+  }
+  // never more segments than straddler slots (scratch_len - 2)
+  const uint64_t s_min = (total + a.scratch_len - 3) / (a.scratch_len - 2);
+  if (S < s_min) S = s_min;
+  uint64_t nseg = (total + S - 1) / S;
   if (nseg == 0) nseg = 1;
 
   for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; k < nseg;
        k += lanes) {
-    const uint64_t s0 = base + (k << s);
+    const uint64_t s0 = base + k * S;
     const uint64_t s1 = (k + 1 == nseg) ? base + total : s0 + S;
     const bool last_seg = (k + 1 == nseg);
     uint32_t e = lower_bound_off(a.offsets, a.n, s0);
@@ -245,23 +275,12 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a)
     if (e > 0 && oe > s0) {
       const uint32_t t = e - 1;
       const uint64_t pe = oe < s1 ? oe : s1;
-      uint64_t c = crc_range(a.payload, s0, pe, lds, lc);
+      uint64_t c = crc_range<BV>(a.payload, s0, pe, lds, lc);
       c = crc_shift(c, oe - pe, a.shift);
       const uint64_t ot = a.offsets[t];
-      const uint64_t first = (ot - base) >> s, lastseg = (oe - 1 - base) >> s;
-      const uint32_t parts = static_cast<uint32_t>(lastseg - first + 1);
-      const uint32_t slot = static_cast<uint32_t>(first);
-      __hip_atomic_fetch_xor(&a.acc[slot], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t arrived =
-          __hip_atomic_fetch_add(&a.cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (arrived + 1 == parts) {
-        const uint64_t v =
-            __hip_atomic_fetch_xor(&a.acc[slot], 0ull, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        emit<kLogEntry>(a, t, v);
-        __hip_atomic_store(&a.acc[slot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.cnt[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      const uint64_t first = (ot - base) / S, lastseg = (oe - 1 - base) / S;
+      straddle_piece<kLogEntry>(a, t, static_cast<uint32_t>(first),
+                                static_cast<uint32_t>(lastseg - first + 1), c);
     }
 
     // entries that begin inside this segment (zero-length ones at the very end go to the last)
@@ -269,26 +288,15 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a)
       const uint64_t oe1 = a.offsets[e + 1];
       const uint64_t pe = oe1 < s1 ? oe1 : s1;
       const uint64_t fields = entry_fields<kLogEntry>(a, e, lds, lc);
-      uint64_t c = crc_range(a.payload, oe, pe, lds, lc);
+      uint64_t c = crc_range<BV>(a.payload, oe, pe, lds, lc);
       if (oe1 <= s1) {
         emit<kLogEntry>(a, e, c ^ fields);  // whole entry inside the segment
       } else {
         // head piece of a straddling entry: shift its data CRC to the entry end, add the fields
         c = crc_shift(c, oe1 - pe, a.shift) ^ fields;
-        const uint32_t slot = static_cast<uint32_t>(k);
-        const uint64_t lastseg = (oe1 - 1 - base) >> s;
-        const uint32_t parts = static_cast<uint32_t>(lastseg - k + 1);
-        __hip_atomic_fetch_xor(&a.acc[slot], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t arrived =
-            __hip_atomic_fetch_add(&a.cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (arrived + 1 == parts) {
-          const uint64_t v = __hip_atomic_fetch_xor(&a.acc[slot], 0ull, __ATOMIC_ACQUIRE,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-          emit<kLogEntry>(a, e, v);
-          __hip_atomic_store(&a.acc[slot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(&a.cnt[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        const uint64_t lastseg = (oe1 - 1 - base) / S;
+        straddle_piece<kLogEntry>(a, e, static_cast<uint32_t>(k),
+                                  static_cast<uint32_t>(lastseg - k + 1), c);
       }
       ++e;
       oe = oe1;
@@ -300,11 +308,14 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a)
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64(const JrqCrcArgs* args, int log_entry, int grid,
                                        hipStream_t stream) {
-  if (log_entry)
-    hipLaunchKernelGGL(jrq::crc64_segments_kernel<true>, dim3(grid), dim3(jrq::kCrcBlock), 0,
-                       stream, *args);
-  else
-    hipLaunchKernelGGL(jrq::crc64_segments_kernel<false>, dim3(grid), dim3(jrq::kCrcBlock), 0,
-                       stream, *args);
+  const dim3 g(grid), blk(jrq::kCrcBlock);
+  const bool wide = args->block_bytes >= 128;  // per-lane load block: 128 B or 64 B
+  if (log_entry) {
+    if (wide) hipLaunchKernelGGL((jrq::crc64_segments_kernel<true, 8>), g, blk, 0, stream, *args);
+    else hipLaunchKernelGGL((jrq::crc64_segments_kernel<true, 4>), g, blk, 0, stream, *args);
+  } else {
+    if (wide) hipLaunchKernelGGL((jrq::crc64_segments_kernel<false, 8>), g, blk, 0, stream, *args);
+    else hipLaunchKernelGGL((jrq::crc64_segments_kernel<false, 4>), g, blk, 0, stream, *args);
+  }
   return hipGetLastError();
 }

@@ -9,6 +9,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -43,6 +44,11 @@ struct jrq_engine {
   uint32_t* cnt = nullptr;    // straddler counters
   uint32_t scratch_len = 0;
   int crc_grid = 0;
+  // tuning knobs (JRQ_CRC_SEG_MODE / JRQ_CRC_SEG_BYTES / JRQ_CRC_BLOCK); defaults are the
+  // measured best (profiles/README.md): power-of-two segments, 128-B per-lane blocks
+  uint32_t crc_seg_mode = 0;
+  uint64_t crc_seg_bytes = 0;
+  uint32_t crc_block = 128;
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
   DevBuf stage[16];
@@ -163,6 +169,9 @@ int crc_dispatch(jrq_engine* e, JrqCrcArgs& a, int log_entry) {
   a.cnt = e->cnt;
   a.scratch_len = e->scratch_len;
   a.min_seg_log2 = 8;
+  a.seg_mode = e->crc_seg_mode;
+  a.seg_bytes = e->crc_seg_bytes;
+  a.block_bytes = e->crc_block;
   JRQ_HIP(e, jrq_launch_crc64(&a, log_entry, e->crc_grid, e->stream));
   return JRQ_OK;
 }
@@ -208,6 +217,13 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   e->max_groups = max_groups;
   e->max_peers = max_peers;
   e->crc_grid = e->num_cus;  // persistent: one 1024-thread workgroup per CU (128 KiB LDS)
+  if (const char* v = std::getenv("JRQ_CRC_SEG_MODE")) e->crc_seg_mode = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("JRQ_CRC_BLOCK")) e->crc_block = (uint32_t)std::atoi(v) >= 128 ? 128 : 64;
+  if (const char* v = std::getenv("JRQ_CRC_SEG_BYTES")) {
+    // fixed segment size; at least 64 B and large enough for the straddler scratch
+    uint64_t b = std::strtoull(v, nullptr, 10);
+    e->crc_seg_bytes = (b == 0) ? 0 : (b < 64 ? 64 : b);  // 0 = automatic
+  }
   e->scratch_len = static_cast<uint32_t>(2ull * e->crc_grid * jrq::kCrcBlock + 2);
   int rc = JRQ_OK;
   std::vector<uint64_t> slice, shift;

@@ -53,6 +53,9 @@ struct JrqCrcArgs {
   uint32_t* cnt;           // straddler arrival counters, zero between launches
   uint32_t scratch_len;    // entries in acc/cnt
   uint32_t min_seg_log2;   // smallest segment size (log2 bytes)
+  uint32_t seg_mode;       // 1: odd multiple of 64 B (default), 0: power of two
+  uint64_t seg_bytes;      // nonzero: fixed segment size (tuning / tests)
+  uint32_t block_bytes;    // per-lane load block: 64 or 128
 };
 
 struct JrqQuorumArgs {

@@ -70,6 +70,20 @@ def test_mixed_huge_and_tiny(engine, oracle):
     np.testing.assert_array_equal(engine.crc64_batch(payload, offs), oracle.crc64_batch(payload, offs))
 
 
+@pytest.mark.parametrize("seg", ["64", "100", "1000"])
+def test_tiny_segments_stress_straddlers(oracle, seg, monkeypatch):
+    """Forced tiny segments: nearly every entry spans many segments, so every result goes
+    through the x^(8n) shifts and the atomic last-arriver hand-off (all lanes, all XCDs)."""
+    from jraft_amd import Engine
+    monkeypatch.setenv("JRQ_CRC_SEG_BYTES", seg)
+    with Engine(0) as e:
+        offs = W.ragged_offsets(int(seg), 20000, 3000, start=3)
+        payload = W.random_bytes(int(seg), int(offs[-1]) + 1)
+        exp = oracle.crc64_batch(payload, offs)
+        for _ in range(3):
+            np.testing.assert_array_equal(e.crc64_batch(payload, offs), exp)
+
+
 def test_repeat_is_stable(engine, oracle):
     """Straddler scratch slots are re-zeroed by the last arriver: back-to-back calls agree."""
     offs = W.ragged_offsets(77, 5000, 9000)
