@@ -167,6 +167,36 @@ int jrq_logentry_checksum_batch(jrq_engine *e, const uint8_t *type, const int64_
                                 uint64_t *out, const uint64_t *expected, const uint8_t *has,
                                 uint8_t *corrupt_out);
 
+/* ------------------------------------------- follower verify on receive -- */
+
+/* Batched follower-side verify of R AppendEntries requests holding N EntryMetas in total
+ * (NodeImpl.handleAppendEntriesRequest, JC/core/NodeImpl.java:1766-1792; logEntryFromMeta
+ * :1809-1823; wire format raft.proto EntryMeta / rpc.proto AppendEntriesRequest):
+ *   req_off[R+1]      entries of request r are [req_off[r], req_off[r+1])
+ *   prev_log_index[R] entry i of request r has index prev_log_index[r] + 1 + (i - req_off[r])
+ *   term/type/data_len/checksum/has_checksum[N]   the EntryMeta fields (has_checksum nullable:
+ *                     every entry carries one); peer_xor[N] nullable (XOR of the entry's
+ *                     PeerId checksums, as for jrq_logentry_checksum_batch)
+ *   data              every request's consumed data bytes, back to back in request order;
+ *                     an ENTRY_TYPE_UNKNOWN (0) entry consumes no bytes and is never corrupt
+ * Out: checksum_out[N] = LogEntry.checksum() of each entry as received, corrupt_out[N] =
+ * isCorrupted(), first_corrupt_out[R] = position in its request of the first corrupt
+ * entry (the one the reference rejects with EINVAL, :1777-1789), or -1. */
+int jrq_append_entries_verify_dev(jrq_engine *e, uint32_t R, const uint32_t *req_off_dev,
+                                  const int64_t *prev_log_index_dev, uint32_t N,
+                                  const int64_t *term_dev, const uint8_t *type_dev,
+                                  const int64_t *data_len_dev, const uint64_t *peer_xor_dev,
+                                  const uint64_t *checksum_dev, const uint8_t *has_checksum_dev,
+                                  const uint8_t *data_dev, uint64_t *checksum_out_dev,
+                                  uint8_t *corrupt_out_dev, int32_t *first_corrupt_out_dev);
+int jrq_append_entries_verify(jrq_engine *e, uint32_t R, const uint32_t *req_off,
+                              const int64_t *prev_log_index, uint32_t N, const int64_t *term,
+                              const uint8_t *type, const int64_t *data_len,
+                              const uint64_t *peer_xor, const uint64_t *checksum,
+                              const uint8_t *has_checksum, const uint8_t *data,
+                              uint64_t *checksum_out, uint8_t *corrupt_out,
+                              int32_t *first_corrupt_out);
+
 /* --------------------------------------------------- node-wide publication -- */
 
 /* Multi-GPU (one process per GPU): groups are sharded by contiguous groupId blocks.

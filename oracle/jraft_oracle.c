@@ -108,6 +108,37 @@ void jo_logentry_checksum_batch(const uint8_t *type, const int64_t *index, const
     }
 }
 
+/* ======================= follower receive (JC/core/NodeImpl.java) ========== */
+
+void jo_append_entries_verify(uint32_t R, const uint32_t *req_off, const int64_t *prev_log_index,
+                              const int64_t *term, const uint8_t *type, const int64_t *data_len,
+                              const uint64_t *peer_xor, const uint64_t *checksum,
+                              const uint8_t *has_checksum, const uint8_t *data,
+                              uint64_t *checksum_out, uint8_t *corrupt_out, int32_t *first_corrupt) {
+    size_t pos = 0; /* allData position: requests are back to back */
+    for (uint32_t r = 0; r < R; ++r) {
+        int64_t index = prev_log_index[r]; /* long index = prevLogIndex (:1763) */
+        first_corrupt[r] = -1;
+        for (uint32_t i = req_off[r]; i < req_off[r + 1]; ++i) {
+            index++;
+            corrupt_out[i] = 0;
+            if (type[i] == 0) { /* ENTRY_TYPE_UNKNOWN: logEntryFromMeta returns null */
+                checksum_out[i] = jo_logentry_checksum(0, index, term[i], peer_xor ? peer_xor[i] : 0,
+                                                       NULL, 0);
+                continue;
+            }
+            const size_t len = (size_t)(data_len[i] > 0 ? data_len[i] : 0);
+            const uint64_t c = jo_logentry_checksum(type[i], index, term[i], peer_xor ? peer_xor[i] : 0,
+                                                    data + pos, len);
+            pos += len;
+            checksum_out[i] = c;
+            const int has = has_checksum == NULL || has_checksum[i];
+            corrupt_out[i] = (uint8_t)(has && checksum[i] != c);
+            if (corrupt_out[i] && first_corrupt[r] < 0) first_corrupt[r] = (int32_t)(i - req_off[r]);
+        }
+    }
+}
+
 /* ======================= Ballot (JC/entity/Ballot.java) ==================== */
 
 static void list_init(jo_peer_list *l, const int32_t *ids, int32_t n) {

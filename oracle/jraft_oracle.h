@@ -52,6 +52,19 @@ void jo_logentry_checksum_batch(const uint8_t *type, const int64_t *index, const
                                 const uint64_t *offsets, uint32_t n, uint64_t *out,
                                 const uint64_t *expected, const uint8_t *has, uint8_t *corrupt);
 
+/* Follower receive path (JC/core/NodeImpl.java:1766-1792, logEntryFromMeta :1809-1823):
+ * per request r, index runs from prev_log_index[r]+1; an entry of type UNKNOWN (0) is
+ * skipped and consumes no data; otherwise it takes the next data_len bytes of `data`
+ * (requests back to back) and, if has_checksum (NULL = all), is corrupt when the stored
+ * checksum differs from LogEntry.checksum().  first_corrupt[r] = position of the first
+ * corrupt entry (where the reference returns EINVAL) or -1.  checksum_out gets every
+ * entry's computed checksum. */
+void jo_append_entries_verify(uint32_t R, const uint32_t *req_off, const int64_t *prev_log_index,
+                              const int64_t *term, const uint8_t *type, const int64_t *data_len,
+                              const uint64_t *peer_xor, const uint64_t *checksum,
+                              const uint8_t *has_checksum, const uint8_t *data,
+                              uint64_t *checksum_out, uint8_t *corrupt_out, int32_t *first_corrupt);
+
 /* ---------------- Ballot (JC/entity/Ballot.java) --------------------------- */
 
 #define JO_MAX_CONF 32 /* peers per Configuration list kept by the oracle */

@@ -67,6 +67,8 @@ def lib():
         L.jo_logentry_checksum_batch.argtypes = [_u8p, _i64p, _i64p, C.c_void_p, _u8p, _u64p,
                                                  C.c_uint32, _u64p, C.c_void_p, C.c_void_p,
                                                  C.c_void_p]
+        L.jo_append_entries_verify.restype = None
+        L.jo_append_entries_verify.argtypes = [C.c_uint32] + [C.c_void_p] * 12
         L.jo_bb_new.restype = C.c_void_p
         L.jo_bb_free.argtypes = [C.c_void_p]
         for name in ("jo_bb_last_committed_index", "jo_bb_pending_index", "jo_bb_queue_size",
@@ -153,6 +155,29 @@ def logentry_checksum_batch(etype, index, term, peer_xor, payload, offsets, expe
     lib().jo_logentry_checksum_batch(etype, index, term, _ptr(px), payload, offsets, n, out,
                                      _ptr(ex), _ptr(hs), _ptr(corrupt))
     return out if corrupt is None else (out, corrupt)
+
+
+def append_entries_verify(req_off, prev_log_index, term, etype, data_len, checksum, data,
+                          has_checksum=None, peer_xor=None):
+    """NodeImpl.handleAppendEntriesRequest's receive loop (NodeImpl.java:1766-1792) for a
+    batch of requests; returns (checksum_out, corrupt, first_corrupt)."""
+    ro = np.ascontiguousarray(req_off, np.uint32)
+    prev = np.ascontiguousarray(prev_log_index, np.int64)
+    term = np.ascontiguousarray(term, np.int64)
+    et = np.ascontiguousarray(etype, np.uint8)
+    dl = np.ascontiguousarray(data_len, np.int64)
+    ck = np.ascontiguousarray(checksum, np.uint64)
+    hs = None if has_checksum is None else np.ascontiguousarray(has_checksum, np.uint8)
+    px = None if peer_xor is None else np.ascontiguousarray(peer_xor, np.uint64)
+    d = np.ascontiguousarray(data, np.uint8) if data is not None and len(data) else np.zeros(1, np.uint8)
+    N, R = len(term), len(prev)
+    out = np.zeros(N, np.uint64)
+    cor = np.zeros(N, np.uint8)
+    first = np.zeros(R, np.int32)
+    lib().jo_append_entries_verify(R, _ptr(ro), _ptr(prev), _ptr(term), _ptr(et), _ptr(dl),
+                                   _ptr(px), _ptr(ck), _ptr(hs), _ptr(d), _ptr(out), _ptr(cor),
+                                   _ptr(first))
+    return out, cor, first
 
 
 # ------------------------------------------------- pure-Python cross-checks --

@@ -157,7 +157,8 @@ __device__ __forceinline__ uint64_t logid_crc(int64_t index, int64_t term, const
 }
 
 // c * x^(8n) mod P via the global power tables: one 8-lookup pass per set bit of n.
-__device__ uint64_t crc_shift(uint64_t c, uint64_t n, const uint64_t* __restrict__ shift) {
+__device__ __forceinline__ uint64_t crc_shift(uint64_t c, uint64_t n,
+                                              const uint64_t* __restrict__ shift) {
   for (int t = 0; n != 0 && t < kShiftTables; ++t, n >>= 1) {
     if (!(n & 1u)) continue;
     const uint64_t* tb = shift + static_cast<size_t>(t) * 8 * 256;
@@ -167,6 +168,83 @@ __device__ uint64_t crc_shift(uint64_t c, uint64_t n, const uint64_t* __restrict
     c = v;
   }
   return c;
+}
+
+// Two independent chains per lane: [a, b) is cut at m into halves that are hashed in
+// lockstep (their 2-byte steps interleave, so one chain's LDS latency hides under the
+// other's), then crc = crc(X) * x^(8|Y|) ^ crc(Y).  Both halves move through 64-B
+// blocks with a 2-deep register ring each; X takes the unaligned head first, Y the tail
+// last.  Short ranges fall back to one chain.
+__device__ __forceinline__ uint64_t crc_range2(const uint8_t* __restrict__ payload, uint64_t a,
+                                               uint64_t b, const char* lds, uint32_t lc,
+                                               const uint64_t* __restrict__ shift) {
+  constexpr uint64_t kBB = 64;  // block bytes per chain
+  if (b - a < 4 * kBB) return crc_range<4>(payload, a, b, lds, lc);
+  RState x{0u, 0u}, y{0u, 0u};
+  uint64_t p = a;
+  const uint64_t mis = reinterpret_cast<uintptr_t>(payload) & 15u;
+  while (p < b && ((p + mis) & 15u)) {
+    step1(x, payload[p], lds, lc);
+    ++p;
+  }
+  const uint64_t nb = (b - p) / (2 * kBB);  // blocks per chain (>= 1 here)
+  const uint64_t m = p + nb * kBB;
+  const uint4* qx = reinterpret_cast<const uint4*>(payload + p);
+  const uint4* qy = reinterpret_cast<const uint4*>(payload + m);
+  const uint64_t last = nb - 1;
+  uint4 XA[4], XB[4], YA[4], YB[4];
+#define JRQ_LOAD2(X, Y, blk)                                            \
+  do {                                                                  \
+    const uint64_t bb = (blk) < last ? (blk) : last;                    \
+    _Pragma("unroll") for (int v = 0; v < 4; ++v) X[v] = qx[4 * bb + v]; \
+    _Pragma("unroll") for (int v = 0; v < 4; ++v) Y[v] = qy[4 * bb + v]; \
+    asm volatile("" ::: "memory");                                      \
+  } while (0)
+#define JRQ_HASH2(X, Y)                          \
+  do {                                           \
+    _Pragma("unroll") for (int v = 0; v < 4; ++v) { \
+      x.lo ^= X[v].x;                            \
+      x.hi ^= X[v].y;                            \
+      y.lo ^= Y[v].x;                            \
+      y.hi ^= Y[v].y;                            \
+      _Pragma("unroll") for (int s = 0; s < 4; ++s) { \
+        step2(x, lds, lc);                       \
+        step2(y, lds, lc);                       \
+      }                                          \
+      x.lo ^= X[v].z;                            \
+      x.hi ^= X[v].w;                            \
+      y.lo ^= Y[v].z;                            \
+      y.hi ^= Y[v].w;                            \
+      _Pragma("unroll") for (int s = 0; s < 4; ++s) { \
+        step2(x, lds, lc);                       \
+        step2(y, lds, lc);                       \
+      }                                          \
+    }                                            \
+  } while (0)
+  JRQ_LOAD2(XA, YA, 0);
+  for (uint64_t i = 0;;) {
+    JRQ_LOAD2(XB, YB, i + 1);
+    JRQ_HASH2(XA, YA);
+    if (++i == nb) break;
+    JRQ_LOAD2(XA, YA, i + 1);
+    JRQ_HASH2(XB, YB);
+    if (++i == nb) break;
+  }
+#undef JRQ_LOAD2
+#undef JRQ_HASH2
+  // Y continues over the tail [m + nb*kBB, b)
+  uint64_t q = m + nb * kBB;
+  while (q + 16 <= b) {
+    step16(y, *reinterpret_cast<const uint4*>(payload + q), lds, lc);
+    q += 16;
+  }
+  while (q + 2 <= b) {
+    y.lo ^= payload[q] | (static_cast<uint32_t>(payload[q + 1]) << 8);
+    step2(y, lds, lc);
+    q += 2;
+  }
+  if (q < b) step1(y, payload[q], lds, lc);
+  return crc_shift(crc_value(x), b - m, shift) ^ crc_value(y);
 }
 
 template <bool kLogEntry>
@@ -222,7 +300,15 @@ __device__ __forceinline__ uint32_t lower_bound_off(const uint64_t* __restrict__
   return lo;
 }
 
-template <bool kLogEntry, int BV>
+// Hash one piece: kVariant 4 / 8 = one chain with 64-B / 128-B blocks, 2 = two chains.
+template <int kVariant>
+__device__ __forceinline__ uint64_t crc_piece(const JrqCrcArgs& a, uint64_t lo, uint64_t hi,
+                                              const char* lds, uint32_t lc) {
+  if (kVariant == 2) return crc_range2(a.payload, lo, hi, lds, lc, a.shift);
+  return crc_range<kVariant == 8 ? 8 : 4>(a.payload, lo, hi, lds, lc);
+}
+
+template <bool kLogEntry, int kVariant>
 __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
   const char* lds = reinterpret_cast<const char*>(lds_tab);
@@ -275,7 +361,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a)
     if (e > 0 && oe > s0) {
       const uint32_t t = e - 1;
       const uint64_t pe = oe < s1 ? oe : s1;
-      uint64_t c = crc_range<BV>(a.payload, s0, pe, lds, lc);
+      uint64_t c = crc_piece<kVariant>(a, s0, pe, lds, lc);
       c = crc_shift(c, oe - pe, a.shift);
       const uint64_t ot = a.offsets[t];
       const uint64_t first = (ot - base) / S, lastseg = (oe - 1 - base) / S;
@@ -288,7 +374,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a)
       const uint64_t oe1 = a.offsets[e + 1];
       const uint64_t pe = oe1 < s1 ? oe1 : s1;
       const uint64_t fields = entry_fields<kLogEntry>(a, e, lds, lc);
-      uint64_t c = crc_range<BV>(a.payload, oe, pe, lds, lc);
+      uint64_t c = crc_piece<kVariant>(a, oe, pe, lds, lc);
       if (oe1 <= s1) {
         emit<kLogEntry>(a, e, c ^ fields);  // whole entry inside the segment
       } else {
@@ -309,13 +395,19 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a)
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64(const JrqCrcArgs* args, int log_entry, int grid,
                                        hipStream_t stream) {
   const dim3 g(grid), blk(jrq::kCrcBlock);
-  const bool wide = args->block_bytes >= 128;  // per-lane load block: 128 B or 64 B
+  // variant: two chains per lane, or one chain with 128-B / 64-B per-lane load blocks
+  const int v = args->chains >= 2 ? 2 : (args->block_bytes >= 128 ? 8 : 4);
+#define JRQ_LAUNCH(LE, V) \
+  hipLaunchKernelGGL((jrq::crc64_segments_kernel<LE, V>), g, blk, 0, stream, *args)
   if (log_entry) {
-    if (wide) hipLaunchKernelGGL((jrq::crc64_segments_kernel<true, 8>), g, blk, 0, stream, *args);
-    else hipLaunchKernelGGL((jrq::crc64_segments_kernel<true, 4>), g, blk, 0, stream, *args);
+    if (v == 2) JRQ_LAUNCH(true, 2);
+    else if (v == 8) JRQ_LAUNCH(true, 8);
+    else JRQ_LAUNCH(true, 4);
   } else {
-    if (wide) hipLaunchKernelGGL((jrq::crc64_segments_kernel<false, 8>), g, blk, 0, stream, *args);
-    else hipLaunchKernelGGL((jrq::crc64_segments_kernel<false, 4>), g, blk, 0, stream, *args);
+    if (v == 2) JRQ_LAUNCH(false, 2);
+    else if (v == 8) JRQ_LAUNCH(false, 8);
+    else JRQ_LAUNCH(false, 4);
   }
+#undef JRQ_LAUNCH
   return hipGetLastError();
 }

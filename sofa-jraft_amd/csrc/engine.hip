@@ -20,7 +20,9 @@
 
 extern "C" hipError_t jrq_launch_crc64(const JrqCrcArgs* args, int log_entry, int grid,
                                        hipStream_t stream);
-extern "C" hipError_t jrq_launch_quorum(const JrqQuorumArgs* args, int grid, hipStream_t stream);
+extern "C" hipError_t jrq_launch_quorum(const JrqQuorumArgs* args, int num_cus, hipStream_t stream);
+extern "C" hipError_t jrq_launch_ae_meta(const JrqAeArgs* a, hipStream_t stream);
+extern "C" hipError_t jrq_launch_ae_first_corrupt(const JrqAeArgs* a, hipStream_t stream);
 
 namespace {
 
@@ -49,9 +51,10 @@ struct jrq_engine {
   uint32_t crc_seg_mode = 0;
   uint64_t crc_seg_bytes = 0;
   uint32_t crc_block = 128;
+  uint32_t crc_chains = 1;
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
-  DevBuf stage[16];
+  DevBuf stage[24];  // 0-13 host-variant staging, 16-19 AppendEntries scratch
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = -1;
   std::string err;
@@ -172,6 +175,7 @@ int crc_dispatch(jrq_engine* e, JrqCrcArgs& a, int log_entry) {
   a.seg_mode = e->crc_seg_mode;
   a.seg_bytes = e->crc_seg_bytes;
   a.block_bytes = e->crc_block;
+  a.chains = e->crc_chains;
   JRQ_HIP(e, jrq_launch_crc64(&a, log_entry, e->crc_grid, e->stream));
   return JRQ_OK;
 }
@@ -219,6 +223,7 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   e->crc_grid = e->num_cus;  // persistent: one 1024-thread workgroup per CU (128 KiB LDS)
   if (const char* v = std::getenv("JRQ_CRC_SEG_MODE")) e->crc_seg_mode = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("JRQ_CRC_BLOCK")) e->crc_block = (uint32_t)std::atoi(v) >= 128 ? 128 : 64;
+  if (const char* v = std::getenv("JRQ_CRC_CHAINS")) e->crc_chains = std::atoi(v) >= 2 ? 2 : 1;
   if (const char* v = std::getenv("JRQ_CRC_SEG_BYTES")) {
     // fixed segment size; at least 64 B and large enough for the straddler scratch
     uint64_t b = std::strtoull(v, nullptr, 10);
@@ -320,10 +325,7 @@ int jrq_quorum_epoch_dev(jrq_engine* e, const jrq_group_batch* in, int64_t* comm
   a.status = status_out;
   a.G = G;
   // enough 256-thread blocks for ~8 per CU, grid-stride beyond
-  const uint64_t need = (static_cast<uint64_t>(G) + 255) / 256;
-  const uint64_t cap = static_cast<uint64_t>(e->num_cus) * 8;
-  const int grid = static_cast<int>(need < cap ? need : cap);
-  JRQ_HIP(e, jrq_launch_quorum(&a, grid, e->stream));
+  JRQ_HIP(e, jrq_launch_quorum(&a, e->num_cus, e->stream));
   return JRQ_OK;
 }
 
@@ -462,6 +464,116 @@ int jrq_logentry_checksum_batch(jrq_engine* e, const uint8_t* type, const int64_
     return rc;
   JRQ_HIP(e, hipMemcpyAsync(out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
   if (corrupt_out) JRQ_HIP(e, hipMemcpyAsync(corrupt_out, dcor, N, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
+// ------------------------------------------------------- AppendEntries -----
+
+int jrq_append_entries_verify_dev(jrq_engine* e, uint32_t R, const uint32_t* req_off,
+                                  const int64_t* prev_log_index, uint32_t N, const int64_t* term,
+                                  const uint8_t* type, const int64_t* data_len,
+                                  const uint64_t* peer_xor, const uint64_t* checksum,
+                                  const uint8_t* has_checksum, const uint8_t* data,
+                                  uint64_t* checksum_out, uint8_t* corrupt_out,
+                                  int32_t* first_corrupt_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (R == 0) return JRQ_OK;
+  if (!req_off || !prev_log_index || !first_corrupt_out)
+    return fail(e, JRQ_E_INVALID, "null request array");
+  if (N > 0 && (!term || !type || !data_len || !checksum || !data || !checksum_out || !corrupt_out))
+    return fail(e, JRQ_E_INVALID, "null entry array");
+  DeviceGuard guard(e->device);
+  int rc;
+  void *offs, *idx, *has, *tiles;
+  const size_t ntiles = (static_cast<size_t>(N) + 4095) / 4096 + 1;
+  if ((rc = ensure_stage(e, 16, (static_cast<size_t>(N) + 1) * 8, &offs))) return rc;
+  if ((rc = ensure_stage(e, 17, static_cast<size_t>(N) * 8 + 8, &idx))) return rc;
+  if ((rc = ensure_stage(e, 18, static_cast<size_t>(N) + 1, &has))) return rc;
+  if ((rc = ensure_stage(e, 19, ntiles * 8, &tiles))) return rc;
+  JrqAeArgs ae{};
+  ae.r = R;
+  ae.req_off = req_off;
+  ae.prev_log_index = prev_log_index;
+  ae.n = N;
+  ae.type = type;
+  ae.data_len = data_len;
+  ae.has_checksum = has_checksum;
+  ae.offsets = static_cast<uint64_t*>(offs);
+  ae.index = static_cast<int64_t*>(idx);
+  ae.has_eff = static_cast<uint8_t*>(has);
+  ae.tile_sums = static_cast<uint64_t*>(tiles);
+  ae.corrupt = corrupt_out;
+  ae.first_corrupt = first_corrupt_out;
+  if (N > 0) {
+    JRQ_HIP(e, jrq_launch_ae_meta(&ae, e->stream));
+    JrqCrcArgs a{};
+    a.payload = data;
+    a.offsets = ae.offsets;
+    a.n = N;
+    a.out = checksum_out;
+    a.type = type;
+    a.index = ae.index;
+    a.term = term;
+    a.peer_xor = peer_xor;
+    a.expected = checksum;
+    a.has = ae.has_eff;
+    a.corrupt = corrupt_out;
+    if ((rc = crc_dispatch(e, a, 1))) return rc;
+  }
+  JRQ_HIP(e, jrq_launch_ae_first_corrupt(&ae, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_append_entries_verify(jrq_engine* e, uint32_t R, const uint32_t* req_off,
+                              const int64_t* prev_log_index, uint32_t N, const int64_t* term,
+                              const uint8_t* type, const int64_t* data_len,
+                              const uint64_t* peer_xor, const uint64_t* checksum,
+                              const uint8_t* has_checksum, const uint8_t* data,
+                              uint64_t* checksum_out, uint8_t* corrupt_out,
+                              int32_t* first_corrupt_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (R == 0) return JRQ_OK;
+  if (!req_off || !prev_log_index || !first_corrupt_out)
+    return fail(e, JRQ_E_INVALID, "null request array");
+  if (req_off[0] != 0 || req_off[R] != N) return fail(e, JRQ_E_INVALID, "req_off must span [0, N]");
+  if (N > 0 && (!term || !type || !data_len || !checksum || !checksum_out || !corrupt_out))
+    return fail(e, JRQ_E_INVALID, "null entry array");
+  DeviceGuard guard(e->device);
+  uint64_t bytes = 0;  // consumed payload bytes (host arrays are readable here)
+  for (uint32_t i = 0; i < N; ++i) {
+    if (data_len[i] < 0) return fail(e, JRQ_E_INVALID, "negative data_len");
+    if (type[i] != 0) bytes += static_cast<uint64_t>(data_len[i]);
+  }
+  if (bytes && !data) return fail(e, JRQ_E_INVALID, "null data");
+  int rc;
+  const uint32_t *dro;
+  const int64_t *dpli, *dterm, *dlen;
+  const uint8_t *dtype, *dhas, *ddata;
+  const uint64_t *dpx, *dck;
+  if ((rc = stage_in(e, 0, req_off, static_cast<size_t>(R) + 1, &dro))) return rc;
+  if ((rc = stage_in(e, 1, prev_log_index, R, &dpli))) return rc;
+  if ((rc = stage_in(e, 2, term, N, &dterm))) return rc;
+  if ((rc = stage_in(e, 3, type, N, &dtype))) return rc;
+  if ((rc = stage_in(e, 4, data_len, N, &dlen))) return rc;
+  if ((rc = stage_in(e, 5, peer_xor, N, &dpx))) return rc;
+  if ((rc = stage_in(e, 6, checksum, N, &dck))) return rc;
+  if ((rc = stage_in(e, 7, has_checksum, N, &dhas))) return rc;
+  if ((rc = stage_in(e, 10, data ? data : reinterpret_cast<const uint8_t*>(&bytes), bytes, &ddata)))
+    return rc;
+  void *dout, *dcor, *dfirst;
+  if ((rc = ensure_stage(e, 12, static_cast<size_t>(N) * 8 + 8, &dout))) return rc;
+  if ((rc = ensure_stage(e, 13, static_cast<size_t>(N) + 1, &dcor))) return rc;
+  if ((rc = ensure_stage(e, 9, static_cast<size_t>(R) * 4, &dfirst))) return rc;
+  if ((rc = jrq_append_entries_verify_dev(e, R, dro, dpli, N, dterm, dtype, dlen, dpx, dck, dhas,
+                                          ddata, static_cast<uint64_t*>(dout),
+                                          static_cast<uint8_t*>(dcor), static_cast<int32_t*>(dfirst))))
+    return rc;
+  if (N) {
+    JRQ_HIP(e, hipMemcpyAsync(checksum_out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
+    JRQ_HIP(e, hipMemcpyAsync(corrupt_out, dcor, N, hipMemcpyDeviceToHost, e->stream));
+  }
+  JRQ_HIP(e, hipMemcpyAsync(first_corrupt_out, dfirst, static_cast<size_t>(R) * 4, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }

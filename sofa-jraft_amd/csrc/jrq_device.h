@@ -56,6 +56,24 @@ struct JrqCrcArgs {
   uint32_t seg_mode;       // 1: odd multiple of 64 B (default), 0: power of two
   uint64_t seg_bytes;      // nonzero: fixed segment size (tuning / tests)
   uint32_t block_bytes;    // per-lane load block: 64 or 128
+  uint32_t chains;         // independent CRC chains per lane: 1 or 2
+};
+
+// AppendEntries batch verify (append_entries.hip): inputs + engine scratch.
+struct JrqAeArgs {
+  uint32_t r;                      // requests
+  const uint32_t* req_off;         // [r+1] entry ranges per request
+  const int64_t* prev_log_index;   // [r]
+  uint32_t n;                      // entries
+  const uint8_t* type;             // [n] EntryType number
+  const int64_t* data_len;         // [n]
+  const uint8_t* has_checksum;     // [n] nullable (= all have one)
+  uint64_t* offsets;               // scratch [n+1] payload offsets
+  int64_t* index;                  // scratch [n] log indexes
+  uint8_t* has_eff;                // scratch [n] has && type != UNKNOWN
+  uint64_t* tile_sums;             // scratch [ceil(n/4096)]
+  const uint8_t* corrupt;          // [n] verify flags (from the checksum kernel)
+  int32_t* first_corrupt;          // [r] out
 };
 
 struct JrqQuorumArgs {

@@ -54,63 +54,148 @@ __device__ __forceinline__ int64_t run_bound(const int64_t (&m)[P], uint64_t cw)
   return kn < ko ? kn : ko;
 }
 
+// Acks past the queue would throw ArrayIndexOutOfBoundsException and change nothing
+// (BallotBox.java:107-109): that peer grants no entry in this epoch.
+template <int P>
+__device__ __forceinline__ uint8_t mask_out_of_range(int64_t (&m)[P], int64_t la) {
+  uint8_t st = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const bool oor = m[p] > la;
+    st |= oor ? kStOutOfRange : 0;
+    m[p] = oor ? kI64Min : m[p];
+  }
+  return st;
+}
+
+// One group with a single conf word (no conf change inside the pending window).
+template <int P>
+__device__ __forceinline__ void decide_single(int64_t pi, int64_t la, int64_t lc, uint64_t cw,
+                                              int64_t (&m)[P], int64_t& out, uint8_t& st_out) {
+  uint8_t st = mask_out_of_range<P>(m, la);
+  if ((cw & 0xFFFFu) == 0 && la >= pi) st |= kStEmptyConf;
+  int64_t cand = run_bound<P>(m, cw);
+  cand = cand < la ? cand : la;
+  const int64_t best = (cand >= pi && cand > lc) ? cand : lc;
+  // commitAt returns false when not the leader (BallotBox.java:101-103): state unchanged
+  out = pi == 0 ? lc : best;
+  st_out = pi == 0 ? kStNotLeader : st;
+}
+
+// General path: one lane per group, optional conf runs.  Every load of the group is
+// issued before any decision, so a group costs one memory round trip.
 template <int P>
 __global__ __launch_bounds__(256) void quorum_epoch_kernel(JrqQuorumArgs a) {
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G; g += stride) {
     const int64_t pi = a.pending_index[g];
     const int64_t lc = a.last_committed[g];
-    if (pi == 0) {  // commitAt returns false: not the leader (BallotBox.java:101-103)
+    const int64_t la = a.last_appended[g];
+    int64_t m[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
+    if (a.run_off == nullptr) {
+      const uint64_t cw = a.conf[g];
+      int64_t out;
+      uint8_t st;
+      decide_single<P>(pi, la, lc, cw, m, out, st);
+      a.committed[g] = out;
+      a.status[g] = st;
+      continue;
+    }
+    const uint32_t r0 = a.run_off[g], r1 = a.run_off[g + 1];
+    if (pi == 0) {
       a.committed[g] = lc;
       a.status[g] = kStNotLeader;
       continue;
     }
-    const int64_t la = a.last_appended[g];
-    int64_t m[P];
-    uint8_t st = 0;
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      const int64_t v = a.match[static_cast<size_t>(p) * a.match_ld + g];
-      // an ack past the queue would throw ArrayIndexOutOfBoundsException and change
-      // nothing (BallotBox.java:107-109): that peer grants no entry in this epoch
-      const bool oor = v > la;
-      st |= oor ? kStOutOfRange : 0;
-      m[p] = oor ? kI64Min : v;
-    }
+    uint8_t st = mask_out_of_range<P>(m, la);
     int64_t best = lc;
-    if (a.run_off == nullptr) {
-      const uint64_t cw = a.conf[g];
-      if ((cw & 0xFFFFu) == 0 && la >= pi) st |= kStEmptyConf;
+    for (uint32_t r = r0; r < r1; ++r) {
+      const int64_t s = (r == r0) ? pi : (a.run_start[r] > pi ? a.run_start[r] : pi);
+      const int64_t e = (r + 1 < r1) ? a.run_start[r + 1] - 1 : la;
+      const int64_t ee = e < la ? e : la;
+      if (ee < s) continue;  // run entirely committed already (or empty)
+      const uint64_t cw = a.run_conf[r];
+      if ((cw & 0xFFFFu) == 0) st |= kStEmptyConf;
       int64_t cand = run_bound<P>(m, cw);
-      cand = cand < la ? cand : la;
-      best = (cand >= pi && cand > best) ? cand : best;
-    } else {
-      const uint32_t r0 = a.run_off[g], r1 = a.run_off[g + 1];
-      for (uint32_t r = r0; r < r1; ++r) {
-        const int64_t s = (r == r0) ? pi : (a.run_start[r] > pi ? a.run_start[r] : pi);
-        const int64_t e = (r + 1 < r1) ? a.run_start[r + 1] - 1 : la;
-        const int64_t ee = e < la ? e : la;
-        if (ee < s) continue;  // run entirely committed already (or empty)
-        const uint64_t cw = a.run_conf[r];
-        if ((cw & 0xFFFFu) == 0) st |= kStEmptyConf;
-        int64_t cand = run_bound<P>(m, cw);
-        cand = cand < ee ? cand : ee;
-        best = (cand >= s && cand > best) ? cand : best;
-      }
+      cand = cand < ee ? cand : ee;
+      best = (cand >= s && cand > best) ? cand : best;
     }
     a.committed[g] = best;
     a.status[g] = st;
   }
 }
 
+// Fast path (no run table, 16-B aligned arrays, even match_ld): one lane decides two
+// adjacent groups; every stream is read with 16-byte loads (1 KiB per wave instruction)
+// and the two status bytes are stored as one 16-bit word.
+template <int P>
+__global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
+  const uint32_t pairs = a.G >> 1;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < pairs; t += stride) {
+    const uint32_t g = t << 1;
+    const longlong2 pi = *reinterpret_cast<const longlong2*>(a.pending_index + g);
+    const longlong2 lc = *reinterpret_cast<const longlong2*>(a.last_committed + g);
+    const longlong2 la = *reinterpret_cast<const longlong2*>(a.last_appended + g);
+    const ulonglong2 cw = *reinterpret_cast<const ulonglong2*>(a.conf + g);
+    int64_t m0[P], m1[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const longlong2 v =
+          *reinterpret_cast<const longlong2*>(a.match + static_cast<size_t>(p) * a.match_ld + g);
+      m0[p] = v.x;
+      m1[p] = v.y;
+    }
+    int64_t o0, o1;
+    uint8_t s0, s1;
+    decide_single<P>(pi.x, la.x, lc.x, cw.x, m0, o0, s0);
+    decide_single<P>(pi.y, la.y, lc.y, cw.y, m1, o1, s1);
+    longlong2 out;
+    out.x = o0;
+    out.y = o1;
+    *reinterpret_cast<longlong2*>(a.committed + g) = out;
+    *reinterpret_cast<uint16_t*>(a.status + g) = static_cast<uint16_t>(s0 | (s1 << 8));
+  }
+  // odd G: the last group goes through the scalar decision
+  if ((a.G & 1u) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint32_t g = a.G - 1;
+    int64_t m[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
+    int64_t out;
+    uint8_t st;
+    decide_single<P>(a.pending_index[g], a.last_appended[g], a.last_committed[g], a.conf[g], m,
+                     out, st);
+    a.committed[g] = out;
+    a.status[g] = st;
+  }
+}
+
 }  // namespace jrq
 
-extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(const JrqQuorumArgs* args, int grid, hipStream_t stream) {
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
+    const JrqQuorumArgs* args, int num_cus, hipStream_t stream) {
   const dim3 blk(256);
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+  const JrqQuorumArgs& a = *args;
+  const bool pair = a.run_off == nullptr && (a.match_ld & 1u) == 0 && al16(a.match) &&
+                    al16(a.pending_index) && al16(a.last_appended) && al16(a.last_committed) &&
+                    al16(a.conf) && al16(a.committed) &&
+                    (reinterpret_cast<uintptr_t>(a.status) & 1u) == 0 && a.G >= 2;
+  // enough 256-thread blocks for one lane per group (pair: per two), at most 8 per CU
+  const uint64_t lanes = pair ? (a.G >> 1) : a.G;
+  const uint64_t need = (lanes + 255) / 256;
+  const uint64_t cap = static_cast<uint64_t>(num_cus) * 8;
+  const int grid = static_cast<int>(need < cap ? (need ? need : 1) : cap);
   switch (args->num_peers) {
-#define JRQ_CASE(P)                                                                  \
-  case P:                                                                            \
-    hipLaunchKernelGGL(jrq::quorum_epoch_kernel<P>, dim3(grid), blk, 0, stream, *args); \
+#define JRQ_CASE(P)                                                                            \
+  case P:                                                                                      \
+    if (pair)                                                                                  \
+      hipLaunchKernelGGL(jrq::quorum_epoch_pair_kernel<P>, dim3(grid), blk, 0, stream, *args); \
+    else                                                                                       \
+      hipLaunchKernelGGL(jrq::quorum_epoch_kernel<P>, dim3(grid), blk, 0, stream, *args);      \
     break;
     JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
     JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)

@@ -63,6 +63,10 @@ SIGNATURES = [
      [_V, _V, _V, _V, _V, _V, _V, C.c_uint32, _V, _V, _V, _V]),
     ("jrq_logentry_checksum_batch", C.c_int,
      [_V, _V, _V, _V, _V, _V, _V, C.c_uint32, _V, _V, _V, _V]),
+    ("jrq_append_entries_verify_dev", C.c_int,
+     [_V, C.c_uint32, _V, _V, C.c_uint32, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+    ("jrq_append_entries_verify", C.c_int,
+     [_V, C.c_uint32, _V, _V, C.c_uint32, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
     ("jrq_rccl_get_unique_id", C.c_int, [_V]),
     ("jrq_rccl_init", C.c_int, [_V, C.c_int, C.c_int, _V]),
     ("jrq_publish_committed_dev", C.c_int, [_V, _V, _V, C.c_uint64]),

@@ -167,6 +167,41 @@ class Engine:
             _dev_ptr(payload), _dev_ptr(offsets), n, _dev_ptr(out), _dev_ptr(expected),
             _dev_ptr(has), _dev_ptr(corrupt)), self._h)
 
+    # ------------------------------------------------- AppendEntries verify --
+    def append_entries_verify(self, req_off, prev_log_index, term, etype, data_len, checksum,
+                              data, has_checksum=None, peer_xor=None):
+        """Host variant: returns (checksum_out uint64[N], corrupt uint8[N], first_corrupt int32[R])."""
+        req_off = _c(req_off, np.uint32)
+        prev = _c(prev_log_index, np.int64)
+        R = len(prev)
+        term = _c(term, np.int64)
+        N = len(term)
+        etype = _c(etype, np.uint8)
+        data_len = _c(data_len, np.int64)
+        checksum = _c(checksum, np.uint64)
+        has = _c(has_checksum, np.uint8)
+        px = _c(peer_xor, np.uint64)
+        data = _c(data, np.uint8)
+        if data is None or data.size == 0:
+            data = np.zeros(1, np.uint8)
+        out = np.zeros(N, np.uint64)
+        cor = np.zeros(N, np.uint8)
+        first = np.zeros(R, np.int32)
+        check(self._L.jrq_append_entries_verify(
+            self._h, R, _np_ptr(req_off), _np_ptr(prev), N, _np_ptr(term), _np_ptr(etype),
+            _np_ptr(data_len), _np_ptr(px), _np_ptr(checksum), _np_ptr(has), _np_ptr(data),
+            _np_ptr(out), _np_ptr(cor), _np_ptr(first)), self._h)
+        return out, cor, first
+
+    def append_entries_verify_dev(self, req_off, prev_log_index, term, etype, data_len, checksum,
+                                  data, checksum_out, corrupt_out, first_corrupt_out,
+                                  has_checksum=None, peer_xor=None):
+        check(self._L.jrq_append_entries_verify_dev(
+            self._h, prev_log_index.shape[0], _dev_ptr(req_off), _dev_ptr(prev_log_index),
+            term.shape[0], _dev_ptr(term), _dev_ptr(etype), _dev_ptr(data_len),
+            _dev_ptr(peer_xor), _dev_ptr(checksum), _dev_ptr(has_checksum), _dev_ptr(data),
+            _dev_ptr(checksum_out), _dev_ptr(corrupt_out), _dev_ptr(first_corrupt_out)), self._h)
+
     # ---------------------------------------------------------------- RCCL --
     @staticmethod
     def rccl_unique_id() -> bytes:

@@ -1,0 +1,59 @@
+"""Follower verify on receive: the oracle's restatement of
+NodeImpl.handleAppendEntriesRequest (NodeImpl.java:1766-1792) on CPU, and the GPU batch
+(jrq_append_entries_verify) against it."""
+import numpy as np
+import pytest
+
+from ae_cases import random_requests
+
+
+def test_oracle_follows_reference_loop(oracle):
+    """index = prevLogIndex + 1 + i; UNKNOWN entries take no bytes; first corrupt wins."""
+    payload = b"hello" + b"world!" + b"xyz"
+    # request 0: NO_OP "hello", UNKNOWN (data_len 4 but consumes nothing), DATA "world!"
+    # request 1: DATA "xyz"
+    req_off = [0, 3, 4]
+    prev = [99, 7]
+    term = [3, 3, 3, 5]
+    etype = [1, 0, 2, 2]
+    data_len = [5, 4, 6, 3]
+    exp = [oracle.logentry_checksum(1, 100, 3, 0, b"hello"),
+           oracle.logentry_checksum(0, 101, 3, 0, b""),
+           oracle.logentry_checksum(2, 102, 3, 0, b"world!"),
+           oracle.logentry_checksum(2, 8, 5, 0, b"xyz")]
+    data = np.frombuffer(payload, np.uint8)
+    out, cor, first = oracle.append_entries_verify(req_off, prev, term, etype, data_len,
+                                                   np.array(exp, np.uint64), data)
+    assert [int(x) for x in out] == exp
+    assert not cor.any() and list(first) == [-1, -1]
+    bad = np.array(exp, np.uint64)
+    bad[2] ^= np.uint64(5)
+    bad[3] ^= np.uint64(1)
+    _, cor, first = oracle.append_entries_verify(req_off, prev, term, etype, data_len, bad, data)
+    assert list(cor) == [0, 0, 1, 1] and list(first) == [2, 0]
+    # no checksum on the entry -> never corrupt (hasChecksum false)
+    _, cor, first = oracle.append_entries_verify(req_off, prev, term, etype, data_len, bad, data,
+                                                 has_checksum=[1, 1, 0, 1])
+    assert list(first) == [-1, 0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,max_entries,max_len", [(1, 1, 10), (7, 64, 3000), (300, 100, 2000),
+                                                   (50, 1024, 256), (3, 5, 200000)])
+def test_gpu_matches_oracle(engine, oracle, R, max_entries, max_len):
+    b = random_requests(R * 7 + max_len, R, max_entries, max_len, oracle=oracle)
+    args = (b["req_off"], b["prev_log_index"], b["term"], b["etype"], b["data_len"],
+            b["checksum"], b["data"])
+    kw = dict(has_checksum=b["has_checksum"], peer_xor=b["peer_xor"])
+    e_out, e_cor, e_first = oracle.append_entries_verify(*args, **kw)
+    g_out, g_cor, g_first = engine.append_entries_verify(*args, **kw)
+    np.testing.assert_array_equal(g_out, e_out)
+    np.testing.assert_array_equal(g_cor, e_cor)
+    np.testing.assert_array_equal(g_first, e_first)
+
+
+@pytest.mark.gpu
+def test_gpu_empty_requests(engine, oracle):
+    req_off = np.array([0, 0, 0], np.uint32)
+    out, cor, first = engine.append_entries_verify(req_off, [5, 6], [], [], [], [], None)
+    assert list(first) == [-1, -1] and out.size == 0

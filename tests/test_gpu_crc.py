@@ -84,6 +84,22 @@ def test_tiny_segments_stress_straddlers(oracle, seg, monkeypatch):
             np.testing.assert_array_equal(e.crc64_batch(payload, offs), exp)
 
 
+@pytest.mark.parametrize("block,chains", [("64", "1"), ("128", "1"), ("64", "2"), ("128", "2")])
+def test_every_kernel_variant(oracle, block, chains, monkeypatch):
+    """Each load-block / chain variant is bit-exact on ragged, unaligned and long entries."""
+    from jraft_amd import Engine
+    monkeypatch.setenv("JRQ_CRC_BLOCK", block)
+    monkeypatch.setenv("JRQ_CRC_CHAINS", chains)
+    lens = [0, 1, 15, 16, 17, 255, 256, 257, 1023, 4099, 16384, 100000, 3 << 20, 7]
+    offs = np.concatenate([[5], 5 + np.cumsum(lens)]).astype(np.uint64)
+    payload = W.random_bytes(11, int(offs[-1]) + 2)
+    rag = W.ragged_offsets(12, 5000, 9000, start=1)
+    payload2 = W.random_bytes(13, int(rag[-1]) + 1)
+    with Engine(0) as e:
+        np.testing.assert_array_equal(e.crc64_batch(payload, offs), oracle.crc64_batch(payload, offs))
+        np.testing.assert_array_equal(e.crc64_batch(payload2, rag), oracle.crc64_batch(payload2, rag))
+
+
 def test_repeat_is_stable(engine, oracle):
     """Straddler scratch slots are re-zeroed by the last arriver: back-to-back calls agree."""
     offs = W.ragged_offsets(77, 5000, 9000)

@@ -72,6 +72,31 @@ def test_random_batches_single_run(engine, oracle, P):
     np.testing.assert_array_equal(s, se)
 
 
+@pytest.mark.parametrize("G", [1, 2, 3, 2999, 3001])
+def test_pair_and_scalar_paths(engine, oracle, G):
+    """Even G with aligned arrays takes the two-groups-per-lane kernel, odd G the scalar one;
+    a device batch whose match rows have an odd stride is forced onto the scalar kernel."""
+    import torch
+    b = random_batch(300 + G, G, 5, run_prob=0.0)
+    ce, se = _replay(oracle, b, runs=False)
+    c, s = _gpu(engine, b, runs=False)
+    np.testing.assert_array_equal(c, ce)
+    np.testing.assert_array_equal(s, se)
+    dev = torch.device("cuda:0")
+    wide = np.zeros((5, G + 1), np.int64)
+    wide[:, :G] = b["match"]
+    tm = torch.from_numpy(wide).to(dev)[:, :G]  # row stride G + 1
+    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v).to(dev)
+         for k, v in b.items() if k in ("pending_index", "last_appended", "last_committed", "conf")}
+    out = torch.empty(G, dtype=torch.int64, device=dev)
+    st = torch.empty(G, dtype=torch.uint8, device=dev)
+    engine.quorum_epoch_dev(tm, t["pending_index"], t["last_appended"], t["last_committed"],
+                            t["conf"], out, st)
+    engine.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), ce)
+    np.testing.assert_array_equal(st.cpu().numpy(), se)
+
+
 @pytest.mark.parametrize("cfg", ["C2", "C3"])
 def test_config_shapes_vs_replay(engine, oracle, cfg):
     """C2 / C3 shaped groups (1k pending each, 1024-entry ack chunks as the Replicator sends,

@@ -23,16 +23,18 @@ def main():
     dev = torch.device("cuda:0")
     s = torch.cuda.Stream(dev)
     torch.cuda.set_stream(s)
-    # variant = seg_mode:seg_bytes:block_bytes (seg_bytes 0 = automatic)
-    variants = [(v.split(":") + ["128"])[:3] for v in (sys.argv[1:] or ["0:0:128", "0:0:64"])]
+    # variant = seg_mode:seg_bytes:block_bytes:chains (seg_bytes 0 = automatic)
+    variants = [(v.split(":") + ["0", "0", "128", "1"][len(v.split(":")):])
+                for v in (sys.argv[1:] or ["0:0:128:1", "0:0:64:1", "0:0:64:2"])]
     engines = []
-    for mode, nbytes, blk in variants:
+    for mode, nbytes, blk, ch in variants:
         os.environ["JRQ_CRC_SEG_MODE"] = mode
         os.environ["JRQ_CRC_SEG_BYTES"] = nbytes
         os.environ["JRQ_CRC_BLOCK"] = blk
+        os.environ["JRQ_CRC_CHAINS"] = ch
         e = Engine(0)
         e.use_stream(s.cuda_stream)
-        engines.append((f"mode{mode}/S{nbytes}/B{blk}", e))
+        engines.append((f"mode{mode}/S{nbytes}/B{blk}/C{ch}", e))
     res = {}
     for cfg, n, eb in (("C5", 64 << 10, 16 << 10), ("C1", 1 << 20, 256)):
         b = W.entry_batch(n, eb, seed=3)
