@@ -197,6 +197,28 @@ int jrq_append_entries_verify(jrq_engine *e, uint32_t R, const uint32_t *req_off
                               uint64_t *checksum_out, uint8_t *corrupt_out,
                               int32_t *first_corrupt_out);
 
+/* ------------------------------------------------- leader lease / alive quorum -- */
+
+/* The q-of-n primitive on timestamps for G leader groups:
+ * NodeImpl.handleStepDownTimeout (JC/core/NodeImpl.java:2003-2016) -> checkDeadNodes0
+ * (:1970-2000) for the conf and, when not empty, the old conf.  Per group g:
+ *   last_rpc_ts[p*ld + g]  ReplicatorGroup.getLastRpcSendTimestamp of peer slot p
+ *   conf[g]                packed conf word (masks + quorums, JRQ_CONF)
+ *   self_slot[g]           the leader's own slot (always alive)
+ * A member is alive if now_ms - ts <= lease_timeout_ms.  ok_out[g] bit0 = the conf has an
+ * alive quorum, bit1 = the old conf has one (or there is none); lease_start_inout[g] is
+ * lastLeaderTimestamp, moved to the oldest alive timestamp by every passing check;
+ * dead_out[g] (nullable) = slots found dead.  A group with ok_out != 3 steps down
+ * (ERAFTTIMEDOUT "Majority of the group dies"). */
+int jrq_lease_check_dev(jrq_engine *e, const int64_t *last_rpc_ts_dev, uint64_t ld,
+                        uint32_t num_peers, const uint64_t *conf_dev, const uint8_t *self_slot_dev,
+                        uint32_t G, int64_t now_ms, int64_t lease_timeout_ms, uint8_t *ok_out_dev,
+                        int64_t *lease_start_inout_dev, uint16_t *dead_out_dev);
+int jrq_lease_check(jrq_engine *e, const int64_t *last_rpc_ts, uint64_t ld, uint32_t num_peers,
+                    const uint64_t *conf, const uint8_t *self_slot, uint32_t G, int64_t now_ms,
+                    int64_t lease_timeout_ms, uint8_t *ok_out, int64_t *lease_start_inout,
+                    uint16_t *dead_out);
+
 /* --------------------------------------------------- node-wide publication -- */
 
 /* Multi-GPU (one process per GPU): groups are sharded by contiguous groupId blocks.

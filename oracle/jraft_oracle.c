@@ -139,6 +139,62 @@ void jo_append_entries_verify(uint32_t R, const uint32_t *req_off, const int64_t
     }
 }
 
+/* ======================= leader lease (JC/core/NodeImpl.java) ============== */
+
+static int32_t mask_to_ids(uint32_t mask, int32_t *ids);
+
+int jo_check_dead_nodes(const int32_t *peers, int32_t n, const int64_t *ts, int32_t self,
+                        int64_t now_ms, int64_t lease_timeout_ms, int64_t *lease_start,
+                        uint32_t *dead_mask) {
+    int alive = 0;
+    int64_t start = INT64_MAX; /* long startLease = Long.MAX_VALUE */
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t p = peers[i];
+        if (p == self) { /* peer.equals(this.serverId) */
+            alive++;
+            continue;
+        }
+        /* monotonicNowMs - lastRpcSendTimestamp, Java long (wrapping) arithmetic */
+        const int64_t age = (int64_t)((uint64_t)now_ms - (uint64_t)ts[p]);
+        if (age <= lease_timeout_ms) {
+            alive++;
+            if (start > ts[p]) start = ts[p];
+            continue;
+        }
+        *dead_mask |= 1u << p;
+    }
+    if (alive >= n / 2 + 1) {
+        *lease_start = start; /* updateLastLeaderTimestamp(startLease) */
+        return 1;
+    }
+    return 0;
+}
+
+void jo_lease_check(uint32_t G, uint32_t P, const int64_t *ts, const uint64_t *conf,
+                    const uint8_t *self_slot, int64_t now_ms, int64_t lease_timeout_ms,
+                    uint8_t *ok, int64_t *lease_start, uint16_t *dead) {
+    int64_t *t = (int64_t *)malloc(sizeof(int64_t) * (P ? P : 1));
+    for (uint32_t g = 0; g < G; ++g) {
+        for (uint32_t p = 0; p < P; ++p) t[p] = ts[(size_t)p * G + g];
+        int32_t nids[16], oids[16];
+        const int32_t nn = mask_to_ids((uint32_t)(conf[g] & 0xFFFF), nids);
+        const int32_t no = mask_to_ids((uint32_t)((conf[g] >> 16) & 0xFFFF), oids);
+        uint32_t dm = 0;
+        uint8_t k = 0;
+        if (jo_check_dead_nodes(nids, nn, t, self_slot[g], now_ms, lease_timeout_ms, &lease_start[g], &dm))
+            k |= 1;
+        if (no > 0) { /* if (!this.conf.getOldConf().isEmpty()) */
+            if (jo_check_dead_nodes(oids, no, t, self_slot[g], now_ms, lease_timeout_ms, &lease_start[g], &dm))
+                k |= 2;
+        } else {
+            k |= 2;
+        }
+        ok[g] = k;
+        if (dead) dead[g] = (uint16_t)dm;
+    }
+    free(t);
+}
+
 /* ======================= Ballot (JC/entity/Ballot.java) ==================== */
 
 static void list_init(jo_peer_list *l, const int32_t *ids, int32_t n) {

@@ -65,6 +65,20 @@ void jo_append_entries_verify(uint32_t R, const uint32_t *req_off, const int64_t
                               const uint8_t *has_checksum, const uint8_t *data,
                               uint64_t *checksum_out, uint8_t *corrupt_out, int32_t *first_corrupt);
 
+/* NodeImpl.checkDeadNodes0 (JC/core/NodeImpl.java:1970-2000) over a peer list (ids),
+ * with lastRpcSendTimestamp per id in ts[] and the leader's own id `self`.  Returns 1 when
+ * the alive count reaches size/2+1 and then stores the lease start (oldest alive
+ * timestamp of a non-self member, INT64_MAX if none) in *lease_start; ORs the dead ids
+ * into *dead_mask. */
+int jo_check_dead_nodes(const int32_t *peers, int32_t n, const int64_t *ts, int32_t self,
+                        int64_t now_ms, int64_t lease_timeout_ms, int64_t *lease_start,
+                        uint32_t *dead_mask);
+/* handleStepDownTimeout (:2003-2016) for G groups with the engine's packed conf words
+ * (peer lists rebuilt from the masks in slot order): ok bit0 conf, bit1 old conf (or none). */
+void jo_lease_check(uint32_t G, uint32_t P, const int64_t *ts /* [P][G] */, const uint64_t *conf,
+                    const uint8_t *self_slot, int64_t now_ms, int64_t lease_timeout_ms,
+                    uint8_t *ok, int64_t *lease_start /* in/out */, uint16_t *dead);
+
 /* ---------------- Ballot (JC/entity/Ballot.java) --------------------------- */
 
 #define JO_MAX_CONF 32 /* peers per Configuration list kept by the oracle */

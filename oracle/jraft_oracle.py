@@ -69,6 +69,9 @@ def lib():
                                                  C.c_void_p]
         L.jo_append_entries_verify.restype = None
         L.jo_append_entries_verify.argtypes = [C.c_uint32] + [C.c_void_p] * 12
+        L.jo_lease_check.restype = None
+        L.jo_lease_check.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
         L.jo_bb_new.restype = C.c_void_p
         L.jo_bb_free.argtypes = [C.c_void_p]
         for name in ("jo_bb_last_committed_index", "jo_bb_pending_index", "jo_bb_queue_size",
@@ -178,6 +181,20 @@ def append_entries_verify(req_off, prev_log_index, term, etype, data_len, checks
                                    _ptr(px), _ptr(ck), _ptr(hs), _ptr(d), _ptr(out), _ptr(cor),
                                    _ptr(first))
     return out, cor, first
+
+
+def lease_check(last_rpc_ts, conf, self_slot, now_ms, lease_timeout_ms, lease_start):
+    """NodeImpl.handleStepDownTimeout -> checkDeadNodes0 per group (NodeImpl.java:1970-2016)."""
+    ts = np.ascontiguousarray(last_rpc_ts, np.int64)
+    P, G = ts.shape
+    conf = np.ascontiguousarray(conf, np.uint64)
+    ss = np.ascontiguousarray(self_slot, np.uint8)
+    lead = np.array(lease_start, dtype=np.int64, copy=True)
+    ok = np.zeros(G, np.uint8)
+    dead = np.zeros(G, np.uint16)
+    lib().jo_lease_check(G, P, _ptr(ts), _ptr(conf), _ptr(ss), now_ms, lease_timeout_ms,
+                         _ptr(ok), _ptr(lead), _ptr(dead))
+    return ok, lead, dead
 
 
 # ------------------------------------------------- pure-Python cross-checks --

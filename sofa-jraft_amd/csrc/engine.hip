@@ -22,6 +22,7 @@ extern "C" hipError_t jrq_launch_crc64(const JrqCrcArgs* args, int log_entry, in
                                        hipStream_t stream);
 extern "C" hipError_t jrq_launch_quorum(const JrqQuorumArgs* args, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_meta(const JrqAeArgs* a, hipStream_t stream);
+extern "C" hipError_t jrq_launch_lease(const JrqLeaseArgs* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_first_corrupt(const JrqAeArgs* a, hipStream_t stream);
 
 namespace {
@@ -464,6 +465,67 @@ int jrq_logentry_checksum_batch(jrq_engine* e, const uint8_t* type, const int64_
     return rc;
   JRQ_HIP(e, hipMemcpyAsync(out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
   if (corrupt_out) JRQ_HIP(e, hipMemcpyAsync(corrupt_out, dcor, N, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
+// --------------------------------------------------------------- lease -----
+
+int jrq_lease_check_dev(jrq_engine* e, const int64_t* ts, uint64_t ld, uint32_t num_peers,
+                        const uint64_t* conf, const uint8_t* self_slot, uint32_t G, int64_t now_ms,
+                        int64_t lease_timeout_ms, uint8_t* ok_out, int64_t* lease_start,
+                        uint16_t* dead_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (G == 0) return JRQ_OK;
+  if (!ts || !conf || !self_slot || !ok_out || !lease_start || ld < G || num_peers == 0 ||
+      num_peers > JRQ_MAX_PEERS)
+    return fail(e, JRQ_E_INVALID, "bad lease batch");
+  DeviceGuard guard(e->device);
+  JrqLeaseArgs a{};
+  a.last_rpc_ts = ts;
+  a.ld = ld;
+  a.conf = conf;
+  a.self_slot = self_slot;
+  a.now_ms = now_ms;
+  a.lease_timeout_ms = lease_timeout_ms;
+  a.num_peers = num_peers;
+  a.G = G;
+  a.ok = ok_out;
+  a.lease_start = lease_start;
+  a.dead = dead_out;
+  JRQ_HIP(e, jrq_launch_lease(&a, e->num_cus, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_lease_check(jrq_engine* e, const int64_t* ts, uint64_t ld, uint32_t num_peers,
+                    const uint64_t* conf, const uint8_t* self_slot, uint32_t G, int64_t now_ms,
+                    int64_t lease_timeout_ms, uint8_t* ok_out, int64_t* lease_start,
+                    uint16_t* dead_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (G == 0) return JRQ_OK;
+  if (!ts || !conf || !self_slot || !ok_out || !lease_start || ld < G || num_peers == 0 ||
+      num_peers > JRQ_MAX_PEERS)
+    return fail(e, JRQ_E_INVALID, "bad lease batch");
+  DeviceGuard guard(e->device);
+  int rc;
+  const int64_t* dts;
+  const uint64_t* dconf;
+  const uint8_t* dself;
+  const int64_t* dlead;
+  if ((rc = stage_in(e, 0, ts, (num_peers - 1) * ld + G, &dts))) return rc;
+  if ((rc = stage_in(e, 1, conf, G, &dconf))) return rc;
+  if ((rc = stage_in(e, 2, self_slot, G, &dself))) return rc;
+  if ((rc = stage_in(e, 3, lease_start, G, &dlead))) return rc;
+  void *dok, *ddead;
+  if ((rc = ensure_stage(e, 8, G, &dok))) return rc;
+  if ((rc = ensure_stage(e, 9, static_cast<size_t>(G) * 2, &ddead))) return rc;
+  if ((rc = jrq_lease_check_dev(e, dts, ld, num_peers, dconf, dself, G, now_ms, lease_timeout_ms,
+                                static_cast<uint8_t*>(dok), const_cast<int64_t*>(dlead),
+                                static_cast<uint16_t*>(ddead))))
+    return rc;
+  JRQ_HIP(e, hipMemcpyAsync(ok_out, dok, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(lease_start, dlead, static_cast<size_t>(G) * 8, hipMemcpyDeviceToHost, e->stream));
+  if (dead_out) JRQ_HIP(e, hipMemcpyAsync(dead_out, ddead, static_cast<size_t>(G) * 2, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }

@@ -59,6 +59,21 @@ struct JrqCrcArgs {
   uint32_t chains;         // independent CRC chains per lane: 1 or 2
 };
 
+// Leader lease / alive-quorum check (quorum.hip, lease kernel).
+struct JrqLeaseArgs {
+  const int64_t* last_rpc_ts;   // [P][ld] lastRpcSendTimestamp per peer slot
+  uint64_t ld;
+  const uint64_t* conf;         // [G] packed conf word (masks + quorums)
+  const uint8_t* self_slot;     // [G] the leader's own slot (always alive)
+  int64_t now_ms;
+  int64_t lease_timeout_ms;
+  uint32_t num_peers;
+  uint32_t G;
+  uint8_t* ok;                  // [G] bit0 conf quorum alive, bit1 old-conf quorum alive (or no old conf)
+  int64_t* lease_start;         // [G] lastLeaderTimestamp after the checks (in/out)
+  uint16_t* dead;               // [G] peer slots found dead (new | old conf), nullable
+};
+
 // AppendEntries batch verify (append_entries.hip): inputs + engine scratch.
 struct JrqAeArgs {
   uint32_t r;                      // requests

@@ -173,7 +173,88 @@ __global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a)
   }
 }
 
+// ------------------------------------------------------------------ lease ---
+// NodeImpl.checkDeadNodes0 (jraft-core/.../core/NodeImpl.java:1970-2000) for one conf:
+// the leader itself is alive; another member is alive when now - lastRpcSendTimestamp <=
+// leaderLeaseTimeoutMs (Java long arithmetic: wrapping subtraction); the lease starts at
+// the oldest alive timestamp (Long.MAX_VALUE if none); the check passes when
+// alive >= quorum (peers.size()/2 + 1).
+template <int P>
+__device__ __forceinline__ bool alive_quorum(const int64_t (&ts)[P], uint32_t mask, uint32_t q,
+                                             uint32_t self, int64_t now, int64_t timeout,
+                                             int64_t& start, uint16_t& dead) {
+  uint32_t alive = 0;
+  start = kI64Max;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const bool member = (mask >> p) & 1u;
+    const bool is_self = static_cast<uint32_t>(p) == self;
+    const int64_t age = static_cast<int64_t>(static_cast<uint64_t>(now) - static_cast<uint64_t>(ts[p]));
+    const bool fresh = age <= timeout;
+    alive += (member && (is_self || fresh)) ? 1u : 0u;
+    start = (member && !is_self && fresh && ts[p] < start) ? ts[p] : start;
+    dead |= (member && !is_self && !fresh) ? static_cast<uint16_t>(1u << p) : 0;
+  }
+  return alive >= q;
+}
+
+// NodeImpl.handleStepDownTimeout (:2003-2016): check the conf, then the old conf when it
+// is not empty; every passing check moves lastLeaderTimestamp to its lease start.
+template <int P>
+__global__ __launch_bounds__(256) void lease_check_kernel(JrqLeaseArgs a) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G; g += stride) {
+    int64_t ts[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) ts[p] = a.last_rpc_ts[static_cast<size_t>(p) * a.ld + g];
+    const uint64_t cw = a.conf[g];
+    const uint32_t self = a.self_slot[g];
+    int64_t lead = a.lease_start[g];
+    uint16_t dead = 0;
+    int64_t start;
+    uint8_t ok = 0;
+    if (alive_quorum<P>(ts, cw & 0xFFFFu, (cw >> 32) & 0xFFu, self, a.now_ms, a.lease_timeout_ms,
+                        start, dead)) {
+      lead = start;
+      ok |= 1;
+    }
+    const uint32_t omask = (cw >> 16) & 0xFFFFu;
+    if (omask != 0) {
+      if (alive_quorum<P>(ts, omask, (cw >> 40) & 0xFFu, self, a.now_ms, a.lease_timeout_ms,
+                          start, dead)) {
+        lead = start;
+        ok |= 2;
+      }
+    } else {
+      ok |= 2;  // no old conf to check
+    }
+    a.ok[g] = ok;
+    a.lease_start[g] = lead;
+    if (a.dead) a.dead[g] = dead;
+  }
+}
+
 }  // namespace jrq
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_lease(
+    const JrqLeaseArgs* args, int num_cus, hipStream_t stream) {
+  const uint64_t need = (static_cast<uint64_t>(args->G) + 255) / 256;
+  const uint64_t cap = static_cast<uint64_t>(num_cus) * 8;
+  const dim3 grid(static_cast<unsigned>(need < cap ? (need ? need : 1) : cap)), blk(256);
+  switch (args->num_peers) {
+#define JRQ_CASE(P)                                                                    \
+  case P:                                                                              \
+    hipLaunchKernelGGL(jrq::lease_check_kernel<P>, grid, blk, 0, stream, *args); \
+    break;
+    JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
+    JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
+    JRQ_CASE(15) JRQ_CASE(16)
+#undef JRQ_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
     const JrqQuorumArgs* args, int num_cus, hipStream_t stream) {

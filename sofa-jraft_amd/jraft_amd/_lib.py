@@ -67,6 +67,10 @@ SIGNATURES = [
      [_V, C.c_uint32, _V, _V, C.c_uint32, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
     ("jrq_append_entries_verify", C.c_int,
      [_V, C.c_uint32, _V, _V, C.c_uint32, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+    ("jrq_lease_check_dev", C.c_int,
+     [_V, _V, C.c_uint64, C.c_uint32, _V, _V, C.c_uint32, C.c_int64, C.c_int64, _V, _V, _V]),
+    ("jrq_lease_check", C.c_int,
+     [_V, _V, C.c_uint64, C.c_uint32, _V, _V, C.c_uint32, C.c_int64, C.c_int64, _V, _V, _V]),
     ("jrq_rccl_get_unique_id", C.c_int, [_V]),
     ("jrq_rccl_init", C.c_int, [_V, C.c_int, C.c_int, _V]),
     ("jrq_publish_committed_dev", C.c_int, [_V, _V, _V, C.c_uint64]),

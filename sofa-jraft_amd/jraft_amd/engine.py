@@ -167,6 +167,22 @@ class Engine:
             _dev_ptr(payload), _dev_ptr(offsets), n, _dev_ptr(out), _dev_ptr(expected),
             _dev_ptr(has), _dev_ptr(corrupt)), self._h)
 
+    # ------------------------------------------------------------ lease --
+    def lease_check(self, last_rpc_ts, conf, self_slot, now_ms, lease_timeout_ms,
+                    lease_start):
+        """Host variant: returns (ok uint8[G], lease_start int64[G], dead uint16[G])."""
+        ts = _c(last_rpc_ts, np.int64)
+        P, G = ts.shape
+        conf = _c(conf, np.uint64)
+        self_slot = _c(self_slot, np.uint8)
+        lead = np.array(lease_start, dtype=np.int64, copy=True)
+        ok = np.zeros(G, np.uint8)
+        dead = np.zeros(G, np.uint16)
+        check(self._L.jrq_lease_check(self._h, _np_ptr(ts), G, P, _np_ptr(conf), _np_ptr(self_slot),
+                                      G, now_ms, lease_timeout_ms, _np_ptr(ok), _np_ptr(lead),
+                                      _np_ptr(dead)), self._h)
+        return ok, lead, dead
+
     # ------------------------------------------------- AppendEntries verify --
     def append_entries_verify(self, req_off, prev_log_index, term, etype, data_len, checksum,
                               data, has_checksum=None, peer_xor=None):
