@@ -57,6 +57,25 @@ def to_dev(arr, dev):
     return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/<tag>_pmc.json, written by tools/summarize_profiles.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench); None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                ks = json.load(fh).get("kernels", {})
+        except (OSError, ValueError):
+            continue
+        for name, d in ks.items():
+            if kernel in name and "hbm_bytes_per_launch_corrected" in d:
+                return {"bytes": d["hbm_bytes_per_launch_corrected"],
+                        "source": os.path.relpath(f, ROOT) + " (2*FETCH_SIZE+WRITE_SIZE, KiB->B)"}
+    return None
+
+
 def timed_launches(fn, steps, warmup, stream, sync):
     """warmup untimed, then `steps` launches each bracketed by HIP events on `stream`."""
     import torch
@@ -279,6 +298,56 @@ def main():
                          "frac": alg / (crc_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None},
         }
 
+    # ------------------------------------------------ §8f legs ---------------
+    extras = {}
+    if not args.no_crc:
+        # follower verify on receive: the C5 payload as 64 AppendEntries of 1024 entries
+        R = n // 1024
+        req_off = torch.arange(0, n + 1, 1024, dtype=torch.int32, device=dev)
+        prev = torch.arange(0, n, 1024, dtype=torch.int64, device=dev)  # index = 1..n
+        dlen = torch.full((n,), c5["entry_bytes"], dtype=torch.int64, device=dev)
+        ae_out = torch.empty(n, dtype=torch.int64, device=dev)
+        ae_cor = torch.empty(n, dtype=torch.uint8, device=dev)
+        ae_first = torch.empty(R, dtype=torch.int32, device=dev)
+
+        def ae_step(i=None):
+            eng.append_entries_verify_dev(req_off, prev, d["term"], d["etype"], dlen, d_exp,
+                                          d["payload"], ae_out, ae_cor, ae_first)
+
+        _, ae_ms = timed_launches(ae_step, max(5, args.steps // 5), 2, stream, sync)
+        ae_avg = float(np.mean(ae_ms))
+        ae_ok = None
+        if rank == 0 and not args.no_cpu:
+            ae_ok = bool(np.array_equal(ae_out.cpu().numpy().view(np.uint64), expected)) and \
+                bool((ae_first.cpu().numpy() == 0).all())  # entry 0 of each request is flipped
+        extras["append_entries_verify"] = {
+            "workload": f"{R} AppendEntries requests x 1024 EntryMeta x 16 KiB (C5 payload)",
+            "GBps_payload": pay / (ae_avg * 1e-3) / 1e9, "ms_per_batch": ae_avg,
+            "bit_exact_vs_oracle": ae_ok}
+    # leader lease / alive quorum on C3-shaped groups
+    rng = np.random.default_rng(rank)
+    now_ms, lease_to = 1 << 40, 900
+    ts_np = (now_ms - rng.integers(0, 2 * lease_to, (P, G))).astype(np.int64)
+    ts = to_dev(ts_np, dev)
+    self_slot = torch.zeros(G, dtype=torch.uint8, device=dev)
+    lead = torch.zeros(G, dtype=torch.int64, device=dev)
+    lok = torch.empty(G, dtype=torch.uint8, device=dev)
+    ldead = torch.empty(G, dtype=torch.int16, device=dev)
+    lconf = epochs[0]["conf"]
+
+    def lease_step(i=None):
+        eng.lease_check_dev(ts, lconf, self_slot, now_ms, lease_to, lok, lead, ldead)
+
+    _, lease_ms = timed_launches(lease_step, args.steps, args.warmup, stream, sync)
+    lease_avg = float(np.mean(lease_ms))
+    lb = (8 * P + 28) * G
+    extras["lease_check"] = {
+        "workload": f"{G} leader groups x {P} peers (conf + old conf), checkDeadNodes0",
+        "decisions_per_s": G / (lease_avg * 1e-3), "kernel_ms": lease_avg,
+        "roofline": {"bound": "hbm", "achieved": lb / (lease_avg * 1e-3) / 1e9,
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": lb / (lease_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS}}
+
     # ------------------------------------------------ CPU baselines ---------
     cpu_q = cpu_c = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -312,14 +381,25 @@ def main():
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                         "kernel": "quorum_epoch_kernel<5>", "kernel_ms": k_avg_ms,
+                         "kernel": "quorum_epoch_pair_kernel<5>", "kernel_ms": k_avg_ms,
                          "bytes_per_launch": q_bytes},
             "cpu_baseline": cpu_q,
             "crc64": crc,
             "C2": {"workload": "C2: 10k groups x 3 peers x 1k pending (configs[1])",
                    "decisions_per_s": G2 * args.steps / c2_wall,
+                   "entry_ballots_per_s": G2 * 1024 * args.steps / c2_wall,
                    "kernel_ms": float(np.mean(c2_ms))},
+            "next_rows": extras,
         }
+        tr = pmc_traffic("quorum_epoch_pair_kernel<5>")
+        if tr is not None:
+            line["roofline"]["traffic"] = tr["bytes"]
+            line["roofline"]["traffic_source"] = tr["source"]
+        if crc is not None:
+            tr = pmc_traffic("crc64_segments_kernel<true")
+            if tr is not None:
+                crc["roofline"]["traffic"] = tr["bytes"]
+                crc["roofline"]["traffic_source"] = tr["source"]
         print(json.dumps(line))
     eng.use_stream(None)
     if world > 1:

@@ -183,6 +183,15 @@ class Engine:
                                       _np_ptr(dead)), self._h)
         return ok, lead, dead
 
+    def lease_check_dev(self, last_rpc_ts, conf, self_slot, now_ms, lease_timeout_ms, ok_out,
+                        lease_start_inout, dead_out=None):
+        P = last_rpc_ts.shape[0]
+        G = conf.shape[0]
+        check(self._L.jrq_lease_check_dev(self._h, _dev_ptr(last_rpc_ts), last_rpc_ts.stride(0), P,
+                                          _dev_ptr(conf), _dev_ptr(self_slot), G, now_ms,
+                                          lease_timeout_ms, _dev_ptr(ok_out),
+                                          _dev_ptr(lease_start_inout), _dev_ptr(dead_out)), self._h)
+
     # ------------------------------------------------- AppendEntries verify --
     def append_entries_verify(self, req_off, prev_log_index, term, etype, data_len, checksum,
                               data, has_checksum=None, peer_xor=None):
