@@ -6,115 +6,164 @@
 //   LogEntry.checksum()     jraft-core/.../entity/LogEntry.java:88-108
 //   LogEntry.isCorrupted()  jraft-core/.../entity/LogEntry.java:156-158
 //
-// Design (DESIGN.md §CRC64 has the roofline):
-//  * The payload is cut into equal flat SEGMENTS of S = 2^s bytes (S from the
-//    batch size so that every lane of the persistent grid gets ~1 segment); each
-//    lane walks its segment entry by entry with a serial table CRC.  Work per
-//    lane is the same whatever the entry-length distribution.
-//  * The CRC is linear over GF(2) with init 0, so a piece of an entry that ends
-//    n bytes before the entry's end contributes crc(piece) * x^(8n) mod P, and
-//    the entry's CRC is the XOR of its pieces.  Pieces of entries that straddle a
-//    segment boundary are XOR-combined in a scratch slot with agent-scope
-//    atomics; the last arriving piece (arrival counter) writes the result and
-//    re-zeroes the slot.
-//  * Byte-serial update in the "reversed domain": with r = bswap64(crc), one
-//    2-byte step is r = (r >> 16) ^ R1[r & 0xFF] ^ R0[(r >> 8) & 0xFF], and a
-//    little-endian 8-byte load XORs straight into r (no byte swaps).  R0/R1 live
-//    in LDS replicated 32x so that lane l only touches bank slot l&31: every
-//    ds_read_b64 is conflict-free.  One step = 2 v_perm (LDS address), 2 LDS
-//    reads, 1 v_alignbit + 1 shift, 2 v_bitop3 (XOR3).
-//  * The x^(8n) multiplications use byte tables in global memory (one per power
-//    of two, L2-resident); they run at most once per piece that does not end its
-//    entry, i.e. at most once per segment.
+// Design (DESIGN.md §4.2 has the roofline):
+//  * The payload is cut into equal flat SEGMENTS of S bytes (S from the batch size so
+//    that every lane of the persistent grid gets ~1 segment); each lane walks its
+//    segment entry by entry with a serial table CRC.  Work per lane is the same
+//    whatever the entry-length distribution.
+//  * The CRC is linear over GF(2) with init 0, so a piece of an entry that ends n bytes
+//    before the entry's end contributes crc(piece) * x^(8n) mod P, and the entry's CRC is
+//    the XOR of its pieces.  Pieces of entries that straddle a segment boundary are
+//    XOR-combined in a scratch slot with agent-scope atomics; the last arriving piece
+//    (arrival counter) writes the result and re-zeroes the slot.
+//  * Table CRC in the "reversed domain" r = bswap64(crc): a little-endian 8-byte load
+//    XORs straight into r (no byte swaps), and one k-byte step is
+//      r = (r >> 8k) ^ R_{k-1}[byte 0 of r] ^ ... ^ R_0[byte k-1 of r],
+//    R_j = bswap(T_j), T_j[i] = i * x^(64 + 8j) mod P.  Two LDS table flavours:
+//      Tab2: slice-by-2, R0/R1 replicated 32x so lane l only touches bank pair l&31
+//            (conflict-free): per 2 bytes 2 v_perm + 2 ds_read_b64 + 2 shifts + 2 XOR3.
+//      Tab4: slice-by-4, R0..R3 replicated 16x, two tables interleaved per 16-B slot:
+//            per 4 bytes 4 v_perm + 4 ds_read_b64 (2-way bank conflicts) + 4 XOR3/XOR,
+//            the 32-bit shift is free (register rename); half the dependent LDS round
+//            trips per byte of Tab2.
+//    Either way an LDS address is one v_perm of a data byte and a lane constant.
+//  * The x^(8n) multiplications use byte tables in global memory (one per power of two,
+//    L2-resident); they run at most once per piece that does not end its entry.
 #include "jrq_device.h"
 
 namespace jrq {
 
-// LDS address selectors for v_perm_b32 (S0 = lane constant, S1 = r.lo):
-//   lane constant: byte0 = (l&31)<<3, byte2 = 1 (table R1 at +64 KiB)
-//   R1 index = r byte 0 -> address byte1; R0 index = r byte 1 -> address byte1.
-constexpr uint32_t kSelR1 = 0x0C060004u;  // {lc.b0, lo.b0, lc.b2, 0}
-constexpr uint32_t kSelR0 = 0x0C0C0104u;  // {lc.b0, lo.b1, 0, 0}
-
 struct RState {
   uint32_t lo, hi;
 };
-
-__device__ __forceinline__ void step2(RState& r, const char* lds, uint32_t lc) {
-  const uint32_t a1 = __builtin_amdgcn_perm(lc, r.lo, kSelR1);
-  const uint32_t a0 = __builtin_amdgcn_perm(lc, r.lo, kSelR0);
-  const uint2 t1 = *reinterpret_cast<const uint2*>(lds + a1);
-  const uint2 t0 = *reinterpret_cast<const uint2*>(lds + a0);
-  const uint32_t nlo = __builtin_amdgcn_alignbit(r.hi, r.lo, 16);
-  const uint32_t nhi = r.hi >> 16;
-  r.lo = xor3(nlo, t1.x, t0.x);
-  r.hi = xor3(nhi, t1.y, t0.y);
-}
-
-// One byte: r = R0[(r ^ b) & 0xFF] ^ (r >> 8)   (CRC64.update(byte), CRC64.java:100-103)
-__device__ __forceinline__ void step1(RState& r, uint32_t b, const char* lds, uint32_t lc) {
-  const uint32_t a0 = __builtin_amdgcn_perm(lc, r.lo ^ b, 0x0C0C0004u);
-  const uint2 t0 = *reinterpret_cast<const uint2*>(lds + a0);
-  const uint32_t nlo = __builtin_amdgcn_alignbit(r.hi, r.lo, 8);
-  r.lo = nlo ^ t0.x;
-  r.hi = (r.hi >> 8) ^ t0.y;
-}
-
-// Eight bytes given as a little-endian (lo, hi) dword pair.
-__device__ __forceinline__ void step8(RState& r, uint32_t dlo, uint32_t dhi, const char* lds,
-                                      uint32_t lc) {
-  r.lo ^= dlo;
-  r.hi ^= dhi;
-  step2(r, lds, lc);
-  step2(r, lds, lc);
-  step2(r, lds, lc);
-  step2(r, lds, lc);
-}
-
-__device__ __forceinline__ void step16(RState& r, const uint4& v, const char* lds, uint32_t lc) {
-  step8(r, v.x, v.y, lds, lc);
-  step8(r, v.z, v.w, lds, lc);
-}
 
 __device__ __forceinline__ uint64_t crc_value(const RState& r) {
   // crc = bswap64(r)
   return (static_cast<uint64_t>(__builtin_bswap32(r.lo)) << 32) | __builtin_bswap32(r.hi);
 }
 
-// CRC of payload[a, b) from a zero register.
-template <int BV>
-__device__ __forceinline__ uint64_t crc_range(const uint8_t* __restrict__ payload, uint64_t a,
-                                              uint64_t b, const char* lds, uint32_t lc) {
+__device__ __forceinline__ uint2 lds_u2(const char* lds, uint32_t addr) {
+  return *reinterpret_cast<const uint2*>(lds + addr);
+}
+
+// ------------------------------------------------------------ slice-by-2 ---
+// LDS image: byte address = table<<16 | index<<8 | (lane&31)<<3 (R0 at 0, R1 at 64 KiB).
+struct Tab2 {
+  static constexpr uint32_t kSelR1 = 0x0C060004u;  // {lc.b0, lo.b0, lc.b2, 0}
+  static constexpr uint32_t kSelR0 = 0x0C0C0104u;  // {lc.b0, lo.b1, 0, 0}
+  uint32_t lc;  // byte0 = (lane&31)<<3, byte2 = 1
+  __device__ explicit Tab2(uint32_t lane) : lc(((lane & 31u) << 3) | (1u << 16)) {}
+
+  // word w of the image holds R_{w>>13}[(w>>5)&255]
+  __device__ static uint32_t src_index(uint32_t w) { return (w >> 13) * 256 + ((w >> 5) & 255u); }
+
+  __device__ __forceinline__ void step2(RState& r, const char* lds) const {
+    const uint2 t1 = lds_u2(lds, __builtin_amdgcn_perm(lc, r.lo, kSelR1));
+    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc, r.lo, kSelR0));
+    const uint32_t nlo = __builtin_amdgcn_alignbit(r.hi, r.lo, 16);
+    const uint32_t nhi = r.hi >> 16;
+    r.lo = xor3(nlo, t1.x, t0.x);
+    r.hi = xor3(nhi, t1.y, t0.y);
+  }
+  // one byte: r = R0[(r ^ b) & 0xFF] ^ (r >> 8)   (CRC64.update(byte), CRC64.java:100-103)
+  __device__ __forceinline__ void step1(RState& r, uint32_t b, const char* lds) const {
+    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc, r.lo ^ b, 0x0C0C0004u));
+    const uint32_t nlo = __builtin_amdgcn_alignbit(r.hi, r.lo, 8);
+    r.lo = nlo ^ t0.x;
+    r.hi = (r.hi >> 8) ^ t0.y;
+  }
+  // eight bytes as a little-endian (lo, hi) dword pair
+  __device__ __forceinline__ void step8(RState& r, uint32_t dlo, uint32_t dhi,
+                                        const char* lds) const {
+    r.lo ^= dlo;
+    r.hi ^= dhi;
+    step2(r, lds);
+    step2(r, lds);
+    step2(r, lds);
+    step2(r, lds);
+  }
+};
+
+// ------------------------------------------------------------ slice-by-4 ---
+// LDS image: byte address = (k>>1)<<16 | index<<8 | (lane&15)<<4 | (k&1)<<3 for table R_k
+// (16 replicas; R0/R1 share the 16-B slots of the first 64 KiB, R2/R3 of the second).
+struct Tab4 {
+  uint32_t lc0, lc1, lc2, lc3;  // byte0 = (lane&15)<<4 | (k&1)<<3, byte2 = k>>1
+  __device__ explicit Tab4(uint32_t lane)
+      : lc0(((lane & 15u) << 4)),
+        lc1(((lane & 15u) << 4) | 8u),
+        lc2(((lane & 15u) << 4) | (1u << 16)),
+        lc3(((lane & 15u) << 4) | 8u | (1u << 16)) {}
+
+  // word w = (k>>1)<<13 | index<<5 | replica<<1 | (k&1)
+  __device__ static uint32_t src_index(uint32_t w) {
+    return (((w >> 13) << 1) | (w & 1u)) * 256 + ((w >> 5) & 255u);
+  }
+
+  // four bytes already XORed into r.lo: r = (r >> 32) ^ R3[b0] ^ R2[b1] ^ R1[b2] ^ R0[b3]
+  __device__ __forceinline__ void step4(RState& r, const char* lds) const {
+    const uint2 t3 = lds_u2(lds, __builtin_amdgcn_perm(lc3, r.lo, 0x0C060004u));
+    const uint2 t2 = lds_u2(lds, __builtin_amdgcn_perm(lc2, r.lo, 0x0C060104u));
+    const uint2 t1 = lds_u2(lds, __builtin_amdgcn_perm(lc1, r.lo, 0x0C060204u));
+    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc0, r.lo, 0x0C060304u));
+    r.lo = xor3(xor3(r.hi, t3.x, t2.x), t1.x, t0.x);
+    r.hi = xor3(t3.y, t2.y, t1.y) ^ t0.y;
+  }
+  __device__ __forceinline__ void step1(RState& r, uint32_t b, const char* lds) const {
+    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc0, r.lo ^ b, 0x0C060004u));
+    const uint32_t nlo = __builtin_amdgcn_alignbit(r.hi, r.lo, 8);
+    r.lo = nlo ^ t0.x;
+    r.hi = (r.hi >> 8) ^ t0.y;
+  }
+  __device__ __forceinline__ void step8(RState& r, uint32_t dlo, uint32_t dhi,
+                                        const char* lds) const {
+    r.lo ^= dlo;
+    r.hi ^= dhi;
+    step4(r, lds);
+    step4(r, lds);
+  }
+};
+
+template <class Tab>
+__device__ __forceinline__ void step16(const Tab& tb, RState& r, const uint4& v, const char* lds) {
+  tb.step8(r, v.x, v.y, lds);
+  tb.step8(r, v.z, v.w, lds);
+}
+
+// CRC of payload[a, b) from a zero register, one chain.
+// Blocks of 16*BV bytes go through a 2-deep register ring: block i+1's loads are issued
+// before block i is hashed, unconditionally (address clamped to the last block), so the
+// compiler's wait before block i is a counted vmcnt(BV), not vmcnt(0).  Unrolled by two
+// with fixed buffer roles: a loaded register is never copied (a copy would force the wait
+// early).  The empty asm after each load group is a compiler memory barrier: the loads
+// may not be re-issued (rematerialised) at their use a block later; it implies no
+// hardware wait.  BV = 8 reads whole 128-B lines per lane.
+template <class Tab, int BV>
+__device__ __forceinline__ uint64_t crc_range(const Tab& tb, const uint8_t* __restrict__ payload,
+                                              uint64_t a, uint64_t b, const char* lds) {
   RState r{0u, 0u};
   uint64_t p = a;
   const uint64_t mis = reinterpret_cast<uintptr_t>(payload) & 15u;
   while (p < b && ((p + mis) & 15u)) {  // unaligned head (by address), byte-serial
-    step1(r, payload[p], lds, lc);
+    tb.step1(r, payload[p], lds);
     ++p;
   }
-  // Blocks of 16*BV bytes through a 2-deep register ring: block i+1's loads are issued
-  // before block i is hashed, unconditionally (address clamped to the last block), so
-  // the compiler's wait before block i is a counted vmcnt(BV), not vmcnt(0).  Unrolled
-  // by two with fixed buffer roles: a loaded register is never copied (a copy would
-  // force the wait early).  The empty asm after each load group is a compiler memory
-  // barrier: the loads may not be re-issued (rematerialised) at their use a block
-  // later; it implies no hardware wait.  BV = 8 reads whole 128-B lines per lane.
   constexpr uint32_t kBlkBytes = 16u * BV;
   const uint64_t nblk = (b - p) / kBlkBytes;
   if (nblk != 0) {
     const uint4* q = reinterpret_cast<const uint4*>(payload + p);
     const uint64_t last = nblk - 1;
     uint4 A[BV], B[BV];
-#define JRQ_LOAD(X, blk)                                 \
-  do {                                                   \
-    const uint64_t bb = (blk) < last ? (blk) : last;     \
-    const uint4* qq = q + BV * bb;                       \
-    _Pragma("unroll") for (int v = 0; v < BV; ++v) X[v] = qq[v]; \
-    asm volatile("" ::: "memory");                       \
+#define JRQ_LOAD(X, blk)                                             \
+  do {                                                               \
+    const uint64_t bb = (blk) < last ? (blk) : last;                 \
+    const uint4* qq = q + BV * bb;                                   \
+    _Pragma("unroll") for (int v = 0; v < BV; ++v) X[v] = qq[v];     \
+    asm volatile("" ::: "memory");                                   \
   } while (0)
-#define JRQ_HASH(X)                                                          \
-  do {                                                                       \
-    _Pragma("unroll") for (int v = 0; v < BV; ++v) step16(r, X[v], lds, lc); \
+#define JRQ_HASH(X)                                                             \
+  do {                                                                          \
+    _Pragma("unroll") for (int v = 0; v < BV; ++v) step16(tb, r, X[v], lds);    \
   } while (0)
     JRQ_LOAD(A, 0);
     for (uint64_t i = 0;;) {
@@ -130,29 +179,13 @@ __device__ __forceinline__ uint64_t crc_range(const uint8_t* __restrict__ payloa
     p += nblk * kBlkBytes;
   }
   while (p + 16 <= b) {
-    const uint4 v = *reinterpret_cast<const uint4*>(payload + p);
-    step16(r, v, lds, lc);
+    step16(tb, r, *reinterpret_cast<const uint4*>(payload + p), lds);
     p += 16;
   }
-  while (p + 2 <= b) {  // tail
-    const uint32_t w = payload[p] | (static_cast<uint32_t>(payload[p + 1]) << 8);
-    r.lo ^= w;
-    step2(r, lds, lc);
-    p += 2;
+  while (p < b) {  // tail, byte-serial
+    tb.step1(r, payload[p], lds);
+    ++p;
   }
-  if (p < b) step1(r, payload[p], lds, lc);
-  return crc_value(r);
-}
-
-// LogId.checksum(): crc64(BE64(index) || BE64(term))  (LogId.java:45-50, Bits.java:71-80).
-// The big-endian bytes, read as a little-endian u64, are bswap64(v).
-__device__ __forceinline__ uint64_t logid_crc(int64_t index, int64_t term, const char* lds,
-                                              uint32_t lc) {
-  RState r{0u, 0u};
-  const uint64_t bi = bswap64(static_cast<uint64_t>(index));
-  const uint64_t bt = bswap64(static_cast<uint64_t>(term));
-  step8(r, static_cast<uint32_t>(bi), static_cast<uint32_t>(bi >> 32), lds, lc);
-  step8(r, static_cast<uint32_t>(bt), static_cast<uint32_t>(bt >> 32), lds, lc);
   return crc_value(r);
 }
 
@@ -170,21 +203,21 @@ __device__ __forceinline__ uint64_t crc_shift(uint64_t c, uint64_t n,
   return c;
 }
 
-// Two independent chains per lane: [a, b) is cut at m into halves that are hashed in
-// lockstep (their 2-byte steps interleave, so one chain's LDS latency hides under the
-// other's), then crc = crc(X) * x^(8|Y|) ^ crc(Y).  Both halves move through 64-B
-// blocks with a 2-deep register ring each; X takes the unaligned head first, Y the tail
-// last.  Short ranges fall back to one chain.
-__device__ __forceinline__ uint64_t crc_range2(const uint8_t* __restrict__ payload, uint64_t a,
-                                               uint64_t b, const char* lds, uint32_t lc,
+// Two independent chains per lane: [a, b) is cut at m into halves hashed in lockstep
+// (one chain's LDS latency hides under the other's), then crc = crc(X) * x^(8|Y|) ^ crc(Y).
+// 64-B blocks with a 2-deep register ring per chain; X takes the unaligned head first, Y
+// the tail last.  Short ranges fall back to one chain.
+template <class Tab>
+__device__ __forceinline__ uint64_t crc_range2(const Tab& tb, const uint8_t* __restrict__ payload,
+                                               uint64_t a, uint64_t b, const char* lds,
                                                const uint64_t* __restrict__ shift) {
-  constexpr uint64_t kBB = 64;  // block bytes per chain
-  if (b - a < 4 * kBB) return crc_range<4>(payload, a, b, lds, lc);
+  constexpr uint64_t kBB = 64;
+  if (b - a < 4 * kBB) return crc_range<Tab, 4>(tb, payload, a, b, lds);
   RState x{0u, 0u}, y{0u, 0u};
   uint64_t p = a;
   const uint64_t mis = reinterpret_cast<uintptr_t>(payload) & 15u;
   while (p < b && ((p + mis) & 15u)) {
-    step1(x, payload[p], lds, lc);
+    tb.step1(x, payload[p], lds);
     ++p;
   }
   const uint64_t nb = (b - p) / (2 * kBB);  // blocks per chain (>= 1 here)
@@ -193,33 +226,21 @@ __device__ __forceinline__ uint64_t crc_range2(const uint8_t* __restrict__ paylo
   const uint4* qy = reinterpret_cast<const uint4*>(payload + m);
   const uint64_t last = nb - 1;
   uint4 XA[4], XB[4], YA[4], YB[4];
-#define JRQ_LOAD2(X, Y, blk)                                            \
-  do {                                                                  \
-    const uint64_t bb = (blk) < last ? (blk) : last;                    \
+#define JRQ_LOAD2(X, Y, blk)                                             \
+  do {                                                                   \
+    const uint64_t bb = (blk) < last ? (blk) : last;                     \
     _Pragma("unroll") for (int v = 0; v < 4; ++v) X[v] = qx[4 * bb + v]; \
     _Pragma("unroll") for (int v = 0; v < 4; ++v) Y[v] = qy[4 * bb + v]; \
-    asm volatile("" ::: "memory");                                      \
+    asm volatile("" ::: "memory");                                       \
   } while (0)
-#define JRQ_HASH2(X, Y)                          \
-  do {                                           \
+#define JRQ_HASH2(X, Y)                           \
+  do {                                            \
     _Pragma("unroll") for (int v = 0; v < 4; ++v) { \
-      x.lo ^= X[v].x;                            \
-      x.hi ^= X[v].y;                            \
-      y.lo ^= Y[v].x;                            \
-      y.hi ^= Y[v].y;                            \
-      _Pragma("unroll") for (int s = 0; s < 4; ++s) { \
-        step2(x, lds, lc);                       \
-        step2(y, lds, lc);                       \
-      }                                          \
-      x.lo ^= X[v].z;                            \
-      x.hi ^= X[v].w;                            \
-      y.lo ^= Y[v].z;                            \
-      y.hi ^= Y[v].w;                            \
-      _Pragma("unroll") for (int s = 0; s < 4; ++s) { \
-        step2(x, lds, lc);                       \
-        step2(y, lds, lc);                       \
-      }                                          \
-    }                                            \
+      tb.step8(x, X[v].x, X[v].y, lds);           \
+      tb.step8(y, Y[v].x, Y[v].y, lds);           \
+      tb.step8(x, X[v].z, X[v].w, lds);           \
+      tb.step8(y, Y[v].z, Y[v].w, lds);           \
+    }                                             \
   } while (0)
   JRQ_LOAD2(XA, YA, 0);
   for (uint64_t i = 0;;) {
@@ -232,27 +253,37 @@ __device__ __forceinline__ uint64_t crc_range2(const uint8_t* __restrict__ paylo
   }
 #undef JRQ_LOAD2
 #undef JRQ_HASH2
-  // Y continues over the tail [m + nb*kBB, b)
-  uint64_t q = m + nb * kBB;
+  uint64_t q = m + nb * kBB;  // Y continues over the tail
   while (q + 16 <= b) {
-    step16(y, *reinterpret_cast<const uint4*>(payload + q), lds, lc);
+    step16(tb, y, *reinterpret_cast<const uint4*>(payload + q), lds);
     q += 16;
   }
-  while (q + 2 <= b) {
-    y.lo ^= payload[q] | (static_cast<uint32_t>(payload[q + 1]) << 8);
-    step2(y, lds, lc);
-    q += 2;
+  while (q < b) {
+    tb.step1(y, payload[q], lds);
+    ++q;
   }
-  if (q < b) step1(y, payload[q], lds, lc);
   return crc_shift(crc_value(x), b - m, shift) ^ crc_value(y);
 }
 
-template <bool kLogEntry>
-__device__ __forceinline__ uint64_t entry_fields(const JrqCrcArgs& a, uint32_t e, const char* lds,
-                                                 uint32_t lc) {
+// LogId.checksum(): crc64(BE64(index) || BE64(term))  (LogId.java:45-50, Bits.java:71-80).
+// The big-endian bytes, read as a little-endian u64, are bswap64(v).
+template <class Tab>
+__device__ __forceinline__ uint64_t logid_crc(const Tab& tb, int64_t index, int64_t term,
+                                              const char* lds) {
+  RState r{0u, 0u};
+  const uint64_t bi = bswap64(static_cast<uint64_t>(index));
+  const uint64_t bt = bswap64(static_cast<uint64_t>(term));
+  tb.step8(r, static_cast<uint32_t>(bi), static_cast<uint32_t>(bi >> 32), lds);
+  tb.step8(r, static_cast<uint32_t>(bt), static_cast<uint32_t>(bt >> 32), lds);
+  return crc_value(r);
+}
+
+template <bool kLogEntry, class Tab>
+__device__ __forceinline__ uint64_t entry_fields(const Tab& tb, const JrqCrcArgs& a, uint32_t e,
+                                                 const char* lds) {
   if (!kLogEntry) return 0;
   // LogEntry.checksum: type.getNumber() ^ id.checksum() ^ peers' checksums (LogEntry.java:89-94)
-  uint64_t f = static_cast<uint64_t>(a.type[e]) ^ logid_crc(a.index[e], a.term[e], lds, lc);
+  uint64_t f = static_cast<uint64_t>(a.type[e]) ^ logid_crc(tb, a.index[e], a.term[e], lds);
   if (a.peer_xor) f ^= a.peer_xor[e];
   return f;
 }
@@ -300,36 +331,51 @@ __device__ __forceinline__ uint32_t lower_bound_off(const uint64_t* __restrict__
   return lo;
 }
 
-// Hash one piece: kVariant 4 / 8 = one chain with 64-B / 128-B blocks, 2 = two chains.
+// Kernel variants (A/B knobs, include/jrq.h engine notes):
+//   kV2B4  Tab2, one chain, 64-B blocks      kV2B8  Tab2, one chain, 128-B blocks
+//   kV2C2  Tab2, two chains                  kV4B8  Tab4, one chain, 128-B blocks
+//   kV4C2  Tab4, two chains
+enum : int { kV2B4 = 0, kV2B8 = 1, kV2C2 = 2, kV4B8 = 3, kV4C2 = 4 };
+
 template <int kVariant>
-__device__ __forceinline__ uint64_t crc_piece(const JrqCrcArgs& a, uint64_t lo, uint64_t hi,
-                                              const char* lds, uint32_t lc) {
-  if (kVariant == 2) return crc_range2(a.payload, lo, hi, lds, lc, a.shift);
-  return crc_range<kVariant == 8 ? 8 : 4>(a.payload, lo, hi, lds, lc);
+struct VariantTab {
+  using type = Tab2;
+};
+template <>
+struct VariantTab<kV4B8> {
+  using type = Tab4;
+};
+template <>
+struct VariantTab<kV4C2> {
+  using type = Tab4;
+};
+
+template <int kVariant, class Tab>
+__device__ __forceinline__ uint64_t crc_piece(const Tab& tb, const JrqCrcArgs& a, uint64_t lo,
+                                              uint64_t hi, const char* lds) {
+  if (kVariant == kV2C2 || kVariant == kV4C2) return crc_range2(tb, a.payload, lo, hi, lds, a.shift);
+  if (kVariant == kV2B4) return crc_range<Tab, 4>(tb, a.payload, lo, hi, lds);
+  return crc_range<Tab, 8>(tb, a.payload, lo, hi, lds);
 }
 
 template <bool kLogEntry, int kVariant>
 __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a) {
+  using Tab = typename VariantTab<kVariant>::type;
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
   const char* lds = reinterpret_cast<const char*>(lds_tab);
 
-  // Replicate R0/R1 into the lane-private bank image: word w = table<<13 | idx<<5 | slot.
-  for (uint32_t w = threadIdx.x; w < kCrcLdsBytes / 8; w += blockDim.x) {
-    const uint32_t table = w >> 13, idx = (w >> 5) & 255u;
-    lds_tab[w] = a.slice[table * 256 + idx];
-  }
+  // Build the replicated LDS image of the slice tables (a.slice = R0, R1, R2, R3).
+  for (uint32_t w = threadIdx.x; w < kCrcLdsBytes / 8; w += blockDim.x)
+    lds_tab[w] = a.slice[Tab::src_index(w)];
   __syncthreads();
 
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t lc = ((lane & 31u) << 3) | (1u << 16);
+  const Tab tb(threadIdx.x & 63u);
 
   const uint64_t base = a.offsets[0];
   const uint64_t total = a.offsets[a.n] - base;
   const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  // Segment size S ~ total/lanes (>= 2^min_seg_log2).  All lanes walk their segments in
-  // lockstep, so lane l reads near l*S at any moment: S is an ODD multiple of 64 B so
-  // that those addresses spread over the memory channels (a power-of-two stride piles
-  // a whole wave onto a few of them).  seg_mode 0 keeps the power-of-two size (A/B).
+  // Segment size S ~ total/lanes (>= 2^min_seg_log2).  seg_mode 0: a power of two (the
+  // measured best); 1: an odd multiple of 64 B (A/B alternative); seg_bytes: fixed.
   uint64_t S;
   if (a.seg_bytes != 0) {
     S = a.seg_bytes;
@@ -361,7 +407,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a)
     if (e > 0 && oe > s0) {
       const uint32_t t = e - 1;
       const uint64_t pe = oe < s1 ? oe : s1;
-      uint64_t c = crc_piece<kVariant>(a, s0, pe, lds, lc);
+      uint64_t c = crc_piece<kVariant>(tb, a, s0, pe, lds);
       c = crc_shift(c, oe - pe, a.shift);
       const uint64_t ot = a.offsets[t];
       const uint64_t first = (ot - base) / S, lastseg = (oe - 1 - base) / S;
@@ -373,8 +419,8 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a)
     while (e < a.n && (oe < s1 || (last_seg && oe == s1))) {
       const uint64_t oe1 = a.offsets[e + 1];
       const uint64_t pe = oe1 < s1 ? oe1 : s1;
-      const uint64_t fields = entry_fields<kLogEntry>(a, e, lds, lc);
-      uint64_t c = crc_piece<kVariant>(a, oe, pe, lds, lc);
+      const uint64_t fields = entry_fields<kLogEntry>(tb, a, e, lds);
+      uint64_t c = crc_piece<kVariant>(tb, a, oe, pe, lds);
       if (oe1 <= s1) {
         emit<kLogEntry>(a, e, c ^ fields);  // whole entry inside the segment
       } else {
@@ -392,22 +438,29 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a)
 
 }  // namespace jrq
 
-extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64(const JrqCrcArgs* args, int log_entry, int grid,
-                                       hipStream_t stream) {
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64(
+    const JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {
   const dim3 g(grid), blk(jrq::kCrcBlock);
-  // variant: two chains per lane, or one chain with 128-B / 64-B per-lane load blocks
-  const int v = args->chains >= 2 ? 2 : (args->block_bytes >= 128 ? 8 : 4);
+  using namespace jrq;
+  const bool t4 = args->tables >= 4;
+  const int v = args->chains >= 2 ? (t4 ? kV4C2 : kV2C2)
+                                  : (t4 ? kV4B8 : (args->block_bytes >= 128 ? kV2B8 : kV2B4));
 #define JRQ_LAUNCH(LE, V) \
-  hipLaunchKernelGGL((jrq::crc64_segments_kernel<LE, V>), g, blk, 0, stream, *args)
-  if (log_entry) {
-    if (v == 2) JRQ_LAUNCH(true, 2);
-    else if (v == 8) JRQ_LAUNCH(true, 8);
-    else JRQ_LAUNCH(true, 4);
-  } else {
-    if (v == 2) JRQ_LAUNCH(false, 2);
-    else if (v == 8) JRQ_LAUNCH(false, 8);
-    else JRQ_LAUNCH(false, 4);
+  hipLaunchKernelGGL((crc64_segments_kernel<LE, V>), g, blk, 0, stream, *args)
+#define JRQ_VARIANTS(LE)                 \
+  switch (v) {                           \
+    case kV2B4: JRQ_LAUNCH(LE, kV2B4); break; \
+    case kV2B8: JRQ_LAUNCH(LE, kV2B8); break; \
+    case kV2C2: JRQ_LAUNCH(LE, kV2C2); break; \
+    case kV4B8: JRQ_LAUNCH(LE, kV4B8); break; \
+    default: JRQ_LAUNCH(LE, kV4C2); break;    \
   }
+  if (log_entry) {
+    JRQ_VARIANTS(true)
+  } else {
+    JRQ_VARIANTS(false)
+  }
+#undef JRQ_VARIANTS
 #undef JRQ_LAUNCH
   return hipGetLastError();
 }

@@ -53,6 +53,7 @@ struct jrq_engine {
   uint64_t crc_seg_bytes = 0;
   uint32_t crc_block = 128;
   uint32_t crc_chains = 1;
+  uint32_t crc_tables = 2;
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
   DevBuf stage[24];  // 0-13 host-variant staging, 16-19 AppendEntries scratch
@@ -111,18 +112,17 @@ uint64_t mulmod(uint64_t a, uint64_t b) {
 //   slice  = { bswap(T0), bswap(T1) }  (reversed-domain slice-by-2)
 //   shift[t][k][i] = (i * x^(8k)) * x^(8 * 2^t) mod G
 void build_tables(std::vector<uint64_t>& slice, std::vector<uint64_t>& shift) {
-  uint64_t t0[256], t1[256];
+  uint64_t t[4][256];
   for (int i = 0; i < 256; ++i) {
     uint64_t c = static_cast<uint64_t>(i) << 56;
     for (int k = 0; k < 8; ++k) c = (c & 0x8000000000000000ULL) ? (c << 1) ^ jrq::kCrcPoly : (c << 1);
-    t0[i] = c;
+    t[0][i] = c;
   }
-  for (int i = 0; i < 256; ++i) t1[i] = t0[t0[i] >> 56] ^ (t0[i] << 8);
-  slice.resize(512);
-  for (int i = 0; i < 256; ++i) {
-    slice[i] = __builtin_bswap64(t0[i]);
-    slice[256 + i] = __builtin_bswap64(t1[i]);
-  }
+  for (int j = 1; j < 4; ++j)  // T_j = T_{j-1} advanced by one zero byte
+    for (int i = 0; i < 256; ++i) t[j][i] = t[0][t[j - 1][i] >> 56] ^ (t[j - 1][i] << 8);
+  slice.resize(4 * 256);
+  for (int j = 0; j < 4; ++j)
+    for (int i = 0; i < 256; ++i) slice[j * 256 + i] = __builtin_bswap64(t[j][i]);
   shift.resize(static_cast<size_t>(jrq::kShiftTables) * 8 * 256);
   uint64_t K = 0x100;  // x^8
   for (int t = 0; t < jrq::kShiftTables; ++t) {
@@ -177,6 +177,7 @@ int crc_dispatch(jrq_engine* e, JrqCrcArgs& a, int log_entry) {
   a.seg_bytes = e->crc_seg_bytes;
   a.block_bytes = e->crc_block;
   a.chains = e->crc_chains;
+  a.tables = e->crc_tables;
   JRQ_HIP(e, jrq_launch_crc64(&a, log_entry, e->crc_grid, e->stream));
   return JRQ_OK;
 }
@@ -225,6 +226,7 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   if (const char* v = std::getenv("JRQ_CRC_SEG_MODE")) e->crc_seg_mode = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("JRQ_CRC_BLOCK")) e->crc_block = (uint32_t)std::atoi(v) >= 128 ? 128 : 64;
   if (const char* v = std::getenv("JRQ_CRC_CHAINS")) e->crc_chains = std::atoi(v) >= 2 ? 2 : 1;
+  if (const char* v = std::getenv("JRQ_CRC_TABLES")) e->crc_tables = std::atoi(v) >= 4 ? 4 : 2;
   if (const char* v = std::getenv("JRQ_CRC_SEG_BYTES")) {
     // fixed segment size; at least 64 B and large enough for the straddler scratch
     uint64_t b = std::strtoull(v, nullptr, 10);

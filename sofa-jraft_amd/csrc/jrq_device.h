@@ -12,7 +12,7 @@ namespace jrq {
 constexpr uint64_t kCrcPoly = 0x42F0E1EBA9EA3693ULL;
 
 // Device copies of the constant tables (written once by jrq_create):
-//   slice[2][256]  "reversed-domain" slice-by-2 tables, see crc64.hip
+//   slice[4][256]  "reversed-domain" slice tables R0..R3, see crc64.hip
 //   shift[kShiftTables][8][256]  multiply-by-x^(8*2^t) mod P byte tables
 constexpr int kShiftTables = 48;  // shifts up to 2^48 - 1 bytes
 
@@ -47,7 +47,7 @@ struct JrqCrcArgs {
   const uint8_t* has;
   uint8_t* corrupt;
   // engine constants / scratch
-  const uint64_t* slice;   // [2][256]
+  const uint64_t* slice;   // [4][256] reversed-domain slice tables R0..R3
   const uint64_t* shift;   // [kShiftTables][8][256]
   uint64_t* acc;           // straddler accumulators, zero between launches
   uint32_t* cnt;           // straddler arrival counters, zero between launches
@@ -57,6 +57,7 @@ struct JrqCrcArgs {
   uint64_t seg_bytes;      // nonzero: fixed segment size (tuning / tests)
   uint32_t block_bytes;    // per-lane load block: 64 or 128
   uint32_t chains;         // independent CRC chains per lane: 1 or 2
+  uint32_t tables;         // LDS table flavour: 2 (slice-by-2) or 4 (slice-by-4)
 };
 
 // Leader lease / alive-quorum check (quorum.hip, lease kernel).

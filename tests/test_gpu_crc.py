@@ -84,12 +84,16 @@ def test_tiny_segments_stress_straddlers(oracle, seg, monkeypatch):
             np.testing.assert_array_equal(e.crc64_batch(payload, offs), exp)
 
 
-@pytest.mark.parametrize("block,chains", [("64", "1"), ("128", "1"), ("64", "2"), ("128", "2")])
-def test_every_kernel_variant(oracle, block, chains, monkeypatch):
-    """Each load-block / chain variant is bit-exact on ragged, unaligned and long entries."""
+@pytest.mark.parametrize("block,chains,tables", [("64", "1", "2"), ("128", "1", "2"),
+                                                 ("64", "2", "2"), ("128", "1", "4"),
+                                                 ("64", "2", "4")])
+def test_every_kernel_variant(oracle, block, chains, tables, monkeypatch):
+    """Each table-flavour / load-block / chain variant is bit-exact on ragged, unaligned and
+    long entries."""
     from jraft_amd import Engine
     monkeypatch.setenv("JRQ_CRC_BLOCK", block)
     monkeypatch.setenv("JRQ_CRC_CHAINS", chains)
+    monkeypatch.setenv("JRQ_CRC_TABLES", tables)
     lens = [0, 1, 15, 16, 17, 255, 256, 257, 1023, 4099, 16384, 100000, 3 << 20, 7]
     offs = np.concatenate([[5], 5 + np.cumsum(lens)]).astype(np.uint64)
     payload = W.random_bytes(11, int(offs[-1]) + 2)

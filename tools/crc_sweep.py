@@ -23,18 +23,20 @@ def main():
     dev = torch.device("cuda:0")
     s = torch.cuda.Stream(dev)
     torch.cuda.set_stream(s)
-    # variant = seg_mode:seg_bytes:block_bytes:chains (seg_bytes 0 = automatic)
-    variants = [(v.split(":") + ["0", "0", "128", "1"][len(v.split(":")):])
-                for v in (sys.argv[1:] or ["0:0:128:1", "0:0:64:1", "0:0:64:2"])]
+    # variant = seg_mode:seg_bytes:block_bytes:chains:tables (seg_bytes 0 = automatic)
+    dflt = ["0", "0", "128", "1", "2"]
+    variants = [(v.split(":") + dflt[len(v.split(":")):])
+                for v in (sys.argv[1:] or ["0:0:128:1:2", "0:0:128:1:4", "0:0:64:2:4"])]
     engines = []
-    for mode, nbytes, blk, ch in variants:
+    for mode, nbytes, blk, ch, tabs in variants:
         os.environ["JRQ_CRC_SEG_MODE"] = mode
         os.environ["JRQ_CRC_SEG_BYTES"] = nbytes
         os.environ["JRQ_CRC_BLOCK"] = blk
         os.environ["JRQ_CRC_CHAINS"] = ch
+        os.environ["JRQ_CRC_TABLES"] = tabs
         e = Engine(0)
         e.use_stream(s.cuda_stream)
-        engines.append((f"mode{mode}/S{nbytes}/B{blk}/C{ch}", e))
+        engines.append((f"mode{mode}/S{nbytes}/B{blk}/C{ch}/T{tabs}", e))
     res = {}
     for cfg, n, eb in (("C5", 64 << 10, 16 << 10), ("C1", 1 << 20, 256)):
         b = W.entry_batch(n, eb, seed=3)
