@@ -327,15 +327,21 @@ def main():
     # leader lease / alive quorum on C3-shaped groups
     rng = np.random.default_rng(rank)
     now_ms, lease_to = 1 << 40, 900
-    ts_np = (now_ms - rng.integers(0, 2 * lease_to, (P, G))).astype(np.int64)
-    ts = to_dev(ts_np, dev)
+    # rotating timestamp buffers, as for the epochs: no launch re-reads the previous
+    # launch's inputs out of the MALL / L2
+    ts_bufs = [to_dev((now_ms - rng.integers(0, 2 * lease_to, (P, G))).astype(np.int64), dev)
+               for _ in range(QUORUM_EPOCH_BUFFERS)]
     self_slot = torch.zeros(G, dtype=torch.uint8, device=dev)
     lead = torch.zeros(G, dtype=torch.int64, device=dev)
     lok = torch.empty(G, dtype=torch.uint8, device=dev)
     ldead = torch.empty(G, dtype=torch.int16, device=dev)
     lconf = epochs[0]["conf"]
 
+    lstate = {"i": 0}
+
     def lease_step(i=None):
+        ts = ts_bufs[lstate["i"] % QUORUM_EPOCH_BUFFERS]
+        lstate["i"] += 1
         eng.lease_check_dev(ts, lconf, self_slot, now_ms, lease_to, lok, lead, ldead)
 
     _, lease_ms = timed_launches(lease_step, args.steps, args.warmup, stream, sync)

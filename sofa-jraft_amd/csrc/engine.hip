@@ -47,13 +47,13 @@ struct jrq_engine {
   uint32_t* cnt = nullptr;    // straddler counters
   uint32_t scratch_len = 0;
   int crc_grid = 0;
-  // tuning knobs (JRQ_CRC_SEG_MODE / JRQ_CRC_SEG_BYTES / JRQ_CRC_BLOCK); defaults are the
-  // measured best (profiles/README.md): power-of-two segments, 128-B per-lane blocks
+  // tuning knobs (JRQ_CRC_SEG_MODE / _SEG_BYTES / _BLOCK / _CHAINS / _TABLES); defaults are the
+  // measured best (profiles/README.md): power-of-two segments, 128-B blocks, slice-by-4
   uint32_t crc_seg_mode = 0;
   uint64_t crc_seg_bytes = 0;
   uint32_t crc_block = 128;
   uint32_t crc_chains = 1;
-  uint32_t crc_tables = 2;
+  uint32_t crc_tables = 4;
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
   DevBuf stage[24];  // 0-13 host-variant staging, 16-19 AppendEntries scratch
