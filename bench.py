@@ -57,10 +57,11 @@ def to_dev(arr, dev):
     return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/<tag>_pmc.json, written by tools/summarize_profiles.py from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench); None if absent."""
+def pmc_traffic(*kernels: str):
+    """HBM bytes per launch of the timed op, summed over `kernels` (name substrings), from
+    the newest committed PMC summary holding all of them (profiles/<tag>_pmc.json, written
+    by tools/summarize_profiles.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    passes of this bench); None if absent."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     for f in reversed(files):
@@ -69,10 +70,16 @@ def pmc_traffic(kernel: str):
                 ks = json.load(fh).get("kernels", {})
         except (OSError, ValueError):
             continue
-        for name, d in ks.items():
-            if kernel in name and "hbm_bytes_per_launch_corrected" in d:
-                return {"bytes": d["hbm_bytes_per_launch_corrected"],
-                        "source": os.path.relpath(f, ROOT) + " (2*FETCH_SIZE+WRITE_SIZE, KiB->B)"}
+        total = 0.0
+        for kern in kernels:
+            hit = [d["hbm_bytes_per_launch_corrected"] for name, d in ks.items()
+                   if kern in name and "hbm_bytes_per_launch_corrected" in d]
+            if not hit:
+                break
+            total += hit[0]
+        else:
+            return {"bytes": total,
+                    "source": os.path.relpath(f, ROOT) + " (2*FETCH_SIZE+WRITE_SIZE, KiB->B)"}
     return None
 
 
@@ -402,7 +409,7 @@ def main():
             line["roofline"]["traffic"] = tr["bytes"]
             line["roofline"]["traffic_source"] = tr["source"]
         if crc is not None:
-            tr = pmc_traffic("crc64_segments_kernel<true")
+            tr = pmc_traffic("crc64_rounds_kernel", "crc64_finish_kernel<true")
             if tr is not None:
                 crc["roofline"]["traffic"] = tr["bytes"]
                 crc["roofline"]["traffic_source"] = tr["source"]

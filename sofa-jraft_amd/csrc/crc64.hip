@@ -6,32 +6,38 @@
 //   LogEntry.checksum()     jraft-core/.../entity/LogEntry.java:88-108
 //   LogEntry.isCorrupted()  jraft-core/.../entity/LogEntry.java:156-158
 //
-// Design (DESIGN.md §4.2 has the roofline):
-//  * The payload is cut into equal flat SEGMENTS of S bytes (S from the batch size so
-//    that every lane of the persistent grid gets ~1 segment); each lane walks its
-//    segment entry by entry with a serial table CRC.  Work per lane is the same
-//    whatever the entry-length distribution.
-//  * The CRC is linear over GF(2) with init 0, so a piece of an entry that ends n bytes
-//    before the entry's end contributes crc(piece) * x^(8n) mod P, and the entry's CRC is
-//    the XOR of its pieces.  Pieces of entries that straddle a segment boundary are
-//    XOR-combined in a scratch slot with agent-scope atomics; the last arriving piece
-//    (arrival counter) writes the result and re-zeroes the slot.
-//  * Table CRC in the "reversed domain" r = bswap64(crc): a little-endian 8-byte load
-//    XORs straight into r (no byte swaps), and one k-byte step is
-//      r = (r >> 8k) ^ R_{k-1}[byte 0 of r] ^ ... ^ R_0[byte k-1 of r],
-//    R_j = bswap(T_j), T_j[i] = i * x^(64 + 8j) mod P.  Two LDS table flavours:
-//      Tab2: slice-by-2, R0/R1 replicated 32x so lane l only touches bank pair l&31
-//            (conflict-free): per 2 bytes 2 v_perm + 2 ds_read_b64 + 2 shifts + 2 XOR3.
-//      Tab4: slice-by-4, R0..R3 replicated 16x, two tables interleaved per 16-B slot:
-//            per 4 bytes 4 v_perm + 4 ds_read_b64 (2-way bank conflicts) + 4 XOR3/XOR,
-//            the 32-bit shift is free (register rename); half the dependent LDS round
-//            trips per byte of Tab2.
-//    Either way an LDS address is one v_perm of a data byte and a lane constant.
+// Design (DESIGN.md §4.2 has the roofline and the probe numbers behind each choice):
+//  * Flat segments.  The payload window is cut into equal SEGMENTS of S bytes (a multiple of
+//    256, S ~ total / lanes of the persistent grid); each lane owns one segment and walks the
+//    entries inside it in order, so the work per lane does not depend on the entry lengths.
+//    CRC64 here is linear over GF(2) (init 0, xorout 0): a piece of an entry that ends n bytes
+//    before the entry's end contributes crc(piece) * x^(8n) mod P, and the entry's CRC is the
+//    XOR of its pieces.  Pieces of entries that span segments meet in a scratch slot through
+//    agent-scope atomics; the last arriving piece writes the result and re-zeroes the slot.
+//  * Coalesced quad loads + DPP transpose.  A lane reading only its own segment touches 64
+//    different cache lines per wave instruction and streams at ~4.8 TB/s at best; instead the 4
+//    lanes of a quad read 64 contiguous bytes of ONE owner per instruction (8 loads = 128 B per
+//    lane per round, every owner's 128 B in full), and a 2-stage butterfly over the quad
+//    (DPP quad_perm moves + selects) hands every lane its own 8 pieces.  Rounds are
+//    double-buffered in registers; buffer loads with a per-wave descriptor clamp reads past
+//    the data to zero.
+//  * Table CRC in the "reversed domain" r = bswap64(crc): a little-endian load XORs straight
+//    into r, and 4 bytes are one step  r = (r >> 32) ^ R3[b0] ^ R2[b1] ^ R1[b2] ^ R0[b3],
+//    R_j = bswap(T_j), T_j[i] = i * x^(64 + 8j) mod P.  The tables live in LDS, replicated 16x
+//    with two tables sharing each 16-B slot; lanes 16-31 (and 48-63) visit each pair of tables
+//    in the opposite order, so lanes l and l+16 always read opposite halves of a slot: every
+//    ds_read_b64 is bank-conflict free.  An LDS address is one v_perm of a data byte and a
+//    per-lane constant (plus one v_perm per 4 bytes for the swapped lanes' byte order).
+//  * Entry boundaries are events: a round that lies inside one entry is hashed from the
+//    registers; a round holding a boundary or the data edge is finished from global memory
+//    (L2-hot) byte/16-B wise, then the entry is emitted (or its piece handed off).
 //  * The x^(8n) multiplications use byte tables in global memory (one per power of two,
 //    L2-resident); they run at most once per piece that does not end its entry.
 #include "jrq_device.h"
 
 namespace jrq {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct RState {
   uint32_t lo, hi;
@@ -46,28 +52,45 @@ __device__ __forceinline__ uint2 lds_u2(const char* lds, uint32_t addr) {
   return *reinterpret_cast<const uint2*>(lds + addr);
 }
 
-// ------------------------------------------------------------ slice-by-2 ---
-// LDS image: byte address = table<<16 | index<<8 | (lane&31)<<3 (R0 at 0, R1 at 64 KiB).
-struct Tab2 {
-  static constexpr uint32_t kSelR1 = 0x0C060004u;  // {lc.b0, lo.b0, lc.b2, 0}
-  static constexpr uint32_t kSelR0 = 0x0C0C0104u;  // {lc.b0, lo.b1, 0, 0}
-  uint32_t lc;  // byte0 = (lane&31)<<3, byte2 = 1
-  __device__ explicit Tab2(uint32_t lane) : lc(((lane & 31u) << 3) | (1u << 16)) {}
+// ------------------------------------------------------------ slice-by-4 ---
+// LDS image: byte address = (k>>1)<<16 | index<<8 | (lane&15)<<4 | (k&1)<<3 for table R_k
+// (16 replicas; R0/R1 share the 16-B slots of the first 64 KiB, R2/R3 of the second).
+struct Tab4 {
+  // Lanes 16-31 / 48-63 ("swapped" lanes) byte-swap each 16-bit half of r.lo before the
+  // lookups (one v_perm), so instruction i reads their byte i^1 and table R_{3-(i^1)}: the
+  // byte selectors stay wave-uniform constants and only the table constants are per lane.
+  uint32_t lc[4];  // instruction i: LDS address constant of its table (per lane)
+  uint32_t swz;    // v_perm selector: identity, or bytes 0<->1, 2<->3 on swapped lanes
+  __device__ explicit Tab4(uint32_t lane) {
+    const uint32_t sw = (lane >> 4) & 1u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t k = 3u - (static_cast<uint32_t>(i) ^ sw);  // table of instruction i
+      lc[i] = ((lane & 15u) << 4) | ((k & 1u) << 3) | ((k >> 1) << 16);
+    }
+    swz = sw ? 0x02030001u : 0x03020100u;
+  }
 
-  // word w of the image holds R_{w>>13}[(w>>5)&255]
-  __device__ static uint32_t src_index(uint32_t w) { return (w >> 13) * 256 + ((w >> 5) & 255u); }
+  // word w = (k>>1)<<13 | index<<5 | replica<<1 | (k&1)
+  __device__ static uint32_t src_index(uint32_t w) {
+    return (((w >> 13) << 1) | (w & 1u)) * 256 + ((w >> 5) & 255u);
+  }
 
-  __device__ __forceinline__ void step2(RState& r, const char* lds) const {
-    const uint2 t1 = lds_u2(lds, __builtin_amdgcn_perm(lc, r.lo, kSelR1));
-    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc, r.lo, kSelR0));
-    const uint32_t nlo = __builtin_amdgcn_alignbit(r.hi, r.lo, 16);
-    const uint32_t nhi = r.hi >> 16;
-    r.lo = xor3(nlo, t1.x, t0.x);
-    r.hi = xor3(nhi, t1.y, t0.y);
+  // four bytes already XORed into r.lo: r = (r >> 32) ^ R3[b0] ^ R2[b1] ^ R1[b2] ^ R0[b3]
+  // (the LDS address of instruction i = {lc.b0, byte i of x, lc.b2, 0})
+  __device__ __forceinline__ void step4(RState& r, const char* lds) const {
+    const uint32_t x = __builtin_amdgcn_perm(r.lo, r.lo, swz);
+    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc[0], x, 0x0C060004u));
+    const uint2 t1 = lds_u2(lds, __builtin_amdgcn_perm(lc[1], x, 0x0C060104u));
+    const uint2 t2 = lds_u2(lds, __builtin_amdgcn_perm(lc[2], x, 0x0C060204u));
+    const uint2 t3 = lds_u2(lds, __builtin_amdgcn_perm(lc[3], x, 0x0C060304u));
+    r.lo = xor3(xor3(r.hi, t0.x, t1.x), t2.x, t3.x);
+    r.hi = xor3(t0.y, t1.y, t2.y) ^ t3.y;
   }
   // one byte: r = R0[(r ^ b) & 0xFF] ^ (r >> 8)   (CRC64.update(byte), CRC64.java:100-103)
   __device__ __forceinline__ void step1(RState& r, uint32_t b, const char* lds) const {
-    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc, r.lo ^ b, 0x0C0C0004u));
+    const uint32_t lc0 = lc[0] & 0xF0u;  // this lane's replica of R0
+    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc0, r.lo ^ b, 0x0C060004u));
     const uint32_t nlo = __builtin_amdgcn_alignbit(r.hi, r.lo, 8);
     r.lo = nlo ^ t0.x;
     r.hi = (r.hi >> 8) ^ t0.y;
@@ -77,116 +100,70 @@ struct Tab2 {
                                         const char* lds) const {
     r.lo ^= dlo;
     r.hi ^= dhi;
-    step2(r, lds);
-    step2(r, lds);
-    step2(r, lds);
-    step2(r, lds);
-  }
-};
-
-// ------------------------------------------------------------ slice-by-4 ---
-// LDS image: byte address = (k>>1)<<16 | index<<8 | (lane&15)<<4 | (k&1)<<3 for table R_k
-// (16 replicas; R0/R1 share the 16-B slots of the first 64 KiB, R2/R3 of the second).
-struct Tab4 {
-  uint32_t lc0, lc1, lc2, lc3;  // byte0 = (lane&15)<<4 | (k&1)<<3, byte2 = k>>1
-  __device__ explicit Tab4(uint32_t lane)
-      : lc0(((lane & 15u) << 4)),
-        lc1(((lane & 15u) << 4) | 8u),
-        lc2(((lane & 15u) << 4) | (1u << 16)),
-        lc3(((lane & 15u) << 4) | 8u | (1u << 16)) {}
-
-  // word w = (k>>1)<<13 | index<<5 | replica<<1 | (k&1)
-  __device__ static uint32_t src_index(uint32_t w) {
-    return (((w >> 13) << 1) | (w & 1u)) * 256 + ((w >> 5) & 255u);
-  }
-
-  // four bytes already XORed into r.lo: r = (r >> 32) ^ R3[b0] ^ R2[b1] ^ R1[b2] ^ R0[b3]
-  __device__ __forceinline__ void step4(RState& r, const char* lds) const {
-    const uint2 t3 = lds_u2(lds, __builtin_amdgcn_perm(lc3, r.lo, 0x0C060004u));
-    const uint2 t2 = lds_u2(lds, __builtin_amdgcn_perm(lc2, r.lo, 0x0C060104u));
-    const uint2 t1 = lds_u2(lds, __builtin_amdgcn_perm(lc1, r.lo, 0x0C060204u));
-    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc0, r.lo, 0x0C060304u));
-    r.lo = xor3(xor3(r.hi, t3.x, t2.x), t1.x, t0.x);
-    r.hi = xor3(t3.y, t2.y, t1.y) ^ t0.y;
-  }
-  __device__ __forceinline__ void step1(RState& r, uint32_t b, const char* lds) const {
-    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc0, r.lo ^ b, 0x0C060004u));
-    const uint32_t nlo = __builtin_amdgcn_alignbit(r.hi, r.lo, 8);
-    r.lo = nlo ^ t0.x;
-    r.hi = (r.hi >> 8) ^ t0.y;
-  }
-  __device__ __forceinline__ void step8(RState& r, uint32_t dlo, uint32_t dhi,
-                                        const char* lds) const {
-    r.lo ^= dlo;
-    r.hi ^= dhi;
     step4(r, lds);
     step4(r, lds);
   }
+  __device__ __forceinline__ void step16(RState& r, const u32x4& v, const char* lds) const {
+    step8(r, v[0], v[1], lds);
+    step8(r, v[2], v[3], lds);
+  }
 };
 
-template <class Tab>
-__device__ __forceinline__ void step16(const Tab& tb, RState& r, const uint4& v, const char* lds) {
-  tb.step8(r, v.x, v.y, lds);
-  tb.step8(r, v.z, v.w, lds);
+// ------------------------------------------------------- quad transpose ---
+__device__ __forceinline__ uint32_t dpp_quad_xor1(uint32_t v) {
+  return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t dpp_quad_xor2(uint32_t v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
 }
 
-// CRC of payload[a, b) from a zero register, one chain.
-// Blocks of 16*BV bytes go through a 2-deep register ring: block i+1's loads are issued
-// before block i is hashed, unconditionally (address clamped to the last block), so the
-// compiler's wait before block i is a counted vmcnt(BV), not vmcnt(0).  Unrolled by two
-// with fixed buffer roles: a loaded register is never copied (a copy would force the wait
-// early).  The empty asm after each load group is a compiler memory barrier: the loads
-// may not be re-issued (rematerialised) at their use a block later; it implies no
-// hardware wait.  BV = 8 reads whole 128-B lines per lane.
-template <class Tab, int BV>
-__device__ __forceinline__ uint64_t crc_range(const Tab& tb, const uint8_t* __restrict__ payload,
-                                              uint64_t a, uint64_t b, const char* lds) {
-  RState r{0u, 0u};
-  uint64_t p = a;
-  const uint64_t mis = reinterpret_cast<uintptr_t>(payload) & 15u;
-  while (p < b && ((p + mis) & 15u)) {  // unaligned head (by address), byte-serial
-    tb.step1(r, payload[p], lds);
+// One butterfly stage on quad-lane bit B for a register pair (lo: register bit B = 0, hi: 1).
+// An element stays where its lane bit equals its register bit, else it trades places with
+// the partner lane's other register.
+template <int B>
+__device__ __forceinline__ void quad_stage(u32x4& lo, u32x4& hi, bool bit) {
+  u32x4 nlo, nhi;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint32_t plo = B == 0 ? dpp_quad_xor1(lo[c]) : dpp_quad_xor2(lo[c]);
+    const uint32_t phi = B == 0 ? dpp_quad_xor1(hi[c]) : dpp_quad_xor2(hi[c]);
+    nhi[c] = bit ? hi[c] : plo;
+    nlo[c] = bit ? phi : lo[c];
+  }
+  lo = nlo;
+  hi = nhi;
+}
+
+// reg o = piece m of owner o (quad lane m)  ->  reg j = piece j of this lane's own segment.
+// Must run with all four lanes of the quad active (DPP reads the partner lanes).
+__device__ __forceinline__ void quad_transpose(u32x4& a0, u32x4& a1, u32x4& a2, u32x4& a3,
+                                               uint32_t m) {
+  quad_stage<0>(a0, a1, m & 1u);
+  quad_stage<0>(a2, a3, m & 1u);
+  quad_stage<1>(a0, a2, (m >> 1) & 1u);
+  quad_stage<1>(a1, a3, (m >> 1) & 1u);
+}
+
+// --------------------------------------------------------------- helpers ---
+
+// Continue r over virtual bytes [p, q) read from global memory (A = address of virtual byte
+// 0, 16-B aligned).  Slow path: rounds that hold an entry boundary or the data edge.
+__device__ __forceinline__ void hash_global(const Tab4& tb, RState& r, const uint8_t* __restrict__ A,
+                                            uint64_t p, uint64_t q, const char* lds) {
+  while (p < q && (p & 15u)) {
+    tb.step1(r, A[p], lds);
     ++p;
   }
-  constexpr uint32_t kBlkBytes = 16u * BV;
-  const uint64_t nblk = (b - p) / kBlkBytes;
-  if (nblk != 0) {
-    const uint4* q = reinterpret_cast<const uint4*>(payload + p);
-    const uint64_t last = nblk - 1;
-    uint4 A[BV], B[BV];
-#define JRQ_LOAD(X, blk)                                             \
-  do {                                                               \
-    const uint64_t bb = (blk) < last ? (blk) : last;                 \
-    const uint4* qq = q + BV * bb;                                   \
-    _Pragma("unroll") for (int v = 0; v < BV; ++v) X[v] = qq[v];     \
-    asm volatile("" ::: "memory");                                   \
-  } while (0)
-#define JRQ_HASH(X)                                                             \
-  do {                                                                          \
-    _Pragma("unroll") for (int v = 0; v < BV; ++v) step16(tb, r, X[v], lds);    \
-  } while (0)
-    JRQ_LOAD(A, 0);
-    for (uint64_t i = 0;;) {
-      JRQ_LOAD(B, i + 1);
-      JRQ_HASH(A);
-      if (++i == nblk) break;
-      JRQ_LOAD(A, i + 1);
-      JRQ_HASH(B);
-      if (++i == nblk) break;
-    }
-#undef JRQ_LOAD
-#undef JRQ_HASH
-    p += nblk * kBlkBytes;
-  }
-  while (p + 16 <= b) {
-    step16(tb, r, *reinterpret_cast<const uint4*>(payload + p), lds);
+  while (p + 16 <= q) {
+    const uint4 v = *reinterpret_cast<const uint4*>(A + p);
+    tb.step8(r, v.x, v.y, lds);
+    tb.step8(r, v.z, v.w, lds);
     p += 16;
   }
-  while (p < b) {  // tail, byte-serial
-    tb.step1(r, payload[p], lds);
+  while (p < q) {
+    tb.step1(r, A[p], lds);
     ++p;
   }
-  return crc_value(r);
 }
 
 // c * x^(8n) mod P via the global power tables: one 8-lookup pass per set bit of n.
@@ -203,99 +180,9 @@ __device__ __forceinline__ uint64_t crc_shift(uint64_t c, uint64_t n,
   return c;
 }
 
-// Two independent chains per lane: [a, b) is cut at m into halves hashed in lockstep
-// (one chain's LDS latency hides under the other's), then crc = crc(X) * x^(8|Y|) ^ crc(Y).
-// 64-B blocks with a 2-deep register ring per chain; X takes the unaligned head first, Y
-// the tail last.  Short ranges fall back to one chain.
-template <class Tab>
-__device__ __forceinline__ uint64_t crc_range2(const Tab& tb, const uint8_t* __restrict__ payload,
-                                               uint64_t a, uint64_t b, const char* lds,
-                                               const uint64_t* __restrict__ shift) {
-  constexpr uint64_t kBB = 64;
-  if (b - a < 4 * kBB) return crc_range<Tab, 4>(tb, payload, a, b, lds);
-  RState x{0u, 0u}, y{0u, 0u};
-  uint64_t p = a;
-  const uint64_t mis = reinterpret_cast<uintptr_t>(payload) & 15u;
-  while (p < b && ((p + mis) & 15u)) {
-    tb.step1(x, payload[p], lds);
-    ++p;
-  }
-  const uint64_t nb = (b - p) / (2 * kBB);  // blocks per chain (>= 1 here)
-  const uint64_t m = p + nb * kBB;
-  const uint4* qx = reinterpret_cast<const uint4*>(payload + p);
-  const uint4* qy = reinterpret_cast<const uint4*>(payload + m);
-  const uint64_t last = nb - 1;
-  uint4 XA[4], XB[4], YA[4], YB[4];
-#define JRQ_LOAD2(X, Y, blk)                                             \
-  do {                                                                   \
-    const uint64_t bb = (blk) < last ? (blk) : last;                     \
-    _Pragma("unroll") for (int v = 0; v < 4; ++v) X[v] = qx[4 * bb + v]; \
-    _Pragma("unroll") for (int v = 0; v < 4; ++v) Y[v] = qy[4 * bb + v]; \
-    asm volatile("" ::: "memory");                                       \
-  } while (0)
-#define JRQ_HASH2(X, Y)                           \
-  do {                                            \
-    _Pragma("unroll") for (int v = 0; v < 4; ++v) { \
-      tb.step8(x, X[v].x, X[v].y, lds);           \
-      tb.step8(y, Y[v].x, Y[v].y, lds);           \
-      tb.step8(x, X[v].z, X[v].w, lds);           \
-      tb.step8(y, Y[v].z, Y[v].w, lds);           \
-    }                                             \
-  } while (0)
-  JRQ_LOAD2(XA, YA, 0);
-  for (uint64_t i = 0;;) {
-    JRQ_LOAD2(XB, YB, i + 1);
-    JRQ_HASH2(XA, YA);
-    if (++i == nb) break;
-    JRQ_LOAD2(XA, YA, i + 1);
-    JRQ_HASH2(XB, YB);
-    if (++i == nb) break;
-  }
-#undef JRQ_LOAD2
-#undef JRQ_HASH2
-  uint64_t q = m + nb * kBB;  // Y continues over the tail
-  while (q + 16 <= b) {
-    step16(tb, y, *reinterpret_cast<const uint4*>(payload + q), lds);
-    q += 16;
-  }
-  while (q < b) {
-    tb.step1(y, payload[q], lds);
-    ++q;
-  }
-  return crc_shift(crc_value(x), b - m, shift) ^ crc_value(y);
-}
-
-// LogId.checksum(): crc64(BE64(index) || BE64(term))  (LogId.java:45-50, Bits.java:71-80).
-// The big-endian bytes, read as a little-endian u64, are bswap64(v).
-template <class Tab>
-__device__ __forceinline__ uint64_t logid_crc(const Tab& tb, int64_t index, int64_t term,
-                                              const char* lds) {
-  RState r{0u, 0u};
-  const uint64_t bi = bswap64(static_cast<uint64_t>(index));
-  const uint64_t bt = bswap64(static_cast<uint64_t>(term));
-  tb.step8(r, static_cast<uint32_t>(bi), static_cast<uint32_t>(bi >> 32), lds);
-  tb.step8(r, static_cast<uint32_t>(bt), static_cast<uint32_t>(bt >> 32), lds);
-  return crc_value(r);
-}
-
-template <bool kLogEntry, class Tab>
-__device__ __forceinline__ uint64_t entry_fields(const Tab& tb, const JrqCrcArgs& a, uint32_t e,
-                                                 const char* lds) {
-  if (!kLogEntry) return 0;
-  // LogEntry.checksum: type.getNumber() ^ id.checksum() ^ peers' checksums (LogEntry.java:89-94)
-  uint64_t f = static_cast<uint64_t>(a.type[e]) ^ logid_crc(tb, a.index[e], a.term[e], lds);
-  if (a.peer_xor) f ^= a.peer_xor[e];
-  return f;
-}
-
-template <bool kLogEntry>
-__device__ __forceinline__ void emit(const JrqCrcArgs& a, uint32_t e, uint64_t v) {
-  a.out[e] = v;
-  if (kLogEntry && a.expected != nullptr && a.corrupt != nullptr) {
-    const bool has = (a.has == nullptr) || a.has[e];
-    a.corrupt[e] = static_cast<uint8_t>(has && a.expected[e] != v);
-  }
-}
+// Data CRC of entry e is final: plain batches are done; LogEntry batches get their fields
+// from logentry_fields_kernel afterwards (in place).
+__device__ __forceinline__ void emit(const JrqCrcArgs& a, uint32_t e, uint64_t v) { a.out[e] = v; }
 
 // One piece of an entry that spans `parts` segments: XOR its (already shifted) CRC into
 // the entry's scratch slot; the last of the `parts` arrivals publishes and re-zeroes it.
@@ -303,7 +190,6 @@ __device__ __forceinline__ void emit(const JrqCrcArgs& a, uint32_t e, uint64_t v
 // "valid forms"): the XOR is drained (s_waitcnt vmcnt(0)) before the arrival add, the last
 // arriver reads the slot with an atomic after its add returned.  No release/acquire
 // fences: those would write back the XCD's L2 / invalidate L1 on every piece.
-template <bool kLogEntry>
 __device__ __forceinline__ void straddle_piece(const JrqCrcArgs& a, uint32_t e, uint32_t slot,
                                                uint32_t parts, uint64_t c) {
   __hip_atomic_fetch_xor(&a.acc[slot], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -314,15 +200,47 @@ __device__ __forceinline__ void straddle_piece(const JrqCrcArgs& a, uint32_t e, 
     // read-and-zero in one memory-side RMW (an xor-with-0 would be folded into a load)
     const uint64_t v =
         __hip_atomic_exchange(&a.acc[slot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    emit<kLogEntry>(a, e, v);
+    emit(a, e, v);
     __hip_atomic_store(&a.cnt[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-// First e in [0, n] with offsets[e] >= x (offsets[n] >= x is guaranteed by the caller).
-__device__ __forceinline__ uint32_t lower_bound_off(const uint64_t* __restrict__ off, uint32_t n,
-                                                    uint64_t x) {
-  uint32_t lo = 0, hi = n;
+// Entries spanning at most this many segments hand their pieces over through per-segment
+// slots (plain stores) combined by crc64_finish_kernel; longer ones through the atomic slot.
+constexpr uint64_t kMaxSlotParts = 64;
+
+// Segment size (bytes; identical in the rounds and finish kernels): a multiple of 256 (two
+// 128-B rounds), ~span / lanes of the rounds grid, never more segments than straddler slots.
+__device__ __forceinline__ uint64_t seg_size(const JrqCrcArgs& a, uint64_t span) {
+  auto up256 = [](uint64_t x) { return (x + 255) & ~255ull; };
+  const uint64_t lanes = a.lanes;
+  uint64_t S = a.seg_bytes ? up256(a.seg_bytes) : up256((span + lanes - 1) / lanes);
+  if (S < 256) S = 256;
+  const uint64_t s_min = up256((span + a.scratch_len - 3) / (a.scratch_len - 2));
+  return S < s_min ? s_min : S;
+}
+
+// First e in [0, n] with off[e] >= x, given off[0] <= x <= off[n].  Probes off[g-1 .. g+1]
+// around the interpolated guess g (one round trip when entries are evenly sized), then
+// bisects the side that holds the answer.
+__device__ __forceinline__ uint32_t interp_lower_bound(const uint64_t* __restrict__ off, uint32_t n,
+                                                       uint64_t base, uint64_t total, uint64_t x) {
+  if (x <= base) return 0;
+  double f = static_cast<double>(x - base) / static_cast<double>(total) * static_cast<double>(n);
+  uint32_t g = f >= static_cast<double>(n) ? n : static_cast<uint32_t>(f);
+  if (g == 0) g = 1;
+  const uint64_t a0 = off[g - 1], a1 = off[g];
+  const uint64_t a2 = g < n ? off[g + 1] : ~0ull;
+  if (a0 < x && x <= a1) return g;
+  if (a1 < x && x <= a2) return g + 1;
+  uint32_t lo, hi;
+  if (x <= a0) {
+    lo = 0;
+    hi = g - 1;
+  } else {
+    lo = g + 2;
+    hi = n;
+  }
   while (lo < hi) {
     const uint32_t mid = lo + ((hi - lo) >> 1);
     if (off[mid] < x) lo = mid + 1;
@@ -331,136 +249,320 @@ __device__ __forceinline__ uint32_t lower_bound_off(const uint64_t* __restrict__
   return lo;
 }
 
-// Kernel variants (A/B knobs, include/jrq.h engine notes):
-//   kV2B4  Tab2, one chain, 64-B blocks      kV2B8  Tab2, one chain, 128-B blocks
-//   kV2C2  Tab2, two chains                  kV4B8  Tab4, one chain, 128-B blocks
-//   kV4C2  Tab4, two chains
-enum : int { kV2B4 = 0, kV2B8 = 1, kV2C2 = 2, kV4B8 = 3, kV4C2 = 4 };
-
-template <int kVariant>
-struct VariantTab {
-  using type = Tab2;
-};
-template <>
-struct VariantTab<kV4B8> {
-  using type = Tab4;
-};
-template <>
-struct VariantTab<kV4C2> {
-  using type = Tab4;
+// Per-lane walk of one segment.  Positions are VIRTUAL: byte v of the stream is payload
+// offset base - D + v (D = misalignment of payload + base), so segment k = [kS, (k+1)S) and
+// virtual 0 is 16-B aligned.  E(e) = virtual start of entry e.  The walk keeps positions
+// relative to the segment start in 32 bits (S < 2^31; boundaries past 2^32 clamp).
+struct SegWalk {
+  uint32_t pos;      // next byte to hash
+  uint32_t next;     // next event: min(cur_end, hi)
+  uint32_t hi;       // min(S, data end)
+  uint32_t cur;      // entry being hashed (or next to start)
+  uint32_t cur_end;  // E(cur + 1)
+  uint32_t nxt_end;  // E(cur + 2), loaded one entry ahead (the load lands by the next event)
+  uint32_t flags;
+  static constexpr uint32_t kStarted = 1, kLastSeg = 2, kDone = 4;
 };
 
-template <int kVariant, class Tab>
-__device__ __forceinline__ uint64_t crc_piece(const Tab& tb, const JrqCrcArgs& a, uint64_t lo,
-                                              uint64_t hi, const char* lds) {
-  if (kVariant == kV2C2 || kVariant == kV4C2) return crc_range2(tb, a.payload, lo, hi, lds, a.shift);
-  if (kVariant == kV2B4) return crc_range<Tab, 4>(tb, a.payload, lo, hi, lds);
-  return crc_range<Tab, 8>(tb, a.payload, lo, hi, lds);
-}
-
-template <bool kLogEntry, int kVariant>
-__global__ __launch_bounds__(kCrcBlock) void crc64_segments_kernel(JrqCrcArgs a) {
-  using Tab = typename VariantTab<kVariant>::type;
+__global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
   const char* lds = reinterpret_cast<const char*>(lds_tab);
+  if (a.timeline && (threadIdx.x & 63u) == 0)  // diagnostics: wave start (nothing kept live)
+    a.timeline[4 * (blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6))] =
+        __builtin_amdgcn_s_memrealtime();
 
   // Build the replicated LDS image of the slice tables (a.slice = R0, R1, R2, R3).
   for (uint32_t w = threadIdx.x; w < kCrcLdsBytes / 8; w += blockDim.x)
-    lds_tab[w] = a.slice[Tab::src_index(w)];
+    lds_tab[w] = a.slice[Tab4::src_index(w)];
   __syncthreads();
 
-  const Tab tb(threadIdx.x & 63u);
+  const Tab4 tb(threadIdx.x & 63u);
+  const uint32_t n = a.n;
+  const uint64_t* __restrict__ off = a.offsets;
+  const uint64_t base = off[0];
+  const uint64_t total = off[n] - base;
+  const uintptr_t addr0 = reinterpret_cast<uintptr_t>(a.payload + base);
+  const uint64_t D = addr0 & 15u;
+  // virtual byte 0 (up to 15 bytes before payload + base, inside the same 16-B granule)
+  const uint8_t* A = reinterpret_cast<const uint8_t*>(addr0 - D);
+  const uint64_t span = D + total;
+  const uint64_t grid = gridDim.x;
 
-  const uint64_t base = a.offsets[0];
-  const uint64_t total = a.offsets[a.n] - base;
-  const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  // Segment size S ~ total/lanes (>= 2^min_seg_log2).  seg_mode 0: a power of two (the
-  // measured best); 1: an odd multiple of 64 B (A/B alternative); seg_bytes: fixed.
-  uint64_t S;
-  if (a.seg_bytes != 0) {
-    S = a.seg_bytes;
-  } else if (a.seg_mode == 0) {
-    uint32_t s = a.min_seg_log2;
-    while (s < 40 && (total >> (s + 1)) >= lanes) ++s;
-    S = 1ull << s;
-  } else {
-    uint64_t t = (total + lanes - 1) / lanes;
-    const uint64_t floor_bytes = 1ull << a.min_seg_log2;
-    if (t < floor_bytes) t = floor_bytes;
-    S = (((t + 63) >> 6) | 1u) << 6;
-  }
-  // never more segments than straddler slots (scratch_len - 2)
-  const uint64_t s_min = (total + a.scratch_len - 3) / (a.scratch_len - 2);
-  if (S < s_min) S = s_min;
-  uint64_t nseg = (total + S - 1) / S;
-  if (nseg == 0) nseg = 1;
+  // Lane->segment map: every wave owns 64 CONTIGUOUS segments (its window, 64*S bytes: few
+  // DRAM pages and TLB entries per wave), and consecutive 64-segment chunks go round-robin
+  // over the workgroups, so small batches still spread over all CUs.
+  const uint64_t S = seg_size(a, span);
+  const uint64_t nseg = span == 0 ? 1 : (span + S - 1) / S;
+  const uint32_t rounds = static_cast<uint32_t>(S / 128);
 
-  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; k < nseg;
-       k += lanes) {
-    const uint64_t s0 = base + k * S;
-    const uint64_t s1 = (k + 1 == nseg) ? base + total : s0 + S;
-    const bool last_seg = (k + 1 == nseg);
-    uint32_t e = lower_bound_off(a.offsets, a.n, s0);
-    uint64_t oe = a.offsets[e];
+  // L0 (first lane of the wave) through readfirstlane: the compiler then knows the wave's
+  // window and descriptor are uniform (SGPRs; no waterfall loop around each buffer load)
+  const uint32_t L = threadIdx.x, m = L & 3u;
+  const uint32_t L0 = __builtin_amdgcn_readfirstlane(L & ~63u);
+  const uint32_t WS = static_cast<uint32_t>(S);  // lane-to-lane segment step (window < 2^31)
+  const uint32_t lane_off = (L - L0) * WS;       // this lane's segment, relative to the wave's
+  // load (q, h) of a round reads 16 B of quad owner q at round offset 64h + 16m, so the
+  // quad reads 64 contiguous bytes per instruction: offset = qbase + q*WS + 64h + round*128
+  const uint32_t qbase = lane_off - m * WS + 16u * m;
+  const uint64_t waves = blockDim.x / 64;
+  for (uint64_t j = 0;; ++j) {
+    const uint64_t kw = a.seg_map ? ((j * grid + blockIdx.x) * waves + (L0 >> 6)) * 64
+                                  : ((j * waves + (L0 >> 6)) * grid + blockIdx.x) * 64;
+    if (kw >= nseg) break;  // wave-uniform
+    const uint64_t wbase = kw * S;  // the wave's window starts at its first segment
+    const uint64_t k = kw + (L - L0);
+    const uint64_t s0 = wbase + lane_off;
+    auto E = [&](uint32_t e) -> uint64_t { return off[e] - base + D; };
+    auto rel = [&](uint64_t v) -> uint32_t {  // future boundary relative to s0, clamped
+      const uint64_t d = v - s0;
+      return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(d);
+    };
 
-    // piece of the entry that began in an earlier segment
-    if (e > 0 && oe > s0) {
-      const uint32_t t = e - 1;
-      const uint64_t pe = oe < s1 ? oe : s1;
-      uint64_t c = crc_piece<kVariant>(tb, a, s0, pe, lds);
-      c = crc_shift(c, oe - pe, a.shift);
-      const uint64_t ot = a.offsets[t];
-      const uint64_t first = (ot - base) / S, lastseg = (oe - 1 - base) / S;
-      straddle_piece<kLogEntry>(a, t, static_cast<uint32_t>(first),
-                                static_cast<uint32_t>(lastseg - first + 1), c);
-    }
-
-    // entries that begin inside this segment (zero-length ones at the very end go to the last)
-    while (e < a.n && (oe < s1 || (last_seg && oe == s1))) {
-      const uint64_t oe1 = a.offsets[e + 1];
-      const uint64_t pe = oe1 < s1 ? oe1 : s1;
-      const uint64_t fields = entry_fields<kLogEntry>(tb, a, e, lds);
-      uint64_t c = crc_piece<kVariant>(tb, a, oe, pe, lds);
-      if (oe1 <= s1) {
-        emit<kLogEntry>(a, e, c ^ fields);  // whole entry inside the segment
-      } else {
-        // head piece of a straddling entry: shift its data CRC to the entry end, add the fields
-        c = crc_shift(c, oe1 - pe, a.shift) ^ fields;
-        const uint64_t lastseg = (oe1 - 1 - base) / S;
-        straddle_piece<kLogEntry>(a, e, static_cast<uint32_t>(k),
-                                  static_cast<uint32_t>(lastseg - k + 1), c);
+    // ---- segment setup, before this wave's first loads (short memory queues) ----
+    SegWalk sw;
+    RState r{0u, 0u};
+    sw.flags = SegWalk::kStarted | (k + 1 == nseg ? SegWalk::kLastSeg : 0u) |
+               (k < nseg ? 0u : SegWalk::kDone);
+    sw.hi = static_cast<uint32_t>(span - s0 < S ? span - s0 : S);
+    sw.pos = static_cast<uint32_t>(s0 < D ? D - s0 : 0);
+    sw.cur = 0;
+    sw.next = 0;
+    sw.cur_end = 0;
+    sw.nxt_end = 0xFFFFFFFFu;
+    // entry cur starts at pos: skip (emit) zero-length entries there -- they belong to the
+    // segment holding pos, the last segment also owning those at the data end -- then arm
+    // the next event and prefetch the boundary after it
+    auto start_entry = [&]() {
+      while (sw.cur < n) {
+        sw.cur_end = rel(E(sw.cur + 1));
+        if (sw.cur_end != sw.pos || !(sw.pos < S || (sw.flags & SegWalk::kLastSeg))) break;
+        emit(a, sw.cur, 0);  // crc64 of no bytes
+        ++sw.cur;
       }
-      ++e;
-      oe = oe1;
+      if (sw.cur >= n || sw.pos >= sw.hi) {
+        sw.flags |= SegWalk::kDone;
+      } else {
+        sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
+        sw.nxt_end = sw.cur + 2 <= n ? rel(E(sw.cur + 2)) : 0xFFFFFFFFu;
+      }
+    };
+#if defined(JRQ_DIAG_NO_SETUP)  // tools/crc_timeline only: 16 KiB entries, no offset loads
+    if (!(sw.flags & SegWalk::kDone)) {
+      sw.cur = static_cast<uint32_t>(s0 >> 14);
+      if (s0 & 16383) sw.flags &= ~SegWalk::kStarted;
+      sw.cur_end = static_cast<uint32_t>(((s0 >> 14) + 1) * 16384 - s0);
+      sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
+      sw.nxt_end = sw.cur_end + 16384;
     }
+#else
+    if (!(sw.flags & SegWalk::kDone)) {
+      const uint32_t e = interp_lower_bound(off, n, base, total, s0 + sw.pos - D + base);
+      if (e > 0 && E(e) > s0 + sw.pos) {  // entry e-1 began in an earlier segment
+        sw.cur = e - 1;
+        sw.flags &= ~SegWalk::kStarted;
+        sw.cur_end = rel(E(e));
+        sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
+        sw.nxt_end = e + 1 <= n ? rel(E(e + 1)) : 0xFFFFFFFFu;
+      } else {
+        sw.cur = e;
+        start_entry();
+      }
+    }
+#endif
+
+    // An event at pos == next: the entry ends (emit / hand off its tail piece), or the
+    // segment ends inside the entry (hand off a shifted head/middle piece).
+    auto event = [&]() {
+      const bool started = sw.flags & SegWalk::kStarted;
+      if (sw.pos == sw.cur_end) {
+        const uint64_t v = crc_value(r);
+        if (started) {
+          emit(a, sw.cur, v);
+        } else {  // tail piece: this segment is the entry's last
+          const uint64_t first = E(sw.cur) / S;
+          if (k - first + 1 <= kMaxSlotParts)
+            a.piece_tail[k] = v;
+          else
+            straddle_piece(a, sw.cur, static_cast<uint32_t>(first),
+                           static_cast<uint32_t>(k - first + 1), v);
+        }
+        r = RState{0u, 0u};
+        sw.flags |= SegWalk::kStarted;
+        ++sw.cur;
+        if (sw.cur >= n) {
+          sw.flags |= SegWalk::kDone;
+        } else if (sw.nxt_end != sw.pos) {  // common case: the prefetched boundary
+          sw.cur_end = sw.nxt_end;
+          if (sw.pos >= sw.hi) {
+            sw.flags |= SegWalk::kDone;
+          } else {
+            sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
+            sw.nxt_end = sw.cur + 2 <= n ? rel(E(sw.cur + 2)) : 0xFFFFFFFFu;
+          }
+        } else {
+          start_entry();  // zero-length entries here
+        }
+      } else {  // pos == hi < entry end
+#if defined(JRQ_DIAG_NO_TAIL)  // tools/crc_timeline only: drop the head/middle piece
+        a.piece_cont[k] = crc_value(r);
+        sw.flags |= SegWalk::kDone;
+        return;
+#endif
+        const uint64_t ce = E(sw.cur + 1);
+        const uint64_t c = crc_shift(crc_value(r), ce - (s0 + sw.hi), a.shift);
+        const uint64_t first = started ? k : E(sw.cur) / S;
+        const uint64_t last = (ce - 1) / S;
+        if (last - first + 1 <= kMaxSlotParts)  // head / middle piece
+          a.piece_cont[k] = c;
+        else
+          straddle_piece(a, sw.cur, static_cast<uint32_t>(first),
+                         static_cast<uint32_t>(last - first + 1), c);
+        sw.flags |= SegWalk::kDone;
+      }
+    };
+
+    // buffer descriptor: from the wave's first segment to the data end (loads past it
+    // return zero)
+    const uint64_t nrec = span - wbase;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(A + wbase), static_cast<short>(0),
+        static_cast<int>(nrec > 0x7FFFFFFFull ? 0x7FFFFFFFull : nrec), 0x00020000);
+    // empty descriptor: the prefetch past the last round reads nothing (every offset is out
+    // of range), so the ring's loads stay unconditional and the vmcnt accounting static
+    const __amdgpu_buffer_rsrc_t rs_none = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(A + wbase), static_cast<short>(0), 0, 0x00020000);
+
+    // Ring of three half-rounds (64 B per lane each, 16 VGPRs): two in flight while one is
+    // hashed.  Half h of a round: load q reads 16 B of quad owner q at segment offset
+    // 64h' + 16m (h' = the half's index), so the quad reads 64 contiguous bytes of one
+    // owner per instruction.
+    u32x4 h0[4], h1[4], h2[4];
+#define JRQ_LOAD_HALF(H, RS, hh)                                                         \
+  do {                                                                                   \
+    const uint32_t ho = (hh) * 64u;                                                      \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q) H[q] =                                 \
+        __builtin_amdgcn_raw_buffer_load_b128(RS, qbase + (q * WS + ho), 0, 0);          \
+    asm volatile("" ::: "memory");                                                       \
+  } while (0)
+    const uint32_t halves = rounds * 2;
+    JRQ_LOAD_HALF(h0, rs, 0u);
+    JRQ_LOAD_HALF(h1, rs, 1u);
+
+    // one half-round of this lane: segment bytes [hs, hs + 64)
+    auto process = [&](uint32_t hh, const u32x4 (&v)[4]) {
+      if (sw.flags & SegWalk::kDone) return;
+      const uint32_t hs = hh * 64u, he = hs + 64u;
+      if (sw.pos == hs && he <= sw.next) {  // fast path: the half lies inside entry cur
+#pragma unroll
+        for (int p = 0; p < 4; ++p) tb.step16(r, v[p], lds);
+        sw.pos = he;
+      }
+      while (!(sw.flags & SegWalk::kDone)) {
+        if (sw.pos == sw.next) {
+          event();
+          continue;
+        }
+        if (sw.pos >= he) break;
+        const uint32_t lim = he < sw.next ? he : sw.next;
+        hash_global(tb, r, A, s0 + sw.pos, s0 + lim, lds);
+        sw.pos = lim;
+      }
+    };
+
+    // transposes run with the whole wave active (quad DPP), before any per-lane branch; the
+    // asm pin keeps the half's first use below the loads issued before it (otherwise the
+    // scheduler hoists the memory-free transposes and drains the prefetch with vmcnt(0))
+    auto transpose_half = [&](u32x4 (&v)[4]) {
+      asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+      quad_transpose(v[0], v[1], v[2], v[3], m);
+    };
+
+    for (uint32_t hh = 0; hh < halves; hh += 3) {
+      JRQ_LOAD_HALF(h2, (hh + 2 < halves ? rs : rs_none), hh + 2);
+      transpose_half(h0);
+      process(hh, h0);
+      if (hh + 1 >= halves) break;  // wave-uniform
+      JRQ_LOAD_HALF(h0, (hh + 3 < halves ? rs : rs_none), hh + 3);
+      transpose_half(h1);
+      process(hh + 1, h1);
+      if (hh + 2 >= halves) break;
+      JRQ_LOAD_HALF(h1, (hh + 4 < halves ? rs : rs_none), hh + 4);
+      transpose_half(h2);
+      process(hh + 2, h2);
+    }
+#undef JRQ_LOAD_HALF
+  }
+  if (a.timeline && (threadIdx.x & 63u) == 0) {  // diagnostics only
+    uint64_t* t = a.timeline + 4 * (blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6));
+    t[1] = __builtin_amdgcn_s_memrealtime();
+    t[2] = __builtin_amdgcn_s_getreg((23 << 11) | (0 << 6) | 4);   // HW_REG_HW_ID, 24 bits
+    t[3] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);   // HW_REG_XCC_ID, 4 bits
+  }
+}
+
+// Per entry, after the rounds kernel:
+//  * an entry that spans 2..kMaxSlotParts segments: data CRC = XOR of its pieces, the head /
+//    middle pieces in piece_cont[first .. last-1] (already shifted to the entry end), the tail
+//    in piece_tail[last]; every other entry's data CRC is already in out[e];
+//  * LogEntry batches: LogEntry.checksum() = type.getNumber() ^ LogId.checksum() ^ peers'
+//    checksums ^ crc64(data) (LogEntry.java:88-108), LogId.checksum() = crc64(BE64(index) ||
+//    BE64(term)) (LogId.java:45-50, Bits.java:71-80), then isCorrupted() (:156-158).
+// One lane per entry over coalesced streams; the 16 LogId bytes go through table R0 in LDS
+// byte by byte (CRC64.update(byte), CRC64.java:100-103).
+template <bool kLogEntry>
+__global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
+  __shared__ uint64_t r0[256];
+  if (kLogEntry) r0[threadIdx.x] = a.slice[threadIdx.x];  // R0 = bswap(T0) (blockDim == 256)
+  __syncthreads();
+  const uint64_t* __restrict__ off = a.offsets;
+  const uint64_t base = off[0];
+  const uint64_t D = reinterpret_cast<uintptr_t>(a.payload + base) & 15u;
+  const uint64_t span = D + (off[a.n] - base);
+  const uint64_t S = seg_size(a, span);
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < a.n; e += stride) {
+    const uint64_t o0 = off[e], o1 = off[e + 1];
+    uint64_t v;
+    const uint64_t first = (o0 - base + D) / S, last = o1 > o0 ? (o1 - 1 - base + D) / S : first;
+    if (last != first && last - first + 1 <= kMaxSlotParts) {
+      v = a.piece_tail[last];
+      for (uint64_t g = first; g < last; ++g) v ^= a.piece_cont[g];
+    } else {
+      if (!kLogEntry) continue;  // whole entry (or atomic hand-off): out[e] is final
+      v = a.out[e];
+    }
+    if (kLogEntry) {
+      uint64_t r = 0;
+      // the big-endian bytes of index then term, in stream order = little-endian bswap64(v)
+      const uint64_t bi = bswap64(static_cast<uint64_t>(a.index[e]));
+      const uint64_t bt = bswap64(static_cast<uint64_t>(a.term[e]));
+#pragma unroll
+      for (int q = 0; q < 8; ++q) r = r0[(r ^ (bi >> (8 * q))) & 0xFF] ^ (r >> 8);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) r = r0[(r ^ (bt >> (8 * q))) & 0xFF] ^ (r >> 8);
+      v ^= static_cast<uint64_t>(a.type[e]) ^ bswap64(r);
+      if (a.peer_xor) v ^= a.peer_xor[e];
+      if (a.expected != nullptr && a.corrupt != nullptr) {
+        const bool has = (a.has == nullptr) || a.has[e];
+        a.corrupt[e] = static_cast<uint8_t>(has && a.expected[e] != v);
+      }
+    }
+    a.out[e] = v;
   }
 }
 
 }  // namespace jrq
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64(
-    const JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {
-  const dim3 g(grid), blk(jrq::kCrcBlock);
-  using namespace jrq;
-  const bool t4 = args->tables >= 4;
-  const int v = args->chains >= 2 ? (t4 ? kV4C2 : kV2C2)
-                                  : (t4 ? kV4B8 : (args->block_bytes >= 128 ? kV2B8 : kV2B4));
-#define JRQ_LAUNCH(LE, V) \
-  hipLaunchKernelGGL((crc64_segments_kernel<LE, V>), g, blk, 0, stream, *args)
-#define JRQ_VARIANTS(LE)                 \
-  switch (v) {                           \
-    case kV2B4: JRQ_LAUNCH(LE, kV2B4); break; \
-    case kV2B8: JRQ_LAUNCH(LE, kV2B8); break; \
-    case kV2C2: JRQ_LAUNCH(LE, kV2C2); break; \
-    case kV4B8: JRQ_LAUNCH(LE, kV4B8); break; \
-    default: JRQ_LAUNCH(LE, kV4C2); break;    \
-  }
-  if (log_entry) {
-    JRQ_VARIANTS(true)
-  } else {
-    JRQ_VARIANTS(false)
-  }
-#undef JRQ_VARIANTS
-#undef JRQ_LAUNCH
+    JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {
+  args->lanes = static_cast<uint32_t>(grid) * jrq::kCrcBlock;
+  hipLaunchKernelGGL(jrq::crc64_rounds_kernel, dim3(grid), dim3(jrq::kCrcBlock), 0, stream, *args);
+  const uint32_t blocks = (args->n + 255) / 256;
+  const uint32_t cap = static_cast<uint32_t>(grid) * 8;
+  const dim3 fg(blocks < cap ? blocks : cap);
+  if (log_entry)
+    hipLaunchKernelGGL(jrq::crc64_finish_kernel<true>, fg, dim3(256), 0, stream, *args);
+  else
+    hipLaunchKernelGGL(jrq::crc64_finish_kernel<false>, fg, dim3(256), 0, stream, *args);
   return hipGetLastError();
 }

@@ -18,7 +18,7 @@
 #include "../../include/jrq.h"
 #include "jrq_device.h"
 
-extern "C" hipError_t jrq_launch_crc64(const JrqCrcArgs* args, int log_entry, int grid,
+extern "C" hipError_t jrq_launch_crc64(JrqCrcArgs* args, int log_entry, int grid,
                                        hipStream_t stream);
 extern "C" hipError_t jrq_launch_quorum(const JrqQuorumArgs* args, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_meta(const JrqAeArgs* a, hipStream_t stream);
@@ -41,19 +41,17 @@ struct jrq_engine {
   int num_cus = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  uint64_t* slice = nullptr;  // [2][256]
+  uint64_t* slice = nullptr;  // [4][256]
   uint64_t* shift = nullptr;  // [kShiftTables][8][256]
   uint64_t* acc = nullptr;    // straddler accumulators
   uint32_t* cnt = nullptr;    // straddler counters
+  uint64_t* pieces = nullptr; // per-segment straddler pieces: [2][scratch_len]
   uint32_t scratch_len = 0;
   int crc_grid = 0;
-  // tuning knobs (JRQ_CRC_SEG_MODE / _SEG_BYTES / _BLOCK / _CHAINS / _TABLES); defaults are the
-  // measured best (profiles/README.md): power-of-two segments, 128-B blocks, slice-by-4
-  uint32_t crc_seg_mode = 0;
+  // JRQ_CRC_SEG_BYTES: fixed CRC segment size (0 = automatic, ~payload / lanes); tests use it
+  // to force many straddling entries
   uint64_t crc_seg_bytes = 0;
-  uint32_t crc_block = 128;
-  uint32_t crc_chains = 1;
-  uint32_t crc_tables = 4;
+  uint32_t crc_seg_map = 1;  // JRQ_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
   DevBuf stage[24];  // 0-13 host-variant staging, 16-19 AppendEntries scratch
@@ -109,7 +107,7 @@ uint64_t mulmod(uint64_t a, uint64_t b) {
 // Constant tables (see crc64.hip):
 //   T0[i]  = CRC64 table entry (jraft-core/.../util/CRC64.java:41-92, generated from the poly)
 //   T1[i]  = T0[i] advanced by one zero byte
-//   slice  = { bswap(T0), bswap(T1) }  (reversed-domain slice-by-2)
+//   slice  = { bswap(T0) .. bswap(T3) }  (reversed-domain slice-by-4)
 //   shift[t][k][i] = (i * x^(8k)) * x^(8 * 2^t) mod G
 void build_tables(std::vector<uint64_t>& slice, std::vector<uint64_t>& shift) {
   uint64_t t[4][256];
@@ -171,13 +169,11 @@ int crc_dispatch(jrq_engine* e, JrqCrcArgs& a, int log_entry) {
   a.shift = e->shift;
   a.acc = e->acc;
   a.cnt = e->cnt;
+  a.piece_cont = e->pieces;
+  a.piece_tail = e->pieces + e->scratch_len;
   a.scratch_len = e->scratch_len;
-  a.min_seg_log2 = 8;
-  a.seg_mode = e->crc_seg_mode;
   a.seg_bytes = e->crc_seg_bytes;
-  a.block_bytes = e->crc_block;
-  a.chains = e->crc_chains;
-  a.tables = e->crc_tables;
+  a.seg_map = e->crc_seg_map;
   JRQ_HIP(e, jrq_launch_crc64(&a, log_entry, e->crc_grid, e->stream));
   return JRQ_OK;
 }
@@ -223,15 +219,9 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   e->max_groups = max_groups;
   e->max_peers = max_peers;
   e->crc_grid = e->num_cus;  // persistent: one 1024-thread workgroup per CU (128 KiB LDS)
-  if (const char* v = std::getenv("JRQ_CRC_SEG_MODE")) e->crc_seg_mode = (uint32_t)std::atoi(v);
-  if (const char* v = std::getenv("JRQ_CRC_BLOCK")) e->crc_block = (uint32_t)std::atoi(v) >= 128 ? 128 : 64;
-  if (const char* v = std::getenv("JRQ_CRC_CHAINS")) e->crc_chains = std::atoi(v) >= 2 ? 2 : 1;
-  if (const char* v = std::getenv("JRQ_CRC_TABLES")) e->crc_tables = std::atoi(v) >= 4 ? 4 : 2;
-  if (const char* v = std::getenv("JRQ_CRC_SEG_BYTES")) {
-    // fixed segment size; at least 64 B and large enough for the straddler scratch
-    uint64_t b = std::strtoull(v, nullptr, 10);
-    e->crc_seg_bytes = (b == 0) ? 0 : (b < 64 ? 64 : b);  // 0 = automatic
-  }
+  if (const char* v = std::getenv("JRQ_CRC_SEG_MAP")) e->crc_seg_map = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("JRQ_CRC_SEG_BYTES"))  // rounded up to 256 B by the kernel
+    e->crc_seg_bytes = std::strtoull(v, nullptr, 10);
   e->scratch_len = static_cast<uint32_t>(2ull * e->crc_grid * jrq::kCrcBlock + 2);
   int rc = JRQ_OK;
   std::vector<uint64_t> slice, shift;
@@ -245,6 +235,7 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   try_hip(hipMalloc(&e->shift, shift.size() * 8), "hipMalloc(shift)");
   try_hip(hipMalloc(&e->acc, static_cast<size_t>(e->scratch_len) * 8), "hipMalloc(acc)");
   try_hip(hipMalloc(&e->cnt, static_cast<size_t>(e->scratch_len) * 4), "hipMalloc(cnt)");
+  try_hip(hipMalloc(&e->pieces, static_cast<size_t>(e->scratch_len) * 16), "hipMalloc(pieces)");
   if (rc == JRQ_OK) {
     try_hip(hipMemcpy(e->slice, slice.data(), slice.size() * 8, hipMemcpyHostToDevice), "upload slice");
     try_hip(hipMemcpy(e->shift, shift.data(), shift.size() * 8, hipMemcpyHostToDevice), "upload shift");
@@ -271,6 +262,7 @@ void jrq_destroy(jrq_engine* e) {
   if (e->shift) (void)hipFree(e->shift);
   if (e->acc) (void)hipFree(e->acc);
   if (e->cnt) (void)hipFree(e->cnt);
+  if (e->pieces) (void)hipFree(e->pieces);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
 }

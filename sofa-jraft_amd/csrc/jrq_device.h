@@ -16,9 +16,9 @@ constexpr uint64_t kCrcPoly = 0x42F0E1EBA9EA3693ULL;
 //   shift[kShiftTables][8][256]  multiply-by-x^(8*2^t) mod P byte tables
 constexpr int kShiftTables = 48;  // shifts up to 2^48 - 1 bytes
 
-// LDS image of the two slice tables, replicated so that lane l only ever touches
-// bank slot (l & 31): byte address = table<<16 | index<<8 | (l&31)<<3 (128 KiB).
-constexpr int kCrcLdsBytes = 2 * 256 * 32 * 8;
+// LDS image of the four slice tables, 16 replicas, two tables per 16-B slot:
+// byte address = (k>>1)<<16 | index<<8 | (lane&15)<<4 | (k&1)<<3 (128 KiB, crc64.hip Tab4).
+constexpr int kCrcLdsBytes = 4 * 256 * 16 * 8;
 constexpr int kCrcBlock = 1024;  // threads per workgroup (16 waves, 1 workgroup / CU)
 
 // Status flags, identical to include/jrq.h jrq_group_status.
@@ -51,13 +51,14 @@ struct JrqCrcArgs {
   const uint64_t* shift;   // [kShiftTables][8][256]
   uint64_t* acc;           // straddler accumulators, zero between launches
   uint32_t* cnt;           // straddler arrival counters, zero between launches
-  uint32_t scratch_len;    // entries in acc/cnt
-  uint32_t min_seg_log2;   // smallest segment size (log2 bytes)
-  uint32_t seg_mode;       // 1: odd multiple of 64 B (default), 0: power of two
-  uint64_t seg_bytes;      // nonzero: fixed segment size (tuning / tests)
-  uint32_t block_bytes;    // per-lane load block: 64 or 128
-  uint32_t chains;         // independent CRC chains per lane: 1 or 2
-  uint32_t tables;         // LDS table flavour: 2 (slice-by-2) or 4 (slice-by-4)
+  uint64_t* piece_cont;    // per segment: its head/middle piece of a straddling entry
+  uint64_t* piece_tail;    // per segment: its tail piece of a straddling entry
+  uint32_t scratch_len;    // entries in acc/cnt/piece_*
+  uint32_t lanes;          // lanes of the rounds grid (set by the launcher)
+  uint32_t seg_map;        // 0: 64-segment chunks round-robin over workgroups; 1: per workgroup
+  uint64_t* timeline;      // nullable diagnostics (tools/crc_timeline.hip): per wave
+                           // {start, end (s_memrealtime), HW_ID, XCC_ID}
+  uint64_t seg_bytes;      // nonzero: segment size (rounded up to 256 B; tests / tuning)
 };
 
 // Leader lease / alive-quorum check (quorum.hip, lease kernel).

@@ -84,17 +84,16 @@ def test_tiny_segments_stress_straddlers(oracle, seg, monkeypatch):
             np.testing.assert_array_equal(e.crc64_batch(payload, offs), exp)
 
 
-@pytest.mark.parametrize("block,chains,tables", [("64", "1", "2"), ("128", "1", "2"),
-                                                 ("64", "2", "2"), ("128", "1", "4"),
-                                                 ("64", "2", "4")])
-def test_every_kernel_variant(oracle, block, chains, tables, monkeypatch):
-    """Each table-flavour / load-block / chain variant is bit-exact on ragged, unaligned and
-    long entries."""
+@pytest.mark.parametrize("seg,seg_map", [("0", "0"), ("0", "1"), ("256", "1"), ("768", "0"),
+                                         ("4096", "1"), (str(1 << 20), "0")])
+def test_segment_sizes_and_maps(oracle, seg, seg_map, monkeypatch):
+    """Every segment size (rounded to 256 B) and chunk-to-workgroup map is bit-exact on
+    ragged, unaligned and long entries: pieces land in per-segment slots (finish kernel)
+    or go through the atomic hand-off when an entry spans more than 64 segments."""
     from jraft_amd import Engine
-    monkeypatch.setenv("JRQ_CRC_BLOCK", block)
-    monkeypatch.setenv("JRQ_CRC_CHAINS", chains)
-    monkeypatch.setenv("JRQ_CRC_TABLES", tables)
-    lens = [0, 1, 15, 16, 17, 255, 256, 257, 1023, 4099, 16384, 100000, 3 << 20, 7]
+    monkeypatch.setenv("JRQ_CRC_SEG_BYTES", seg)
+    monkeypatch.setenv("JRQ_CRC_SEG_MAP", seg_map)
+    lens = [0, 1, 15, 16, 17, 63, 64, 65, 255, 256, 257, 1023, 4099, 16384, 100000, 3 << 20, 7]
     offs = np.concatenate([[5], 5 + np.cumsum(lens)]).astype(np.uint64)
     payload = W.random_bytes(11, int(offs[-1]) + 2)
     rag = W.ragged_offsets(12, 5000, 9000, start=1)
@@ -102,6 +101,16 @@ def test_every_kernel_variant(oracle, block, chains, tables, monkeypatch):
     with Engine(0) as e:
         np.testing.assert_array_equal(e.crc64_batch(payload, offs), oracle.crc64_batch(payload, offs))
         np.testing.assert_array_equal(e.crc64_batch(payload2, rag), oracle.crc64_batch(payload2, rag))
+
+
+def test_more_segments_than_lanes(oracle, monkeypatch):
+    """256-B segments over ~90 MB: each wave loops over several chunks."""
+    from jraft_amd import Engine
+    monkeypatch.setenv("JRQ_CRC_SEG_BYTES", "256")
+    offs = W.ragged_offsets(21, 40000, 4000, start=9)
+    payload = W.random_bytes(21, int(offs[-1]) + 3)
+    with Engine(0) as e:
+        np.testing.assert_array_equal(e.crc64_batch(payload, offs), oracle.crc64_batch(payload, offs))
 
 
 def test_repeat_is_stable(engine, oracle):

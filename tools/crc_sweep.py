@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""A/B the CRC64 kernel's segment policy in ONE process (interleaved rounds).
+"""A/B the CRC64 kernel's segment size in ONE process (interleaved rounds).
 
-Each variant is an engine created with its own JRQ_CRC_SEG_MODE / JRQ_CRC_SEG_BYTES;
+Each variant is an engine created with its own JRQ_CRC_SEG_BYTES (0 = automatic);
 all variants hash the same device-resident C5 (and C1) batches; HIP-event times per
 launch on one stream; median and min over rounds.  Also checks every variant's output
 equals the first's (bit-exact)."""
@@ -23,20 +23,14 @@ def main():
     dev = torch.device("cuda:0")
     s = torch.cuda.Stream(dev)
     torch.cuda.set_stream(s)
-    # variant = seg_mode:seg_bytes:block_bytes:chains:tables (seg_bytes 0 = automatic)
-    dflt = ["0", "0", "128", "1", "2"]
-    variants = [(v.split(":") + dflt[len(v.split(":")):])
-                for v in (sys.argv[1:] or ["0:0:128:1:2", "0:0:128:1:4", "0:0:64:2:4"])]
     engines = []
-    for mode, nbytes, blk, ch, tabs in variants:
-        os.environ["JRQ_CRC_SEG_MODE"] = mode
+    for var in (sys.argv[1:] or ["0", "1024", "2048", "8192"]):
+        nbytes, _, smap = var.partition(":")  # seg_bytes[:seg_map]
         os.environ["JRQ_CRC_SEG_BYTES"] = nbytes
-        os.environ["JRQ_CRC_BLOCK"] = blk
-        os.environ["JRQ_CRC_CHAINS"] = ch
-        os.environ["JRQ_CRC_TABLES"] = tabs
+        os.environ["JRQ_CRC_SEG_MAP"] = smap or "0"
         e = Engine(0)
         e.use_stream(s.cuda_stream)
-        engines.append((f"mode{mode}/S{nbytes}/B{blk}/C{ch}/T{tabs}", e))
+        engines.append((f"S{nbytes}/M{smap or 0}", e))
     res = {}
     for cfg, n, eb in (("C5", 64 << 10, 16 << 10), ("C1", 1 << 20, 256)):
         b = W.entry_batch(n, eb, seed=3)

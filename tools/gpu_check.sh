@@ -26,5 +26,7 @@ for s in $STEPS; do
     pmcf)  run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
     pmcw)  run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
     host)  run host_test 300 ./sofa-jraft_amd/lib/host_test gpu ;;
+    probe) run mem_probe 300 ./tools/mem_probe ;;
+    sweep) run crc_sweep 600 python tools/crc_sweep.py ${SWEEP_VARIANTS:-} ;;
   esac
 done

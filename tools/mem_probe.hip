@@ -76,26 +76,6 @@ __global__ __launch_bounds__(1024) void per_lane_grp(const uint4* __restrict__ p
   out[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
-// Compute-only ceiling of the CRC kernel's table hash: the same LDS image and step
-// functions as crc64.hip, data synthesised in registers (no global loads).
-template <class Tab>
-__global__ __launch_bounds__(1024) void hash_only(uint64_t S, uint32_t* out) {
-  __shared__ __attribute__((aligned(16))) uint64_t lds_tab[jrq::kCrcLdsBytes / 8];
-  for (uint32_t w = threadIdx.x; w < jrq::kCrcLdsBytes / 8; w += blockDim.x)
-    lds_tab[w] = 0x9E3779B97F4A7C15ull * (w + 1);
-  __syncthreads();
-  const char* lds = reinterpret_cast<const char*>(lds_tab);
-  const Tab tb(threadIdx.x & 63u);
-  jrq::RState r{threadIdx.x, blockIdx.x};
-  uint32_t x = threadIdx.x * 0x9E3779B9u;
-  for (uint64_t i = 0; i < S / 16; ++i) {
-    x += 0x6D2B79F5u;
-    const uint4 v = make_uint4(x, x ^ 0x55u, x + 7u, x ^ 0xAAu);
-    jrq::step16(tb, r, v, lds);
-  }
-  out[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = r.lo ^ r.hi;
-}
-
 // Pattern 1: fully coalesced grid-stride float4 stream.
 __global__ __launch_bounds__(1024) void coalesced(const uint4* __restrict__ p, uint64_t n16,
                                                   uint32_t* out) {
@@ -141,15 +121,6 @@ int main(int argc, char** argv) {
     std::printf("%-44s best %.4f ms  %.0f GB/s   mean %.4f ms\n", name, best,
                 total / (best * 1e-3) / 1e9, sum / reps);
   };
-  {
-    const int grid = cus;  // 1 WG (1024 lanes) per CU, 4 KiB per lane = 1 GiB equivalent
-    time("hash_only Tab4 (1 GiB equiv)", [&] {
-      hipLaunchKernelGGL(hash_only<jrq::Tab4>, dim3(grid), dim3(1024), 0, 0, 4096ull, out);
-    });
-    time("hash_only Tab2 (1 GiB equiv)", [&] {
-      hipLaunchKernelGGL(hash_only<jrq::Tab2>, dim3(grid), dim3(1024), 0, 0, 4096ull, out);
-    });
-  }
   if (argc > 1) return 0;
   for (int wg_per_cu : {1, 2}) {
     const int grid = cus * wg_per_cu;
