@@ -14,13 +14,13 @@
 //    before the entry's end contributes crc(piece) * x^(8n) mod P, and the entry's CRC is the
 //    XOR of its pieces.  Pieces of entries that span segments meet in a scratch slot through
 //    agent-scope atomics; the last arriving piece writes the result and re-zeroes the slot.
-//  * Coalesced quad loads + DPP transpose.  A lane reading only its own segment touches 64
-//    different cache lines per wave instruction and streams at ~4.8 TB/s at best; instead the 4
-//    lanes of a quad read 64 contiguous bytes of ONE owner per instruction (8 loads = 128 B per
-//    lane per round, every owner's 128 B in full), and a 2-stage butterfly over the quad
-//    (DPP quad_perm moves + selects) hands every lane its own 8 pieces.  Rounds are
-//    double-buffered in registers; buffer loads with a per-wave descriptor clamp reads past
-//    the data to zero.
+//  * Coalesced row-group loads + row-swap transpose.  A lane reading only its own segment
+//    touches 64 different cache lines per wave instruction and streams at ~4.8 TB/s at best;
+//    instead the 4 lanes {c, c+16, c+32, c+48} read 64 contiguous bytes of ONE owner per
+//    instruction (4 loads = 64 B per lane per half-round, every owner's 64 B in full), and a
+//    2-stage butterfly of v_permlane16_swap / v_permlane32_swap (16 swaps per half-round,
+//    no selects) hands every lane its own 4 pieces.  Half-rounds run through a 3-deep
+//    register ring; buffer loads with a per-wave descriptor clamp reads past the data to 0.
 //  * Table CRC in the "reversed domain" r = bswap64(crc): a little-endian load XORs straight
 //    into r, and 4 bytes are one step  r = (r >> 32) ^ R3[b0] ^ R2[b1] ^ R1[b2] ^ R0[b3],
 //    R_j = bswap(T_j), T_j[i] = i * x^(64 + 8j) mod P.  The tables live in LDS, replicated 16x
@@ -34,6 +34,10 @@
 //  * The x^(8n) multiplications use byte tables in global memory (one per power of two,
 //    L2-resident); they run at most once per piece that does not end its entry.
 #include "jrq_device.h"
+
+#ifndef JRQ_CRC_RING
+#define JRQ_CRC_RING 3  // half-round register ring depth of the rounds kernel (3 or 4)
+#endif
 
 namespace jrq {
 
@@ -107,48 +111,142 @@ struct Tab4 {
     step8(r, v[0], v[1], lds);
     step8(r, v[2], v[3], lds);
   }
+  // step4 that also XORs the data word two steps ahead into the new r.hi: r.hi becomes the
+  // base of r.lo in the next step, and that r.lo is what the step after consumes, so word
+  // j + 2 enters exactly when step j + 2 needs it -- at no cost (xor3 takes it beside t3.y)
+  __device__ __forceinline__ void step4w(RState& r, uint32_t w, const char* lds) const {
+    const uint32_t x = __builtin_amdgcn_perm(r.lo, r.lo, swz);
+    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc[0], x, 0x0C060004u));
+    const uint2 t1 = lds_u2(lds, __builtin_amdgcn_perm(lc[1], x, 0x0C060104u));
+    const uint2 t2 = lds_u2(lds, __builtin_amdgcn_perm(lc[2], x, 0x0C060204u));
+    const uint2 t3 = lds_u2(lds, __builtin_amdgcn_perm(lc[3], x, 0x0C060304u));
+    r.lo = xor3(xor3(r.hi, t0.x, t1.x), t2.x, t3.x);
+    r.hi = xor3(xor3(t0.y, t1.y, t2.y), t3.y, w);
+  }
+  // 64 bytes = 16 data words: words 0, 1 XOR in directly, words 2..15 ride step4w
+  __device__ __forceinline__ void step64(RState& r, const u32x4 (&v)[4], const char* lds) const {
+    r.lo ^= v[0][0];
+    r.hi ^= v[0][1];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) step4w(r, v[(j + 2) >> 2][(j + 2) & 3], lds);
+    step4(r, lds);
+    step4(r, lds);
+  }
 };
 
-// ------------------------------------------------------- quad transpose ---
-__device__ __forceinline__ uint32_t dpp_quad_xor1(uint32_t v) {
-  return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
-}
-__device__ __forceinline__ uint32_t dpp_quad_xor2(uint32_t v) {
-  return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
-}
+// ------------------------------------------------------------ slice-by-8 ---
+// 8 bytes per step: r = R7[b0] ^ R6[b1] ^ R5[b2] ^ R4[b3] ^ R3[b4] ^ R2[b5] ^ R1[b6] ^ R0[b7]
+// (b0..b3 = r.lo, b4..b7 = r.hi after the data XOR).  Half as many dependent LDS round
+// trips per byte as slice-by-4 at the same VALU count per byte.
+// LDS image, 8 replicas: byte address = g<<16 | index<<8 | replica<<5 | p<<3 holds R_{4g+p}
+// (g = 1: tables R4..R7, used with r.lo; g = 0: R0..R3, used with r.hi; p = 3 - byte).
+// Conflict-free ds_read_b64: in a 32-lane group the 4 lanes sharing a replica (lane & 7) are
+// its 4 rotations rot = (lane >> 3) & 3, and instruction i reads table position
+// p = (i + rot) & 3 -- all 32 lanes on distinct bank pairs.  The rotation is one v_perm of
+// each state word (swz), so the address v_perm's byte selector stays an immediate.
+struct Tab8 {
+  uint32_t lc[4];  // instruction i: b0 = replica<<5 | p_i<<3, b1 = 1 (g = 1), b2 = 0 (g = 0)
+  uint32_t swz;    // v_perm selector: byte i of x = byte 3 - p_i of the word
+  __device__ explicit Tab8(uint32_t lane) {
+    const uint32_t rep = lane & 7u, rot = (lane >> 3) & 3u;
+    swz = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t p = (static_cast<uint32_t>(i) + rot) & 3u;
+      lc[i] = (rep << 5) | (p << 3) | (1u << 8);
+      swz |= (3u - p) << (8 * i);
+    }
+  }
 
-// One butterfly stage on quad-lane bit B for a register pair (lo: register bit B = 0, hi: 1).
-// An element stays where its lane bit equals its register bit, else it trades places with
-// the partner lane's other register.
-template <int B>
-__device__ __forceinline__ void quad_stage(u32x4& lo, u32x4& hi, bool bit) {
-  u32x4 nlo, nhi;
+  // word w = g<<13 | index<<5 | replica<<2 | p  ->  R_{4g+p}[index]
+  __device__ static uint32_t src_index(uint32_t w) {
+    return (((w >> 13) << 2) | (w & 3u)) * 256 + ((w >> 5) & 255u);
+  }
+
+  // eight bytes already XORed into r; the new r.lo / r.hi also take the words wl / wh (the
+  // next step's data, folded into the XOR trees)
+  __device__ __forceinline__ void step8w(RState& r, uint32_t wl, uint32_t wh,
+                                         const char* lds) const {
+    const uint32_t xl = __builtin_amdgcn_perm(r.lo, r.lo, swz);
+    const uint32_t xh = __builtin_amdgcn_perm(r.hi, r.hi, swz);
+    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc[0], xl, 0x0C050004u));
+    const uint2 t1 = lds_u2(lds, __builtin_amdgcn_perm(lc[1], xl, 0x0C050104u));
+    const uint2 t2 = lds_u2(lds, __builtin_amdgcn_perm(lc[2], xl, 0x0C050204u));
+    const uint2 t3 = lds_u2(lds, __builtin_amdgcn_perm(lc[3], xl, 0x0C050304u));
+    const uint2 u0 = lds_u2(lds, __builtin_amdgcn_perm(lc[0], xh, 0x0C060004u));
+    const uint2 u1 = lds_u2(lds, __builtin_amdgcn_perm(lc[1], xh, 0x0C060104u));
+    const uint2 u2 = lds_u2(lds, __builtin_amdgcn_perm(lc[2], xh, 0x0C060204u));
+    const uint2 u3 = lds_u2(lds, __builtin_amdgcn_perm(lc[3], xh, 0x0C060304u));
+    r.lo = xor3(xor3(xor3(t0.x, t1.x, t2.x), t3.x, u0.x), xor3(u1.x, u2.x, u3.x), wl);
+    r.hi = xor3(xor3(xor3(t0.y, t1.y, t2.y), t3.y, u0.y), xor3(u1.y, u2.y, u3.y), wh);
+  }
+  __device__ __forceinline__ void step8(RState& r, uint32_t dlo, uint32_t dhi,
+                                        const char* lds) const {
+    r.lo ^= dlo;
+    r.hi ^= dhi;
+    step8w(r, 0u, 0u, lds);
+  }
+  // one byte: r = R0[(r ^ b) & 0xFF] ^ (r >> 8)   (CRC64.update(byte), CRC64.java:100-103)
+  __device__ __forceinline__ void step1(RState& r, uint32_t b, const char* lds) const {
+    const uint32_t lc0 = lc[0] & 0xE0u;  // this lane's replica of R0 (g = 0, p = 0)
+    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc0, r.lo ^ b, 0x0C060004u));
+    const uint32_t nlo = __builtin_amdgcn_alignbit(r.hi, r.lo, 8);
+    r.lo = nlo ^ t0.x;
+    r.hi = (r.hi >> 8) ^ t0.y;
+  }
+  // 64 bytes = 8 steps; words 2s+2, 2s+3 ride step s's XOR trees
+  __device__ __forceinline__ void step64(RState& r, const u32x4 (&v)[4], const char* lds) const {
+    r.lo ^= v[0][0];
+    r.hi ^= v[0][1];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const int wl = 2 * s + 2, wh = 2 * s + 3;
+      step8w(r, v[wl >> 2][wl & 3], v[wh >> 2][wh & 3], lds);
+    }
+    step8w(r, 0u, 0u, lds);
+  }
+};
+
+// The table flavour the rounds kernel uses (Tab4 stays for the design probes).
+using CrcTab = Tab8;
+
+// -------------------------------------------------------- row transpose ---
+// The four lanes {c, c+16, c+32, c+48} of a wave (one per 16-lane row) read the 64
+// contiguous bytes of one owner segment per load instruction: load q of the lane in row i
+// holds piece i (16 B at 16i) of owner lane 16q + c.  Two butterfly stages of gfx950's
+// row-swap instructions turn that back into "register j = piece j of this lane's own
+// segment"; each swap exchanges one register pair in place, no lane selects.
+//   stage 1 (row bit 0): v_permlane16_swap  -- odd rows of a <-> even rows of b
+//   stage 2 (row bit 1): v_permlane32_swap  -- rows 2,3 of a <-> rows 0,1 of b
+__device__ __forceinline__ void swap16(u32x4& a, u32x4& b) {
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    const uint32_t plo = B == 0 ? dpp_quad_xor1(lo[c]) : dpp_quad_xor2(lo[c]);
-    const uint32_t phi = B == 0 ? dpp_quad_xor1(hi[c]) : dpp_quad_xor2(hi[c]);
-    nhi[c] = bit ? hi[c] : plo;
-    nlo[c] = bit ? phi : lo[c];
+    const auto r = __builtin_amdgcn_permlane16_swap(a[c], b[c], false, false);
+    a[c] = r[0];
+    b[c] = r[1];
   }
-  lo = nlo;
-  hi = nhi;
 }
-
-// reg o = piece m of owner o (quad lane m)  ->  reg j = piece j of this lane's own segment.
-// Must run with all four lanes of the quad active (DPP reads the partner lanes).
-__device__ __forceinline__ void quad_transpose(u32x4& a0, u32x4& a1, u32x4& a2, u32x4& a3,
-                                               uint32_t m) {
-  quad_stage<0>(a0, a1, m & 1u);
-  quad_stage<0>(a2, a3, m & 1u);
-  quad_stage<1>(a0, a2, (m >> 1) & 1u);
-  quad_stage<1>(a1, a3, (m >> 1) & 1u);
+__device__ __forceinline__ void swap32(u32x4& a, u32x4& b) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const auto r = __builtin_amdgcn_permlane32_swap(a[c], b[c], false, false);
+    a[c] = r[0];
+    b[c] = r[1];
+  }
+}
+// Must run with the whole wave active (the swaps read the partner rows).
+__device__ __forceinline__ void row_transpose(u32x4& a0, u32x4& a1, u32x4& a2, u32x4& a3) {
+  swap16(a0, a1);
+  swap16(a2, a3);
+  swap32(a0, a2);
+  swap32(a1, a3);
 }
 
 // --------------------------------------------------------------- helpers ---
 
 // Continue r over virtual bytes [p, q) read from global memory (A = address of virtual byte
 // 0, 16-B aligned).  Slow path: rounds that hold an entry boundary or the data edge.
-__device__ __forceinline__ void hash_global(const Tab4& tb, RState& r, const uint8_t* __restrict__ A,
+__device__ __forceinline__ void hash_global(const CrcTab& tb, RState& r, const uint8_t* __restrict__ A,
                                             uint64_t p, uint64_t q, const char* lds) {
   while (p < q && (p & 15u)) {
     tb.step1(r, A[p], lds);
@@ -259,7 +357,6 @@ struct SegWalk {
   uint32_t hi;       // min(S, data end)
   uint32_t cur;      // entry being hashed (or next to start)
   uint32_t cur_end;  // E(cur + 1)
-  uint32_t nxt_end;  // E(cur + 2), loaded one entry ahead (the load lands by the next event)
   uint32_t flags;
   static constexpr uint32_t kStarted = 1, kLastSeg = 2, kDone = 4;
 };
@@ -273,10 +370,10 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
 
   // Build the replicated LDS image of the slice tables (a.slice = R0, R1, R2, R3).
   for (uint32_t w = threadIdx.x; w < kCrcLdsBytes / 8; w += blockDim.x)
-    lds_tab[w] = a.slice[Tab4::src_index(w)];
+    lds_tab[w] = a.slice[CrcTab::src_index(w)];
   __syncthreads();
 
-  const Tab4 tb(threadIdx.x & 63u);
+  const CrcTab tb(threadIdx.x & 63u);
   const uint32_t n = a.n;
   const uint64_t* __restrict__ off = a.offsets;
   const uint64_t base = off[0];
@@ -297,14 +394,33 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
 
   // L0 (first lane of the wave) through readfirstlane: the compiler then knows the wave's
   // window and descriptor are uniform (SGPRs; no waterfall loop around each buffer load)
-  const uint32_t L = threadIdx.x, m = L & 3u;
+  const uint32_t L = threadIdx.x;
   const uint32_t L0 = __builtin_amdgcn_readfirstlane(L & ~63u);
   const uint32_t WS = static_cast<uint32_t>(S);  // lane-to-lane segment step (window < 2^31)
   const uint32_t lane_off = (L - L0) * WS;       // this lane's segment, relative to the wave's
-  // load (q, h) of a round reads 16 B of quad owner q at round offset 64h + 16m, so the
-  // quad reads 64 contiguous bytes per instruction: offset = qbase + q*WS + 64h + round*128
-  const uint32_t qbase = lane_off - m * WS + 16u * m;
+  // load q of half-round h reads 16 B of owner lane 16q + c at offset 64h + 16*row, so the
+  // lanes {c, c+16, c+32, c+48} read 64 contiguous bytes per instruction
+  const uint32_t qbase = (L & 15u) * WS + 16u * ((L >> 4) & 3u);
   const uint64_t waves = blockDim.x / 64;
+  // Wave priority by progress: the SIMD arbiter otherwise serves its 4 waves oldest-first,
+  // so equal shares of work finish at 4 distinct times and the last quarter of the launch
+  // runs with few waves in flight.  Waves start at priority 3 and step down at 1/2, 3/4 and
+  // 7/8 of their own work (chunk c = j * G + g over all G waves of the grid), letting the
+  // waves behind them catch up.
+  // (all of it wave-uniform, kept in SGPRs through readfirstlane: VALU temporaries here
+  // collided with the prefetch ring's registers and cost a vmcnt(0) per iteration)
+  uint32_t prio_lvl = 0, pt0 = ~0u, pt1 = ~0u, pt2 = ~0u;
+  if (a.prio_steps) {
+    const uint64_t G = grid * waves, C = (nseg + 63) / 64;
+    const uint64_t g = a.seg_map ? blockIdx.x * waves + (L0 >> 6) : (L0 >> 6) * grid + blockIdx.x;
+    const uint64_t w64 = (g < C ? (C - g + G - 1) / G : 0) * rounds * 2;
+    const uint32_t work = __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(w64 > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : w64));
+    pt0 = work / 2;
+    pt1 = work - work / 4;
+    pt2 = work - work / 8;
+    __builtin_amdgcn_s_setprio(3);
+  }
   for (uint64_t j = 0;; ++j) {
     const uint64_t kw = a.seg_map ? ((j * grid + blockIdx.x) * waves + (L0 >> 6)) * 64
                                   : ((j * waves + (L0 >> 6)) * grid + blockIdx.x) * 64;
@@ -328,10 +444,11 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     sw.cur = 0;
     sw.next = 0;
     sw.cur_end = 0;
-    sw.nxt_end = 0xFFFFFFFFu;
     // entry cur starts at pos: skip (emit) zero-length entries there -- they belong to the
     // segment holding pos, the last segment also owning those at the data end -- then arm
-    // the next event and prefetch the boundary after it
+    // the next event.  The boundary is loaded here, not prefetched an entry ahead: a load
+    // still in flight across ring iterations made the compiler drain the whole prefetch
+    // ring (vmcnt(0)) at the top of every iteration.
     auto start_entry = [&]() {
       while (sw.cur < n) {
         sw.cur_end = rel(E(sw.cur + 1));
@@ -343,7 +460,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
         sw.flags |= SegWalk::kDone;
       } else {
         sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
-        sw.nxt_end = sw.cur + 2 <= n ? rel(E(sw.cur + 2)) : 0xFFFFFFFFu;
       }
     };
 #if defined(JRQ_DIAG_NO_SETUP)  // tools/crc_timeline only: 16 KiB entries, no offset loads
@@ -352,7 +468,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
       if (s0 & 16383) sw.flags &= ~SegWalk::kStarted;
       sw.cur_end = static_cast<uint32_t>(((s0 >> 14) + 1) * 16384 - s0);
       sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
-      sw.nxt_end = sw.cur_end + 16384;
     }
 #else
     if (!(sw.flags & SegWalk::kDone)) {
@@ -362,7 +477,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
         sw.flags &= ~SegWalk::kStarted;
         sw.cur_end = rel(E(e));
         sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
-        sw.nxt_end = e + 1 <= n ? rel(E(e + 1)) : 0xFFFFFFFFu;
       } else {
         sw.cur = e;
         start_entry();
@@ -389,19 +503,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
         r = RState{0u, 0u};
         sw.flags |= SegWalk::kStarted;
         ++sw.cur;
-        if (sw.cur >= n) {
-          sw.flags |= SegWalk::kDone;
-        } else if (sw.nxt_end != sw.pos) {  // common case: the prefetched boundary
-          sw.cur_end = sw.nxt_end;
-          if (sw.pos >= sw.hi) {
-            sw.flags |= SegWalk::kDone;
-          } else {
-            sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
-            sw.nxt_end = sw.cur + 2 <= n ? rel(E(sw.cur + 2)) : 0xFFFFFFFFu;
-          }
-        } else {
-          start_entry();  // zero-length entries here
-        }
+        start_entry();
       } else {  // pos == hi < entry end
 #if defined(JRQ_DIAG_NO_TAIL)  // tools/crc_timeline only: drop the head/middle piece
         a.piece_cont[k] = crc_value(r);
@@ -422,29 +524,60 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     };
 
     // buffer descriptor: from the wave's first segment to the data end (loads past it
-    // return zero)
+    // return zero).  Its words pass through readfirstlane: the compiler then keeps it in
+    // SGPRs (otherwise it may hold it in VGPRs and wrap each load in a waterfall loop).
     const uint64_t nrec = span - wbase;
+    const uintptr_t wptr = reinterpret_cast<uintptr_t>(A + wbase);
+    const uint32_t wlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wptr));
+    const uint32_t whi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wptr >> 32));
+    const uint32_t nr = __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(nrec > 0x7FFFFFFFull ? 0x7FFFFFFFull : nrec));
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(A + wbase), static_cast<short>(0),
-        static_cast<int>(nrec > 0x7FFFFFFFull ? 0x7FFFFFFFull : nrec), 0x00020000);
-    // empty descriptor: the prefetch past the last round reads nothing (every offset is out
-    // of range), so the ring's loads stay unconditional and the vmcnt accounting static
-    const __amdgpu_buffer_rsrc_t rs_none = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(A + wbase), static_cast<short>(0), 0, 0x00020000);
+        reinterpret_cast<uint8_t*>((static_cast<uint64_t>(whi) << 32) | wlo),
+        static_cast<short>(0), static_cast<int>(nr), 0x00020000);
 
     // Ring of three half-rounds (64 B per lane each, 16 VGPRs): two in flight while one is
-    // hashed.  Half h of a round: load q reads 16 B of quad owner q at segment offset
-    // 64h' + 16m (h' = the half's index), so the quad reads 64 contiguous bytes of one
-    // owner per instruction.
+    // hashed.  Half-round h: load q reads 16 B of owner lane 16q + c at segment offset
+    // 64h + 16*row, so each row group reads 64 contiguous bytes of one owner per instruction.
+#if JRQ_CRC_RING == 4
+    u32x4 h0[4], h1[4], h2[4], h3[4];
+#else
     u32x4 h0[4], h1[4], h2[4];
+#endif
+    // Each half-round's loads use a descriptor whose base is advanced by the half's offset
+    // (scalar adds), so the per-lane voffsets stay loop-invariant: no VALU address temps
+    // that the register allocator could place on a ring slot still being loaded (such a
+    // write-after-write made the compiler wait for the whole ring, vmcnt(0)).
+    const uint32_t qa0 = qbase, qa1 = qbase + 16u * WS, qa2 = qbase + 32u * WS,
+                   qa3 = qbase + 48u * WS;
+    const uint64_t wptr_u = (static_cast<uint64_t>(whi) << 32) | wlo;
 #define JRQ_LOAD_HALF(H, RS, hh)                                                         \
   do {                                                                                   \
-    const uint32_t ho = (hh) * 64u;                                                      \
-    _Pragma("unroll") for (int q = 0; q < 4; ++q) H[q] =                                 \
-        __builtin_amdgcn_raw_buffer_load_b128(RS, qbase + (q * WS + ho), 0, 0);          \
+    const uint32_t ho = __builtin_amdgcn_readfirstlane((hh) * 64u);                      \
+    const uint64_t hp = wptr_u + ho;                                                     \
+    const uint32_t hlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp));      \
+    const uint32_t hhi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp >> 32)); \
+    uint32_t hn; /* nr - min(ho, nr) on the scalar unit (no VALU temp; see above) */     \
+    asm("s_min_u32 %0, %1, %2\n\ts_sub_u32 %0, %2, %0" : "=&s"(hn) : "s"(ho), "s"(nr));   \
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(                 \
+        reinterpret_cast<uint8_t*>((static_cast<uint64_t>(hhi) << 32) | hlo),            \
+        static_cast<short>(0), static_cast<int>(hn), 0x00020000);                        \
+    H[0] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa0, 0, 0);                         \
+    H[1] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa1, 0, 0);                         \
+    H[2] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa2, 0, 0);                         \
+    H[3] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa3, 0, 0);                         \
     asm volatile("" ::: "memory");                                                       \
   } while (0)
-    const uint32_t halves = rounds * 2;
+    const uint32_t halves = __builtin_amdgcn_readfirstlane(rounds * 2);
+    const uint32_t prog0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(j * halves));
+    // prefetches past the chunk's last half-round re-read that half (L2-hot): the half
+    // index stays wave-uniform and the descriptor a single SGPR quad -- selecting an empty
+    // descriptor instead put it in VGPRs and wrapped every load in a waterfall loop
+    auto last_half = [&](uint32_t h) -> uint32_t { return h < halves ? h : halves - 1u; };
+    // settle the setup's loads first (e.g. an unused interpolation probe): a load the
+    // compiler still counts as in flight when the ring starts costs a vmcnt(0) at the top
+    // of every ring iteration
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     JRQ_LOAD_HALF(h0, rs, 0u);
     JRQ_LOAD_HALF(h1, rs, 1u);
 
@@ -453,43 +586,95 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
       if (sw.flags & SegWalk::kDone) return;
       const uint32_t hs = hh * 64u, he = hs + 64u;
       if (sw.pos == hs && he <= sw.next) {  // fast path: the half lies inside entry cur
-#pragma unroll
-        for (int p = 0; p < 4; ++p) tb.step16(r, v[p], lds);
+        tb.step64(r, v, lds);
         sw.pos = he;
       }
-      while (!(sw.flags & SegWalk::kDone)) {
-        if (sw.pos == sw.next) {
-          event();
-          continue;
+      if (sw.flags & SegWalk::kDone) return;
+      if (sw.pos == sw.next || sw.pos < he) {  // slow path: events / bytes from memory
+        while (!(sw.flags & SegWalk::kDone)) {
+          if (sw.pos == sw.next) {
+            event();
+            continue;
+          }
+          if (sw.pos >= he) break;
+          const uint32_t lim = he < sw.next ? he : sw.next;
+          hash_global(tb, r, A, s0 + sw.pos, s0 + lim, lds);
+          sw.pos = lim;
         }
-        if (sw.pos >= he) break;
-        const uint32_t lim = he < sw.next ? he : sw.next;
-        hash_global(tb, r, A, s0 + sw.pos, s0 + lim, lds);
-        sw.pos = lim;
+        // settle the slow path's own loads here (vmcnt(0); it waits on its last load
+        // anyway): a load the compiler still counts as in flight at the ring's loop head
+        // makes it drain the whole prefetch ring there on every iteration
+        __builtin_amdgcn_s_waitcnt(0x0F70);
       }
     };
 
-    // transposes run with the whole wave active (quad DPP), before any per-lane branch; the
+    // transposes run with the whole wave active (row swaps), before any per-lane branch; the
     // asm pin keeps the half's first use below the loads issued before it (otherwise the
     // scheduler hoists the memory-free transposes and drains the prefetch with vmcnt(0))
     auto transpose_half = [&](u32x4 (&v)[4]) {
       asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
-      quad_transpose(v[0], v[1], v[2], v[3], m);
+      row_transpose(v[0], v[1], v[2], v[3]);
     };
 
-    for (uint32_t hh = 0; hh < halves; hh += 3) {
-      JRQ_LOAD_HALF(h2, (hh + 2 < halves ? rs : rs_none), hh + 2);
+#if JRQ_CRC_RING == 4
+    // 4-slot ring: three half-rounds in flight while one is hashed
+    JRQ_LOAD_HALF(h2, rs, last_half(2u));
+    for (uint32_t hh0 = 0; hh0 < halves; hh0 += 4) {
+      const uint32_t hh = __builtin_amdgcn_readfirstlane(hh0);  // keep the counter in SGPRs
+      if (a.prio_steps) {  // wave-uniform: lower this wave's priority as it gets ahead
+        const uint32_t prog = prog0 + hh;
+        const uint32_t lvl = __builtin_amdgcn_readfirstlane(
+            static_cast<uint32_t>(prog >= pt0) + (prog >= pt1) + (prog >= pt2));
+        if (lvl != prio_lvl) {
+          prio_lvl = lvl;
+          if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+          else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+          else __builtin_amdgcn_s_setprio(0);
+        }
+      }
+      JRQ_LOAD_HALF(h3, rs, last_half(hh + 3));
       transpose_half(h0);
       process(hh, h0);
       if (hh + 1 >= halves) break;  // wave-uniform
-      JRQ_LOAD_HALF(h0, (hh + 3 < halves ? rs : rs_none), hh + 3);
+      JRQ_LOAD_HALF(h0, rs, last_half(hh + 4));
       transpose_half(h1);
       process(hh + 1, h1);
       if (hh + 2 >= halves) break;
-      JRQ_LOAD_HALF(h1, (hh + 4 < halves ? rs : rs_none), hh + 4);
+      JRQ_LOAD_HALF(h1, rs, last_half(hh + 5));
+      transpose_half(h2);
+      process(hh + 2, h2);
+      if (hh + 3 >= halves) break;
+      JRQ_LOAD_HALF(h2, rs, last_half(hh + 6));
+      transpose_half(h3);
+      process(hh + 3, h3);
+    }
+#else
+    for (uint32_t hh0 = 0; hh0 < halves; hh0 += 3) {
+      const uint32_t hh = __builtin_amdgcn_readfirstlane(hh0);  // keep the counter in SGPRs
+      if (a.prio_steps) {  // wave-uniform: lower this wave's priority as it gets ahead
+        const uint32_t prog = prog0 + hh;
+        const uint32_t lvl = __builtin_amdgcn_readfirstlane(
+            static_cast<uint32_t>(prog >= pt0) + (prog >= pt1) + (prog >= pt2));
+        if (lvl != prio_lvl) {
+          prio_lvl = lvl;
+          if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+          else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+          else __builtin_amdgcn_s_setprio(0);
+        }
+      }
+      JRQ_LOAD_HALF(h2, rs, last_half(hh + 2));
+      transpose_half(h0);
+      process(hh, h0);
+      if (hh + 1 >= halves) break;  // wave-uniform
+      JRQ_LOAD_HALF(h0, rs, last_half(hh + 3));
+      transpose_half(h1);
+      process(hh + 1, h1);
+      if (hh + 2 >= halves) break;
+      JRQ_LOAD_HALF(h1, rs, last_half(hh + 4));
       transpose_half(h2);
       process(hh + 2, h2);
     }
+#endif
 #undef JRQ_LOAD_HALF
   }
   if (a.timeline && (threadIdx.x & 63u) == 0) {  // diagnostics only

@@ -41,7 +41,7 @@ struct jrq_engine {
   int num_cus = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  uint64_t* slice = nullptr;  // [4][256]
+  uint64_t* slice = nullptr;  // [kSliceTables][256]
   uint64_t* shift = nullptr;  // [kShiftTables][8][256]
   uint64_t* acc = nullptr;    // straddler accumulators
   uint32_t* cnt = nullptr;    // straddler counters
@@ -51,6 +51,7 @@ struct jrq_engine {
   // JRQ_CRC_SEG_BYTES: fixed CRC segment size (0 = automatic, ~payload / lanes); tests use it
   // to force many straddling entries
   uint64_t crc_seg_bytes = 0;
+  uint32_t crc_prio = 1;     // JRQ_CRC_PRIO: progress-stepped wave priority (A/B knob)
   uint32_t crc_seg_map = 1;  // JRQ_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
@@ -107,19 +108,19 @@ uint64_t mulmod(uint64_t a, uint64_t b) {
 // Constant tables (see crc64.hip):
 //   T0[i]  = CRC64 table entry (jraft-core/.../util/CRC64.java:41-92, generated from the poly)
 //   T1[i]  = T0[i] advanced by one zero byte
-//   slice  = { bswap(T0) .. bswap(T3) }  (reversed-domain slice-by-4)
+//   slice  = { bswap(T0) .. bswap(T7) }  (reversed-domain slice-by-8)
 //   shift[t][k][i] = (i * x^(8k)) * x^(8 * 2^t) mod G
 void build_tables(std::vector<uint64_t>& slice, std::vector<uint64_t>& shift) {
-  uint64_t t[4][256];
+  uint64_t t[jrq::kSliceTables][256];
   for (int i = 0; i < 256; ++i) {
     uint64_t c = static_cast<uint64_t>(i) << 56;
     for (int k = 0; k < 8; ++k) c = (c & 0x8000000000000000ULL) ? (c << 1) ^ jrq::kCrcPoly : (c << 1);
     t[0][i] = c;
   }
-  for (int j = 1; j < 4; ++j)  // T_j = T_{j-1} advanced by one zero byte
+  for (int j = 1; j < jrq::kSliceTables; ++j)  // T_j = T_{j-1} advanced by one zero byte
     for (int i = 0; i < 256; ++i) t[j][i] = t[0][t[j - 1][i] >> 56] ^ (t[j - 1][i] << 8);
-  slice.resize(4 * 256);
-  for (int j = 0; j < 4; ++j)
+  slice.resize(jrq::kSliceTables * 256);
+  for (int j = 0; j < jrq::kSliceTables; ++j)
     for (int i = 0; i < 256; ++i) slice[j * 256 + i] = __builtin_bswap64(t[j][i]);
   shift.resize(static_cast<size_t>(jrq::kShiftTables) * 8 * 256);
   uint64_t K = 0x100;  // x^8
@@ -174,6 +175,7 @@ int crc_dispatch(jrq_engine* e, JrqCrcArgs& a, int log_entry) {
   a.scratch_len = e->scratch_len;
   a.seg_bytes = e->crc_seg_bytes;
   a.seg_map = e->crc_seg_map;
+  a.prio_steps = e->crc_prio;
   JRQ_HIP(e, jrq_launch_crc64(&a, log_entry, e->crc_grid, e->stream));
   return JRQ_OK;
 }
@@ -219,6 +221,7 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   e->max_groups = max_groups;
   e->max_peers = max_peers;
   e->crc_grid = e->num_cus;  // persistent: one 1024-thread workgroup per CU (128 KiB LDS)
+  if (const char* v = std::getenv("JRQ_CRC_PRIO")) e->crc_prio = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("JRQ_CRC_SEG_MAP")) e->crc_seg_map = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("JRQ_CRC_SEG_BYTES"))  // rounded up to 256 B by the kernel
     e->crc_seg_bytes = std::strtoull(v, nullptr, 10);

@@ -12,13 +12,14 @@ namespace jrq {
 constexpr uint64_t kCrcPoly = 0x42F0E1EBA9EA3693ULL;
 
 // Device copies of the constant tables (written once by jrq_create):
-//   slice[4][256]  "reversed-domain" slice tables R0..R3, see crc64.hip
+//   slice[8][256]  "reversed-domain" slice tables R0..R7, see crc64.hip
 //   shift[kShiftTables][8][256]  multiply-by-x^(8*2^t) mod P byte tables
 constexpr int kShiftTables = 48;  // shifts up to 2^48 - 1 bytes
 
-// LDS image of the four slice tables, 16 replicas, two tables per 16-B slot:
-// byte address = (k>>1)<<16 | index<<8 | (lane&15)<<4 | (k&1)<<3 (128 KiB, crc64.hip Tab4).
-constexpr int kCrcLdsBytes = 4 * 256 * 16 * 8;
+// LDS image of the slice tables (128 KiB): 8 tables x 8 replicas (crc64.hip Tab8), or the
+// first 4 tables x 16 replicas (Tab4, design probes).
+constexpr int kSliceTables = 8;
+constexpr int kCrcLdsBytes = 8 * 256 * 8 * 8;
 constexpr int kCrcBlock = 1024;  // threads per workgroup (16 waves, 1 workgroup / CU)
 
 // Status flags, identical to include/jrq.h jrq_group_status.
@@ -47,7 +48,7 @@ struct JrqCrcArgs {
   const uint8_t* has;
   uint8_t* corrupt;
   // engine constants / scratch
-  const uint64_t* slice;   // [4][256] reversed-domain slice tables R0..R3
+  const uint64_t* slice;   // [8][256] reversed-domain slice tables R0..R7
   const uint64_t* shift;   // [kShiftTables][8][256]
   uint64_t* acc;           // straddler accumulators, zero between launches
   uint32_t* cnt;           // straddler arrival counters, zero between launches
@@ -59,6 +60,7 @@ struct JrqCrcArgs {
   uint64_t* timeline;      // nullable diagnostics (tools/crc_timeline.hip): per wave
                            // {start, end (s_memrealtime), HW_ID, XCC_ID}
   uint64_t seg_bytes;      // nonzero: segment size (rounded up to 256 B; tests / tuning)
+  uint32_t prio_steps;     // 1: waves lower their priority as they progress (crc64.hip)
 };
 
 // Leader lease / alive-quorum check (quorum.hip, lease kernel).

@@ -5,7 +5,7 @@
 // (s_memrealtime, 100 MHz) by XCC, plus the spread of start times: shows whether every
 // workgroup runs concurrently and how evenly the waves finish.
 //   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/crc_timeline tools/crc_timeline.hip
-//   run:   tools/crc_timeline [grid] [seg_bytes] [seg_map]
+//   run:   tools/crc_timeline [grid] [seg_bytes] [seg_map] [prio_steps]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -44,16 +44,16 @@ int main(int argc, char** argv) {
   const uint32_t n = 64 << 10, L = 16 << 10;
   const uint64_t total = (uint64_t)n * L;
   // tables (engine.hip build_tables): slice R_j = bswap(T_j); shift[t][k][i]
-  uint64_t t[4][256], T0[256];
+  uint64_t t[8][256], T0[256];
   for (int i = 0; i < 256; ++i) {
     uint64_t c = (uint64_t)i << 56;
     for (int k = 0; k < 8; ++k) c = (c & 0x8000000000000000ULL) ? (c << 1) ^ jrq::kCrcPoly : (c << 1);
     t[0][i] = T0[i] = c;
   }
-  for (int j = 1; j < 4; ++j)
+  for (int j = 1; j < 8; ++j)
     for (int i = 0; i < 256; ++i) t[j][i] = t[0][t[j - 1][i] >> 56] ^ (t[j - 1][i] << 8);
-  std::vector<uint64_t> slice(4 * 256), shift((size_t)jrq::kShiftTables * 8 * 256);
-  for (int j = 0; j < 4; ++j)
+  std::vector<uint64_t> slice(8 * 256), shift((size_t)jrq::kShiftTables * 8 * 256);
+  for (int j = 0; j < 8; ++j)
     for (int i = 0; i < 256; ++i) slice[j * 256 + i] = __builtin_bswap64(t[j][i]);
   uint64_t K = 0x100;
   for (int tt = 0; tt < jrq::kShiftTables; ++tt) {
@@ -104,6 +104,7 @@ int main(int argc, char** argv) {
   a.seg_bytes = seg_bytes;
   a.seg_map = seg_map;
   a.timeline = d_tl;
+  a.prio_steps = argc > 4 ? std::atoi(argv[4]) : 1;
   hipEvent_t ev0, ev1;
   CK(hipEventCreate(&ev0));
   CK(hipEventCreate(&ev1));
@@ -154,6 +155,31 @@ int main(int argc, char** argv) {
     std::printf("xcc %d: waves %zu cus %zu  start %.1f..%.1f  end %.1f..%.1f  mean dur %.1f us\n",
                 kv.first, kv.second.size(), cus.size(), s_lo, s_hi, e_lo, e_hi,
                 dur / kv.second.size());
+  }
+  // within-workgroup vs across-workgroup spread of wave end times; per-SIMD order
+  {
+    const int wpb = jrq::kCrcBlock / 64;
+    double in_spread = 0, wg_lo = 1e18, wg_hi = 0;
+    std::vector<double> simd_mean(4, 0.0), slot_mean(wpb, 0.0);
+    for (int b = 0; b < grid; ++b) {
+      double lo = 1e18, hi = 0, mean = 0;
+      for (int v = 0; v < wpb; ++v) {
+        const size_t w = (size_t)b * wpb + v;
+        const double e = (tl[4 * w + 1] - s_min) / 100.0;
+        lo = std::min(lo, e); hi = std::max(hi, e); mean += e / wpb;
+        simd_mean[(tl[4 * w + 2] >> 4) & 3] += e / (grid * (double)wpb / 4);
+        slot_mean[v] += e / grid;
+      }
+      in_spread += (hi - lo) / grid;
+      wg_lo = std::min(wg_lo, mean); wg_hi = std::max(wg_hi, mean);
+    }
+    std::printf("wave end: mean within-WG spread %.1f us; WG mean end %.1f..%.1f us\n", in_spread,
+                wg_lo, wg_hi);
+    std::printf("mean end by SIMD:");
+    for (double m : simd_mean) std::printf(" %.1f", m);
+    std::printf("\nmean end by wave slot:");
+    for (double m : slot_mean) std::printf(" %.0f", m);
+    std::printf("\n");
   }
   // histogram of wave start times (us, 10 bins)
   std::vector<int> hist(10, 0);
