@@ -22,12 +22,11 @@
 //    no selects) hands every lane its own 4 pieces.  Half-rounds run through a 3-deep
 //    register ring; buffer loads with a per-wave descriptor clamp reads past the data to 0.
 //  * Table CRC in the "reversed domain" r = bswap64(crc): a little-endian load XORs straight
-//    into r, and 4 bytes are one step  r = (r >> 32) ^ R3[b0] ^ R2[b1] ^ R1[b2] ^ R0[b3],
-//    R_j = bswap(T_j), T_j[i] = i * x^(64 + 8j) mod P.  The tables live in LDS, replicated 16x
-//    with two tables sharing each 16-B slot; lanes 16-31 (and 48-63) visit each pair of tables
-//    in the opposite order, so lanes l and l+16 always read opposite halves of a slot: every
-//    ds_read_b64 is bank-conflict free.  An LDS address is one v_perm of a data byte and a
-//    per-lane constant (plus one v_perm per 4 bytes for the swapped lanes' byte order).
+//    into r, and 8 bytes are one step  r = R7[b0] ^ R6[b1] ^ ... ^ R0[b7] (slice-by-8, Tab8;
+//    Tab4 is the slice-by-4 flavour kept for the design probes), R_j = bswap(T_j),
+//    T_j[i] = i * x^(64 + 8j) mod P.  The tables live in LDS, replicated 8x, and the 4 lanes
+//    sharing a replica visit its tables in 4 rotations, so every ds_read_b64 is bank-conflict
+//    free.  An LDS address is one v_perm of a data byte and a per-lane constant.
 //  * Entry boundaries are events: a round that lies inside one entry is hashed from the
 //    registers; a round holding a boundary or the data edge is finished from global memory
 //    (L2-hot) byte/16-B wise, then the entry is emitted (or its piece handed off).
@@ -532,9 +531,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     const uint32_t whi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wptr >> 32));
     const uint32_t nr = __builtin_amdgcn_readfirstlane(
         static_cast<uint32_t>(nrec > 0x7FFFFFFFull ? 0x7FFFFFFFull : nrec));
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<uint8_t*>((static_cast<uint64_t>(whi) << 32) | wlo),
-        static_cast<short>(0), static_cast<int>(nr), 0x00020000);
 
     // Ring of three half-rounds (64 B per lane each, 16 VGPRs): two in flight while one is
     // hashed.  Half-round h: load q reads 16 B of owner lane 16q + c at segment offset
@@ -551,7 +547,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     const uint32_t qa0 = qbase, qa1 = qbase + 16u * WS, qa2 = qbase + 32u * WS,
                    qa3 = qbase + 48u * WS;
     const uint64_t wptr_u = (static_cast<uint64_t>(whi) << 32) | wlo;
-#define JRQ_LOAD_HALF(H, RS, hh)                                                         \
+#define JRQ_LOAD_HALF(H, hh)                                                             \
   do {                                                                                   \
     const uint32_t ho = __builtin_amdgcn_readfirstlane((hh) * 64u);                      \
     const uint64_t hp = wptr_u + ho;                                                     \
@@ -578,8 +574,8 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     // compiler still counts as in flight when the ring starts costs a vmcnt(0) at the top
     // of every ring iteration
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    JRQ_LOAD_HALF(h0, rs, 0u);
-    JRQ_LOAD_HALF(h1, rs, 1u);
+    JRQ_LOAD_HALF(h0, 0u);
+    JRQ_LOAD_HALF(h1, 1u);
 
     // one half-round of this lane: segment bytes [hs, hs + 64)
     auto process = [&](uint32_t hh, const u32x4 (&v)[4]) {
@@ -618,7 +614,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
 
 #if JRQ_CRC_RING == 4
     // 4-slot ring: three half-rounds in flight while one is hashed
-    JRQ_LOAD_HALF(h2, rs, last_half(2u));
+    JRQ_LOAD_HALF(h2, last_half(2u));
     for (uint32_t hh0 = 0; hh0 < halves; hh0 += 4) {
       const uint32_t hh = __builtin_amdgcn_readfirstlane(hh0);  // keep the counter in SGPRs
       if (a.prio_steps) {  // wave-uniform: lower this wave's priority as it gets ahead
@@ -632,19 +628,19 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
           else __builtin_amdgcn_s_setprio(0);
         }
       }
-      JRQ_LOAD_HALF(h3, rs, last_half(hh + 3));
+      JRQ_LOAD_HALF(h3, last_half(hh + 3));
       transpose_half(h0);
       process(hh, h0);
       if (hh + 1 >= halves) break;  // wave-uniform
-      JRQ_LOAD_HALF(h0, rs, last_half(hh + 4));
+      JRQ_LOAD_HALF(h0, last_half(hh + 4));
       transpose_half(h1);
       process(hh + 1, h1);
       if (hh + 2 >= halves) break;
-      JRQ_LOAD_HALF(h1, rs, last_half(hh + 5));
+      JRQ_LOAD_HALF(h1, last_half(hh + 5));
       transpose_half(h2);
       process(hh + 2, h2);
       if (hh + 3 >= halves) break;
-      JRQ_LOAD_HALF(h2, rs, last_half(hh + 6));
+      JRQ_LOAD_HALF(h2, last_half(hh + 6));
       transpose_half(h3);
       process(hh + 3, h3);
     }
@@ -662,15 +658,15 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
           else __builtin_amdgcn_s_setprio(0);
         }
       }
-      JRQ_LOAD_HALF(h2, rs, last_half(hh + 2));
+      JRQ_LOAD_HALF(h2, last_half(hh + 2));
       transpose_half(h0);
       process(hh, h0);
       if (hh + 1 >= halves) break;  // wave-uniform
-      JRQ_LOAD_HALF(h0, rs, last_half(hh + 3));
+      JRQ_LOAD_HALF(h0, last_half(hh + 3));
       transpose_half(h1);
       process(hh + 1, h1);
       if (hh + 2 >= halves) break;
-      JRQ_LOAD_HALF(h1, rs, last_half(hh + 4));
+      JRQ_LOAD_HALF(h1, last_half(hh + 4));
       transpose_half(h2);
       process(hh + 2, h2);
     }

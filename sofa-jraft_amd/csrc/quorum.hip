@@ -127,36 +127,66 @@ __global__ __launch_bounds__(256) void quorum_epoch_kernel(JrqQuorumArgs a) {
   }
 }
 
+typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__device__ __forceinline__ i64x2 ld2(const int64_t* p) {
+  const i64x2* q = reinterpret_cast<const i64x2*>(p);
+  if (NT) return __builtin_nontemporal_load(q);
+  return *q;
+}
+
 // Fast path (no run table, 16-B aligned arrays, even match_ld): one lane decides two
-// adjacent groups; every stream is read with 16-byte loads (1 KiB per wave instruction)
-// and the two status bytes are stored as one 16-bit word.
-template <int P>
+// adjacent groups per unit; every stream is read with 16-byte loads (1 KiB per wave
+// instruction) and the two status bytes are stored as one 16-bit word.  A lane takes U
+// units 256 pairs apart (its workgroup's block of 256*U pairs) and issues every load of
+// all U units before the first decision; NT marks the streams non-temporal (read once,
+// never re-read: no point keeping them in L2 / MALL).
+template <int P, int U, bool NT>
 __global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
   const uint32_t pairs = a.G >> 1;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < pairs; t += stride) {
-    const uint32_t g = t << 1;
-    const longlong2 pi = *reinterpret_cast<const longlong2*>(a.pending_index + g);
-    const longlong2 lc = *reinterpret_cast<const longlong2*>(a.last_committed + g);
-    const longlong2 la = *reinterpret_cast<const longlong2*>(a.last_appended + g);
-    const ulonglong2 cw = *reinterpret_cast<const ulonglong2*>(a.conf + g);
-    int64_t m0[P], m1[P];
+  const uint32_t step = gridDim.x * 256u * U;
+  for (uint32_t t0 = blockIdx.x * 256u * U + threadIdx.x; t0 < pairs; t0 += step) {
+    i64x2 pi[U], lc[U], la[U], cw[U], m[U][P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) {
-      const longlong2 v =
-          *reinterpret_cast<const longlong2*>(a.match + static_cast<size_t>(p) * a.match_ld + g);
-      m0[p] = v.x;
-      m1[p] = v.y;
+    for (int u = 0; u < U; ++u) {
+      const uint32_t t = t0 + 256u * u;
+      if (t >= pairs) continue;
+      const uint32_t g = t << 1;
+      pi[u] = ld2<NT>(a.pending_index + g);
+      lc[u] = ld2<NT>(a.last_committed + g);
+      la[u] = ld2<NT>(a.last_appended + g);
+      cw[u] = ld2<NT>(reinterpret_cast<const int64_t*>(a.conf) + g);
+#pragma unroll
+      for (int p = 0; p < P; ++p) m[u][p] = ld2<NT>(a.match + static_cast<size_t>(p) * a.match_ld + g);
     }
-    int64_t o0, o1;
-    uint8_t s0, s1;
-    decide_single<P>(pi.x, la.x, lc.x, cw.x, m0, o0, s0);
-    decide_single<P>(pi.y, la.y, lc.y, cw.y, m1, o1, s1);
-    longlong2 out;
-    out.x = o0;
-    out.y = o1;
-    *reinterpret_cast<longlong2*>(a.committed + g) = out;
-    *reinterpret_cast<uint16_t*>(a.status + g) = static_cast<uint16_t>(s0 | (s1 << 8));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t t = t0 + 256u * u;
+      if (t >= pairs) continue;
+      const uint32_t g = t << 1;
+      int64_t m0[P], m1[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        m0[p] = m[u][p].x;
+        m1[p] = m[u][p].y;
+      }
+      int64_t o0, o1;
+      uint8_t s0, s1;
+      decide_single<P>(pi[u].x, la[u].x, lc[u].x, static_cast<uint64_t>(cw[u].x), m0, o0, s0);
+      decide_single<P>(pi[u].y, la[u].y, lc[u].y, static_cast<uint64_t>(cw[u].y), m1, o1, s1);
+      i64x2 out;
+      out.x = o0;
+      out.y = o1;
+      const uint16_t st = static_cast<uint16_t>(s0 | (s1 << 8));
+      if (NT) {
+        __builtin_nontemporal_store(out, reinterpret_cast<i64x2*>(a.committed + g));
+        __builtin_nontemporal_store(st, reinterpret_cast<uint16_t*>(a.status + g));
+      } else {
+        *reinterpret_cast<i64x2*>(a.committed + g) = out;
+        *reinterpret_cast<uint16_t*>(a.status + g) = st;
+      }
+    }
   }
   // odd G: the last group goes through the scalar decision
   if ((a.G & 1u) && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -206,8 +236,9 @@ __global__ __launch_bounds__(256) void lease_check_kernel(JrqLeaseArgs a) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G; g += stride) {
     int64_t ts[P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) ts[p] = a.last_rpc_ts[static_cast<size_t>(p) * a.ld + g];
-    const uint64_t cw = a.conf[g];
+    for (int p = 0; p < P; ++p)
+      ts[p] = __builtin_nontemporal_load(a.last_rpc_ts + static_cast<size_t>(p) * a.ld + g);
+    const uint64_t cw = __builtin_nontemporal_load(a.conf + g);
     const uint32_t self = a.self_slot[g];
     int64_t lead = a.lease_start[g];
     uint16_t dead = 0;
@@ -265,18 +296,36 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
                     al16(a.pending_index) && al16(a.last_appended) && al16(a.last_committed) &&
                     al16(a.conf) && al16(a.committed) &&
                     (reinterpret_cast<uintptr_t>(a.status) & 1u) == 0 && a.G >= 2;
-  // enough 256-thread blocks for one lane per group (pair: per two), at most 8 per CU
-  const uint64_t lanes = pair ? (a.G >> 1) : a.G;
+  // pair-kernel variant (A/B knob JRQ_Q_VARIANT): 0 = 1 unit/lane, 1 = 1 unit/lane with
+  // non-temporal streams (default: 4.96 vs 4.58-4.74 TB/s on C3), 2 = 2 units/lane,
+  // 3 = 2 units/lane non-temporal
+  static const int variant = [] {
+    const char* v = std::getenv("JRQ_Q_VARIANT");
+    return v ? std::atoi(v) : 1;
+  }();
+  const int units = (variant == 2 || variant == 3) ? 2 : 1;
+  // enough 256-thread blocks for one lane per group (pair: per two per unit), at most 8 per CU
+  const uint64_t lanes = pair ? ((a.G >> 1) + units - 1) / units : a.G;
   const uint64_t need = (lanes + 255) / 256;
   const uint64_t cap = static_cast<uint64_t>(num_cus) * 8;
   const int grid = static_cast<int>(need < cap ? (need ? need : 1) : cap);
   switch (args->num_peers) {
 #define JRQ_CASE(P)                                                                            \
   case P:                                                                                      \
-    if (pair)                                                                                  \
-      hipLaunchKernelGGL(jrq::quorum_epoch_pair_kernel<P>, dim3(grid), blk, 0, stream, *args); \
-    else                                                                                       \
+    if (!pair)                                                                                 \
       hipLaunchKernelGGL(jrq::quorum_epoch_kernel<P>, dim3(grid), blk, 0, stream, *args);      \
+    else if (variant == 0)                                                                     \
+      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, 1, false>), dim3(grid), blk, 0,    \
+                         stream, *args);                                                       \
+    else if (variant == 2)                                                                     \
+      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, 2, false>), dim3(grid), blk, 0,    \
+                         stream, *args);                                                       \
+    else if (variant == 3)                                                                     \
+      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, 2, true>), dim3(grid), blk, 0,     \
+                         stream, *args);                                                       \
+    else                                                                                       \
+      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, 1, true>), dim3(grid), blk, 0,     \
+                         stream, *args);                                                       \
     break;
     JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
     JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
