@@ -419,6 +419,61 @@ def main():
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": lb / (lease_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS}}
 
+    # commit fan-out (FSMCaller.doCommitted / ClosureQueue.popClosureUntil) of the C3 epochs:
+    # each epoch's committed[] feeds the fan-out of its groups; every launch starts from
+    # fresh closure queues (restored outside the timed event pair)
+    fan_sets = []
+    for t in epochs:
+        c = torch.empty(G, dtype=torch.int64, device=dev)
+        eng.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
+                             t["last_committed"], t["conf"], c, status)
+        cq_size0 = t["last_appended"] - t["pending_index"] + 1
+        fan_sets.append({"prev": t["last_committed"], "c": c, "la": t["last_committed"],
+                         "cf0": t["pending_index"], "cs0": cq_size0,
+                         "cf": torch.empty_like(c), "cs": torch.empty_like(c)})
+    fan_fc = torch.empty(G, dtype=torch.int64, device=dev)
+    fan_st = torch.empty(G, dtype=torch.uint8, device=dev)
+    fan_list = torch.empty(G, dtype=torch.int32, device=dev)
+    fan_num = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def fan_restore():
+        for f in fan_sets:
+            f["cf"].copy_(f["cf0"])
+            f["cs"].copy_(f["cs0"])
+
+    def fan_launch(f):
+        eng.commit_fanout_dev(f["prev"], f["c"], f["la"], f["cf"], f["cs"], fan_fc, fan_st,
+                              fan_list, fan_num)
+
+    fan_restore()
+    fan_launch(fan_sets[0])
+    sync()
+    n_listed = int(fan_num.item())
+    n_pop = int((fan_sets[0]["cf"] != fan_sets[0]["cf0"]).sum().item())
+    fan_ms = []
+    for rep in range(max(1, args.warmup) + max(1, args.steps // 4)):
+        fan_restore()
+        sync()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for f in fan_sets:
+            fan_launch(f)
+        e1.record(stream)
+        sync()
+        if rep >= max(1, args.warmup):
+            fan_ms.append(e0.elapsed_time(e1) / len(fan_sets))
+    fan_avg = float(np.mean(fan_ms))
+    # reads prev/committed/lastApplied/cqFirst/cqSize 40 B, writes firstClosure 8 + status 1,
+    # compaction re-reads status 1; + 16 B queue write-back per popping group, 4 B per listed id
+    fb = 50 * G + 16 * n_pop + 4 * n_listed
+    extras["commit_fanout"] = {
+        "workload": f"{G} groups (C3 epoch output) -> doCommitted/popClosureUntil, "
+                    f"{n_listed} listed, {n_pop} popping",
+        "groups_per_s": G / (fan_avg * 1e-3), "ms_per_launch": fan_avg,
+        "roofline": {"bound": "hbm", "achieved": fb / (fan_avg * 1e-3) / 1e9,
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": fb / (fan_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS}}
+
     # ------------------------------------------------ measured HBM ceiling --
     # device-to-device copy of 2 GiB (torch's copy kernel): read + write bytes / time, the
     # "peak_measured" of SURVEY.md §8d (frac stays against the 8 TB/s spec)

@@ -219,6 +219,40 @@ int jrq_lease_check(jrq_engine *e, const int64_t *last_rpc_ts, uint64_t ld, uint
                     int64_t lease_timeout_ms, uint8_t *ok_out, int64_t *lease_start_inout,
                     uint16_t *dead_out);
 
+/* ------------------------------------------------------- commit fan-out -- */
+
+/* What each group's FSMCaller does with the epoch's commit, for G groups:
+ * BallotBox.commitAt -> onCommitted(committed) (JC/core/BallotBox.java:131-137) ->
+ * FSMCallerImpl.doCommitted (JC/core/FSMCallerImpl.java:462-482) ->
+ * ClosureQueueImpl.popClosureUntil (JC/closure/ClosureQueueImpl.java:113-142).
+ *   prev_committed[g]  lastCommittedIndex before the epoch (the quorum epoch's input)
+ *   committed[g]       after the epoch (the quorum epoch's output)
+ *   last_applied[g]    FSMCaller lastAppliedIndex
+ *   cq_first/cq_size   the group's ClosureQueue (firstIndex, number of queued closures),
+ *                      updated in place by the pop
+ * Out: status_out[g] (jrq_fanout_status); first_closure_out[g] = popClosureUntil's return
+ * for APPLY (the log index of the first popped closure, or committed+1 when none is popped),
+ * -1 for INVALID, 0 otherwise; listed_out[0..*num_listed_out) = the APPLY and INVALID group
+ * ids in ascending order -- the groups whose state machine must apply
+ * (last_applied, committed] (or fail with "Invalid firstClosureIndex"). */
+typedef enum {
+    JRQ_FAN_NONE = 0,    /* commit did not move: no onCommitted */
+    JRQ_FAN_APPLY = 1,   /* doCommitted pops closures (maybe none) and applies entries */
+    JRQ_FAN_SKIP = 2,    /* lastAppliedIndex >= committed: doCommitted returns at once */
+    JRQ_FAN_INVALID = 3  /* committed beyond the closure queue: popClosureUntil returns -1 */
+} jrq_fanout_status;
+
+int jrq_commit_fanout_dev(jrq_engine *e, uint32_t G, const int64_t *prev_committed_dev,
+                          const int64_t *committed_dev, const int64_t *last_applied_dev,
+                          int64_t *cq_first_inout_dev, int64_t *cq_size_inout_dev,
+                          int64_t *first_closure_out_dev, uint8_t *status_out_dev,
+                          uint32_t *listed_out_dev, uint32_t *num_listed_out_dev);
+int jrq_commit_fanout(jrq_engine *e, uint32_t G, const int64_t *prev_committed,
+                      const int64_t *committed, const int64_t *last_applied,
+                      int64_t *cq_first_inout, int64_t *cq_size_inout,
+                      int64_t *first_closure_out, uint8_t *status_out, uint32_t *listed_out,
+                      uint32_t *num_listed_out);
+
 /* --------------------------------------------------- node-wide publication -- */
 
 /* Multi-GPU (one process per GPU): groups are sharded by contiguous groupId blocks.

@@ -464,3 +464,75 @@ int64_t jo_quorum_epoch_replay(uint32_t G, uint32_t P, const int64_t *match, con
     jo_bb_free(bb);
     return grants;
 }
+
+
+/* ---------------- commit fan-out (ClosureQueueImpl, FSMCallerImpl) -------- */
+
+/* ClosureQueueImpl (JC/closure/ClosureQueueImpl.java:45-142) with closures as the log index
+ * they were appended for (a LinkedList in the reference; a ring of ids here). */
+typedef struct {
+    int64_t first_index;
+    int64_t *ids;
+    int64_t head, size;
+} jo_closure_queue;
+
+/* popClosureUntil(endIndex, closures) (:113-142); returns the first index or endIndex+1 / -1,
+ * and the number popped in *popped. */
+static int64_t jo_cq_pop_until(jo_closure_queue *q, int64_t end_index, int64_t *popped) {
+    *popped = 0;
+    const int64_t queue_size = q->size;
+    if (queue_size == 0 || end_index < q->first_index) return end_index + 1;
+    if (end_index > q->first_index + queue_size - 1) return -1; /* LOG.error + return -1 */
+    const int64_t out_first = q->first_index;
+    for (int64_t i = out_first; i <= end_index; i++) { /* queue.pollFirst() per index */
+        (void)q->ids[q->head];
+        q->head++;
+        q->size--;
+        (*popped)++;
+    }
+    q->first_index = end_index + 1;
+    return out_first;
+}
+
+int64_t jo_commit_fanout_replay(uint32_t G, const uint64_t *seq_off, const int64_t *seq,
+                                int64_t *last_applied, int64_t *cq_first, int64_t *cq_size,
+                                int64_t *first_closure, uint8_t *status) {
+    int64_t total = 0;
+    for (uint32_t g = 0; g < G; g++) {
+        jo_closure_queue q;
+        q.first_index = cq_first[g];
+        q.head = 0;
+        q.size = cq_size[g];
+        q.ids = (int64_t *)malloc((size_t)(q.size > 0 ? q.size : 1) * sizeof(int64_t));
+        for (int64_t i = 0; i < q.size; i++) q.ids[i] = q.first_index + i; /* appendPendingClosure */
+        uint8_t st = seq_off[g] == seq_off[g + 1] ? JO_FAN_NONE : JO_FAN_SKIP;
+        int64_t first = 0, first_pop = 0, last_c = 0;
+        int have_first = 0;
+        for (uint64_t k = seq_off[g]; k < seq_off[g + 1]; k++) {
+            const int64_t c = seq[k]; /* FSMCallerImpl.doCommitted(c) */
+            if (last_applied[g] >= c) continue; /* :466-470 */
+            int64_t popped;
+            const int64_t r = jo_cq_pop_until(&q, c, &popped);
+            if (r < 0) { /* Requires.requireTrue(firstClosureIndex >= 0) throws (:480) */
+                st = JO_FAN_INVALID;
+                break;
+            }
+            total += popped;
+            if (popped > 0 && !have_first) {
+                first_pop = r;
+                have_first = 1;
+            }
+            last_c = c;
+            st = JO_FAN_APPLY;
+            last_applied[g] = c; /* setLastApplied after the iterator ran to c */
+        }
+        if (st == JO_FAN_APPLY) first = have_first ? first_pop : last_c + 1;
+        else if (st == JO_FAN_INVALID) first = -1;
+        first_closure[g] = first;
+        status[g] = st;
+        cq_first[g] = q.first_index;
+        cq_size[g] = q.size;
+        free(q.ids);
+    }
+    return total;
+}

@@ -161,6 +161,25 @@ int64_t jo_quorum_epoch_replay(uint32_t G, uint32_t P, const int64_t *match /* [
                                const uint64_t *run_conf, int64_t chunk,
                                int64_t *committed_out, uint8_t *status_out);
 
+/* ---------------- commit fan-out (ClosureQueueImpl, FSMCallerImpl) -------- */
+enum { JO_FAN_NONE = 0, JO_FAN_APPLY = 1, JO_FAN_SKIP = 2, JO_FAN_INVALID = 3 };
+/*
+ * Per group g: a ClosureQueue holding cq_size[g] closures for log indices cq_first[g]..
+ * (resetFirstIndex + appendPendingClosure, JC/closure/ClosureQueueImpl.java:83-105), then
+ * the epoch's onCommitted calls seq[seq_off[g] .. seq_off[g+1]) (increasing, as BallotBox
+ * emits them), each run through FSMCallerImpl.doCommitted (JC/core/FSMCallerImpl.java:
+ * 462-482: skip if lastAppliedIndex >= c; popClosureUntil(c), :113-142; a -1 return fails
+ * Requires.requireTrue and the call ends; else entries up to c are applied and
+ * lastAppliedIndex = c).  Outputs per group: status (NONE: no call; INVALID: some pop
+ * returned -1; APPLY: some call popped/applied; SKIP otherwise), first_closure = index of
+ * the first closure popped during the epoch, or (last call's c)+1 when none was popped
+ * (-1 for INVALID, 0 for NONE/SKIP); cq_first/cq_size/last_applied updated in place.
+ * Returns the number of closures popped in total.
+ */
+int64_t jo_commit_fanout_replay(uint32_t G, const uint64_t *seq_off, const int64_t *seq,
+                                int64_t *last_applied, int64_t *cq_first, int64_t *cq_size,
+                                int64_t *first_closure, uint8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

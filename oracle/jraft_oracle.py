@@ -92,6 +92,8 @@ def lib():
         L.jo_quorum_epoch_replay.argtypes = [C.c_uint32, C.c_uint32, _i64p, _i64p, _i64p, _i64p,
                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_int64, _i64p, _u8p]
+        L.jo_commit_fanout_replay.restype = C.c_int64
+        L.jo_commit_fanout_replay.argtypes = [C.c_uint32] + [C.c_void_p] * 7
         _lib = L
     return _lib
 
@@ -195,6 +197,28 @@ def lease_check(last_rpc_ts, conf, self_slot, now_ms, lease_timeout_ms, lease_st
     lib().jo_lease_check(G, P, _ptr(ts), _ptr(conf), _ptr(ss), now_ms, lease_timeout_ms,
                          _ptr(ok), _ptr(lead), _ptr(dead))
     return ok, lead, dead
+
+
+FAN_NONE, FAN_APPLY, FAN_SKIP, FAN_INVALID = 0, 1, 2, 3
+
+
+def commit_fanout_replay(seq_off, seq, last_applied, cq_first, cq_size):
+    """FSMCallerImpl.doCommitted per onCommitted call (FSMCallerImpl.java:462-482) over a
+    ClosureQueueImpl (ClosureQueueImpl.java:113-142), call by call.  Returns
+    (status u8[G], first_closure i64[G], last_applied, cq_first, cq_size, popped_total)."""
+    so = np.ascontiguousarray(seq_off, np.uint64)
+    G = len(so) - 1
+    sq = np.ascontiguousarray(seq, np.int64)
+    if sq.size == 0:
+        sq = np.zeros(1, np.int64)
+    la = np.array(last_applied, dtype=np.int64, copy=True)
+    cf = np.array(cq_first, dtype=np.int64, copy=True)
+    cs = np.array(cq_size, dtype=np.int64, copy=True)
+    fc = np.zeros(G, np.int64)
+    st = np.zeros(G, np.uint8)
+    n = lib().jo_commit_fanout_replay(G, _ptr(so), _ptr(sq), _ptr(la), _ptr(cf), _ptr(cs),
+                                      _ptr(fc), _ptr(st))
+    return st, fc, la, cf, cs, int(n)
 
 
 # ------------------------------------------------- pure-Python cross-checks --

@@ -27,36 +27,6 @@ __device__ __forceinline__ uint64_t eff_len(const JrqAeArgs& a, uint32_t e) {
   return a.type[e] == 0 ? 0ull : static_cast<uint64_t>(a.data_len[e]);
 }
 
-// Block-wide exclusive scan of one value per thread (wave shuffles + LDS).
-__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* lds_warp,
-                                                         uint64_t* total) {
-  using u64 = unsigned long long;  // the __shfl_* overloads take (unsigned) long long
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  u64 x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const u64 y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  if (lane == 63) lds_warp[wave] = x;
-  __syncthreads();
-  if (wave == 0) {
-    const int nw = blockDim.x >> 6;
-    u64 s = lane < nw ? lds_warp[lane] : 0;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const u64 y = __shfl_up(s, d, 64);
-      if (lane >= d) s += y;
-    }
-    if (lane < nw) lds_warp[lane] = s;  // inclusive wave totals
-  }
-  __syncthreads();
-  const uint64_t before = wave ? lds_warp[wave - 1] : 0;
-  *total = lds_warp[(blockDim.x >> 6) - 1];
-  __syncthreads();
-  return before + x - v;
-}
-
 // Phase 1: per-tile sums of effective lengths.
 __global__ __launch_bounds__(kScanBlock) void ae_block_sums(JrqAeArgs a) {
   __shared__ uint64_t w[kScanBlock / 64];

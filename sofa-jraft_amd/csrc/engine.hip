@@ -23,6 +23,7 @@ extern "C" hipError_t jrq_launch_crc64(JrqCrcArgs* args, int log_entry, int grid
 extern "C" hipError_t jrq_launch_quorum(const JrqQuorumArgs* args, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_meta(const JrqAeArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_lease(const JrqLeaseArgs* a, int num_cus, hipStream_t stream);
+extern "C" hipError_t jrq_launch_fanout(const JrqFanoutArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_first_corrupt(const JrqAeArgs* a, hipStream_t stream);
 
 namespace {
@@ -55,7 +56,7 @@ struct jrq_engine {
   uint32_t crc_seg_map = 1;  // JRQ_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
-  DevBuf stage[24];  // 0-13 host-variant staging, 16-19 AppendEntries scratch
+  DevBuf stage[24];  // 0-13 host-variant staging, 16-19 AppendEntries scratch, 20 fan-out scratch
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = -1;
   std::string err;
@@ -634,6 +635,85 @@ int jrq_append_entries_verify(jrq_engine* e, uint32_t R, const uint32_t* req_off
   }
   JRQ_HIP(e, hipMemcpyAsync(first_corrupt_out, dfirst, static_cast<size_t>(R) * 4, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
+// ------------------------------------------------------ commit fan-out -----
+
+int jrq_commit_fanout_dev(jrq_engine* e, uint32_t G, const int64_t* prev_committed,
+                          const int64_t* committed, const int64_t* last_applied,
+                          int64_t* cq_first, int64_t* cq_size, int64_t* first_closure_out,
+                          uint8_t* status_out, uint32_t* listed_out, uint32_t* num_listed_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (!num_listed_out) return fail(e, JRQ_E_INVALID, "null num_listed_out");
+  if (G > 0 && (!prev_committed || !committed || !last_applied || !cq_first || !cq_size ||
+                !first_closure_out || !status_out || !listed_out))
+    return fail(e, JRQ_E_INVALID, "null fan-out array");
+  DeviceGuard guard(e->device);
+  if (G == 0) {
+    JRQ_HIP(e, hipMemsetAsync(num_listed_out, 0, 4, e->stream));
+    return JRQ_OK;
+  }
+  void* tiles;
+  int rc;
+  if ((rc = ensure_stage(e, 20, ((static_cast<size_t>(G) + 4095) / 4096) * 4, &tiles))) return rc;
+  JrqFanoutArgs a{};
+  a.G = G;
+  a.prev_committed = prev_committed;
+  a.committed = committed;
+  a.last_applied = last_applied;
+  a.cq_first = cq_first;
+  a.cq_size = cq_size;
+  a.first_closure = first_closure_out;
+  a.status = status_out;
+  a.listed = listed_out;
+  a.num_listed = num_listed_out;
+  a.tile_count = static_cast<uint32_t*>(tiles);
+  JRQ_HIP(e, jrq_launch_fanout(&a, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_commit_fanout(jrq_engine* e, uint32_t G, const int64_t* prev_committed,
+                      const int64_t* committed, const int64_t* last_applied, int64_t* cq_first,
+                      int64_t* cq_size, int64_t* first_closure_out, uint8_t* status_out,
+                      uint32_t* listed_out, uint32_t* num_listed_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (!num_listed_out) return fail(e, JRQ_E_INVALID, "null num_listed_out");
+  if (G == 0) {
+    *num_listed_out = 0;
+    return JRQ_OK;
+  }
+  if (!prev_committed || !committed || !last_applied || !cq_first || !cq_size ||
+      !first_closure_out || !status_out || !listed_out)
+    return fail(e, JRQ_E_INVALID, "null fan-out array");
+  DeviceGuard guard(e->device);
+  int rc;
+  const int64_t *dprev, *dcom, *dla, *dcf0, *dcs0;
+  if ((rc = stage_in(e, 0, prev_committed, G, &dprev))) return rc;
+  if ((rc = stage_in(e, 1, committed, G, &dcom))) return rc;
+  if ((rc = stage_in(e, 2, last_applied, G, &dla))) return rc;
+  if ((rc = stage_in(e, 3, cq_first, G, &dcf0))) return rc;
+  if ((rc = stage_in(e, 4, cq_size, G, &dcs0))) return rc;
+  void *dfc, *dst, *dlist, *dnum;
+  if ((rc = ensure_stage(e, 8, static_cast<size_t>(G) * 8, &dfc))) return rc;
+  if ((rc = ensure_stage(e, 9, G, &dst))) return rc;
+  if ((rc = ensure_stage(e, 12, static_cast<size_t>(G) * 4, &dlist))) return rc;
+  if ((rc = ensure_stage(e, 13, 16, &dnum))) return rc;
+  int64_t* dcf = const_cast<int64_t*>(dcf0);
+  int64_t* dcs = const_cast<int64_t*>(dcs0);
+  if ((rc = jrq_commit_fanout_dev(e, G, dprev, dcom, dla, dcf, dcs, static_cast<int64_t*>(dfc),
+                                  static_cast<uint8_t*>(dst), static_cast<uint32_t*>(dlist),
+                                  static_cast<uint32_t*>(dnum))))
+    return rc;
+  const size_t b8 = static_cast<size_t>(G) * 8;
+  JRQ_HIP(e, hipMemcpyAsync(cq_first, dcf, b8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(cq_size, dcs, b8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(first_closure_out, dfc, b8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(status_out, dst, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(num_listed_out, dnum, 4, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  if (*num_listed_out)
+    JRQ_HIP(e, hipMemcpy(listed_out, dlist, static_cast<size_t>(*num_listed_out) * 4, hipMemcpyDeviceToHost));
   return JRQ_OK;
 }
 

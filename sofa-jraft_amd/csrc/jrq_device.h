@@ -31,6 +31,36 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 
 __device__ __forceinline__ uint64_t bswap64(uint64_t v) { return __builtin_bswap64(v); }
 
+// Block-wide exclusive scan of one value per thread (wave shuffles + LDS).
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* lds_warp,
+                                                         uint64_t* total) {
+  using u64 = unsigned long long;  // the __shfl_* overloads take (unsigned) long long
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  u64 x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u64 y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) lds_warp[wave] = x;
+  __syncthreads();
+  if (wave == 0) {
+    const int nw = blockDim.x >> 6;
+    u64 s = lane < nw ? lds_warp[lane] : 0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const u64 y = __shfl_up(s, d, 64);
+      if (lane >= d) s += y;
+    }
+    if (lane < nw) lds_warp[lane] = s;  // inclusive wave totals
+  }
+  __syncthreads();
+  const uint64_t before = wave ? lds_warp[wave - 1] : 0;
+  *total = lds_warp[(blockDim.x >> 6) - 1];
+  __syncthreads();
+  return before + x - v;
+}
+
 }  // namespace jrq
 
 // Host-visible launch parameter blocks (plain structs, passed by value).
@@ -93,6 +123,21 @@ struct JrqAeArgs {
   uint64_t* tile_sums;             // scratch [ceil(n/4096)]
   const uint8_t* corrupt;          // [n] verify flags (from the checksum kernel)
   int32_t* first_corrupt;          // [r] out
+};
+
+// Commit fan-out after an epoch (commit_fanout.hip).
+struct JrqFanoutArgs {
+  uint32_t G;
+  const int64_t* prev_committed;  // [G] BallotBox.lastCommittedIndex before the epoch
+  const int64_t* committed;       // [G] after the epoch
+  const int64_t* last_applied;    // [G] FSMCaller.lastAppliedIndex
+  int64_t* cq_first;              // [G] ClosureQueue.firstIndex (in/out)
+  int64_t* cq_size;               // [G] ClosureQueue size (in/out)
+  int64_t* first_closure;         // [G] out: popClosureUntil result
+  uint8_t* status;                // [G] out: jrq_fanout_status
+  uint32_t* listed;               // [G] out: APPLY / INVALID group ids, ascending
+  uint32_t* num_listed;           // [1] out
+  uint32_t* tile_count;           // scratch [ceil(G/4096)]
 };
 
 struct JrqQuorumArgs {

@@ -227,6 +227,33 @@ class Engine:
             _dev_ptr(peer_xor), _dev_ptr(checksum), _dev_ptr(has_checksum), _dev_ptr(data),
             _dev_ptr(checksum_out), _dev_ptr(corrupt_out), _dev_ptr(first_corrupt_out)), self._h)
 
+    # ---------------------------------------------------------- commit fan-out --
+    def commit_fanout(self, prev_committed, committed, last_applied, cq_first, cq_size):
+        """Host variant: returns (status u8[G], first_closure i64[G], listed u32[n],
+        cq_first i64[G], cq_size i64[G]) -- FSMCallerImpl.doCommitted per group."""
+        prev = _c(prev_committed, np.int64)
+        com = _c(committed, np.int64)
+        la = _c(last_applied, np.int64)
+        G = len(com)
+        cf = np.array(cq_first, dtype=np.int64, copy=True)
+        cs = np.array(cq_size, dtype=np.int64, copy=True)
+        fc = np.zeros(G, np.int64)
+        st = np.zeros(G, np.uint8)
+        listed = np.zeros(max(G, 1), np.uint32)
+        num = np.zeros(1, np.uint32)
+        check(self._L.jrq_commit_fanout(self._h, G, _np_ptr(prev), _np_ptr(com), _np_ptr(la),
+                                        _np_ptr(cf), _np_ptr(cs), _np_ptr(fc), _np_ptr(st),
+                                        _np_ptr(listed), _np_ptr(num)), self._h)
+        return st, fc, listed[:int(num[0])].copy(), cf, cs
+
+    def commit_fanout_dev(self, prev_committed, committed, last_applied, cq_first, cq_size,
+                          first_closure_out, status_out, listed_out, num_listed_out):
+        check(self._L.jrq_commit_fanout_dev(
+            self._h, committed.shape[0], _dev_ptr(prev_committed), _dev_ptr(committed),
+            _dev_ptr(last_applied), _dev_ptr(cq_first), _dev_ptr(cq_size),
+            _dev_ptr(first_closure_out), _dev_ptr(status_out), _dev_ptr(listed_out),
+            _dev_ptr(num_listed_out)), self._h)
+
     # ---------------------------------------------------------------- RCCL --
     @staticmethod
     def rccl_unique_id() -> bytes:
