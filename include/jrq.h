@@ -253,6 +253,43 @@ int jrq_commit_fanout(jrq_engine *e, uint32_t G, const int64_t *prev_committed,
                       int64_t *first_closure_out, uint8_t *status_out, uint32_t *listed_out,
                       uint32_t *num_listed_out);
 
+/* ----------------------------------------- V2 decode + verify on read -- */
+
+/* Batched read-side decode of N stored V2 log entries and their checksum verify
+ * (SURVEY §8f #4): AutoDetectDecoder.decode (JC/entity/codec/AutoDetectDecoder.java:41-52)
+ * -> V2Decoder.decode (JC/entity/codec/v2/V2Decoder.java:46-110; PBLogEntry, log.proto:10-20,
+ * protobuf 3.5.1) -> LogEntry.isCorrupted (JC/entity/LogEntry.java:88-108,156-158), as
+ * LogManagerImpl checks every entry it reads (JC/core/LogManagerImpl.java:733-745).
+ *   records[offsets[r] .. offsets[r+1])  the stored bytes of entry r (any base/alignment)
+ * Out per record: status_out (jrq_v2_status); for JRQ_V2_OK: type (EntryType number), index,
+ * term, stored checksum + has_checksum, data_off (absolute into `records`) / data_len of the
+ * data field, peer_counts (nullable: peers | old_peers<<8 | learners<<16 | old_learners<<24,
+ * each saturating at 255), checksum_out = LogEntry.checksum() of the decoded entry and
+ * corrupt_out = isCorrupted().  Other statuses zero those fields (data_off = offsets[r]). */
+typedef enum {
+    JRQ_V2_OK = 0,
+    JRQ_V2_NULL = 1,  /* the reference decoder returns null (empty record, short header, bad
+                         magic/version, InvalidProtocolBufferException, missing required field) */
+    JRQ_V2_V1 = 2,    /* first byte is not the V2 magic: AutoDetectDecoder routes it to V1Decoder */
+    JRQ_V2_HOST = 3   /* decode on the host with the reference decoder: a peer string that is not
+                         PeerId.toString() of itself (re-rendered or rejected by getPeerId), or
+                         unknown-field groups nested deeper than 2 */
+} jrq_v2_status;
+
+int jrq_v2_decode_verify_dev(jrq_engine *e, const uint8_t *records_dev, const uint64_t *offsets_dev,
+                             uint32_t N, uint8_t *status_out_dev, uint8_t *type_out_dev,
+                             int64_t *index_out_dev, int64_t *term_out_dev,
+                             uint64_t *stored_checksum_out_dev, uint8_t *has_checksum_out_dev,
+                             uint64_t *data_off_out_dev, uint64_t *data_len_out_dev,
+                             uint32_t *peer_counts_out_dev, uint64_t *checksum_out_dev,
+                             uint8_t *corrupt_out_dev);
+int jrq_v2_decode_verify(jrq_engine *e, const uint8_t *records, const uint64_t *offsets, uint32_t N,
+                         uint8_t *status_out, uint8_t *type_out, int64_t *index_out,
+                         int64_t *term_out, uint64_t *stored_checksum_out,
+                         uint8_t *has_checksum_out, uint64_t *data_off_out,
+                         uint64_t *data_len_out, uint32_t *peer_counts_out,
+                         uint64_t *checksum_out, uint8_t *corrupt_out);
+
 /* --------------------------------------------------- node-wide publication -- */
 
 /* Multi-GPU (one process per GPU): groups are sharded by contiguous groupId blocks.

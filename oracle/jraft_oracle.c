@@ -536,3 +536,280 @@ int64_t jo_commit_fanout_replay(uint32_t G, const uint64_t *seq_off, const int64
     }
     return total;
 }
+
+/* ---------------- V2 log entry decode + verify (entity/codec/v2) ----------- */
+
+/* CodedInputStream over one record body (protobuf-java 3.5.1, the reference's pinned version,
+ * pom.xml:74; array-backed decoder semantics). */
+typedef struct {
+    const uint8_t *b;
+    int64_t pos, limit;
+    uint32_t last_tag;
+    int err; /* InvalidProtocolBufferException raised */
+} jo_cis;
+
+static uint8_t jo_cis_byte(jo_cis *in) {
+    if (in->pos >= in->limit) {
+        in->err = 1; /* truncatedMessage */
+        return 0;
+    }
+    return in->b[in->pos++];
+}
+
+/* readRawVarint32: 5 bytes of value; a 5th byte with its high bit set is followed by up to
+ * 5 discarded bytes; more -> malformedVarint. */
+static uint32_t jo_cis_varint32(jo_cis *in) {
+    uint32_t r = 0;
+    for (int i = 0; i < 5; i++) {
+        const uint8_t x = jo_cis_byte(in);
+        if (in->err) return 0;
+        r |= (uint32_t)(x & 0x7F) << (7 * i);
+        if (!(x & 0x80)) return r;
+    }
+    for (int i = 0; i < 5; i++) {
+        const uint8_t x = jo_cis_byte(in);
+        if (in->err) return 0;
+        if (!(x & 0x80)) return r;
+    }
+    in->err = 1;
+    return 0;
+}
+
+/* readRawVarint64: up to 10 bytes, bits past 64 dropped; an 11th byte -> malformedVarint. */
+static uint64_t jo_cis_varint64(jo_cis *in) {
+    uint64_t r = 0;
+    for (int shift = 0; shift < 64; shift += 7) {
+        const uint8_t x = jo_cis_byte(in);
+        if (in->err) return 0;
+        r |= (uint64_t)(x & 0x7F) << shift;
+        if (!(x & 0x80)) return r;
+    }
+    in->err = 1;
+    return 0;
+}
+
+/* readTag: 0 at the end of input; field number 0 -> invalidTag. */
+static uint32_t jo_cis_tag(jo_cis *in) {
+    if (in->pos >= in->limit) {
+        in->last_tag = 0;
+        return 0;
+    }
+    in->last_tag = jo_cis_varint32(in);
+    if (!in->err && (in->last_tag >> 3) == 0) in->err = 1;
+    return in->err ? 0 : in->last_tag;
+}
+
+/* length-delimited payload: returns its offset, *len its size */
+static int64_t jo_cis_bytes(jo_cis *in, int64_t *len) {
+    const int32_t size = (int32_t)jo_cis_varint32(in);
+    if (in->err) return 0;
+    if (size < 0 || size > in->limit - in->pos) { /* negativeSize / truncatedMessage */
+        in->err = 1;
+        return 0;
+    }
+    const int64_t at = in->pos;
+    in->pos += size;
+    *len = size;
+    return at;
+}
+
+static int jo_cis_skip_field(jo_cis *in, uint32_t tag, int depth);
+
+/* UnknownFieldSet.mergeFieldFrom for a START_GROUP: readGroup (recursion limit 100) until the
+ * matching END_GROUP tag. */
+static void jo_cis_skip_group(jo_cis *in, uint32_t field, int depth) {
+    if (depth + 1 >= 100) { /* recursionLimitExceeded */
+        in->err = 1;
+        return;
+    }
+    for (;;) {
+        const uint32_t t = jo_cis_tag(in);
+        if (in->err) return;
+        if (t == 0 || !jo_cis_skip_field(in, t, depth + 1)) break;
+        if (in->err) return;
+    }
+    if (in->last_tag != ((field << 3) | 4)) in->err = 1; /* checkLastTagWas(END_GROUP) */
+}
+
+/* skipField/mergeFieldFrom: 0 = END_GROUP seen (stop), 1 = skipped */
+static int jo_cis_skip_field(jo_cis *in, uint32_t tag, int depth) {
+    int64_t len;
+    switch (tag & 7) {
+    case 0: (void)jo_cis_varint64(in); return 1;
+    case 1: for (int i = 0; i < 8; i++) (void)jo_cis_byte(in); return 1;
+    case 2: (void)jo_cis_bytes(in, &len); return 1;
+    case 3: jo_cis_skip_group(in, tag >> 3, depth); return 1;
+    case 4: return 0;
+    case 5: for (int i = 0; i < 4; i++) (void)jo_cis_byte(in); return 1;
+    default: in->err = 1; return 1; /* invalidWireType */
+    }
+}
+
+static int jo_is_java_whitespace(uint8_t c) {
+    return c == ' ' || (c >= 0x09 && c <= 0x0D) || (c >= 0x1C && c <= 0x1F);
+}
+
+/* Integer.parseInt over latin-1 chars: optional sign, ASCII digits, int32 range. */
+static int jo_parse_int(const uint8_t *s, int64_t n, int32_t *out) {
+    int64_t i = 0, v = 0;
+    int neg = 0;
+    if (n == 0) return 0;
+    if (s[0] == '-' || s[0] == '+') {
+        neg = s[0] == '-';
+        i = 1;
+        if (n == 1) return 0;
+    }
+    for (; i < n; i++) {
+        if (s[i] < '0' || s[i] > '9') return 0;
+        v = v * 10 + (s[i] - '0');
+        if (v > 2147483648LL) return 0;
+    }
+    if (neg) v = -v;
+    if (v > 2147483647LL || v < -2147483648LL) return 0;
+    *out = (int32_t)v;
+    return 1;
+}
+
+/* JRaftUtils.getPeerId(AsciiStringUtil.unsafeDecode(bytes)).checksum()
+ * (JC/JRaftUtils.java:113-122, JC/entity/PeerId.java:60-65,135-171): blank -> the empty
+ * PeerId "0.0.0.0:0"; else StringUtils.split(s, ':') (empty tokens dropped), 2 or 3 tokens,
+ * Integer.parseInt port [and idx]; toString = ip ":" port [":" idx if idx != 0].
+ * *kind: 0 = the bytes are already the canonical toString, 1 = parsed but re-rendered
+ * differently, 2 = IllegalArgumentException ("Invalid peer str"). */
+uint64_t jo_v2_peer_checksum(const uint8_t *s, int64_t n, int *kind) {
+    int blank = 1;
+    for (int64_t i = 0; i < n; i++)
+        if (!jo_is_java_whitespace(s[i])) blank = 0;
+    char buf[1024];
+    int len;
+    if (blank) {
+        len = snprintf(buf, sizeof buf, "0.0.0.0:0");
+    } else {
+        int64_t tb[4], te[4];
+        int nt = 0;
+        for (int64_t i = 0; i < n;) {
+            while (i < n && s[i] == ':') i++;
+            if (i >= n) break;
+            const int64_t b = i;
+            while (i < n && s[i] != ':') i++;
+            if (nt < 4) {
+                tb[nt] = b;
+                te[nt] = i;
+            }
+            nt++;
+        }
+        int32_t port = 0, idx = 0;
+        if ((nt != 2 && nt != 3) || !jo_parse_int(s + tb[1], te[1] - tb[1], &port) ||
+            (nt == 3 && !jo_parse_int(s + tb[2], te[2] - tb[2], &idx))) {
+            *kind = 2;
+            return 0;
+        }
+        const int64_t iplen = te[0] - tb[0];
+        if (iplen > 900) {
+            *kind = 2;
+            return 0;
+        }
+        memcpy(buf, s + tb[0], (size_t)iplen);
+        len = (int)iplen;
+        len += idx != 0 ? snprintf(buf + len, sizeof buf - (size_t)len, ":%d:%d", port, idx)
+                        : snprintf(buf + len, sizeof buf - (size_t)len, ":%d", port);
+    }
+    *kind = (len == n && memcmp(buf, s, (size_t)n) == 0) ? 0 : 1;
+    return jo_crc64((const uint8_t *)buf, (size_t)len);
+}
+
+void jo_v2_decode_batch(const uint8_t *rec, const uint64_t *off, uint32_t n, uint8_t *status,
+                        uint8_t *type, int64_t *index, int64_t *term, uint64_t *stored,
+                        uint8_t *has_checksum, uint64_t *data_off, uint64_t *data_len,
+                        uint32_t *peer_counts, uint64_t *computed, uint8_t *corrupt) {
+    static const uint8_t MAGIC0 = 0xBB, MAGIC1 = 0xD2, VERSION = 1; /* LogEntryV2CodecFactory.java:52-57 */
+    const int HEADER = 6;
+    for (uint32_t r = 0; r < n; r++) {
+        const uint8_t *bs = rec + off[r];
+        const int64_t L = (int64_t)(off[r + 1] - off[r]);
+        uint8_t st = JO_V2_OK;
+        int64_t idx = 0, tm = 0, doff = (int64_t)off[r], dlen = 0;
+        uint64_t ck = 0, pxor = 0;
+        int have_type = 0, have_term = 0, have_index = 0, have_data = 0, have_ck = 0, worst = 0;
+        int32_t etype = 0;
+        uint32_t counts = 0;
+        /* AutoDetectDecoder.decode (JC/entity/codec/AutoDetectDecoder.java:41-52) */
+        if (L < 1) st = JO_V2_NULL;
+        else if (bs[0] != MAGIC0) st = JO_V2_V1;
+        /* V2Decoder.decode (JC/entity/codec/v2/V2Decoder.java:46-63) */
+        else if (L < HEADER || bs[1] != MAGIC1 || bs[2] != VERSION) st = JO_V2_NULL;
+        else {
+            jo_cis in = {bs, HEADER, L, 0, 0};
+            for (;;) { /* PBLogEntry parsing constructor (generated, log.proto:10-20) */
+                const uint32_t tag = jo_cis_tag(&in);
+                if (in.err || tag == 0) break;
+                int64_t at, len;
+                switch (tag) {
+                case 8: { /* type: readEnum, unknown numbers go to the unknown fields */
+                    const int32_t v = (int32_t)jo_cis_varint32(&in);
+                    if (!in.err && v >= 0 && v <= 3) {
+                        etype = v;
+                        have_type = 1;
+                    }
+                    break;
+                }
+                case 16: tm = (int64_t)jo_cis_varint64(&in); have_term = 1; break;
+                case 24: idx = (int64_t)jo_cis_varint64(&in); have_index = 1; break;
+                case 34: case 42: case 66: case 74: { /* peers, old_peers, learners, old_learners */
+                    at = jo_cis_bytes(&in, &len);
+                    if (in.err) break;
+                    int kind;
+                    pxor ^= jo_v2_peer_checksum(bs + at, len, &kind);
+                    if (kind > worst) worst = kind;
+                    const int list = tag == 34 ? 0 : tag == 42 ? 1 : tag == 66 ? 2 : 3;
+                    if (((counts >> (8 * list)) & 0xFF) != 0xFF) counts += 1u << (8 * list);
+                    break;
+                }
+                case 50: /* data: the last occurrence wins */
+                    at = jo_cis_bytes(&in, &len);
+                    if (!in.err) {
+                        doff = (int64_t)off[r] + at;
+                        dlen = len;
+                        have_data = 1;
+                    }
+                    break;
+                case 56: ck = jo_cis_varint64(&in); have_ck = 1; break;
+                default:
+                    if (!jo_cis_skip_field(&in, tag, 0)) goto end_group; /* END_GROUP stops */
+                }
+                if (in.err) break;
+            }
+            if (0) {
+            end_group:
+                in.err = 1; /* checkLastTagWas(0) fails after a top-level END_GROUP */
+            }
+            /* required type/term/index/data (isInitialized) */
+            if (in.err || !have_type || !have_term || !have_index || !have_data) st = JO_V2_NULL;
+            else if (worst == 2) st = JO_V2_PEER_THROWS;
+            else if (worst == 1) st = JO_V2_PEER_NONCANON;
+        }
+        const int ok = st == JO_V2_OK || st == JO_V2_PEER_NONCANON;
+        if (!ok) {
+            etype = 0;
+            idx = tm = 0;
+            ck = 0;
+            have_ck = 0;
+            doff = (int64_t)off[r];
+            dlen = 0;
+            counts = 0;
+        }
+        /* LogEntry.checksum / isCorrupted (JC/entity/LogEntry.java:88-108,156-158) */
+        const uint64_t c = ok ? jo_logentry_checksum(etype, idx, tm, pxor, rec + doff, (size_t)dlen) : 0;
+        status[r] = st;
+        type[r] = (uint8_t)etype;
+        index[r] = idx;
+        term[r] = tm;
+        stored[r] = ck;
+        has_checksum[r] = (uint8_t)have_ck;
+        data_off[r] = (uint64_t)doff;
+        data_len[r] = (uint64_t)dlen;
+        if (peer_counts) peer_counts[r] = counts;
+        computed[r] = c;
+        corrupt[r] = (uint8_t)(ok && have_ck && ck != c);
+    }
+}

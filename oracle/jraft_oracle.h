@@ -180,6 +180,30 @@ int64_t jo_commit_fanout_replay(uint32_t G, const uint64_t *seq_off, const int64
                                 int64_t *last_applied, int64_t *cq_first, int64_t *cq_size,
                                 int64_t *first_closure, uint8_t *status);
 
+/* ---------------- V2 log entry decode + verify on read ---------------------- */
+/* Statuses: OK; NULL = the reference decoder returns null (AutoDetectDecoder on an empty
+ * record, V2Decoder on a short header / bad magic / bad version, or protobuf's
+ * InvalidProtocolBufferException incl. missing required fields); V1 = first byte is not the
+ * V2 magic (routed to V1Decoder, not restated); PEER_NONCANON = decodes, but a peer string
+ * re-renders differently through PeerId.parse/toString (the checksum uses the re-rendered
+ * string); PEER_THROWS = JRaftUtils.getPeerId throws IllegalArgumentException. */
+enum { JO_V2_OK = 0, JO_V2_NULL = 1, JO_V2_V1 = 2, JO_V2_PEER_NONCANON = 3, JO_V2_PEER_THROWS = 4 };
+uint64_t jo_v2_peer_checksum(const uint8_t *s, int64_t n, int *kind);
+/*
+ * Record r = rec[off[r] .. off[r+1]): the bytes a LogStorage holds for one index
+ * (LogEntryV2CodecFactory header 0xBB 0xD2 0x01 + 3 reserved, then a PBLogEntry,
+ * JC/entity/codec/v2/V2Encoder.java:76-130), decoded as AutoDetectDecoder/V2Decoder do
+ * (JC/entity/codec/AutoDetectDecoder.java:41-52, v2/V2Decoder.java:46-110) and verified as
+ * LogManagerImpl does on read (JC/core/LogManagerImpl.java:733-745: isCorrupted).
+ * peer_counts[r] (nullable) = peers | old_peers<<8 | learners<<16 | old_learners<<24 (each
+ * saturating at 255).  data_off is absolute into rec.  Undecodable records get zeros,
+ * data_off = off[r], data_len 0.
+ */
+void jo_v2_decode_batch(const uint8_t *rec, const uint64_t *off, uint32_t n, uint8_t *status,
+                        uint8_t *type, int64_t *index, int64_t *term, uint64_t *stored,
+                        uint8_t *has_checksum, uint64_t *data_off, uint64_t *data_len,
+                        uint32_t *peer_counts, uint64_t *computed, uint8_t *corrupt);
+
 #ifdef __cplusplus
 }
 #endif

@@ -92,6 +92,10 @@ def lib():
         L.jo_quorum_epoch_replay.argtypes = [C.c_uint32, C.c_uint32, _i64p, _i64p, _i64p, _i64p,
                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_int64, _i64p, _u8p]
+        L.jo_v2_decode_batch.restype = None
+        L.jo_v2_decode_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32] + [C.c_void_p] * 11
+        L.jo_v2_peer_checksum.restype = C.c_uint64
+        L.jo_v2_peer_checksum.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_int)]
         L.jo_commit_fanout_replay.restype = C.c_int64
         L.jo_commit_fanout_replay.argtypes = [C.c_uint32] + [C.c_void_p] * 7
         _lib = L
@@ -219,6 +223,81 @@ def commit_fanout_replay(seq_off, seq, last_applied, cq_first, cq_size):
     n = lib().jo_commit_fanout_replay(G, _ptr(so), _ptr(sq), _ptr(la), _ptr(cf), _ptr(cs),
                                       _ptr(fc), _ptr(st))
     return st, fc, la, cf, cs, int(n)
+
+
+# ------------------------------------------------------- V2 codec ------------
+
+V2_OK, V2_NULL, V2_V1, V2_PEER_NONCANON, V2_PEER_THROWS = 0, 1, 2, 3, 4
+V2_HEADER = bytes([0xBB, 0xD2, 0x01, 0, 0, 0])  # LogEntryV2CodecFactory.java:52-60
+
+
+def pb_varint(v: int) -> bytes:
+    """protobuf varint of a (two's complement, 64-bit) integer."""
+    v &= M64
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if v:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def pb_field(num: int, wire: int, payload: bytes) -> bytes:
+    return pb_varint((num << 3) | wire) + payload
+
+
+def v2_encode(etype: int, index: int, term: int, peers=(), old_peers=(), learners=(),
+              old_learners=(), checksum=None, data: bytes | None = b"") -> bytes:
+    """V2Encoder.encode (JC/entity/codec/v2/V2Encoder.java:76-130): header + PBLogEntry in
+    the generated writeTo order (v2/LogOutter.java:518-546): type 1, term 2, index 3,
+    peers 4, old_peers 5, data 6 (always set, EMPTY for null), checksum 7 (if set),
+    learners 8, old_learners 9.  Peers are their toString() bytes (latin-1)."""
+    b = bytearray(V2_HEADER)
+    b += pb_field(1, 0, pb_varint(etype))
+    b += pb_field(2, 0, pb_varint(term))
+    b += pb_field(3, 0, pb_varint(index))
+    for num, lst in ((4, peers), (5, old_peers)):
+        for p in lst:
+            pb = p.encode("latin-1") if isinstance(p, str) else bytes(p)
+            b += pb_field(num, 2, pb_varint(len(pb)) + pb)
+    d = data or b""
+    b += pb_field(6, 2, pb_varint(len(d)) + d)
+    if checksum is not None:
+        b += pb_field(7, 0, pb_varint(checksum))
+    for num, lst in ((8, learners), (9, old_learners)):
+        for p in lst:
+            pb = p.encode("latin-1") if isinstance(p, str) else bytes(p)
+            b += pb_field(num, 2, pb_varint(len(pb)) + pb)
+    return bytes(b)
+
+
+def v2_peer_checksum(s: bytes):
+    """(checksum, kind) of JRaftUtils.getPeerId(s).checksum(); kind 0 canonical, 1 re-rendered,
+    2 throws."""
+    k = C.c_int(0)
+    v = lib().jo_v2_peer_checksum(bytes(s), len(s), C.byref(k))
+    return int(v), k.value
+
+
+def v2_decode_batch(records: np.ndarray, offsets: np.ndarray) -> dict:
+    """AutoDetectDecoder/V2Decoder + LogEntry.isCorrupted per record (jo_v2_decode_batch)."""
+    rec = np.ascontiguousarray(records, np.uint8)
+    if rec.size == 0:
+        rec = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(offsets, np.uint64)
+    n = len(off) - 1
+    o = {k: np.zeros(n, t) for k, t in (
+        ("status", np.uint8), ("type", np.uint8), ("index", np.int64), ("term", np.int64),
+        ("stored", np.uint64), ("has_checksum", np.uint8), ("data_off", np.uint64),
+        ("data_len", np.uint64), ("peer_counts", np.uint32), ("computed", np.uint64),
+        ("corrupt", np.uint8))}
+    lib().jo_v2_decode_batch(_ptr(rec), _ptr(off), n, *[_ptr(o[k]) for k in (
+        "status", "type", "index", "term", "stored", "has_checksum", "data_off", "data_len",
+        "peer_counts", "computed", "corrupt")])
+    return o
 
 
 # ------------------------------------------------- pure-Python cross-checks --

@@ -24,6 +24,8 @@ extern "C" hipError_t jrq_launch_quorum(const JrqQuorumArgs* args, int num_cus, 
 extern "C" hipError_t jrq_launch_ae_meta(const JrqAeArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_lease(const JrqLeaseArgs* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_fanout(const JrqFanoutArgs* a, hipStream_t stream);
+extern "C" hipError_t jrq_launch_v2_parse(const JrqV2Args* a, hipStream_t stream);
+extern "C" hipError_t jrq_launch_v2_finish(const JrqV2Args* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_first_corrupt(const JrqAeArgs* a, hipStream_t stream);
 
 namespace {
@@ -56,7 +58,7 @@ struct jrq_engine {
   uint32_t crc_seg_map = 1;  // JRQ_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
-  DevBuf stage[24];  // 0-13 host-variant staging, 16-19 AppendEntries scratch, 20 fan-out scratch
+  DevBuf stage[24];  // 0-13 host-variant staging, 16-19 AppendEntries scratch, 20 fan-out scratch, 21-23 V2 decode scratch
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = -1;
   std::string err;
@@ -714,6 +716,112 @@ int jrq_commit_fanout(jrq_engine* e, uint32_t G, const int64_t* prev_committed,
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   if (*num_listed_out)
     JRQ_HIP(e, hipMemcpy(listed_out, dlist, static_cast<size_t>(*num_listed_out) * 4, hipMemcpyDeviceToHost));
+  return JRQ_OK;
+}
+
+// ------------------------------------------------------- V2 decode -----
+
+int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* off, uint32_t N,
+                             uint8_t* status, uint8_t* type, int64_t* index, int64_t* term,
+                             uint64_t* stored, uint8_t* has_checksum, uint64_t* data_off,
+                             uint64_t* data_len, uint32_t* peer_counts, uint64_t* computed,
+                             uint8_t* corrupt) {
+  if (!e) return JRQ_E_INVALID;
+  if (N == 0) return JRQ_OK;
+  if (N >= 0x7FFFFFFFu) return fail(e, JRQ_E_INVALID, "N too large");
+  if (!rec || !off || !status || !type || !index || !term || !stored || !has_checksum ||
+      !data_off || !data_len || !computed || !corrupt)
+    return fail(e, JRQ_E_INVALID, "null V2 decode array");
+  DeviceGuard guard(e->device);
+  int rc;
+  void *partial, *off2, *crc2;
+  if ((rc = ensure_stage(e, 21, static_cast<size_t>(N) * 8, &partial))) return rc;
+  if ((rc = ensure_stage(e, 22, (2 * static_cast<size_t>(N) + 2) * 8, &off2))) return rc;
+  if ((rc = ensure_stage(e, 23, (2 * static_cast<size_t>(N) + 1) * 8, &crc2))) return rc;
+  JrqV2Args v{};
+  v.rec = rec;
+  v.off = off;
+  v.n = N;
+  v.slice = e->slice;
+  v.status = status;
+  v.type = type;
+  v.index = index;
+  v.term = term;
+  v.stored = stored;
+  v.has_checksum = has_checksum;
+  v.data_off = data_off;
+  v.data_len = data_len;
+  v.peer_counts = peer_counts;
+  v.computed = computed;
+  v.corrupt = corrupt;
+  v.partial = static_cast<uint64_t*>(partial);
+  v.off2 = static_cast<uint64_t*>(off2);
+  v.crc2 = static_cast<const uint64_t*>(crc2);
+  JRQ_HIP(e, jrq_launch_v2_parse(&v, e->stream));
+  // data ranges interleaved with the gaps between them: one streaming pass over the records
+  JrqCrcArgs a{};
+  a.payload = rec;
+  a.offsets = v.off2;
+  a.n = 2 * N + 1;
+  a.out = static_cast<uint64_t*>(crc2);
+  if ((rc = crc_dispatch(e, a, 0))) return rc;
+  JRQ_HIP(e, jrq_launch_v2_finish(&v, e->num_cus, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_v2_decode_verify(jrq_engine* e, const uint8_t* rec, const uint64_t* off, uint32_t N,
+                         uint8_t* status, uint8_t* type, int64_t* index, int64_t* term,
+                         uint64_t* stored, uint8_t* has_checksum, uint64_t* data_off,
+                         uint64_t* data_len, uint32_t* peer_counts, uint64_t* computed,
+                         uint8_t* corrupt) {
+  if (!e) return JRQ_E_INVALID;
+  if (N == 0) return JRQ_OK;
+  if (!off || !status || !type || !index || !term || !stored || !has_checksum || !data_off ||
+      !data_len || !computed || !corrupt)
+    return fail(e, JRQ_E_INVALID, "null V2 decode array");
+  const uint64_t lo = off[0], hi = off[N];
+  for (uint32_t i = 0; i < N; ++i)
+    if (off[i + 1] < off[i]) return fail(e, JRQ_E_INVALID, "offsets not monotone");
+  if (hi > lo && !rec) return fail(e, JRQ_E_INVALID, "null records");
+  DeviceGuard guard(e->device);
+  int rc;
+  const uint8_t* drec;
+  const uint64_t* doff;
+  uint8_t dummy = 0;
+  if ((rc = stage_in(e, 10, hi > lo ? rec + lo : &dummy, hi > lo ? hi - lo : 1, &drec))) return rc;
+  std::vector<uint64_t> rebased(off, off + N + 1);
+  for (auto& o : rebased) o -= lo;
+  if ((rc = stage_in(e, 11, rebased.data(), rebased.size(), &doff))) return rc;
+  const size_t n8 = static_cast<size_t>(N) * 8;
+  void *dst, *dty, *didx, *dtm, *dsto, *dhas, *ddo, *ddl, *dpc, *dcmp, *dcor;
+  if ((rc = ensure_stage(e, 0, N, &dst)) || (rc = ensure_stage(e, 1, N, &dty)) ||
+      (rc = ensure_stage(e, 2, n8, &didx)) || (rc = ensure_stage(e, 3, n8, &dtm)) ||
+      (rc = ensure_stage(e, 4, n8, &dsto)) || (rc = ensure_stage(e, 5, N, &dhas)) ||
+      (rc = ensure_stage(e, 6, n8, &ddo)) || (rc = ensure_stage(e, 7, n8, &ddl)) ||
+      (rc = ensure_stage(e, 8, static_cast<size_t>(N) * 4, &dpc)) ||
+      (rc = ensure_stage(e, 9, n8, &dcmp)) || (rc = ensure_stage(e, 12, N, &dcor)))
+    return rc;
+  if ((rc = jrq_v2_decode_verify_dev(
+           e, drec, doff, N, static_cast<uint8_t*>(dst), static_cast<uint8_t*>(dty),
+           static_cast<int64_t*>(didx), static_cast<int64_t*>(dtm), static_cast<uint64_t*>(dsto),
+           static_cast<uint8_t*>(dhas), static_cast<uint64_t*>(ddo), static_cast<uint64_t*>(ddl),
+           peer_counts ? static_cast<uint32_t*>(dpc) : nullptr, static_cast<uint64_t*>(dcmp),
+           static_cast<uint8_t*>(dcor))))
+    return rc;
+  JRQ_HIP(e, hipMemcpyAsync(status, dst, N, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(type, dty, N, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(index, didx, n8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(term, dtm, n8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(stored, dsto, n8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(has_checksum, dhas, N, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(data_off, ddo, n8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(data_len, ddl, n8, hipMemcpyDeviceToHost, e->stream));
+  if (peer_counts)
+    JRQ_HIP(e, hipMemcpyAsync(peer_counts, dpc, static_cast<size_t>(N) * 4, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(computed, dcmp, n8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(corrupt, dcor, N, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  for (uint32_t i = 0; i < N; ++i) data_off[i] += lo;  // back to the caller's base
   return JRQ_OK;
 }
 

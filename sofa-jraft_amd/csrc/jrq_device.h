@@ -140,6 +140,28 @@ struct JrqFanoutArgs {
   uint32_t* tile_count;           // scratch [ceil(G/4096)]
 };
 
+// V2 log-entry decode + verify (v2_decode.hip).
+struct JrqV2Args {
+  const uint8_t* rec;
+  const uint64_t* off;     // [n+1]
+  uint32_t n;
+  const uint64_t* slice;   // engine slice tables (R0 = bswap of the CRC64 byte table)
+  uint8_t* status;
+  uint8_t* type;
+  int64_t* index;
+  int64_t* term;
+  uint64_t* stored;
+  uint8_t* has_checksum;
+  uint64_t* data_off;
+  uint64_t* data_len;
+  uint32_t* peer_counts;   // nullable
+  uint64_t* computed;
+  uint8_t* corrupt;
+  uint64_t* partial;       // scratch [n]
+  uint64_t* off2;          // scratch [2n+2]
+  const uint64_t* crc2;    // scratch [2n+1] (CRC of the interleaved ranges)
+};
+
 struct JrqQuorumArgs {
   const int64_t* match;
   const int64_t* pending_index;

@@ -1,0 +1,344 @@
+// v2_decode.hip -- batched V2 log-entry decode + checksum verify on read.
+//
+// Reference, per record a LogStorage returns for one log index:
+//   AutoDetectDecoder.decode   jraft-core/.../entity/codec/AutoDetectDecoder.java:41-52
+//   V2Decoder.decode           jraft-core/.../entity/codec/v2/V2Decoder.java:46-110
+//   PBLogEntry parsing         jraft-core/.../entity/codec/v2/LogOutter.java:185-275 (protobuf
+//                              3.5.1 CodedInputStream, pom.xml:74), log.proto:10-20
+//   LogEntry.isCorrupted       jraft-core/.../entity/LogEntry.java:88-108,156-158, checked on
+//                              read by LogManagerImpl (core/LogManagerImpl.java:733-745)
+//
+// Record layout (V2Encoder.java:76-130, LogEntryV2CodecFactory.java:52-60):
+//   0xBB 0xD2 0x01 <3 reserved> PBLogEntry{type 1, term 2, index 3, peers 4*, old_peers 5*,
+//   data 6, checksum 7?, learners 8*, old_learners 9*}
+//
+// Design: the records are one flat buffer with offsets[N+1] (the batch a segment / RocksDB
+// scan hands over).
+//   v2_parse   one lane per record walks the protobuf fields through a 16-B aligned chunk
+//              cache (a handful of dependent loads per record: the header fields, then a jump
+//              over `data` to the trailing checksum / learner fields).  Peer strings are hashed
+//              byte-wise from an LDS copy of the CRC table while their canonical form is
+//              checked; type ^ crc(LogId) ^ peers goes to a partial word.  It also writes the
+//              interleaved range list  gap0, data0, gap1, data1, ..., dataN-1, gapN  whose
+//              boundaries are [off[0], d0, e0, d1, e1, ..., off[N]].
+//   crc64      the batched CRC kernels (crc64.hip) over those 2N+1 ranges: one pass over the
+//              record bytes at streaming bandwidth (gap ranges -- headers -- are hashed too and
+//              dropped; they are a few dozen bytes per record).
+//   v2_finish  computed = partial ^ crc(data range), corrupt = has_checksum && stored != computed.
+//
+// A peer string is hashed as stored when it is already what PeerId.toString() would render
+// from it (V2Encoder always writes toString(), so this is every record it produced).  A
+// record with any other peer string -- which the reference re-renders or rejects with
+// IllegalArgumentException -- or with unknown-field groups nested deeper than 2 gets status
+// HOST: the host decodes it with the reference decoder.
+#include "jrq_device.h"
+
+namespace jrq {
+
+typedef uint32_t v2u32x4 __attribute__((ext_vector_type(4)));
+
+// include/jrq.h jrq_v2_status
+constexpr uint8_t kV2Ok = 0, kV2Null = 1, kV2V1 = 2, kV2Host = 3;
+
+struct ChunkReader {
+  const uint8_t* rec;  // record start
+  int64_t limit;       // record length
+  uintptr_t chunk_addr;
+  v2u32x4 chunk;
+  bool err;
+  __device__ explicit ChunkReader(const uint8_t* r, int64_t len)
+      : rec(r), limit(len), chunk_addr(~static_cast<uintptr_t>(0)), err(false) {}
+  // byte at record position pos (< limit): its 16-B granule holds a valid byte, so the
+  // aligned load never leaves the mapped buffer
+  __device__ __forceinline__ uint32_t at(int64_t pos) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(rec) + static_cast<uintptr_t>(pos);
+    const uintptr_t ca = a & ~static_cast<uintptr_t>(15);
+    if (ca != chunk_addr) {
+      chunk = *reinterpret_cast<const v2u32x4*>(ca);
+      chunk_addr = ca;
+    }
+    const uint32_t o = static_cast<uint32_t>(a & 15u);
+    const uint32_t w = o < 8 ? (o < 4 ? chunk[0] : chunk[1]) : (o < 12 ? chunk[2] : chunk[3]);
+    return (w >> (8 * (o & 3u))) & 0xFFu;
+  }
+};
+
+struct PbIn {
+  ChunkReader rd;
+  int64_t pos;
+  uint32_t last_tag;
+  __device__ PbIn(const uint8_t* r, int64_t len) : rd(r, len), pos(6), last_tag(0) {}
+  __device__ __forceinline__ uint32_t byte() {
+    if (pos >= rd.limit) {
+      rd.err = true;  // truncatedMessage
+      return 0;
+    }
+    return rd.at(pos++);
+  }
+  // readRawVarint32 (5 value bytes + up to 5 discarded)
+  __device__ uint32_t varint32() {
+    uint32_t r = 0;
+    for (int i = 0; i < 5; ++i) {
+      const uint32_t x = byte();
+      if (rd.err) return 0;
+      r |= (x & 0x7Fu) << (7 * i);
+      if (!(x & 0x80u)) return r;
+    }
+    for (int i = 0; i < 5; ++i) {
+      const uint32_t x = byte();
+      if (rd.err) return 0;
+      if (!(x & 0x80u)) return r;
+    }
+    rd.err = true;  // malformedVarint
+    return 0;
+  }
+  __device__ uint64_t varint64() {
+    uint64_t r = 0;
+    for (int shift = 0; shift < 64; shift += 7) {
+      const uint32_t x = byte();
+      if (rd.err) return 0;
+      r |= static_cast<uint64_t>(x & 0x7Fu) << shift;
+      if (!(x & 0x80u)) return r;
+    }
+    rd.err = true;
+    return 0;
+  }
+  __device__ uint32_t tag() {
+    if (pos >= rd.limit) {
+      last_tag = 0;
+      return 0;
+    }
+    last_tag = varint32();
+    if (!rd.err && (last_tag >> 3) == 0) rd.err = true;  // invalidTag
+    return rd.err ? 0 : last_tag;
+  }
+  // length-delimited field: offset of its payload, *len its size
+  __device__ int64_t bytes(int64_t* len) {
+    const int32_t size = static_cast<int32_t>(varint32());
+    if (rd.err) return 0;
+    if (size < 0 || size > rd.limit - pos) {
+      rd.err = true;
+      return 0;
+    }
+    const int64_t at = pos;
+    pos += size;
+    *len = size;
+    return at;
+  }
+  __device__ void skip(int64_t n) {
+    if (n > rd.limit - pos) {
+      rd.err = true;
+      pos = rd.limit;
+    } else {
+      pos += n;
+    }
+  }
+};
+
+// Integer.toString canonical decimal of an int32 (sign only for negatives, no leading zeros)
+struct CanonInt {
+  int64_t v = 0;
+  uint32_t n = 0;
+  bool neg = false, ok = true;
+  __device__ __forceinline__ void push(uint32_t c) {
+    if (n == 0 && c == '-') {
+      neg = true;
+    } else if (c >= '0' && c <= '9') {
+      const uint32_t digits = n - (neg ? 1u : 0u);
+      if (digits == 1 && v == 0) ok = false;  // leading zero
+      v = v * 10 + (c - '0');
+      if (v > 2147483648LL) ok = false;
+    } else {
+      ok = false;
+    }
+    ++n;
+  }
+  __device__ __forceinline__ bool canonical() const {
+    const uint32_t digits = n - (neg ? 1u : 0u);
+    if (!ok || digits == 0) return false;
+    if (neg && v == 0) return false;  // "-0"
+    return neg ? v <= 2147483648LL : v <= 2147483647LL;
+  }
+};
+
+// crc64 of the peer string at [at, at+len) (MSB-first byte table in LDS); *canon = the
+// bytes are exactly PeerId.toString() of what they parse to: ip ":" port [":" idx != 0]
+__device__ uint64_t peer_crc(PbIn& in, int64_t at, int64_t len, const uint64_t* T, bool* canon) {
+  uint64_t crc = 0;
+  uint32_t colons = 0, tok_len = 0;
+  bool ok = true;
+  CanonInt port, idx;
+  for (int64_t i = 0; i < len; ++i) {
+    const uint32_t c = in.rd.at(at + i);
+    crc = T[((crc >> 56) ^ c) & 0xFFu] ^ (crc << 8);
+    if (c == ':') {
+      ok = ok && tok_len > 0;
+      ++colons;
+      tok_len = 0;
+      continue;
+    }
+    ++tok_len;
+    if (colons == 1) port.push(c);
+    else if (colons == 2) idx.push(c);
+  }
+  ok = ok && tok_len > 0 && (colons == 1 || colons == 2) && port.canonical();
+  if (colons == 2) ok = ok && idx.canonical() && idx.v != 0;
+  *canon = ok;
+  return crc;
+}
+
+__device__ __forceinline__ uint64_t crc_bytes_be(uint64_t crc, uint64_t v, const uint64_t* T) {
+#pragma unroll
+  for (int s = 56; s >= 0; s -= 8) crc = T[((crc >> 56) ^ (v >> s)) & 0xFFu] ^ (crc << 8);
+  return crc;
+}
+
+__global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
+  __shared__ uint64_t T[256];
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) T[i] = bswap64(a.slice[i]);
+  __syncthreads();
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r == 0) {
+    a.off2[0] = a.off[0];
+    a.off2[2ull * a.n + 1] = a.off[a.n];
+  }
+  if (r >= a.n) return;
+  const uint64_t b0 = a.off[r];
+  const int64_t L = static_cast<int64_t>(a.off[r + 1] - b0);
+  const uint8_t* rec = a.rec + b0;
+  uint8_t st = kV2Ok;
+  int64_t idx = 0, tm = 0, doff = 0, dlen = 0;
+  uint64_t ck = 0, pxor = 0;
+  bool have_type = false, have_term = false, have_index = false, have_data = false,
+       have_ck = false, host = false, deep = false;
+  uint32_t etype = 0, counts = 0;
+  if (L < 1) {
+    st = kV2Null;
+  } else {
+    PbIn in(rec, L);
+    const uint32_t m0 = in.rd.at(0);
+    if (m0 != 0xBBu) {
+      st = kV2V1;
+    } else if (L < 6 || in.rd.at(1) != 0xD2u || in.rd.at(2) != 1u) {
+      st = kV2Null;
+    } else {
+      uint32_t grp[2] = {0, 0};  // open unknown-field groups (field numbers)
+      int depth = 0;
+      bool stop = false;  // END_GROUP at top level
+      while (!in.rd.err && !deep && !stop) {
+        const uint32_t t = in.tag();
+        if (in.rd.err) break;
+        if (t == 0) {
+          if (depth) in.rd.err = true;  // input ended inside a group
+          break;
+        }
+        int64_t len = 0, at;
+        if (depth == 0) {
+          switch (t) {
+            case 8: {  // type (enum): numbers outside EntryType stay unknown
+              const int32_t v = static_cast<int32_t>(in.varint32());
+              if (!in.rd.err && v >= 0 && v <= 3) {
+                etype = static_cast<uint32_t>(v);
+                have_type = true;
+              }
+              continue;
+            }
+            case 16: tm = static_cast<int64_t>(in.varint64()); have_term = true; continue;
+            case 24: idx = static_cast<int64_t>(in.varint64()); have_index = true; continue;
+            case 34: case 42: case 66: case 74: {
+              at = in.bytes(&len);
+              if (in.rd.err) continue;
+              bool canon;
+              pxor ^= peer_crc(in, at, len, T, &canon);
+              host = host || !canon;
+              const uint32_t sh = t == 34 ? 0 : t == 42 ? 8 : t == 66 ? 16 : 24;
+              if (((counts >> sh) & 0xFFu) != 0xFFu) counts += 1u << sh;
+              continue;
+            }
+            case 50:  // data: the last occurrence wins
+              at = in.bytes(&len);
+              if (!in.rd.err) {
+                doff = at;
+                dlen = len;
+                have_data = true;
+              }
+              continue;
+            case 56: ck = in.varint64(); have_ck = true; continue;
+            default: break;
+          }
+        }
+        // unknown field (any number / wire-type mismatch), inside a group or not
+        switch (t & 7u) {
+          case 0: (void)in.varint64(); break;
+          case 1: in.skip(8); break;
+          case 2: (void)in.bytes(&len); break;
+          case 3:
+            if (depth == 2) deep = true;  // deeper nesting: stop, decode on the host
+            else grp[depth++] = t >> 3;
+            break;
+          case 4:
+            if (depth == 0) stop = true;  // checkLastTagWas(0) fails below
+            else if (grp[--depth] != (t >> 3)) in.rd.err = true;
+            break;
+          case 5: in.skip(4); break;
+          default: in.rd.err = true;  // invalidWireType
+        }
+      }
+      if (deep) st = kV2Host;
+      else if (in.rd.err || stop || !have_type || !have_term || !have_index || !have_data) st = kV2Null;
+      else if (host) st = kV2Host;
+    }
+  }
+  if (st != kV2Ok) {
+    etype = 0;
+    idx = tm = 0;
+    ck = 0;
+    have_ck = false;
+    doff = 0;
+    dlen = 0;
+    counts = 0;
+    pxor = 0;
+  }
+  const uint64_t logid = crc_bytes_be(crc_bytes_be(0, static_cast<uint64_t>(idx), T),
+                                      static_cast<uint64_t>(tm), T);
+  a.partial[r] = st == kV2Ok ? (static_cast<uint64_t>(etype) ^ logid ^ pxor) : 0;
+  a.status[r] = st;
+  a.type[r] = static_cast<uint8_t>(etype);
+  a.index[r] = idx;
+  a.term[r] = tm;
+  a.stored[r] = ck;
+  a.has_checksum[r] = have_ck ? 1 : 0;
+  a.data_off[r] = b0 + static_cast<uint64_t>(doff);
+  a.data_len[r] = static_cast<uint64_t>(dlen);
+  if (a.peer_counts) a.peer_counts[r] = counts;
+  a.off2[2ull * r + 1] = b0 + static_cast<uint64_t>(doff);
+  a.off2[2ull * r + 2] = b0 + static_cast<uint64_t>(doff + dlen);
+}
+
+__global__ __launch_bounds__(256) void v2_finish(JrqV2Args a) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
+    const bool ok = a.status[r] == kV2Ok;
+    const uint64_t c = ok ? (a.partial[r] ^ a.crc2[2ull * r + 1]) : 0;
+    a.computed[r] = c;
+    a.corrupt[r] = (ok && a.has_checksum[r] && a.stored[r] != c) ? 1 : 0;
+  }
+}
+
+}  // namespace jrq
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_v2_parse(
+    const JrqV2Args* a, hipStream_t stream) {
+  const uint32_t blocks = (a->n + 255) / 256;
+  hipLaunchKernelGGL(jrq::v2_parse, dim3(blocks ? blocks : 1), dim3(256), 0, stream, *a);
+  return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_v2_finish(
+    const JrqV2Args* a, int num_cus, hipStream_t stream) {
+  uint32_t blocks = (a->n + 255) / 256;
+  const uint32_t cap = static_cast<uint32_t>(num_cus) * 8u;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(jrq::v2_finish, dim3(blocks ? blocks : 1), dim3(256), 0, stream, *a);
+  return hipGetLastError();
+}

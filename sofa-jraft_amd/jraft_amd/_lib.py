@@ -18,6 +18,7 @@ ERRORS = {-1: "JRQ_E_INVALID", -2: "JRQ_E_NOMEM", -3: "JRQ_E_HIP", -4: "JRQ_E_RC
           -5: "JRQ_E_NODEV", -6: "JRQ_E_STATE"}
 ST_OK, ST_NOT_LEADER, ST_OUT_OF_RANGE, ST_EMPTY_CONF = 0, 1, 2, 4
 FAN_NONE, FAN_APPLY, FAN_SKIP, FAN_INVALID = 0, 1, 2, 3  # jrq_fanout_status
+V2_OK, V2_NULL, V2_V1, V2_HOST = 0, 1, 2, 3  # jrq_v2_status
 MAX_PEERS = 16
 
 
@@ -74,6 +75,8 @@ SIGNATURES = [
      [_V, _V, C.c_uint64, C.c_uint32, _V, _V, C.c_uint32, C.c_int64, C.c_int64, _V, _V, _V]),
     ("jrq_commit_fanout_dev", C.c_int, [_V, C.c_uint32] + [_V] * 9),
     ("jrq_commit_fanout", C.c_int, [_V, C.c_uint32] + [_V] * 9),
+    ("jrq_v2_decode_verify_dev", C.c_int, [_V, _V, _V, C.c_uint32] + [_V] * 11),
+    ("jrq_v2_decode_verify", C.c_int, [_V, _V, _V, C.c_uint32] + [_V] * 11),
     ("jrq_rccl_get_unique_id", C.c_int, [_V]),
     ("jrq_rccl_init", C.c_int, [_V, C.c_int, C.c_int, _V]),
     ("jrq_publish_committed_dev", C.c_int, [_V, _V, _V, C.c_uint64]),

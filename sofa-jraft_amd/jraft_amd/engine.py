@@ -254,6 +254,29 @@ class Engine:
             _dev_ptr(first_closure_out), _dev_ptr(status_out), _dev_ptr(listed_out),
             _dev_ptr(num_listed_out)), self._h)
 
+    # --------------------------------------------------- V2 decode + verify --
+    V2_FIELDS = (("status", np.uint8), ("type", np.uint8), ("index", np.int64),
+                 ("term", np.int64), ("stored", np.uint64), ("has_checksum", np.uint8),
+                 ("data_off", np.uint64), ("data_len", np.uint64), ("peer_counts", np.uint32),
+                 ("computed", np.uint64), ("corrupt", np.uint8))
+
+    def v2_decode_verify(self, records, offsets):
+        """Host variant: dict of per-record arrays (jrq_v2_decode_verify)."""
+        rec = _c(records, np.uint8)
+        off = _c(offsets, np.uint64)
+        n = len(off) - 1
+        o = {k: np.zeros(n, t) for k, t in self.V2_FIELDS}
+        check(self._L.jrq_v2_decode_verify(self._h, _np_ptr(rec), _np_ptr(off), n,
+                                           *[_np_ptr(o[k]) for k, _ in self.V2_FIELDS]), self._h)
+        return o
+
+    def v2_decode_verify_dev(self, records, offsets, out: dict, n=None):
+        """Device variant: `out` maps the V2_FIELDS names to device tensors."""
+        n = offsets.shape[0] - 1 if n is None else n
+        check(self._L.jrq_v2_decode_verify_dev(self._h, _dev_ptr(records), _dev_ptr(offsets), n,
+                                               *[_dev_ptr(out.get(k)) for k, _ in self.V2_FIELDS]),
+              self._h)
+
     # ---------------------------------------------------------------- RCCL --
     @staticmethod
     def rccl_unique_id() -> bytes:

@@ -121,3 +121,40 @@ def ragged_offsets(seed: int, n: int, max_len: int, start: int = 0, zero_frac: f
     off[0] = start
     off[1:] = start + np.cumsum(lens).astype(np.uint64)
     return off
+
+
+# ------------------------------------------------ stored V2 records (read path) --
+
+V2_HEADER = bytes([0xBB, 0xD2, 0x01, 0, 0, 0])  # LogEntryV2CodecFactory.java:52-60
+
+
+def pb_varint(v: int) -> bytes:
+    """protobuf varint of a 64-bit two's complement integer."""
+    v &= (1 << 64) - 1
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if not v:
+            out.append(b)
+            return bytes(out)
+        out.append(b | 0x80)
+
+
+def v2_records(etype, index, term, payload, offsets, checksum):
+    """DATA entries as V2Encoder writes them (V2Encoder.java:76-130, field order of the
+    generated writeTo, v2/LogOutter.java:518-546): header, type 1, term 2, index 3, data 6,
+    checksum 7.  Returns (records u8[], record offsets u64[N+1])."""
+    n = len(offsets) - 1
+    parts = []
+    roff = np.zeros(n + 1, np.uint64)
+    pos = 0
+    for i in range(n):
+        ln = int(offsets[i + 1] - offsets[i])
+        head = (V2_HEADER + b"\x08" + pb_varint(int(etype[i])) + b"\x10" + pb_varint(int(term[i]))
+                + b"\x18" + pb_varint(int(index[i])) + b"\x32" + pb_varint(ln))
+        tail = b"\x38" + pb_varint(int(checksum[i]))
+        parts += [head, payload[offsets[i]:offsets[i + 1]].tobytes(), tail]
+        pos += len(head) + ln + len(tail)
+        roff[i + 1] = pos
+    return np.frombuffer(b"".join(parts), np.uint8), roff

@@ -1,0 +1,278 @@
+"""V2 log-entry decode + verify on read.
+
+Reference: AutoDetectDecoder / V2Decoder / PBLogEntry (JC/entity/codec/AutoDetectDecoder.java:
+41-52, JC/entity/codec/v2/V2Decoder.java:46-110, v2/LogOutter.java:185-275, log.proto:10-20),
+LogEntry.checksum / isCorrupted (JC/entity/LogEntry.java:88-108,156-158) as LogManagerImpl
+checks on read (JC/core/LogManagerImpl.java:733-745).
+
+Pinning: the reference holds no encoded byte fixtures for this path, and no JVM exists here.
+The record bytes of the codec tests' entry are derived from the protobuf wire format and the
+generated writeTo order (v2/LogOutter.java:518-546) and asserted literally; its checksum is the
+LogEntryTest known answer.  The reference codec tests
+(JT/entity/codec/BaseLogEntryCodecFactoryTest.java, v2/LogEntryV2CodecFactoryTest.java) are
+restated.  Malformed inputs follow protobuf-java 3.5.1's CodedInputStream rules, restated in
+oracle/jraft_oracle.c (jo_v2_decode_batch).
+"""
+import numpy as np
+import pytest
+
+import jraft_oracle as O
+
+HOSTLIKE = (O.V2_PEER_NONCANON, O.V2_PEER_THROWS)
+V2_HOST = 3  # include/jrq.h JRQ_V2_HOST
+
+
+def batch(records):
+    off = np.zeros(len(records) + 1, np.uint64)
+    off[1:] = np.cumsum([len(r) for r in records])
+    buf = np.frombuffer(b"".join(records), np.uint8) if off[-1] else np.zeros(0, np.uint8)
+    return buf, off
+
+
+def codec_entry(**kw):
+    args = dict(etype=1, index=100, term=3, peers=["localhost:99:1", "localhost:100:2"])
+    args.update(kw)
+    return O.v2_encode(**args)
+
+
+# ------------------------------------------------------------------ CPU ---
+
+def test_wire_bytes_known_answer():
+    """The codec tests' entry (NO_OP, LogId(100,3), peers localhost:99:1, localhost:100:2,
+    data "hello") in V2 bytes, from the protobuf wire format (tag = field<<3 | wire type)."""
+    rec = codec_entry(data=b"hello")
+    expect = (bytes([0xBB, 0xD2, 0x01, 0, 0, 0]) + bytes([0x08, 0x01, 0x10, 0x03, 0x18, 0x64])
+              + bytes([0x22, 14]) + b"localhost:99:1" + bytes([0x22, 15]) + b"localhost:100:2"
+              + bytes([0x32, 5]) + b"hello")
+    assert rec == expect
+    d = O.v2_decode_batch(*batch([rec]))
+    assert d["status"][0] == O.V2_OK
+    assert int(d["computed"][0]) == 0x670396DD526CA3BD  # LogEntryTest known answer
+    assert (d["type"][0], d["index"][0], d["term"][0]) == (1, 100, 3)
+    assert d["peer_counts"][0] == 2 and d["data_len"][0] == 5
+
+
+def test_codec_tests_restated():
+    """BaseLogEntryCodecFactoryTest + LogEntryV2CodecFactoryTest, decoder side."""
+    recs = [
+        b"",                                                     # decode(new byte[0]) -> null
+        codec_entry(data=None),                                  # testEncodeDecodeWithoutData
+        codec_entry(data=b"hello"),                              # testEncodeDecodeWithData
+        codec_entry(learners=["192.168.1.1:8081", "192.168.1.2:8081"]),
+        codec_entry(learners=["192.168.1.1:8081", "192.168.1.2:8081"],
+                    old_learners=["192.168.1.1:8081"]),          # testEncodeDecodeWithLearners
+        bytes([0xB8]) + b"v1-encoded",                           # testDecodeV1LogEntry (routing)
+    ]
+    d = O.v2_decode_batch(*batch(recs))
+    assert list(d["status"]) == [O.V2_NULL, O.V2_OK, O.V2_OK, O.V2_OK, O.V2_OK, O.V2_V1]
+    assert d["data_len"][1] == 0 and d["data_len"][2] == 5
+    assert d["peer_counts"][3] == 2 | (2 << 16)
+    assert d["peer_counts"][4] == 2 | (2 << 16) | (1 << 24)
+    # entries carry no checksum field here: never corrupt
+    assert not d["corrupt"].any() and not d["has_checksum"].any()
+
+
+def test_checksum_field_and_corruption():
+    good = O.v2_decode_batch(*batch([codec_entry(data=b"hello")]))["computed"][0]
+    recs = [codec_entry(data=b"hello", checksum=int(good)),
+            codec_entry(data=b"hEllo", checksum=int(good)),      # LogEntryTest: data changed
+            codec_entry(index=1, data=b"hello", checksum=int(good))]
+    d = O.v2_decode_batch(*batch(recs))
+    assert list(d["corrupt"]) == [0, 1, 1]
+    assert int(d["computed"][1]) == 0x69E2DBCC4CF8FE53 and int(d["computed"][2]) == 0xF41932E9037E7E00
+
+
+def test_peer_string_round_trip_classes():
+    assert O.v2_peer_checksum(b"localhost:99:1") == (O.peerid_checksum("localhost", 99, 1), 0)
+    assert O.v2_peer_checksum(b"10.0.0.1:8080") == (O.peerid_checksum("10.0.0.1", 8080, 0), 0)
+    # re-rendered by PeerId.parse/toString
+    assert O.v2_peer_checksum(b"localhost:099:1") == (O.peerid_checksum("localhost", 99, 1), 1)
+    assert O.v2_peer_checksum(b"h:80:0") == (O.peerid_checksum("h", 80, 0), 1)
+    assert O.v2_peer_checksum(b"h::80") == (O.peerid_checksum("h", 80, 0), 1)
+    assert O.v2_peer_checksum(b"h:+80") == (O.peerid_checksum("h", 80, 0), 1)
+    assert O.v2_peer_checksum(b" \t") == (O.crc64(b"0.0.0.0:0"), 1)     # blank -> empty PeerId
+    # IllegalArgumentException("Invalid peer str")
+    for bad in (b"h", b"h:x", b"a:1:2:3", b"h:2147483648", b"h:1:-"):
+        assert O.v2_peer_checksum(bad)[1] == 2, bad
+
+
+def malformed_corpus(seed, n):
+    """Valid and broken records: (bytes, deep) where deep marks groups nested > 2."""
+    rng = np.random.default_rng(seed)
+    F, V = O.pb_field, O.pb_varint
+    H = O.V2_HEADER
+
+    def body(extra=b"", front=b""):
+        return (front + F(1, 0, V(2)) + F(2, 0, V(int(rng.integers(1, 9)))) +
+                F(3, 0, V(int(rng.integers(1, 1 << 40)))) + F(6, 2, V(3) + b"abc") + extra)
+
+    def group(num, depth):
+        inner = F(15, 0, V(5)) + (group(num + 1, depth - 1) if depth > 1 else b"")
+        return F(num, 3, b"") + inner + F(num, 4, b"")
+
+    out = []
+    for _ in range(n):
+        k = int(rng.integers(0, 24))
+        deep = False
+        if k == 0:
+            r = H + body(F(20, 0, V(7)) + F(21, 1, bytes(8)) + F(22, 5, bytes(4)) + F(23, 2, V(2) + b"zz"))
+        elif k == 1:
+            r = H + body(F(2, 2, V(1) + b"x"))           # known number, wrong wire type: unknown
+        elif k == 2:
+            r = H + body(F(1, 0, V(9)))                   # unknown enum value: ignored
+        elif k == 3:
+            r = H + F(1, 0, V(9)) + F(2, 0, V(1)) + F(3, 0, V(1)) + F(6, 2, V(0))  # type unset
+        elif k == 4:
+            r = H + F(1, 0, V(2)) + F(2, 0, V(1)) + F(6, 2, V(0))                   # no index
+        elif k == 5:
+            r = H + body(F(6, 2, V(2) + b"zz") + F(7, 0, V(12345)))  # data twice: last wins
+        elif k == 6:
+            r = H + body(group(30, 1))
+        elif k == 7:
+            r = H + body(group(30, 2))
+        elif k == 8:
+            r = H + body(group(30, 3))
+            deep = True
+        elif k == 9:
+            r = H + body(F(31, 4, b""))                   # END_GROUP at top level -> null
+        elif k == 10:
+            r = H + body(F(30, 3, b"") + F(15, 0, V(1)))  # group never closed -> null
+        elif k == 11:
+            r = H + body(F(30, 3, b"") + F(29, 4, b""))   # mismatched END_GROUP -> null
+        elif k == 12:
+            r = H + body(bytes([0x80] * 11))              # overlong varint tag -> null
+        elif k == 13:
+            r = H + body(F(24, 2, bytes([0xFF, 0xFF, 0xFF, 0xFF, 0x0F])))  # negative length
+        elif k == 14:
+            r = H + body(F(25, 6, b""))                   # invalid wire type 6
+        elif k == 15:
+            r = H + body(bytes([0x00]))                   # tag 0 -> invalid tag
+        elif k == 16:
+            full = codec_entry(data=bytes(rng.integers(0, 256, 40, dtype=np.uint8)))
+            r = full[:int(rng.integers(6, len(full)))]    # truncated
+        elif k == 17:
+            r = bytes([0xBB, 0xD2, 0x02, 0, 0, 0]) + body()   # bad version
+        elif k == 18:
+            r = bytes([0xBB, 0xD2, 0x01])                 # short header
+        elif k == 19:
+            r = codec_entry(peers=["h:080"], data=b"q")   # re-rendered peer
+        elif k == 20:
+            r = codec_entry(old_peers=["nonsense"], data=b"q")  # getPeerId throws
+        elif k == 21:
+            # int32 tag with the 5th byte continued: the extra bytes are discarded
+            r = H + body(bytes([0xA0 | 0x80, 0x81, 0x80, 0x80, 0x80, 0x01]) + V(3))
+        elif k == 22:
+            r = H + body(F(3, 0, bytes([0xFF] * 9 + [0x01])))   # index = -1 (10-byte varint)
+        else:
+            r = codec_entry(etype=int(rng.integers(0, 4)), checksum=int(rng.integers(0, 1 << 63)),
+                            learners=["1.2.3.4:5:-6"], data=bytes(rng.integers(0, 256, int(rng.integers(0, 100)), dtype=np.uint8)))
+        out.append((r, deep))
+    return out
+
+
+def test_malformed_corpus_oracle_classes():
+    corpus = malformed_corpus(5, 400)
+    d = O.v2_decode_batch(*batch([r for r, _ in corpus]))
+    st = set(d["status"].tolist())
+    assert st == {O.V2_OK, O.V2_NULL, O.V2_PEER_NONCANON, O.V2_PEER_THROWS}
+    ok = d["status"] == O.V2_OK
+    assert ok.sum() > 100
+
+
+def random_valid(seed, n, max_len=3000, corrupt_frac=0.05):
+    """Encoder-produced records (the common read path) with ragged data."""
+    rng = np.random.default_rng(seed)
+    recs, expect_corrupt = [], []
+    for i in range(n):
+        t = int(rng.integers(0, 4))
+        peers = [f"10.0.{int(rng.integers(0, 256))}.{j}:{8000 + j}" + (f":{j}" if j % 2 else "")
+                 for j in range(int(rng.integers(0, 6)))] if t == 3 else []
+        oldp = peers[:int(rng.integers(0, len(peers) + 1))] if t == 3 and rng.random() < 0.5 else []
+        ln = int(rng.integers(0, max_len)) if rng.random() < 0.9 else 0
+        data = bytes(rng.integers(0, 256, ln, dtype=np.uint8))
+        idx, term = int(rng.integers(1, 1 << 50)), int(rng.integers(1, 1 << 20))
+        rec = O.v2_encode(t, idx, term, peers=peers, old_peers=oldp, data=data)
+        ck = int(O.v2_decode_batch(*batch([rec]))["computed"][0])
+        bad = rng.random() < corrupt_frac
+        with_ck = rng.random() < 0.9
+        rec = O.v2_encode(t, idx, term, peers=peers, old_peers=oldp, data=data,
+                          checksum=(ck ^ 1 if bad else ck) if with_ck else None)
+        recs.append(rec)
+        expect_corrupt.append(bad and with_ck)
+    return recs, np.array(expect_corrupt)
+
+
+def test_oracle_random_valid_round_trip():
+    recs, bad = random_valid(11, 300)
+    d = O.v2_decode_batch(*batch(recs))
+    assert (d["status"] == O.V2_OK).all()
+    assert np.array_equal(d["corrupt"].astype(bool), bad)
+
+
+# ------------------------------------------------------------------ GPU ---
+
+def check_gpu_vs_oracle(g, o, deep=None):
+    host = g["status"] == V2_HOST
+    exp_host = np.isin(o["status"], HOSTLIKE)
+    if deep is not None:
+        exp_host |= deep
+    assert np.array_equal(host, exp_host)
+    keep = ~host
+    for k in ("status", "type", "index", "term", "stored", "has_checksum", "data_off",
+              "data_len", "peer_counts", "computed", "corrupt"):
+        assert np.array_equal(g[k][keep], o[k][keep]), k
+
+
+@pytest.mark.gpu
+def test_gpu_codec_tests_and_kats(engine):
+    recs = [b"", codec_entry(data=None), codec_entry(data=b"hello"),
+            codec_entry(learners=["192.168.1.1:8081", "192.168.1.2:8081"],
+                        old_learners=["192.168.1.1:8081"]),
+            bytes([0xB8]) + b"v1", codec_entry(data=b"hEllo", checksum=0x670396DD526CA3BD)]
+    buf, off = batch(recs)
+    g = engine.v2_decode_verify(buf, off)
+    o = O.v2_decode_batch(buf, off)
+    check_gpu_vs_oracle(g, o)
+    assert int(g["computed"][2]) == 0x670396DD526CA3BD
+    assert list(g["corrupt"]) == [0, 0, 0, 0, 0, 1]
+
+
+@pytest.mark.gpu
+def test_gpu_malformed_corpus(engine):
+    corpus = malformed_corpus(7, 2000)
+    buf, off = batch([r for r, _ in corpus])
+    g = engine.v2_decode_verify(buf, off)
+    o = O.v2_decode_batch(buf, off)
+    check_gpu_vs_oracle(g, o, np.array([d for _, d in corpus]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,max_len", [(1, 100), (777, 3000), (3000, 20000)])
+def test_gpu_random_valid(engine, n, max_len):
+    recs, bad = random_valid(n, n, max_len)
+    buf, off = batch(recs)
+    g = engine.v2_decode_verify(buf, off)
+    o = O.v2_decode_batch(buf, off)
+    check_gpu_vs_oracle(g, o)
+    assert np.array_equal(g["corrupt"].astype(bool), bad)
+
+
+@pytest.mark.gpu
+def test_gpu_unaligned_base_and_device_variant(engine):
+    import torch
+    recs, _ = random_valid(3, 500, 5000)
+    buf, off = batch(recs)
+    pad = 13
+    big = np.concatenate([np.full(pad, 0x5A, np.uint8), buf, np.full(7, 0xA5, np.uint8)])
+    off2 = off + np.uint64(pad)
+    o = O.v2_decode_batch(big, off2)
+    dev = torch.device("cuda", 0)
+    d_rec = torch.from_numpy(big).to(dev)
+    d_off = torch.from_numpy(off2.view(np.int64)).to(dev)
+    n = len(recs)
+    tdt = {np.uint8: torch.uint8, np.int64: torch.int64, np.uint64: torch.int64, np.uint32: torch.int32}
+    out = {k: torch.empty(n, dtype=tdt[t], device=dev) for k, t in engine.V2_FIELDS}
+    engine.v2_decode_verify_dev(d_rec, d_off, out)
+    engine.synchronize()
+    g = {k: out[k].cpu().numpy().view(t) for k, t in engine.V2_FIELDS}
+    check_gpu_vs_oracle(g, o)
