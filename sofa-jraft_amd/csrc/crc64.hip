@@ -263,6 +263,27 @@ __device__ __forceinline__ void hash_global(const CrcTab& tb, RState& r, const u
   }
 }
 
+// Bytes [p, q) (0 <= p < q <= 64) of the lane's current half-round, from its registers (the
+// transposed ring slot: dword w of the half = v[w >> 2][w & 3]).  Whole 8-byte words inside
+// the range take one slice-by-8 step, the partial words at the range's ends go byte by byte.
+__device__ __forceinline__ void hash_regs(const CrcTab& tb, RState& r, const u32x4 (&v)[4],
+                                          uint32_t p, uint32_t q, const char* lds) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t w0 = v[k >> 1][(k & 1) * 2], w1 = v[k >> 1][(k & 1) * 2 + 1];
+    const uint32_t b = 8u * k, e = b + 8u;
+    if (p <= b && e <= q) {
+      tb.step8(r, w0, w1, lds);
+    } else if (p < e && b < q) {
+      const uint32_t lo = p > b ? p : b, hi = q < e ? q : e;
+      for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t sh = (i - b) * 8u;
+        tb.step1(r, (sh < 32 ? (w0 >> sh) : (w1 >> (sh - 32))) & 0xFFu, lds);
+      }
+    }
+  }
+}
+
 // c * x^(8n) mod P via the global power tables: one 8-lookup pass per set bit of n.
 __device__ __forceinline__ uint64_t crc_shift(uint64_t c, uint64_t n,
                                               const uint64_t* __restrict__ shift) {
@@ -360,6 +381,11 @@ struct SegWalk {
   static constexpr uint32_t kStarted = 1, kLastSeg = 2, kDone = 4;
 };
 
+// kRegs: a half-round holding an entry boundary hashes its bytes from the ring registers
+// (hash_regs) instead of re-reading them from L2 (hash_global).  Faster when boundaries are
+// frequent and unaligned (V2 records, ragged batches), but the extra live ranges spill a few
+// VGPRs at the 128-VGPR budget, which costs ~9 % on boundary-free aligned batches.
+template <bool kRegs>
 __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
   const char* lds = reinterpret_cast<const char*>(lds_tab);
@@ -594,7 +620,12 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
           }
           if (sw.pos >= he) break;
           const uint32_t lim = he < sw.next ? he : sw.next;
-          hash_global(tb, r, A, s0 + sw.pos, s0 + lim, lds);
+          // (not in the data's last half-round: a buffer load reaching past the data end
+          // returns zero for the whole 16 B, so those bytes come from memory)
+          if (kRegs && sw.pos >= hs && s0 + he <= span)
+            hash_regs(tb, r, v, sw.pos - hs, lim - hs, lds);
+          else
+            hash_global(tb, r, A, s0 + sw.pos, s0 + lim, lds);
           sw.pos = lim;
         }
         // settle the slow path's own loads here (vmcnt(0); it waits on its last load
@@ -737,7 +768,10 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64(
     JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {
   args->lanes = static_cast<uint32_t>(grid) * jrq::kCrcBlock;
-  hipLaunchKernelGGL(jrq::crc64_rounds_kernel, dim3(grid), dim3(jrq::kCrcBlock), 0, stream, *args);
+  if (args->regs_slowpath)
+    hipLaunchKernelGGL(jrq::crc64_rounds_kernel<true>, dim3(grid), dim3(jrq::kCrcBlock), 0, stream, *args);
+  else
+    hipLaunchKernelGGL(jrq::crc64_rounds_kernel<false>, dim3(grid), dim3(jrq::kCrcBlock), 0, stream, *args);
   const uint32_t blocks = (args->n + 255) / 256;
   const uint32_t cap = static_cast<uint32_t>(grid) * 8;
   const dim3 fg(blocks < cap ? blocks : cap);

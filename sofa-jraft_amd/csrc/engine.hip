@@ -54,6 +54,8 @@ struct jrq_engine {
   // JRQ_CRC_SEG_BYTES: fixed CRC segment size (0 = automatic, ~payload / lanes); tests use it
   // to force many straddling entries
   uint64_t crc_seg_bytes = 0;
+  int crc_regs = -1;         // JRQ_CRC_REGS: force the boundary path (-1: per call site)
+  uint32_t regs_hint = 0;    // set by host variants around their _dev call (unaligned_bounds)
   uint32_t crc_prio = 1;     // JRQ_CRC_PRIO: progress-stepped wave priority (A/B knob)
   uint32_t crc_seg_map = 1;  // JRQ_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
   uint32_t max_groups = 0;
@@ -167,6 +169,14 @@ int stage_in(jrq_engine* e, int slot, const T* host, size_t count, const T** dev
   return JRQ_OK;
 }
 
+// Entry boundaries off the 64-B half-round grid make the CRC kernel's boundary path frequent:
+// host variants then pick the register boundary path (crc64_rounds_kernel<true>).
+uint32_t unaligned_bounds(const uint64_t* off, uint32_t n) {
+  for (uint32_t i = 1; i <= n; ++i)
+    if ((off[i] - off[0]) & 63u) return 1;
+  return 0;
+}
+
 int crc_dispatch(jrq_engine* e, JrqCrcArgs& a, int log_entry) {
   if (a.n == 0) return JRQ_OK;
   a.slice = e->slice;
@@ -179,6 +189,8 @@ int crc_dispatch(jrq_engine* e, JrqCrcArgs& a, int log_entry) {
   a.seg_bytes = e->crc_seg_bytes;
   a.seg_map = e->crc_seg_map;
   a.prio_steps = e->crc_prio;
+  if (e->crc_regs >= 0) a.regs_slowpath = static_cast<uint32_t>(e->crc_regs);
+  else a.regs_slowpath |= e->regs_hint;
   JRQ_HIP(e, jrq_launch_crc64(&a, log_entry, e->crc_grid, e->stream));
   return JRQ_OK;
 }
@@ -225,6 +237,7 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   e->max_peers = max_peers;
   e->crc_grid = e->num_cus;  // persistent: one 1024-thread workgroup per CU (128 KiB LDS)
   if (const char* v = std::getenv("JRQ_CRC_PRIO")) e->crc_prio = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("JRQ_CRC_REGS")) e->crc_regs = std::atoi(v);
   if (const char* v = std::getenv("JRQ_CRC_SEG_MAP")) e->crc_seg_map = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("JRQ_CRC_SEG_BYTES"))  // rounded up to 256 B by the kernel
     e->crc_seg_bytes = std::strtoull(v, nullptr, 10);
@@ -396,7 +409,13 @@ int jrq_crc64_batch(jrq_engine* e, const uint8_t* payload, const uint64_t* offse
   if ((rc = stage_in(e, 11, rebased.data(), rebased.size(), &doff))) return rc;
   void* dout = nullptr;
   if ((rc = ensure_stage(e, 12, static_cast<size_t>(N) * 8, &dout))) return rc;
-  if ((rc = jrq_crc64_batch_dev(e, dp, doff, N, static_cast<uint64_t*>(dout)))) return rc;
+  JrqCrcArgs a{};
+  a.payload = dp;
+  a.offsets = doff;
+  a.n = N;
+  a.out = static_cast<uint64_t*>(dout);
+  a.regs_slowpath = unaligned_bounds(offsets, N);
+  if ((rc = crc_dispatch(e, a, 0))) return rc;
   JRQ_HIP(e, hipMemcpyAsync(crc_out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
@@ -460,9 +479,11 @@ int jrq_logentry_checksum_batch(jrq_engine* e, const uint8_t* type, const int64_
   void *dout = nullptr, *dcor = nullptr;
   if ((rc = ensure_stage(e, 12, static_cast<size_t>(N) * 8, &dout))) return rc;
   if (corrupt_out && (rc = ensure_stage(e, 13, N, &dcor))) return rc;
-  if ((rc = jrq_logentry_checksum_batch_dev(e, dt, di, dtm, dpx, dp, doff, N, static_cast<uint64_t*>(dout),
-                                            dex, dh, static_cast<uint8_t*>(dcor))))
-    return rc;
+  e->regs_hint = unaligned_bounds(offsets, N);
+  rc = jrq_logentry_checksum_batch_dev(e, dt, di, dtm, dpx, dp, doff, N, static_cast<uint64_t*>(dout),
+                                       dex, dh, static_cast<uint8_t*>(dcor));
+  e->regs_hint = 0;
+  if (rc) return rc;
   JRQ_HIP(e, hipMemcpyAsync(out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
   if (corrupt_out) JRQ_HIP(e, hipMemcpyAsync(corrupt_out, dcor, N, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
@@ -764,6 +785,7 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
   a.offsets = v.off2;
   a.n = 2 * N + 1;
   a.out = static_cast<uint64_t*>(crc2);
+  a.regs_slowpath = 1;  // two unaligned boundaries per record
   if ((rc = crc_dispatch(e, a, 0))) return rc;
   JRQ_HIP(e, jrq_launch_v2_finish(&v, e->num_cus, e->stream));
   return JRQ_OK;

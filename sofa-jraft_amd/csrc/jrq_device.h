@@ -91,6 +91,7 @@ struct JrqCrcArgs {
                            // {start, end (s_memrealtime), HW_ID, XCC_ID}
   uint64_t seg_bytes;      // nonzero: segment size (rounded up to 256 B; tests / tuning)
   uint32_t prio_steps;     // 1: waves lower their priority as they progress (crc64.hip)
+  uint32_t regs_slowpath;  // 1: boundary half-rounds hash from registers (crc64_rounds_kernel<true>)
 };
 
 // Leader lease / alive-quorum check (quorum.hip, lease kernel).

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libjrq.so")
+LIB_PATH = os.environ.get("JRQ_LIB") or os.path.join(os.path.dirname(_PKG), "lib", "libjrq.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_PKG)), "include", "jrq.h")
 
 JRQ_OK = 0
