@@ -428,6 +428,45 @@ def main():
                          "frac": v2_alg / (v2_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS}}
         del d_rec, v2_out
 
+    if not args.no_crc:
+        # C1 (configs[0], the reference's CPU case) on the GPU: 1 group x 3 peers, 1M appended
+        # 256-B DATA entries -- one step = LogEntry.checksum of every entry (stamped on append,
+        # LogManagerImpl.java:313-318) + the group's commit over its 1M pending ballots
+        c1 = W.CONFIGS["C1"]
+        n1 = c1["pending"]
+        e1 = W.entry_batch(n1, c1["entry_bytes"], seed=W.SEED_BASE ^ 1)
+        d1 = {k: to_dev(v, dev) for k, v in e1.items() if isinstance(v, np.ndarray)}
+        out1 = torch.empty(n1, dtype=torch.int64, device=dev)
+        q1 = W.quorum_batch("C1")
+        q1d = {k: to_dev(v, dev) for k, v in q1.items()}
+        c1c = torch.empty(1, dtype=torch.int64, device=dev)
+        c1s = torch.empty(1, dtype=torch.uint8, device=dev)
+
+        def c1_step(i=None):
+            eng.logentry_checksum_batch_dev(d1["etype"], d1["index"], d1["term"], None,
+                                            d1["payload"], d1["offsets"], out1)
+            eng.quorum_epoch_dev(q1d["match"], q1d["pending_index"], q1d["last_appended"],
+                                 q1d["last_committed"], q1d["conf"], c1c, c1s)
+
+        _, c1_ms, c1_b = timed_launches(c1_step, max(10, args.steps), 2, stream, sync)
+        c1_avg = min(c1_b, float(np.mean(c1_ms)))
+        c1_ok = None
+        if rank == 0 and not args.no_cpu:
+            import jraft_oracle as O
+            exp1 = O.logentry_checksum_batch(e1["etype"], e1["index"], e1["term"], None,
+                                             e1["payload"], e1["offsets"])
+            ce, se, _ = O.quorum_epoch_replay(q1["match"], q1["pending_index"],
+                                              q1["last_appended"], q1["last_committed"],
+                                              q1["conf"], chunk=1024)
+            c1_ok = bool(np.array_equal(out1.cpu().numpy().view(np.uint64), exp1)) and \
+                bool(np.array_equal(c1c.cpu().numpy(), ce))
+        extras["C1"] = {
+            "workload": "C1: 1 group x 3 peers, 1M appended 256-B LogEntries: checksum + commitAt",
+            "ms_per_step": c1_avg, "entries_per_s": n1 / (c1_avg * 1e-3),
+            "GBps_payload": n1 * c1["entry_bytes"] / (c1_avg * 1e-3) / 1e9,
+            "bit_exact_vs_oracle": c1_ok}
+        del d1, out1
+
     # leader lease / alive quorum on C3-shaped groups
     rng = np.random.default_rng(rank)
     now_ms, lease_to = 1 << 40, 900
