@@ -83,6 +83,11 @@ def pmc_traffic(*kernels: str):
     return None
 
 
+def traffic_fields(*kernels: str) -> dict:
+    t = pmc_traffic(*kernels)
+    return {"traffic": t["bytes"] if t else None, "traffic_source": t["source"] if t else None}
+
+
 def timed_launches(fn, steps, warmup, stream, sync):
     """warmup untimed, then `steps` launches each bracketed by HIP events on `stream`.
 
@@ -209,6 +214,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-crc", action="store_true")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="quorum + C2 + C5 CRC only (the PMC passes use it: per-kernel counters "
+                         "are averaged over every dispatch of a kernel name)")
     args = ap.parse_args()
 
     import torch
@@ -365,7 +373,7 @@ def main():
 
     # ------------------------------------------------ §8f legs ---------------
     extras = {}
-    if not args.no_crc:
+    if not args.no_crc and not args.headline_only:
         # follower verify on receive: the C5 payload as 64 AppendEntries of 1024 entries
         R = n // 1024
         req_off = torch.arange(0, n + 1, 1024, dtype=torch.int32, device=dev)
@@ -389,7 +397,7 @@ def main():
             "workload": f"{R} AppendEntries requests x 1024 EntryMeta x 16 KiB (C5 payload)",
             "GBps_payload": pay / (ae_avg * 1e-3) / 1e9, "ms_per_batch": ae_avg,
             "bit_exact_vs_oracle": ae_ok}
-    if not args.no_crc:
+    if not args.no_crc and not args.headline_only:
         # read path: the C5 entries as stored V2 records (header + PBLogEntry with the
         # checksum field, 1/1024 corrupted), decoded and verified in one batch
         ck = out.cpu().numpy().view(np.uint64) ^ flip.astype(np.uint64)
@@ -425,10 +433,12 @@ def main():
             "consistent_with_logentry_kernel": v2_ok, "oracle_sample_ok": sample_ok,
             "roofline": {"bound": "hbm", "achieved": v2_alg / (v2_avg * 1e-3) / 1e9,
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": v2_alg / (v2_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS}}
+                         "frac": v2_alg / (v2_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                         **traffic_fields("v2_parse", "crc64_rounds_kernel<true",
+                                          "crc64_finish_kernel<false", "v2_finish")}}
         del d_rec, v2_out
 
-    if not args.no_crc:
+    if not args.no_crc and not args.headline_only:
         # C1 (configs[0], the reference's CPU case) on the GPU: 1 group x 3 peers, 1M appended
         # 256-B DATA entries -- one step = LogEntry.checksum of every entry (stamped on append,
         # LogManagerImpl.java:313-318) + the group's commit over its 1M pending ballots
@@ -467,90 +477,93 @@ def main():
             "bit_exact_vs_oracle": c1_ok}
         del d1, out1
 
-    # leader lease / alive quorum on C3-shaped groups
-    rng = np.random.default_rng(rank)
-    now_ms, lease_to = 1 << 40, 900
-    # rotating timestamp buffers, as for the epochs: no launch re-reads the previous
-    # launch's inputs out of the MALL / L2
-    ts_bufs = [to_dev((now_ms - rng.integers(0, 2 * lease_to, (P, G))).astype(np.int64), dev)
-               for _ in range(QUORUM_EPOCH_BUFFERS)]
-    self_slot = torch.zeros(G, dtype=torch.uint8, device=dev)
-    lead = torch.zeros(G, dtype=torch.int64, device=dev)
-    lok = torch.empty(G, dtype=torch.uint8, device=dev)
-    ldead = torch.empty(G, dtype=torch.int16, device=dev)
-    lconf = epochs[0]["conf"]
+    if not args.headline_only:
+        # leader lease / alive quorum on C3-shaped groups
+        rng = np.random.default_rng(rank)
+        now_ms, lease_to = 1 << 40, 900
+        # rotating timestamp buffers, as for the epochs: no launch re-reads the previous
+        # launch's inputs out of the MALL / L2
+        ts_bufs = [to_dev((now_ms - rng.integers(0, 2 * lease_to, (P, G))).astype(np.int64), dev)
+                   for _ in range(QUORUM_EPOCH_BUFFERS)]
+        self_slot = torch.zeros(G, dtype=torch.uint8, device=dev)
+        lead = torch.zeros(G, dtype=torch.int64, device=dev)
+        lok = torch.empty(G, dtype=torch.uint8, device=dev)
+        ldead = torch.empty(G, dtype=torch.int16, device=dev)
+        lconf = epochs[0]["conf"]
 
-    lstate = {"i": 0}
+        lstate = {"i": 0}
 
-    def lease_step(i=None):
-        ts = ts_bufs[lstate["i"] % QUORUM_EPOCH_BUFFERS]
-        lstate["i"] += 1
-        eng.lease_check_dev(ts, lconf, self_slot, now_ms, lease_to, lok, lead, ldead)
+        def lease_step(i=None):
+            ts = ts_bufs[lstate["i"] % QUORUM_EPOCH_BUFFERS]
+            lstate["i"] += 1
+            eng.lease_check_dev(ts, lconf, self_slot, now_ms, lease_to, lok, lead, ldead)
 
-    _, lease_ms, lease_b = timed_launches(lease_step, args.steps, args.warmup, stream, sync)
-    lease_avg = min(lease_b, float(np.mean(lease_ms)))
-    lb = (8 * P + 28) * G
-    extras["lease_check"] = {
-        "workload": f"{G} leader groups x {P} peers (conf + old conf), checkDeadNodes0",
-        "decisions_per_s": G / (lease_avg * 1e-3), "kernel_ms": lease_avg,
-        "roofline": {"bound": "hbm", "achieved": lb / (lease_avg * 1e-3) / 1e9,
-                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": lb / (lease_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS}}
+        _, lease_ms, lease_b = timed_launches(lease_step, args.steps, args.warmup, stream, sync)
+        lease_avg = min(lease_b, float(np.mean(lease_ms)))
+        lb = (8 * P + 28) * G
+        extras["lease_check"] = {
+            "workload": f"{G} leader groups x {P} peers (conf + old conf), checkDeadNodes0",
+            "decisions_per_s": G / (lease_avg * 1e-3), "kernel_ms": lease_avg,
+            "roofline": {"bound": "hbm", "achieved": lb / (lease_avg * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": lb / (lease_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                         **traffic_fields("lease_check_kernel<5")}}
 
-    # commit fan-out (FSMCaller.doCommitted / ClosureQueue.popClosureUntil) of the C3 epochs:
-    # each epoch's committed[] feeds the fan-out of its groups; every launch starts from
-    # fresh closure queues (restored outside the timed event pair)
-    fan_sets = []
-    for t in epochs:
-        c = torch.empty(G, dtype=torch.int64, device=dev)
-        eng.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
-                             t["last_committed"], t["conf"], c, status)
-        cq_size0 = t["last_appended"] - t["pending_index"] + 1
-        fan_sets.append({"prev": t["last_committed"], "c": c, "la": t["last_committed"],
-                         "cf0": t["pending_index"], "cs0": cq_size0,
-                         "cf": torch.empty_like(c), "cs": torch.empty_like(c)})
-    fan_fc = torch.empty(G, dtype=torch.int64, device=dev)
-    fan_st = torch.empty(G, dtype=torch.uint8, device=dev)
-    fan_list = torch.empty(G, dtype=torch.int32, device=dev)
-    fan_num = torch.zeros(1, dtype=torch.int32, device=dev)
+        # commit fan-out (FSMCaller.doCommitted / ClosureQueue.popClosureUntil) of the C3 epochs:
+        # each epoch's committed[] feeds the fan-out of its groups; every launch starts from
+        # fresh closure queues (restored outside the timed event pair)
+        fan_sets = []
+        for t in epochs:
+            c = torch.empty(G, dtype=torch.int64, device=dev)
+            eng.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
+                                 t["last_committed"], t["conf"], c, status)
+            cq_size0 = t["last_appended"] - t["pending_index"] + 1
+            fan_sets.append({"prev": t["last_committed"], "c": c, "la": t["last_committed"],
+                             "cf0": t["pending_index"], "cs0": cq_size0,
+                             "cf": torch.empty_like(c), "cs": torch.empty_like(c)})
+        fan_fc = torch.empty(G, dtype=torch.int64, device=dev)
+        fan_st = torch.empty(G, dtype=torch.uint8, device=dev)
+        fan_list = torch.empty(G, dtype=torch.int32, device=dev)
+        fan_num = torch.zeros(1, dtype=torch.int32, device=dev)
 
-    def fan_restore():
-        for f in fan_sets:
-            f["cf"].copy_(f["cf0"])
-            f["cs"].copy_(f["cs0"])
+        def fan_restore():
+            for f in fan_sets:
+                f["cf"].copy_(f["cf0"])
+                f["cs"].copy_(f["cs0"])
 
-    def fan_launch(f):
-        eng.commit_fanout_dev(f["prev"], f["c"], f["la"], f["cf"], f["cs"], fan_fc, fan_st,
-                              fan_list, fan_num)
+        def fan_launch(f):
+            eng.commit_fanout_dev(f["prev"], f["c"], f["la"], f["cf"], f["cs"], fan_fc, fan_st,
+                                  fan_list, fan_num)
 
-    fan_restore()
-    fan_launch(fan_sets[0])
-    sync()
-    n_listed = int(fan_num.item())
-    n_pop = int((fan_sets[0]["cf"] != fan_sets[0]["cf0"]).sum().item())
-    fan_ms = []
-    for rep in range(max(1, args.warmup) + max(1, args.steps // 4)):
         fan_restore()
+        fan_launch(fan_sets[0])
         sync()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for f in fan_sets:
-            fan_launch(f)
-        e1.record(stream)
-        sync()
-        if rep >= max(1, args.warmup):
-            fan_ms.append(e0.elapsed_time(e1) / len(fan_sets))
-    fan_avg = float(np.mean(fan_ms))
-    # reads prev/committed/lastApplied/cqFirst/cqSize 40 B, writes firstClosure 8 + status 1,
-    # compaction re-reads status 1; + 16 B queue write-back per popping group, 4 B per listed id
-    fb = 50 * G + 16 * n_pop + 4 * n_listed
-    extras["commit_fanout"] = {
-        "workload": f"{G} groups (C3 epoch output) -> doCommitted/popClosureUntil, "
-                    f"{n_listed} listed, {n_pop} popping",
-        "groups_per_s": G / (fan_avg * 1e-3), "ms_per_launch": fan_avg,
-        "roofline": {"bound": "hbm", "achieved": fb / (fan_avg * 1e-3) / 1e9,
-                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": fb / (fan_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS}}
+        n_listed = int(fan_num.item())
+        n_pop = int((fan_sets[0]["cf"] != fan_sets[0]["cf0"]).sum().item())
+        fan_ms = []
+        for rep in range(max(1, args.warmup) + max(1, args.steps // 4)):
+            fan_restore()
+            sync()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for f in fan_sets:
+                fan_launch(f)
+            e1.record(stream)
+            sync()
+            if rep >= max(1, args.warmup):
+                fan_ms.append(e0.elapsed_time(e1) / len(fan_sets))
+        fan_avg = float(np.mean(fan_ms))
+        # reads prev/committed/lastApplied/cqFirst/cqSize 40 B, writes firstClosure 8 + status 1,
+        # compaction re-reads status 1; + 16 B queue write-back per popping group, 4 B per listed id
+        fb = 50 * G + 16 * n_pop + 4 * n_listed
+        extras["commit_fanout"] = {
+            "workload": f"{G} groups (C3 epoch output) -> doCommitted/popClosureUntil, "
+                        f"{n_listed} listed, {n_pop} popping",
+            "groups_per_s": G / (fan_avg * 1e-3), "ms_per_launch": fan_avg,
+            "roofline": {"bound": "hbm", "achieved": fb / (fan_avg * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": fb / (fan_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                         **traffic_fields("fanout_eval", "fanout_scan", "fanout_compact")}}
 
     # ------------------------------------------------ measured HBM ceiling --
     # device-to-device copy of 2 GiB (torch's copy kernel): read + write bytes / time, the
@@ -618,7 +631,7 @@ def main():
             line["roofline"]["traffic"] = tr["bytes"]
             line["roofline"]["traffic_source"] = tr["source"]
         if crc is not None:
-            tr = pmc_traffic("crc64_rounds_kernel", "crc64_finish_kernel<true")
+            tr = pmc_traffic("crc64_rounds_kernel<false", "crc64_finish_kernel<true")
             if tr is not None:
                 crc["roofline"]["traffic"] = tr["bytes"]
                 crc["roofline"]["traffic_source"] = tr["source"]

@@ -23,8 +23,8 @@ for s in $STEPS; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu ;;
-    pmcf)  run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
-    pmcw)  run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
+    pmcf)  run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --headline-only ;;
+    pmcw)  run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --headline-only ;;
     host)  run host_test 300 ./sofa-jraft_amd/lib/host_test gpu ;;
     probe) run mem_probe 300 ./tools/mem_probe ;;
     sweep) run crc_sweep 600 python tools/crc_sweep.py ${SWEEP_VARIANTS:-} ;;
