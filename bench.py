@@ -523,7 +523,7 @@ def main():
                              "cf": torch.empty_like(c), "cs": torch.empty_like(c)})
         fan_fc = torch.empty(G, dtype=torch.int64, device=dev)
         fan_st = torch.empty(G, dtype=torch.uint8, device=dev)
-        fan_list = torch.empty(G, dtype=torch.int32, device=dev)
+        fan_list = torch.empty((G + 63) // 64, dtype=torch.int64, device=dev)
         fan_num = torch.zeros(1, dtype=torch.int32, device=dev)
 
         def fan_restore():
@@ -553,9 +553,9 @@ def main():
             if rep >= max(1, args.warmup):
                 fan_ms.append(e0.elapsed_time(e1) / len(fan_sets))
         fan_avg = float(np.mean(fan_ms))
-        # reads prev/committed/lastApplied/cqFirst/cqSize 40 B, writes firstClosure 8 + status 1,
-        # compaction re-reads status 1; + 16 B queue write-back per popping group, 4 B per listed id
-        fb = 50 * G + 16 * n_pop + 4 * n_listed
+        # reads prev/committed/lastApplied/cqFirst/cqSize 40 B, writes firstClosure 8 + status 1
+        # + the listed bitmap 1/8; + 16 B queue write-back per popping group
+        fb = 49 * G + G // 8 + 16 * n_pop
         extras["commit_fanout"] = {
             "workload": f"{G} groups (C3 epoch output) -> doCommitted/popClosureUntil, "
                         f"{n_listed} listed, {n_pop} popping",
@@ -563,7 +563,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": fb / (fan_avg * 1e-3) / 1e9,
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": fb / (fan_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                         **traffic_fields("fanout_eval", "fanout_scan", "fanout_compact")}}
+                         **traffic_fields("fanout_eval")}}
 
     # ------------------------------------------------ measured HBM ceiling --
     # device-to-device copy of 2 GiB (torch's copy kernel): read + write bytes / time, the

@@ -232,9 +232,10 @@ int jrq_lease_check(jrq_engine *e, const int64_t *last_rpc_ts, uint64_t ld, uint
  *                      updated in place by the pop
  * Out: status_out[g] (jrq_fanout_status); first_closure_out[g] = popClosureUntil's return
  * for APPLY (the log index of the first popped closure, or committed+1 when none is popped),
- * -1 for INVALID, 0 otherwise; listed_out[0..*num_listed_out) = the APPLY and INVALID group
- * ids in ascending order -- the groups whose state machine must apply
- * (last_applied, committed] (or fail with "Invalid firstClosureIndex"). */
+ * -1 for INVALID, 0 otherwise; listed_bitmap_out[ceil(G/64)]: bit (g & 63) of word g >> 6 is
+ * set for the APPLY and INVALID groups -- those whose state machine must apply
+ * (last_applied, committed] (or fail with "Invalid firstClosureIndex") -- and
+ * *num_listed_out counts them. */
 typedef enum {
     JRQ_FAN_NONE = 0,    /* commit did not move: no onCommitted */
     JRQ_FAN_APPLY = 1,   /* doCommitted pops closures (maybe none) and applies entries */
@@ -246,12 +247,12 @@ int jrq_commit_fanout_dev(jrq_engine *e, uint32_t G, const int64_t *prev_committ
                           const int64_t *committed_dev, const int64_t *last_applied_dev,
                           int64_t *cq_first_inout_dev, int64_t *cq_size_inout_dev,
                           int64_t *first_closure_out_dev, uint8_t *status_out_dev,
-                          uint32_t *listed_out_dev, uint32_t *num_listed_out_dev);
+                          uint64_t *listed_bitmap_out_dev, uint32_t *num_listed_out_dev);
 int jrq_commit_fanout(jrq_engine *e, uint32_t G, const int64_t *prev_committed,
                       const int64_t *committed, const int64_t *last_applied,
                       int64_t *cq_first_inout, int64_t *cq_size_inout,
-                      int64_t *first_closure_out, uint8_t *status_out, uint32_t *listed_out,
-                      uint32_t *num_listed_out);
+                      int64_t *first_closure_out, uint8_t *status_out,
+                      uint64_t *listed_bitmap_out, uint32_t *num_listed_out);
 
 /* ----------------------------------------- V2 decode + verify on read -- */
 

@@ -49,6 +49,7 @@ struct jrq_engine {
   uint64_t* acc = nullptr;    // straddler accumulators
   uint32_t* cnt = nullptr;    // straddler counters
   uint64_t* pieces = nullptr; // per-segment straddler pieces: [2][scratch_len]
+  uint32_t* fan_ctr = nullptr; // commit fan-out {listed sum, blocks done}, zero between launches
   uint32_t scratch_len = 0;
   int crc_grid = 0;
   // JRQ_CRC_SEG_BYTES: fixed CRC segment size (0 = automatic, ~payload / lanes); tests use it
@@ -60,7 +61,7 @@ struct jrq_engine {
   uint32_t crc_seg_map = 1;  // JRQ_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
-  DevBuf stage[24];  // 0-13 host-variant staging, 16-19 AppendEntries scratch, 20 fan-out scratch, 21-23 V2 decode scratch
+  DevBuf stage[24];  // 0-13 host-variant staging, 16-19 AppendEntries scratch, 21-23 V2 decode scratch
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = -1;
   std::string err;
@@ -255,7 +256,9 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   try_hip(hipMalloc(&e->acc, static_cast<size_t>(e->scratch_len) * 8), "hipMalloc(acc)");
   try_hip(hipMalloc(&e->cnt, static_cast<size_t>(e->scratch_len) * 4), "hipMalloc(cnt)");
   try_hip(hipMalloc(&e->pieces, static_cast<size_t>(e->scratch_len) * 16), "hipMalloc(pieces)");
+  try_hip(hipMalloc(&e->fan_ctr, 16), "hipMalloc(fan_ctr)");
   if (rc == JRQ_OK) {
+    try_hip(hipMemset(e->fan_ctr, 0, 16), "zero fan_ctr");
     try_hip(hipMemcpy(e->slice, slice.data(), slice.size() * 8, hipMemcpyHostToDevice), "upload slice");
     try_hip(hipMemcpy(e->shift, shift.data(), shift.size() * 8, hipMemcpyHostToDevice), "upload shift");
     try_hip(hipMemset(e->acc, 0, static_cast<size_t>(e->scratch_len) * 8), "zero acc");
@@ -282,6 +285,7 @@ void jrq_destroy(jrq_engine* e) {
   if (e->acc) (void)hipFree(e->acc);
   if (e->cnt) (void)hipFree(e->cnt);
   if (e->pieces) (void)hipFree(e->pieces);
+  if (e->fan_ctr) (void)hipFree(e->fan_ctr);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
 }
@@ -666,7 +670,7 @@ int jrq_append_entries_verify(jrq_engine* e, uint32_t R, const uint32_t* req_off
 int jrq_commit_fanout_dev(jrq_engine* e, uint32_t G, const int64_t* prev_committed,
                           const int64_t* committed, const int64_t* last_applied,
                           int64_t* cq_first, int64_t* cq_size, int64_t* first_closure_out,
-                          uint8_t* status_out, uint32_t* listed_out, uint32_t* num_listed_out) {
+                          uint8_t* status_out, uint64_t* listed_out, uint32_t* num_listed_out) {
   if (!e) return JRQ_E_INVALID;
   if (!num_listed_out) return fail(e, JRQ_E_INVALID, "null num_listed_out");
   if (G > 0 && (!prev_committed || !committed || !last_applied || !cq_first || !cq_size ||
@@ -677,9 +681,6 @@ int jrq_commit_fanout_dev(jrq_engine* e, uint32_t G, const int64_t* prev_committ
     JRQ_HIP(e, hipMemsetAsync(num_listed_out, 0, 4, e->stream));
     return JRQ_OK;
   }
-  void* tiles;
-  int rc;
-  if ((rc = ensure_stage(e, 20, ((static_cast<size_t>(G) + 4095) / 4096) * 4, &tiles))) return rc;
   JrqFanoutArgs a{};
   a.G = G;
   a.prev_committed = prev_committed;
@@ -691,7 +692,7 @@ int jrq_commit_fanout_dev(jrq_engine* e, uint32_t G, const int64_t* prev_committ
   a.status = status_out;
   a.listed = listed_out;
   a.num_listed = num_listed_out;
-  a.tile_count = static_cast<uint32_t*>(tiles);
+  a.ctr = e->fan_ctr;
   JRQ_HIP(e, jrq_launch_fanout(&a, e->stream));
   return JRQ_OK;
 }
@@ -699,7 +700,7 @@ int jrq_commit_fanout_dev(jrq_engine* e, uint32_t G, const int64_t* prev_committ
 int jrq_commit_fanout(jrq_engine* e, uint32_t G, const int64_t* prev_committed,
                       const int64_t* committed, const int64_t* last_applied, int64_t* cq_first,
                       int64_t* cq_size, int64_t* first_closure_out, uint8_t* status_out,
-                      uint32_t* listed_out, uint32_t* num_listed_out) {
+                      uint64_t* listed_out, uint32_t* num_listed_out) {
   if (!e) return JRQ_E_INVALID;
   if (!num_listed_out) return fail(e, JRQ_E_INVALID, "null num_listed_out");
   if (G == 0) {
@@ -720,12 +721,13 @@ int jrq_commit_fanout(jrq_engine* e, uint32_t G, const int64_t* prev_committed,
   void *dfc, *dst, *dlist, *dnum;
   if ((rc = ensure_stage(e, 8, static_cast<size_t>(G) * 8, &dfc))) return rc;
   if ((rc = ensure_stage(e, 9, G, &dst))) return rc;
-  if ((rc = ensure_stage(e, 12, static_cast<size_t>(G) * 4, &dlist))) return rc;
+  const size_t words = (static_cast<size_t>(G) + 63) / 64;
+  if ((rc = ensure_stage(e, 12, words * 8, &dlist))) return rc;
   if ((rc = ensure_stage(e, 13, 16, &dnum))) return rc;
   int64_t* dcf = const_cast<int64_t*>(dcf0);
   int64_t* dcs = const_cast<int64_t*>(dcs0);
   if ((rc = jrq_commit_fanout_dev(e, G, dprev, dcom, dla, dcf, dcs, static_cast<int64_t*>(dfc),
-                                  static_cast<uint8_t*>(dst), static_cast<uint32_t*>(dlist),
+                                  static_cast<uint8_t*>(dst), static_cast<uint64_t*>(dlist),
                                   static_cast<uint32_t*>(dnum))))
     return rc;
   const size_t b8 = static_cast<size_t>(G) * 8;
@@ -734,9 +736,8 @@ int jrq_commit_fanout(jrq_engine* e, uint32_t G, const int64_t* prev_committed,
   JRQ_HIP(e, hipMemcpyAsync(first_closure_out, dfc, b8, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipMemcpyAsync(status_out, dst, G, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipMemcpyAsync(num_listed_out, dnum, 4, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(listed_out, dlist, words * 8, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
-  if (*num_listed_out)
-    JRQ_HIP(e, hipMemcpy(listed_out, dlist, static_cast<size_t>(*num_listed_out) * 4, hipMemcpyDeviceToHost));
   return JRQ_OK;
 }
 

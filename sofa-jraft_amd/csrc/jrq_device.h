@@ -136,9 +136,9 @@ struct JrqFanoutArgs {
   int64_t* cq_size;               // [G] ClosureQueue size (in/out)
   int64_t* first_closure;         // [G] out: popClosureUntil result
   uint8_t* status;                // [G] out: jrq_fanout_status
-  uint32_t* listed;               // [G] out: APPLY / INVALID group ids, ascending
+  uint64_t* listed;               // [ceil(G/64)] out: bitmap of APPLY / INVALID groups
   uint32_t* num_listed;           // [1] out
-  uint32_t* tile_count;           // scratch [ceil(G/4096)]
+  uint32_t* ctr;                  // engine scratch: u64 {blocks done << 32 | sum}, zero between launches
 };
 
 // V2 log-entry decode + verify (v2_decode.hip).

@@ -27,6 +27,12 @@ def _c(a, dtype):
     return None if a is None else np.ascontiguousarray(a, dtype=dtype)
 
 
+def listed_ids(bitmap, G: int) -> np.ndarray:
+    """Ascending group ids of the set bits of a jrq_commit_fanout bitmap (bit g&63 of word g>>6)."""
+    bits = np.unpackbits(np.ascontiguousarray(bitmap, np.uint64).view(np.uint8), bitorder="little")
+    return np.nonzero(bits[:G])[0].astype(np.uint32)
+
+
 class Engine:
     def __init__(self, device: int = 0, max_groups: int = 1 << 20, max_peers: int = 16):
         self._L = _lib.load()
@@ -229,8 +235,9 @@ class Engine:
 
     # ---------------------------------------------------------- commit fan-out --
     def commit_fanout(self, prev_committed, committed, last_applied, cq_first, cq_size):
-        """Host variant: returns (status u8[G], first_closure i64[G], listed u32[n],
-        cq_first i64[G], cq_size i64[G]) -- FSMCallerImpl.doCommitted per group."""
+        """Host variant: returns (status u8[G], first_closure i64[G], listed u32[n] (ascending
+        group ids decoded from the bitmap), cq_first i64[G], cq_size i64[G]) --
+        FSMCallerImpl.doCommitted per group."""
         prev = _c(prev_committed, np.int64)
         com = _c(committed, np.int64)
         la = _c(last_applied, np.int64)
@@ -239,19 +246,22 @@ class Engine:
         cs = np.array(cq_size, dtype=np.int64, copy=True)
         fc = np.zeros(G, np.int64)
         st = np.zeros(G, np.uint8)
-        listed = np.zeros(max(G, 1), np.uint32)
+        bitmap = np.zeros(max((G + 63) // 64, 1), np.uint64)
         num = np.zeros(1, np.uint32)
         check(self._L.jrq_commit_fanout(self._h, G, _np_ptr(prev), _np_ptr(com), _np_ptr(la),
                                         _np_ptr(cf), _np_ptr(cs), _np_ptr(fc), _np_ptr(st),
-                                        _np_ptr(listed), _np_ptr(num)), self._h)
-        return st, fc, listed[:int(num[0])].copy(), cf, cs
+                                        _np_ptr(bitmap), _np_ptr(num)), self._h)
+        listed = listed_ids(bitmap, G)
+        if len(listed) != int(num[0]):
+            raise _lib.JrqError(-6, "listed bitmap / count mismatch")
+        return st, fc, listed, cf, cs
 
     def commit_fanout_dev(self, prev_committed, committed, last_applied, cq_first, cq_size,
-                          first_closure_out, status_out, listed_out, num_listed_out):
+                          first_closure_out, status_out, listed_bitmap_out, num_listed_out):
         check(self._L.jrq_commit_fanout_dev(
             self._h, committed.shape[0], _dev_ptr(prev_committed), _dev_ptr(committed),
             _dev_ptr(last_applied), _dev_ptr(cq_first), _dev_ptr(cq_size),
-            _dev_ptr(first_closure_out), _dev_ptr(status_out), _dev_ptr(listed_out),
+            _dev_ptr(first_closure_out), _dev_ptr(status_out), _dev_ptr(listed_bitmap_out),
             _dev_ptr(num_listed_out)), self._h)
 
     # --------------------------------------------------- V2 decode + verify --

@@ -201,8 +201,8 @@ def test_gpu_fanout_after_quorum_epoch_dev(engine):
     d_cs = torch.from_numpy(cq_size).to(dev)
     fc = torch.empty(G, dtype=torch.int64, device=dev)
     st = torch.empty(G, dtype=torch.uint8, device=dev)
-    listed = torch.empty(G, dtype=torch.int32, device=dev)
-    num = torch.zeros(1, dtype=torch.int32, device=dev)
+    listed = torch.empty((G + 63) // 64, dtype=torch.int64, device=dev)
+    num = torch.full((1,), 12345, dtype=torch.int32, device=dev)  # the launch resets it
     engine.commit_fanout_dev(t["last_committed"], committed, d_la, d_cf, d_cs, fc, st, listed, num)
     engine.synchronize()
     c = committed.cpu().numpy()
@@ -215,6 +215,7 @@ def test_gpu_fanout_after_quorum_epoch_dev(engine):
     assert np.array_equal(fc.cpu().numpy(), efc)
     assert np.array_equal(d_cf.cpu().numpy(), ecf)
     assert np.array_equal(d_cs.cpu().numpy(), ecs)
-    n = int(num.item())
-    assert np.array_equal(listed[:n].cpu().numpy().astype(np.uint32), elisted)
+    from jraft_amd.engine import listed_ids
+    assert int(num.item()) == len(elisted)
+    assert np.array_equal(listed_ids(listed.cpu().numpy(), G), elisted)
     assert (est == O.FAN_APPLY).sum() > G // 2
