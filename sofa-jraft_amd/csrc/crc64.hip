@@ -34,6 +34,10 @@
 //    L2-resident); they run at most once per piece that does not end its entry.
 #include "jrq_device.h"
 
+#ifndef JRQ_CRC_LOAD_AUX
+#define JRQ_CRC_LOAD_AUX 0  // cache-policy bits of the payload ring loads (2 = nt on gfx950)
+#endif
+
 #ifndef JRQ_CRC_RING
 #define JRQ_CRC_RING 3  // half-round register ring depth of the rounds kernel (3 or 4)
 #endif
@@ -584,10 +588,10 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(                 \
         reinterpret_cast<uint8_t*>((static_cast<uint64_t>(hhi) << 32) | hlo),            \
         static_cast<short>(0), static_cast<int>(hn), 0x00020000);                        \
-    H[0] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa0, 0, 0);                         \
-    H[1] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa1, 0, 0);                         \
-    H[2] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa2, 0, 0);                         \
-    H[3] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa3, 0, 0);                         \
+    H[0] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa0, 0, JRQ_CRC_LOAD_AUX);                         \
+    H[1] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa1, 0, JRQ_CRC_LOAD_AUX);                         \
+    H[2] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa2, 0, JRQ_CRC_LOAD_AUX);                         \
+    H[3] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa3, 0, JRQ_CRC_LOAD_AUX);                         \
     asm volatile("" ::: "memory");                                                       \
   } while (0)
     const uint32_t halves = __builtin_amdgcn_readfirstlane(rounds * 2);
