@@ -219,3 +219,24 @@ def test_gpu_fanout_after_quorum_epoch_dev(engine):
     assert int(num.item()) == len(elisted)
     assert np.array_equal(listed_ids(listed.cpu().numpy(), G), elisted)
     assert (est == O.FAN_APPLY).sum() > G // 2
+
+
+@pytest.mark.gpu
+def test_gpu_fanout_full_size_closed_form(engine):
+    """C3-sized batch (1M groups): the kernel against the numpy closed form (the form the
+    call-by-call replay pins above), including a non-multiple-of-64 tail."""
+    G = (1 << 20) + 37
+    rng = np.random.default_rng(99)
+    prev = rng.integers(0, 1 << 40, G).astype(np.int64)
+    committed = prev + np.where(rng.random(G) < 0.8, rng.integers(1, 1024, G), 0)
+    la = prev - rng.integers(0, 3, G)
+    la[rng.random(G) < 0.03] += 1 << 20
+    cf = prev + 1
+    cs = np.where(rng.random(G) < 0.3, 0, 1024 + rng.integers(0, 8, G)).astype(np.int64)
+    cs[rng.random(G) < 0.01] = 1  # some commits beyond the queue -> INVALID
+    st, fc, listed, gcf, gcs = engine.commit_fanout(prev, committed, la, cf, cs)
+    est, efc, ecf, ecs = closed_form(prev, committed, la, cf, cs)
+    assert np.array_equal(st, est) and np.array_equal(fc, efc)
+    assert np.array_equal(gcf, ecf) and np.array_equal(gcs, ecs)
+    assert np.array_equal(listed, np.nonzero((est == O.FAN_APPLY) | (est == O.FAN_INVALID))[0])
+    assert (est == O.FAN_INVALID).any() and (est == O.FAN_SKIP).any()
