@@ -322,6 +322,35 @@ def main():
 
     c2_wall, c2_ms, c2_b = timed_launches(c2_step, args.steps, args.warmup, stream, sync)
     c2_batched_ms = min(c2_b, float(np.mean(c2_ms)))
+    # C2 is launch-bound one epoch at a time: K successive epochs per launch, the group state
+    # carried between them on the GPU (jrq_quorum_epochs_dev)
+    KE = 64
+    ser = W.quorum_epoch_series("C2", KE)
+    ser_d = {k: to_dev(v, dev) for k, v in ser.items()}
+    kc = torch.empty((KE, G2), dtype=torch.int64, device=dev)
+    ks = torch.empty((KE, G2), dtype=torch.uint8, device=dev)
+
+    def c2k_step(i=None):
+        eng.quorum_epochs_dev(ser_d["match"], ser_d["pending_index"], ser_d["last_appended"],
+                              ser_d["last_committed"], ser_d["conf"], kc, ks)
+
+    _, c2k_ms, c2k_b = timed_launches(c2k_step, args.steps, args.warmup, stream, sync)
+    c2k_avg = min(c2k_b, float(np.mean(c2k_ms)))
+    c2k_ok = None
+    if rank == 0 and not args.no_cpu:  # oracle on the first 64 groups, all KE epochs
+        import jraft_oracle as O
+        sub = 64
+        pi = ser["pending_index"][:sub].copy()
+        lc = ser["last_committed"][:sub].copy()
+        got = kc.cpu().numpy()
+        c2k_ok = True
+        for k in range(KE):
+            ce, _, _ = O.quorum_epoch_replay(ser["match"][k][:, :sub], pi,
+                                             ser["last_appended"][k][:sub], lc,
+                                             ser["conf"][:sub], chunk=1024)
+            pi = np.where((pi != 0) & (ce > lc), ce + 1, pi)
+            lc = ce
+            c2k_ok = c2k_ok and bool(np.array_equal(got[k, :sub], ce))
 
     # ------------------------------------------------ CRC64 (C5) ------------
     crc = None
@@ -623,7 +652,15 @@ def main():
             "C2": {"workload": "C2: 10k groups x 3 peers x 1k pending (configs[1])",
                    "decisions_per_s": G2 * args.steps / c2_wall,
                    "entry_ballots_per_s": G2 * 1024 * args.steps / c2_wall,
-                   "kernel_ms": c2_batched_ms},
+                   "kernel_ms": c2_batched_ms,
+                   "batched_epochs": {
+                       "epochs_per_launch": KE, "kernel_ms": c2k_avg,
+                       "decisions_per_s": G2 * KE / (c2k_avg * 1e-3),
+                       # per group-epoch: match 8P + lastAppended 8 read, committed 8 + status 1
+                       # written (41 B at P = 3); pendingIndex/lastCommitted/conf once per group
+                       "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBPS,
+                                    "achieved": (G2 * KE * 41 + G2 * 24) / (c2k_avg * 1e-3) / 1e9},
+                       "bit_exact_vs_oracle_64_groups": c2k_ok}},
             "next_rows": extras,
         }
         tr = pmc_traffic("quorum_epoch_pair_kernel<5")

@@ -138,6 +138,19 @@ int jrq_quorum_epoch_dev(jrq_engine *e, const jrq_group_batch *in_dev, int64_t *
 int jrq_quorum_epoch(jrq_engine *e, const jrq_group_batch *in_host, int64_t *committed_out,
                      uint8_t *status_out, uint32_t G);
 
+/* K successive epochs of the same G groups in one launch (the launch-bound small-G case,
+ * e.g. C2's 10k groups; SURVEY.md §7 hard part 4).  Epoch k reads
+ *   match + k*match_epoch_ld   (rows of in->match_ld, as jrq_quorum_epoch)
+ *   last_appended + k*la_epoch_ld
+ * and the group state carried from epoch k-1 exactly as BallotBox carries it: a commit sets
+ * lastCommittedIndex and pendingIndex = lastCommittedIndex + 1 (JC/core/BallotBox.java:
+ * 131-134); pendingIndex 0 (not leader) stays 0.  in->pending_index / last_committed / conf
+ * are the state before epoch 0 (one conf per group: run_off must be NULL).
+ * Out: committed_out[k*G + g], status_out[k*G + g] after each epoch. */
+int jrq_quorum_epochs_dev(jrq_engine *e, const jrq_group_batch *in_dev, uint32_t K,
+                          uint64_t match_epoch_ld, uint64_t la_epoch_ld,
+                          int64_t *committed_out_dev, uint8_t *status_out_dev, uint32_t G);
+
 /* --------------------------------------------------------------- checksum -- */
 
 /* crc_out[i] = CrcUtil.crc64(payload[offsets[i] .. offsets[i+1]))

@@ -21,6 +21,9 @@
 extern "C" hipError_t jrq_launch_crc64(JrqCrcArgs* args, int log_entry, int grid,
                                        hipStream_t stream);
 extern "C" hipError_t jrq_launch_quorum(const JrqQuorumArgs* args, int num_cus, hipStream_t stream);
+extern "C" hipError_t jrq_launch_quorum_epochs(const JrqQuorumArgs* args, uint32_t K,
+                                               uint64_t match_eld, uint64_t la_eld,
+                                               int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_meta(const JrqAeArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_lease(const JrqLeaseArgs* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_fanout(const JrqFanoutArgs* a, hipStream_t stream);
@@ -380,6 +383,34 @@ int jrq_quorum_epoch(jrq_engine* e, const jrq_group_batch* in, int64_t* committe
 }
 
 // --------------------------------------------------------------- checksum ---
+
+int jrq_quorum_epochs_dev(jrq_engine* e, const jrq_group_batch* in, uint32_t K,
+                          uint64_t match_eld, uint64_t la_eld, int64_t* committed_out,
+                          uint8_t* status_out, uint32_t G) {
+  if (!e || !in) return e ? fail(e, JRQ_E_INVALID, "null batch") : JRQ_E_INVALID;
+  if (G == 0 || K == 0) return JRQ_OK;
+  if (!committed_out || !status_out) return fail(e, JRQ_E_INVALID, "null output");
+  if (in->num_peers == 0 || in->num_peers > JRQ_MAX_PEERS || in->match_ld < G || !in->match ||
+      !in->pending_index || !in->last_appended || !in->last_committed || !in->conf)
+    return fail(e, JRQ_E_INVALID, "bad num_peers / match_ld / null array");
+  if (in->run_off) return fail(e, JRQ_E_INVALID, "conf runs are not supported across epochs");
+  if (K > 1 && (match_eld < static_cast<uint64_t>(in->num_peers) * in->match_ld || la_eld < G))
+    return fail(e, JRQ_E_INVALID, "epoch strides overlap");
+  DeviceGuard guard(e->device);
+  JrqQuorumArgs a{};
+  a.match = in->match;
+  a.pending_index = in->pending_index;
+  a.last_appended = in->last_appended;
+  a.last_committed = in->last_committed;
+  a.conf = in->conf;
+  a.num_peers = in->num_peers;
+  a.match_ld = in->match_ld;
+  a.committed = committed_out;
+  a.status = status_out;
+  a.G = G;
+  JRQ_HIP(e, jrq_launch_quorum_epochs(&a, K, match_eld, la_eld, e->num_cus, e->stream));
+  return JRQ_OK;
+}
 
 int jrq_crc64_batch_dev(jrq_engine* e, const uint8_t* payload, const uint64_t* offsets, uint32_t N,
                         uint64_t* crc_out) {

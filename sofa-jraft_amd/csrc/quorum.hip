@@ -203,6 +203,49 @@ __global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a)
   }
 }
 
+// K successive epochs of the same groups in one launch (hard part 4: a
+// 10k-group epoch is launch-bound).  Between epochs the group state moves as BallotBox
+// moves it: a commit sets lastCommittedIndex and pendingIndex = lastCommittedIndex + 1
+// (BallotBox.java:131-134); a group that is not the leader stays so.  Epoch k reads its
+// own match snapshot and lastAppended (entries appended since); the conf is per group.
+// One lane per group; the loads of kEpochUnroll epochs are issued before their decisions.
+constexpr uint32_t kEpochUnroll = 4;
+
+template <int P>
+__global__ __launch_bounds__(256) void quorum_epochs_kernel(JrqQuorumArgs a, uint32_t K,
+                                                            uint64_t match_eld, uint64_t la_eld) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G; g += stride) {
+    int64_t pi = a.pending_index[g];
+    int64_t lc = a.last_committed[g];
+    const uint64_t cw = a.conf[g];
+    for (uint32_t k0 = 0; k0 < K; k0 += kEpochUnroll) {
+      int64_t m[kEpochUnroll][P], la[kEpochUnroll];
+#pragma unroll
+      for (uint32_t u = 0; u < kEpochUnroll; ++u) {
+        if (k0 + u >= K) break;
+        const size_t k = k0 + u;
+        la[u] = a.last_appended[k * la_eld + g];
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+          m[u][p] = a.match[k * match_eld + static_cast<size_t>(p) * a.match_ld + g];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kEpochUnroll; ++u) {
+        if (k0 + u >= K) break;
+        const size_t k = k0 + u;
+        int64_t out;
+        uint8_t st;
+        decide_single<P>(pi, la[u], lc, cw, m[u], out, st);
+        a.committed[k * a.G + g] = out;
+        a.status[k * a.G + g] = st;
+        if (pi != 0 && out > lc) pi = out + 1;
+        lc = out;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ lease ---
 // NodeImpl.checkDeadNodes0 (jraft-core/.../core/NodeImpl.java:1970-2000) for one conf:
 // the leader itself is alive; another member is alive when now - lastRpcSendTimestamp <=
@@ -326,6 +369,28 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
     else                                                                                       \
       hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, 1, true>), dim3(grid), blk, 0,     \
                          stream, *args);                                                       \
+    break;
+    JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
+    JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
+    JRQ_CASE(15) JRQ_CASE(16)
+#undef JRQ_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum_epochs(
+    const JrqQuorumArgs* args, uint32_t K, uint64_t match_eld, uint64_t la_eld, int num_cus,
+    hipStream_t stream) {
+  const uint64_t need = (static_cast<uint64_t>(args->G) + 255) / 256;
+  const uint64_t cap = static_cast<uint64_t>(num_cus) * 8;
+  const dim3 grid(static_cast<unsigned>(need < cap ? (need ? need : 1) : cap)), blk(256);
+  switch (args->num_peers) {
+#define JRQ_CASE(P)                                                                      \
+  case P:                                                                                \
+    hipLaunchKernelGGL(jrq::quorum_epochs_kernel<P>, grid, blk, 0, stream, *args, K,     \
+                       match_eld, la_eld);                                               \
     break;
     JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
     JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)

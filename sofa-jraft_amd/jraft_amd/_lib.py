@@ -59,6 +59,8 @@ SIGNATURES = [
     ("jrq_host_unregister", C.c_int, [_V]),
     ("jrq_quorum_epoch_dev", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
     ("jrq_quorum_epoch", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
+    ("jrq_quorum_epochs_dev", C.c_int,
+     [_V, C.POINTER(GroupBatch), C.c_uint32, C.c_uint64, C.c_uint64, _V, _V, C.c_uint32]),
     ("jrq_crc64_batch_dev", C.c_int, [_V, _V, _V, C.c_uint32, _V]),
     ("jrq_crc64_batch", C.c_int, [_V, _V, _V, C.c_uint32, _V]),
     ("jrq_logentry_checksum_batch_dev", C.c_int,

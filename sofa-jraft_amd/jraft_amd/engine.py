@@ -125,6 +125,18 @@ class Engine:
         check(self._L.jrq_quorum_epoch_dev(self._h, C.byref(b), _dev_ptr(committed_out),
                                            _dev_ptr(status_out), G), self._h)
 
+    def quorum_epochs_dev(self, match, pending_index, last_appended, last_committed, conf,
+                          committed_out, status_out):
+        """K epochs in one launch: match [K, P, ld], last_appended [K, G] (torch tensors);
+        committed_out / status_out [K, G]."""
+        K, P = match.shape[0], match.shape[1]
+        G = pending_index.shape[0]
+        b = self._batch(_dev_ptr, match, pending_index, last_appended, last_committed, conf,
+                        None, None, None, num_peers=P, match_ld=match.stride(1), num_runs=0)
+        check(self._L.jrq_quorum_epochs_dev(self._h, C.byref(b), K, match.stride(0),
+                                            last_appended.stride(0), _dev_ptr(committed_out),
+                                            _dev_ptr(status_out), G), self._h)
+
     # ------------------------------------------------------------ checksum --
     def crc64_batch(self, payload, offsets):
         payload = _c(payload, np.uint8)

@@ -158,3 +158,25 @@ def v2_records(etype, index, term, payload, offsets, checksum):
         pos += len(head) + ln + len(tail)
         roff[i + 1] = pos
     return np.frombuffer(b"".join(parts), np.uint8), roff
+
+
+def quorum_epoch_series(cfg: str, K: int, groups: int | None = None, step: int = 16,
+                        seed: int | None = None):
+    """K successive epochs of one group batch: epoch 0 = quorum_batch(cfg); each later epoch
+    appends `step` entries per group (lastAppended grows) and every follower's match index
+    moves forward by 0..2*step, capped at lastAppended (acks stay contiguous, Replicator.java:
+    1387-1401).  Returns dict(match[K][P][G], last_appended[K][G], pending_index,
+    last_committed, conf) -- the state before epoch 0 plus per-epoch snapshots."""
+    b = quorum_batch(cfg, groups=groups, seed=seed)
+    P, G = b["match"].shape
+    match = np.empty((K, P, G), np.int64)
+    la = np.empty((K, G), np.int64)
+    match[0], la[0] = b["match"], b["last_appended"]
+    s = (SEED_BASE ^ 0xE0) if seed is None else seed ^ 0xE0
+    for k in range(1, K):
+        la[k] = la[k - 1] + step
+        adv = (splitmix64(s + k, P * G).reshape(P, G) % np.uint64(2 * step + 1)).astype(np.int64)
+        match[k] = np.minimum(match[k - 1] + adv, la[k])
+        match[k, 0] = la[k]  # the leader's own stable ack
+    return dict(match=match, last_appended=la, pending_index=b["pending_index"],
+                last_committed=b["last_committed"], conf=b["conf"])
