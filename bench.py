@@ -338,6 +338,7 @@ def main():
     c2k_avg = min(c2k_b, float(np.mean(c2k_ms)))
     c2k_ok = None
     if rank == 0 and not args.no_cpu:  # oracle on the first 64 groups, all KE epochs
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import jraft_oracle as O
         sub = 64
         pi = ser["pending_index"][:sub].copy()

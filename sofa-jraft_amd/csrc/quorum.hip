@@ -208,12 +208,12 @@ __global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a)
 // moves it: a commit sets lastCommittedIndex and pendingIndex = lastCommittedIndex + 1
 // (BallotBox.java:131-134); a group that is not the leader stays so.  Epoch k reads its
 // own match snapshot and lastAppended (entries appended since); the conf is per group.
-// One lane per group; the loads of kEpochUnroll epochs are issued before their decisions.
-constexpr uint32_t kEpochUnroll = 4;
-
+// One lane per group; the loads of 4 epochs are issued before their decisions (8 measured
+// slower on C2: 31.6 vs 27.8 us for 64 epochs).
 template <int P>
 __global__ __launch_bounds__(256) void quorum_epochs_kernel(JrqQuorumArgs a, uint32_t K,
                                                             uint64_t match_eld, uint64_t la_eld) {
+  constexpr uint32_t kEpochUnroll = 4;
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G; g += stride) {
     int64_t pi = a.pending_index[g];
