@@ -353,6 +353,21 @@ def main():
             lc = ce
             c2k_ok = c2k_ok and bool(np.array_equal(got[k, :sub], ce))
 
+    # end to end from host buffers (the JNI/DirectByteBuffer path): H2D of the epoch's SoA,
+    # the kernel, D2H of committed/status -- PCIe-inclusive, never the headline value
+    hb = W.quorum_batch(cfg, groups=G, group_offset=rank * G)
+    eng.quorum_epoch(hb["match"], hb["pending_index"], hb["last_appended"],
+                     hb["last_committed"], hb["conf"])
+    t0 = time.perf_counter()
+    e2e_reps = 5
+    for _ in range(e2e_reps):
+        eng.quorum_epoch(hb["match"], hb["pending_index"], hb["last_appended"],
+                         hb["last_committed"], hb["conf"])
+    e2e_s = (time.perf_counter() - t0) / e2e_reps
+    e2e = {"decisions_per_s": G / e2e_s, "ms_per_epoch": e2e_s * 1e3,
+           "note": "jrq_quorum_epoch host variant (pageable numpy buffers): H2D + kernel + D2H"}
+    del hb
+
     # ------------------------------------------------ CRC64 (C5) ------------
     crc = None
     if not args.no_crc:
@@ -663,6 +678,7 @@ def main():
                                     "achieved": (G2 * KE * 41 + G2 * 24) / (c2k_avg * 1e-3) / 1e9},
                        "bit_exact_vs_oracle_64_groups": c2k_ok}},
             "next_rows": extras,
+            "end_to_end_host_buffers": e2e,
         }
         tr = pmc_traffic("quorum_epoch_pair_kernel<5")
         if tr is not None:
