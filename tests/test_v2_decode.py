@@ -276,3 +276,54 @@ def test_gpu_unaligned_base_and_device_variant(engine):
     engine.synchronize()
     g = {k: out[k].cpu().numpy().view(t) for k, t in engine.V2_FIELDS}
     check_gpu_vs_oracle(g, o)
+
+
+def mutated_corpus(seed, n):
+    """Encoder-produced records with random byte flips, insertions and truncations: every
+    decoder branch (varint limits, tags, lengths, groups, required fields) gets random input."""
+    rng = np.random.default_rng(seed)
+    recs, _ = random_valid(seed, n, max_len=200, corrupt_frac=0.0)
+    out = []
+    for r in recs:
+        b = bytearray(r)
+        for _ in range(int(rng.integers(1, 4))):
+            op = int(rng.integers(0, 4))
+            pos = int(rng.integers(0, len(b))) if b else 0
+            if op == 0 and b:
+                b[pos] = int(rng.integers(0, 256))
+            elif op == 1 and b:
+                b[pos] ^= 1 << int(rng.integers(0, 8))
+            elif op == 2:
+                b[pos:pos] = bytes(rng.integers(0, 256, int(rng.integers(1, 6)), dtype=np.uint8))
+            elif op == 3 and len(b) > 7:
+                del b[int(rng.integers(6, len(b))):]
+        if rng.random() < 0.7 and len(b) >= 3:
+            b[0:3] = bytes([0xBB, 0xD2, 0x01])  # keep most records on the V2 path
+        out.append(bytes(b))
+    return out
+
+
+def test_mutated_corpus_oracle_mix():
+    d = O.v2_decode_batch(*batch(mutated_corpus(3, 1500)))
+    st = d["status"]
+    assert (st == O.V2_OK).sum() > 100 and (st == O.V2_NULL).sum() > 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [21, 22])
+def test_gpu_mutated_corpus(engine, seed):
+    recs = mutated_corpus(seed, 4000)
+    buf, off = batch(recs)
+    g = engine.v2_decode_verify(buf, off)
+    o = O.v2_decode_batch(buf, off)
+    # groups nested deeper than 2 can appear by mutation and the kernel may hand those to the
+    # host: allowed only where some byte could be a START_GROUP tag (wire type 3)
+    deep = np.array([any((b & 7) == 3 for b in r[6:]) for r in recs])
+    host = g["status"] == V2_HOST
+    exp_host = np.isin(o["status"], HOSTLIKE)
+    assert not (exp_host & ~host).any()
+    assert not (host & ~exp_host & ~deep).any()
+    keep = ~host
+    for k in ("status", "type", "index", "term", "stored", "has_checksum", "data_off",
+              "data_len", "peer_counts", "computed", "corrupt"):
+        assert np.array_equal(g[k][keep], o[k][keep]), k
