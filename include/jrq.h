@@ -162,6 +162,21 @@ int jrq_crc64_batch_dev(jrq_engine *e, const uint8_t *payload_dev, const uint64_
 int jrq_crc64_batch(jrq_engine *e, const uint8_t *payload, const uint64_t *offsets, uint32_t N,
                     uint64_t *crc_out);
 
+/* Streaming CRC64 as a java.util.zip.Checksum (JC/util/CRC64.java:26,106-126), batched over S
+ * independent streams: the RheaKV snapshot archive checksum, fed by CheckedOutputStream /
+ * CheckedInputStream around ZipUtil.compress / decompress
+ * (RK/storage/AbstractKVStoreSnapshotFile.java:121-123,139-143; RK/util/ZipUtil.java:45-94).
+ * For each s: state[s] = the CRC64 register after CRC64.update(chunk_s) where
+ * chunk_s = payload[offsets[s] .. offsets[s+1]) and the register held state[s] before, i.e.
+ *   state[s] = state[s] * x^(8 |chunk_s|) ^ crc64(chunk_s)   (mod the ECMA-182 poly).
+ * getValue() = state[s]; reset() = set it to 0 (host-side, no call).  Successive calls on
+ * the same state array continue the streams, so an archive can be fed in pieces of any size.
+ * The _dev variant keeps state on the device (in/out); the host variant copies it both ways. */
+int jrq_crc64_stream_update_dev(jrq_engine *e, uint64_t *state_dev, const uint8_t *payload_dev,
+                                const uint64_t *offsets_dev, uint32_t S);
+int jrq_crc64_stream_update(jrq_engine *e, uint64_t *state, const uint8_t *payload,
+                            const uint64_t *offsets, uint32_t S);
+
 /* out[i] = LogEntry.checksum() of entry i (JC/entity/LogEntry.java:88-108):
  *   (uint64)type[i] ^ LogId(index[i],term[i]).checksum() ^ peer_xor[i] ^ crc64(data_i)
  * with LogId.checksum = crc64(BE64(index) || BE64(term)) (JC/entity/LogId.java:45-50) and

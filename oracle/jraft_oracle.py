@@ -133,6 +133,23 @@ def crc64_batch(payload: np.ndarray, offsets: np.ndarray) -> np.ndarray:
     return out
 
 
+def crc64_stream_update(state: np.ndarray, payload: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    """S streaming java.util.zip.Checksum objects (`new CRC64()`, JC/util/CRC64.java:26), each
+    fed one chunk by CRC64.update(byte[],off,len) (:106-110) starting from register state[s],
+    as CheckedOutputStream/CheckedInputStream do around ZipUtil.compress/decompress
+    (RK/util/ZipUtil.java:45-94; RK/storage/AbstractKVStoreSnapshotFile.java:121,139).
+    Returns the registers after the chunks (getValue(), :119-121)."""
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    out = np.array(state, dtype=np.uint64, copy=True)
+    L = lib()
+    base = payload.ctypes.data
+    for s in range(len(offsets) - 1):
+        o0, o1 = int(offsets[s]), int(offsets[s + 1])
+        out[s] = L.jo_crc64_update(int(out[s]), C.c_void_p(base + o0), o1 - o0)
+    return out
+
+
 def logid_checksum(index: int, term: int) -> int:
     return int(lib().jo_logid_checksum(index, term))
 

@@ -30,6 +30,10 @@ extern "C" hipError_t jrq_launch_fanout(const JrqFanoutArgs* a, hipStream_t stre
 extern "C" hipError_t jrq_launch_v2_parse(const JrqV2Args* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_v2_finish(const JrqV2Args* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_first_corrupt(const JrqAeArgs* a, hipStream_t stream);
+extern "C" hipError_t jrq_launch_crc64_stream_combine(uint64_t* state, const uint64_t* chunk_crc,
+                                                      const uint64_t* off, uint32_t S,
+                                                      const uint64_t* shift, int num_cus,
+                                                      hipStream_t stream);
 
 namespace {
 
@@ -64,7 +68,7 @@ struct jrq_engine {
   uint32_t crc_seg_map = 1;  // JRQ_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
-  DevBuf stage[24];  // 0-13 host-variant staging, 16-19 AppendEntries scratch, 21-23 V2 decode scratch
+  DevBuf stage[24];  // 0-13 host-variant staging, 14 stream-update chunk CRCs, 16-19 AppendEntries scratch, 21-23 V2 decode scratch
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = -1;
   std::string err;
@@ -452,6 +456,55 @@ int jrq_crc64_batch(jrq_engine* e, const uint8_t* payload, const uint64_t* offse
   a.regs_slowpath = unaligned_bounds(offsets, N);
   if ((rc = crc_dispatch(e, a, 0))) return rc;
   JRQ_HIP(e, hipMemcpyAsync(crc_out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
+int jrq_crc64_stream_update_dev(jrq_engine* e, uint64_t* state, const uint8_t* payload,
+                                const uint64_t* offsets, uint32_t S) {
+  if (!e) return JRQ_E_INVALID;
+  if (S == 0) return JRQ_OK;
+  if (!state || !payload || !offsets) return fail(e, JRQ_E_INVALID, "null pointer");
+  DeviceGuard guard(e->device);
+  void* chunk = nullptr;
+  int rc;
+  if ((rc = ensure_stage(e, 14, static_cast<size_t>(S) * 8, &chunk))) return rc;
+  JrqCrcArgs a{};
+  a.payload = payload;
+  a.offsets = offsets;
+  a.n = S;
+  a.out = static_cast<uint64_t*>(chunk);
+  if ((rc = crc_dispatch(e, a, 0))) return rc;
+  JRQ_HIP(e, jrq_launch_crc64_stream_combine(state, a.out, offsets, S, e->shift, e->num_cus,
+                                             e->stream));
+  return JRQ_OK;
+}
+
+int jrq_crc64_stream_update(jrq_engine* e, uint64_t* state, const uint8_t* payload,
+                            const uint64_t* offsets, uint32_t S) {
+  if (!e) return JRQ_E_INVALID;
+  if (S == 0) return JRQ_OK;
+  if (!state || !payload || !offsets) return fail(e, JRQ_E_INVALID, "null pointer");
+  DeviceGuard guard(e->device);
+  int rc;
+  const uint64_t lo = offsets[0], hi = offsets[S];
+  if (hi < lo) return fail(e, JRQ_E_INVALID, "offsets not monotone");
+  for (uint32_t s = 0; s < S; ++s)
+    if (offsets[s + 1] < offsets[s]) return fail(e, JRQ_E_INVALID, "offsets not monotone");
+  const uint8_t* dp;
+  const uint64_t* doff;
+  const uint64_t* dstate;
+  if ((rc = stage_in(e, 10, payload + lo, hi - lo, &dp))) return rc;
+  std::vector<uint64_t> rebased(offsets, offsets + S + 1);
+  for (auto& o : rebased) o -= lo;
+  if ((rc = stage_in(e, 11, rebased.data(), rebased.size(), &doff))) return rc;
+  if ((rc = stage_in(e, 13, static_cast<const uint64_t*>(state), S, &dstate))) return rc;
+  uint64_t* ds = const_cast<uint64_t*>(dstate);
+  e->regs_hint = unaligned_bounds(offsets, S);
+  rc = jrq_crc64_stream_update_dev(e, ds, dp, doff, S);
+  e->regs_hint = 0;
+  if (rc) return rc;
+  JRQ_HIP(e, hipMemcpyAsync(state, ds, static_cast<size_t>(S) * 8, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }

@@ -162,6 +162,26 @@ uint64_t CrcUtil::crc64(Engine& eng, const uint8_t* array, size_t offset, size_t
   return eng.crc64(one)[0];
 }
 
+void CRC64::update(const uint8_t* b, size_t off, size_t len) {
+  if (len == 0) return;
+  if (b == nullptr) throw std::invalid_argument("null buffer");  // Java: NullPointerException
+  buf_.insert(buf_.end(), b + off, b + off + len);
+  maybeFlush();
+}
+
+void CRC64::flush() {
+  if (buf_.empty()) return;
+  const uint64_t offs[2] = {0, buf_.size()};
+  throwIfError(jrq_crc64_stream_update(eng_->raw(), &crc_, buf_.data(), offs, 1), eng_->raw(),
+               "jrq_crc64_stream_update");
+  buf_.clear();
+}
+
+uint64_t CRC64::getValue() {
+  flush();
+  return crc_;
+}
+
 // --------------------------------------------------------------- ballot box
 
 GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)

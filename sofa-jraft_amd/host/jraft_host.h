@@ -114,6 +114,28 @@ class CrcUtil {
   }
 };
 
+// CRC64 implements java.util.zip.Checksum (CRC64.java:26,100-126), the checksum RheaKV
+// wraps around snapshot archives (AbstractKVStoreSnapshotFile.java:121-123,139-143 via
+// CheckedOutputStream/CheckedInputStream in ZipUtil.java:45-94).  Bytes are buffered on the
+// host (as the BufferedOutputStream in front of the checked stream does) and folded into
+// the register on the GPU by jrq_crc64_stream_update in chunks of up to flushBytes.
+class CRC64 {
+ public:
+  explicit CRC64(Engine& eng, size_t flushBytes = 64u << 20) : eng_(&eng), flush_(flushBytes) {}
+  void update(int b) { buf_.push_back(static_cast<uint8_t>(b)); maybeFlush(); }  // :100-103
+  void update(const uint8_t* b, size_t off, size_t len);                        // :106-110
+  uint64_t getValue();                                                          // :119-121
+  void reset() { buf_.clear(); crc_ = 0; }                                      // :124-126
+
+ private:
+  void maybeFlush() { if (buf_.size() >= flush_) flush(); }
+  void flush();
+  Engine* eng_;
+  size_t flush_;
+  uint64_t crc_ = 0;
+  std::vector<uint8_t> buf_;
+};
+
 // --------------------------------------------------------------- ballot box
 
 // FSMCaller.onCommitted (FSMCallerImpl.java:239-244) as seen by BallotBox.

@@ -155,6 +155,27 @@ class Engine:
         check(self._L.jrq_crc64_batch_dev(self._h, _dev_ptr(payload), _dev_ptr(offsets), n,
                                           _dev_ptr(out)), self._h)
 
+    def crc64_stream_update(self, state, payload, offsets):
+        """CRC64.update(chunk) on S streaming Checksums (include/jrq.h); returns the new
+        registers (getValue()).  `state` is not modified."""
+        offsets = _c(offsets, np.uint64)
+        n = len(offsets) - 1
+        st = np.array(state, dtype=np.uint64, copy=True)
+        if n > 0:
+            if st.shape != (n,):
+                raise ValueError("state must hold one register per stream")
+            payload = _c(payload, np.uint8)
+            if payload.size == 0:
+                payload = np.zeros(1, np.uint8)
+            check(self._L.jrq_crc64_stream_update(self._h, _np_ptr(st), _np_ptr(payload),
+                                                  _np_ptr(offsets), n), self._h)
+        return st
+
+    def crc64_stream_update_dev(self, state, payload, offsets, n=None):
+        n = offsets.shape[0] - 1 if n is None else n
+        check(self._L.jrq_crc64_stream_update_dev(self._h, _dev_ptr(state), _dev_ptr(payload),
+                                                  _dev_ptr(offsets), n), self._h)
+
     def logentry_checksum_batch(self, etype, index, term, peer_xor, payload, offsets,
                                 expected=None, has=None):
         etype = _c(etype, np.uint8)

@@ -5,6 +5,7 @@
 // Sources restated (jraft-core/src/test/java/com/alipay/sofa/jraft/...):
 //   core/BallotBoxTest.java:62-154, entity/BallotTest.java:37-50,
 //   entity/LogEntryTest.java:95-125, util/CrcUtilTest.java:27-42
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -267,6 +268,28 @@ static void testCrcUtilOnGpu(Engine& eng) {
   CHECK(CrcUtil::crc64(eng, nullptr, 0, 0) == 0);
 }
 
+static void testCRC64ChecksumOnGpu(Engine& eng) {
+  // java.util.zip.Checksum use by RheaKV snapshots: update(byte), update(byte[],off,len) in
+  // pieces, getValue mid-stream, reset; small flush threshold forces many GPU folds.
+  const char* s = "123456789";
+  CRC64 c(eng, 4);
+  c.update(s[0]);
+  c.update(reinterpret_cast<const uint8_t*>(s), 1, 3);
+  CHECK(c.getValue() == CrcUtil::crc64(eng, reinterpret_cast<const uint8_t*>(s), 0, 4));
+  c.update(reinterpret_cast<const uint8_t*>(s), 4, 5);
+  CHECK(c.getValue() == 0x6C40DF5F0B497347ull);
+  c.update(reinterpret_cast<const uint8_t*>(s), 0, 0);
+  CHECK(c.getValue() == 0x6C40DF5F0B497347ull);
+  c.reset();
+  CHECK(c.getValue() == 0);
+  std::vector<uint8_t> big(1 << 20);
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  for (auto& b : big) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; b = (uint8_t)x; }
+  CRC64 d(eng, 100000);
+  for (size_t o = 0; o < big.size(); o += 77777) d.update(big.data(), o, std::min<size_t>(77777, big.size() - o));
+  CHECK(d.getValue() == CrcUtil::crc64(eng, big));
+}
+
 int main(int argc, char** argv) {
   const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
   struct T {
@@ -293,6 +316,7 @@ int main(int argc, char** argv) {
     tests.push_back({"testManyGroupsJointConsensusOnGpu", [&] { testManyGroupsJointConsensusOnGpu(e); }});
     tests.push_back({"testLogEntryChecksumOnGpu", [&] { testLogEntryChecksumOnGpu(e); }});
     tests.push_back({"testCrcUtilOnGpu", [&] { testCrcUtilOnGpu(e); }});
+    tests.push_back({"testCRC64ChecksumOnGpu", [&] { testCRC64ChecksumOnGpu(e); }});
   }
   for (auto& t : tests) {
     const int before = g_fail;

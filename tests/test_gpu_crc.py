@@ -188,3 +188,52 @@ def test_full_size_configs(engine, oracle, cfg):
     exp = oracle.logentry_checksum_batch(b["etype"], b["index"], b["term"], None, b["payload"],
                                          b["offsets"])
     np.testing.assert_array_equal(got, exp)
+
+
+# ---- streaming Checksum (RheaKV snapshot archive CRC64, §8f row 4) ----------------------------
+
+@pytest.mark.parametrize("S,max_len,start", [(1, 1, 0), (5, 40, 3), (300, 5000, 0),
+                                             (4096, 2000, 1), (2, 3_000_000, 0)])
+def test_stream_update_vs_oracle(engine, oracle, S, max_len, start):
+    """state[s] <- CRC64.update(chunk_s) from a nonzero register (CRC64.java:106-110)."""
+    offs = W.ragged_offsets(77 + S, S, max_len, start=start)
+    payload = W.random_bytes(S + 3, int(offs[-1]) + 9)
+    rng = np.random.default_rng(S)
+    st0 = rng.integers(0, 2**63, S, dtype=np.int64).astype(np.uint64)
+    st0[0] = 0
+    got = engine.crc64_stream_update(st0, payload, offs)
+    exp = oracle.crc64_stream_update(st0, payload, offs)
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_stream_archive_in_pieces(engine, oracle):
+    """One 40 MB archive fed through CheckedInputStream-sized pieces (ZipUtil.java:74-94):
+    the final getValue() equals CrcUtil.crc64 of the whole archive."""
+    data = W.random_bytes(4242, 40 << 20)
+    cuts = np.sort(np.random.default_rng(1).choice(np.arange(1, data.size), 23, replace=False))
+    offs = np.concatenate([[0], cuts, [data.size]]).astype(np.uint64)
+    reg = np.zeros(1, np.uint64)
+    for a, b in zip(offs[:-1], offs[1:]):
+        reg = engine.crc64_stream_update(reg, data, np.array([a, b], np.uint64))
+    whole = engine.crc64_batch(data, np.array([0, data.size], np.uint64))
+    assert int(reg[0]) == int(whole[0])
+    exp = oracle.crc64_stream_update(np.zeros(1, np.uint64), data,
+                                     np.array([0, data.size], np.uint64))
+    assert int(reg[0]) == int(exp[0])
+
+
+def test_stream_update_dev_resident_state(engine, oracle):
+    """_dev variant: registers stay on the device across calls (many regions' snapshots)."""
+    import torch
+    S = 1000
+    dev = torch.device("cuda:0")
+    reg = torch.zeros(S, dtype=torch.int64, device=dev)
+    exp = np.zeros(S, np.uint64)
+    for k in range(3):
+        offs = W.ragged_offsets(500 + k, S, 3000)
+        payload = W.random_bytes(600 + k, int(offs[-1]) + 1)
+        engine.crc64_stream_update_dev(reg, torch.from_numpy(payload).to(dev),
+                                       torch.from_numpy(offs.view(np.int64)).to(dev))
+        exp = oracle.crc64_stream_update(exp, payload, offs)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(reg.cpu().numpy().view(np.uint64), exp)

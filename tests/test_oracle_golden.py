@@ -71,6 +71,25 @@ def test_continuation_equals_concatenation(oracle):
 
 # ------------------------------------------------------------ entities ---
 
+def test_stream_update_equals_whole(oracle):
+    """Snapshot-archive Checksum (RK/util/ZipUtil.java:45-94): feeding a stream in chunks of any
+    size through CRC64.update (CRC64.java:106-110) gives crc64 of the whole stream."""
+    rng = np.random.default_rng(7)
+    data = rng.integers(0, 256, 50000, dtype=np.uint8)
+    cuts = np.sort(rng.choice(np.arange(1, data.size), 40, replace=False))
+    offs = np.concatenate([[0], cuts, [data.size]]).astype(np.uint64)
+    reg = np.zeros(1, np.uint64)
+    for a, b in zip(offs[:-1], offs[1:]):
+        reg = oracle.crc64_stream_update(reg, data, np.array([a, b], np.uint64))
+    assert int(reg[0]) == oracle.crc64(data.tobytes())
+    # S streams at once, each from its own register
+    st0 = rng.integers(0, 2**63, offs.size - 1, dtype=np.int64).astype(np.uint64)
+    got = oracle.crc64_stream_update(st0, data, offs)
+    for s in range(offs.size - 1):
+        piece = data[int(offs[s]):int(offs[s + 1])].tobytes()
+        assert int(got[s]) == oracle.py_crc64(piece, int(st0[s]))
+
+
 def test_entity_vectors(oracle):
     g = load("entity_vectors.json")
     assert int(g["crc64_check_123456789"], 16) == 0x6C40DF5F0B497347
