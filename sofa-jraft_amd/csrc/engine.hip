@@ -260,16 +260,18 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   e->stream = e->own_stream;
   try_hip(hipMalloc(&e->slice, slice.size() * 8), "hipMalloc(slice)");
   try_hip(hipMalloc(&e->shift, shift.size() * 8), "hipMalloc(shift)");
-  try_hip(hipMalloc(&e->acc, static_cast<size_t>(e->scratch_len) * 8), "hipMalloc(acc)");
-  try_hip(hipMalloc(&e->cnt, static_cast<size_t>(e->scratch_len) * 4), "hipMalloc(cnt)");
+  // acc/cnt: [scratch_len] entry slots + [2 * (scratch_len / 64 + 2)] 64-segment group slots
+  const size_t slots = e->scratch_len + 2 * (e->scratch_len / 64 + 2);
+  try_hip(hipMalloc(&e->acc, slots * 8), "hipMalloc(acc)");
+  try_hip(hipMalloc(&e->cnt, slots * 4), "hipMalloc(cnt)");
   try_hip(hipMalloc(&e->pieces, static_cast<size_t>(e->scratch_len) * 16), "hipMalloc(pieces)");
   try_hip(hipMalloc(&e->fan_ctr, 16), "hipMalloc(fan_ctr)");
   if (rc == JRQ_OK) {
     try_hip(hipMemset(e->fan_ctr, 0, 16), "zero fan_ctr");
     try_hip(hipMemcpy(e->slice, slice.data(), slice.size() * 8, hipMemcpyHostToDevice), "upload slice");
     try_hip(hipMemcpy(e->shift, shift.data(), shift.size() * 8, hipMemcpyHostToDevice), "upload shift");
-    try_hip(hipMemset(e->acc, 0, static_cast<size_t>(e->scratch_len) * 8), "zero acc");
-    try_hip(hipMemset(e->cnt, 0, static_cast<size_t>(e->scratch_len) * 4), "zero cnt");
+    try_hip(hipMemset(e->acc, 0, slots * 8), "zero acc");
+    try_hip(hipMemset(e->cnt, 0, slots * 4), "zero cnt");
   }
   if (rc != JRQ_OK) {
     set(rc);

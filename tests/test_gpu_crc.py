@@ -103,6 +103,24 @@ def test_segment_sizes_and_maps(oracle, seg, seg_map, monkeypatch):
         np.testing.assert_array_equal(e.crc64_batch(payload2, rag), oracle.crc64_batch(payload2, rag))
 
 
+@pytest.mark.parametrize("seg", ["256", "512"])
+def test_adjacent_long_entries_group_slots(oracle, seg, monkeypatch):
+    """Back-to-back entries of 65..400 segments: every 64-segment group slot is shared by one
+    long entry ending in it and one starting in it (two-level hand-off keys)."""
+    from jraft_amd import Engine
+    monkeypatch.setenv("JRQ_CRC_SEG_BYTES", seg)
+    S = int(seg)
+    lens = W.uniform(31, 600, 65 * S, 400 * S, stream=5)
+    lens[::7] = 64 * S + 1   # exactly 65 parts when aligned
+    lens[3::11] = 5          # a short entry between two long ones now and then
+    offs = np.concatenate([[3], 3 + np.cumsum(lens)]).astype(np.uint64)
+    payload = W.random_bytes(31, int(offs[-1]) + 1)
+    exp = oracle.crc64_batch(payload, offs)
+    with Engine(0) as e:
+        for _ in range(2):
+            np.testing.assert_array_equal(e.crc64_batch(payload, offs), exp)
+
+
 def test_more_segments_than_lanes(oracle, monkeypatch):
     """256-B segments over ~90 MB: each wave loops over several chunks."""
     from jraft_amd import Engine
