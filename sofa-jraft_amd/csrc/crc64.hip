@@ -313,11 +313,11 @@ __device__ __forceinline__ void emit(const JrqCrcArgs& a, uint32_t e, uint64_t v
 // arriver reads the slot with an atomic after its add returned.  No release/acquire
 // fences: those would write back the XCD's L2 / invalidate L1 on every piece.
 __device__ __forceinline__ bool arrive_xor(uint64_t* acc, uint32_t* cnt, uint32_t parts,
-                                           uint64_t c, uint64_t* v) {
+                                           uint64_t c, uint64_t* v, uint32_t n = 1) {
   __hip_atomic_fetch_xor(acc, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const uint32_t arrived = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (arrived + 1 != parts) return false;
+  const uint32_t arrived = __hip_atomic_fetch_add(cnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (arrived + n != parts) return false;
   // read-and-zero in one memory-side RMW (an xor-with-0 would be folded into a load)
   *v = __hip_atomic_exchange(acc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -329,7 +329,8 @@ __device__ __forceinline__ bool arrive_xor(uint64_t* acc, uint32_t* cnt, uint32_
 // 64-segment group meet in a group slot (acc/cnt + scratch_len; key 2*group + 1 for the
 // entry's first group, 2*group otherwise -- a group is touched by at most one long entry
 // ending in it and one starting in it), and each group's last arriver carries the group XOR
-// to the entry slot acc[first].  A single 1 GiB entry (a snapshot archive) otherwise put
+// to the entry slot acc[first] -- through a third, supergroup level (64 groups, same keying)
+// when the entry spans more than 64 groups.  A single 1 GiB entry (a snapshot archive) otherwise put
 // every segment's atomics on one address: 3.5 ms instead of ~0.2 ms.
 __device__ __forceinline__ void straddle_piece(const JrqCrcArgs& a, uint32_t e, uint64_t first,
                                                uint64_t parts, uint64_t k, uint64_t c) {
@@ -338,11 +339,39 @@ __device__ __forceinline__ void straddle_piece(const JrqCrcArgs& a, uint32_t e, 
   const uint64_t lo = first > (grp << 6) ? first : (grp << 6);
   const uint64_t hi = last < (grp << 6) + 63 ? last : (grp << 6) + 63;
   const uint64_t key = 2 * grp + (grp == fg ? 1 : 0);
+  // A whole wave handing off pieces of one entry (the wave's 64 segments are one group, as
+  // chunks start on 64-segment boundaries): XOR them across lanes and arrive once with 64.
+  // A snapshot archive hits this at every wave's end; 64 same-address atomics per wave
+  // instruction otherwise serialize at the memory-side atomic unit.
+  uint32_t n = 1;
+  if (__builtin_amdgcn_read_exec() == ~0ull &&
+      __ballot(e == __builtin_amdgcn_readfirstlane(e)) == ~0ull) {
+    uint32_t clo = static_cast<uint32_t>(c), chi = static_cast<uint32_t>(c >> 32);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      clo ^= __shfl_xor(clo, o);
+      chi ^= __shfl_xor(chi, o);
+    }
+    if (__lane_id() != 0) return;
+    c = (static_cast<uint64_t>(chi) << 32) | clo;
+    n = 64;
+  }
   uint64_t v;
   if (!arrive_xor(a.acc + a.scratch_len + key, a.cnt + a.scratch_len + key,
-                  static_cast<uint32_t>(hi - lo + 1), c, &v))
+                  static_cast<uint32_t>(hi - lo + 1), c, &v, n))
     return;
-  if (arrive_xor(a.acc + first, a.cnt + first, static_cast<uint32_t>(lg - fg + 1), v, &v))
+  uint64_t entry_parts = lg - fg + 1;
+  if (entry_parts > 64) {  // > 64 groups (a GiB-scale archive): 64-group supergroup level
+    const uint64_t l1 = 2 * (static_cast<uint64_t>(a.scratch_len) / 64 + 2);
+    const uint64_t sg = grp >> 6, fsg = fg >> 6, lsg = lg >> 6;
+    const uint64_t glo = fg > (sg << 6) ? fg : (sg << 6);
+    const uint64_t ghi = lg < (sg << 6) + 63 ? lg : (sg << 6) + 63;
+    const uint64_t key2 = a.scratch_len + l1 + 2 * sg + (sg == fsg ? 1 : 0);
+    if (!arrive_xor(a.acc + key2, a.cnt + key2, static_cast<uint32_t>(ghi - glo + 1), v, &v))
+      return;
+    entry_parts = lsg - fsg + 1;
+  }
+  if (arrive_xor(a.acc + first, a.cnt + first, static_cast<uint32_t>(entry_parts), v, &v))
     emit(a, e, v);
 }
 

@@ -261,7 +261,8 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   try_hip(hipMalloc(&e->slice, slice.size() * 8), "hipMalloc(slice)");
   try_hip(hipMalloc(&e->shift, shift.size() * 8), "hipMalloc(shift)");
   // acc/cnt: [scratch_len] entry slots + [2 * (scratch_len / 64 + 2)] 64-segment group slots
-  const size_t slots = e->scratch_len + 2 * (e->scratch_len / 64 + 2);
+  // + [2 * (scratch_len / 4096 + 2)] 64-group supergroup slots (crc64.hip straddle_piece)
+  const size_t slots = e->scratch_len + 2 * (e->scratch_len / 64 + 2) + 2 * (e->scratch_len / 4096 + 2);
   try_hip(hipMalloc(&e->acc, slots * 8), "hipMalloc(acc)");
   try_hip(hipMalloc(&e->cnt, slots * 4), "hipMalloc(cnt)");
   try_hip(hipMalloc(&e->pieces, static_cast<size_t>(e->scratch_len) * 16), "hipMalloc(pieces)");

@@ -103,15 +103,17 @@ def test_segment_sizes_and_maps(oracle, seg, seg_map, monkeypatch):
         np.testing.assert_array_equal(e.crc64_batch(payload2, rag), oracle.crc64_batch(payload2, rag))
 
 
-@pytest.mark.parametrize("seg", ["256", "512"])
-def test_adjacent_long_entries_group_slots(oracle, seg, monkeypatch):
-    """Back-to-back entries of 65..400 segments: every 64-segment group slot is shared by one
-    long entry ending in it and one starting in it (two-level hand-off keys)."""
+@pytest.mark.parametrize("seg,n,lo,hi", [("256", 600, 65, 400), ("512", 600, 65, 400),
+                                         ("256", 24, 4097, 12000)])
+def test_adjacent_long_entries_group_slots(oracle, seg, n, lo, hi, monkeypatch):
+    """Back-to-back entries of lo..hi segments: every 64-segment group slot (and, past 4096
+    segments, every 64-group supergroup slot) is shared by one long entry ending in it and
+    one starting in it (multi-level hand-off keys)."""
     from jraft_amd import Engine
     monkeypatch.setenv("JRQ_CRC_SEG_BYTES", seg)
     S = int(seg)
-    lens = W.uniform(31, 600, 65 * S, 400 * S, stream=5)
-    lens[::7] = 64 * S + 1   # exactly 65 parts when aligned
+    lens = W.uniform(31, n, lo * S, hi * S, stream=5)
+    lens[::7] = (lo - 1) * S + 1   # exactly lo parts when aligned
     lens[3::11] = 5          # a short entry between two long ones now and then
     offs = np.concatenate([[3], 3 + np.cumsum(lens)]).astype(np.uint64)
     payload = W.random_bytes(31, int(offs[-1]) + 1)
