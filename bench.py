@@ -175,7 +175,23 @@ def cpu_quorum_baseline(budget_s: float, threads: int = CPU_THREADS):
                                      b["last_committed"], b["conf"], chunk=1024)[2]
     n1, t1, g1 = _threaded(replay, chunks, 1, budget_s / 2)
     nt, tt, gt = _threaded(replay, chunks, threads, budget_s / 2)
+    # optimised CPU line: closed-form epoch per group (oracle/cpu_fast.c),
+    # over full 64k-group C3 chunks
+    fast_groups = 1 << 16
+    fchunks = [W.quorum_batch("C3", groups=fast_groups, group_offset=k * fast_groups)
+               for k in range(threads)]
+
+    def fast(b):
+        O.fast_quorum_epoch(b["match"], b["pending_index"], b["last_appended"],
+                            b["last_committed"], b["conf"])
+        return 0
+    fn1, ft1, _ = _threaded(fast, fchunks, 1, 1.0)
+    fnt, ftt, _ = _threaded(fast, fchunks, threads, 1.0)
+    optimised = dict(value=fnt * fast_groups / ftt, single_thread=fn1 * fast_groups / ft1,
+                     cores=threads, how="closed-form q-th largest per conf mask per group "
+                     "(oracle/cpu_fast.c, same results as the BallotBox replay), C3 groups")
     return dict(value=nt * chunk_groups / tt, unit="decisions/s", cores=threads, kind="port",
+                optimised=optimised,
                 single_thread=n1 * chunk_groups / t1, cpu=cpu_model(),
                 sample=f"C3 groups (1k pending, 5 peers, joint) replayed through the Java-faithful "
                        f"BallotBox restatement: {nt * chunk_groups} groups / {gt} Ballot.grant "
@@ -198,7 +214,17 @@ def cpu_crc_baseline(budget_s: float, threads: int = CPU_THREADS):
     n1, t1, _ = _threaded(run, batches, 1, budget_s / 2)
     nt, tt, _ = _threaded(run, batches, threads, budget_s / 2)
     gb1, gbt = n1 * n * (16 << 10) / 1e9, nt * n * (16 << 10) / 1e9
-    return dict(value=gbt / tt, unit="GB/s", cores=threads, kind="port",
+
+    def fast(b):  # optimised CPU line: slice-by-8 CRC64 of the same payloads
+        O.fast_crc64_batch(b["payload"], b["offsets"])
+        return 0
+    fast(batches[0])  # builds the slice tables before the threads start
+    fn1, ft1, _ = _threaded(fast, batches, 1, 1.0)
+    fnt, ftt, _ = _threaded(fast, batches, threads, 1.0)
+    optimised = dict(value=fnt * n * (16 << 10) / 1e9 / ftt,
+                     single_thread=fn1 * n * (16 << 10) / 1e9 / ft1, cores=threads,
+                     how="slice-by-8 CRC64 (oracle/cpu_fast.c) over the same C5 payloads")
+    return dict(value=gbt / tt, unit="GB/s", cores=threads, kind="port", optimised=optimised,
                 single_thread=gb1 / t1, cpu=cpu_model(),
                 sample=f"C5 LogEntries x 16 KiB through the byte-at-a-time CRC64.update "
                        f"restatement: {gbt:.2f} GB in {tt:.1f} s on {threads} threads; "

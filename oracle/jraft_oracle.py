@@ -98,6 +98,11 @@ def lib():
         L.jo_v2_peer_checksum.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_int)]
         L.jo_commit_fanout_replay.restype = C.c_int64
         L.jo_commit_fanout_replay.argtypes = [C.c_uint32] + [C.c_void_p] * 7
+        # cpu_fast.c: optimised CPU baselines (bench.py), checked against the above
+        L.jo_fast_crc64_batch.restype = None
+        L.jo_fast_crc64_batch.argtypes = [_u8p, _u64p, C.c_uint32, _u64p]
+        L.jo_fast_quorum_epoch.restype = None
+        L.jo_fast_quorum_epoch.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64] + [C.c_void_p] * 7
         _lib = L
     return _lib
 
@@ -148,6 +153,31 @@ def crc64_stream_update(state: np.ndarray, payload: np.ndarray, offsets: np.ndar
         o0, o1 = int(offsets[s]), int(offsets[s + 1])
         out[s] = L.jo_crc64_update(int(out[s]), C.c_void_p(base + o0), o1 - o0)
     return out
+
+
+def fast_crc64_batch(payload: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    """Slice-by-8 CRC64 (cpu_fast.c): the optimised-CPU baseline, same results as crc64_batch."""
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    out = np.zeros(max(n, 0), dtype=np.uint64)
+    if n > 0:
+        lib().jo_fast_crc64_batch(payload if payload.size else np.zeros(1, np.uint8), offsets, n, out)
+    return out
+
+
+def fast_quorum_epoch(match, pending_index, last_appended, last_committed, conf):
+    """Closed-form epoch per group (cpu_fast.c): the optimised-CPU quorum baseline."""
+    match = np.ascontiguousarray(match, dtype=np.int64)
+    P, G = match.shape
+    arrs = [np.ascontiguousarray(a, dtype=np.int64) for a in (pending_index, last_appended,
+                                                               last_committed)]
+    conf = np.ascontiguousarray(conf, dtype=np.uint64)
+    committed = np.empty(G, np.int64)
+    status = np.empty(G, np.uint8)
+    lib().jo_fast_quorum_epoch(P, G, G, _ptr(match), *[_ptr(a) for a in arrs], _ptr(conf),
+                               _ptr(committed), _ptr(status))
+    return committed, status
 
 
 def logid_checksum(index: int, term: int) -> int:

@@ -90,6 +90,23 @@ def test_stream_update_equals_whole(oracle):
         assert int(got[s]) == oracle.py_crc64(piece, int(st0[s]))
 
 
+def test_fast_cpu_baselines_match_oracle(oracle):
+    """bench.py's optimised-CPU lines (oracle/cpu_fast.c) compute the oracle's results."""
+    from jraft_amd import workloads as W
+    offs = W.ragged_offsets(5, 3000, 5000, start=3)
+    payload = W.random_bytes(5, int(offs[-1]) + 1)
+    np.testing.assert_array_equal(oracle.fast_crc64_batch(payload, offs),
+                                  oracle.crc64_batch(payload, offs))
+    for cfg in ("C2", "C3"):
+        b = W.quorum_batch(cfg, groups=512)
+        c, s = oracle.fast_quorum_epoch(b["match"], b["pending_index"], b["last_appended"],
+                                        b["last_committed"], b["conf"])
+        ce, se, _ = oracle.quorum_epoch_replay(b["match"], b["pending_index"], b["last_appended"],
+                                               b["last_committed"], b["conf"], chunk=1024)
+        np.testing.assert_array_equal(c, ce)
+        np.testing.assert_array_equal(s, se)
+
+
 def test_entity_vectors(oracle):
     g = load("entity_vectors.json")
     assert int(g["crc64_check_123456789"], 16) == 0x6C40DF5F0B497347
