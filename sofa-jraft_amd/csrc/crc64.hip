@@ -790,8 +790,15 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
       v = a.piece_tail[last];
       for (uint64_t g = first; g < last; ++g) v ^= a.piece_cont[g];
     } else {
-      if (!kLogEntry) continue;  // whole entry (or atomic hand-off): out[e] is final
+      // whole entry (or atomic hand-off): out[e] is final
+      if (!kLogEntry && a.stream_state == nullptr) continue;
       v = a.out[e];
+    }
+    if (!kLogEntry && a.stream_state != nullptr) {
+      // streaming Checksum (CRC64.update, CRC64.java:106-110): register * x^(8 len) ^ crc(chunk);
+      // init 0 and xorout 0 make CRC64 linear
+      const uint64_t len = o1 - o0;
+      a.stream_state[e] = crc_shift(a.stream_state[e], len, a.shift) ^ (len ? v : 0);
     }
     if (kLogEntry) {
       uint64_t r = 0;
@@ -813,31 +820,7 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
   }
 }
 
-// Streaming java.util.zip.Checksum update (CRC64.update(byte[],off,len), CRC64.java:106-110)
-// of S independent streams by one chunk each: the register after the chunk is
-//   state * x^(8 len) ^ crc64(chunk)   (mod P; init 0 and xorout 0 make CRC64 linear),
-// with crc64(chunk) already in chunk_crc[s] from the rounds/finish kernels.
-__global__ __launch_bounds__(256) void crc64_stream_combine_kernel(
-    uint64_t* __restrict__ state, const uint64_t* __restrict__ chunk_crc,
-    const uint64_t* __restrict__ off, uint32_t S, const uint64_t* __restrict__ shift) {
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < S; s += stride) {
-    const uint64_t len = off[s + 1] - off[s];
-    state[s] = crc_shift(state[s], len, shift) ^ (len ? chunk_crc[s] : 0);
-  }
-}
-
 }  // namespace jrq
-
-extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64_stream_combine(
-    uint64_t* state, const uint64_t* chunk_crc, const uint64_t* off, uint32_t S,
-    const uint64_t* shift, int num_cus, hipStream_t stream) {
-  const uint32_t blocks = (S + 255) / 256;
-  const uint32_t cap = static_cast<uint32_t>(num_cus) * 8;
-  hipLaunchKernelGGL(jrq::crc64_stream_combine_kernel, dim3(blocks < cap ? blocks : cap), dim3(256),
-                     0, stream, state, chunk_crc, off, S, shift);
-  return hipGetLastError();
-}
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64(
     JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {

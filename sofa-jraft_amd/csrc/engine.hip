@@ -30,10 +30,6 @@ extern "C" hipError_t jrq_launch_fanout(const JrqFanoutArgs* a, hipStream_t stre
 extern "C" hipError_t jrq_launch_v2_parse(const JrqV2Args* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_v2_finish(const JrqV2Args* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_first_corrupt(const JrqAeArgs* a, hipStream_t stream);
-extern "C" hipError_t jrq_launch_crc64_stream_combine(uint64_t* state, const uint64_t* chunk_crc,
-                                                      const uint64_t* off, uint32_t S,
-                                                      const uint64_t* shift, int num_cus,
-                                                      hipStream_t stream);
 
 namespace {
 
@@ -477,10 +473,8 @@ int jrq_crc64_stream_update_dev(jrq_engine* e, uint64_t* state, const uint8_t* p
   a.offsets = offsets;
   a.n = S;
   a.out = static_cast<uint64_t*>(chunk);
-  if ((rc = crc_dispatch(e, a, 0))) return rc;
-  JRQ_HIP(e, jrq_launch_crc64_stream_combine(state, a.out, offsets, S, e->shift, e->num_cus,
-                                             e->stream));
-  return JRQ_OK;
+  a.stream_state = state;  // folded into the registers by crc64_finish_kernel
+  return crc_dispatch(e, a, 0);
 }
 
 int jrq_crc64_stream_update(jrq_engine* e, uint64_t* state, const uint8_t* payload,

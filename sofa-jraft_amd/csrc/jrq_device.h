@@ -92,6 +92,7 @@ struct JrqCrcArgs {
   uint64_t seg_bytes;      // nonzero: segment size (rounded up to 256 B; tests / tuning)
   uint32_t prio_steps;     // 1: waves lower their priority as they progress (crc64.hip)
   uint32_t regs_slowpath;  // 1: boundary half-rounds hash from registers (crc64_rounds_kernel<true>)
+  uint64_t* stream_state;  // nullable: streaming Checksum registers folded by the finish kernel
 };
 
 // Leader lease / alive-quorum check (quorum.hip, lease kernel).
