@@ -257,3 +257,21 @@ def test_stream_update_dev_resident_state(engine, oracle):
         exp = oracle.crc64_stream_update(exp, payload, offs)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(reg.cpu().numpy().view(np.uint64), exp)
+
+
+def test_stream_update_errors_and_empty(engine):
+    """Error conventions (include/jrq.h): non-monotone offsets -> JRQ_E_INVALID, nothing
+    written; S = 0 is a no-op; an all-empty chunk batch leaves every register unchanged
+    (CRC64.update with len 0, CRC64.java:106-110)."""
+    from jraft_amd._lib import JrqError
+    st = np.array([5, 7], np.uint64)
+    with pytest.raises(JrqError):
+        engine.crc64_stream_update(st, np.zeros(16, np.uint8), np.array([0, 9, 4], np.uint64))
+    assert engine.crc64_stream_update(np.zeros(0, np.uint64), np.zeros(1, np.uint8),
+                                      np.array([0], np.uint64)).size == 0
+    regs = np.array([0, 0x123456789ABCDEF0, 2**64 - 1], np.uint64)
+    got = engine.crc64_stream_update(regs, np.zeros(4, np.uint8), np.array([2, 2, 2, 2], np.uint64))
+    np.testing.assert_array_equal(got, regs)
+    with pytest.raises(ValueError):
+        engine.crc64_stream_update(np.zeros(3, np.uint64), np.zeros(4, np.uint8),
+                                   np.array([0, 4], np.uint64))
