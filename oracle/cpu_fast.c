@@ -28,6 +28,13 @@ static void t8_init(void) {
     t8_ready = 1;
 }
 
+/* Build both the oracle's table and the slice tables when the library loads, before any
+ * baseline thread runs (their lazy initialisation is otherwise a benign but real race). */
+__attribute__((constructor)) static void tables_at_load(void) {
+    (void)jo_crc64_table();
+    t8_init();
+}
+
 uint64_t jo_fast_crc64_update(uint64_t crc, const uint8_t *p, size_t n) {
     if (!t8_ready) t8_init();
     const uint64_t *t = T8[0];
