@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define JRQ_ABI_VERSION 1
+#define JRQ_ABI_VERSION 2
 #define JRQ_MAX_PEERS 16 /* peer slots per group (16-bit masks) */
 
 typedef struct jrq_engine jrq_engine;
@@ -72,6 +72,11 @@ typedef enum {
 #define JRQ_CONF(newMask, oldMask, newQ, oldQ)                                                 \
     ((uint64_t)(uint16_t)(newMask) | ((uint64_t)(uint16_t)(oldMask) << 16) |                    \
      ((uint64_t)(uint8_t)(newQ) << 32) | ((uint64_t)(uint8_t)(oldQ) << 40))
+/* Flag bit of conf[g] (bits 48-62 are reserved, 0): group g's pending window holds more than
+ * one conf run (a conf change inside it: NodeImpl.unsafeApplyConfiguration, JC/core/
+ * NodeImpl.java:2065-2086, then (conf, oldConf) per entry, :1195-1196).  Only flagged groups
+ * walk a run table; every other group is decided from its conf word alone, on the fast path. */
+#define JRQ_CONF_RUNS (1ull << 63)
 
 /* One epoch of a group batch, structure-of-arrays (all arrays length G unless noted).
  * Replaces the per-call state of JC/core/BallotBox.java:50-55 for G groups at once:
@@ -82,12 +87,16 @@ typedef enum {
  *   pending_index[g]       BallotBox.pendingIndex (0 = not leader)
  *   last_appended[g]       pendingIndex + pendingMetaQueue.size() - 1
  *   last_committed[g]      BallotBox.lastCommittedIndex before the epoch
- *   conf[g]                packed conf of every pending entry (used when run_off == NULL)
+ *   conf[g]                packed conf of every pending entry, or JRQ_CONF_RUNS: the group's
+ *                          entries follow its runs in the run table
  *   run_off[G+1]           optional CSR of conf runs (joint consensus, conf changes):
  *                          runs of group g are [run_off[g], run_off[g+1]); run r covers log
  *                          indices [run_start[r], run_start[r+1]) (the group's last run ends at
  *                          last_appended; the first run's start is treated as <= pendingIndex);
- *                          run_conf[r] is its packed conf.
+ *                          run_conf[r] is its packed conf.  *_dev: consulted only for groups
+ *                          whose conf[g] carries JRQ_CONF_RUNS.  Host variant: the engine
+ *                          derives the flags itself (a group with exactly one run is decided
+ *                          from that run's conf; conf may then be NULL).
  */
 typedef struct {
     const int64_t *match;
@@ -145,7 +154,9 @@ int jrq_quorum_epoch(jrq_engine *e, const jrq_group_batch *in_host, int64_t *com
  * and the group state carried from epoch k-1 exactly as BallotBox carries it: a commit sets
  * lastCommittedIndex and pendingIndex = lastCommittedIndex + 1 (JC/core/BallotBox.java:
  * 131-134); pendingIndex 0 (not leader) stays 0.  in->pending_index / last_committed / conf
- * are the state before epoch 0 (one conf per group: run_off must be NULL).
+ * are the state before epoch 0; the conf runs (JRQ_CONF_RUNS groups, as for
+ * jrq_quorum_epoch_dev) hold for all K epochs, entries appended in later epochs extending a
+ * group's last run.
  * Out: committed_out[k*G + g], status_out[k*G + g] after each epoch. */
 int jrq_quorum_epochs_dev(jrq_engine *e, const jrq_group_batch *in_dev, uint32_t K,
                           uint64_t match_epoch_ld, uint64_t la_epoch_ld,
@@ -328,6 +339,9 @@ int jrq_v2_decode_verify(jrq_engine *e, const uint8_t *records, const uint64_t *
  * The unique id is 128 opaque bytes produced on rank 0 and shared out of band. */
 int jrq_rccl_get_unique_id(uint8_t id_out[128]);
 int jrq_rccl_init(jrq_engine *e, int nranks, int rank, const uint8_t id[128]);
+/* Ranks of the engine's communicator as RCCL itself counts them (ncclCommCount); 0 before
+ * jrq_rccl_init, negative on error. */
+int jrq_rccl_nranks(jrq_engine *e);
 int jrq_publish_committed_dev(jrq_engine *e, const int64_t *local_dev, int64_t *global_dev,
                               uint64_t count_per_rank);
 

@@ -22,8 +22,8 @@
 //    no selects) hands every lane its own 4 pieces.  Half-rounds run through a 3-deep
 //    register ring; buffer loads with a per-wave descriptor clamp reads past the data to 0.
 //  * Table CRC in the "reversed domain" r = bswap64(crc): a little-endian load XORs straight
-//    into r, and 8 bytes are one step  r = R7[b0] ^ R6[b1] ^ ... ^ R0[b7] (slice-by-8, Tab8;
-//    Tab4 is the slice-by-4 flavour kept for the design probes), R_j = bswap(T_j),
+//    into r, and 8 bytes are one step  r = R7[b0] ^ R6[b1] ^ ... ^ R0[b7] (slice-by-8, Tab8),
+//    R_j = bswap(T_j),
 //    T_j[i] = i * x^(64 + 8j) mod P.  The tables live in LDS, replicated 8x, and the 4 lanes
 //    sharing a replica visit its tables in 4 rotations, so every ds_read_b64 is bank-conflict
 //    free.  An LDS address is one v_perm of a data byte and a per-lane constant.
@@ -58,84 +58,6 @@ __device__ __forceinline__ uint64_t crc_value(const RState& r) {
 __device__ __forceinline__ uint2 lds_u2(const char* lds, uint32_t addr) {
   return *reinterpret_cast<const uint2*>(lds + addr);
 }
-
-// ------------------------------------------------------------ slice-by-4 ---
-// LDS image: byte address = (k>>1)<<16 | index<<8 | (lane&15)<<4 | (k&1)<<3 for table R_k
-// (16 replicas; R0/R1 share the 16-B slots of the first 64 KiB, R2/R3 of the second).
-struct Tab4 {
-  // Lanes 16-31 / 48-63 ("swapped" lanes) byte-swap each 16-bit half of r.lo before the
-  // lookups (one v_perm), so instruction i reads their byte i^1 and table R_{3-(i^1)}: the
-  // byte selectors stay wave-uniform constants and only the table constants are per lane.
-  uint32_t lc[4];  // instruction i: LDS address constant of its table (per lane)
-  uint32_t swz;    // v_perm selector: identity, or bytes 0<->1, 2<->3 on swapped lanes
-  __device__ explicit Tab4(uint32_t lane) {
-    const uint32_t sw = (lane >> 4) & 1u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t k = 3u - (static_cast<uint32_t>(i) ^ sw);  // table of instruction i
-      lc[i] = ((lane & 15u) << 4) | ((k & 1u) << 3) | ((k >> 1) << 16);
-    }
-    swz = sw ? 0x02030001u : 0x03020100u;
-  }
-
-  // word w = (k>>1)<<13 | index<<5 | replica<<1 | (k&1)
-  __device__ static uint32_t src_index(uint32_t w) {
-    return (((w >> 13) << 1) | (w & 1u)) * 256 + ((w >> 5) & 255u);
-  }
-
-  // four bytes already XORed into r.lo: r = (r >> 32) ^ R3[b0] ^ R2[b1] ^ R1[b2] ^ R0[b3]
-  // (the LDS address of instruction i = {lc.b0, byte i of x, lc.b2, 0})
-  __device__ __forceinline__ void step4(RState& r, const char* lds) const {
-    const uint32_t x = __builtin_amdgcn_perm(r.lo, r.lo, swz);
-    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc[0], x, 0x0C060004u));
-    const uint2 t1 = lds_u2(lds, __builtin_amdgcn_perm(lc[1], x, 0x0C060104u));
-    const uint2 t2 = lds_u2(lds, __builtin_amdgcn_perm(lc[2], x, 0x0C060204u));
-    const uint2 t3 = lds_u2(lds, __builtin_amdgcn_perm(lc[3], x, 0x0C060304u));
-    r.lo = xor3(xor3(r.hi, t0.x, t1.x), t2.x, t3.x);
-    r.hi = xor3(t0.y, t1.y, t2.y) ^ t3.y;
-  }
-  // one byte: r = R0[(r ^ b) & 0xFF] ^ (r >> 8)   (CRC64.update(byte), CRC64.java:100-103)
-  __device__ __forceinline__ void step1(RState& r, uint32_t b, const char* lds) const {
-    const uint32_t lc0 = lc[0] & 0xF0u;  // this lane's replica of R0
-    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc0, r.lo ^ b, 0x0C060004u));
-    const uint32_t nlo = __builtin_amdgcn_alignbit(r.hi, r.lo, 8);
-    r.lo = nlo ^ t0.x;
-    r.hi = (r.hi >> 8) ^ t0.y;
-  }
-  // eight bytes as a little-endian (lo, hi) dword pair
-  __device__ __forceinline__ void step8(RState& r, uint32_t dlo, uint32_t dhi,
-                                        const char* lds) const {
-    r.lo ^= dlo;
-    r.hi ^= dhi;
-    step4(r, lds);
-    step4(r, lds);
-  }
-  __device__ __forceinline__ void step16(RState& r, const u32x4& v, const char* lds) const {
-    step8(r, v[0], v[1], lds);
-    step8(r, v[2], v[3], lds);
-  }
-  // step4 that also XORs the data word two steps ahead into the new r.hi: r.hi becomes the
-  // base of r.lo in the next step, and that r.lo is what the step after consumes, so word
-  // j + 2 enters exactly when step j + 2 needs it -- at no cost (xor3 takes it beside t3.y)
-  __device__ __forceinline__ void step4w(RState& r, uint32_t w, const char* lds) const {
-    const uint32_t x = __builtin_amdgcn_perm(r.lo, r.lo, swz);
-    const uint2 t0 = lds_u2(lds, __builtin_amdgcn_perm(lc[0], x, 0x0C060004u));
-    const uint2 t1 = lds_u2(lds, __builtin_amdgcn_perm(lc[1], x, 0x0C060104u));
-    const uint2 t2 = lds_u2(lds, __builtin_amdgcn_perm(lc[2], x, 0x0C060204u));
-    const uint2 t3 = lds_u2(lds, __builtin_amdgcn_perm(lc[3], x, 0x0C060304u));
-    r.lo = xor3(xor3(r.hi, t0.x, t1.x), t2.x, t3.x);
-    r.hi = xor3(xor3(t0.y, t1.y, t2.y), t3.y, w);
-  }
-  // 64 bytes = 16 data words: words 0, 1 XOR in directly, words 2..15 ride step4w
-  __device__ __forceinline__ void step64(RState& r, const u32x4 (&v)[4], const char* lds) const {
-    r.lo ^= v[0][0];
-    r.hi ^= v[0][1];
-#pragma unroll
-    for (int j = 0; j < 14; ++j) step4w(r, v[(j + 2) >> 2][(j + 2) & 3], lds);
-    step4(r, lds);
-    step4(r, lds);
-  }
-};
 
 // ------------------------------------------------------------ slice-by-8 ---
 // 8 bytes per step: r = R7[b0] ^ R6[b1] ^ R5[b2] ^ R4[b3] ^ R3[b4] ^ R2[b5] ^ R1[b6] ^ R0[b7]
@@ -210,7 +132,6 @@ struct Tab8 {
   }
 };
 
-// The table flavour the rounds kernel uses (Tab4 stays for the design probes).
 using CrcTab = Tab8;
 
 // -------------------------------------------------------- row transpose ---
@@ -441,9 +362,6 @@ template <bool kRegs>
 __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
   const char* lds = reinterpret_cast<const char*>(lds_tab);
-  if (a.timeline && (threadIdx.x & 63u) == 0)  // diagnostics: wave start (nothing kept live)
-    a.timeline[4 * (blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6))] =
-        __builtin_amdgcn_s_memrealtime();
 
   // Build the replicated LDS image of the slice tables (a.slice = R0, R1, R2, R3).
   for (uint32_t w = threadIdx.x; w < kCrcLdsBytes / 8; w += blockDim.x)
@@ -539,14 +457,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
         sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
       }
     };
-#if defined(JRQ_DIAG_NO_SETUP)  // tools/crc_timeline only: 16 KiB entries, no offset loads
-    if (!(sw.flags & SegWalk::kDone)) {
-      sw.cur = static_cast<uint32_t>(s0 >> 14);
-      if (s0 & 16383) sw.flags &= ~SegWalk::kStarted;
-      sw.cur_end = static_cast<uint32_t>(((s0 >> 14) + 1) * 16384 - s0);
-      sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
-    }
-#else
     if (!(sw.flags & SegWalk::kDone)) {
       const uint32_t e = interp_lower_bound(off, n, base, total, s0 + sw.pos - D + base);
       if (e > 0 && E(e) > s0 + sw.pos) {  // entry e-1 began in an earlier segment
@@ -559,7 +469,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
         start_entry();
       }
     }
-#endif
 
     // An event at pos == next: the entry ends (emit / hand off its tail piece), or the
     // segment ends inside the entry (hand off a shifted head/middle piece).
@@ -581,11 +490,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
         ++sw.cur;
         start_entry();
       } else {  // pos == hi < entry end
-#if defined(JRQ_DIAG_NO_TAIL)  // tools/crc_timeline only: drop the head/middle piece
-        a.piece_cont[k] = crc_value(r);
-        sw.flags |= SegWalk::kDone;
-        return;
-#endif
         const uint64_t ce = E(sw.cur + 1);
         const uint64_t c = crc_shift(crc_value(r), ce - (s0 + sw.hi), a.shift);
         const uint64_t first = started ? k : E(sw.cur) / S;
@@ -753,12 +657,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     }
 #endif
 #undef JRQ_LOAD_HALF
-  }
-  if (a.timeline && (threadIdx.x & 63u) == 0) {  // diagnostics only
-    uint64_t* t = a.timeline + 4 * (blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6));
-    t[1] = __builtin_amdgcn_s_memrealtime();
-    t[2] = __builtin_amdgcn_s_getreg((23 << 11) | (0 << 6) | 4);   // HW_REG_HW_ID, 24 bits
-    t[3] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);   // HW_REG_XCC_ID, 4 bits
   }
 }
 

@@ -173,6 +173,15 @@ int stage_in(jrq_engine* e, int slot, const T* host, size_t count, const T** dev
   return JRQ_OK;
 }
 
+// offsets[0..n] must be monotone: the CRC kernels' segment walk and lower-bound search assume
+// it, and an interior offset below offsets[0] would wrap in the host variants' rebase and send
+// the kernels past the staged window.
+int check_monotone(jrq_engine* e, const uint64_t* off, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i]) return fail(e, JRQ_E_INVALID, "offsets not monotone at entry %u", i);
+  return JRQ_OK;
+}
+
 // Entry boundaries off the 64-B half-round grid make the CRC kernel's boundary path frequent:
 // host variants then pick the register boundary path (crc64_rounds_kernel<true>).
 uint32_t unaligned_bounds(const uint64_t* off, uint32_t n) {
@@ -330,7 +339,7 @@ int jrq_quorum_epoch_dev(jrq_engine* e, const jrq_group_batch* in, int64_t* comm
   if (in->num_peers == 0 || in->num_peers > JRQ_MAX_PEERS)
     return fail(e, JRQ_E_INVALID, "num_peers %u outside 1..%d", in->num_peers, JRQ_MAX_PEERS);
   if (!in->match || !in->pending_index || !in->last_appended || !in->last_committed ||
-      !committed_out || !status_out || (!in->run_off && !in->conf) ||
+      !committed_out || !status_out || !in->conf ||
       (in->run_off && (!in->run_start || !in->run_conf)) || in->match_ld < G)
     return fail(e, JRQ_E_INVALID, "missing array or match_ld < G");
   DeviceGuard guard(e->device);
@@ -360,19 +369,38 @@ int jrq_quorum_epoch(jrq_engine* e, const jrq_group_batch* in, int64_t* committe
   if (!committed_out || !status_out) return fail(e, JRQ_E_INVALID, "null output");
   if (in->num_peers == 0 || in->num_peers > JRQ_MAX_PEERS || in->match_ld < G || !in->match)
     return fail(e, JRQ_E_INVALID, "bad num_peers / match_ld");
+  if (!in->pending_index || !in->last_appended || !in->last_committed ||
+      (!in->run_off && !in->conf) || (in->run_off && (!in->run_start || !in->run_conf)))
+    return fail(e, JRQ_E_INVALID, "missing group array");
   DeviceGuard guard(e->device);
   jrq_group_batch d = *in;
   int rc;
   const size_t P = in->num_peers;
+  std::vector<uint64_t> cw;  // flagged conf words (outlives the asynchronous staging copy)
   if ((rc = stage_in(e, 0, in->match, (P - 1) * in->match_ld + G, &d.match))) return rc;
   if ((rc = stage_in(e, 1, in->pending_index, G, &d.pending_index))) return rc;
   if ((rc = stage_in(e, 2, in->last_appended, G, &d.last_appended))) return rc;
   if ((rc = stage_in(e, 3, in->last_committed, G, &d.last_committed))) return rc;
-  if ((rc = stage_in(e, 4, in->conf, G, &d.conf))) return rc;
   if (in->run_off) {
+    // the CSR is host memory here: check it before any kernel indexes with it
+    const uint32_t* ro = in->run_off;
+    if (ro[0] != 0 || ro[G] > in->num_runs)
+      return fail(e, JRQ_E_INVALID, "run_off must start at 0 and end <= num_runs");
+    // conf words with JRQ_CONF_RUNS on exactly the groups whose runs the kernels must walk:
+    // a group with one run is an ordinary single-conf group (the fast path)
+    cw.resize(G);
+    for (uint32_t g = 0; g < G; ++g) {
+      if (ro[g + 1] < ro[g]) return fail(e, JRQ_E_INVALID, "run_off not monotone at group %u", g);
+      const uint32_t n = ro[g + 1] - ro[g];
+      cw[g] = n == 1 ? (in->run_conf[ro[g]] & ~JRQ_CONF_RUNS)
+                     : (JRQ_CONF_RUNS | (in->conf ? in->conf[g] : 0));
+    }
+    if ((rc = stage_in(e, 4, cw.data(), G, &d.conf))) return rc;
     if ((rc = stage_in(e, 5, in->run_off, static_cast<size_t>(G) + 1, &d.run_off))) return rc;
     if ((rc = stage_in(e, 6, in->run_start, in->num_runs, &d.run_start))) return rc;
     if ((rc = stage_in(e, 7, in->run_conf, in->num_runs, &d.run_conf))) return rc;
+  } else {
+    if ((rc = stage_in(e, 4, in->conf, G, &d.conf))) return rc;
   }
   void *dc = nullptr, *ds = nullptr;
   if ((rc = ensure_stage(e, 8, static_cast<size_t>(G) * 8, &dc))) return rc;
@@ -396,7 +424,8 @@ int jrq_quorum_epochs_dev(jrq_engine* e, const jrq_group_batch* in, uint32_t K,
   if (in->num_peers == 0 || in->num_peers > JRQ_MAX_PEERS || in->match_ld < G || !in->match ||
       !in->pending_index || !in->last_appended || !in->last_committed || !in->conf)
     return fail(e, JRQ_E_INVALID, "bad num_peers / match_ld / null array");
-  if (in->run_off) return fail(e, JRQ_E_INVALID, "conf runs are not supported across epochs");
+  if (in->run_off && (!in->run_start || !in->run_conf))
+    return fail(e, JRQ_E_INVALID, "run_off without run_start / run_conf");
   if (K > 1 && (match_eld < static_cast<uint64_t>(in->num_peers) * in->match_ld || la_eld < G))
     return fail(e, JRQ_E_INVALID, "epoch strides overlap");
   DeviceGuard guard(e->device);
@@ -406,6 +435,9 @@ int jrq_quorum_epochs_dev(jrq_engine* e, const jrq_group_batch* in, uint32_t K,
   a.last_appended = in->last_appended;
   a.last_committed = in->last_committed;
   a.conf = in->conf;
+  a.run_off = in->run_off;
+  a.run_start = in->run_start;
+  a.run_conf = in->run_conf;
   a.num_peers = in->num_peers;
   a.match_ld = in->match_ld;
   a.committed = committed_out;
@@ -436,8 +468,8 @@ int jrq_crc64_batch(jrq_engine* e, const uint8_t* payload, const uint64_t* offse
   if (!payload || !offsets || !crc_out) return fail(e, JRQ_E_INVALID, "null pointer");
   DeviceGuard guard(e->device);
   int rc;
+  if ((rc = check_monotone(e, offsets, N))) return rc;
   const uint64_t lo = offsets[0], hi = offsets[N];
-  if (hi < lo) return fail(e, JRQ_E_INVALID, "offsets not monotone");
   // stage only the referenced payload window and rebase the offsets onto it
   const uint8_t* dp;
   const uint64_t* doff;
@@ -484,10 +516,8 @@ int jrq_crc64_stream_update(jrq_engine* e, uint64_t* state, const uint8_t* paylo
   if (!state || !payload || !offsets) return fail(e, JRQ_E_INVALID, "null pointer");
   DeviceGuard guard(e->device);
   int rc;
+  if ((rc = check_monotone(e, offsets, S))) return rc;
   const uint64_t lo = offsets[0], hi = offsets[S];
-  if (hi < lo) return fail(e, JRQ_E_INVALID, "offsets not monotone");
-  for (uint32_t s = 0; s < S; ++s)
-    if (offsets[s + 1] < offsets[s]) return fail(e, JRQ_E_INVALID, "offsets not monotone");
   const uint8_t* dp;
   const uint64_t* doff;
   const uint64_t* dstate;
@@ -546,8 +576,8 @@ int jrq_logentry_checksum_batch(jrq_engine* e, const uint8_t* type, const int64_
     return fail(e, JRQ_E_INVALID, "expected and corrupt_out go together");
   DeviceGuard guard(e->device);
   int rc;
+  if ((rc = check_monotone(e, offsets, N))) return rc;
   const uint64_t lo = offsets[0], hi = offsets[N];
-  if (hi < lo) return fail(e, JRQ_E_INVALID, "offsets not monotone");
   const uint8_t *dp, *dt, *dh;
   const uint64_t *doff, *dpx, *dex;
   const int64_t *di, *dtm;
@@ -883,12 +913,11 @@ int jrq_v2_decode_verify(jrq_engine* e, const uint8_t* rec, const uint64_t* off,
   if (!off || !status || !type || !index || !term || !stored || !has_checksum || !data_off ||
       !data_len || !computed || !corrupt)
     return fail(e, JRQ_E_INVALID, "null V2 decode array");
+  int rc;
+  if ((rc = check_monotone(e, off, N))) return rc;
   const uint64_t lo = off[0], hi = off[N];
-  for (uint32_t i = 0; i < N; ++i)
-    if (off[i + 1] < off[i]) return fail(e, JRQ_E_INVALID, "offsets not monotone");
   if (hi > lo && !rec) return fail(e, JRQ_E_INVALID, "null records");
   DeviceGuard guard(e->device);
-  int rc;
   const uint8_t* drec;
   const uint64_t* doff;
   uint8_t dummy = 0;
@@ -954,6 +983,15 @@ int jrq_rccl_init(jrq_engine* e, int nranks, int rank, const uint8_t id_in[128])
   e->nranks = nranks;
   e->rank = rank;
   return JRQ_OK;
+}
+
+int jrq_rccl_nranks(jrq_engine* e) {
+  if (!e) return JRQ_E_INVALID;
+  if (!e->comm) return 0;
+  int n = 0;
+  ncclResult_t r = ncclCommCount(e->comm, &n);
+  if (r != ncclSuccess) return fail(e, JRQ_E_RCCL, "ncclCommCount: %s", ncclGetErrorString(r));
+  return n;
 }
 
 int jrq_publish_committed_dev(jrq_engine* e, const int64_t* local, int64_t* global,

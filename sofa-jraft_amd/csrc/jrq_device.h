@@ -16,8 +16,7 @@ constexpr uint64_t kCrcPoly = 0x42F0E1EBA9EA3693ULL;
 //   shift[kShiftTables][8][256]  multiply-by-x^(8*2^t) mod P byte tables
 constexpr int kShiftTables = 48;  // shifts up to 2^48 - 1 bytes
 
-// LDS image of the slice tables (128 KiB): 8 tables x 8 replicas (crc64.hip Tab8), or the
-// first 4 tables x 16 replicas (Tab4, design probes).
+// LDS image of the slice tables (128 KiB): 8 tables x 8 replicas (crc64.hip Tab8).
 constexpr int kSliceTables = 8;
 constexpr int kCrcLdsBytes = 8 * 256 * 8 * 8;
 constexpr int kCrcBlock = 1024;  // threads per workgroup (16 waves, 1 workgroup / CU)
@@ -87,8 +86,6 @@ struct JrqCrcArgs {
   uint32_t scratch_len;    // entries in acc/cnt/piece_*
   uint32_t lanes;          // lanes of the rounds grid (set by the launcher)
   uint32_t seg_map;        // 0: 64-segment chunks round-robin over workgroups; 1: per workgroup
-  uint64_t* timeline;      // nullable diagnostics (tools/crc_timeline.hip): per wave
-                           // {start, end (s_memrealtime), HW_ID, XCC_ID}
   uint64_t seg_bytes;      // nonzero: segment size (rounded up to 256 B; tests / tuning)
   uint32_t prio_steps;     // 1: waves lower their priority as they progress (crc64.hip)
   uint32_t regs_slowpath;  // 1: boundary half-rounds hash from registers (crc64_rounds_kernel<true>)

@@ -16,14 +16,16 @@
 // The result does not depend on the order of the epoch's acks, as for the reference
 // (every grant is idempotent and a commit takes the max granted index).
 //
-// One lane per group, grid-stride; every per-peer match row is a coalesced int64 stream.
-// HBM-bound: 8P + 41 bytes per group decision (roofline).
+// Groups whose conf word carries JRQ_CONF_RUNS walk their conf runs (run table); every other
+// group is decided from its conf word alone.  HBM-bound: 8P + 41 bytes per group decision
+// (roofline).
 #include "jrq_device.h"
 
 namespace jrq {
 
 constexpr int64_t kI64Min = INT64_MIN;
 constexpr int64_t kI64Max = INT64_MAX;
+constexpr uint64_t kConfRuns = 1ull << 63;  // include/jrq.h JRQ_CONF_RUNS
 
 // q-th largest of v[p] over the peers in `mask` (q >= 1); kI64Min if fewer than q members.
 // P <= 16: rank-by-counting, branch-free, P^2 compares on 64-bit values in registers.
@@ -82,8 +84,72 @@ __device__ __forceinline__ void decide_single(int64_t pi, int64_t la, int64_t lc
   st_out = pi == 0 ? kStNotLeader : st;
 }
 
-// General path: one lane per group, optional conf runs.  Every load of the group is
-// issued before any decision, so a group costs one memory round trip.
+// Runs [r0, r1) of one group: run r covers [run_start[r], run_start[r+1]) (the last run ends at
+// lastAppended, the first starts at or before pendingIndex).  best is max(lc, the largest
+// granted index over the runs); each run is evaluated on its own, which reproduces the
+// reference's non-monotone commit when an even-size conf shrinks (BallotBox.java:124-129).
+template <int P>
+__device__ __forceinline__ int64_t runs_best(const JrqQuorumArgs& a, uint32_t r0, uint32_t r1,
+                                             int64_t pi, int64_t la, int64_t lc,
+                                             const int64_t (&m)[P], uint8_t& st) {
+  int64_t best = lc;
+#pragma unroll 1
+  for (uint32_t r = r0; r < r1; ++r) {
+    const int64_t s = (r == r0) ? pi : (a.run_start[r] > pi ? a.run_start[r] : pi);
+    const int64_t e = (r + 1 < r1) ? a.run_start[r + 1] - 1 : la;
+    const int64_t ee = e < la ? e : la;
+    if (ee < s) continue;  // run entirely committed already (or empty)
+    const uint64_t cw = a.run_conf[r];
+    if ((cw & 0xFFFFu) == 0) st |= kStEmptyConf;
+    int64_t cand = run_bound<P>(m, cw);
+    cand = cand < ee ? cand : ee;
+    best = (cand >= s && cand > best) ? cand : best;
+  }
+  return best;
+}
+
+// A group flagged JRQ_CONF_RUNS: its runs from the CSR run table.
+template <int P>
+__device__ __forceinline__ void decide_runs(const JrqQuorumArgs& a, uint32_t g, int64_t pi,
+                                            int64_t la, int64_t lc, int64_t (&m)[P],
+                                            int64_t& out, uint8_t& st_out) {
+  if (pi == 0) {
+    out = lc;
+    st_out = kStNotLeader;
+    return;
+  }
+  uint8_t st = mask_out_of_range<P>(m, la);
+  out = runs_best<P>(a, a.run_off[g], a.run_off[g + 1], pi, la, lc, m, st);
+  st_out = st;
+}
+
+// The run path of the pair kernel: reloads the group (L2 / HBM, flagged groups only) so that
+// no register of the fast path stays live across it (occupancy of the common case).
+template <int P>
+__device__ __forceinline__ void redecide_runs(const JrqQuorumArgs& a, uint32_t g) {
+  int64_t m[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
+  int64_t out;
+  uint8_t st;
+  decide_runs<P>(a, g, a.pending_index[g], a.last_appended[g], a.last_committed[g], m, out, st);
+  a.committed[g] = out;
+  a.status[g] = st;
+}
+
+template <int P>
+__device__ __forceinline__ void decide(const JrqQuorumArgs& a, uint32_t g, int64_t pi, int64_t la,
+                                       int64_t lc, uint64_t cw, int64_t (&m)[P], int64_t& out,
+                                       uint8_t& st) {
+  if (a.run_off != nullptr && (cw & kConfRuns))
+    decide_runs<P>(a, g, pi, la, lc, m, out, st);
+  else
+    decide_single<P>(pi, la, lc, cw, m, out, st);
+}
+
+// General path (unaligned arrays, odd strides): one lane per group.  Every load of the group
+// is issued before any decision, so a group costs one memory round trip (two more for a
+// group that walks its runs).
 template <int P>
 __global__ __launch_bounds__(256) void quorum_epoch_kernel(JrqQuorumArgs a) {
   const uint32_t stride = gridDim.x * blockDim.x;
@@ -91,157 +157,191 @@ __global__ __launch_bounds__(256) void quorum_epoch_kernel(JrqQuorumArgs a) {
     const int64_t pi = a.pending_index[g];
     const int64_t lc = a.last_committed[g];
     const int64_t la = a.last_appended[g];
+    const uint64_t cw = a.conf[g];
     int64_t m[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
-    if (a.run_off == nullptr) {
-      const uint64_t cw = a.conf[g];
-      int64_t out;
-      uint8_t st;
-      decide_single<P>(pi, la, lc, cw, m, out, st);
-      a.committed[g] = out;
-      a.status[g] = st;
-      continue;
-    }
-    const uint32_t r0 = a.run_off[g], r1 = a.run_off[g + 1];
-    if (pi == 0) {
-      a.committed[g] = lc;
-      a.status[g] = kStNotLeader;
-      continue;
-    }
-    uint8_t st = mask_out_of_range<P>(m, la);
-    int64_t best = lc;
-    for (uint32_t r = r0; r < r1; ++r) {
-      const int64_t s = (r == r0) ? pi : (a.run_start[r] > pi ? a.run_start[r] : pi);
-      const int64_t e = (r + 1 < r1) ? a.run_start[r + 1] - 1 : la;
-      const int64_t ee = e < la ? e : la;
-      if (ee < s) continue;  // run entirely committed already (or empty)
-      const uint64_t cw = a.run_conf[r];
-      if ((cw & 0xFFFFu) == 0) st |= kStEmptyConf;
-      int64_t cand = run_bound<P>(m, cw);
-      cand = cand < ee ? cand : ee;
-      best = (cand >= s && cand > best) ? cand : best;
-    }
-    a.committed[g] = best;
+    int64_t out;
+    uint8_t st;
+    decide<P>(a, g, pi, la, lc, cw, m, out, st);
+    a.committed[g] = out;
     a.status[g] = st;
   }
 }
 
 typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
 
-template <bool NT>
-__device__ __forceinline__ i64x2 ld2(const int64_t* p) {
-  const i64x2* q = reinterpret_cast<const i64x2*>(p);
-  if (NT) return __builtin_nontemporal_load(q);
-  return *q;
+__device__ __forceinline__ i64x2 ld2nt(const int64_t* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(p));
 }
 
-// Fast path (no run table, 16-B aligned arrays, even match_ld): one lane decides two
-// adjacent groups per unit; every stream is read with 16-byte loads (1 KiB per wave
-// instruction) and the two status bytes are stored as one 16-bit word.  A lane takes U
-// units 256 pairs apart (its workgroup's block of 256*U pairs) and issues every load of
-// all U units before the first decision; NT marks the streams non-temporal (read once,
-// never re-read: no point keeping them in L2 / MALL).
-template <int P, int U, bool NT>
+// Fast path (16-B aligned arrays, even match_ld): one lane decides two adjacent groups; every
+// stream is read with 16-byte non-temporal loads (1 KiB per wave instruction; each input is
+// read once per epoch, so it is not kept in L2 / MALL) and the two status bytes are stored as
+// one 16-bit word.  A group flagged JRQ_CONF_RUNS (joint consensus with a conf change in its
+// pending window) walks its runs in place: only that lane's wave waits on the run table.
+template <int P>
 __global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
+  // one pair per lane, no grid-stride loop: the rare run path at the end then shares the
+  // register budget with nothing (the launcher sizes the grid to G / 512 workgroups)
   const uint32_t pairs = a.G >> 1;
-  const uint32_t step = gridDim.x * 256u * U;
-  for (uint32_t t0 = blockIdx.x * 256u * U + threadIdx.x; t0 < pairs; t0 += step) {
-    i64x2 pi[U], lc[U], la[U], cw[U], m[U][P];
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  if (t < pairs) {
+    const uint32_t g = t << 1;
+    const i64x2 pi = ld2nt(a.pending_index + g);
+    const i64x2 lc = ld2nt(a.last_committed + g);
+    const i64x2 la = ld2nt(a.last_appended + g);
+    const i64x2 cw = ld2nt(reinterpret_cast<const int64_t*>(a.conf) + g);
+    i64x2 m[P];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t t = t0 + 256u * u;
-      if (t >= pairs) continue;
-      const uint32_t g = t << 1;
-      pi[u] = ld2<NT>(a.pending_index + g);
-      lc[u] = ld2<NT>(a.last_committed + g);
-      la[u] = ld2<NT>(a.last_appended + g);
-      cw[u] = ld2<NT>(reinterpret_cast<const int64_t*>(a.conf) + g);
+    for (int p = 0; p < P; ++p) m[p] = ld2nt(a.match + static_cast<size_t>(p) * a.match_ld + g);
+    int64_t m0[P], m1[P];
 #pragma unroll
-      for (int p = 0; p < P; ++p) m[u][p] = ld2<NT>(a.match + static_cast<size_t>(p) * a.match_ld + g);
+    for (int p = 0; p < P; ++p) {
+      m0[p] = m[p].x;
+      m1[p] = m[p].y;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t t = t0 + 256u * u;
-      if (t >= pairs) continue;
-      const uint32_t g = t << 1;
-      int64_t m0[P], m1[P];
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        m0[p] = m[u][p].x;
-        m1[p] = m[u][p].y;
-      }
-      int64_t o0, o1;
-      uint8_t s0, s1;
-      decide_single<P>(pi[u].x, la[u].x, lc[u].x, static_cast<uint64_t>(cw[u].x), m0, o0, s0);
-      decide_single<P>(pi[u].y, la[u].y, lc[u].y, static_cast<uint64_t>(cw[u].y), m1, o1, s1);
-      i64x2 out;
-      out.x = o0;
-      out.y = o1;
-      const uint16_t st = static_cast<uint16_t>(s0 | (s1 << 8));
-      if (NT) {
-        __builtin_nontemporal_store(out, reinterpret_cast<i64x2*>(a.committed + g));
-        __builtin_nontemporal_store(st, reinterpret_cast<uint16_t*>(a.status + g));
-      } else {
-        *reinterpret_cast<i64x2*>(a.committed + g) = out;
-        *reinterpret_cast<uint16_t*>(a.status + g) = st;
-      }
+    const uint32_t flags = static_cast<uint32_t>(static_cast<uint64_t>(cw.x) >> 63) |
+                           (static_cast<uint32_t>(static_cast<uint64_t>(cw.y) >> 63) << 1);
+    int64_t o0, o1;
+    uint8_t s0, s1;
+    decide_single<P>(pi.x, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
+    decide_single<P>(pi.y, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
+    i64x2 out;
+    out.x = o0;
+    out.y = o1;
+    __builtin_nontemporal_store(out, reinterpret_cast<i64x2*>(a.committed + g));
+    __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
+                                reinterpret_cast<uint16_t*>(a.status + g));
+    // rare: a flagged group is re-decided from its runs and its outputs rewritten (same lane,
+    // same addresses: program order), so nothing of the fast path stays live across this
+    if (a.run_off != nullptr && flags != 0) {
+      if (flags & 1u) redecide_runs<P>(a, g);
+      if (flags & 2u) redecide_runs<P>(a, g + 1);
     }
   }
   // odd G: the last group goes through the scalar decision
-  if ((a.G & 1u) && blockIdx.x == 0 && threadIdx.x == 0) {
+  if ((a.G & 1u) && t == 0) {
     const uint32_t g = a.G - 1;
     int64_t m[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
     int64_t out;
     uint8_t st;
-    decide_single<P>(a.pending_index[g], a.last_appended[g], a.last_committed[g], a.conf[g], m,
-                     out, st);
+    decide<P>(a, g, a.pending_index[g], a.last_appended[g], a.last_committed[g], a.conf[g], m,
+              out, st);
     a.committed[g] = out;
     a.status[g] = st;
   }
 }
 
-// K successive epochs of the same groups in one launch (hard part 4: a
-// 10k-group epoch is launch-bound).  Between epochs the group state moves as BallotBox
-// moves it: a commit sets lastCommittedIndex and pendingIndex = lastCommittedIndex + 1
-// (BallotBox.java:131-134); a group that is not the leader stays so.  Epoch k reads its
-// own match snapshot and lastAppended (entries appended since); the conf is per group.
-// One lane per group; the loads of 4 epochs are issued before their decisions (8 measured
-// slower on C2: 31.6 vs 27.8 us for 64 epochs).
+// ------------------------------------------------------ K epochs per launch ---
+// K successive epochs of the same G groups (hard part 4: a 10k-group epoch is
+// launch-bound).  Between epochs the group state moves as BallotBox moves it: a commit sets
+// lastCommittedIndex and pendingIndex = lastCommittedIndex + 1 (BallotBox.java:131-134); a
+// group that is not the leader stays so.  That carried state is a thresholded prefix max:
+//   v_k = max over the group's runs r of { cand_rk : cand_rk >= s_r },
+//         cand_rk = min(end_r, la_k, bound_r(match_k)),  s_r = max(start_r, pi_0) (first: pi_0)
+//   committed_k = max(lc_0, max_{j <= k} v_j)
+//   pi_k = committed_{k-1} + 1 once a commit happened (max_{j<k} v_j > lc_0), else pi_0
+// (a candidate in [s_r, committed_{k-1}] that the reference would refuse because it is below
+// pi_k cannot raise the max, so the threshold may stay at pi_0).  v_k depends on epoch k's
+// inputs only: lanes run over (group, epoch) -- a workgroup holds 64 groups, each of its W
+// waves C epochs of them -- and a scan over the waves' chunk maxima in LDS stitches the
+// prefix.  Loads stay coalesced (64 consecutive groups per row and epoch).
 template <int P>
-__global__ __launch_bounds__(256) void quorum_epochs_kernel(JrqQuorumArgs a, uint32_t K,
-                                                            uint64_t match_eld, uint64_t la_eld) {
-  constexpr uint32_t kEpochUnroll = 4;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G; g += stride) {
-    int64_t pi = a.pending_index[g];
-    int64_t lc = a.last_committed[g];
-    const uint64_t cw = a.conf[g];
-    for (uint32_t k0 = 0; k0 < K; k0 += kEpochUnroll) {
-      int64_t m[kEpochUnroll][P], la[kEpochUnroll];
+struct EpochChunk {
+  static constexpr int kC = (16 / (P + 1)) < 1 ? 1 : ((16 / (P + 1)) > 8 ? 8 : 16 / (P + 1));
+  static constexpr int kMaxWaves = P <= 8 ? 16 : 8;  // 128 / 256 VGPRs per lane
+};
+
+template <int P>
+__global__ __launch_bounds__(64 * EpochChunk<P>::kMaxWaves) void quorum_epochs_kernel(JrqQuorumArgs a, uint32_t K,
+                                                             uint64_t match_eld, uint64_t la_eld) {
+  constexpr int C = EpochChunk<P>::kC;
+  __shared__ int64_t chunk_max[16][64];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, W = blockDim.x >> 6;
+  const uint32_t g = blockIdx.x * 64u + lane;
+  const bool live = g < a.G;
+  const int64_t pi0 = live ? a.pending_index[g] : 0;
+  const int64_t lc0 = live ? a.last_committed[g] : 0;
+  const uint64_t cw = live ? a.conf[g] : 0;
+  const bool runs = a.run_off != nullptr && (cw & kConfRuns);
+  const uint32_t r0 = runs ? a.run_off[g] : 0, r1 = runs ? a.run_off[g + 1] : 0;
+  int64_t carry = kI64Min;  // max v over the epochs of earlier super-chunks
+  for (uint32_t base = 0; base < K; base += W * C) {
+    const uint32_t k0 = base + w * C;
+    int64_t la[C], pre[C];
+    uint8_t st[C];
+    {
+      int64_t m[C][P];
 #pragma unroll
-      for (uint32_t u = 0; u < kEpochUnroll; ++u) {
-        if (k0 + u >= K) break;
-        const size_t k = k0 + u;
-        la[u] = a.last_appended[k * la_eld + g];
+      for (int c = 0; c < C; ++c) {
+        const size_t k = k0 + c;
+        if (!live || k >= K) continue;
+        la[c] = __builtin_nontemporal_load(a.last_appended + k * la_eld + g);
 #pragma unroll
         for (int p = 0; p < P; ++p)
-          m[u][p] = a.match[k * match_eld + static_cast<size_t>(p) * a.match_ld + g];
+          m[c][p] = __builtin_nontemporal_load(a.match + k * match_eld +
+                                               static_cast<size_t>(p) * a.match_ld + g);
       }
+      int64_t run_max = kI64Min;
 #pragma unroll
-      for (uint32_t u = 0; u < kEpochUnroll; ++u) {
-        if (k0 + u >= K) break;
-        const size_t k = k0 + u;
-        int64_t out;
-        uint8_t st;
-        decide_single<P>(pi, la[u], lc, cw, m[u], out, st);
-        a.committed[k * a.G + g] = out;
-        a.status[k * a.G + g] = st;
-        if (pi != 0 && out > lc) pi = out + 1;
-        lc = out;
+      for (int c = 0; c < C; ++c) {
+        st[c] = 0;
+        if (live && k0 + c < K) {
+          st[c] = mask_out_of_range<P>(m[c], la[c]);
+          int64_t v;
+          if (!runs) {
+            int64_t cand = run_bound<P>(m[c], cw);
+            cand = cand < la[c] ? cand : la[c];
+            v = cand >= pi0 ? cand : kI64Min;
+          } else {
+            uint8_t unused = 0;
+            v = runs_best<P>(a, r0, r1, pi0, la[c], kI64Min, m[c], unused);
+          }
+          run_max = v > run_max ? v : run_max;
+        }
+        pre[c] = run_max;  // inclusive max over this wave's chunk
       }
+    }
+    chunk_max[w][lane] = pre[C - 1];
+    __syncthreads();
+    int64_t excl = carry, all = carry;
+    for (uint32_t u = 0; u < W; ++u) {
+      const int64_t t = chunk_max[u][lane];
+      if (u < w) excl = t > excl ? t : excl;
+      all = t > all ? t : all;
+    }
+    __syncthreads();  // chunk_max is rewritten by the next super-chunk
+    carry = all;
+    if (!live) continue;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const uint32_t k = k0 + c;
+      if (k >= K) break;
+      const int64_t prev = c == 0 ? excl : (pre[c - 1] > excl ? pre[c - 1] : excl);
+      const int64_t mk = pre[c] > excl ? pre[c] : excl;
+      int64_t out = mk > lc0 ? mk : lc0;
+      uint8_t s = st[c];
+      if (pi0 == 0) {
+        out = lc0;
+        s = kStNotLeader;
+      } else {
+        const int64_t pik = prev > lc0 ? prev + 1 : pi0;  // pendingIndex before epoch k
+        if (!runs) {
+          if ((cw & 0xFFFFu) == 0 && la[c] >= pik) s |= kStEmptyConf;
+        } else {  // runs still pending at epoch k with an empty conf (L2-hot re-read)
+          for (uint32_t r = r0; r < r1; ++r) {
+            const int64_t sr = (r == r0) ? pik : (a.run_start[r] > pik ? a.run_start[r] : pik);
+            const int64_t er = (r + 1 < r1) ? a.run_start[r + 1] - 1 : la[c];
+            if ((er < la[c] ? er : la[c]) >= sr && (a.run_conf[r] & 0xFFFFu) == 0)
+              s |= kStEmptyConf;
+          }
+        }
+      }
+      a.committed[static_cast<size_t>(k) * a.G + g] = out;
+      a.status[static_cast<size_t>(k) * a.G + g] = s;
     }
   }
 }
@@ -335,40 +435,23 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
   const dim3 blk(256);
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
   const JrqQuorumArgs& a = *args;
-  const bool pair = a.run_off == nullptr && (a.match_ld & 1u) == 0 && al16(a.match) &&
-                    al16(a.pending_index) && al16(a.last_appended) && al16(a.last_committed) &&
-                    al16(a.conf) && al16(a.committed) &&
-                    (reinterpret_cast<uintptr_t>(a.status) & 1u) == 0 && a.G >= 2;
-  // pair-kernel variant (A/B knob JRQ_Q_VARIANT): 0 = 1 unit/lane, 1 = 1 unit/lane with
-  // non-temporal streams (default: 4.96 vs 4.58-4.74 TB/s on C3), 2 = 2 units/lane,
-  // 3 = 2 units/lane non-temporal
-  static const int variant = [] {
-    const char* v = std::getenv("JRQ_Q_VARIANT");
-    return v ? std::atoi(v) : 1;
-  }();
-  const int units = (variant == 2 || variant == 3) ? 2 : 1;
-  // enough 256-thread blocks for one lane per group (pair: per two per unit), at most 8 per CU
-  const uint64_t lanes = pair ? ((a.G >> 1) + units - 1) / units : a.G;
+  const bool pair = (a.match_ld & 1u) == 0 && al16(a.match) && al16(a.pending_index) &&
+                    al16(a.last_appended) && al16(a.last_committed) && al16(a.conf) &&
+                    al16(a.committed) && (reinterpret_cast<uintptr_t>(a.status) & 1u) == 0 &&
+                    a.G >= 2;
+  // pair kernel: one lane per two groups, the whole grid at once; scalar kernel: one lane per
+  // group, at most 8 workgroups per CU, grid-stride beyond
+  const uint64_t lanes = pair ? (a.G >> 1) : a.G;
   const uint64_t need = (lanes + 255) / 256;
-  const uint64_t cap = static_cast<uint64_t>(num_cus) * 8;
-  const int grid = static_cast<int>(need < cap ? (need ? need : 1) : cap);
+  const uint64_t cap = pair ? need : static_cast<uint64_t>(num_cus) * 8;
+  const dim3 grid(static_cast<unsigned>(need < cap ? (need ? need : 1) : cap));
   switch (args->num_peers) {
-#define JRQ_CASE(P)                                                                            \
-  case P:                                                                                      \
-    if (!pair)                                                                                 \
-      hipLaunchKernelGGL(jrq::quorum_epoch_kernel<P>, dim3(grid), blk, 0, stream, *args);      \
-    else if (variant == 0)                                                                     \
-      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, 1, false>), dim3(grid), blk, 0,    \
-                         stream, *args);                                                       \
-    else if (variant == 2)                                                                     \
-      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, 2, false>), dim3(grid), blk, 0,    \
-                         stream, *args);                                                       \
-    else if (variant == 3)                                                                     \
-      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, 2, true>), dim3(grid), blk, 0,     \
-                         stream, *args);                                                       \
-    else                                                                                       \
-      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, 1, true>), dim3(grid), blk, 0,     \
-                         stream, *args);                                                       \
+#define JRQ_CASE(P)                                                                      \
+  case P:                                                                                \
+    if (pair)                                                                            \
+      hipLaunchKernelGGL(jrq::quorum_epoch_pair_kernel<P>, grid, blk, 0, stream, *args); \
+    else                                                                                 \
+      hipLaunchKernelGGL(jrq::quorum_epoch_kernel<P>, grid, blk, 0, stream, *args);      \
     break;
     JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
     JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
@@ -383,14 +466,18 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum_epochs(
     const JrqQuorumArgs* args, uint32_t K, uint64_t match_eld, uint64_t la_eld, int num_cus,
     hipStream_t stream) {
-  const uint64_t need = (static_cast<uint64_t>(args->G) + 255) / 256;
-  const uint64_t cap = static_cast<uint64_t>(num_cus) * 8;
-  const dim3 grid(static_cast<unsigned>(need < cap ? (need ? need : 1) : cap)), blk(256);
+  (void)num_cus;
+  // one workgroup per 64 groups; W waves of C epochs each (W <= 16), super-chunks beyond W*C
+  const dim3 grid(static_cast<unsigned>((static_cast<uint64_t>(args->G) + 63) / 64));
+  auto waves = [K](uint32_t C, uint32_t wmax) {
+    const uint32_t w = (K + C - 1) / C;
+    return dim3(64u * (w < wmax ? w : wmax));
+  };
   switch (args->num_peers) {
-#define JRQ_CASE(P)                                                                      \
-  case P:                                                                                \
-    hipLaunchKernelGGL(jrq::quorum_epochs_kernel<P>, grid, blk, 0, stream, *args, K,     \
-                       match_eld, la_eld);                                               \
+#define JRQ_CASE(P)                                                                         \
+  case P:                                                                                   \
+    hipLaunchKernelGGL(jrq::quorum_epochs_kernel<P>, grid, waves(jrq::EpochChunk<P>::kC, jrq::EpochChunk<P>::kMaxWaves), 0, \
+                       stream, *args, K, match_eld, la_eld);                                \
     break;
     JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
     JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)

@@ -20,6 +20,7 @@ ST_OK, ST_NOT_LEADER, ST_OUT_OF_RANGE, ST_EMPTY_CONF = 0, 1, 2, 4
 FAN_NONE, FAN_APPLY, FAN_SKIP, FAN_INVALID = 0, 1, 2, 3  # jrq_fanout_status
 V2_OK, V2_NULL, V2_V1, V2_HOST = 0, 1, 2, 3  # jrq_v2_status
 MAX_PEERS = 16
+CONF_RUNS = 1 << 63  # JRQ_CONF_RUNS: the group's pending window holds several conf runs
 
 
 class JrqError(RuntimeError):
@@ -83,6 +84,7 @@ SIGNATURES = [
     ("jrq_v2_decode_verify", C.c_int, [_V, _V, _V, C.c_uint32] + [_V] * 11),
     ("jrq_rccl_get_unique_id", C.c_int, [_V]),
     ("jrq_rccl_init", C.c_int, [_V, C.c_int, C.c_int, _V]),
+    ("jrq_rccl_nranks", C.c_int, [_V]),
     ("jrq_publish_committed_dev", C.c_int, [_V, _V, _V, C.c_uint64]),
 ]
 

@@ -68,3 +68,50 @@ def shard_batch(batch: dict, G: int, world: int, rank: int) -> dict:
         out["run_start"] = np.ascontiguousarray(batch["run_start"][a:b])
         out["run_conf"] = np.ascontiguousarray(batch["run_conf"][a:b])
     return out
+
+
+class ShardedEpochs:
+    """One rank's share of the node-wide multi-Raft epoch loop -- the orchestration
+    `bench.py --gpus N` runs, with the kernel and the collective injected so that CPU tests
+    (gloo, the oracle as the kernel) exercise the same code.
+
+    Each step runs the rank's epoch on its contiguous groupId block (`epoch_fn(i, local)` writes
+    the block's committed[] into `local`, the padded all-gather send buffer of `per_rank(G,
+    world)` slots); every `publish_every`-th step publishes the node-wide snapshot with
+    `allgather_fn(local, snapshot)` (RCCL over xGMI on GPUs: jrq_publish_committed_dev).
+    Publishing every K epochs trades snapshot staleness for collective time (SURVEY.md §8e,
+    §7 hard part 5): getLastCommittedIndex readers on other GPUs see commits up to K-1 epochs
+    late, never wrong ones, since committed indices only grow."""
+
+    def __init__(self, G: int, world: int, rank: int, epoch_fn, allgather_fn, local, snapshot,
+                 publish_every: int = 1):
+        if publish_every < 1:
+            raise ValueError("publish_every must be >= 1")
+        if len(local) != per_rank(G, world) or len(snapshot) != per_rank(G, world) * world:
+            raise ValueError("local / snapshot sizes do not match the padded shard layout")
+        self.G, self.world, self.rank = G, world, rank
+        self.lo, self.hi = shard_bounds(G, world, rank)
+        self.epoch_fn, self.allgather_fn = epoch_fn, allgather_fn
+        self.local, self.snapshot = local, snapshot
+        self.publish_every = publish_every
+        self.steps = 0
+        self.published = 0
+
+    def epoch(self):
+        """The rank's epoch only (the kernel-only timing)."""
+        self.epoch_fn(self.steps, self.local)
+        self.steps += 1
+
+    def publish(self):
+        self.allgather_fn(self.local, self.snapshot)
+        self.published += 1
+
+    def step(self):
+        """One epoch, plus the publication when it is due."""
+        self.epoch()
+        if self.steps % self.publish_every == 0:
+            self.publish()
+
+    def snapshot_groups(self, to_numpy=np.asarray) -> np.ndarray:
+        """The last published snapshot as committed[G] in groupId order."""
+        return unpad_snapshot(to_numpy(self.snapshot), self.G, self.world)

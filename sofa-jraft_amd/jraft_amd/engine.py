@@ -126,13 +126,15 @@ class Engine:
                                            _dev_ptr(status_out), G), self._h)
 
     def quorum_epochs_dev(self, match, pending_index, last_appended, last_committed, conf,
-                          committed_out, status_out):
+                          committed_out, status_out, run_off=None, run_start=None, run_conf=None):
         """K epochs in one launch: match [K, P, ld], last_appended [K, G] (torch tensors);
-        committed_out / status_out [K, G]."""
+        committed_out / status_out [K, G].  Conf runs (groups flagged CONF_RUNS in conf) hold
+        for all K epochs."""
         K, P = match.shape[0], match.shape[1]
         G = pending_index.shape[0]
         b = self._batch(_dev_ptr, match, pending_index, last_appended, last_committed, conf,
-                        None, None, None, num_peers=P, match_ld=match.stride(1), num_runs=0)
+                        run_off, run_start, run_conf, num_peers=P, match_ld=match.stride(1),
+                        num_runs=0 if run_start is None else run_start.shape[0])
         check(self._L.jrq_quorum_epochs_dev(self._h, C.byref(b), K, match.stride(0),
                                             last_appended.stride(0), _dev_ptr(committed_out),
                                             _dev_ptr(status_out), G), self._h)
@@ -331,6 +333,13 @@ class Engine:
     def rccl_init(self, nranks: int, rank: int, uid: bytes):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         check(self._L.jrq_rccl_init(self._h, nranks, rank, buf), self._h)
+
+    def rccl_nranks(self) -> int:
+        """Ranks RCCL counts in this engine's communicator (0 before rccl_init)."""
+        n = self._L.jrq_rccl_nranks(self._h)
+        if n < 0:
+            check(n, self._h)
+        return n
 
     def publish_committed_dev(self, local, global_out):
         check(self._L.jrq_publish_committed_dev(self._h, _dev_ptr(local), _dev_ptr(global_out),

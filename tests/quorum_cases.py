@@ -81,3 +81,56 @@ def even_removal_batch():
     run_conf = np.array([conf_word(0b1111), conf_word(0b0111)], np.uint64)
     return dict(match=match, pending_index=pi, last_appended=la, last_committed=lc,
                 conf=run_conf[:1].copy(), run_off=run_off, run_start=run_start, run_conf=run_conf)
+
+
+def flag_runs(b):
+    """conf words flagged CONF_RUNS for the groups with more than one run (as the host variant
+    derives them), for calling the *_dev entry points with a run table."""
+    from jraft_amd import CONF_RUNS
+    ro = b["run_off"]
+    cnt = ro[1:] - ro[:-1]
+    one = b["run_conf"][np.minimum(ro[:-1], len(b["run_conf"]) - 1)] if len(b["run_conf"]) else b["conf"]
+    conf = np.where(cnt == 1, one & np.uint64(~CONF_RUNS & (2**64 - 1)),
+                    b["conf"] | np.uint64(CONF_RUNS))
+    return conf.astype(np.uint64)
+
+
+def random_series(seed, G, P, K, run_prob=0.3, step=8):
+    """K successive epochs of one group batch with fixed conf runs: epoch k's match snapshot and
+    lastAppended (both non-decreasing over k), the state before epoch 0 and the run table.
+    Some groups are not the leader, some acks run past lastAppended."""
+    b = random_batch(seed, G, P, pend_max=32, run_prob=run_prob)
+    rng = np.random.default_rng(seed + 7)
+    la = np.empty((K, G), np.int64)
+    match = np.empty((K, P, G), np.int64)
+    la[0] = b["last_appended"]
+    match[0] = b["match"]
+    for k in range(1, K):
+        la[k] = la[k - 1] + rng.integers(0, step + 1, G)
+        adv = rng.integers(0, 2 * step + 1, (P, G))
+        stay = rng.random((P, G)) < 0.3
+        match[k] = np.where(stay, match[k - 1], np.minimum(np.maximum(match[k - 1], 0) + adv, la[k]))
+        oor = rng.random(G) < 0.02
+        rows = np.where(oor)[0]
+        match[k, rng.integers(0, P, len(rows)), rows] = la[k, rows] + 1
+    return dict(match=match, last_appended=la, pending_index=b["pending_index"],
+                last_committed=b["last_committed"], conf=b["conf"], run_off=b["run_off"],
+                run_start=b["run_start"], run_conf=b["run_conf"])
+
+
+def series_replay(oracle, s, chunk=5):
+    """Expected committed/status of every epoch: K sequential oracle replays, the state carried
+    as BallotBox carries it (commit -> lastCommittedIndex, pendingIndex = commit + 1)."""
+    K = s["match"].shape[0]
+    pi = s["pending_index"].copy()
+    lc = s["last_committed"].copy()
+    outs, sts = [], []
+    for k in range(K):
+        ce, se, _ = oracle.quorum_epoch_replay(s["match"][k], pi, s["last_appended"][k], lc,
+                                               s["conf"], s.get("run_off"), s.get("run_start"),
+                                               s.get("run_conf"), chunk=chunk)
+        pi = np.where((pi != 0) & (ce > lc), ce + 1, pi)
+        lc = ce
+        outs.append(ce)
+        sts.append(se)
+    return np.stack(outs), np.stack(sts)

@@ -55,6 +55,78 @@ def _worker(rank, world, port, G, q):
         dist.destroy_process_group()
 
 
+def _engine_worker(rank, world, port, G, K, every, q):
+    """The bench's orchestration (jraft_amd.dist.ShardedEpochs) with the oracle standing in for
+    the epoch kernel and gloo for RCCL: K epochs of a C3-shaped series, publish every `every`."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "sofa-jraft_amd"), os.path.join(root, "oracle")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+
+    import jraft_oracle as O
+    from jraft_amd import dist as D
+    from jraft_amd import workloads as W
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = D.shard_bounds(G, world, rank)
+        series = W.quorum_epoch_series("C3", K, groups=G)
+        state = {"pi": series["pending_index"][lo:hi].copy(), "lc": series["last_committed"][lo:hi].copy()}
+
+        def epoch_fn(i, local):
+            c, _, _ = O.quorum_epoch_replay(series["match"][i][:, lo:hi], state["pi"],
+                                            series["last_appended"][i][lo:hi], state["lc"],
+                                            series["conf"][lo:hi], chunk=1024)
+            state["pi"] = np.where((state["pi"] != 0) & (c > state["lc"]), c + 1, state["pi"])
+            state["lc"] = c
+            local[: hi - lo] = torch.from_numpy(c)
+
+        k = D.per_rank(G, world)
+        local = torch.full((k,), -1, dtype=torch.int64)
+        snap = torch.empty(k * world, dtype=torch.int64)
+        se = D.ShardedEpochs(G, world, rank, epoch_fn,
+                             lambda send, recv: dist.all_gather_into_tensor(recv, send), local,
+                             snap, publish_every=every)
+        snaps = []
+        for _ in range(K):
+            before = se.published
+            se.step()
+            if se.published != before:
+                snaps.append(se.snapshot_groups(lambda t: t.numpy()).copy())
+        if rank == 0:
+            q.put((se.published, snaps))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("G,K,every", [(1001, 4, 1), (513, 5, 2)])
+def test_sharded_epochs_orchestration(oracle, G, K, every):
+    """bench.py --gpus N's loop (ShardedEpochs) at world 2: every published snapshot equals the
+    unsharded oracle series at that epoch; publications happen every `every` epochs."""
+    from quorum_cases import series_replay
+    from jraft_amd import workloads as W
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engine_worker, args=(r, world, port, G, K, every, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    published, snaps = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert published == K // every == len(snaps)
+    series = W.quorum_epoch_series("C3", K, groups=G)
+    expect, _ = series_replay(oracle, series, chunk=1024)
+    for j, snap in enumerate(snaps):
+        np.testing.assert_array_equal(snap, expect[(j + 1) * every - 1])
+
+
 @pytest.mark.parametrize("G", [1001, 64])
 def test_sharded_snapshot_equals_unsharded(oracle, G):
     from quorum_cases import random_batch

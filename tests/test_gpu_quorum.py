@@ -179,3 +179,52 @@ def test_gpu_quorum_epochs_series_vs_oracle(engine, cfg, G, K):
     assert np.array_equal(st.cpu().numpy(), se)
     if K > 1:
         assert (ce[-1] > ce[0]).any()  # commits actually move across epochs
+
+
+def _to_dev(b, keys):
+    import torch
+    dev = torch.device("cuda:0")
+    return {k: torch.from_numpy(np.ascontiguousarray(b[k].view(np.int64) if b[k].dtype == np.uint64
+                                                     else b[k])).to(dev) for k in keys}
+
+
+@pytest.mark.parametrize("P,run_prob", [(5, 0.01), (3, 0.3), (8, 0.05)])
+def test_dev_fast_path_with_flagged_runs(engine, oracle, P, run_prob):
+    """Device batch with aligned arrays (pair kernel) where only JRQ_CONF_RUNS groups walk the
+    run table: a conf-changing group no longer demotes the launch, and every group -- flagged
+    or not -- matches the replay through real BallotBoxes."""
+    import torch
+    from quorum_cases import flag_runs
+    G = 4096
+    b = random_batch(500 + P, G, P, run_prob=run_prob)
+    b["conf"] = flag_runs(b)
+    ce, se = _replay(oracle, b)
+    t = _to_dev(b, ["match", "pending_index", "last_appended", "last_committed", "conf",
+                    "run_off", "run_start", "run_conf"])
+    out = torch.empty(G, dtype=torch.int64, device="cuda:0")
+    st = torch.empty(G, dtype=torch.uint8, device="cuda:0")
+    engine.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
+                            t["last_committed"], t["conf"], out, st, run_off=t["run_off"],
+                            run_start=t["run_start"], run_conf=t["run_conf"])
+    engine.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), ce)
+    np.testing.assert_array_equal(st.cpu().numpy(), se)
+
+
+@pytest.mark.parametrize("P,G,K", [(3, 1000, 9), (5, 777, 40), (2, 64, 1), (3, 130, 200)])
+def test_gpu_quorum_epochs_with_runs(engine, oracle, P, G, K):
+    """K epochs in one launch with conf runs and flagged groups == K sequential replays."""
+    import torch
+    from quorum_cases import flag_runs, random_series, series_replay
+    s = random_series(900 + K, G, P, K)
+    s["conf"] = flag_runs(s)
+    ce, se = series_replay(oracle, s)
+    t = _to_dev(s, list(s.keys()))
+    c = torch.empty((K, G), dtype=torch.int64, device="cuda:0")
+    st = torch.empty((K, G), dtype=torch.uint8, device="cuda:0")
+    engine.quorum_epochs_dev(t["match"], t["pending_index"], t["last_appended"],
+                             t["last_committed"], t["conf"], c, st, run_off=t["run_off"],
+                             run_start=t["run_start"], run_conf=t["run_conf"])
+    engine.synchronize()
+    np.testing.assert_array_equal(c.cpu().numpy(), ce)
+    np.testing.assert_array_equal(st.cpu().numpy(), se)

@@ -92,3 +92,61 @@ def test_ack_chunking_and_order_do_not_matter(oracle):
     base = replay(oracle, b, chunk=1)
     for ch in (2, 3, 64, 1024):
         np.testing.assert_array_equal(replay(oracle, b, chunk=ch)[0], base[0])
+
+
+def scan_model(s):
+    """The K-epoch kernel's formulation (quorum.hip quorum_epochs_kernel): per epoch an
+    independent candidate v_k thresholded at pi_0, committed_k = max(lc_0, prefix max of v),
+    pendingIndex before epoch k = committed_{k-1} + 1 once a commit happened."""
+    K, P, G = s["match"].shape
+    out = np.zeros((K, G), np.int64)
+    st = np.zeros((K, G), np.uint8)
+    for g in range(G):
+        pi0, lc0 = int(s["pending_index"][g]), int(s["last_committed"][g])
+        r0, r1 = int(s["run_off"][g]), int(s["run_off"][g + 1])
+        runs = [(int(s["run_start"][r]), int(s["run_conf"][r])) for r in range(r0, r1)]
+        M = I64MIN
+        for k in range(K):
+            la = int(s["last_appended"][k, g])
+            if pi0 == 0:
+                out[k, g], st[k, g] = lc0, 1
+                continue
+            pik = M + 1 if M > lc0 else pi0
+            flags = 0
+            m = []
+            for p in range(P):
+                v = int(s["match"][k, p, g])
+                if v > la:
+                    flags |= 2
+                    v = I64MIN
+                m.append(v)
+            v = I64MIN
+            for i, (start, cw) in enumerate(runs):
+                thr = pi0 if i == 0 else max(start, pi0)
+                end = runs[i + 1][0] - 1 if i + 1 < len(runs) else la
+                ee = min(end, la)
+                nm, om, nq, oq = cw & 0xFFFF, (cw >> 16) & 0xFFFF, (cw >> 32) & 0xFF, (cw >> 40) & 0xFF
+                kn = I64MAX if nq == 0 else kth(m, nm, nq)
+                ko = I64MAX if oq == 0 else kth(m, om, oq)
+                cand = min(ee, kn, ko)
+                if cand >= thr:
+                    v = max(v, cand)
+                sk = pik if i == 0 else max(start, pik)
+                if ee >= sk and nm == 0:
+                    flags |= 4
+            M = max(M, v)
+            out[k, g], st[k, g] = max(lc0, M), flags
+    return out, st
+
+
+@pytest.mark.parametrize("P,seed", [(3, 11), (5, 12), (2, 13)])
+def test_epoch_scan_model_matches_sequential_replays(oracle, P, seed):
+    """The thresholded prefix max over epochs equals K sequential BallotBox replays with the
+    state carried between them (BallotBox.java:131-134), conf runs included."""
+    from quorum_cases import random_series, series_replay
+    s = random_series(seed, 300, P, 9)
+    ce, se = series_replay(oracle, s)
+    mc, ms = scan_model(s)
+    np.testing.assert_array_equal(mc, ce)
+    np.testing.assert_array_equal(ms, se)
+    assert (ce[-1] > ce[0]).any()

@@ -16,15 +16,20 @@ run() {  # run <name> <seconds> <cmd...>
 STEPS=${STEPS:-"tests smoke bench"}
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     crc)   run crc_tests 600 python -m pytest tests/test_gpu_crc.py -q -x -p no:cacheprovider --timeout 300 ;;
     quorum) run quorum_tests 600 python -m pytest tests/test_gpu_quorum.py -q -x -p no:cacheprovider --timeout 300 ;;
     quick) run bench_quick 600 python bench.py --steps 20 --warmup 3 --no-cpu ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu ;;
-    pmcf)  run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --headline-only ;;
-    pmcw)  run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --headline-only ;;
+    tbl)   run table_tests 600 python -m pytest tests/test_gpu_table.py -q -x -p no:cacheprovider --timeout 300 ;;
+    pmc)   # one rocprofv3 --pmc pass per (leg, counter): every kernel name then carries one workload
+           for leg in ${PMC_LEGS:-quorum C2 C5 C1 v2 snapshot lease fanout}; do
+             for c in FETCH_SIZE WRITE_SIZE; do
+               run pmc_${leg}_$c 180 rocprofv3 --kernel-trace --pmc $c -d gpurun_out/pmc_${leg}_$c -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs $leg
+             done
+           done ;;
     host)  run host_test 300 ./sofa-jraft_amd/lib/host_test gpu ;;
     probe) run mem_probe 300 ./tools/mem_probe ;;
     sweep) run crc_sweep 600 python tools/crc_sweep.py ${SWEEP_VARIANTS:-} ;;

@@ -1,18 +1,19 @@
 #!/usr/bin/env python3
 """Condense rocprofv3 outputs under gpurun_out/ into committed summaries under profiles/.
 
-  python tools/summarize_profiles.py <tag>        (e.g. r01)
+  python tools/summarize_profiles.py <tag>        (e.g. r02a)
 
 Reads (when present):
-  gpurun_out/prof/run_kernel_stats.csv            rocprofv3 --kernel-trace --stats
-  gpurun_out/pmc_fetch/run_counter_collection.csv rocprofv3 --kernel-trace --pmc FETCH_SIZE
-  gpurun_out/pmc_write/run_counter_collection.csv rocprofv3 --kernel-trace --pmc WRITE_SIZE
-  gpurun_out/pmc*_C*/run_counter_collection.csv   tools/pmc_crc.sh SQ / TCC groups
-Writes profiles/<tag>_kernel_stats.csv (verbatim copy) and profiles/<tag>_pmc.json:
-per kernel, the mean of each counter over its dispatches.  HBM traffic per launch is
-(2 * FETCH_SIZE + WRITE_SIZE) KiB: on gfx950 FETCH_SIZE counts 128-B read requests as
-64 B, i.e. half the bytes of a wide streaming read (MI355X_MICROARCH.md, HBM section);
-the raw values are kept next to the corrected ones.
+  gpurun_out/prof/run_kernel_stats.csv                  rocprofv3 --kernel-trace --stats
+  gpurun_out/pmc_<leg>_<COUNTER>/*counter_collection.csv  tools/gpu_check.sh `pmc`: one
+      rocprofv3 --pmc pass per bench leg (`bench.py --legs <leg>`) and counter
+Writes profiles/<tag>_kernel_stats.csv (verbatim copy) and profiles/<tag>_pmc.json: per leg
+and kernel, the mean of each counter over its dispatches, and the HBM bytes per launch
+(2 * FETCH_SIZE + WRITE_SIZE) KiB -- on gfx950 FETCH_SIZE counts a wide streaming read at
+half its bytes (MI355X_MICROARCH.md, HBM section).  The snapshot leg (one 1 GiB stream
+through the CRC kernel, ~1 GiB of reads) checks that factor on the CRC kernel's own access
+pattern: `calibration`.  `csrc_sha` = bench.csrc_sha() of the tree the passes ran on; bench.py
+cites a summary only when it matches its own sources.
 """
 import collections
 import csv
@@ -25,6 +26,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
+sys.path.insert(0, ROOT)
 
 
 def kernel_key(name):
@@ -39,31 +41,44 @@ def counters(path):
 
 
 def main():
-    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    import bench
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
     os.makedirs(PROF, exist_ok=True)
-    res = {"tag": tag, "kernels": collections.defaultdict(dict)}
+    res = {"tag": tag, "csrc_sha": bench.csrc_sha(), "correction": "2*FETCH_SIZE+WRITE_SIZE, KiB->B",
+           "kernel_stats": {}, "legs": collections.defaultdict(lambda: collections.defaultdict(dict))}
     st = os.path.join(OUT, "prof", "run_kernel_stats.csv")
     if os.path.exists(st):
         shutil.copy(st, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
         for r in csv.DictReader(open(st)):
-            res["kernels"][kernel_key(r["Name"])]["avg_duration_ns"] = float(r["AverageNs"])
-            res["kernels"][kernel_key(r["Name"])]["calls"] = int(r["Calls"])
-    files = glob.glob(os.path.join(OUT, "pmc_*", "*counter_collection.csv")) + \
-        glob.glob(os.path.join(OUT, "pmc*_C*", "*counter_collection.csv"))
-    for f in sorted(files):
-        src = os.path.basename(os.path.dirname(f))
-        for k, d in counters(f).items():
-            for c, v in d.items():
-                res["kernels"][k][c] = v
-                res["kernels"][k].setdefault("sources", []).append(f"{src}:{c}")
-    for k, d in res["kernels"].items():
-        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
-            d["hbm_bytes_per_launch_corrected"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
-            d["hbm_bytes_per_launch_raw"] = (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
-    res["kernels"] = {k: v for k, v in res["kernels"].items() if "jrq" in k}
+            res["kernel_stats"][kernel_key(r["Name"])] = {"avg_duration_ns": float(r["AverageNs"]),
+                                                          "calls": int(r["Calls"])}
+    for f in sorted(glob.glob(os.path.join(OUT, "pmc_*_*", "*counter_collection.csv"))):
+        d = os.path.basename(os.path.dirname(f))[4:]   # <leg>_<COUNTER>
+        leg, counter = d.split("_", 1)
+        for k, vals in counters(f).items():
+            if "jrq" not in k:
+                continue
+            for c, v in vals.items():
+                res["legs"][leg][k][c] = v
+    for leg, ks in res["legs"].items():
+        for k, v in ks.items():
+            if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+                v["hbm_bytes_per_launch"] = (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
+                v["hbm_bytes_per_launch_raw"] = (v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
+    snap = res["legs"].get("snapshot", {})
+    rk = [v for k, v in snap.items() if "crc64_rounds_kernel" in k and "FETCH_SIZE" in v]
+    if rk:
+        # the archive launch reads the 1 GiB payload once (+ 128 KiB LDS tables per workgroup
+        # from L2 and a few KiB of offsets/scratch); the same kernel name also ran the 64k
+        # region streams (same bytes) in that pass
+        fetched = rk[0]["FETCH_SIZE"] * 1024
+        res["calibration"] = {"kernel": "crc64_rounds_kernel (snapshot leg)",
+                              "known_read_bytes": 1 << 30, "FETCH_SIZE_bytes": fetched,
+                              "bytes_per_FETCH_byte": (1 << 30) / fetched}
+    res["legs"] = {k: dict(v) for k, v in res["legs"].items()}
     with open(os.path.join(PROF, f"{tag}_pmc.json"), "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
-    print(json.dumps(res, indent=1, sort_keys=True)[:4000])
+    print(json.dumps(res, indent=1, sort_keys=True)[:3000])
 
 
 if __name__ == "__main__":
