@@ -38,7 +38,8 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 QUORUM_EPOCH_BUFFERS = 6
-LEGS = ("quorum", "C2", "C5", "C1", "ae", "v2", "snapshot", "lease", "fanout", "peak", "cpu")
+LEGS = ("quorum", "table", "drive", "C2", "C5", "C1", "ae", "v2", "snapshot", "lease", "fanout",
+        "peak", "cpu")
 
 
 def quorum_bytes_per_group(P: int) -> int:
@@ -353,7 +354,8 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
     k = D.per_rank(Gtot, world)
     local = torch.empty(k, dtype=torch.int64, device=dev)
     status = torch.empty(G, dtype=torch.uint8, device=dev)
-    snapshot = torch.empty(k * world, dtype=torch.int64, device=dev)
+    # one GPU: the local committed[] already is the node-wide snapshot (nothing to gather)
+    snapshot = torch.empty(k * world, dtype=torch.int64, device=dev) if world > 1 else local
     nranks = 1
     if world > 1:
         uid = [Engine.rccl_unique_id() if rank == 0 else None]
@@ -370,8 +372,6 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
     def allgather(send, recv):
         if world > 1:
             eng.publish_committed_dev(send, recv)
-        else:
-            recv.copy_(send)
     se = D.ShardedEpochs(Gtot, world, rank, epoch_fn, allgather, local, snapshot,
                          publish_every=args.publish_every)
     # kernel only (HIP events on the engine's stream)
@@ -420,6 +420,180 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
                       "snapshot_bytes": 8 * k * world},
         "bit_exact_vs_oracle_4096_groups": ok,
     }
+
+
+def table_load(table, s):
+    """Load epoch 0 of a host_series batch into a Table the way a host does: one header per
+    group (resetPendingIndex + its conf runs), then one 8-B record per peer slot (its acks)."""
+    from jraft_amd import Table, _lib
+    G = len(s["pending_index"])
+    pi = s["pending_index"]
+    st = Table.states(G)
+    joint = s["switch_at"] != 0
+    st["group"] = np.arange(G)
+    st["num_runs"] = np.where(joint, 2, 1)
+    st["flags"] = _lib.STATE_RESET_MATCH
+    st["pending_index"] = pi
+    st["last_appended"] = s["last_appended"][0]
+    st["last_committed"] = s["last_committed"]
+    st["run_conf"][:, 0] = s["conf_a"]
+    st["run_conf"][:, 1] = np.where(joint, s["conf_b"], 0)
+    st["run_start"][:, 1] = s["switch_at"]
+    m = s["match"][0]
+    gs = np.arange(G)
+    recs = np.concatenate([_lib.rec(gs, p, np.maximum(m[p] - (pi - 1), 0)) for p in range(m.shape[0])])
+    table.update(st, recs)  # on the engine stream, before any later epoch
+    return st, recs
+
+
+def leg_table(ctx, args, G, pair_ms):
+    """The drop-in path's device cost: one epoch of the resident group table (csrc/table.hip)
+    over C3 (1M groups x 5 peers, joint) with 1% of the groups holding a conf change inside
+    their pending window, against the stateless pair kernel on the same inputs.  Each timed
+    epoch starts from a pristine copy of its table (jrq_table_copy, outside the event pair), so
+    every launch commits as many groups as the first one would."""
+    import torch
+
+    from jraft_amd import Table, decode_changed
+    from jraft_amd import workloads as W
+    eng, dev = ctx.eng, ctx.dev
+    P = 5
+    nb = 3
+    pristine, series = [], []
+    for e in range(nb):
+        s = W.host_series("C3", 1, groups=G, joint_frac=0.01, seed=(W.SEED_BASE ^ 3) + 7919 * e)
+        t = Table(eng, G, P)
+        table_load(t, s)
+        pristine.append(t)
+        series.append(s)
+    ctx.sync()
+    work = Table(eng, G, P)
+    changed = torch.empty(G, dtype=torch.int64, device=dev)
+    n = torch.zeros(1, dtype=torch.int32, device=dev)
+    steps = max(10, args.steps)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    for i in range(args.warmup):
+        work.copy_from(pristine[i % nb])
+        work.epoch_dev(changed, n)
+    for i in range(steps):
+        work.copy_from(pristine[i % nb])
+        ev[i][0].record(ctx.stream)
+        work.epoch_dev(changed, n)
+        ev[i][1].record(ctx.stream)
+    ctx.sync()
+    t_ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+    last = (steps - 1) % nb
+    n_changed = int(n.item())
+    words = changed[:n_changed].cpu().numpy().view(np.uint64)
+    # the stateless pair kernel on the same inputs (CSR run table, flagged groups), same timing
+    s = series[last]
+    d = {k: to_dev(s[k] if k != "match" else s["match"][0], dev)
+         for k in ("match", "pending_index", "last_committed", "conf", "run_off", "run_start",
+                   "run_conf")}
+    d["last_appended"] = to_dev(s["last_appended"][0], dev)
+    pc = torch.empty(G, dtype=torch.int64, device=dev)
+    pst = torch.empty(G, dtype=torch.uint8, device=dev)
+
+    def pair(i):
+        eng.quorum_epoch_dev(d["match"], d["pending_index"], d["last_appended"],
+                             d["last_committed"], d["conf"], pc, pst, run_off=d["run_off"],
+                             run_start=d["run_start"], run_conf=d["run_conf"])
+    for i in range(args.warmup):
+        pair(i)
+    ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    for i in range(steps):
+        work.copy_from(pristine[i % nb])  # same cache state as the table launches
+        ev2[i][0].record(ctx.stream)
+        pair(i)
+        ev2[i][1].record(ctx.stream)
+    ctx.sync()
+    p_ms = float(np.median([a.elapsed_time(b) for a, b in ev2]))
+    g, delta = decode_changed(words)
+    got = s["last_committed"].copy()
+    got[g] = s["pending_index"][g] - 1 + delta
+    ok = bool(np.array_equal(got, pc.cpu().numpy()))  # table == stateless kernel, every group
+    if ctx.oracle_checks:  # and 512 groups (the joint ones first) against the oracle
+        import jraft_oracle as O
+        jg = np.nonzero(s["switch_at"])[0][:256]
+        sub = np.unique(np.concatenate([jg, np.random.default_rng(5).choice(G, 256, replace=False)]))
+        ro = s["run_off"]
+        cnt = (ro[sub + 1] - ro[sub]).astype(np.uint32)
+        idx = np.concatenate([np.arange(ro[x], ro[x + 1]) for x in sub])
+        ce, _, _ = O.quorum_epoch_replay(s["match"][0][:, sub], s["pending_index"][sub],
+                                         s["last_appended"][0][sub], s["last_committed"][sub],
+                                         s["conf"][sub], np.concatenate([[0], np.cumsum(cnt)]),
+                                         s["run_start"][idx], s["run_conf"][idx], chunk=1024)
+        ok = ok and bool(np.array_equal(got[sub], ce))
+    alg = G * (8 * P + 32) + n_changed * 16
+    for t in pristine:
+        t.close()
+    work.close()
+    return {"workload": f"C3 resident table: {G} groups x {P} peers, joint, 1% with a conf "
+                        f"change in the pending window; one epoch, in place",
+            "kernel_ms": t_ms, "changed_groups": n_changed,
+            "stateless_pair_kernel_ms_same_inputs": p_ms,
+            "table_over_pair": t_ms / p_ms,
+            "headline_pair_kernel_ms": pair_ms,
+            "timing": "median of per-launch HIP event pairs (the pristine-table copy before each "
+                      "launch is outside the pair); both kernels timed the same way",
+            "bit_exact_vs_stateless_kernel_and_oracle": ok,
+            "roofline": roofline(alg, t_ms, kernel="table_epoch_kernel<5>",
+                                 bytes_note="reads 8P+32 B per group, writes lastCommitted + list "
+                                            "entry 16 B per committing group",
+                                 **pmc_traffic("table", "table_epoch_kernel<5>"))}
+
+
+def leg_drive(ctx, args, G):
+    """The drop-in path end to end from the host: C3 epochs replayed through the C++ host
+    mirror's BallotBox API (appendPendingTask / commitAt) over the resident table, one
+    GroupBatch::flush() per epoch (libjraft_drive.so): changed records from page-locked
+    buffers -> H2D -> apply + epoch kernels -> D2H of the changed commits -> closures /
+    onCommitted.  Reported per steady epoch (epochs 1..K-1; epoch 0 loads every group)."""
+    import torch
+
+    from jraft_amd import drive
+    from jraft_amd import workloads as W
+    K = 6
+    out = {}
+    for active in (1.0, 0.1):
+        s = W.host_series("C3", K, groups=G, joint_frac=0.01, active=active)
+        committed, st = drive.drive_epochs(ctx.dev.index, s)
+        ok = None
+        if active == 1.0:  # every group against the stateless K-epoch kernel
+            d = {k: to_dev(s[k], ctx.dev) for k in ("match", "last_appended", "pending_index",
+                                                    "last_committed", "conf", "run_off",
+                                                    "run_start", "run_conf")}
+            c = torch.empty((K, G), dtype=torch.int64, device=ctx.dev)
+            cs = torch.empty((K, G), dtype=torch.uint8, device=ctx.dev)
+            ctx.eng.quorum_epochs_dev(d["match"], d["pending_index"], d["last_appended"],
+                                      d["last_committed"], d["conf"], c, cs, run_off=d["run_off"],
+                                      run_start=d["run_start"], run_conf=d["run_conf"])
+            ctx.sync()
+            ok = bool(np.array_equal(committed, c.cpu().numpy()))
+            del d, c, cs
+        sl = slice(1, K)
+        f = float(np.mean(st["flush_ms"][sl]))
+        pcie = float(np.mean(st["h2d_bytes"][sl] + st["d2h_bytes"][sl]))
+        out[f"active_{int(active * 100)}pct"] = {
+            "flush_ms": f, "pack_ms": float(np.mean(st["pack_ms"][sl])),
+            "device_ms": float(np.mean(st["device_ms"][sl])),
+            "deliver_ms": float(np.mean(st["deliver_ms"][sl])),
+            "decisions_per_s": G / (f * 1e-3),
+            "records_per_epoch": float(np.mean(st["records"][sl])),
+            "changed_per_epoch": float(np.mean(st["changed"][sl])),
+            "pcie_bytes_per_epoch": pcie, "pcie_GBps": pcie / (f * 1e-3) / 1e9,
+            "api_calls_per_epoch": float(np.mean(st["api_calls"][sl])),
+            "api_ms_per_epoch": float(np.mean(st["api_ms"][sl])),
+            "first_epoch_flush_ms": float(st["flush_ms"][0]),
+            "bit_exact_vs_stateless_kernel": ok}
+    return {"workload": f"C3 through the C++ BallotBox host mirror: {G} groups x 5 peers, joint, "
+                        f"1% with a conf change in the pending window, {K} epochs",
+            "how": "flush = pack changed records + H2D (pinned) + apply + epoch kernels + D2H of "
+                   "the changed commits + closures / onCommitted; api = the appendPendingTask / "
+                   "commitAt calls before it (host-side, not part of flush)",
+            **out}
 
 
 def leg_c2(ctx, args):
@@ -898,6 +1072,11 @@ def main():
                 "parallelism": f"groupId shards x{world}"},
             "roofline": q["roofline"], "multi_gpu": q["multi_gpu"],
             "bit_exact_vs_oracle_4096_groups": q["bit_exact_vs_oracle_4096_groups"]})
+    if "table" in legs:
+        pair_ms = line.get("roofline", {}).get("kernel_ms")
+        line["resident_table"] = leg_table(ctx, args, G, pair_ms)
+    if "drive" in legs:
+        line["end_to_end_host_mirror"] = leg_drive(ctx, args, G)
     if "C2" in legs:
         line["C2"] = leg_c2(ctx, args)
     extras = {}

@@ -162,6 +162,102 @@ int jrq_quorum_epochs_dev(jrq_engine *e, const jrq_group_batch *in_dev, uint32_t
                           uint64_t match_epoch_ld, uint64_t la_epoch_ld,
                           int64_t *committed_out_dev, uint8_t *status_out_dev, uint32_t G);
 
+/* -------------------------------------------------- resident group table -- */
+
+/* The drop-in path for a long-running multi-Raft host: the BallotBox state of G groups lives
+ * on the device (HBM), the host ships only what changed since the previous epoch, and an epoch
+ * returns only the groups whose lastCommittedIndex advanced.  Per group it holds exactly what
+ * BallotBox holds (JC/core/BallotBox.java:50-55): pendingIndex, lastCommittedIndex, the
+ * pending queue as lastAppended plus its conf runs (one Ballot.init(conf, oldConf) per run
+ * instead of per entry, :197-215), and, per peer slot, the highest index the peer has
+ * acknowledged through commitAt (Replicator acks are contiguous, Replicator.java:1387-1401).
+ *
+ * Device layout (SoA, 8-byte words, rows of ld >= G): match[P][ld], pending_index, last_appended,
+ * last_committed, conf (run 0 + JRQ_CONF_RUNS), and JRQ_TABLE_MAX_RUNS - 1 inline extra runs
+ * (run_start, run_conf) read only by flagged groups.  After its first commit a group's
+ * pending_index word holds JRQ_PI_FOLLOWS_LC (pendingIndex = lastCommittedIndex + 1,
+ * BallotBox.java:131-132), so a commit writes one word of state. */
+#define JRQ_TABLE_MAX_RUNS 4            /* conf runs per pending window (NodeImpl has <= 2) */
+#define JRQ_TABLE_MAX_GROUPS (1u << 27) /* groups per table (27-bit group ids in records) */
+#define JRQ_PI_FOLLOWS_LC INT64_MIN
+
+typedef struct jrq_table jrq_table;
+
+/* Full header of one group: what resetPendingIndex (:167-186), clearPendingTasks (:147-156),
+ * setLastCommittedIndex (:223-248) and a conf-changing appendPendingTask (:197-215) leave
+ * behind.  Runs: run 0 covers [pendingIndex, run_start[1]), run r covers [run_start[r],
+ * run_start[r+1]) and the last run ends at last_appended; num_runs 0 = nothing pending. */
+typedef struct {
+    uint32_t group;
+    uint16_t num_runs;       /* 0..JRQ_TABLE_MAX_RUNS */
+    uint16_t flags;          /* JRQ_STATE_RESET_MATCH: every slot's match = pendingIndex - 1 */
+    int64_t pending_index;   /* 0 = not the leader */
+    int64_t last_appended;   /* pendingIndex + pendingMetaQueue.size() - 1 */
+    int64_t last_committed;
+    uint64_t run_conf[JRQ_TABLE_MAX_RUNS];  /* JRQ_CONF words */
+    int64_t run_start[JRQ_TABLE_MAX_RUNS];  /* run_start[0] is ignored (<= pendingIndex) */
+} jrq_group_state;           /* 96 bytes */
+#define JRQ_STATE_RESET_MATCH 1u
+
+/* 8-byte update record: bits 0-4 field, bits 5-31 group, bits 32-63 v, a value relative to
+ * the group's pendingIndex pi (after this call's group states are applied):
+ *   field 0..15  match of peer slot `field` = pi - 1 + v: the `last` of the peer's latest
+ *                BallotBox.commitAt(first, last, peer) (v = 0: no pending entry acked)
+ *   field 16     last_appended = pi - 1 + v: v = pendingMetaQueue.size() after
+ *                appendPendingTask calls that kept the conf (BallotBox.java:197-215)
+ * v fits 32 bits because the pending queue is a Java ArrayList (int size).  At most one
+ * record per (group, field) per call. */
+#define JRQ_REC_LAST_APPENDED 16u
+#define JRQ_REC(group, field, v)                                                               \
+    (((uint64_t)(uint32_t)(v) << 32) | ((uint64_t)(uint32_t)(group) << 5) | (uint64_t)(field))
+
+/* A table of G groups x num_peers slots on the engine's device, every group initially not
+ * the leader (pendingIndex 0, nothing pending).  Destroy before the engine. */
+jrq_table *jrq_table_create(jrq_engine *e, uint32_t G, uint32_t num_peers, int *err);
+void jrq_table_destroy(jrq_table *t);
+
+/* Apply n_states group headers, then n_recs update records, on the engine's stream.  Host
+ * variant: states / recs are host memory (ideally jrq_host_register'ed, e.g. DirectByteBuffers)
+ * copied with one H2D transfer each; they must stay unchanged until the next jrq_table_epoch
+ * or jrq_synchronize returns.  Records are checked on the host (group < G, field valid). */
+int jrq_table_update(jrq_table *t, const jrq_group_state *states, uint32_t n_states,
+                     const uint64_t *recs, uint32_t n_recs);
+int jrq_table_update_dev(jrq_table *t, const jrq_group_state *states_dev, uint32_t n_states,
+                         const uint64_t *recs_dev, uint32_t n_recs);
+
+/* One quorum epoch over every group of the table, state updated in place as BallotBox.commitAt
+ * leaves it (BallotBox.java:96-139; commit -> lastCommittedIndex, pendingIndex = commit + 1).
+ * changed_out[k] = (uint64)(commit - pi + 1) << 32 | group for each group whose
+ * lastCommittedIndex advanced (pi = its pendingIndex before the epoch; any order), *n_changed
+ * = their number; status_out[g] (nullable) = jrq_group_status.  _dev: device pointers,
+ * capacity G.  Host variant: synchronises and copies back n_changed entries only. */
+int jrq_table_epoch_dev(jrq_table *t, uint64_t *changed_out_dev, uint32_t *n_changed_dev,
+                        uint8_t *status_out_dev);
+int jrq_table_epoch(jrq_table *t, uint64_t *changed_out, uint32_t *n_changed,
+                    uint8_t *status_out);
+
+/* Copy the table's state to host arrays (each nullable): pendingIndex resolved (never
+ * JRQ_PI_FOLLOWS_LC), last_appended, last_committed [G], match [num_peers][G]. */
+int jrq_table_read(jrq_table *t, int64_t *pending_index, int64_t *last_appended,
+                   int64_t *last_committed, int64_t *match);
+
+/* Copy the whole state of src into dst (same G and num_peers), on dst's engine stream: a
+ * device-side snapshot / restore of the group table. */
+int jrq_table_copy(jrq_table *dst, const jrq_table *src);
+
+/* Device views of the table (e.g. last_committed as the rank's jrq_publish_committed_dev
+ * send buffer, the node-wide getLastCommittedIndex snapshot). */
+typedef struct {
+    int64_t *match;          /* [num_peers][ld] */
+    int64_t *pending_index;  /* JRQ_PI_FOLLOWS_LC after a commit */
+    int64_t *last_appended;
+    int64_t *last_committed;
+    uint64_t *conf;
+    uint64_t ld;
+    uint32_t G, num_peers;
+} jrq_table_view;
+int jrq_table_view_get(jrq_table *t, jrq_table_view *view_out);
+
 /* --------------------------------------------------------------- checksum -- */
 
 /* crc_out[i] = CrcUtil.crc64(payload[offsets[i] .. offsets[i+1]))

@@ -30,6 +30,13 @@ extern "C" hipError_t jrq_launch_fanout(const JrqFanoutArgs* a, hipStream_t stre
 extern "C" hipError_t jrq_launch_v2_parse(const JrqV2Args* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_v2_finish(const JrqV2Args* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_first_corrupt(const JrqAeArgs* a, hipStream_t stream);
+extern "C" hipError_t jrq_launch_table_update(const JrqTableArgs* a, const JrqGroupState* states,
+                                              uint32_t n_states, const uint64_t* recs,
+                                              uint32_t n_recs, hipStream_t stream);
+extern "C" hipError_t jrq_launch_table_epoch(const JrqTableArgs* a, hipStream_t stream);
+
+static_assert(sizeof(jrq_group_state) == sizeof(JrqGroupState), "jrq_group_state layout");
+static_assert(JRQ_TABLE_MAX_RUNS == jrq::kTableMaxRuns, "table runs");
 
 namespace {
 
@@ -955,6 +962,222 @@ int jrq_v2_decode_verify(jrq_engine* e, const uint8_t* rec, const uint64_t* off,
   JRQ_HIP(e, hipMemcpyAsync(corrupt, dcor, N, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   for (uint32_t i = 0; i < N; ++i) data_off[i] += lo;  // back to the caller's base
+  return JRQ_OK;
+}
+
+// -------------------------------------------------- resident group table -----
+
+struct jrq_table {
+  jrq_engine* e = nullptr;
+  void* mem = nullptr;        // every device array of the table, one allocation
+  JrqTableArgs a{};           // device pointers (changed / n_changed / status set per epoch)
+  DevBuf st_stage, rec_stage, changed_stage;  // staging of the host variants
+  uint32_t* n_dev = nullptr;  // device count word of the host-variant epoch
+  uint32_t* n_host = nullptr; // pinned
+};
+
+namespace {
+
+static int table_check(jrq_table* t) {
+  if (!t || !t->e) return JRQ_E_INVALID;
+  return JRQ_OK;
+}
+
+static int stage_buf(jrq_engine* e, DevBuf& b, size_t bytes, void** out) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap < bytes) {
+    if (b.p) {
+      JRQ_HIP(e, hipStreamSynchronize(e->stream));
+      JRQ_HIP(e, hipFree(b.p));
+      b.p = nullptr;
+      b.cap = 0;
+    }
+    const size_t cap = bytes + bytes / 4;
+    JRQ_HIP(e, hipMalloc(&b.p, cap));
+    b.cap = cap;
+  }
+  *out = b.p;
+  return JRQ_OK;
+}
+
+}  // namespace
+
+jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
+  auto set = [&](int c) {
+    if (err) *err = c;
+  };
+  if (!e || G == 0 || G > JRQ_TABLE_MAX_GROUPS || P == 0 || P > JRQ_MAX_PEERS) {
+    if (e) fail(e, JRQ_E_INVALID, "table: bad G %u or num_peers %u", G, P);
+    set(JRQ_E_INVALID);
+    return nullptr;
+  }
+  DeviceGuard guard(e->device);
+  auto* t = new jrq_table();
+  t->e = e;
+  const uint64_t ld = (static_cast<uint64_t>(G) + 63) & ~63ull;  // pairs + 512-B rows
+  const uint64_t words = ld * (P + 4 + 2 * (jrq::kTableMaxRuns - 1));
+  const size_t bytes = words * 8 + 64;
+  if (hipMalloc(&t->mem, bytes) != hipSuccess || hipMemset(t->mem, 0, bytes) != hipSuccess ||
+      hipMalloc(&t->n_dev, 16) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&t->n_host), 16, hipHostMallocDefault) != hipSuccess) {
+    fail(e, JRQ_E_NOMEM, "table: allocation of %zu bytes failed", bytes);
+    jrq_table_destroy(t);
+    set(JRQ_E_NOMEM);
+    return nullptr;
+  }
+  int64_t* w = static_cast<int64_t*>(t->mem);
+  JrqTableArgs& a = t->a;
+  a.match = w;
+  a.pi = w + ld * P;
+  a.la = a.pi + ld;
+  a.lc = a.la + ld;
+  a.conf = reinterpret_cast<uint64_t*>(a.lc + ld);
+  a.xstart = reinterpret_cast<int64_t*>(a.conf + ld);
+  a.xconf = reinterpret_cast<uint64_t*>(a.xstart + ld * (jrq::kTableMaxRuns - 1));
+  a.ctr = reinterpret_cast<unsigned long long*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
+  a.ld = ld;
+  a.G = G;
+  a.P = P;
+  set(JRQ_OK);
+  return t;
+}
+
+void jrq_table_destroy(jrq_table* t) {
+  if (!t) return;
+  if (t->e) {
+    DeviceGuard guard(t->e->device);
+    (void)hipStreamSynchronize(t->e->stream);
+    for (DevBuf* b : {&t->st_stage, &t->rec_stage, &t->changed_stage})
+      if (b->p) (void)hipFree(b->p);
+    if (t->mem) (void)hipFree(t->mem);
+    if (t->n_dev) (void)hipFree(t->n_dev);
+    if (t->n_host) (void)hipHostFree(t->n_host);
+  }
+  delete t;
+}
+
+int jrq_table_update_dev(jrq_table* t, const jrq_group_state* states, uint32_t n_states,
+                         const uint64_t* recs, uint32_t n_recs) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if ((n_states && !states) || (n_recs && !recs)) return fail(e, JRQ_E_INVALID, "null update array");
+  DeviceGuard guard(e->device);
+  JRQ_HIP(e, jrq_launch_table_update(&t->a, reinterpret_cast<const JrqGroupState*>(states),
+                                     n_states, recs, n_recs, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_table_update(jrq_table* t, const jrq_group_state* states, uint32_t n_states,
+                     const uint64_t* recs, uint32_t n_recs) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if ((n_states && !states) || (n_recs && !recs)) return fail(e, JRQ_E_INVALID, "null update array");
+  const uint32_t G = t->a.G, P = t->a.P;
+  for (uint32_t i = 0; i < n_states; ++i)
+    if (states[i].group >= G || states[i].num_runs > JRQ_TABLE_MAX_RUNS)
+      return fail(e, JRQ_E_INVALID, "group state %u: group %u / num_runs %u out of range", i,
+                  states[i].group, states[i].num_runs);
+  for (uint32_t i = 0; i < n_recs; ++i) {
+    const uint32_t f = static_cast<uint32_t>(recs[i] & 31u);
+    const uint32_t g = static_cast<uint32_t>(recs[i] >> 5) & ((1u << 27) - 1u);
+    if (g >= G || f > JRQ_REC_LAST_APPENDED || (f < JRQ_REC_LAST_APPENDED && f >= P))
+      return fail(e, JRQ_E_INVALID, "record %u: group %u / field %u out of range", i, g, f);
+  }
+  DeviceGuard guard(e->device);
+  int rc;
+  void *ds = nullptr, *dr = nullptr;
+  if (n_states) {
+    if ((rc = stage_buf(e, t->st_stage, static_cast<size_t>(n_states) * sizeof(jrq_group_state), &ds))) return rc;
+    JRQ_HIP(e, hipMemcpyAsync(ds, states, static_cast<size_t>(n_states) * sizeof(jrq_group_state),
+                              hipMemcpyHostToDevice, e->stream));
+  }
+  if (n_recs) {
+    if ((rc = stage_buf(e, t->rec_stage, static_cast<size_t>(n_recs) * 8, &dr))) return rc;
+    JRQ_HIP(e, hipMemcpyAsync(dr, recs, static_cast<size_t>(n_recs) * 8, hipMemcpyHostToDevice, e->stream));
+  }
+  return jrq_table_update_dev(t, static_cast<const jrq_group_state*>(ds), n_states,
+                              static_cast<const uint64_t*>(dr), n_recs);
+}
+
+int jrq_table_epoch_dev(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, uint8_t* status_out) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if (!changed_out || !n_changed) return fail(e, JRQ_E_INVALID, "null changed output");
+  DeviceGuard guard(e->device);
+  JrqTableArgs a = t->a;
+  a.changed = changed_out;
+  a.n_changed = n_changed;
+  a.status = status_out;
+  JRQ_HIP(e, jrq_launch_table_epoch(&a, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_table_epoch(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, uint8_t* status_out) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if (!changed_out || !n_changed) return fail(e, JRQ_E_INVALID, "null changed output");
+  DeviceGuard guard(e->device);
+  const uint32_t G = t->a.G;
+  int rc;
+  void *dch = nullptr, *dst = nullptr;
+  if ((rc = stage_buf(e, t->changed_stage, static_cast<size_t>(G) * 9, &dch))) return rc;
+  if (status_out) dst = static_cast<uint8_t*>(dch) + static_cast<size_t>(G) * 8;
+  if ((rc = jrq_table_epoch_dev(t, static_cast<uint64_t*>(dch), t->n_dev, static_cast<uint8_t*>(dst))))
+    return rc;
+  JRQ_HIP(e, hipMemcpyAsync(t->n_host, t->n_dev, 4, hipMemcpyDeviceToHost, e->stream));
+  if (status_out) JRQ_HIP(e, hipMemcpyAsync(status_out, dst, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  const uint32_t n = *t->n_host;
+  *n_changed = n;
+  if (n) {
+    JRQ_HIP(e, hipMemcpyAsync(changed_out, dch, static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, e->stream));
+    JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  }
+  return JRQ_OK;
+}
+
+int jrq_table_read(jrq_table* t, int64_t* pending_index, int64_t* last_appended,
+                   int64_t* last_committed, int64_t* match) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  DeviceGuard guard(e->device);
+  const size_t G = t->a.G, ld = t->a.ld, b = G * 8;
+  std::vector<int64_t> lc(G);
+  JRQ_HIP(e, hipMemcpyAsync(lc.data(), t->a.lc, b, hipMemcpyDeviceToHost, e->stream));
+  if (pending_index) JRQ_HIP(e, hipMemcpyAsync(pending_index, t->a.pi, b, hipMemcpyDeviceToHost, e->stream));
+  if (last_appended) JRQ_HIP(e, hipMemcpyAsync(last_appended, t->a.la, b, hipMemcpyDeviceToHost, e->stream));
+  if (match)
+    for (uint32_t p = 0; p < t->a.P; ++p)
+      JRQ_HIP(e, hipMemcpyAsync(match + p * G, t->a.match + p * ld, b, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  if (pending_index)
+    for (size_t g = 0; g < G; ++g)
+      if (pending_index[g] == JRQ_PI_FOLLOWS_LC) pending_index[g] = lc[g] + 1;
+  if (last_committed) std::memcpy(last_committed, lc.data(), b);
+  return JRQ_OK;
+}
+
+int jrq_table_copy(jrq_table* dst, const jrq_table* src) {
+  if (table_check(dst) || !src || !src->e) return JRQ_E_INVALID;
+  jrq_engine* e = dst->e;
+  if (src->a.G != dst->a.G || src->a.P != dst->a.P || src->a.ld != dst->a.ld)
+    return fail(e, JRQ_E_INVALID, "table shapes differ");
+  DeviceGuard guard(e->device);
+  const size_t bytes = dst->a.ld * (dst->a.P + 4 + 2 * (jrq::kTableMaxRuns - 1)) * 8;
+  JRQ_HIP(e, hipMemcpyAsync(dst->mem, src->mem, bytes, hipMemcpyDeviceToDevice, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_table_view_get(jrq_table* t, jrq_table_view* v) {
+  if (table_check(t) || !v) return JRQ_E_INVALID;
+  v->match = t->a.match;
+  v->pending_index = t->a.pi;
+  v->last_appended = t->a.la;
+  v->last_committed = t->a.lc;
+  v->conf = t->a.conf;
+  v->ld = t->a.ld;
+  v->G = t->a.G;
+  v->num_peers = t->a.P;
   return JRQ_OK;
 }
 

@@ -176,3 +176,38 @@ struct JrqQuorumArgs {
   uint8_t* status;
   uint32_t G;
 };
+
+// Resident group table (table.hip; include/jrq.h jrq_table).
+namespace jrq {
+constexpr int kTableMaxRuns = 4;                   // JRQ_TABLE_MAX_RUNS
+constexpr int64_t kPiFollowsLc = INT64_MIN;        // JRQ_PI_FOLLOWS_LC
+}  // namespace jrq
+struct JrqTableArgs {
+  int64_t* match;        // [P][ld]
+  int64_t* pi;           // [ld] pendingIndex, or kPiFollowsLc
+  int64_t* la;           // [ld]
+  int64_t* lc;           // [ld]
+  uint64_t* conf;        // [ld] run 0 conf word | JRQ_CONF_RUNS
+  int64_t* xstart;       // [jrq::kTableMaxRuns - 1][ld] extra run starts (INT64_MAX = unused)
+  uint64_t* xconf;       // [kTableMaxRuns - 1][ld]
+  uint64_t ld;
+  uint32_t G;            // groups (ld >= G rounded up to pairs; pad groups are not leaders)
+  uint32_t P;
+  unsigned long long* ctr;  // compaction counter {blocks done << 32 | entries}, zero between launches
+  uint64_t* changed;     // [G] out
+  uint32_t* n_changed;   // [1] out
+  uint8_t* status;       // [G] out, nullable
+};
+
+// One group header as the ABI carries it (include/jrq.h jrq_group_state).
+struct JrqGroupState {
+  uint32_t group;
+  uint16_t num_runs;
+  uint16_t flags;
+  int64_t pending_index;
+  int64_t last_appended;
+  int64_t last_committed;
+  uint64_t run_conf[jrq::kTableMaxRuns];
+  int64_t run_start[jrq::kTableMaxRuns];
+};
+static_assert(sizeof(JrqGroupState) == 96, "jrq_group_state layout");

@@ -19,93 +19,25 @@
 // Groups whose conf word carries JRQ_CONF_RUNS walk their conf runs (run table); every other
 // group is decided from its conf word alone.  HBM-bound: 8P + 41 bytes per group decision
 // (roofline).
-#include "jrq_device.h"
+#include "quorum_core.h"
 
 namespace jrq {
 
-constexpr int64_t kI64Min = INT64_MIN;
-constexpr int64_t kI64Max = INT64_MAX;
-constexpr uint64_t kConfRuns = 1ull << 63;  // include/jrq.h JRQ_CONF_RUNS
-
-// q-th largest of v[p] over the peers in `mask` (q >= 1); kI64Min if fewer than q members.
-// P <= 16: rank-by-counting, branch-free, P^2 compares on 64-bit values in registers.
-template <int P>
-__device__ __forceinline__ int64_t kth_largest(const int64_t (&v)[P], uint32_t mask, uint32_t q) {
-  int64_t best = kI64Min;
-#pragma unroll
-  for (int a = 0; a < P; ++a) {
-    // members at least as large as v[a] (ties count): v[a] qualifies as a q-th-largest bound
-    uint32_t ge = 0;
-#pragma unroll
-    for (int b = 0; b < P; ++b) ge += ((mask >> b) & 1u) & (v[b] >= v[a] ? 1u : 0u);
-    const bool ok = ((mask >> a) & 1u) && ge >= q;
-    best = (ok && v[a] > best) ? v[a] : best;
-  }
-  return best;
-}
+// The CSR run table of the stateless ABI: runs [r0, r1) of one group.
+struct CsrRuns {
+  const int64_t* run_start;
+  const uint64_t* run_conf;
+  uint32_t r0;
+  __device__ int64_t start(uint32_t r) const { return run_start[r0 + r]; }
+  __device__ uint64_t conf(uint32_t r) const { return run_conf[r0 + r]; }
+};
 
 template <int P>
-__device__ __forceinline__ int64_t run_bound(const int64_t (&m)[P], uint64_t cw) {
-  const uint32_t nmask = static_cast<uint32_t>(cw & 0xFFFFu);
-  const uint32_t omask = static_cast<uint32_t>((cw >> 16) & 0xFFFFu);
-  const uint32_t nq = static_cast<uint32_t>((cw >> 32) & 0xFFu);
-  const uint32_t oq = static_cast<uint32_t>((cw >> 40) & 0xFFu);
-  // quorum 0 is always met (Ballot.isGranted: quorum <= 0, Ballot.java:138-140)
-  const int64_t kn = nq == 0 ? kI64Max : kth_largest<P>(m, nmask, nq);
-  const int64_t ko = oq == 0 ? kI64Max : kth_largest<P>(m, omask, oq);
-  return kn < ko ? kn : ko;
-}
-
-// Acks past the queue would throw ArrayIndexOutOfBoundsException and change nothing
-// (BallotBox.java:107-109): that peer grants no entry in this epoch.
-template <int P>
-__device__ __forceinline__ uint8_t mask_out_of_range(int64_t (&m)[P], int64_t la) {
-  uint8_t st = 0;
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    const bool oor = m[p] > la;
-    st |= oor ? kStOutOfRange : 0;
-    m[p] = oor ? kI64Min : m[p];
-  }
-  return st;
-}
-
-// One group with a single conf word (no conf change inside the pending window).
-template <int P>
-__device__ __forceinline__ void decide_single(int64_t pi, int64_t la, int64_t lc, uint64_t cw,
-                                              int64_t (&m)[P], int64_t& out, uint8_t& st_out) {
-  uint8_t st = mask_out_of_range<P>(m, la);
-  if ((cw & 0xFFFFu) == 0 && la >= pi) st |= kStEmptyConf;
-  int64_t cand = run_bound<P>(m, cw);
-  cand = cand < la ? cand : la;
-  const int64_t best = (cand >= pi && cand > lc) ? cand : lc;
-  // commitAt returns false when not the leader (BallotBox.java:101-103): state unchanged
-  out = pi == 0 ? lc : best;
-  st_out = pi == 0 ? kStNotLeader : st;
-}
-
-// Runs [r0, r1) of one group: run r covers [run_start[r], run_start[r+1]) (the last run ends at
-// lastAppended, the first starts at or before pendingIndex).  best is max(lc, the largest
-// granted index over the runs); each run is evaluated on its own, which reproduces the
-// reference's non-monotone commit when an even-size conf shrinks (BallotBox.java:124-129).
-template <int P>
-__device__ __forceinline__ int64_t runs_best(const JrqQuorumArgs& a, uint32_t r0, uint32_t r1,
-                                             int64_t pi, int64_t la, int64_t lc,
-                                             const int64_t (&m)[P], uint8_t& st) {
-  int64_t best = lc;
-#pragma unroll 1
-  for (uint32_t r = r0; r < r1; ++r) {
-    const int64_t s = (r == r0) ? pi : (a.run_start[r] > pi ? a.run_start[r] : pi);
-    const int64_t e = (r + 1 < r1) ? a.run_start[r + 1] - 1 : la;
-    const int64_t ee = e < la ? e : la;
-    if (ee < s) continue;  // run entirely committed already (or empty)
-    const uint64_t cw = a.run_conf[r];
-    if ((cw & 0xFFFFu) == 0) st |= kStEmptyConf;
-    int64_t cand = run_bound<P>(m, cw);
-    cand = cand < ee ? cand : ee;
-    best = (cand >= s && cand > best) ? cand : best;
-  }
-  return best;
+__device__ __forceinline__ int64_t csr_runs_best(const JrqQuorumArgs& a, uint32_t r0, uint32_t r1,
+                                                 int64_t pi, int64_t la, int64_t lc,
+                                                 const int64_t (&m)[P], uint8_t& st) {
+  const CsrRuns R{a.run_start, a.run_conf, r0};
+  return runs_best<P>(R, r1 - r0, pi, la, lc, m, st);
 }
 
 // A group flagged JRQ_CONF_RUNS: its runs from the CSR run table.
@@ -119,7 +51,7 @@ __device__ __forceinline__ void decide_runs(const JrqQuorumArgs& a, uint32_t g, 
     return;
   }
   uint8_t st = mask_out_of_range<P>(m, la);
-  out = runs_best<P>(a, a.run_off[g], a.run_off[g + 1], pi, la, lc, m, st);
+  out = csr_runs_best<P>(a, a.run_off[g], a.run_off[g + 1], pi, la, lc, m, st);
   st_out = st;
 }
 
@@ -246,22 +178,28 @@ __global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a)
 //   pi_k = committed_{k-1} + 1 once a commit happened (max_{j<k} v_j > lc_0), else pi_0
 // (a candidate in [s_r, committed_{k-1}] that the reference would refuse because it is below
 // pi_k cannot raise the max, so the threshold may stay at pi_0).  v_k depends on epoch k's
-// inputs only: lanes run over (group, epoch) -- a workgroup holds 64 groups, each of its W
-// waves C epochs of them -- and a scan over the waves' chunk maxima in LDS stitches the
-// prefix.  Loads stay coalesced (64 consecutive groups per row and epoch).
+// inputs only: lanes run over (group, epoch) -- a workgroup holds a tile of 32 groups, each
+// half-wave a chunk of C epochs of them -- and a scan over the chunk maxima in LDS stitches
+// the prefix.  Loads stay coalesced (32 consecutive groups = 256 B per row and epoch); small
+// tiles spread a 10k-group batch over all 256 CUs.
 template <int P>
 struct EpochChunk {
-  static constexpr int kC = (16 / (P + 1)) < 1 ? 1 : ((16 / (P + 1)) > 8 ? 8 : 16 / (P + 1));
+  static constexpr int kC = (8 / (P + 1)) < 1 ? 1 : ((8 / (P + 1)) > 8 ? 8 : 8 / (P + 1));
   static constexpr int kMaxWaves = P <= 8 ? 16 : 8;  // 128 / 256 VGPRs per lane
+  static constexpr int kTile = 32;                  // groups per workgroup
 };
 
 template <int P>
-__global__ __launch_bounds__(64 * EpochChunk<P>::kMaxWaves) void quorum_epochs_kernel(JrqQuorumArgs a, uint32_t K,
-                                                             uint64_t match_eld, uint64_t la_eld) {
+__global__ __launch_bounds__(64 * EpochChunk<P>::kMaxWaves) void quorum_epochs_kernel(
+    JrqQuorumArgs a, uint32_t K, uint64_t match_eld, uint64_t la_eld) {
   constexpr int C = EpochChunk<P>::kC;
-  __shared__ int64_t chunk_max[16][64];
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, W = blockDim.x >> 6;
-  const uint32_t g = blockIdx.x * 64u + lane;
+  constexpr uint32_t T = EpochChunk<P>::kTile;
+  __shared__ int64_t chunk_max[2 * 16][T];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t gl = lane & (T - 1u);
+  const uint32_t chunk = (threadIdx.x >> 6) * 2u + (lane >> 5);  // this half-wave's chunk
+  const uint32_t nchunks = (blockDim.x >> 6) * 2u;
+  const uint32_t g = blockIdx.x * T + gl;
   const bool live = g < a.G;
   const int64_t pi0 = live ? a.pending_index[g] : 0;
   const int64_t lc0 = live ? a.last_committed[g] : 0;
@@ -269,8 +207,8 @@ __global__ __launch_bounds__(64 * EpochChunk<P>::kMaxWaves) void quorum_epochs_k
   const bool runs = a.run_off != nullptr && (cw & kConfRuns);
   const uint32_t r0 = runs ? a.run_off[g] : 0, r1 = runs ? a.run_off[g + 1] : 0;
   int64_t carry = kI64Min;  // max v over the epochs of earlier super-chunks
-  for (uint32_t base = 0; base < K; base += W * C) {
-    const uint32_t k0 = base + w * C;
+  for (uint32_t base = 0; base < K; base += nchunks * C) {
+    const uint32_t k0 = base + chunk * C;
     int64_t la[C], pre[C];
     uint8_t st[C];
     {
@@ -298,19 +236,19 @@ __global__ __launch_bounds__(64 * EpochChunk<P>::kMaxWaves) void quorum_epochs_k
             v = cand >= pi0 ? cand : kI64Min;
           } else {
             uint8_t unused = 0;
-            v = runs_best<P>(a, r0, r1, pi0, la[c], kI64Min, m[c], unused);
+            v = csr_runs_best<P>(a, r0, r1, pi0, la[c], kI64Min, m[c], unused);
           }
           run_max = v > run_max ? v : run_max;
         }
-        pre[c] = run_max;  // inclusive max over this wave's chunk
+        pre[c] = run_max;  // inclusive max over this half-wave's chunk
       }
     }
-    chunk_max[w][lane] = pre[C - 1];
+    chunk_max[chunk][gl] = pre[C - 1];
     __syncthreads();
     int64_t excl = carry, all = carry;
-    for (uint32_t u = 0; u < W; ++u) {
-      const int64_t t = chunk_max[u][lane];
-      if (u < w) excl = t > excl ? t : excl;
+    for (uint32_t u = 0; u < nchunks; ++u) {
+      const int64_t t = chunk_max[u][gl];
+      if (u < chunk) excl = t > excl ? t : excl;
       all = t > all ? t : all;
     }
     __syncthreads();  // chunk_max is rewritten by the next super-chunk
@@ -467,10 +405,11 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum_ep
     const JrqQuorumArgs* args, uint32_t K, uint64_t match_eld, uint64_t la_eld, int num_cus,
     hipStream_t stream) {
   (void)num_cus;
-  // one workgroup per 64 groups; W waves of C epochs each (W <= 16), super-chunks beyond W*C
-  const dim3 grid(static_cast<unsigned>((static_cast<uint64_t>(args->G) + 63) / 64));
+  // one workgroup per 32-group tile; two chunks of C epochs per wave (<= 16 waves), super-
+  // chunks beyond that
+  const dim3 grid(static_cast<unsigned>((static_cast<uint64_t>(args->G) + 31) / 32));
   auto waves = [K](uint32_t C, uint32_t wmax) {
-    const uint32_t w = (K + C - 1) / C;
+    const uint32_t chunks = (K + C - 1) / C, w = (chunks + 1) / 2;
     return dim3(64u * (w < wmax ? w : wmax));
   };
   switch (args->num_peers) {

@@ -1,0 +1,216 @@
+// table.hip -- the resident group table (include/jrq.h jrq_table): BallotBox state of G groups
+// kept in HBM across epochs, incremental updates, and an epoch that returns only the groups
+// whose commit advanced.
+//
+// Replaces, for a long-running multi-Raft host, the per-group state and calls of
+//   BallotBox.commitAt / appendPendingTask / resetPendingIndex / clearPendingTasks
+//   (jraft-core/.../core/BallotBox.java:96-215) and Ballot.grant/isGranted (entity/Ballot.java:
+//   100-140), with the formulation of quorum.hip (quorum_core.h).
+//
+// Kernels:
+//   table_states_kernel  group headers (one lane per header; rare: leader changes, conf runs)
+//   table_recs_kernel    8-B update records: match of one peer slot / queue size of one group
+//   table_epoch_kernel   one epoch over every group, in place; a commit writes lastCommitted
+//                        (pendingIndex becomes JRQ_PI_FOLLOWS_LC once), and the group is
+//                        appended to a compacted list with one 64-bit atomic per workgroup.
+// HBM per group per epoch: reads match 8P + pendingIndex, lastAppended, lastCommitted, conf
+// 32 B; writes 8 B lastCommitted + 8 B list entry per committing group.
+#include "quorum_core.h"
+
+namespace jrq {
+
+typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ i64x2 tld2(const int64_t* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(p));
+}
+
+// Runs of a flagged group: run 0 = the conf word (starts at or before pendingIndex), runs
+// 1..kTableMaxRuns-1 in the inline slots (start INT64_MAX = unused: an empty run).
+struct TableRuns {
+  const JrqTableArgs* t;
+  uint32_t g;
+  uint64_t c0;
+  __device__ int64_t start(uint32_t r) const {
+    return r == 0 ? kI64Min : t->xstart[static_cast<size_t>(r - 1) * t->ld + g];
+  }
+  __device__ uint64_t conf(uint32_t r) const {
+    return r == 0 ? c0 : t->xconf[static_cast<size_t>(r - 1) * t->ld + g];
+  }
+};
+
+// The run path (flagged groups only): reloads the group so that no register of the fast path
+// stays live across it.
+template <int P>
+__device__ __forceinline__ void table_redecide(const JrqTableArgs& t, uint32_t g, int64_t& out,
+                                               uint8_t& st) {
+  const int64_t pr = t.pi[g], lc = t.lc[g], la = t.la[g];
+  const uint64_t cw = t.conf[g];
+  int64_t m[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) m[p] = t.match[static_cast<size_t>(p) * t.ld + g];
+  const int64_t pi = pr == kPiFollowsLc ? lc + 1 : pr;
+  if (pi == 0) {
+    out = lc;
+    st = kStNotLeader;
+    return;
+  }
+  st = mask_out_of_range<P>(m, la);
+  const TableRuns R{&t, g, cw & ~kConfRuns};
+  out = runs_best<P>(R, kTableMaxRuns, pi, la, lc, m, st);
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void table_epoch_kernel(JrqTableArgs t) {
+  __shared__ uint32_t wave_cnt[4];
+  __shared__ uint32_t blk_base;
+  const uint32_t pairs = (t.G + 1) >> 1;  // ld covers the pad group of an odd G (not a leader)
+  const uint32_t tt = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t g = tt << 1;
+  bool c0 = false, c1 = false;
+  uint64_t e0 = 0, e1 = 0;
+  if (tt < pairs) {
+    const i64x2 pr = tld2(t.pi + g);
+    const i64x2 lc = tld2(t.lc + g);
+    const i64x2 la = tld2(t.la + g);
+    const i64x2 cw = tld2(reinterpret_cast<const int64_t*>(t.conf) + g);
+    i64x2 mv[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) mv[p] = tld2(t.match + static_cast<size_t>(p) * t.ld + g);
+    const int64_t pi0 = pr.x == kPiFollowsLc ? lc.x + 1 : pr.x;
+    const int64_t pi1 = pr.y == kPiFollowsLc ? lc.y + 1 : pr.y;
+    const uint32_t flags = static_cast<uint32_t>(static_cast<uint64_t>(cw.x) >> 63) |
+                           (static_cast<uint32_t>(static_cast<uint64_t>(cw.y) >> 63) << 1);
+    int64_t m0[P], m1[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      m0[p] = mv[p].x;
+      m1[p] = mv[p].y;
+    }
+    int64_t o0, o1;
+    uint8_t s0, s1;
+    decide_single<P>(pi0, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
+    decide_single<P>(pi1, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
+    if (flags) {  // rare: groups with a conf change inside their pending window
+      if (flags & 1u) table_redecide<P>(t, g, o0, s0);
+      if (flags & 2u) table_redecide<P>(t, g + 1, o1, s1);
+    }
+    c0 = o0 > lc.x;  // decide_* return lastCommitted unless a commit happened
+    c1 = o1 > lc.y;
+    if (c0 || c1) {
+      i64x2 o;
+      o.x = o0;
+      o.y = o1;
+      __builtin_nontemporal_store(o, reinterpret_cast<i64x2*>(t.lc + g));
+      // pendingIndex = lastCommittedIndex + 1 from now on (BallotBox.java:131-132): one store
+      // per group and leadership, the steady state writes lastCommitted only
+      if (c0 && pr.x != kPiFollowsLc) t.pi[g] = kPiFollowsLc;
+      if (c1 && pr.y != kPiFollowsLc) t.pi[g + 1] = kPiFollowsLc;
+    }
+    if (t.status) {
+      if (g + 1 < t.G)
+        __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
+                                    reinterpret_cast<uint16_t*>(t.status + g));
+      else
+        t.status[g] = s0;
+    }
+    e0 = (static_cast<uint64_t>(o0 - pi0 + 1) << 32) | g;
+    e1 = (static_cast<uint64_t>(o1 - pi1 + 1) << 32) | (g + 1);
+  }
+  // compaction: lane-major order inside a wave, waves in order inside the workgroup, and one
+  // 64-bit atomic per workgroup ({workgroups done << 32 | entries}) reserves its slice of the
+  // list; the last workgroup to arrive publishes the count and re-zeroes the counter
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint32_t pre = __popcll(b0 & below) + __popcll(b1 & below);
+  if (lane == 0) wave_cnt[w] = __popcll(b0) + __popcll(b1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+    const unsigned long long old = atomicAdd(t.ctr, (1ull << 32) | tot);
+    blk_base = static_cast<uint32_t>(old);
+    if (static_cast<uint32_t>(old >> 32) + 1u == gridDim.x) {
+      *t.n_changed = static_cast<uint32_t>(old) + tot;
+      atomicExch(t.ctr, 0ull);
+    }
+  }
+  __syncthreads();
+  uint32_t pos = blk_base + pre;
+  for (uint32_t u = 0; u < w; ++u) pos += wave_cnt[u];
+  if (c0) t.changed[pos++] = e0;
+  if (c1) t.changed[pos] = e1;
+}
+
+// Group headers: one lane per header (a group appears at most once per call).
+__global__ __launch_bounds__(256) void table_states_kernel(JrqTableArgs t, const JrqGroupState* s,
+                                                          uint32_t n) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const JrqGroupState st = s[i];
+  const uint32_t g = st.group;
+  if (g >= t.G) return;
+  const uint32_t nr = st.num_runs < kTableMaxRuns ? st.num_runs : kTableMaxRuns;
+  t.pi[g] = st.pending_index;
+  t.la[g] = st.last_appended;
+  t.lc[g] = st.last_committed;
+  const uint64_t c0 = nr ? (st.run_conf[0] & ~kConfRuns) : 0;
+  t.conf[g] = c0 | (nr > 1 ? kConfRuns : 0ull);
+#pragma unroll
+  for (int k = 1; k < kTableMaxRuns; ++k) {
+    const size_t o = static_cast<size_t>(k - 1) * t.ld + g;
+    t.xstart[o] = static_cast<uint32_t>(k) < nr ? st.run_start[k] : kI64Max;
+    t.xconf[o] = static_cast<uint32_t>(k) < nr ? (st.run_conf[k] & ~kConfRuns) : 0ull;
+  }
+  if (st.flags & 1u)  // JRQ_STATE_RESET_MATCH: a new leader's replicators start over
+    for (uint32_t p = 0; p < t.P; ++p) t.match[static_cast<size_t>(p) * t.ld + g] = st.pending_index - 1;
+}
+
+// 8-byte update records (include/jrq.h JRQ_REC): value relative to the group's pendingIndex.
+__global__ __launch_bounds__(256) void table_recs_kernel(JrqTableArgs t, const uint64_t* recs,
+                                                         uint32_t n) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t r = recs[i];
+  const uint32_t f = static_cast<uint32_t>(r & 31u);
+  const uint32_t g = static_cast<uint32_t>(r >> 5) & ((1u << 27) - 1u);
+  const uint32_t v = static_cast<uint32_t>(r >> 32);
+  if (g >= t.G || f > 16u || (f < 16u && f >= t.P)) return;
+  const int64_t pr = t.pi[g], lc = t.lc[g];
+  const int64_t val = (pr == kPiFollowsLc ? lc + 1 : pr) - 1 + static_cast<int64_t>(v);
+  if (f == 16u) t.la[g] = val;
+  else t.match[static_cast<size_t>(f) * t.ld + g] = val;
+}
+
+}  // namespace jrq
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_update(
+    const JrqTableArgs* a, const JrqGroupState* states, uint32_t n_states, const uint64_t* recs,
+    uint32_t n_recs, hipStream_t stream) {
+  if (n_states)
+    hipLaunchKernelGGL(jrq::table_states_kernel, dim3((n_states + 255) / 256), dim3(256), 0,
+                       stream, *a, states, n_states);
+  if (n_recs)
+    hipLaunchKernelGGL(jrq::table_recs_kernel, dim3((n_recs + 255) / 256), dim3(256), 0, stream,
+                       *a, recs, n_recs);
+  return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_epoch(
+    const JrqTableArgs* a, hipStream_t stream) {
+  const uint32_t pairs = (a->G + 1) >> 1;
+  const dim3 grid((pairs + 255) / 256), blk(256);
+  switch (a->P) {
+#define JRQ_CASE(P)                                                                   \
+  case P:                                                                             \
+    hipLaunchKernelGGL(jrq::table_epoch_kernel<P>, grid, blk, 0, stream, *a);         \
+    break;
+    JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
+    JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
+    JRQ_CASE(15) JRQ_CASE(16)
+#undef JRQ_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}

@@ -4,6 +4,9 @@
 #include "jraft_host.h"
 
 #include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <sstream>
 
@@ -184,92 +187,226 @@ uint64_t CRC64::getValue() {
 
 // --------------------------------------------------------------- ballot box
 
+template <class T>
+void GroupBatch::PinnedBuf<T>::reserve(size_t n) {
+  if (n <= cap) return;
+  const size_t want = std::max(n, 2 * cap);
+  const size_t bytes = ((want * sizeof(T)) + 4095) & ~size_t(4095);
+  release();
+  p = static_cast<T*>(std::aligned_alloc(4096, bytes));
+  if (!p) throw std::bad_alloc();
+  registered = jrq_host_register(p, bytes) == JRQ_OK;  // DMA straight from these pages
+  cap = bytes / sizeof(T);
+}
+
+template <class T>
+void GroupBatch::PinnedBuf<T>::release() {
+  if (p) {
+    if (registered) jrq_host_unregister(p);
+    std::free(p);
+  }
+  p = nullptr;
+  cap = 0;
+  registered = false;
+}
+
 GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
-    : eng_(eng), G_(groups), P_(peers), grp_(groups) {
+    : eng_(eng), G_(groups), P_(peers) {
   if (peers == 0 || peers > JRQ_MAX_PEERS) throw std::invalid_argument("peers must be 1..16");
-  for (auto& g : grp_) g.match.assign(P_, 0);
+  if (groups == 0 || groups > JRQ_TABLE_MAX_GROUPS) throw std::invalid_argument("groups must be 1..2^27");
+  const size_t GP = static_cast<size_t>(G_) * P_;
+  pi_.assign(G_, 0);
+  lc_.assign(G_, 0);
+  la_.assign(G_, -1);
+  runs_.assign(static_cast<size_t>(G_) * JRQ_TABLE_MAX_RUNS, Run{0, 0});
+  nruns_.assign(G_, 0);
+  slotPeer_.assign(GP, kNoPeer);
+  slotUse_.assign(GP, 0);
+  match_.assign(GP, 0);
+  dirty_.assign(G_, 0);
+  waiter_.resize(G_);
+  inited_.assign(G_, 0);
+  closures_.resize(G_);
 }
 
-int GroupBatch::slotOf(Group& g, const PeerId& p, bool create) {
-  auto it = g.slot.find(p);
-  if (it != g.slot.end()) return it->second;
+GroupBatch::~GroupBatch() {
+  if (table_) jrq_table_destroy(table_);
+}
+
+uint32_t GroupBatch::internPeer(const PeerId& p) {
+  auto it = peerIds_.find(p);
+  if (it != peerIds_.end()) return it->second;
+  const uint32_t id = static_cast<uint32_t>(peerIds_.size());
+  peerIds_.emplace(p, id);
+  return id;
+}
+
+// Slots named by the masks of the group's live conf runs: their peers vote on pending entries.
+uint32_t GroupBatch::liveMask(uint32_t g) const {
+  uint32_t m = 0;
+  for (uint32_t r = 0; r < nruns_[g]; ++r) {
+    const uint64_t cw = runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS + r].conf;
+    m |= static_cast<uint32_t>(cw & 0xFFFFu) | static_cast<uint32_t>((cw >> 16) & 0xFFFFu);
+  }
+  return m;
+}
+
+// The slot of `peer` in group g.  create: a free slot, else the least recently acked slot that
+// no live conf run names (and that is not in `reserved`), its match reset (its peer's acks no
+// longer matter to any pending ballot).  Throws std::length_error when every slot is live.
+int GroupBatch::slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved) {
+  const size_t base = static_cast<size_t>(g) * P_;
+  int victim = -1;
+  for (uint32_t s = 0; s < P_; ++s) {
+    if (slotPeer_[base + s] == peer) return static_cast<int>(s);
+    if (victim < 0 && slotPeer_[base + s] == kNoPeer) victim = static_cast<int>(s);
+  }
   if (!create) return -1;
-  if ((uint32_t)g.slot.size() >= P_) throw std::length_error("more distinct peers than slots");
-  int s = (int)g.slot.size();
-  g.slot.emplace(p, s);
-  return s;
+  if (victim < 0) {
+    const uint32_t busy = liveMask(g) | reserved;
+    for (uint32_t s = 0; s < P_; ++s)
+      if (!((busy >> s) & 1u) && (victim < 0 || slotUse_[base + s] < slotUse_[base + victim]))
+        victim = static_cast<int>(s);
+    if (victim < 0)
+      throw std::length_error("more distinct live peers in group " + std::to_string(g) +
+                              " than the " + std::to_string(P_) + " peer slots");
+  }
+  slotPeer_[base + victim] = peer;
+  slotUse_[base + victim] = flushes_;
+  if (match_[base + victim] != 0) {
+    match_[base + victim] = 0;
+    markDirty(g, 1u << victim);
+  }
+  return victim;
 }
 
-uint64_t GroupBatch::confWord(Group& g, const Configuration& conf, const Configuration* old) {
+uint64_t GroupBatch::confWord(uint32_t g, const Configuration& conf, const Configuration* old) {
   // Ballot.init (Ballot.java:63-85): peers only, quorum = size/2+1, oldQuorum 0 if null
   uint32_t nm = 0, om = 0;
-  for (auto& p : conf.peers) nm |= 1u << slotOf(g, p, true);
-  uint32_t nq = (uint32_t)conf.peers.size() / 2 + 1, oq = 0;
+  for (auto& p : conf.peers) nm |= 1u << slotOf(g, internPeer(p), true, nm | om);
+  uint32_t nq = static_cast<uint32_t>(conf.peers.size()) / 2 + 1, oq = 0;
   if (old) {
-    for (auto& p : old->peers) om |= 1u << slotOf(g, p, true);
-    oq = (uint32_t)old->peers.size() / 2 + 1;
+    for (auto& p : old->peers) om |= 1u << slotOf(g, internPeer(p), true, nm | om);
+    oq = static_cast<uint32_t>(old->peers.size()) / 2 + 1;
   }
   return JRQ_CONF(nm, om, nq, oq);
 }
 
-uint32_t GroupBatch::flush() {
-  std::vector<uint32_t> live;
-  for (uint32_t i = 0; i < G_; ++i)
-    if (grp_[i].pendingIndex != 0 && grp_[i].lastAppended >= grp_[i].pendingIndex) live.push_back(i);
-  if (live.empty()) return 0;
-  const uint32_t G = (uint32_t)live.size();
-  std::vector<int64_t> match((size_t)P_ * G), pi(G), la(G), lc(G), committed(G);
-  std::vector<uint64_t> conf(G);
-  std::vector<uint32_t> run_off(G + 1, 0);
-  std::vector<int64_t> run_start;
-  std::vector<uint64_t> run_conf;
-  for (uint32_t k = 0; k < G; ++k) {
-    Group& g = grp_[live[k]];
-    for (uint32_t p = 0; p < P_; ++p) match[(size_t)p * G + k] = g.match[p];
-    pi[k] = g.pendingIndex;
-    la[k] = g.lastAppended;
-    lc[k] = g.lastCommitted;
-    conf[k] = g.runs.empty() ? 0 : g.runs.front().conf;
-    for (auto& r : g.runs) {
-      run_start.push_back(r.start);
-      run_conf.push_back(r.conf);
+// Would a gap [lo, hi] in `slot`'s acks skip a pending entry whose ballot counts that slot?
+bool GroupBatch::gapCountsPeer(uint32_t g, int slot, int64_t lo, int64_t hi) const {
+  const Run* R = &runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS];
+  const uint32_t n = nruns_[g];
+  for (uint32_t r = 0; r < n; ++r) {
+    const int64_t s = r == 0 ? pi_[g] : R[r].start;
+    const int64_t e = r + 1 < n ? R[r + 1].start - 1 : la_[g];
+    const uint64_t cw = R[r].conf;
+    const uint32_t m = static_cast<uint32_t>(cw & 0xFFFFu) | static_cast<uint32_t>((cw >> 16) & 0xFFFFu);
+    if (std::max(s, lo) <= std::min(e, hi) && ((m >> slot) & 1u)) return true;
+  }
+  return false;
+}
+
+// Drop runs wholly below pendingIndex (pendingMetaQueue.removeRange, BallotBox.java:130).
+void GroupBatch::dropDeadRuns(uint32_t g) {
+  Run* R = &runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS];
+  uint32_t n = nruns_[g], k = 0;
+  while (k + 1 < n && R[k + 1].start <= pi_[g]) ++k;
+  if (k) {
+    for (uint32_t r = k; r < n; ++r) R[r - k] = R[r];
+    nruns_[g] = static_cast<uint8_t>(n - k);
+  }
+}
+
+// BallotBox.commitAt's commit, after the epoch (:130-137): drop the ballots up to c, run their
+// closures (ClosureQueue.popClosureUntil -> done.run(OK)), then waiter.onCommitted(c).
+void GroupBatch::commitTo(uint32_t g, int64_t c) {
+  if (auto& q = closures_[g]) {
+    while (!q->empty() && q->front().first <= c) {
+      auto done = std::move(q->front().second);
+      q->pop_front();
+      done(true);
     }
-    run_off[k + 1] = (uint32_t)run_start.size();
   }
-  std::vector<uint8_t> status(G);
-  jrq_group_batch b{};
-  b.match = match.data();
-  b.pending_index = pi.data();
-  b.last_appended = la.data();
-  b.last_committed = lc.data();
-  b.conf = conf.data();
-  b.run_off = run_off.data();
-  b.run_start = run_start.data();
-  b.run_conf = run_conf.data();
-  b.num_peers = P_;
-  b.num_runs = (uint32_t)run_start.size();
-  b.match_ld = G;
+  pi_[g] = c + 1;
+  lc_[g] = c;
+  dropDeadRuns(g);
+  if (waiter_[g]) waiter_[g](c);
+}
+
+uint32_t GroupBatch::flush() {
   if (!eng_) throw std::logic_error("GroupBatch::flush needs an Engine");
-  throwIfError(jrq_quorum_epoch(eng_->raw(), &b, committed.data(), status.data(), G), eng_->raw(),
-               "jrq_quorum_epoch");
-  uint32_t advanced = 0;
-  for (uint32_t k = 0; k < G; ++k) {
-    Group& g = grp_[live[k]];
-    const int64_t c = committed[k];
-    if (c <= g.lastCommitted) continue;
-    // pendingMetaQueue.removeRange(0, c - pendingIndex + 1); pendingIndex = c + 1 (:130-132)
-    const int64_t ncommitted = c - g.pendingIndex + 1;
-    for (int64_t i = 0; i < ncommitted && i < (int64_t)g.closures.size(); ++i)
-      if (g.closures[i]) g.closures[i](true);  // ClosureQueue.popClosureUntil -> done.run(OK)
-    g.closures.erase(g.closures.begin(),
-                     g.closures.begin() + std::min<int64_t>(ncommitted, (int64_t)g.closures.size()));
-    g.pendingIndex = c + 1;
-    g.lastCommitted = c;
-    while (g.runs.size() > 1 && g.runs[1].start <= g.pendingIndex) g.runs.erase(g.runs.begin());
-    ++advanced;
-    if (g.waiter) g.waiter(c);  // waiter.onCommitted(lastCommittedIndex), after the "unlock"
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  stats_ = FlushStats{};
+  if (!table_) {  // first flush: the device table starts empty, ship every group's state
+    int err = 0;
+    table_ = jrq_table_create(eng_->raw(), G_, P_, &err);
+    if (!table_) throwIfError(err ? err : JRQ_E_NOMEM, eng_->raw(), "jrq_table_create");
+    for (uint32_t g = 0; g < G_; ++g) {
+      uint32_t bits = 0;
+      if (pi_[g] != 0 || lc_[g] != 0 || nruns_[g] != 0) bits |= kDirtyHeader;
+      for (uint32_t s = 0; s < P_; ++s)
+        if (match_[static_cast<size_t>(g) * P_ + s] != 0) bits |= 1u << s;
+      if (bits) markDirty(g, bits);
+    }
   }
-  return advanced;
+  // pack the changes: one header per group whose header changed, else 8-B records
+  const size_t nd = dirtyList_.size();
+  states_.reserve(nd + 1);
+  recs_.reserve(nd * (P_ + 1) + 1);
+  uint32_t ns = 0, nr = 0;
+  for (uint32_t g : dirtyList_) {
+    const uint32_t d = dirty_[g];
+    dirty_[g] = 0;
+    const int64_t pi = pi_[g], base = pi - 1;
+    if (d & kDirtyHeader) {
+      jrq_group_state& st = states_.p[ns++];
+      std::memset(&st, 0, sizeof st);
+      st.group = g;
+      st.num_runs = nruns_[g];
+      st.flags = (d & kDirtyReset) ? JRQ_STATE_RESET_MATCH : 0;
+      st.pending_index = pi;
+      st.last_appended = la_[g];
+      st.last_committed = lc_[g];
+      const Run* R = &runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS];
+      for (uint32_t r = 0; r < nruns_[g]; ++r) {
+        st.run_conf[r] = R[r].conf;
+        st.run_start[r] = R[r].start;
+      }
+    } else if ((d & kDirtyLa) && pi != 0) {
+      recs_.p[nr++] = JRQ_REC(g, JRQ_REC_LAST_APPENDED, la_[g] - base);
+    }
+    if (pi == 0) continue;  // not the leader: its acks are refused (commitAt returns false)
+    for (uint32_t m = d & 0xFFFFu; m; m &= m - 1) {
+      const uint32_t s = static_cast<uint32_t>(__builtin_ctz(m));
+      const int64_t v = match_[static_cast<size_t>(g) * P_ + s] - base;
+      recs_.p[nr++] = JRQ_REC(g, s, v > 0 ? v : 0);
+    }
+  }
+  dirtyList_.clear();
+  changed_.reserve(G_);
+  const auto t1 = clk::now();
+  throwIfError(jrq_table_update(table_, states_.p, ns, recs_.p, nr), eng_->raw(), "jrq_table_update");
+  uint32_t n = 0;
+  throwIfError(jrq_table_epoch(table_, changed_.p, &n, nullptr), eng_->raw(), "jrq_table_epoch");
+  const auto t2 = clk::now();
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t w = changed_.p[i];
+    const uint32_t g = static_cast<uint32_t>(w);
+    commitTo(g, pi_[g] - 1 + static_cast<int64_t>(w >> 32));
+  }
+  ++flushes_;
+  const auto t3 = clk::now();
+  auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
+  stats_.states = ns;
+  stats_.records = nr;
+  stats_.changed = n;
+  stats_.h2d_bytes = static_cast<uint64_t>(ns) * sizeof(jrq_group_state) + static_cast<uint64_t>(nr) * 8;
+  stats_.d2h_bytes = 4 + static_cast<uint64_t>(n) * 8;
+  stats_.pack_ms = ms(t1 - t0);
+  stats_.device_ms = ms(t2 - t1);
+  stats_.deliver_ms = ms(t3 - t2);
+  return n;
 }
 
 BallotBox::BallotBox(std::shared_ptr<GroupBatch> batch, uint32_t group) : batch_(std::move(batch)), g_(group) {
@@ -278,81 +415,119 @@ BallotBox::BallotBox(std::shared_ptr<GroupBatch> batch, uint32_t group) : batch_
 
 bool BallotBox::init(const BallotBoxOptions& opts) {
   if (!opts.waiter || !opts.closureQueue) return false;  // "waiter or closure queue is null."
-  auto& g = batch_->grp_[g_];
-  g.waiter = opts.waiter;
-  g.inited = true;
+  batch_->waiter_[g_] = opts.waiter;
+  batch_->inited_[g_] = 1;
   return true;
 }
 
 bool BallotBox::commitAt(int64_t first, int64_t last, const PeerId& peer) {
-  auto& g = batch_->grp_[g_];
-  if (g.pendingIndex == 0) return false;                         // :101-103
-  if (last < g.pendingIndex) return true;                        // :104-106
-  if (last > g.lastAppended) throw std::out_of_range("ArrayIndexOutOfBoundsException");  // :107-109
-  const int s = batch_->slotOf(g, peer, false);
-  if (s < 0) return true;  // not in any conf of this group: Ballot.grant finds nothing
-  int64_t& m = g.match[s];
-  if (first > std::max(m + 1, g.pendingIndex))
+  GroupBatch& b = *batch_;
+  const int64_t pi = b.pi_[g_];
+  if (pi == 0) return false;                                     // :101-103
+  if (last < pi) return true;                                    // :104-106
+  if (last > b.la_[g_]) throw std::out_of_range("ArrayIndexOutOfBoundsException");  // :107-109
+  const int s = b.slotOf(g_, b.internPeer(peer), true);
+  const size_t k = static_cast<size_t>(g_) * b.P_ + s;
+  int64_t& m = b.match_[k];
+  const int64_t lo = std::max(m + 1, pi);
+  if (first > lo && b.gapCountsPeer(g_, s, lo, first - 1))
     throw std::logic_error("non-contiguous ack: the Replicator never skips entries");
-  if (last > m) m = last;
+  if (last > m) {
+    m = last;
+    b.markDirty(g_, 1u << s);
+  }
+  b.slotUse_[k] = b.flushes_;
   return true;
 }
 
 void BallotBox::clearPendingTasks() {
-  auto& g = batch_->grp_[g_];
-  for (auto& c : g.closures)
-    if (c) c(false);  // ClosureQueue.clear runs closures with EPERM
-  g.closures.clear();
-  g.runs.clear();
-  g.pendingIndex = 0;
-  g.lastAppended = -1;
+  GroupBatch& b = *batch_;
+  if (auto& q = b.closures_[g_]) {
+    for (auto& c : *q) c.second(false);  // ClosureQueue.clear runs closures with EPERM
+    q->clear();
+  }
+  b.nruns_[g_] = 0;
+  b.pi_[g_] = 0;
+  b.la_[g_] = -1;
+  b.markDirty(g_, GroupBatch::kDirtyHeader);
 }
 
 bool BallotBox::resetPendingIndex(int64_t n) {
-  auto& g = batch_->grp_[g_];
-  if (!(g.pendingIndex == 0 && g.lastAppended < g.pendingIndex)) return false;
-  if (n <= g.lastCommitted) return false;
-  g.pendingIndex = n;
-  g.lastAppended = n - 1;
-  g.runs.clear();
-  std::fill(g.match.begin(), g.match.end(), 0);  // a new leader's replicators start over
+  GroupBatch& b = *batch_;
+  if (!(b.pi_[g_] == 0 && b.la_[g_] < b.pi_[g_])) return false;
+  if (n <= b.lc_[g_]) return false;
+  b.pi_[g_] = n;
+  b.la_[g_] = n - 1;
+  b.nruns_[g_] = 0;
+  // a new leader's replicators start over
+  std::fill(b.match_.begin() + static_cast<size_t>(g_) * b.P_,
+            b.match_.begin() + static_cast<size_t>(g_ + 1) * b.P_, 0);
+  b.markDirty(g_, GroupBatch::kDirtyHeader | GroupBatch::kDirtyReset);
+  return true;
+}
+
+bool BallotBox::appendPendingTasks(const Configuration& conf, const Configuration* oldConf,
+                                   int64_t count) {
+  GroupBatch& b = *batch_;
+  if (b.pi_[g_] <= 0) return false;  // :204-207
+  if (count <= 0) return true;
+  if (b.la_[g_] + count - b.pi_[g_] + 1 > INT32_MAX)  // pendingMetaQueue is a Java ArrayList
+    throw std::length_error("pending queue larger than an ArrayList");
+  const uint64_t cw = b.confWord(g_, conf, oldConf);
+  GroupBatch::Run* R = &b.runs_[static_cast<size_t>(g_) * JRQ_TABLE_MAX_RUNS];
+  uint8_t& n = b.nruns_[g_];
+  const int64_t idx = b.la_[g_] + 1;
+  if (n == 0 || R[n - 1].conf != cw) {  // Ballot.init with a new conf: a new conf run
+    if (n == JRQ_TABLE_MAX_RUNS) {
+      if (idx > b.pi_[g_])  // NodeImpl never has more than 2 (joint, then stable) pending
+        throw std::length_error("more conf runs pending than JRQ_TABLE_MAX_RUNS");
+      n = 0;  // the queue is empty: every earlier run is dead
+    }
+    R[n++] = GroupBatch::Run{idx, cw};
+    b.dropDeadRuns(g_);
+    b.markDirty(g_, GroupBatch::kDirtyHeader);
+  }
+  b.la_[g_] = idx + count - 1;
+  b.markDirty(g_, GroupBatch::kDirtyLa);
   return true;
 }
 
 bool BallotBox::appendPendingTask(const Configuration& conf, const Configuration* oldConf,
                                   std::function<void(bool)> done) {
-  auto& g = batch_->grp_[g_];
-  if (g.pendingIndex <= 0) return false;  // :204-207
-  const uint64_t cw = batch_->confWord(g, conf, oldConf);
-  const int64_t idx = g.lastAppended + 1;
-  if (g.runs.empty() || g.runs.back().conf != cw) g.runs.push_back({idx, cw});
-  g.lastAppended = idx;
-  g.closures.push_back(std::move(done));
+  GroupBatch& b = *batch_;
+  if (b.pi_[g_] <= 0) return false;  // :204-207
+  if (!appendPendingTasks(conf, oldConf, 1)) return false;
+  if (done) {
+    auto& q = b.closures_[g_];
+    if (!q) q.reset(new std::deque<std::pair<int64_t, std::function<void(bool)>>>());
+    q->emplace_back(b.la_[g_], std::move(done));
+  }
   return true;
 }
 
 bool BallotBox::setLastCommittedIndex(int64_t c) {
-  auto& g = batch_->grp_[g_];
-  if (g.pendingIndex != 0 || g.lastAppended >= g.pendingIndex) {
-    if (!(c < g.pendingIndex))  // Requires.requireTrue (:229-231)
+  GroupBatch& b = *batch_;
+  if (b.pi_[g_] != 0 || b.la_[g_] >= b.pi_[g_]) {
+    if (!(c < b.pi_[g_]))  // Requires.requireTrue (:229-231)
       throw std::invalid_argument("Node changes to leader, pendingIndex=" +
-                                  std::to_string(g.pendingIndex) +
+                                  std::to_string(b.pi_[g_]) +
                                   ", param lastCommittedIndex=" + std::to_string(c));
     return false;
   }
-  if (c < g.lastCommitted) return false;
-  if (c > g.lastCommitted) {
-    g.lastCommitted = c;
-    if (g.waiter) g.waiter(c);
+  if (c < b.lc_[g_]) return false;
+  if (c > b.lc_[g_]) {
+    b.lc_[g_] = c;
+    b.markDirty(g_, GroupBatch::kDirtyHeader);
+    if (b.waiter_[g_]) b.waiter_[g_](c);
   }
   return true;
 }
 
-int64_t BallotBox::getLastCommittedIndex() const { return batch_->grp_[g_].lastCommitted; }
-int64_t BallotBox::getPendingIndex() const { return batch_->grp_[g_].pendingIndex; }
+int64_t BallotBox::getLastCommittedIndex() const { return batch_->lc_[g_]; }
+int64_t BallotBox::getPendingIndex() const { return batch_->pi_[g_]; }
 int64_t BallotBox::getPendingMetaQueueSize() const {
-  auto& g = batch_->grp_[g_];
-  return g.pendingIndex == 0 ? 0 : g.lastAppended - g.pendingIndex + 1;
+  const GroupBatch& b = *batch_;
+  return b.pi_[g_] == 0 ? 0 : b.la_[g_] - b.pi_[g_] + 1;
 }
 
 std::string BallotBox::describe() const {

@@ -13,17 +13,20 @@
 // std::invalid_argument for IllegalArgumentException (Requires.requireTrue).
 //
 // Every checksum and every quorum decision is computed by libjrq.so on the GPU.  The
-// BallotBox objects of many groups share one GroupBatch; acks are recorded at call time
-// (with the reference's synchronous checks) and decided in batched epochs by flush(),
-// after which the FSMCaller waiter sees onCommitted(index) exactly as the reference calls it.
+// BallotBox objects of many groups share one GroupBatch, whose state lives in a resident
+// device table (jrq_table); acks are recorded at call time (with the reference's synchronous
+// checks), only the changes are uploaded, and flush() decides an epoch on the GPU, after
+// which the FSMCaller waiter sees onCommitted(index) exactly as the reference calls it.
 #pragma once
 
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/jrq.h"
@@ -155,15 +158,19 @@ class BallotBox {
   bool init(const BallotBoxOptions& opts);                                     // :82-90
   // :96-139 -- false if not leader; true if last < pendingIndex (stale); throws
   // std::out_of_range when last >= pendingIndex + queue size; otherwise records the ack,
-  // decided at the next GroupBatch::flush().  Acks of one peer must be contiguous from
-  // pendingIndex (the Replicator invariant, Replicator.java:1387-1401): a gap throws
-  // std::logic_error.
+  // decided at the next GroupBatch::flush().  Any peer may ack (a catch-up replicator of a
+  // peer not yet in a conf included, Replicator.java:1387-1392).  A peer's acks must be
+  // contiguous over the entries whose ballots count it (the Replicator invariant,
+  // Replicator.java:1387-1401): a gap over such an entry throws std::logic_error.
   bool commitAt(int64_t firstLogIndex, int64_t lastLogIndex, const PeerId& peer);
   void clearPendingTasks();                                                    // :147-156
   bool resetPendingIndex(int64_t newPendingIndex);                             // :167-186
   // :197-215 -- oldConf == nullptr means a stable configuration
   bool appendPendingTask(const Configuration& conf, const Configuration* oldConf,
                          std::function<void(bool)> done = {});
+  // `count` appendPendingTask calls with the same conf and no closures (NodeImpl.
+  // executeApplyingTasks appends its batch of tasks under one conf, NodeImpl.java:1182-1200)
+  bool appendPendingTasks(const Configuration& conf, const Configuration* oldConf, int64_t count);
   bool setLastCommittedIndex(int64_t lastCommittedIndex);                      // :223-248
   int64_t getLastCommittedIndex() const;                                       // :67-79
   int64_t getPendingIndex() const;
@@ -176,17 +183,34 @@ class BallotBox {
   uint32_t g_;
 };
 
-// Engine-backed state of G groups (SoA, include/jrq.h jrq_group_batch layout).
+// What one GroupBatch::flush() moved and how long each part took.
+struct FlushStats {
+  uint32_t states = 0;       // group headers uploaded (96 B each)
+  uint32_t records = 0;      // 8-B update records uploaded (changed acks / queue sizes)
+  uint32_t changed = 0;      // groups whose commit advanced (8-B entries downloaded)
+  uint64_t h2d_bytes = 0, d2h_bytes = 0;
+  double pack_ms = 0, device_ms = 0, deliver_ms = 0;
+};
+
+// BallotBox state of G groups, resident on the GPU (include/jrq.h jrq_table): the host keeps
+// a shadow of what Java's BallotBox holds, records what the API calls change, and flush()
+// ships only those changes (from page-locked buffers), runs one epoch and delivers the
+// commits -- closures, then waiter.onCommitted(index), as BallotBox.commitAt does after
+// unlocking (BallotBox.java:131-137).  Not thread-safe: one host thread per batch.
 class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
  public:
   // eng may be null until the first flush() (host-only state checks need no GPU)
   GroupBatch(Engine* eng, uint32_t groups, uint32_t peers);
+  ~GroupBatch();
+  GroupBatch(const GroupBatch&) = delete;
+  GroupBatch& operator=(const GroupBatch&) = delete;
   uint32_t groups() const { return G_; }
   uint32_t peers() const { return P_; }
-  // One epoch: evaluate every group with a pending queue on the GPU, advance
-  // pendingIndex / lastCommittedIndex, drop committed ballots, call waiters.
+  // One epoch: upload what changed, evaluate every group on the GPU, advance
+  // pendingIndex / lastCommittedIndex, drop committed ballots, run closures, call waiters.
   // Returns the number of groups whose commit index advanced.
   uint32_t flush();
+  const FlushStats& lastFlush() const { return stats_; }
 
  private:
   friend class BallotBox;
@@ -194,22 +218,56 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
     int64_t start;
     uint64_t conf;
   };
-  struct Group {
-    CommitWaiter waiter;
-    bool inited = false;
-    int64_t pendingIndex = 0;
-    int64_t lastCommitted = 0;
-    int64_t lastAppended = -1;  // pendingIndex + queue size - 1
-    std::vector<Run> runs;
-    std::map<PeerId, int> slot;  // PeerId -> peer slot (<= P)
-    std::vector<int64_t> match;  // per slot, highest contiguous ack
-    std::vector<std::function<void(bool)>> closures;
+  struct PeerHash {
+    size_t operator()(const PeerId& p) const {
+      return std::hash<std::string>()(p.ip) ^ (static_cast<size_t>(p.port) << 20) ^
+             (static_cast<size_t>(p.idx) << 40);
+    }
   };
-  int slotOf(Group& g, const PeerId& p, bool create);
-  uint64_t confWord(Group& g, const Configuration& conf, const Configuration* old);
+  template <class T>
+  struct PinnedBuf {  // page-locked host staging (pageable when registration fails)
+    T* p = nullptr;
+    size_t cap = 0;
+    bool registered = false;
+    void reserve(size_t n);
+    void release();
+    ~PinnedBuf() { release(); }
+  };
+  static constexpr uint32_t kNoPeer = 0xFFFFFFFFu;
+  static constexpr uint32_t kDirtyLa = 1u << 16, kDirtyHeader = 1u << 17, kDirtyReset = 1u << 18;
+
+  uint32_t internPeer(const PeerId& p);
+  int slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved = 0);
+  uint32_t liveMask(uint32_t g) const;
+  uint64_t confWord(uint32_t g, const Configuration& conf, const Configuration* old);
+  bool gapCountsPeer(uint32_t g, int slot, int64_t lo, int64_t hi) const;
+  void markDirty(uint32_t g, uint32_t bits) {
+    if (dirty_[g] == 0) dirtyList_.push_back(g);
+    dirty_[g] |= bits;
+  }
+  void commitTo(uint32_t g, int64_t c);
+  void dropDeadRuns(uint32_t g);
+
   Engine* eng_;
   uint32_t G_, P_;
-  std::vector<Group> grp_;
+  std::vector<int64_t> pi_, lc_, la_;     // pendingIndex, lastCommittedIndex, lastAppended
+  std::vector<Run> runs_;                 // [G][JRQ_TABLE_MAX_RUNS] conf runs of the queue
+  std::vector<uint8_t> nruns_;
+  std::vector<uint32_t> slotPeer_;        // [G][P] interned PeerId of each slot
+  std::vector<uint32_t> slotUse_;         // [G][P] flush count of the slot's last ack
+  std::vector<int64_t> match_;            // [G][P] highest acked index per slot
+  std::vector<uint32_t> dirty_;           // [G] slots / lastAppended / header changed
+  std::vector<uint32_t> dirtyList_;
+  std::vector<CommitWaiter> waiter_;
+  std::vector<uint8_t> inited_;
+  // ClosureQueue (ClosureQueueImpl.java): only non-null closures, per group, in index order
+  std::vector<std::unique_ptr<std::deque<std::pair<int64_t, std::function<void(bool)>>>>> closures_;
+  std::unordered_map<PeerId, uint32_t, PeerHash> peerIds_;
+  jrq_table* table_ = nullptr;
+  PinnedBuf<jrq_group_state> states_;
+  PinnedBuf<uint64_t> recs_, changed_;
+  uint32_t flushes_ = 0;
+  FlushStats stats_;
 };
 
 }  // namespace jraft

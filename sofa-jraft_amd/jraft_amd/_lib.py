@@ -46,6 +46,41 @@ class GroupBatch(C.Structure):
     ]
 
 
+TABLE_MAX_RUNS = 4                     # JRQ_TABLE_MAX_RUNS
+TABLE_MAX_GROUPS = 1 << 27             # JRQ_TABLE_MAX_GROUPS
+PI_FOLLOWS_LC = -(1 << 63)             # JRQ_PI_FOLLOWS_LC
+REC_LAST_APPENDED = 16                 # JRQ_REC_LAST_APPENDED
+STATE_RESET_MATCH = 1                  # JRQ_STATE_RESET_MATCH
+
+try:
+    import numpy as _np
+    # jrq_group_state (96 bytes)
+    GROUP_STATE = _np.dtype([("group", "<u4"), ("num_runs", "<u2"), ("flags", "<u2"),
+                             ("pending_index", "<i8"), ("last_appended", "<i8"),
+                             ("last_committed", "<i8"), ("run_conf", "<u8", (TABLE_MAX_RUNS,)),
+                             ("run_start", "<i8", (TABLE_MAX_RUNS,))])
+    assert GROUP_STATE.itemsize == 96
+except ImportError:  # pragma: no cover
+    GROUP_STATE = None
+
+
+class TableView(C.Structure):
+    """jrq_table_view (include/jrq.h)."""
+    _fields_ = [("match", C.c_void_p), ("pending_index", C.c_void_p),
+                ("last_appended", C.c_void_p), ("last_committed", C.c_void_p),
+                ("conf", C.c_void_p), ("ld", C.c_uint64), ("G", C.c_uint32),
+                ("num_peers", C.c_uint32)]
+
+
+def rec(group, field, v):
+    """JRQ_REC(group, field, v) -- vectorised over numpy arrays."""
+    import numpy as np
+    g = np.asarray(group, dtype=np.uint64)
+    f = np.asarray(field, dtype=np.uint64)
+    vv = np.asarray(v, dtype=np.int64).astype(np.uint64) & np.uint64(0xFFFFFFFF)
+    return (vv << np.uint64(32)) | (g << np.uint64(5)) | f
+
+
 # (name, restype, argtypes) for every function declared in include/jrq.h
 _V = C.c_void_p
 SIGNATURES = [
@@ -82,6 +117,15 @@ SIGNATURES = [
     ("jrq_commit_fanout", C.c_int, [_V, C.c_uint32] + [_V] * 9),
     ("jrq_v2_decode_verify_dev", C.c_int, [_V, _V, _V, C.c_uint32] + [_V] * 11),
     ("jrq_v2_decode_verify", C.c_int, [_V, _V, _V, C.c_uint32] + [_V] * 11),
+    ("jrq_table_create", _V, [_V, C.c_uint32, C.c_uint32, C.POINTER(C.c_int)]),
+    ("jrq_table_destroy", None, [_V]),
+    ("jrq_table_update", C.c_int, [_V, _V, C.c_uint32, _V, C.c_uint32]),
+    ("jrq_table_update_dev", C.c_int, [_V, _V, C.c_uint32, _V, C.c_uint32]),
+    ("jrq_table_epoch_dev", C.c_int, [_V, _V, _V, _V]),
+    ("jrq_table_epoch", C.c_int, [_V, _V, _V, _V]),
+    ("jrq_table_read", C.c_int, [_V, _V, _V, _V, _V]),
+    ("jrq_table_copy", C.c_int, [_V, _V]),
+    ("jrq_table_view_get", C.c_int, [_V, C.POINTER(TableView)]),
     ("jrq_rccl_get_unique_id", C.c_int, [_V]),
     ("jrq_rccl_init", C.c_int, [_V, C.c_int, C.c_int, _V]),
     ("jrq_rccl_nranks", C.c_int, [_V]),

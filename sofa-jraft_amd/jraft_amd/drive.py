@@ -1,0 +1,50 @@
+"""ctypes binding of libjraft_drive.so (sofa-jraft_amd/host/jraft_drive.cpp): a multi-Raft
+load driver that replays an epoch series through the C++ host mirror's BallotBox API over
+the resident device table, one GroupBatch::flush() per epoch."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _lib
+
+DRIVE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
+                          "libjraft_drive.so")
+STATS = ("api_ms", "pack_ms", "device_ms", "deliver_ms", "flush_ms", "h2d_bytes", "d2h_bytes",
+         "states", "records", "changed", "api_calls")
+_drv = None
+
+
+def load():
+    global _drv
+    if _drv is None:
+        _lib.load()  # torch's HIP runtime first (see _lib.load)
+        if not os.path.exists(DRIVE_PATH):
+            raise FileNotFoundError(f"{DRIVE_PATH} missing: run `make -C sofa-jraft_amd`")
+        d = C.CDLL(DRIVE_PATH)
+        d.jraft_drive_last_error.restype = C.c_char_p
+        d.jraft_drive_epochs.restype = C.c_int
+        d.jraft_drive_epochs.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32] + [C.c_void_p] * 9
+        _drv = d
+    return _drv
+
+
+def drive_epochs(device: int, s: dict):
+    """Replay series `s` (workloads.host_series) through BallotBox; returns (committed [K][G]
+    after each flush, stats dict of per-epoch arrays named by STATS)."""
+    d = load()
+    K, P, G = s["match"].shape
+    arrs = {k: np.ascontiguousarray(s[k]) for k in ("pending_index", "last_committed", "conf_a",
+                                                    "conf_b", "switch_at", "last_appended",
+                                                    "match")}
+    out = np.zeros((K, G), np.int64)
+    stats = np.zeros((K, len(STATS)), np.float64)
+    ptr = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+    rc = d.jraft_drive_epochs(device, G, P, K, ptr(arrs["pending_index"]), ptr(arrs["last_committed"]),
+                              ptr(arrs["conf_a"]), ptr(arrs["conf_b"]), ptr(arrs["switch_at"]),
+                              ptr(arrs["last_appended"]), ptr(arrs["match"]), ptr(out), ptr(stats))
+    if rc != 0:
+        raise RuntimeError("jraft_drive_epochs: " + (d.jraft_drive_last_error() or b"").decode())
+    return out, {k: stats[:, i] for i, k in enumerate(STATS)}

@@ -12,7 +12,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import GroupBatch, check
+from ._lib import GROUP_STATE, GroupBatch, TableView, check
 
 
 def _np_ptr(a):
@@ -344,3 +344,89 @@ class Engine:
     def publish_committed_dev(self, local, global_out):
         check(self._L.jrq_publish_committed_dev(self._h, _dev_ptr(local), _dev_ptr(global_out),
                                                 local.shape[0]), self._h)
+
+
+class Table:
+    """A resident group table (include/jrq.h jrq_table) on an Engine's device: the BallotBox
+    state of G groups x P peer slots kept in HBM, incremental updates, epochs that return only
+    the groups whose commit advanced."""
+
+    def __init__(self, engine: Engine, G: int, num_peers: int):
+        self._eng = engine
+        self._L = engine._L
+        err = C.c_int(0)
+        h = self._L.jrq_table_create(engine.handle, G, num_peers, C.byref(err))
+        if not h:
+            raise _lib.JrqError(err.value, (self._L.jrq_last_error(engine.handle) or b"").decode())
+        self._h = C.c_void_p(h)
+        self.G, self.P = G, num_peers
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.jrq_table_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def states(n: int) -> np.ndarray:
+        """A zeroed array of n jrq_group_state records."""
+        return np.zeros(n, dtype=GROUP_STATE)
+
+    def update(self, states=None, recs=None):
+        """Host variant: states (GROUP_STATE array) then recs (uint64 JRQ_REC words)."""
+        st = None if states is None else np.ascontiguousarray(states, dtype=GROUP_STATE)
+        rc = None if recs is None else np.ascontiguousarray(recs, dtype=np.uint64)
+        check(self._L.jrq_table_update(self._h, _np_ptr(st), 0 if st is None else len(st),
+                                       _np_ptr(rc), 0 if rc is None else len(rc)), self._eng.handle)
+        # the host buffers must outlive the asynchronous copies: keep them until the next epoch
+        self._keep = (st, rc)
+
+    def update_dev(self, states=None, recs=None, n_states=None, n_recs=None):
+        ns = 0 if states is None else (states.numel() // 96 if n_states is None else n_states)
+        nr = 0 if recs is None else (recs.numel() if n_recs is None else n_recs)
+        check(self._L.jrq_table_update_dev(self._h, _dev_ptr(states), ns, _dev_ptr(recs), nr),
+              self._eng.handle)
+
+    def epoch(self, status: bool = False):
+        """Host variant: returns (changed uint64[n] as JRQ words, status uint8[G] or None)."""
+        out = np.zeros(max(self.G, 1), np.uint64)
+        n = C.c_uint32(0)
+        st = np.zeros(self.G, np.uint8) if status else None
+        check(self._L.jrq_table_epoch(self._h, _np_ptr(out), C.byref(n), _np_ptr(st)),
+              self._eng.handle)
+        self._keep = None
+        return out[: n.value].copy(), st
+
+    def epoch_dev(self, changed_out, n_changed_out, status_out=None):
+        check(self._L.jrq_table_epoch_dev(self._h, _dev_ptr(changed_out), _dev_ptr(n_changed_out),
+                                          _dev_ptr(status_out)), self._eng.handle)
+
+    def read(self) -> dict:
+        G, P = self.G, self.P
+        o = dict(pending_index=np.zeros(G, np.int64), last_appended=np.zeros(G, np.int64),
+                 last_committed=np.zeros(G, np.int64), match=np.zeros((P, G), np.int64))
+        check(self._L.jrq_table_read(self._h, _np_ptr(o["pending_index"]),
+                                     _np_ptr(o["last_appended"]), _np_ptr(o["last_committed"]),
+                                     _np_ptr(o["match"])), self._eng.handle)
+        return o
+
+    def copy_from(self, src: "Table"):
+        """Device-side copy of src's whole state (same shape), on this engine's stream."""
+        check(self._L.jrq_table_copy(self._h, src._h), self._eng.handle)
+
+    def view(self) -> TableView:
+        v = TableView()
+        check(self._L.jrq_table_view_get(self._h, C.byref(v)), self._eng.handle)
+        return v
+
+
+def decode_changed(words) -> tuple[np.ndarray, np.ndarray]:
+    """(group uint32[n], delta int64[n]) of jrq_table_epoch's output words: the group's new
+    lastCommittedIndex = its pendingIndex before the epoch - 1 + delta."""
+    w = np.asarray(words, dtype=np.uint64)
+    return (w & np.uint64(0xFFFFFFFF)).astype(np.uint32), (w >> np.uint64(32)).astype(np.int64)

@@ -180,3 +180,48 @@ def quorum_epoch_series(cfg: str, K: int, groups: int | None = None, step: int =
         match[k, 0] = la[k]  # the leader's own stable ack
     return dict(match=match, last_appended=la, pending_index=b["pending_index"],
                 last_committed=b["last_committed"], conf=b["conf"])
+
+
+def host_series(cfg: str, K: int, groups: int | None = None, joint_frac: float = 0.01,
+                active: float = 1.0, step: int = 16, seed: int | None = None):
+    """An epoch series for the host-mirror driver (jraft_amd.drive): quorum_epoch_series plus
+    (a) a conf change inside the pending window of `joint_frac` of the groups -- entries from
+    switch_at[g] on are under conf_b = the stable new conf (NodeImpl's STAGE_STABLE entry after
+    the joint one), the earlier ones under conf_a = the group's joint conf -- and (b) per
+    epoch only an `active` fraction of the groups gets new entries and acks.  Also returns the
+    run table (run_off / run_start / run_conf, conf flagged CONF_RUNS) of the same batch for
+    the stateless kernels and the oracle."""
+    from ._lib import CONF_RUNS
+    s = quorum_epoch_series(cfg, K, groups=groups, step=step, seed=seed)
+    P, G = s["match"].shape[1], s["match"].shape[2]
+    sd = (SEED_BASE ^ 0xC0) if seed is None else seed ^ 0xC0
+    r = splitmix64(sd, G, 1)
+    joint = (r % np.uint64(1_000_000)).astype(np.float64) / 1e6 < joint_frac
+    pend = s["last_appended"][0] - s["pending_index"] + 1
+    off = 1 + (splitmix64(sd, G, 2) % np.maximum(pend - 1, 1).astype(np.uint64)).astype(np.int64)
+    switch_at = np.where(joint, s["pending_index"] + off, 0).astype(np.int64)
+    conf_a = s["conf"].astype(np.uint64)
+    conf_b = np.full(G, conf_word((1 << P) - 1), np.uint64)
+    if active < 1.0:
+        la, m = s["last_appended"], s["match"]
+        for k in range(1, K):
+            idle = (splitmix64(sd + k, G, 3) % np.uint64(1_000_000)).astype(np.float64) / 1e6 >= active
+            # held at epoch k-1's values; later epochs stay non-decreasing (each was drawn
+            # at or above the original epoch k)
+            la[k, idle] = la[k - 1, idle]
+            m[k][:, idle] = m[k - 1][:, idle]
+    nruns = np.where(joint, 2, 1)
+    run_off = np.zeros(G + 1, np.uint32)
+    run_off[1:] = np.cumsum(nruns)
+    run_start = np.zeros(int(run_off[-1]), np.int64)
+    run_conf = np.zeros(int(run_off[-1]), np.uint64)
+    run_start[run_off[:-1]] = 0
+    run_conf[run_off[:-1]] = conf_a
+    jr = np.nonzero(joint)[0]
+    run_start[run_off[jr] + 1] = switch_at[jr]
+    run_conf[run_off[jr] + 1] = conf_b[jr]
+    conf = np.where(joint, conf_a | np.uint64(CONF_RUNS), conf_a).astype(np.uint64)
+    return dict(match=s["match"], last_appended=s["last_appended"], pending_index=s["pending_index"],
+                last_committed=s["last_committed"], conf_a=conf_a, conf_b=conf_b,
+                switch_at=switch_at, conf=conf, run_off=run_off, run_start=run_start,
+                run_conf=run_conf)

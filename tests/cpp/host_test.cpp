@@ -2,6 +2,8 @@
 // mirror (sofa-jraft_amd/host) over libjrq.so.  Run by tests/test_host_cpp.py:
 //   host_test cpu   -> tests that need no GPU (synchronous BallotBox semantics)
 //   host_test gpu   -> everything, decisions and checksums computed on the GPU
+// The differential tests replay the same calls through the oracle's Java-faithful BallotBox
+// (oracle/jraft_oracle.c, test infrastructure) and compare the state after every flush.
 // Sources restated (jraft-core/src/test/java/com/alipay/sofa/jraft/...):
 //   core/BallotBoxTest.java:62-154, entity/BallotTest.java:37-50,
 //   entity/LogEntryTest.java:95-125, util/CrcUtilTest.java:27-42
@@ -12,6 +14,10 @@
 #include <string>
 #include <vector>
 
+#include <random>
+#include <set>
+
+#include "../../oracle/jraft_oracle.h"
 #include "../../sofa-jraft_amd/host/jraft_host.h"
 
 using namespace jraft;
@@ -290,6 +296,175 @@ static void testCRC64ChecksumOnGpu(Engine& eng) {
   CHECK(d.getValue() == CrcUtil::crc64(eng, big));
 }
 
+// ------------------------------------------------------- differential tests
+
+// One group driven identically through the host mirror and the oracle's BallotBox; peers are
+// PeerId("p", id) on the mirror side and `id` on the oracle side.
+struct Twin {
+  BallotBox box;
+  jo_ballot_box* bb;
+  Waiter w;
+  Twin(std::shared_ptr<GroupBatch> b, uint32_t g) : box(std::move(b), g), bb(jo_bb_new()) {
+    box.init({w.fn()});
+  }
+  Twin(Twin&& o) noexcept : box(o.box), bb(o.bb), w(std::move(o.w)) {
+    o.bb = nullptr;
+    box.init({w.fn()});
+  }
+  ~Twin() {
+    if (bb) jo_bb_free(bb);
+  }
+  static Configuration confOf(const std::vector<int32_t>& ids) {
+    Configuration c;
+    for (int32_t i : ids) c.peers.emplace_back("p", i);
+    return c;
+  }
+  bool append(const std::vector<int32_t>& cur, const std::vector<int32_t>* old, int64_t n) {
+    const Configuration c = confOf(cur);
+    const Configuration o = old ? confOf(*old) : Configuration();
+    bool ok = true;
+    for (int64_t i = 0; i < n; ++i) {
+      ok = box.appendPendingTask(c, old ? &o : nullptr) && ok;
+      jo_bb_append_pending_task(bb, cur.data(), (int32_t)cur.size(), old ? old->data() : nullptr,
+                                old ? (int32_t)old->size() : -1);
+    }
+    return ok;
+  }
+  void ack(int64_t first, int64_t last, int32_t peer) {
+    box.commitAt(first, last, PeerId("p", peer));
+    jo_bb_commit_at(bb, first, last, peer);
+  }
+  bool same() const {
+    return box.getLastCommittedIndex() == jo_bb_last_committed_index(bb) &&
+           box.getPendingIndex() == jo_bb_pending_index(bb) &&
+           box.getPendingMetaQueueSize() == jo_bb_queue_size(bb) &&
+           (w.calls.empty() ? jo_bb_on_committed_calls(bb) == 0
+                            : w.calls.back() == jo_bb_on_committed_last(bb));
+  }
+};
+
+static void testAddPeerCatchUpOnGpu(Engine& eng) {
+  // A peer being added is acked by its catch-up replicator before any conf names it
+  // (Replicator.java:1387-1392); the joint conf entry then counts it, and its next, contiguous
+  // ack must be accepted (pendingIndex 100, the new peer caught up to 105, joint conf at 111).
+  auto batch = std::make_shared<GroupBatch>(&eng, 1, 8);
+  Twin t(batch, 0);
+  CHECK(t.box.resetPendingIndex(100) && jo_bb_reset_pending_index(t.bb, 100) == JO_TRUE);
+  const std::vector<int32_t> c3 = {1, 2, 3}, c4 = {1, 2, 3, 4};
+  CHECK(t.append(c3, nullptr, 11));  // 100..110
+  t.ack(100, 105, 4);                // not in any conf yet
+  CHECK(t.append(c4, &c3, 1));       // 111: joint {1,2,3,4} / {1,2,3}
+  t.ack(106, 111, 4);
+  t.ack(100, 111, 1);
+  t.ack(100, 108, 2);
+  batch->flush();
+  CHECK(t.same());
+  CHECK(t.box.getLastCommittedIndex() == 108);  // 111 needs 3 of 4 and 2 of 3: {1, 4} only
+  t.ack(109, 111, 2);
+  batch->flush();
+  CHECK(t.same() && t.box.getLastCommittedIndex() == 111);
+}
+
+// Random call sequences (appends under stable and joint confs, conf changes that replace
+// peers, contiguous acks from members and catch-up peers, step-downs and new terms) through
+// the mirror and the oracle; the state must agree after every flush.  More distinct peers
+// than slots pass through each group over time, so slots are recycled.
+static void testRandomDifferentialOnGpu(Engine& eng) {
+  const uint32_t G = 96, P = 8;
+  auto batch = std::make_shared<GroupBatch>(&eng, G, P);
+  std::vector<Twin> tw;
+  tw.reserve(G);
+  std::mt19937_64 rng(20240611);
+  auto R = [&](int64_t n) { return static_cast<int64_t>(rng() % static_cast<uint64_t>(n)); };
+  struct S {
+    std::vector<int32_t> cur, old;
+    bool joint = false;
+    std::map<int32_t, int64_t> m;  // peer -> highest acked index (the Replicator's view)
+    int64_t la = 0;
+  };
+  std::vector<S> st(G);
+  auto pickConf = [&](std::vector<int32_t> keep) {
+    std::set<int32_t> s(keep.begin(), keep.end());
+    const size_t n = 1 + R(3);
+    while (s.size() < n) s.insert(1 + static_cast<int32_t>(R(12)));
+    while (s.size() > n) s.erase(std::next(s.begin(), R(s.size())));
+    return std::vector<int32_t>(s.begin(), s.end());
+  };
+  for (uint32_t g = 0; g < G; ++g) {
+    tw.emplace_back(batch, g);
+    Twin& t = tw.back();
+    const int64_t lc = R(50);
+    t.box.setLastCommittedIndex(lc);
+    jo_bb_set_last_committed_index(t.bb, lc);
+    const int64_t pi = lc + 1 + R(5);
+    CHECK(t.box.resetPendingIndex(pi) && jo_bb_reset_pending_index(t.bb, pi) == JO_TRUE);
+    st[g].cur = pickConf({});
+    st[g].la = pi - 1;
+    for (int32_t p = 1; p <= 12; ++p) st[g].m[p] = pi - 1 - R(3);
+  }
+  int flushes = 0;
+  for (int step = 0; step < 6000; ++step) {
+    const uint32_t g = static_cast<uint32_t>(R(G));
+    Twin& t = tw[g];
+    S& s = st[g];
+    const int64_t a = R(100);
+    if (t.box.getPendingIndex() == 0) {  // stepped down: a new term later
+      if (a < 20) {
+        const int64_t pi = std::max(s.la + 1, t.box.getLastCommittedIndex() + 1) + R(3);
+        CHECK(t.box.resetPendingIndex(pi) && jo_bb_reset_pending_index(t.bb, pi) == JO_TRUE);
+        s.la = pi - 1;
+        s.joint = false;
+        for (auto& kv : s.m) kv.second = pi - 1 - R(3);
+      }
+    } else if (a < 35) {  // appendPendingTask x k under the current conf
+      const int64_t k = 1 + R(4);
+      CHECK(t.append(s.cur, s.joint ? &s.old : nullptr, k));
+      s.la += k;
+    } else if (a < 40) {  // conf change: stable -> joint (replacing peers), joint -> stable
+      if (!s.joint) {
+        s.old = s.cur;
+        s.cur = pickConf(std::vector<int32_t>(s.old.begin(), s.old.begin() + R(s.old.size() + 1)));
+        s.joint = true;
+      } else {
+        s.joint = false;
+      }
+      CHECK(t.append(s.cur, s.joint ? &s.old : nullptr, 1));
+      s.la += 1;
+    } else if (a < 94) {  // an ack, contiguous per peer: members mostly, any peer sometimes
+      int32_t p;
+      if (R(10) < 8) {
+        const auto& pool = (s.joint && R(2)) ? s.old : s.cur;
+        p = pool[R(pool.size())];
+      } else {
+        p = 1 + static_cast<int32_t>(R(12));
+      }
+      const int64_t first = s.m[p] + 1;
+      const int64_t last = std::min(s.la, first + R(6));
+      if (last >= first) {
+        t.ack(first, last, p);
+        s.m[p] = last;
+      }
+    } else if (a < 96) {  // the leader steps down
+      t.box.clearPendingTasks();
+      jo_bb_clear_pending_tasks(t.bb);
+    } else {
+      batch->flush();
+      ++flushes;
+      for (uint32_t h = 0; h < G; ++h) {
+        if (!tw[h].same()) {
+          std::fprintf(stderr, "  group %u: mirror lc %lld pi %lld q %lld | oracle lc %lld pi %lld q %lld\n", h,
+                       (long long)tw[h].box.getLastCommittedIndex(), (long long)tw[h].box.getPendingIndex(),
+                       (long long)tw[h].box.getPendingMetaQueueSize(),
+                       (long long)jo_bb_last_committed_index(tw[h].bb), (long long)jo_bb_pending_index(tw[h].bb),
+                       (long long)jo_bb_queue_size(tw[h].bb));
+          CHECK(false);
+        }
+      }
+    }
+  }
+  CHECK(flushes > 10);
+}
+
 int main(int argc, char** argv) {
   const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
   struct T {
@@ -312,6 +487,8 @@ int main(int argc, char** argv) {
     eng.reset(new Engine(0));
     Engine& e = *eng;
     tests.push_back({"testCommitAtOnGpu", [&] { testCommitAtOnGpu(e); }});
+    tests.push_back({"testAddPeerCatchUpOnGpu", [&] { testAddPeerCatchUpOnGpu(e); }});
+    tests.push_back({"testRandomDifferentialOnGpu", [&] { testRandomDifferentialOnGpu(e); }});
     tests.push_back({"testBallotGrantOnGpu", [&] { testBallotGrantOnGpu(e); }});
     tests.push_back({"testManyGroupsJointConsensusOnGpu", [&] { testManyGroupsJointConsensusOnGpu(e); }});
     tests.push_back({"testLogEntryChecksumOnGpu", [&] { testLogEntryChecksumOnGpu(e); }});

@@ -1,0 +1,192 @@
+"""GPU parity of the resident group table (include/jrq.h jrq_table, csrc/table.hip) against the
+oracle's Java-faithful BallotBox replays (jraft-core/.../core/BallotBox.java:96-248).
+
+The table is loaded the way a host drives it: group headers for resetPendingIndex / conf runs,
+8-byte records for commitAt acks and appendPendingTask queue growth (values relative to the
+group's pendingIndex), then epochs that return only the groups whose commit advanced.
+"""
+import numpy as np
+import pytest
+
+from jraft_amd import JrqError, Table, decode_changed
+from jraft_amd import _lib
+from quorum_cases import random_batch, random_series, series_replay
+
+pytestmark = pytest.mark.gpu
+
+
+def states_of(b, groups=None):
+    """jrq_group_state records of a random_batch / random_series dict (runs from its CSR)."""
+    G = len(b["pending_index"])
+    groups = np.arange(G) if groups is None else groups
+    st = Table.states(len(groups))
+    ro = b["run_off"]
+    for i, g in enumerate(groups):
+        r0, r1 = int(ro[g]), int(ro[g + 1])
+        st[i]["group"] = g
+        st[i]["num_runs"] = r1 - r0
+        st[i]["flags"] = _lib.STATE_RESET_MATCH
+        st[i]["pending_index"] = b["pending_index"][g]
+        la = b["last_appended"]
+        st[i]["last_appended"] = la[g] if la.ndim == 1 else la[0][g]
+        st[i]["last_committed"] = b["last_committed"][g]
+        st[i]["run_conf"][: r1 - r0] = b["run_conf"][r0:r1]
+        st[i]["run_start"][: r1 - r0] = b["run_start"][r0:r1]
+    return st
+
+
+def match_recs(match, pi, groups=None):
+    """Records setting every slot's match (relative to pendingIndex; below it = 0)."""
+    P, G = match.shape
+    gs = np.arange(G) if groups is None else np.asarray(groups)
+    lead = pi[gs] != 0
+    gs = gs[lead]
+    out = []
+    for p in range(P):
+        v = np.maximum(match[p, gs] - (pi[gs] - 1), 0)
+        out.append(_lib.rec(gs, p, v))
+    return np.concatenate(out) if out else np.zeros(0, np.uint64)
+
+
+def la_recs(la, pi, groups):
+    gs = np.asarray(groups)
+    gs = gs[pi[gs] != 0]
+    return _lib.rec(gs, _lib.REC_LAST_APPENDED, la[gs] - (pi[gs] - 1))
+
+
+def committed_from(changed, pi_before, lc_before):
+    g, d = decode_changed(changed)
+    out = lc_before.copy()
+    assert len(np.unique(g)) == len(g), "a group listed twice"
+    out[g] = pi_before[g] - 1 + d
+    return out, g
+
+
+@pytest.mark.parametrize("P,G", [(5, 4096), (3, 3001), (16, 777), (1, 64)])
+def test_one_epoch_vs_replay(engine, oracle, P, G):
+    b = random_batch(1000 + P, G, P, run_prob=0.4)
+    ce, se, _ = oracle.quorum_epoch_replay(b["match"], b["pending_index"], b["last_appended"],
+                                           b["last_committed"], b["conf"], b["run_off"],
+                                           b["run_start"], b["run_conf"], chunk=7)
+    t = Table(engine, G, P)
+    t.update(states_of(b), match_recs(b["match"], b["pending_index"]))
+    changed, st = t.epoch(status=True)
+    got, listed = committed_from(changed, b["pending_index"], b["last_committed"])
+    np.testing.assert_array_equal(got, ce)
+    np.testing.assert_array_equal(np.sort(listed), np.nonzero(ce > b["last_committed"])[0])
+    np.testing.assert_array_equal(st, se)
+    # the state moved as BallotBox moves it (pendingIndex = commit + 1, read through the
+    # JRQ_PI_FOLLOWS_LC word), and a second epoch with no new acks commits nothing
+    r = t.read()
+    np.testing.assert_array_equal(r["last_committed"], ce)
+    moved = ce > b["last_committed"]
+    np.testing.assert_array_equal(r["pending_index"][moved], ce[moved] + 1)
+    np.testing.assert_array_equal(r["pending_index"][~moved], b["pending_index"][~moved])
+    again, _ = t.epoch()
+    assert len(again) == 0
+    t.close()
+
+
+@pytest.mark.parametrize("P,G,K", [(3, 2000, 6), (5, 1500, 5)])
+def test_epochs_incremental_vs_replays(engine, oracle, P, G, K):
+    """K epochs driven incrementally -- per epoch only the queue sizes and the acks that
+    changed -- equal K sequential BallotBox replays with carried state."""
+    s = random_series(77 + P, G, P, K)
+    ce, se = series_replay(oracle, s)
+    t = Table(engine, G, P)
+    pi = s["pending_index"].copy()
+    lc = s["last_committed"].copy()
+    t.update(states_of(s), match_recs(s["match"][0], pi))
+    for k in range(K):
+        if k > 0:
+            la_changed = np.nonzero(s["last_appended"][k] != s["last_appended"][k - 1])[0]
+            recs = [la_recs(s["last_appended"][k], pi, la_changed)]
+            for p in range(P):
+                ch = np.nonzero(s["match"][k, p] != s["match"][k - 1, p])[0]
+                ch = ch[pi[ch] != 0]
+                recs.append(_lib.rec(ch, p, np.maximum(s["match"][k, p, ch] - (pi[ch] - 1), 0)))
+            t.update(None, np.concatenate(recs))
+        changed, st = t.epoch(status=True)
+        got, listed = committed_from(changed, pi, lc)
+        np.testing.assert_array_equal(got, ce[k], err_msg=f"epoch {k}")
+        np.testing.assert_array_equal(st, se[k], err_msg=f"epoch {k}")
+        pi[listed] = got[listed] + 1
+        lc = got
+    t.close()
+
+
+def test_group_state_resets_and_clears(engine, oracle):
+    """resetPendingIndex with RESET_MATCH wipes old acks; clearPendingTasks (pendingIndex 0)
+    stops commits; records are relative to the pendingIndex the headers just set."""
+    from jraft_amd import conf_word
+    G = 256
+    b = random_batch(5, G, 3, run_prob=0.0, edge=False)
+    t = Table(engine, G, 3)
+    t.update(states_of(b), match_recs(b["match"], b["pending_index"]))
+    t.epoch()
+    st = states_of(b)
+    st["pending_index"] = b["pending_index"] + 5000
+    st["last_appended"] = st["pending_index"] + 9  # 10 entries pending
+    st["last_committed"] = b["pending_index"] + 4000
+    st["num_runs"] = 1
+    st["run_conf"][:, 0] = conf_word(0b111)
+    t.update(st)
+    changed, _ = t.epoch()
+    assert len(changed) == 0  # every match was reset below the new pendingIndex
+    clr = states_of(b, groups=[0, 1])
+    clr["pending_index"] = 0
+    clr["num_runs"] = 0
+    gs = np.arange(G)
+    t.update(clr, np.concatenate([_lib.rec(gs[2:], 0, 10), _lib.rec(gs[2:], 1, 7)]))
+    changed, stt = t.epoch(status=True)
+    g, d = decode_changed(changed)
+    assert sorted(g.tolist()) == list(range(2, G))
+    assert (d == 7).all()  # quorum 2 of 3: the 7th pending entry
+    assert (stt[:2] == _lib.ST_NOT_LEADER).all()
+    r = t.read()
+    np.testing.assert_array_equal(r["last_committed"][2:], st["pending_index"][2:] + 6)
+    t.close()
+
+
+def test_invalid_records_rejected(engine):
+    t = Table(engine, 100, 3)
+    for bad in (_lib.rec(100, 0, 1), _lib.rec(5, 3, 1), _lib.rec(5, 17, 1)):
+        with pytest.raises(JrqError):
+            t.update(None, np.atleast_1d(bad))
+    st = Table.states(1)
+    st["group"] = 100
+    with pytest.raises(JrqError):
+        t.update(st)
+    st["group"] = 1
+    st["num_runs"] = 5
+    with pytest.raises(JrqError):
+        t.update(st)
+    t.close()
+
+
+def test_device_variant_and_view(engine, oracle):
+    """The _dev entry points on torch buffers, and the view's lastCommitted row (the rank's
+    all-gather send buffer)."""
+    import torch
+    G, P = 2048, 5
+    b = random_batch(9, G, P, run_prob=0.1)
+    ce, _, _ = oracle.quorum_epoch_replay(b["match"], b["pending_index"], b["last_appended"],
+                                          b["last_committed"], b["conf"], b["run_off"],
+                                          b["run_start"], b["run_conf"], chunk=3)
+    t = Table(engine, G, P)
+    dev = torch.device("cuda:0")
+    st = torch.from_numpy(states_of(b).view(np.uint8)).to(dev)
+    rc = torch.from_numpy(match_recs(b["match"], b["pending_index"]).view(np.int64)).to(dev)
+    t.update_dev(st, rc)
+    out = torch.empty(G, dtype=torch.int64, device=dev)
+    n = torch.zeros(1, dtype=torch.int32, device=dev)
+    t.epoch_dev(out, n)
+    engine.synchronize()
+    cnt = int(n.item())
+    got, _ = committed_from(out[:cnt].cpu().numpy().view(np.uint64), b["pending_index"],
+                            b["last_committed"])
+    np.testing.assert_array_equal(got, ce)
+    v = t.view()
+    assert v.G == G and v.num_peers == P and v.ld >= G and v.last_committed
+    np.testing.assert_array_equal(t.read()["last_committed"], ce)
+    t.close()

@@ -6,12 +6,12 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BIN = os.path.join(ROOT, "sofa-jraft_amd", "lib", "host_test")
+BIN = os.path.join(ROOT, "tests", "_build", "host_test")
 
 
 def _run(mode):
     if not os.path.exists(BIN):
-        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "sofa-jraft_amd")])
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")])
     r = subprocess.run([BIN, mode], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     return r.stdout
@@ -25,4 +25,5 @@ def test_host_mirror_cpu_semantics():
 @pytest.mark.gpu
 def test_host_mirror_on_gpu():
     out = _run("gpu")
-    assert "testManyGroupsJointConsensusOnGpu" in out and "0 failed" in out
+    assert "testManyGroupsJointConsensusOnGpu" in out and "testRandomDifferentialOnGpu" in out
+    assert "0 failed" in out

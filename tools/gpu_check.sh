@@ -20,6 +20,7 @@ for s in $STEPS; do
     crc)   run crc_tests 600 python -m pytest tests/test_gpu_crc.py -q -x -p no:cacheprovider --timeout 300 ;;
     quorum) run quorum_tests 600 python -m pytest tests/test_gpu_quorum.py -q -x -p no:cacheprovider --timeout 300 ;;
     quick) run bench_quick 600 python bench.py --steps 20 --warmup 3 --no-cpu ;;
+    legs)  run bench_legs 600 python bench.py --steps 20 --warmup 3 --no-cpu --legs ${BENCH_LEGS:-quorum,table,drive,C2} ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu ;;
@@ -30,7 +31,7 @@ for s in $STEPS; do
                run pmc_${leg}_$c 180 rocprofv3 --kernel-trace --pmc $c -d gpurun_out/pmc_${leg}_$c -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs $leg
              done
            done ;;
-    host)  run host_test 300 ./sofa-jraft_amd/lib/host_test gpu ;;
+    host)  run host_test 300 ./tests/_build/host_test gpu ;;
     probe) run mem_probe 300 ./tools/mem_probe ;;
     sweep) run crc_sweep 600 python tools/crc_sweep.py ${SWEEP_VARIANTS:-} ;;
   esac
