@@ -191,7 +191,7 @@ typedef struct {
     uint32_t group;
     uint16_t num_runs;       /* 0..JRQ_TABLE_MAX_RUNS */
     uint16_t flags;          /* JRQ_STATE_RESET_MATCH: every slot's match = pendingIndex - 1 */
-    int64_t pending_index;   /* 0 = not the leader */
+    int64_t pending_index;   /* 0 = not the leader; JRQ_PI_FOLLOWS_LC = last_committed + 1 */
     int64_t last_appended;   /* pendingIndex + pendingMetaQueue.size() - 1 */
     int64_t last_committed;
     uint64_t run_conf[JRQ_TABLE_MAX_RUNS];  /* JRQ_CONF words */

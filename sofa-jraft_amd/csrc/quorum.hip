@@ -55,20 +55,6 @@ __device__ __forceinline__ void decide_runs(const JrqQuorumArgs& a, uint32_t g, 
   st_out = st;
 }
 
-// The run path of the pair kernel: reloads the group (L2 / HBM, flagged groups only) so that
-// no register of the fast path stays live across it (occupancy of the common case).
-template <int P>
-__device__ __forceinline__ void redecide_runs(const JrqQuorumArgs& a, uint32_t g) {
-  int64_t m[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
-  int64_t out;
-  uint8_t st;
-  decide_runs<P>(a, g, a.pending_index[g], a.last_appended[g], a.last_committed[g], m, out, st);
-  a.committed[g] = out;
-  a.status[g] = st;
-}
-
 template <int P>
 __device__ __forceinline__ void decide(const JrqQuorumArgs& a, uint32_t g, int64_t pi, int64_t la,
                                        int64_t lc, uint64_t cw, int64_t (&m)[P], int64_t& out,
@@ -110,14 +96,17 @@ __device__ __forceinline__ i64x2 ld2nt(const int64_t* p) {
 // Fast path (16-B aligned arrays, even match_ld): one lane decides two adjacent groups; every
 // stream is read with 16-byte non-temporal loads (1 KiB per wave instruction; each input is
 // read once per epoch, so it is not kept in L2 / MALL) and the two status bytes are stored as
-// one 16-bit word.  A group flagged JRQ_CONF_RUNS (joint consensus with a conf change in its
-// pending window) walks its runs in place: only that lane's wave waits on the run table.
+// one 16-bit word.  A group flagged JRQ_CONF_RUNS (a conf change inside its pending window) is
+// deferred to the workgroup's second phase, where one lane per deferred group walks its runs:
+// the run walk then shares no registers with the fast path (occupancy of the common case).
 template <int P>
 __global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
-  // one pair per lane, no grid-stride loop: the rare run path at the end then shares the
-  // register budget with nothing (the launcher sizes the grid to G / 512 workgroups)
+  __shared__ uint32_t n_deferred;
+  __shared__ uint32_t deferred[512];
   const uint32_t pairs = a.G >> 1;
   const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  if (threadIdx.x == 0) n_deferred = 0;
+  __syncthreads();
   if (t < pairs) {
     const uint32_t g = t << 1;
     const i64x2 pi = ld2nt(a.pending_index + g);
@@ -127,30 +116,52 @@ __global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a)
     i64x2 m[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) m[p] = ld2nt(a.match + static_cast<size_t>(p) * a.match_ld + g);
+    const bool runs = a.run_off != nullptr;
+    const bool f0 = runs && (static_cast<uint64_t>(cw.x) & kConfRuns);
+    const bool f1 = runs && (static_cast<uint64_t>(cw.y) & kConfRuns);
     int64_t m0[P], m1[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) {
       m0[p] = m[p].x;
       m1[p] = m[p].y;
     }
-    const uint32_t flags = static_cast<uint32_t>(static_cast<uint64_t>(cw.x) >> 63) |
-                           (static_cast<uint32_t>(static_cast<uint64_t>(cw.y) >> 63) << 1);
     int64_t o0, o1;
     uint8_t s0, s1;
     decide_single<P>(pi.x, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
     decide_single<P>(pi.y, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
-    i64x2 out;
-    out.x = o0;
-    out.y = o1;
-    __builtin_nontemporal_store(out, reinterpret_cast<i64x2*>(a.committed + g));
-    __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
-                                reinterpret_cast<uint16_t*>(a.status + g));
-    // rare: a flagged group is re-decided from its runs and its outputs rewritten (same lane,
-    // same addresses: program order), so nothing of the fast path stays live across this
-    if (a.run_off != nullptr && flags != 0) {
-      if (flags & 1u) redecide_runs<P>(a, g);
-      if (flags & 2u) redecide_runs<P>(a, g + 1);
+    if (!f0 && !f1) {
+      i64x2 out;
+      out.x = o0;
+      out.y = o1;
+      __builtin_nontemporal_store(out, reinterpret_cast<i64x2*>(a.committed + g));
+      __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
+                                  reinterpret_cast<uint16_t*>(a.status + g));
+    } else {  // rare: a deferred group's outputs are written by the second phase only
+      if (!f0) {
+        a.committed[g] = o0;
+        a.status[g] = s0;
+      } else {
+        deferred[atomicAdd(&n_deferred, 1u)] = g;
+      }
+      if (!f1) {
+        a.committed[g + 1] = o1;
+        a.status[g + 1] = s1;
+      } else {
+        deferred[atomicAdd(&n_deferred, 1u)] = g + 1;
+      }
     }
+  }
+  __syncthreads();
+  if (threadIdx.x < n_deferred) {
+    const uint32_t g = deferred[threadIdx.x];
+    int64_t m[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
+    int64_t out;
+    uint8_t st;
+    decide_runs<P>(a, g, a.pending_index[g], a.last_appended[g], a.last_committed[g], m, out, st);
+    a.committed[g] = out;
+    a.status[g] = st;
   }
   // odd G: the last group goes through the scalar decision
   if ((a.G & 1u) && t == 0) {

@@ -39,34 +39,24 @@ struct TableRuns {
   }
 };
 
-// The run path (flagged groups only): reloads the group so that no register of the fast path
-// stays live across it.
-template <int P>
-__device__ __forceinline__ void table_redecide(const JrqTableArgs& t, uint32_t g, int64_t& out,
-                                               uint8_t& st) {
-  const int64_t pr = t.pi[g], lc = t.lc[g], la = t.la[g];
-  const uint64_t cw = t.conf[g];
-  int64_t m[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) m[p] = t.match[static_cast<size_t>(p) * t.ld + g];
-  const int64_t pi = pr == kPiFollowsLc ? lc + 1 : pr;
-  if (pi == 0) {
-    out = lc;
-    st = kStNotLeader;
-    return;
-  }
-  st = mask_out_of_range<P>(m, la);
-  const TableRuns R{&t, g, cw & ~kConfRuns};
-  out = runs_best<P>(R, kTableMaxRuns, pi, la, lc, m, st);
+// Writes of a committing group: lastCommitted, and pendingIndex -> JRQ_PI_FOLLOWS_LC once.
+__device__ __forceinline__ void table_commit_one(const JrqTableArgs& t, uint32_t g, int64_t pr,
+                                                 int64_t out) {
+  t.lc[g] = out;
+  if (pr != kPiFollowsLc) t.pi[g] = kPiFollowsLc;
 }
 
 template <int P>
 __global__ __launch_bounds__(256) void table_epoch_kernel(JrqTableArgs t) {
   __shared__ uint32_t wave_cnt[4];
   __shared__ uint32_t blk_base;
+  __shared__ uint32_t n_deferred;
+  __shared__ uint32_t deferred[512];
   const uint32_t pairs = (t.G + 1) >> 1;  // ld covers the pad group of an odd G (not a leader)
   const uint32_t tt = blockIdx.x * 256u + threadIdx.x;
   const uint32_t g = tt << 1;
+  if (threadIdx.x == 0) n_deferred = 0;
+  __syncthreads();
   bool c0 = false, c1 = false;
   uint64_t e0 = 0, e1 = 0;
   if (tt < pairs) {
@@ -79,8 +69,7 @@ __global__ __launch_bounds__(256) void table_epoch_kernel(JrqTableArgs t) {
     for (int p = 0; p < P; ++p) mv[p] = tld2(t.match + static_cast<size_t>(p) * t.ld + g);
     const int64_t pi0 = pr.x == kPiFollowsLc ? lc.x + 1 : pr.x;
     const int64_t pi1 = pr.y == kPiFollowsLc ? lc.y + 1 : pr.y;
-    const uint32_t flags = static_cast<uint32_t>(static_cast<uint64_t>(cw.x) >> 63) |
-                           (static_cast<uint32_t>(static_cast<uint64_t>(cw.y) >> 63) << 1);
+    const bool f0 = static_cast<uint64_t>(cw.x) >> 63, f1 = static_cast<uint64_t>(cw.y) >> 63;
     int64_t m0[P], m1[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -91,40 +80,70 @@ __global__ __launch_bounds__(256) void table_epoch_kernel(JrqTableArgs t) {
     uint8_t s0, s1;
     decide_single<P>(pi0, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
     decide_single<P>(pi1, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
-    if (flags) {  // rare: groups with a conf change inside their pending window
-      if (flags & 1u) table_redecide<P>(t, g, o0, s0);
-      if (flags & 2u) table_redecide<P>(t, g + 1, o1, s1);
-    }
-    c0 = o0 > lc.x;  // decide_* return lastCommitted unless a commit happened
-    c1 = o1 > lc.y;
-    if (c0 || c1) {
+    // a group with a conf change inside its pending window (JRQ_CONF_RUNS) is deferred to
+    // the workgroup's second phase below, so that the run walk shares no registers with this
+    c0 = !f0 && o0 > lc.x;  // decide_single returns lastCommitted unless a commit happened
+    c1 = !f1 && o1 > lc.y;
+    if (c0 && c1) {
       i64x2 o;
       o.x = o0;
       o.y = o1;
       __builtin_nontemporal_store(o, reinterpret_cast<i64x2*>(t.lc + g));
-      // pendingIndex = lastCommittedIndex + 1 from now on (BallotBox.java:131-132): one store
-      // per group and leadership, the steady state writes lastCommitted only
-      if (c0 && pr.x != kPiFollowsLc) t.pi[g] = kPiFollowsLc;
-      if (c1 && pr.y != kPiFollowsLc) t.pi[g + 1] = kPiFollowsLc;
+      // pendingIndex = lastCommittedIndex + 1 from now on (BallotBox.java:131-132): one
+      // store per group and leadership, the steady state writes lastCommitted only
+      if (pr.x != kPiFollowsLc) t.pi[g] = kPiFollowsLc;
+      if (pr.y != kPiFollowsLc) t.pi[g + 1] = kPiFollowsLc;
+    } else {
+      if (c0) table_commit_one(t, g, pr.x, o0);
+      if (c1) table_commit_one(t, g + 1, pr.y, o1);
     }
-    if (t.status) {
-      if (g + 1 < t.G)
+    if (t.status) {  // a deferred group's status is written by the second phase only
+      if (g + 1 < t.G && !f0 && !f1)
         __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
                                     reinterpret_cast<uint16_t*>(t.status + g));
-      else
-        t.status[g] = s0;
+      else {
+        if (!f0) t.status[g] = s0;
+        if (!f1 && g + 1 < t.G) t.status[g + 1] = s1;
+      }
     }
     e0 = (static_cast<uint64_t>(o0 - pi0 + 1) << 32) | g;
     e1 = (static_cast<uint64_t>(o1 - pi1 + 1) << 32) | (g + 1);
+    if (f0) deferred[atomicAdd(&n_deferred, 1u)] = g;
+    if (f1) deferred[atomicAdd(&n_deferred, 1u)] = g + 1;
+  }
+  __syncthreads();
+  // second phase: the deferred groups walk their conf runs (the inline run slots), one lane
+  // each, reloading the group (L2-hot)
+  bool c2 = false;
+  uint64_t e2 = 0;
+  if (threadIdx.x < n_deferred) {
+    const uint32_t h = deferred[threadIdx.x];
+    const int64_t pr = t.pi[h], lc = t.lc[h], la = t.la[h];
+    const uint64_t cw = t.conf[h];
+    int64_t m[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) m[p] = t.match[static_cast<size_t>(p) * t.ld + h];
+    const int64_t pi = pr == kPiFollowsLc ? lc + 1 : pr;
+    int64_t out = lc;
+    uint8_t st = kStNotLeader;
+    if (pi != 0) {
+      st = mask_out_of_range<P>(m, la);
+      const TableRuns R{&t, h, cw & ~kConfRuns};
+      out = runs_best<P>(R, kTableMaxRuns, pi, la, lc, m, st);
+    }
+    if (t.status) t.status[h] = st;
+    c2 = out > lc;
+    if (c2) table_commit_one(t, h, pr, out);
+    e2 = (static_cast<uint64_t>(out - pi + 1) << 32) | h;
   }
   // compaction: lane-major order inside a wave, waves in order inside the workgroup, and one
   // 64-bit atomic per workgroup ({workgroups done << 32 | entries}) reserves its slice of the
   // list; the last workgroup to arrive publishes the count and re-zeroes the counter
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
+  const uint64_t b0 = __ballot(c0), b1 = __ballot(c1), b2 = __ballot(c2);
   const uint64_t below = (1ull << lane) - 1ull;
-  const uint32_t pre = __popcll(b0 & below) + __popcll(b1 & below);
-  if (lane == 0) wave_cnt[w] = __popcll(b0) + __popcll(b1);
+  const uint32_t pre = __popcll(b0 & below) + __popcll(b1 & below) + __popcll(b2 & below);
+  if (lane == 0) wave_cnt[w] = __popcll(b0) + __popcll(b1) + __popcll(b2);
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t tot = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
@@ -139,7 +158,8 @@ __global__ __launch_bounds__(256) void table_epoch_kernel(JrqTableArgs t) {
   uint32_t pos = blk_base + pre;
   for (uint32_t u = 0; u < w; ++u) pos += wave_cnt[u];
   if (c0) t.changed[pos++] = e0;
-  if (c1) t.changed[pos] = e1;
+  if (c1) t.changed[pos++] = e1;
+  if (c2) t.changed[pos] = e2;
 }
 
 // Group headers: one lane per header (a group appears at most once per call).

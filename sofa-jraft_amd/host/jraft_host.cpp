@@ -365,7 +365,9 @@ uint32_t GroupBatch::flush() {
       st.group = g;
       st.num_runs = nruns_[g];
       st.flags = (d & kDirtyReset) ? JRQ_STATE_RESET_MATCH : 0;
-      st.pending_index = pi;
+      // the table's steady-state encoding of pendingIndex = lastCommittedIndex + 1: the
+      // group's next commit then writes lastCommitted only
+      st.pending_index = (pi != 0 && pi == lc_[g] + 1) ? JRQ_PI_FOLLOWS_LC : pi;
       st.last_appended = la_[g];
       st.last_committed = lc_[g];
       const Run* R = &runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS];
@@ -442,6 +444,9 @@ bool BallotBox::commitAt(int64_t first, int64_t last, const PeerId& peer) {
 
 void BallotBox::clearPendingTasks() {
   GroupBatch& b = *batch_;
+  // Acks recorded since the last epoch would have committed at once in the reference
+  // (BallotBox.commitAt decides synchronously): decide them before the queue is dropped.
+  if ((b.dirty_[g_] & 0xFFFFu) && b.pi_[g_] != 0 && b.eng_) b.flush();
   if (auto& q = b.closures_[g_]) {
     for (auto& c : *q) c.second(false);  // ClosureQueue.clear runs closures with EPERM
     q->clear();

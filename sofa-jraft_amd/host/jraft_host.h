@@ -163,7 +163,9 @@ class BallotBox {
   // contiguous over the entries whose ballots count it (the Replicator invariant,
   // Replicator.java:1387-1401): a gap over such an entry throws std::logic_error.
   bool commitAt(int64_t firstLogIndex, int64_t lastLogIndex, const PeerId& peer);
-  void clearPendingTasks();                                                    // :147-156
+  // :147-156 -- acks recorded since the last epoch are decided first (one flush of the
+  // batch), as the reference has already committed them when the leader steps down
+  void clearPendingTasks();
   bool resetPendingIndex(int64_t newPendingIndex);                             // :167-186
   // :197-215 -- oldConf == nullptr means a stable configuration
   bool appendPendingTask(const Configuration& conf, const Configuration* oldConf,

@@ -381,6 +381,7 @@ static void testRandomDifferentialOnGpu(Engine& eng) {
     bool joint = false;
     std::map<int32_t, int64_t> m;  // peer -> highest acked index (the Replicator's view)
     int64_t la = 0;
+    int64_t confEntry = 0;  // index of the last conf entry appended
   };
   std::vector<S> st(G);
   auto pickConf = [&](std::vector<int32_t> keep) {
@@ -414,6 +415,7 @@ static void testRandomDifferentialOnGpu(Engine& eng) {
         CHECK(t.box.resetPendingIndex(pi) && jo_bb_reset_pending_index(t.bb, pi) == JO_TRUE);
         s.la = pi - 1;
         s.joint = false;
+        s.confEntry = 0;
         for (auto& kv : s.m) kv.second = pi - 1 - R(3);
       }
     } else if (a < 35) {  // appendPendingTask x k under the current conf
@@ -421,6 +423,9 @@ static void testRandomDifferentialOnGpu(Engine& eng) {
       CHECK(t.append(s.cur, s.joint ? &s.old : nullptr, k));
       s.la += k;
     } else if (a < 40) {  // conf change: stable -> joint (replacing peers), joint -> stable
+      // NodeImpl starts the next stage only once the previous conf entry is committed
+      // (ConfigurationCtx.nextStage on onConfigurationChangeDone, NodeImpl.java:457-487)
+      if (t.box.getLastCommittedIndex() < s.confEntry) continue;
       if (!s.joint) {
         s.old = s.cur;
         s.cur = pickConf(std::vector<int32_t>(s.old.begin(), s.old.begin() + R(s.old.size() + 1)));
@@ -430,6 +435,7 @@ static void testRandomDifferentialOnGpu(Engine& eng) {
       }
       CHECK(t.append(s.cur, s.joint ? &s.old : nullptr, 1));
       s.la += 1;
+      s.confEntry = s.la;
     } else if (a < 94) {  // an ack, contiguous per peer: members mostly, any peer sometimes
       int32_t p;
       if (R(10) < 8) {

@@ -24,6 +24,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu ;;
+    profd) run prof_drive 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/profd -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs table,drive ;;
     tbl)   run table_tests 600 python -m pytest tests/test_gpu_table.py -q -x -p no:cacheprovider --timeout 300 ;;
     pmc)   # one rocprofv3 --pmc pass per (leg, counter): every kernel name then carries one workload
            for leg in ${PMC_LEGS:-quorum C2 C5 C1 v2 snapshot lease fanout}; do
