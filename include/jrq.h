@@ -219,7 +219,8 @@ void jrq_table_destroy(jrq_table *t);
 /* Apply n_states group headers, then n_recs update records, on the engine's stream.  Host
  * variant: states / recs are host memory (ideally jrq_host_register'ed, e.g. DirectByteBuffers)
  * copied with one H2D transfer each; they must stay unchanged until the next jrq_table_epoch
- * or jrq_synchronize returns.  Records are checked on the host (group < G, field valid). */
+ * or jrq_synchronize returns.  Invalid headers / records (group >= G, num_runs or field out of
+ * range) are skipped on the device and counted: jrq_table_check reports them. */
 int jrq_table_update(jrq_table *t, const jrq_group_state *states, uint32_t n_states,
                      const uint64_t *recs, uint32_t n_recs);
 int jrq_table_update_dev(jrq_table *t, const jrq_group_state *states_dev, uint32_t n_states,
@@ -240,6 +241,10 @@ int jrq_table_epoch(jrq_table *t, uint64_t *changed_out, uint32_t *n_changed,
  * JRQ_PI_FOLLOWS_LC), last_appended, last_committed [G], match [num_peers][G]. */
 int jrq_table_read(jrq_table *t, int64_t *pending_index, int64_t *last_appended,
                    int64_t *last_committed, int64_t *match);
+
+/* JRQ_E_INVALID if headers or records were skipped as invalid since the last check (the
+ * count is then reset); synchronises. */
+int jrq_table_check(jrq_table *t);
 
 /* Copy the whole state of src into dst (same G and num_peers), on dst's engine stream: a
  * device-side snapshot / restore of the group table. */

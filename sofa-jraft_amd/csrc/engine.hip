@@ -1035,6 +1035,7 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   a.xstart = reinterpret_cast<int64_t*>(a.conf + ld);
   a.xconf = reinterpret_cast<uint64_t*>(a.xstart + ld * (jrq::kTableMaxRuns - 1));
   a.ctr = reinterpret_cast<unsigned long long*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
+  a.invalid = reinterpret_cast<uint32_t*>(a.ctr + 2);
   a.ld = ld;
   a.G = G;
   a.P = P;
@@ -1072,17 +1073,8 @@ int jrq_table_update(jrq_table* t, const jrq_group_state* states, uint32_t n_sta
   if (table_check(t)) return JRQ_E_INVALID;
   jrq_engine* e = t->e;
   if ((n_states && !states) || (n_recs && !recs)) return fail(e, JRQ_E_INVALID, "null update array");
-  const uint32_t G = t->a.G, P = t->a.P;
-  for (uint32_t i = 0; i < n_states; ++i)
-    if (states[i].group >= G || states[i].num_runs > JRQ_TABLE_MAX_RUNS)
-      return fail(e, JRQ_E_INVALID, "group state %u: group %u / num_runs %u out of range", i,
-                  states[i].group, states[i].num_runs);
-  for (uint32_t i = 0; i < n_recs; ++i) {
-    const uint32_t f = static_cast<uint32_t>(recs[i] & 31u);
-    const uint32_t g = static_cast<uint32_t>(recs[i] >> 5) & ((1u << 27) - 1u);
-    if (g >= G || f > JRQ_REC_LAST_APPENDED || (f < JRQ_REC_LAST_APPENDED && f >= P))
-      return fail(e, JRQ_E_INVALID, "record %u: group %u / field %u out of range", i, g, f);
-  }
+  // no host pass over the records (it would cost as much as their PCIe transfer): the
+  // kernels skip and count invalid ones, reported by jrq_table_check
   DeviceGuard guard(e->device);
   int rc;
   void *ds = nullptr, *dr = nullptr;
@@ -1154,6 +1146,19 @@ int jrq_table_read(jrq_table* t, int64_t* pending_index, int64_t* last_appended,
     for (size_t g = 0; g < G; ++g)
       if (pending_index[g] == JRQ_PI_FOLLOWS_LC) pending_index[g] = lc[g] + 1;
   if (last_committed) std::memcpy(last_committed, lc.data(), b);
+  return JRQ_OK;
+}
+
+int jrq_table_check(jrq_table* t) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  DeviceGuard guard(e->device);
+  JRQ_HIP(e, hipMemcpyAsync(t->n_host + 1, t->a.invalid, 4, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemsetAsync(t->a.invalid, 0, 4, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  if (t->n_host[1])
+    return fail(e, JRQ_E_INVALID, "%u group headers / records skipped: group >= G, field or num_runs out of range",
+                t->n_host[1]);
   return JRQ_OK;
 }
 

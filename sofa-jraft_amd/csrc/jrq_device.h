@@ -194,6 +194,7 @@ struct JrqTableArgs {
   uint32_t G;            // groups (ld >= G rounded up to pairs; pad groups are not leaders)
   uint32_t P;
   unsigned long long* ctr;  // compaction counter {blocks done << 32 | entries}, zero between launches
+  uint32_t* invalid;     // records / headers skipped as invalid since the last jrq_table_check
   uint64_t* changed;     // [G] out
   uint32_t* n_changed;   // [1] out
   uint8_t* status;       // [G] out, nullable

@@ -152,8 +152,8 @@ __global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a)
     }
   }
   __syncthreads();
-  if (threadIdx.x < n_deferred) {
-    const uint32_t g = deferred[threadIdx.x];
+  for (uint32_t i = threadIdx.x; i < n_deferred; i += 256u) {  // up to 2 per lane
+    const uint32_t g = deferred[i];
     int64_t m[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];

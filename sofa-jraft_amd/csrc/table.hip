@@ -46,14 +46,20 @@ __device__ __forceinline__ void table_commit_one(const JrqTableArgs& t, uint32_t
   if (pr != kPiFollowsLc) t.pi[g] = kPiFollowsLc;
 }
 
+// 1024-thread workgroups of 2048 groups: the compaction's one atomic per workgroup then
+// costs 512 atomics on one address per 1M groups (2048 with 256-thread workgroups measured
+// +20 us: same-address atomics serialise), and 63 VGPRs keep 2 workgroups per CU resident.
+constexpr uint32_t kTableBlock = 1024;
+
 template <int P>
-__global__ __launch_bounds__(256) void table_epoch_kernel(JrqTableArgs t) {
-  __shared__ uint32_t wave_cnt[4];
+__global__ __launch_bounds__(kTableBlock) void table_epoch_kernel(JrqTableArgs t) {
+  constexpr uint32_t kWaves = kTableBlock / 64;
+  __shared__ uint32_t wave_cnt[kWaves];
   __shared__ uint32_t blk_base;
   __shared__ uint32_t n_deferred;
-  __shared__ uint32_t deferred[512];
+  __shared__ uint32_t deferred[2 * kTableBlock];
   const uint32_t pairs = (t.G + 1) >> 1;  // ld covers the pad group of an odd G (not a leader)
-  const uint32_t tt = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t tt = blockIdx.x * kTableBlock + threadIdx.x;
   const uint32_t g = tt << 1;
   if (threadIdx.x == 0) n_deferred = 0;
   __syncthreads();
@@ -113,11 +119,14 @@ __global__ __launch_bounds__(256) void table_epoch_kernel(JrqTableArgs t) {
   }
   __syncthreads();
   // second phase: the deferred groups walk their conf runs (the inline run slots), one lane
-  // each, reloading the group (L2-hot)
-  bool c2 = false;
-  uint64_t e2 = 0;
-  if (threadIdx.x < n_deferred) {
-    const uint32_t h = deferred[threadIdx.x];
+  // each (up to two per lane), reloading the group (L2-hot)
+  bool cd[2] = {false, false};
+  uint64_t ed[2] = {0, 0};
+#pragma unroll
+  for (uint32_t j = 0; j < 2; ++j) {
+    const uint32_t i = threadIdx.x + kTableBlock * j;
+    if (i >= n_deferred) break;
+    const uint32_t h = deferred[i];
     const int64_t pr = t.pi[h], lc = t.lc[h], la = t.la[h];
     const uint64_t cw = t.conf[h];
     int64_t m[P];
@@ -132,21 +141,23 @@ __global__ __launch_bounds__(256) void table_epoch_kernel(JrqTableArgs t) {
       out = runs_best<P>(R, kTableMaxRuns, pi, la, lc, m, st);
     }
     if (t.status) t.status[h] = st;
-    c2 = out > lc;
-    if (c2) table_commit_one(t, h, pr, out);
-    e2 = (static_cast<uint64_t>(out - pi + 1) << 32) | h;
+    cd[j] = out > lc;
+    if (cd[j]) table_commit_one(t, h, pr, out);
+    ed[j] = (static_cast<uint64_t>(out - pi + 1) << 32) | h;
   }
   // compaction: lane-major order inside a wave, waves in order inside the workgroup, and one
   // 64-bit atomic per workgroup ({workgroups done << 32 | entries}) reserves its slice of the
   // list; the last workgroup to arrive publishes the count and re-zeroes the counter
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  const uint64_t b0 = __ballot(c0), b1 = __ballot(c1), b2 = __ballot(c2);
+  const uint64_t b0 = __ballot(c0), b1 = __ballot(c1), b2 = __ballot(cd[0]), b3 = __ballot(cd[1]);
   const uint64_t below = (1ull << lane) - 1ull;
-  const uint32_t pre = __popcll(b0 & below) + __popcll(b1 & below) + __popcll(b2 & below);
-  if (lane == 0) wave_cnt[w] = __popcll(b0) + __popcll(b1) + __popcll(b2);
+  const uint32_t pre = __popcll(b0 & below) + __popcll(b1 & below) + __popcll(b2 & below) +
+                       __popcll(b3 & below);
+  if (lane == 0) wave_cnt[w] = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t tot = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+    uint32_t tot = 0;
+    for (uint32_t u = 0; u < kWaves; ++u) tot += wave_cnt[u];
     const unsigned long long old = atomicAdd(t.ctr, (1ull << 32) | tot);
     blk_base = static_cast<uint32_t>(old);
     if (static_cast<uint32_t>(old >> 32) + 1u == gridDim.x) {
@@ -159,7 +170,8 @@ __global__ __launch_bounds__(256) void table_epoch_kernel(JrqTableArgs t) {
   for (uint32_t u = 0; u < w; ++u) pos += wave_cnt[u];
   if (c0) t.changed[pos++] = e0;
   if (c1) t.changed[pos++] = e1;
-  if (c2) t.changed[pos] = e2;
+  if (cd[0]) t.changed[pos++] = ed[0];
+  if (cd[1]) t.changed[pos] = ed[1];
 }
 
 // Group headers: one lane per header (a group appears at most once per call).
@@ -169,8 +181,11 @@ __global__ __launch_bounds__(256) void table_states_kernel(JrqTableArgs t, const
   if (i >= n) return;
   const JrqGroupState st = s[i];
   const uint32_t g = st.group;
-  if (g >= t.G) return;
-  const uint32_t nr = st.num_runs < kTableMaxRuns ? st.num_runs : kTableMaxRuns;
+  if (g >= t.G || st.num_runs > kTableMaxRuns) {  // counted, reported by jrq_table_check
+    atomicAdd(t.invalid, 1u);
+    return;
+  }
+  const uint32_t nr = st.num_runs;
   t.pi[g] = st.pending_index;
   t.la[g] = st.last_appended;
   t.lc[g] = st.last_committed;
@@ -195,7 +210,10 @@ __global__ __launch_bounds__(256) void table_recs_kernel(JrqTableArgs t, const u
   const uint32_t f = static_cast<uint32_t>(r & 31u);
   const uint32_t g = static_cast<uint32_t>(r >> 5) & ((1u << 27) - 1u);
   const uint32_t v = static_cast<uint32_t>(r >> 32);
-  if (g >= t.G || f > 16u || (f < 16u && f >= t.P)) return;
+  if (g >= t.G || f > 16u || (f < 16u && f >= t.P)) {  // counted, reported by jrq_table_check
+    atomicAdd(t.invalid, 1u);
+    return;
+  }
   const int64_t pr = t.pi[g], lc = t.lc[g];
   const int64_t val = (pr == kPiFollowsLc ? lc + 1 : pr) - 1 + static_cast<int64_t>(v);
   if (f == 16u) t.la[g] = val;
@@ -219,7 +237,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_upd
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_epoch(
     const JrqTableArgs* a, hipStream_t stream) {
   const uint32_t pairs = (a->G + 1) >> 1;
-  const dim3 grid((pairs + 255) / 256), blk(256);
+  const dim3 grid((pairs + jrq::kTableBlock - 1) / jrq::kTableBlock), blk(jrq::kTableBlock);
   switch (a->P) {
 #define JRQ_CASE(P)                                                                   \
   case P:                                                                             \

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <sstream>
+#include <thread>
 
 namespace jraft {
 
@@ -187,6 +188,41 @@ uint64_t CRC64::getValue() {
 
 // --------------------------------------------------------------- ballot box
 
+namespace {
+
+// f(begin, end) over [0, n) split across up to 16 threads (the box's CPU share per GPU), only
+// when each gets at least `grain` items; the first exception thrown by any part is rethrown.
+template <class F>
+void parallelFor(size_t n, size_t grain, F&& f) {
+  const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t T = std::min<size_t>(std::min<size_t>(16, hw), std::max<size_t>(1, n / grain));
+  if (T <= 1) {
+    f(size_t(0), n);
+    return;
+  }
+  std::vector<std::thread> th;
+  std::vector<std::exception_ptr> err(T);
+  th.reserve(T - 1);
+  for (size_t i = 1; i < T; ++i)
+    th.emplace_back([&, i] {
+      try {
+        f(n * i / T, n * (i + 1) / T);
+      } catch (...) {
+        err[i] = std::current_exception();
+      }
+    });
+  try {
+    f(size_t(0), n / T);
+  } catch (...) {
+    err[0] = std::current_exception();
+  }
+  for (auto& t : th) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+}
+
+}  // namespace
+
 template <class T>
 void GroupBatch::PinnedBuf<T>::reserve(size_t n) {
   if (n <= cap) return;
@@ -350,41 +386,67 @@ uint32_t GroupBatch::flush() {
       if (bits) markDirty(g, bits);
     }
   }
-  // pack the changes: one header per group whose header changed, else 8-B records
+  // pack the changes: one header per group whose header changed, else 8-B records -- two
+  // passes over the dirty groups (count, then fill at per-chunk offsets), split across threads
   const size_t nd = dirtyList_.size();
-  states_.reserve(nd + 1);
-  recs_.reserve(nd * (P_ + 1) + 1);
-  uint32_t ns = 0, nr = 0;
-  for (uint32_t g : dirtyList_) {
-    const uint32_t d = dirty_[g];
-    dirty_[g] = 0;
-    const int64_t pi = pi_[g], base = pi - 1;
-    if (d & kDirtyHeader) {
-      jrq_group_state& st = states_.p[ns++];
-      std::memset(&st, 0, sizeof st);
-      st.group = g;
-      st.num_runs = nruns_[g];
-      st.flags = (d & kDirtyReset) ? JRQ_STATE_RESET_MATCH : 0;
-      // the table's steady-state encoding of pendingIndex = lastCommittedIndex + 1: the
-      // group's next commit then writes lastCommitted only
-      st.pending_index = (pi != 0 && pi == lc_[g] + 1) ? JRQ_PI_FOLLOWS_LC : pi;
-      st.last_appended = la_[g];
-      st.last_committed = lc_[g];
-      const Run* R = &runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS];
-      for (uint32_t r = 0; r < nruns_[g]; ++r) {
-        st.run_conf[r] = R[r].conf;
-        st.run_start[r] = R[r].start;
+  const size_t kChunk = 1u << 14;
+  const size_t nchunks = (nd + kChunk - 1) / kChunk;
+  std::vector<uint32_t> cs(nchunks + 1, 0), cr(nchunks + 1, 0);
+  parallelFor(nchunks, 1, [&](size_t c0, size_t c1) {
+    for (size_t c = c0; c < c1; ++c) {
+      uint32_t ns = 0, nr = 0;
+      for (size_t i = c * kChunk, e = std::min(nd, (c + 1) * kChunk); i < e; ++i) {
+        const uint32_t g = dirtyList_[i], d = dirty_[g];
+        if (d & kDirtyHeader) ++ns;
+        else if ((d & kDirtyLa) && pi_[g] != 0) ++nr;
+        if (pi_[g] != 0) nr += static_cast<uint32_t>(__builtin_popcount(d & 0xFFFFu));
       }
-    } else if ((d & kDirtyLa) && pi != 0) {
-      recs_.p[nr++] = JRQ_REC(g, JRQ_REC_LAST_APPENDED, la_[g] - base);
+      cs[c + 1] = ns;
+      cr[c + 1] = nr;
     }
-    if (pi == 0) continue;  // not the leader: its acks are refused (commitAt returns false)
-    for (uint32_t m = d & 0xFFFFu; m; m &= m - 1) {
-      const uint32_t s = static_cast<uint32_t>(__builtin_ctz(m));
-      const int64_t v = match_[static_cast<size_t>(g) * P_ + s] - base;
-      recs_.p[nr++] = JRQ_REC(g, s, v > 0 ? v : 0);
-    }
+  });
+  for (size_t c = 0; c < nchunks; ++c) {
+    cs[c + 1] += cs[c];
+    cr[c + 1] += cr[c];
   }
+  const uint32_t ns = cs[nchunks], nr = cr[nchunks];
+  states_.reserve(ns + 1);
+  recs_.reserve(nr + 1);
+  parallelFor(nchunks, 1, [&](size_t c0, size_t c1) {
+    for (size_t c = c0; c < c1; ++c) {
+      uint32_t si = cs[c], ri = cr[c];
+      for (size_t i = c * kChunk, e = std::min(nd, (c + 1) * kChunk); i < e; ++i) {
+        const uint32_t g = dirtyList_[i], d = dirty_[g];
+        dirty_[g] = 0;
+        const int64_t pi = pi_[g], base = pi - 1;
+        if (d & kDirtyHeader) {
+          jrq_group_state& st = states_.p[si++];
+          std::memset(&st, 0, sizeof st);
+          st.group = g;
+          st.num_runs = nruns_[g];
+          st.flags = (d & kDirtyReset) ? JRQ_STATE_RESET_MATCH : 0;
+          // the table's steady-state encoding of pendingIndex = lastCommittedIndex + 1: the
+          // group's next commit then writes lastCommitted only
+          st.pending_index = (pi != 0 && pi == lc_[g] + 1) ? JRQ_PI_FOLLOWS_LC : pi;
+          st.last_appended = la_[g];
+          st.last_committed = lc_[g];
+          const Run* R = &runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS];
+          for (uint32_t r = 0; r < nruns_[g]; ++r) {
+            st.run_conf[r] = R[r].conf;
+            st.run_start[r] = R[r].start;
+          }
+        } else if ((d & kDirtyLa) && pi != 0) {
+          recs_.p[ri++] = JRQ_REC(g, JRQ_REC_LAST_APPENDED, la_[g] - base);
+        }
+        if (pi == 0) continue;  // not the leader: its acks are refused (commitAt returns false)
+        for (uint32_t m = d & 0xFFFFu; m; m &= m - 1) {
+          const uint32_t s = static_cast<uint32_t>(__builtin_ctz(m));
+          const int64_t v = match_[static_cast<size_t>(g) * P_ + s] - base;
+          recs_.p[ri++] = JRQ_REC(g, s, v > 0 ? v : 0);
+        }
+      }
+    }
+  });
   dirtyList_.clear();
   changed_.reserve(G_);
   const auto t1 = clk::now();
@@ -392,11 +454,15 @@ uint32_t GroupBatch::flush() {
   uint32_t n = 0;
   throwIfError(jrq_table_epoch(table_, changed_.p, &n, nullptr), eng_->raw(), "jrq_table_epoch");
   const auto t2 = clk::now();
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint64_t w = changed_.p[i];
-    const uint32_t g = static_cast<uint32_t>(w);
-    commitTo(g, pi_[g] - 1 + static_cast<int64_t>(w >> 32));
-  }
+  // deliver: groups are independent, so their commits (closures, then onCommitted) run split
+  // across threads; one group's callbacks run on one thread, in order
+  parallelFor(n, 1u << 15, [&](size_t i0, size_t i1) {
+    for (size_t i = i0; i < i1; ++i) {
+      const uint64_t w = changed_.p[i];
+      const uint32_t g = static_cast<uint32_t>(w);
+      commitTo(g, pi_[g] - 1 + static_cast<int64_t>(w >> 32));
+    }
+  });
   ++flushes_;
   const auto t3 = clk::now();
   auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };

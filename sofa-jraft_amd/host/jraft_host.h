@@ -198,7 +198,10 @@ struct FlushStats {
 // a shadow of what Java's BallotBox holds, records what the API calls change, and flush()
 // ships only those changes (from page-locked buffers), runs one epoch and delivers the
 // commits -- closures, then waiter.onCommitted(index), as BallotBox.commitAt does after
-// unlocking (BallotBox.java:131-137).  Not thread-safe: one host thread per batch.
+// unlocking (BallotBox.java:131-137).  The batch is driven from one host thread; flush()
+// packs and delivers on up to 16 threads, so the callbacks of different groups may run
+// concurrently (as the reference's replicator threads call commitAt concurrently) and must
+// not call back into the batch.
 class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
  public:
   // eng may be null until the first flush() (host-only state checks need no GPU)

@@ -124,6 +124,7 @@ SIGNATURES = [
     ("jrq_table_epoch_dev", C.c_int, [_V, _V, _V, _V]),
     ("jrq_table_epoch", C.c_int, [_V, _V, _V, _V]),
     ("jrq_table_read", C.c_int, [_V, _V, _V, _V, _V]),
+    ("jrq_table_check", C.c_int, [_V]),
     ("jrq_table_copy", C.c_int, [_V, _V]),
     ("jrq_table_view_get", C.c_int, [_V, C.POINTER(TableView)]),
     ("jrq_rccl_get_unique_id", C.c_int, [_V]),

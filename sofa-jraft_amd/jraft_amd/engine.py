@@ -415,6 +415,10 @@ class Table:
                                      _np_ptr(o["match"])), self._eng.handle)
         return o
 
+    def check(self):
+        """Raise JrqError if invalid headers / records were skipped since the last check."""
+        check(self._L.jrq_table_check(self._h), self._eng.handle)
+
     def copy_from(self, src: "Table"):
         """Device-side copy of src's whole state (same shape), on this engine's stream."""
         check(self._L.jrq_table_copy(self._h, src._h), self._eng.handle)

@@ -148,19 +148,24 @@ def test_group_state_resets_and_clears(engine, oracle):
     t.close()
 
 
-def test_invalid_records_rejected(engine):
+def test_invalid_records_skipped_and_reported(engine):
+    """Out-of-range headers / records never touch the table: the kernels skip and count them,
+    jrq_table_check reports them once."""
     t = Table(engine, 100, 3)
+    t.check()
     for bad in (_lib.rec(100, 0, 1), _lib.rec(5, 3, 1), _lib.rec(5, 17, 1)):
+        t.update(None, np.atleast_1d(bad))
         with pytest.raises(JrqError):
-            t.update(None, np.atleast_1d(bad))
-    st = Table.states(1)
-    st["group"] = 100
-    with pytest.raises(JrqError):
-        t.update(st)
-    st["group"] = 1
-    st["num_runs"] = 5
-    with pytest.raises(JrqError):
-        t.update(st)
+            t.check()
+        t.check()  # reported once, then reset
+    st = Table.states(2)
+    st["group"] = [100, 1]
+    st["num_runs"] = [1, 5]
+    t.update(st)
+    with pytest.raises(JrqError, match="2 group headers"):
+        t.check()
+    r = t.read()
+    assert (r["pending_index"] == 0).all() and (r["match"] == 0).all()
     t.close()
 
 
