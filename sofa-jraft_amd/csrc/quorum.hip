@@ -193,11 +193,14 @@ __global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a)
 // half-wave a chunk of C epochs of them -- and a scan over the chunk maxima in LDS stitches
 // the prefix.  Loads stay coalesced (32 consecutive groups = 256 B per row and epoch); small
 // tiles spread a 10k-group batch over all 256 CUs.
+// C epochs per half-wave (16 loads of P+1 words per lane at P = 3), at most 8 waves per
+// workgroup: a 10k-group batch is 313 workgroups, all resident at once (2 per CU) -- a 16-wave
+// workgroup fits once per CU and left a second, partial round of workgroups (13.5 vs 8.8 us).
 template <int P>
 struct EpochChunk {
-  static constexpr int kC = (8 / (P + 1)) < 1 ? 1 : ((8 / (P + 1)) > 8 ? 8 : 8 / (P + 1));
-  static constexpr int kMaxWaves = P <= 8 ? 16 : 8;  // 128 / 256 VGPRs per lane
-  static constexpr int kTile = 32;                  // groups per workgroup
+  static constexpr int kC = (16 / (P + 1)) < 1 ? 1 : ((16 / (P + 1)) > 8 ? 8 : 16 / (P + 1));
+  static constexpr int kMaxWaves = 8;
+  static constexpr int kTile = 32;  // groups per workgroup
 };
 
 template <int P>
@@ -205,7 +208,7 @@ __global__ __launch_bounds__(64 * EpochChunk<P>::kMaxWaves) void quorum_epochs_k
     JrqQuorumArgs a, uint32_t K, uint64_t match_eld, uint64_t la_eld) {
   constexpr int C = EpochChunk<P>::kC;
   constexpr uint32_t T = EpochChunk<P>::kTile;
-  __shared__ int64_t chunk_max[2 * 16][T];
+  __shared__ int64_t chunk_max[2 * EpochChunk<P>::kMaxWaves][T];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t gl = lane & (T - 1u);
   const uint32_t chunk = (threadIdx.x >> 6) * 2u + (lane >> 5);  // this half-wave's chunk

@@ -8,6 +8,8 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <mutex>
 #include <sstream>
 #include <thread>
 
@@ -188,40 +190,90 @@ uint64_t CRC64::getValue() {
 
 // --------------------------------------------------------------- ballot box
 
-namespace {
+// Persistent workers for flush()'s pack and deliver passes (spawning threads per flush cost
+// ~2 ms on the GPU box): run(f) calls f(part, parts) on every worker and on the caller, and
+// returns when all have finished; the first exception thrown by any part is rethrown.
+struct GroupBatch::Pool {
+  explicit Pool(unsigned n) {
+    for (unsigned i = 1; i < n; ++i) th.emplace_back([this, i] { loop(i); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+  unsigned size() const { return static_cast<unsigned>(th.size()) + 1; }
+  void run(const std::function<void(unsigned, unsigned)>& f) {
+    const unsigned n = size();
+    err.assign(n, nullptr);
+    {
+      std::lock_guard<std::mutex> l(mu);
+      job = &f;
+      pending = n - 1;
+      ++gen;
+    }
+    cv.notify_all();
+    call(f, 0, n);
+    std::unique_lock<std::mutex> l(mu);
+    done.wait(l, [this] { return pending == 0; });
+    job = nullptr;
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
+  }
 
-// f(begin, end) over [0, n) split across up to 16 threads (the box's CPU share per GPU), only
-// when each gets at least `grain` items; the first exception thrown by any part is rethrown.
+ private:
+  void call(const std::function<void(unsigned, unsigned)>& f, unsigned i, unsigned n) {
+    try {
+      f(i, n);
+    } catch (...) {
+      err[i] = std::current_exception();
+    }
+  }
+  void loop(unsigned i) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(unsigned, unsigned)>* f;
+      {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+        f = job;
+      }
+      call(*f, i, size());
+      std::lock_guard<std::mutex> l(mu);
+      if (--pending == 0) done.notify_one();
+    }
+  }
+  std::vector<std::thread> th;
+  std::vector<std::exception_ptr> err;
+  std::mutex mu;
+  std::condition_variable cv, done;
+  const std::function<void(unsigned, unsigned)>* job = nullptr;
+  uint64_t gen = 0;
+  unsigned pending = 0;
+  bool stop = false;
+};
+
+// f(begin, end) over [0, n) on the pool, only when each part gets at least `grain` items.
 template <class F>
-void parallelFor(size_t n, size_t grain, F&& f) {
-  const size_t hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t T = std::min<size_t>(std::min<size_t>(16, hw), std::max<size_t>(1, n / grain));
-  if (T <= 1) {
+void GroupBatch::parallelFor(size_t n, size_t grain, F&& f) {
+  if (n < 2 * grain) {
     f(size_t(0), n);
     return;
   }
-  std::vector<std::thread> th;
-  std::vector<std::exception_ptr> err(T);
-  th.reserve(T - 1);
-  for (size_t i = 1; i < T; ++i)
-    th.emplace_back([&, i] {
-      try {
-        f(n * i / T, n * (i + 1) / T);
-      } catch (...) {
-        err[i] = std::current_exception();
-      }
-    });
-  try {
-    f(size_t(0), n / T);
-  } catch (...) {
-    err[0] = std::current_exception();
+  if (!pool_) {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    pool_.reset(new Pool(std::min(16u, hw)));  // the box's CPU share per GPU
   }
-  for (auto& t : th) t.join();
-  for (auto& e : err)
-    if (e) std::rethrow_exception(e);
+  const size_t parts = std::min<size_t>(pool_->size(), n / grain);
+  pool_->run([&](unsigned i, unsigned) {
+    if (i < parts) f(n * i / parts, n * (i + 1) / parts);
+  });
 }
-
-}  // namespace
 
 template <class T>
 void GroupBatch::PinnedBuf<T>::reserve(size_t n) {

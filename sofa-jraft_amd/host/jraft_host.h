@@ -252,6 +252,9 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   }
   void commitTo(uint32_t g, int64_t c);
   void dropDeadRuns(uint32_t g);
+  struct Pool;
+  template <class F>
+  void parallelFor(size_t n, size_t grain, F&& f);
 
   Engine* eng_;
   uint32_t G_, P_;
@@ -273,6 +276,7 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   PinnedBuf<uint64_t> recs_, changed_;
   uint32_t flushes_ = 0;
   FlushStats stats_;
+  std::unique_ptr<Pool> pool_;
 };
 
 }  // namespace jraft
