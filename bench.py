@@ -469,8 +469,9 @@ def leg_table(ctx, args, G, pair_ms):
         series.append(s)
     ctx.sync()
     work = Table(eng, G, P)
-    changed = torch.empty(G, dtype=torch.int64, device=dev)
-    n = torch.zeros(1, dtype=torch.int32, device=dev)
+    from jraft_amd import _lib
+    changed = torch.empty(_lib.TABLE_SEGMENTS * work.segment_capacity(), dtype=torch.int64, device=dev)
+    n = torch.zeros(_lib.TABLE_SEGMENTS, dtype=torch.int32, device=dev)
     steps = max(10, args.steps)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
@@ -485,8 +486,8 @@ def leg_table(ctx, args, G, pair_ms):
     ctx.sync()
     t_ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
     last = (steps - 1) % nb
-    n_changed = int(n.item())
-    words = changed[:n_changed].cpu().numpy().view(np.uint64)
+    words = work.gather_dev_list(changed, n)
+    n_changed = len(words)
     # the stateless pair kernel on the same inputs (CSR run table, flagged groups), same timing
     s = series[last]
     d = {k: to_dev(s[k] if k != "match" else s["match"][0], dev)

@@ -180,6 +180,7 @@ int jrq_quorum_epochs_dev(jrq_engine *e, const jrq_group_batch *in_dev, uint32_t
 #define JRQ_TABLE_MAX_RUNS 4            /* conf runs per pending window (NodeImpl has <= 2) */
 #define JRQ_TABLE_MAX_GROUPS (1u << 27) /* groups per table (27-bit group ids in records) */
 #define JRQ_PI_FOLLOWS_LC INT64_MIN
+#define JRQ_TABLE_SEGMENTS 16           /* segments of an epoch's changed list (_dev) */
 
 typedef struct jrq_table jrq_table;
 
@@ -228,14 +229,19 @@ int jrq_table_update_dev(jrq_table *t, const jrq_group_state *states_dev, uint32
 
 /* One quorum epoch over every group of the table, state updated in place as BallotBox.commitAt
  * leaves it (BallotBox.java:96-139; commit -> lastCommittedIndex, pendingIndex = commit + 1).
- * changed_out[k] = (uint64)(commit - pi + 1) << 32 | group for each group whose
- * lastCommittedIndex advanced (pi = its pendingIndex before the epoch; any order), *n_changed
- * = their number; status_out[g] (nullable) = jrq_group_status.  _dev: device pointers,
- * capacity G.  Host variant: synchronises and copies back n_changed entries only. */
-int jrq_table_epoch_dev(jrq_table *t, uint64_t *changed_out_dev, uint32_t *n_changed_dev,
-                        uint8_t *status_out_dev);
+ * Each group whose lastCommittedIndex advanced is listed once, as the word
+ * (uint64)(commit - pi + 1) << 32 | group (pi = its pendingIndex before the epoch), in no
+ * particular order; status_out[g] (nullable) = jrq_group_status.
+ * Host variant: changed_out[0 .. *n_changed) (capacity G); synchronises and copies back only
+ * the listed entries.
+ * _dev: the list comes in JRQ_TABLE_SEGMENTS segments (one atomic counter each, so that the
+ * workgroups' reservations do not serialise on one address): segment s holds n_changed_dev[s]
+ * entries at changed_out_dev + s * jrq_table_segment_capacity(t). */
+int jrq_table_epoch_dev(jrq_table *t, uint64_t *changed_out_dev,
+                        uint32_t n_changed_dev[JRQ_TABLE_SEGMENTS], uint8_t *status_out_dev);
 int jrq_table_epoch(jrq_table *t, uint64_t *changed_out, uint32_t *n_changed,
                     uint8_t *status_out);
+uint32_t jrq_table_segment_capacity(const jrq_table *t);
 
 /* Copy the table's state to host arrays (each nullable): pendingIndex resolved (never
  * JRQ_PI_FOLLOWS_LC), last_appended, last_committed [G], match [num_peers][G]. */

@@ -34,6 +34,8 @@ extern "C" hipError_t jrq_launch_table_update(const JrqTableArgs* a, const JrqGr
                                               uint32_t n_states, const uint64_t* recs,
                                               uint32_t n_recs, hipStream_t stream);
 extern "C" hipError_t jrq_launch_table_epoch(const JrqTableArgs* a, hipStream_t stream);
+extern "C" uint32_t jrq_table_seg_cap(uint32_t G);
+static_assert(JRQ_TABLE_SEGMENTS == jrq::kTableSegments, "table list segments");
 
 static_assert(sizeof(jrq_group_state) == sizeof(JrqGroupState), "jrq_group_state layout");
 static_assert(JRQ_TABLE_MAX_RUNS == jrq::kTableMaxRuns, "table runs");
@@ -1016,10 +1018,11 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   t->e = e;
   const uint64_t ld = (static_cast<uint64_t>(G) + 63) & ~63ull;  // pairs + 512-B rows
   const uint64_t words = ld * (P + 4 + 2 * (jrq::kTableMaxRuns - 1));
-  const size_t bytes = words * 8 + 64;
+  const size_t bytes = words * 8 + 8 * jrq::kTableSegments + 64;
   if (hipMalloc(&t->mem, bytes) != hipSuccess || hipMemset(t->mem, 0, bytes) != hipSuccess ||
-      hipMalloc(&t->n_dev, 16) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&t->n_host), 16, hipHostMallocDefault) != hipSuccess) {
+      hipMalloc(&t->n_dev, 4 * jrq::kTableSegments) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&t->n_host), 4 * (jrq::kTableSegments + 1),
+                    hipHostMallocDefault) != hipSuccess) {
     fail(e, JRQ_E_NOMEM, "table: allocation of %zu bytes failed", bytes);
     jrq_table_destroy(t);
     set(JRQ_E_NOMEM);
@@ -1035,7 +1038,8 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   a.xstart = reinterpret_cast<int64_t*>(a.conf + ld);
   a.xconf = reinterpret_cast<uint64_t*>(a.xstart + ld * (jrq::kTableMaxRuns - 1));
   a.ctr = reinterpret_cast<unsigned long long*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
-  a.invalid = reinterpret_cast<uint32_t*>(a.ctr + 2);
+  a.invalid = reinterpret_cast<uint32_t*>(a.ctr + jrq::kTableSegments);
+  a.seg_cap = jrq_table_seg_cap(G);
   a.ld = ld;
   a.G = G;
   a.P = P;
@@ -1110,23 +1114,32 @@ int jrq_table_epoch(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, ui
   if (!changed_out || !n_changed) return fail(e, JRQ_E_INVALID, "null changed output");
   DeviceGuard guard(e->device);
   const uint32_t G = t->a.G;
+  const size_t cap = static_cast<size_t>(t->a.seg_cap) * JRQ_TABLE_SEGMENTS;
   int rc;
   void *dch = nullptr, *dst = nullptr;
-  if ((rc = stage_buf(e, t->changed_stage, static_cast<size_t>(G) * 9, &dch))) return rc;
-  if (status_out) dst = static_cast<uint8_t*>(dch) + static_cast<size_t>(G) * 8;
+  if ((rc = stage_buf(e, t->changed_stage, cap * 8 + G, &dch))) return rc;
+  if (status_out) dst = static_cast<uint8_t*>(dch) + cap * 8;
   if ((rc = jrq_table_epoch_dev(t, static_cast<uint64_t*>(dch), t->n_dev, static_cast<uint8_t*>(dst))))
     return rc;
-  JRQ_HIP(e, hipMemcpyAsync(t->n_host, t->n_dev, 4, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(t->n_host, t->n_dev, 4 * JRQ_TABLE_SEGMENTS, hipMemcpyDeviceToHost, e->stream));
   if (status_out) JRQ_HIP(e, hipMemcpyAsync(status_out, dst, G, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
-  const uint32_t n = *t->n_host;
-  *n_changed = n;
-  if (n) {
-    JRQ_HIP(e, hipMemcpyAsync(changed_out, dch, static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, e->stream));
-    JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  // the segments back to back into the caller's buffer: only the entries cross PCIe
+  uint32_t n = 0;
+  for (uint32_t s = 0; s < JRQ_TABLE_SEGMENTS; ++s) {
+    const uint32_t k = t->n_host[s];
+    if (k > t->a.seg_cap || n + k > G) return fail(e, JRQ_E_STATE, "table list segment %u overflow", s);
+    if (k)
+      JRQ_HIP(e, hipMemcpyAsync(changed_out + n, static_cast<uint64_t*>(dch) + s * static_cast<size_t>(t->a.seg_cap),
+                                static_cast<size_t>(k) * 8, hipMemcpyDeviceToHost, e->stream));
+    n += k;
   }
+  *n_changed = n;
+  if (n) JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
+
+uint32_t jrq_table_segment_capacity(const jrq_table* t) { return t ? t->a.seg_cap : 0; }
 
 int jrq_table_read(jrq_table* t, int64_t* pending_index, int64_t* last_appended,
                    int64_t* last_committed, int64_t* match) {

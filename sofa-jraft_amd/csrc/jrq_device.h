@@ -4,6 +4,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// SGPR budget of a kernel.  Waves per SIMD on gfx950 = min(VGPR bound, 800 / (ceil(sgpr/16)*16
+// + 16)): .sgpr_count <= 80 keeps 8, 82..96 gives 7, while the compiler's occupancy model
+// (and its `Occupancy` remark) still says 8 -- so a 1024-thread workgroup at 96 SGPRs runs 1
+// workgroup per CU, not 2 (table_epoch_kernel<5>: 24.2 -> 20.3 us per 1M groups,
+// tools/table_probe.hip).  amdgpu_num_sgpr(n) yields .sgpr_count = n - 2.
+#define JRQ_SGPRS(n) __attribute__((amdgpu_num_sgpr(n)))
+#define JRQ_SGPRS_8WAVES JRQ_SGPRS(82)
+
 namespace jrq {
 
 // ----------------------------------------------------------------- CRC64 ---
@@ -180,6 +188,8 @@ struct JrqQuorumArgs {
 // Resident group table (table.hip; include/jrq.h jrq_table).
 namespace jrq {
 constexpr int kTableMaxRuns = 4;                   // JRQ_TABLE_MAX_RUNS
+constexpr uint32_t kTableSegments = 16;            // JRQ_TABLE_SEGMENTS
+constexpr uint32_t kTableBlockGroups = 2048;       // groups per epoch workgroup
 constexpr int64_t kPiFollowsLc = INT64_MIN;        // JRQ_PI_FOLLOWS_LC
 }  // namespace jrq
 struct JrqTableArgs {
@@ -193,10 +203,12 @@ struct JrqTableArgs {
   uint64_t ld;
   uint32_t G;            // groups (ld >= G rounded up to pairs; pad groups are not leaders)
   uint32_t P;
-  unsigned long long* ctr;  // compaction counter {blocks done << 32 | entries}, zero between launches
+  unsigned long long* ctr;  // [kTableSegments] compaction counters {blocks done << 32 | entries},
+                            // zero between launches
   uint32_t* invalid;     // records / headers skipped as invalid since the last jrq_table_check
-  uint64_t* changed;     // [G] out
-  uint32_t* n_changed;   // [1] out
+  uint64_t* changed;     // [kTableSegments][seg_cap] out
+  uint32_t* n_changed;   // [kTableSegments] out
+  uint32_t seg_cap;      // entries per list segment
   uint8_t* status;       // [G] out, nullable
 };
 

@@ -69,7 +69,7 @@ __device__ __forceinline__ void decide(const JrqQuorumArgs& a, uint32_t g, int64
 // is issued before any decision, so a group costs one memory round trip (two more for a
 // group that walks its runs).
 template <int P>
-__global__ __launch_bounds__(256) void quorum_epoch_kernel(JrqQuorumArgs a) {
+__global__ __launch_bounds__(256) JRQ_SGPRS_8WAVES void quorum_epoch_kernel(JrqQuorumArgs a) {
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G; g += stride) {
     const int64_t pi = a.pending_index[g];
@@ -100,7 +100,7 @@ __device__ __forceinline__ i64x2 ld2nt(const int64_t* p) {
 // deferred to the workgroup's second phase, where one lane per deferred group walks its runs:
 // the run walk then shares no registers with the fast path (occupancy of the common case).
 template <int P>
-__global__ __launch_bounds__(256) void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
+__global__ __launch_bounds__(256) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
   __shared__ uint32_t n_deferred;
   __shared__ uint32_t deferred[512];
   const uint32_t pairs = a.G >> 1;

@@ -46,24 +46,44 @@ __device__ __forceinline__ void table_commit_one(const JrqTableArgs& t, uint32_t
   if (pr != kPiFollowsLc) t.pi[g] = kPiFollowsLc;
 }
 
-// 1024-thread workgroups of 2048 groups: the compaction's one atomic per workgroup then
-// costs 512 atomics on one address per 1M groups (2048 with 256-thread workgroups measured
-// +20 us: same-address atomics serialise), and 63 VGPRs keep 2 workgroups per CU resident.
-constexpr uint32_t kTableBlock = 1024;
+// 1024-thread workgroups of 2048 groups (63 VGPRs: 2 workgroups per CU resident).  The
+// compacted list is cut into kTableSegments segments, workgroup b appending to segment
+// b % kTableSegments: same-address atomics serialise (~14 ns each, tools/table_probe.hip: one
+// counter for 512 workgroups cost 7 us of a 25 us epoch), so each counter sees 1/16 of them,
+// and the last arriver of each segment publishes its count -- no global arrival counter.
+constexpr uint32_t kTableBlock = kTableBlockGroups / 2;
+
+// The run walk of a group with JRQ_CONF_RUNS, reloading it (L2-hot): lastCommitted after the
+// epoch, status, and the writes of a commit.
+template <int P>
+__device__ __forceinline__ int64_t table_runs_one(const JrqTableArgs& t, uint32_t h, int64_t& pi,
+                                               uint8_t& st) {
+  const int64_t pr = t.pi[h], lc = t.lc[h], la = t.la[h];
+  const uint64_t cw = t.conf[h];
+  int64_t m[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) m[p] = t.match[static_cast<size_t>(p) * t.ld + h];
+  pi = pr == kPiFollowsLc ? lc + 1 : pr;
+  int64_t out = lc;
+  st = kStNotLeader;
+  if (pi != 0) {
+    st = mask_out_of_range<P>(m, la);
+    const TableRuns R{&t, h, cw & ~kConfRuns};
+    out = runs_best<P>(R, kTableMaxRuns, pi, la, lc, m, st);
+  }
+  if (out > lc) table_commit_one(t, h, pr, out);
+  return out - lc;
+}
 
 template <int P>
-__global__ __launch_bounds__(kTableBlock) void table_epoch_kernel(JrqTableArgs t) {
+__global__ __launch_bounds__(kTableBlock) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
   constexpr uint32_t kWaves = kTableBlock / 64;
   __shared__ uint32_t wave_cnt[kWaves];
   __shared__ uint32_t blk_base;
-  __shared__ uint32_t n_deferred;
-  __shared__ uint32_t deferred[2 * kTableBlock];
   const uint32_t pairs = (t.G + 1) >> 1;  // ld covers the pad group of an odd G (not a leader)
   const uint32_t tt = blockIdx.x * kTableBlock + threadIdx.x;
   const uint32_t g = tt << 1;
-  if (threadIdx.x == 0) n_deferred = 0;
-  __syncthreads();
-  bool c0 = false, c1 = false;
+  bool c0 = false, c1 = false, f0 = false, f1 = false;
   uint64_t e0 = 0, e1 = 0;
   if (tt < pairs) {
     const i64x2 pr = tld2(t.pi + g);
@@ -75,7 +95,8 @@ __global__ __launch_bounds__(kTableBlock) void table_epoch_kernel(JrqTableArgs t
     for (int p = 0; p < P; ++p) mv[p] = tld2(t.match + static_cast<size_t>(p) * t.ld + g);
     const int64_t pi0 = pr.x == kPiFollowsLc ? lc.x + 1 : pr.x;
     const int64_t pi1 = pr.y == kPiFollowsLc ? lc.y + 1 : pr.y;
-    const bool f0 = static_cast<uint64_t>(cw.x) >> 63, f1 = static_cast<uint64_t>(cw.y) >> 63;
+    f0 = static_cast<uint64_t>(cw.x) >> 63;
+    f1 = static_cast<uint64_t>(cw.y) >> 63;
     int64_t m0[P], m1[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -86,8 +107,8 @@ __global__ __launch_bounds__(kTableBlock) void table_epoch_kernel(JrqTableArgs t
     uint8_t s0, s1;
     decide_single<P>(pi0, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
     decide_single<P>(pi1, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
-    // a group with a conf change inside its pending window (JRQ_CONF_RUNS) is deferred to
-    // the workgroup's second phase below, so that the run walk shares no registers with this
+    // a group with a conf change inside its pending window (JRQ_CONF_RUNS) is decided again
+    // below with its runs; its single-conf result here is discarded
     c0 = !f0 && o0 > lc.x;  // decide_single returns lastCommitted unless a commit happened
     c1 = !f1 && o1 > lc.y;
     if (c0 && c1) {
@@ -103,7 +124,7 @@ __global__ __launch_bounds__(kTableBlock) void table_epoch_kernel(JrqTableArgs t
       if (c0) table_commit_one(t, g, pr.x, o0);
       if (c1) table_commit_one(t, g + 1, pr.y, o1);
     }
-    if (t.status) {  // a deferred group's status is written by the second phase only
+    if (t.status) {  // a flagged group's status is written by the run walk
       if (g + 1 < t.G && !f0 && !f1)
         __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
                                     reinterpret_cast<uint16_t*>(t.status + g));
@@ -114,64 +135,54 @@ __global__ __launch_bounds__(kTableBlock) void table_epoch_kernel(JrqTableArgs t
     }
     e0 = (static_cast<uint64_t>(o0 - pi0 + 1) << 32) | g;
     e1 = (static_cast<uint64_t>(o1 - pi1 + 1) << 32) | (g + 1);
-    if (f0) deferred[atomicAdd(&n_deferred, 1u)] = g;
-    if (f1) deferred[atomicAdd(&n_deferred, 1u)] = g + 1;
   }
-  __syncthreads();
-  // second phase: the deferred groups walk their conf runs (the inline run slots), one lane
-  // each (up to two per lane), reloading the group (L2-hot)
-  bool cd[2] = {false, false};
-  uint64_t ed[2] = {0, 0};
-#pragma unroll
-  for (uint32_t j = 0; j < 2; ++j) {
-    const uint32_t i = threadIdx.x + kTableBlock * j;
-    if (i >= n_deferred) break;
-    const uint32_t h = deferred[i];
-    const int64_t pr = t.pi[h], lc = t.lc[h], la = t.la[h];
-    const uint64_t cw = t.conf[h];
-    int64_t m[P];
-#pragma unroll
-    for (int p = 0; p < P; ++p) m[p] = t.match[static_cast<size_t>(p) * t.ld + h];
-    const int64_t pi = pr == kPiFollowsLc ? lc + 1 : pr;
-    int64_t out = lc;
-    uint8_t st = kStNotLeader;
-    if (pi != 0) {
-      st = mask_out_of_range<P>(m, la);
-      const TableRuns R{&t, h, cw & ~kConfRuns};
-      out = runs_best<P>(R, kTableMaxRuns, pi, la, lc, m, st);
-    }
-    if (t.status) t.status[h] = st;
-    cd[j] = out > lc;
-    if (cd[j]) table_commit_one(t, h, pr, out);
-    ed[j] = (static_cast<uint64_t>(out - pi + 1) << 32) | h;
+  // flagged groups walk their conf runs in the lane that holds them, after the fast path's
+  // registers are dead (skipped by a wave none of whose groups is flagged).
+  // No workgroup barrier: a barrier here measured +4.7 us per 1M-group epoch
+  // (tools/table_probe.hip).
+  if (__builtin_expect(f0, 0)) {
+    int64_t pi;
+    uint8_t st;
+    const int64_t d = table_runs_one<P>(t, g, pi, st);
+    if (t.status) t.status[g] = st;
+    c0 = d > 0;
+    e0 = (static_cast<uint64_t>(t.lc[g] - pi + 1) << 32) | g;
   }
-  // compaction: lane-major order inside a wave, waves in order inside the workgroup, and one
-  // 64-bit atomic per workgroup ({workgroups done << 32 | entries}) reserves its slice of the
-  // list; the last workgroup to arrive publishes the count and re-zeroes the counter
+  if (__builtin_expect(f1, 0)) {
+    int64_t pi;
+    uint8_t st;
+    const int64_t d = table_runs_one<P>(t, g + 1, pi, st);
+    if (t.status) t.status[g + 1] = st;
+    c1 = d > 0;
+    e1 = (static_cast<uint64_t>(t.lc[g + 1] - pi + 1) << 32) | (g + 1);
+  }
+  // compaction: lane-major order inside a wave, waves in order inside the workgroup; one
+  // 64-bit atomic per workgroup ({workgroups done << 32 | entries}) on its segment's counter
+  // reserves the workgroup's slice, and the last workgroup of a segment publishes its count
+  // and re-zeroes the counter
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  const uint64_t b0 = __ballot(c0), b1 = __ballot(c1), b2 = __ballot(cd[0]), b3 = __ballot(cd[1]);
+  const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
   const uint64_t below = (1ull << lane) - 1ull;
-  const uint32_t pre = __popcll(b0 & below) + __popcll(b1 & below) + __popcll(b2 & below) +
-                       __popcll(b3 & below);
-  if (lane == 0) wave_cnt[w] = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+  const uint32_t pre = __popcll(b0 & below) + __popcll(b1 & below);
+  if (lane == 0) wave_cnt[w] = __popcll(b0) + __popcll(b1);
   __syncthreads();
+  const uint32_t seg = blockIdx.x % kTableSegments;
   if (threadIdx.x == 0) {
     uint32_t tot = 0;
     for (uint32_t u = 0; u < kWaves; ++u) tot += wave_cnt[u];
-    const unsigned long long old = atomicAdd(t.ctr, (1ull << 32) | tot);
-    blk_base = static_cast<uint32_t>(old);
-    if (static_cast<uint32_t>(old >> 32) + 1u == gridDim.x) {
-      *t.n_changed = static_cast<uint32_t>(old) + tot;
-      atomicExch(t.ctr, 0ull);
+    const unsigned long long old = atomicAdd(t.ctr + seg, (1ull << 32) | tot);
+    blk_base = seg * t.seg_cap + static_cast<uint32_t>(old);
+    const uint32_t seg_blocks = (gridDim.x - seg + kTableSegments - 1) / kTableSegments;
+    if (static_cast<uint32_t>(old >> 32) + 1u == seg_blocks) {  // the segment is complete
+      t.n_changed[seg] = static_cast<uint32_t>(old) + tot;
+      atomicExch(t.ctr + seg, 0ull);
     }
   }
   __syncthreads();
   uint32_t pos = blk_base + pre;
   for (uint32_t u = 0; u < w; ++u) pos += wave_cnt[u];
   if (c0) t.changed[pos++] = e0;
-  if (c1) t.changed[pos++] = e1;
-  if (cd[0]) t.changed[pos++] = ed[0];
-  if (cd[1]) t.changed[pos] = ed[1];
+  if (c1) t.changed[pos] = e1;
 }
 
 // Group headers: one lane per header (a group appears at most once per call).
@@ -234,10 +245,17 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_upd
   return hipGetLastError();
 }
 
+extern "C" __attribute__((visibility("hidden"))) uint32_t jrq_table_seg_cap(uint32_t G) {
+  const uint32_t blocks = (G + jrq::kTableBlockGroups - 1) / jrq::kTableBlockGroups;
+  return (blocks + jrq::kTableSegments - 1) / jrq::kTableSegments * jrq::kTableBlockGroups;
+}
+
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_epoch(
     const JrqTableArgs* a, hipStream_t stream) {
   const uint32_t pairs = (a->G + 1) >> 1;
   const dim3 grid((pairs + jrq::kTableBlock - 1) / jrq::kTableBlock), blk(jrq::kTableBlock);
+  if (grid.x < jrq::kTableSegments)  // segments no workgroup appends to: count 0
+    (void)hipMemsetAsync(a->n_changed + grid.x, 0, 4 * (jrq::kTableSegments - grid.x), stream);
   switch (a->P) {
 #define JRQ_CASE(P)                                                                   \
   case P:                                                                             \

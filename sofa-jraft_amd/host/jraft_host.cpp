@@ -522,7 +522,7 @@ uint32_t GroupBatch::flush() {
   stats_.records = nr;
   stats_.changed = n;
   stats_.h2d_bytes = static_cast<uint64_t>(ns) * sizeof(jrq_group_state) + static_cast<uint64_t>(nr) * 8;
-  stats_.d2h_bytes = 4 + static_cast<uint64_t>(n) * 8;
+  stats_.d2h_bytes = 4 * JRQ_TABLE_SEGMENTS + static_cast<uint64_t>(n) * 8;
   stats_.pack_ms = ms(t1 - t0);
   stats_.device_ms = ms(t2 - t1);
   stats_.deliver_ms = ms(t3 - t2);

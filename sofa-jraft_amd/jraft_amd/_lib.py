@@ -50,6 +50,7 @@ TABLE_MAX_RUNS = 4                     # JRQ_TABLE_MAX_RUNS
 TABLE_MAX_GROUPS = 1 << 27             # JRQ_TABLE_MAX_GROUPS
 PI_FOLLOWS_LC = -(1 << 63)             # JRQ_PI_FOLLOWS_LC
 REC_LAST_APPENDED = 16                 # JRQ_REC_LAST_APPENDED
+TABLE_SEGMENTS = 16                    # JRQ_TABLE_SEGMENTS
 STATE_RESET_MATCH = 1                  # JRQ_STATE_RESET_MATCH
 
 try:
@@ -123,6 +124,7 @@ SIGNATURES = [
     ("jrq_table_update_dev", C.c_int, [_V, _V, C.c_uint32, _V, C.c_uint32]),
     ("jrq_table_epoch_dev", C.c_int, [_V, _V, _V, _V]),
     ("jrq_table_epoch", C.c_int, [_V, _V, _V, _V]),
+    ("jrq_table_segment_capacity", C.c_uint32, [_V]),
     ("jrq_table_read", C.c_int, [_V, _V, _V, _V, _V]),
     ("jrq_table_check", C.c_int, [_V]),
     ("jrq_table_copy", C.c_int, [_V, _V]),

@@ -402,9 +402,21 @@ class Table:
         self._keep = None
         return out[: n.value].copy(), st
 
+    def segment_capacity(self) -> int:
+        return int(self._L.jrq_table_segment_capacity(self._h))
+
     def epoch_dev(self, changed_out, n_changed_out, status_out=None):
+        """Device variant: changed_out capacity TABLE_SEGMENTS * segment_capacity() words,
+        n_changed_out int32[TABLE_SEGMENTS] per-segment counts (see include/jrq.h)."""
         check(self._L.jrq_table_epoch_dev(self._h, _dev_ptr(changed_out), _dev_ptr(n_changed_out),
                                           _dev_ptr(status_out)), self._eng.handle)
+
+    def gather_dev_list(self, changed_out, n_changed_out) -> np.ndarray:
+        """Host copy of a device-variant list (segments back to back), as JRQ words."""
+        cap = self.segment_capacity()
+        counts = n_changed_out.cpu().numpy().astype(np.int64)
+        words = changed_out.cpu().numpy().view(np.uint64)
+        return np.concatenate([words[s * cap: s * cap + counts[s]] for s in range(len(counts))])
 
     def read(self) -> dict:
         G, P = self.G, self.P

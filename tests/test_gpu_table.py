@@ -183,13 +183,11 @@ def test_device_variant_and_view(engine, oracle):
     st = torch.from_numpy(states_of(b).view(np.uint8)).to(dev)
     rc = torch.from_numpy(match_recs(b["match"], b["pending_index"]).view(np.int64)).to(dev)
     t.update_dev(st, rc)
-    out = torch.empty(G, dtype=torch.int64, device=dev)
-    n = torch.zeros(1, dtype=torch.int32, device=dev)
+    out = torch.empty(_lib.TABLE_SEGMENTS * t.segment_capacity(), dtype=torch.int64, device=dev)
+    n = torch.zeros(_lib.TABLE_SEGMENTS, dtype=torch.int32, device=dev)
     t.epoch_dev(out, n)
     engine.synchronize()
-    cnt = int(n.item())
-    got, _ = committed_from(out[:cnt].cpu().numpy().view(np.uint64), b["pending_index"],
-                            b["last_committed"])
+    got, _ = committed_from(t.gather_dev_list(out, n), b["pending_index"], b["last_committed"])
     np.testing.assert_array_equal(got, ce)
     v = t.view()
     assert v.G == G and v.num_peers == P and v.ld >= G and v.last_committed
