@@ -73,6 +73,18 @@ __device__ __forceinline__ void decide_single(int64_t pi, int64_t la, int64_t lc
 // run empty).  best is max(lc, the largest granted index over the runs); each run is
 // evaluated on its own, which reproduces the reference's non-monotone commit when an
 // even-size conf shrinks (BallotBox.java:124-129).  `Runs` supplies start(r) / conf(r).
+// One run: the largest index it grants inside [s, ee] (kI64Min when none, or when the run is
+// empty: ee < s); an empty conf on a non-empty run sets kStEmptyConf.
+template <int P>
+__device__ __forceinline__ int64_t run_candidate(const int64_t (&m)[P], uint64_t cw, int64_t s,
+                                                 int64_t ee, uint8_t& st) {
+  if (ee < s) return kI64Min;  // run entirely committed already (or empty)
+  if ((cw & 0xFFFFu) == 0) st |= kStEmptyConf;
+  int64_t cand = run_bound<P>(m, cw);
+  cand = cand < ee ? cand : ee;
+  return cand >= s ? cand : kI64Min;
+}
+
 template <int P, class Runs>
 __device__ __forceinline__ int64_t runs_best(const Runs& R, uint32_t nruns, int64_t pi, int64_t la,
                                              int64_t lc, const int64_t (&m)[P], uint8_t& st) {
@@ -83,12 +95,9 @@ __device__ __forceinline__ int64_t runs_best(const Runs& R, uint32_t nruns, int6
     const int64_t s = (r == 0) ? pi : (rs > pi ? rs : pi);
     const int64_t e = (r + 1 < nruns) ? R.start(r + 1) - 1 : la;
     const int64_t ee = e < la ? e : la;
-    if (ee < s) continue;  // run entirely committed already (or empty)
-    const uint64_t cw = R.conf(r);
-    if ((cw & 0xFFFFu) == 0) st |= kStEmptyConf;
-    int64_t cand = run_bound<P>(m, cw);
-    cand = cand < ee ? cand : ee;
-    best = (cand >= s && cand > best) ? cand : best;
+    if (ee < s) continue;
+    const int64_t cand = run_candidate<P>(m, R.conf(r), s, ee, st);
+    best = cand > best ? cand : best;
   }
   return best;
 }

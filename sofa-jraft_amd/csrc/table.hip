@@ -25,20 +25,6 @@ __device__ __forceinline__ i64x2 tld2(const int64_t* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(p));
 }
 
-// Runs of a flagged group: run 0 = the conf word (starts at or before pendingIndex), runs
-// 1..kTableMaxRuns-1 in the inline slots (start INT64_MAX = unused: an empty run).
-struct TableRuns {
-  const JrqTableArgs* t;
-  uint32_t g;
-  uint64_t c0;
-  __device__ int64_t start(uint32_t r) const {
-    return r == 0 ? kI64Min : t->xstart[static_cast<size_t>(r - 1) * t->ld + g];
-  }
-  __device__ uint64_t conf(uint32_t r) const {
-    return r == 0 ? c0 : t->xconf[static_cast<size_t>(r - 1) * t->ld + g];
-  }
-};
-
 // Writes of a committing group: lastCommitted, and pendingIndex -> JRQ_PI_FOLLOWS_LC once.
 __device__ __forceinline__ void table_commit_one(const JrqTableArgs& t, uint32_t g, int64_t pr,
                                                  int64_t out) {
@@ -53,36 +39,51 @@ __device__ __forceinline__ void table_commit_one(const JrqTableArgs& t, uint32_t
 // and the last arriver of each segment publishes its count -- no global arrival counter.
 constexpr uint32_t kTableBlock = kTableBlockGroups / 2;
 
-// The run walk of a group with JRQ_CONF_RUNS, reloading it (L2-hot): lastCommitted after the
-// epoch, status, and the writes of a commit.
+// The run walk of one flagged group, run r of it on lane r of an aligned lane quad (the table
+// holds at most kTableMaxRuns = 4 runs): each lane reloads the group (the quad's loads of it
+// coalesce) and its run's start, next start and conf word, all in one batch; the quad then
+// max-reduces the runs' candidates.  Returns the group's candidate (kI64Min: none) and status.
 template <int P>
-__device__ __forceinline__ int64_t table_runs_one(const JrqTableArgs& t, uint32_t h, int64_t& pi,
-                                               uint8_t& st) {
-  const int64_t pr = t.pi[h], lc = t.lc[h], la = t.la[h];
-  const uint64_t cw = t.conf[h];
+__device__ __forceinline__ int64_t table_run_lane(const JrqTableArgs& t, uint32_t h, uint32_t r,
+                                                  int64_t& pr, int64_t& lc, int64_t& pi,
+                                                  uint8_t& st) {
+  static_assert(kTableMaxRuns == 4, "one run per lane of a quad");
+  pr = t.pi[h];
+  lc = t.lc[h];
+  const int64_t la = t.la[h];
+  const size_t o = static_cast<size_t>(r) * t.ld + h;  // run r's slot is r - 1; next run's is r
+  const uint64_t cw = r == 0 ? (t.conf[h] & ~kConfRuns) : t.xconf[o - t.ld];
+  const int64_t rs = r == 0 ? kI64Min : t.xstart[o - t.ld];
+  const int64_t nx = r + 1 < kTableMaxRuns ? t.xstart[o] : kI64Max;
   int64_t m[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) m[p] = t.match[static_cast<size_t>(p) * t.ld + h];
   pi = pr == kPiFollowsLc ? lc + 1 : pr;
-  int64_t out = lc;
-  st = kStNotLeader;
-  if (pi != 0) {
-    st = mask_out_of_range<P>(m, la);
-    const TableRuns R{&t, h, cw & ~kConfRuns};
-    out = runs_best<P>(R, kTableMaxRuns, pi, la, lc, m, st);
+  if (pi == 0) {
+    st = kStNotLeader;
+    return kI64Min;
   }
-  if (out > lc) table_commit_one(t, h, pr, out);
-  return out - lc;
+  st = mask_out_of_range<P>(m, la);
+  const int64_t s = rs > pi ? rs : pi;
+  const int64_t e = nx == kI64Max ? la : nx - 1;
+  return run_candidate<P>(m, cw, s, e < la ? e : la, st);
 }
 
 template <int P>
-__global__ __launch_bounds__(kTableBlock) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
+__global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
   constexpr uint32_t kWaves = kTableBlock / 64;
-  __shared__ uint32_t wave_cnt[kWaves];
-  __shared__ uint32_t blk_base;
+  __shared__ uint32_t wave_cnt[kWaves];   // fast-path commits per wave
+  __shared__ uint32_t wave_def[kWaves];   // flagged groups per wave
+  __shared__ uint32_t deferred[kWaves][128];
+  __shared__ uint64_t staged[kWaves][128];  // fast-path list entries, wave-compacted
+  __shared__ uint64_t walk_staged[kTableBlockGroups];  // run-walk list entries
+  __shared__ uint32_t walk_n;
+  __shared__ uint32_t blk_base, blk_walk;
   const uint32_t pairs = (t.G + 1) >> 1;  // ld covers the pad group of an odd G (not a leader)
   const uint32_t tt = blockIdx.x * kTableBlock + threadIdx.x;
   const uint32_t g = tt << 1;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
   bool c0 = false, c1 = false, f0 = false, f1 = false;
   uint64_t e0 = 0, e1 = 0;
   if (tt < pairs) {
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(kTableBlock) JRQ_SGPRS_8WAVES void table_epoch_kern
     decide_single<P>(pi0, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
     decide_single<P>(pi1, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
     // a group with a conf change inside its pending window (JRQ_CONF_RUNS) is decided again
-    // below with its runs; its single-conf result here is discarded
+    // in the second phase with its runs; its single-conf result here is discarded
     c0 = !f0 && o0 > lc.x;  // decide_single returns lastCommitted unless a commit happened
     c1 = !f1 && o1 > lc.y;
     if (c0 && c1) {
@@ -136,42 +137,67 @@ __global__ __launch_bounds__(kTableBlock) JRQ_SGPRS_8WAVES void table_epoch_kern
     e0 = (static_cast<uint64_t>(o0 - pi0 + 1) << 32) | g;
     e1 = (static_cast<uint64_t>(o1 - pi1 + 1) << 32) | (g + 1);
   }
-  // flagged groups walk their conf runs in the lane that holds them, after the fast path's
-  // registers are dead (skipped by a wave none of whose groups is flagged).
-  // No workgroup barrier: a barrier here measured +4.7 us per 1M-group epoch
-  // (tools/table_probe.hip).
-  if (__builtin_expect(f0, 0)) {
-    int64_t pi;
-    uint8_t st;
-    const int64_t d = table_runs_one<P>(t, g, pi, st);
-    if (t.status) t.status[g] = st;
-    c0 = d > 0;
-    e0 = (static_cast<uint64_t>(t.lc[g] - pi + 1) << 32) | g;
+  // list entries and flagged groups -> the wave's slices of LDS (ballot prefixes, no atomics)
+  const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
+  const uint64_t bf0 = __ballot(f0), bf1 = __ballot(f1);
+  if (c0) staged[w][__popcll(b0 & below)] = e0;
+  if (c1) staged[w][__popcll(b0) + __popcll(b1 & below)] = e1;
+  if (f0) deferred[w][__popcll(bf0 & below)] = g;
+  if (f1) deferred[w][__popcll(bf0) + __popcll(bf1 & below)] = g + 1;
+  if (lane == 0) {
+    wave_cnt[w] = __popcll(b0) + __popcll(b1);
+    wave_def[w] = __popcll(bf0) + __popcll(bf1);
   }
-  if (__builtin_expect(f1, 0)) {
-    int64_t pi;
-    uint8_t st;
-    const int64_t d = table_runs_one<P>(t, g + 1, pi, st);
-    if (t.status) t.status[g + 1] = st;
-    c1 = d > 0;
-    e1 = (static_cast<uint64_t>(t.lc[g + 1] - pi + 1) << 32) | (g + 1);
+  if (threadIdx.x == 0) walk_n = 0;
+  __syncthreads();
+  // second phase: the workgroup's flagged groups, packed four lanes each (one per conf run)
+  // onto the first lanes, walk their runs -- ~1% of groups flagged then costs one short pass
+  // of one or two waves per workgroup (the walk is VALU-heavy: one per wave, or one per
+  // lane with the runs in a loop, measured +8..+12 us per 1M-group epoch)
+  uint32_t nd = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < kWaves; ++u) nd += wave_def[u];
+  if (__builtin_expect(nd != 0, 0)) {
+    for (uint32_t base = 0; base < nd * kTableMaxRuns; base += kTableBlock) {
+      const uint32_t q = base + threadIdx.x, i = q / kTableMaxRuns, r = q % kTableMaxRuns;
+      const bool act = i < nd;
+      int64_t cand = kI64Min, pr = 0, lc = 0, pi = 0;
+      uint8_t st = 0;
+      uint32_t h = 0;
+      if (act) {
+        uint32_t k = i, u = 0;
+        while (k >= wave_def[u]) k -= wave_def[u++];
+        h = deferred[u][k];
+        cand = table_run_lane<P>(t, h, r, pr, lc, pi, st);
+      }
+      cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 1)));
+      cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 2)));
+      uint32_t s32 = st;
+      s32 |= __shfl_xor(s32, 1);
+      s32 |= __shfl_xor(s32, 2);
+      if (act && r == 0) {
+        if (t.status) t.status[h] = static_cast<uint8_t>(s32);
+        if (cand > lc) {  // pi == 0 (not the leader) returned kI64Min
+          table_commit_one(t, h, pr, cand);
+          walk_staged[atomicAdd(&walk_n, 1u)] = (static_cast<uint64_t>(cand - pi + 1) << 32) | h;
+        }
+      }
+    }
+    __syncthreads();
   }
-  // compaction: lane-major order inside a wave, waves in order inside the workgroup; one
+  // compaction: fast-path entries in (wave, lane) order, then the run walk's; one
   // 64-bit atomic per workgroup ({workgroups done << 32 | entries}) on its segment's counter
   // reserves the workgroup's slice, and the last workgroup of a segment publishes its count
   // and re-zeroes the counter
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
-  const uint64_t below = (1ull << lane) - 1ull;
-  const uint32_t pre = __popcll(b0 & below) + __popcll(b1 & below);
-  if (lane == 0) wave_cnt[w] = __popcll(b0) + __popcll(b1);
-  __syncthreads();
   const uint32_t seg = blockIdx.x % kTableSegments;
   if (threadIdx.x == 0) {
     uint32_t tot = 0;
     for (uint32_t u = 0; u < kWaves; ++u) tot += wave_cnt[u];
+    blk_walk = tot;
+    tot += walk_n;
     const unsigned long long old = atomicAdd(t.ctr + seg, (1ull << 32) | tot);
     blk_base = seg * t.seg_cap + static_cast<uint32_t>(old);
+    blk_walk += blk_base;
     const uint32_t seg_blocks = (gridDim.x - seg + kTableSegments - 1) / kTableSegments;
     if (static_cast<uint32_t>(old >> 32) + 1u == seg_blocks) {  // the segment is complete
       t.n_changed[seg] = static_cast<uint32_t>(old) + tot;
@@ -179,10 +205,13 @@ __global__ __launch_bounds__(kTableBlock) JRQ_SGPRS_8WAVES void table_epoch_kern
     }
   }
   __syncthreads();
-  uint32_t pos = blk_base + pre;
+  uint32_t pos = blk_base;
   for (uint32_t u = 0; u < w; ++u) pos += wave_cnt[u];
-  if (c0) t.changed[pos++] = e0;
-  if (c1) t.changed[pos] = e1;
+  const uint32_t nw = wave_cnt[w];
+  if (lane < nw) t.changed[pos + lane] = staged[w][lane];
+  if (lane + 64 < nw) t.changed[pos + lane + 64] = staged[w][lane + 64];
+  if (__builtin_expect(nd != 0, 0))
+    for (uint32_t i = threadIdx.x; i < walk_n; i += kTableBlock) t.changed[blk_walk + i] = walk_staged[i];
 }
 
 // Group headers: one lane per header (a group appears at most once per call).
