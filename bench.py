@@ -796,8 +796,9 @@ def leg_v2(ctx, args, c5state):
         eng.v2_decode_verify_dev(d_rec, d_roff, v2_out)
     ms, _ = ctx.timed(v2_step, max(10, args.steps), 2)
     cor = v2_out["corrupt"].cpu().numpy().astype(bool)
-    ok = bool((v2_out["status"].cpu().numpy() == 0).all()) and bool(np.array_equal(cor, flip))
+    ok = None  # the stored checksums are the oracle's: nothing to compare without it
     if ctx.oracle_checks:
+        ok = bool((v2_out["status"].cpu().numpy() == 0).all()) and bool(np.array_equal(cor, flip))
         ok = ok and bool(np.array_equal(v2_out["computed"].cpu().numpy().view(np.uint64), expected))
     sample_ok = None
     if ctx.oracle_checks:  # the oracle decoder on the first 512 records

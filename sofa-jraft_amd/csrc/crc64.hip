@@ -358,9 +358,19 @@ struct SegWalk {
 // (hash_regs) instead of re-reading them from L2 (hash_global).  Faster when boundaries are
 // frequent and unaligned (V2 records, ragged batches), but the extra live ranges spill a few
 // VGPRs at the 128-VGPR budget, which costs ~9 % on boundary-free aligned batches.
+// Entry boundaries of a wave's window, cached in LDS (the rest of the 160 KiB next to the
+// 128 KiB of tables): offsets[eb .. eb + kOffWin) of the window's first entry eb, as u32
+// bytes from the window start (0xFFFFFFFF: 4 GiB or more past it).  An event then looks its
+// next boundary up in LDS instead of global memory: a global load there made every entry end
+// wait for the wave's whole in-flight prefetch ring (vmcnt is in order) -- small entries
+// (C1, V2 ranges) are all events.
+constexpr uint32_t kOffWin = 512;
+static_assert(kCrcLdsBytes + (kCrcBlock / 64) * kOffWin * 4 <= 160 * 1024, "LDS budget");
+
 template <bool kRegs>
 __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
+  __shared__ uint32_t offwin[kCrcBlock / 64][kOffWin];
   const char* lds = reinterpret_cast<const char*>(lds_tab);
 
   // Build the replicated LDS image of the slice tables (a.slice = R0, R1, R2, R3).
@@ -428,6 +438,25 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
       const uint64_t d = v - s0;
       return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(d);
     };
+    uint32_t* const win = offwin[L0 >> 6];
+    uint32_t eb = 0, wcnt = 0;  // the LDS window: entries [eb, eb + wcnt)
+    // rel(E(e)) / E(e) through the window when it holds e
+    auto relE = [&](uint32_t e) -> uint32_t {
+      const uint32_t i = e - eb;
+      if (i < wcnt) {
+        const uint32_t v = win[i];
+        return v == 0xFFFFFFFFu ? v : v - lane_off;
+      }
+      return rel(E(e));
+    };
+    auto absE = [&](uint32_t e) -> uint64_t {
+      const uint32_t i = e - eb;
+      if (i < wcnt) {
+        const uint32_t v = win[i];
+        if (v != 0xFFFFFFFFu) return wbase + v;
+      }
+      return E(e);
+    };
 
     // ---- segment setup, before this wave's first loads (short memory queues) ----
     SegWalk sw;
@@ -446,7 +475,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     // ring (vmcnt(0)) at the top of every iteration.
     auto start_entry = [&]() {
       while (sw.cur < n) {
-        sw.cur_end = rel(E(sw.cur + 1));
+        sw.cur_end = relE(sw.cur + 1);
         if (sw.cur_end != sw.pos || !(sw.pos < S || (sw.flags & SegWalk::kLastSeg))) break;
         emit(a, sw.cur, 0);  // crc64 of no bytes
         ++sw.cur;
@@ -457,12 +486,26 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
         sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
       }
     };
+    uint32_t e0 = 0;
+    if (!(sw.flags & SegWalk::kDone))
+      e0 = interp_lower_bound(off, n, base, total, s0 + sw.pos - D + base);
+    // fill the wave's LDS window from its first lane's entry (lane 0 is never done here: the
+    // chunk's first segment exists), one coalesced pass of up to kOffWin offsets
+    eb = __builtin_amdgcn_readfirstlane(e0);  // wave-uniform (SGPRs): every lane is active
+    wcnt = __builtin_amdgcn_readfirstlane(n + 1 - eb < kOffWin ? n + 1 - eb : kOffWin);
+    for (uint32_t i = L - L0; i < wcnt; i += 64) {
+      const uint64_t d = E(eb + i) - wbase;
+      win[i] = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(d);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (!(sw.flags & SegWalk::kDone)) {
-      const uint32_t e = interp_lower_bound(off, n, base, total, s0 + sw.pos - D + base);
-      if (e > 0 && E(e) > s0 + sw.pos) {  // entry e-1 began in an earlier segment
+      const uint32_t e = e0;
+      if (e > 0 && absE(e) > s0 + sw.pos) {  // entry e-1 began in an earlier segment
         sw.cur = e - 1;
         sw.flags &= ~SegWalk::kStarted;
-        sw.cur_end = rel(E(e));
+        sw.cur_end = relE(e);
         sw.next = sw.cur_end < sw.hi ? sw.cur_end : sw.hi;
       } else {
         sw.cur = e;
@@ -471,7 +514,9 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     }
 
     // An event at pos == next: the entry ends (emit / hand off its tail piece), or the
-    // segment ends inside the entry (hand off a shifted head/middle piece).
+    // segment ends inside the entry (hand off a shifted head/middle piece).  `mem` records
+    // that the walk read global memory (see process()).
+    bool mem = false;
     auto event = [&]() {
       const bool started = sw.flags & SegWalk::kStarted;
       if (sw.pos == sw.cur_end) {
@@ -479,7 +524,8 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
         if (started) {
           emit(a, sw.cur, v);
         } else {  // tail piece: this segment is the entry's last
-          const uint64_t first = E(sw.cur) / S;
+          mem = true;
+          const uint64_t first = absE(sw.cur) / S;
           if (k - first + 1 <= kMaxSlotParts)
             a.piece_tail[k] = v;
           else
@@ -490,9 +536,10 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
         ++sw.cur;
         start_entry();
       } else {  // pos == hi < entry end
-        const uint64_t ce = E(sw.cur + 1);
+        mem = true;
+        const uint64_t ce = absE(sw.cur + 1);
         const uint64_t c = crc_shift(crc_value(r), ce - (s0 + sw.hi), a.shift);
-        const uint64_t first = started ? k : E(sw.cur) / S;
+        const uint64_t first = started ? k : absE(sw.cur) / S;
         const uint64_t last = (ce - 1) / S;
         if (last - first + 1 <= kMaxSlotParts)  // head / middle piece
           a.piece_cont[k] = c;
@@ -557,7 +604,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     JRQ_LOAD_HALF(h0, 0u);
     JRQ_LOAD_HALF(h1, 1u);
 
-    // one half-round of this lane: segment bytes [hs, hs + 64)
     auto process = [&](uint32_t hh, const u32x4 (&v)[4]) {
       if (sw.flags & SegWalk::kDone) return;
       const uint32_t hs = hh * 64u, he = hs + 64u;
@@ -566,26 +612,29 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
         sw.pos = he;
       }
       if (sw.flags & SegWalk::kDone) return;
-      if (sw.pos == sw.next || sw.pos < he) {  // slow path: events / bytes from memory
+      if (sw.pos == sw.next || sw.pos < he) {  // slow path: events / partial halves
+        mem = false;
         while (!(sw.flags & SegWalk::kDone)) {
           if (sw.pos == sw.next) {
             event();
             continue;
           }
           if (sw.pos >= he) break;
+          if (sw.pos == hs && he <= sw.next) {
+            tb.step64(r, v, lds);
+            sw.pos = he;
+            continue;
+          }
           const uint32_t lim = he < sw.next ? he : sw.next;
-          // (not in the data's last half-round: a buffer load reaching past the data end
-          // returns zero for the whole 16 B, so those bytes come from memory)
-          if (kRegs && sw.pos >= hs && s0 + he <= span)
+          if (kRegs && sw.pos >= hs && s0 + he <= span) {
             hash_regs(tb, r, v, sw.pos - hs, lim - hs, lds);
-          else
+          } else {
             hash_global(tb, r, A, s0 + sw.pos, s0 + lim, lds);
+            mem = true;
+          }
           sw.pos = lim;
         }
-        // settle the slow path's own loads here (vmcnt(0); it waits on its last load
-        // anyway): a load the compiler still counts as in flight at the ring's loop head
-        // makes it drain the whole prefetch ring there on every iteration
-        __builtin_amdgcn_s_waitcnt(0x0F70);
+        if (__builtin_amdgcn_ballot_w64(mem)) __builtin_amdgcn_s_waitcnt(0x0F70);
       }
     };
 

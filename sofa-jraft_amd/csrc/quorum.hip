@@ -193,9 +193,11 @@ __global__ __launch_bounds__(256) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel
 // half-wave a chunk of C epochs of them -- and a scan over the chunk maxima in LDS stitches
 // the prefix.  Loads stay coalesced (32 consecutive groups = 256 B per row and epoch); small
 // tiles spread a 10k-group batch over all 256 CUs.
-// C epochs per half-wave (16 loads of P+1 words per lane at P = 3), at most 8 waves per
-// workgroup: a 10k-group batch is 313 workgroups, all resident at once (2 per CU) -- a 16-wave
-// workgroup fits once per CU and left a second, partial round of workgroups (13.5 vs 8.8 us).
+// A chunk = C epochs of the tile's T groups on T lanes (T = 32: two chunks per wave), at most
+// W waves per workgroup, super-chunks beyond that.  Product shape (EpochChunk): C epochs per
+// half-wave (16 loads of P+1 words per lane at P = 3), 8 waves: a 10k-group batch is 313
+// workgroups, all resident at once (2 per CU) -- a 16-wave workgroup fits once per CU and left
+// a second, partial round of workgroups (13.5 vs 8.8 us).
 template <int P>
 struct EpochChunk {
   static constexpr int kC = (16 / (P + 1)) < 1 ? 1 : ((16 / (P + 1)) > 8 ? 8 : 16 / (P + 1));
@@ -203,16 +205,17 @@ struct EpochChunk {
   static constexpr int kTile = 32;  // groups per workgroup
 };
 
-template <int P>
-__global__ __launch_bounds__(64 * EpochChunk<P>::kMaxWaves) void quorum_epochs_kernel(
-    JrqQuorumArgs a, uint32_t K, uint64_t match_eld, uint64_t la_eld) {
-  constexpr int C = EpochChunk<P>::kC;
-  constexpr uint32_t T = EpochChunk<P>::kTile;
-  __shared__ int64_t chunk_max[2 * EpochChunk<P>::kMaxWaves][T];
+template <int P, int C, int T, int W>
+__global__ __launch_bounds__(64 * W) void quorum_epochs_kernel(JrqQuorumArgs a, uint32_t K,
+                                                               uint64_t match_eld,
+                                                               uint64_t la_eld) {
+  static_assert(T == 32 || T == 64, "a chunk is a half or a whole wave");
+  constexpr uint32_t kPerWave = 64 / T;
+  __shared__ int64_t chunk_max[kPerWave * W][T];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t gl = lane & (T - 1u);
-  const uint32_t chunk = (threadIdx.x >> 6) * 2u + (lane >> 5);  // this half-wave's chunk
-  const uint32_t nchunks = (blockDim.x >> 6) * 2u;
+  const uint32_t chunk = (threadIdx.x >> 6) * kPerWave + lane / T;  // this lane's chunk
+  const uint32_t nchunks = (blockDim.x >> 6) * kPerWave;
   const uint32_t g = blockIdx.x * T + gl;
   const bool live = g < a.G;
   const int64_t pi0 = live ? a.pending_index[g] : 0;
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(64 * EpochChunk<P>::kMaxWaves) void quorum_epochs_k
           }
           run_max = v > run_max ? v : run_max;
         }
-        pre[c] = run_max;  // inclusive max over this half-wave's chunk
+        pre[c] = run_max;  // inclusive max over this chunk
       }
     }
     chunk_max[chunk][gl] = pre[C - 1];
@@ -415,23 +418,29 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
   return hipGetLastError();
 }
 
+// Waves per workgroup of quorum_epochs_kernel: enough for ceil(K / C) chunks, at most wmax.
+static inline uint32_t jrq_epochs_waves(uint32_t K, uint32_t C, uint32_t T, uint32_t wmax) {
+  const uint32_t per = 64 / T, chunks = (K + C - 1) / C, w = (chunks + per - 1) / per;
+  return w < wmax ? w : wmax;
+}
+
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum_epochs(
     const JrqQuorumArgs* args, uint32_t K, uint64_t match_eld, uint64_t la_eld, int num_cus,
     hipStream_t stream) {
   (void)num_cus;
-  // one workgroup per 32-group tile; two chunks of C epochs per wave (<= 16 waves), super-
-  // chunks beyond that
-  const dim3 grid(static_cast<unsigned>((static_cast<uint64_t>(args->G) + 31) / 32));
-  auto waves = [K](uint32_t C, uint32_t wmax) {
-    const uint32_t chunks = (K + C - 1) / C, w = (chunks + 1) / 2;
-    return dim3(64u * (w < wmax ? w : wmax));
-  };
+  // one workgroup per tile of groups; chunks of C epochs (two per wave), at most W waves,
+  // super-chunks beyond that
   switch (args->num_peers) {
-#define JRQ_CASE(P)                                                                         \
-  case P:                                                                                   \
-    hipLaunchKernelGGL(jrq::quorum_epochs_kernel<P>, grid, waves(jrq::EpochChunk<P>::kC, jrq::EpochChunk<P>::kMaxWaves), 0, \
-                       stream, *args, K, match_eld, la_eld);                                \
-    break;
+#define JRQ_CASE(P)                                                                           \
+  case P: {                                                                                   \
+    using E = jrq::EpochChunk<P>;                                                             \
+    const dim3 grid(static_cast<unsigned>((static_cast<uint64_t>(args->G) + E::kTile - 1) /   \
+                                          E::kTile));                                         \
+    const uint32_t w = jrq_epochs_waves(K, E::kC, E::kTile, E::kMaxWaves);                    \
+    hipLaunchKernelGGL((jrq::quorum_epochs_kernel<P, E::kC, E::kTile, E::kMaxWaves>), grid,   \
+                       dim3(64u * w), 0, stream, *args, K, match_eld, la_eld);                \
+    break;                                                                                    \
+  }
     JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
     JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
     JRQ_CASE(15) JRQ_CASE(16)

@@ -441,7 +441,7 @@ uint32_t GroupBatch::flush() {
   // pack the changes: one header per group whose header changed, else 8-B records -- two
   // passes over the dirty groups (count, then fill at per-chunk offsets), split across threads
   const size_t nd = dirtyList_.size();
-  const size_t kChunk = 1u << 14;
+  const size_t kChunk = 1u << 12;
   const size_t nchunks = (nd + kChunk - 1) / kChunk;
   std::vector<uint32_t> cs(nchunks + 1, 0), cr(nchunks + 1, 0);
   parallelFor(nchunks, 1, [&](size_t c0, size_t c1) {
@@ -507,9 +507,19 @@ uint32_t GroupBatch::flush() {
   throwIfError(jrq_table_epoch(table_, changed_.p, &n, nullptr), eng_->raw(), "jrq_table_epoch");
   const auto t2 = clk::now();
   // deliver: groups are independent, so their commits (closures, then onCommitted) run split
-  // across threads; one group's callbacks run on one thread, in order
-  parallelFor(n, 1u << 15, [&](size_t i0, size_t i1) {
+  // across threads; one group's callbacks run on one thread, in order.  A commit touches the
+  // group in several host arrays at random places: prefetch a few groups ahead.
+  parallelFor(n, 1u << 12, [&](size_t i0, size_t i1) {
+    constexpr size_t kAhead = 8;
     for (size_t i = i0; i < i1; ++i) {
+      if (i + kAhead < i1) {
+        const uint32_t h = static_cast<uint32_t>(changed_.p[i + kAhead]);
+        __builtin_prefetch(&pi_[h], 1);
+        __builtin_prefetch(&lc_[h], 1);
+        __builtin_prefetch(&nruns_[h], 0);
+        __builtin_prefetch(&closures_[h], 0);
+        __builtin_prefetch(&waiter_[h], 0);
+      }
       const uint64_t w = changed_.p[i];
       const uint32_t g = static_cast<uint32_t>(w);
       commitTo(g, pi_[g] - 1 + static_cast<int64_t>(w >> 32));

@@ -210,6 +210,35 @@ def test_full_size_configs(engine, oracle, cfg):
     np.testing.assert_array_equal(got, exp)
 
 
+def test_c5_step_full_size(engine, oracle):
+    """C5 as BASELINE states it, at full size: 64k regions x 3 replicas, one 16 KiB DATA entry
+    per region.  The step's two halves against the oracle: LogEntry.checksum() + isCorrupted()
+    over the 64k entries with 1/1024 of the stored checksums wrong (LogEntry.java:88-108,
+    156-158), and the commit epoch of the 64k groups (BallotBox.commitAt replayed through real
+    BallotBoxes, BallotBox.java:96-139)."""
+    c = W.CONFIGS["C5"]
+    n = c["groups"]
+    b = W.entry_batch(n, c["entry_bytes"], seed=W.SEED_BASE ^ 5)
+    exp = oracle.logentry_checksum_batch(b["etype"], b["index"], b["term"], None, b["payload"],
+                                         b["offsets"])
+    flip = np.zeros(n, bool)
+    flip[::1024] = True
+    out, corrupt = engine.logentry_checksum_batch(b["etype"], b["index"], b["term"], None,
+                                                  b["payload"], b["offsets"],
+                                                  expected=exp ^ flip.astype(np.uint64))
+    np.testing.assert_array_equal(out, exp)
+    np.testing.assert_array_equal(corrupt.astype(bool), flip)
+    assert int(corrupt.sum()) == n // 1024
+    q = W.quorum_batch("C5")
+    committed, status = engine.quorum_epoch(q["match"], q["pending_index"], q["last_appended"],
+                                            q["last_committed"], q["conf"])
+    ce, se, _ = oracle.quorum_epoch_replay(q["match"], q["pending_index"], q["last_appended"],
+                                           q["last_committed"], q["conf"], chunk=1024)
+    np.testing.assert_array_equal(committed, ce)
+    np.testing.assert_array_equal(status, se)
+    assert (committed > q["last_committed"]).sum() > n // 2
+
+
 # ---- streaming Checksum (RheaKV snapshot archive CRC64, §8f row 4) ----------------------------
 
 @pytest.mark.parametrize("S,max_len,start", [(1, 1, 0), (5, 40, 3), (300, 5000, 0),
