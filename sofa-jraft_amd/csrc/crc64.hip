@@ -458,7 +458,55 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
       return E(e);
     };
 
-    // ---- segment setup, before this wave's first loads (short memory queues) ----
+    // buffer descriptor: from the wave's first segment to the data end (loads past it
+    // return zero).  Its words pass through readfirstlane: the compiler then keeps it in
+    // SGPRs (otherwise it may hold it in VGPRs and wrap each load in a waterfall loop).
+    const uint64_t nrec = span - wbase;
+    const uintptr_t wptr = reinterpret_cast<uintptr_t>(A + wbase);
+    const uint32_t wlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wptr));
+    const uint32_t whi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wptr >> 32));
+    const uint32_t nr = __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(nrec > 0x7FFFFFFFull ? 0x7FFFFFFFull : nrec));
+
+    // Ring of three half-rounds (64 B per lane each, 16 VGPRs): two in flight while one is
+    // hashed.  Half-round h: load q reads 16 B of owner lane 16q + c at segment offset
+    // 64h + 16*row, so each row group reads 64 contiguous bytes of one owner per instruction.
+#if JRQ_CRC_RING == 4
+    u32x4 h0[4], h1[4], h2[4], h3[4];
+#else
+    u32x4 h0[4], h1[4], h2[4];
+#endif
+    // Each half-round's loads use a descriptor whose base is advanced by the half's offset
+    // (scalar adds), so the per-lane voffsets stay loop-invariant: no VALU address temps
+    // that the register allocator could place on a ring slot still being loaded (such a
+    // write-after-write made the compiler wait for the whole ring, vmcnt(0)).
+    const uint32_t qa0 = qbase, qa1 = qbase + 16u * WS, qa2 = qbase + 32u * WS,
+                   qa3 = qbase + 48u * WS;
+    const uint64_t wptr_u = (static_cast<uint64_t>(whi) << 32) | wlo;
+#define JRQ_LOAD_HALF(H, hh)                                                             \
+  do {                                                                                   \
+    const uint32_t ho = __builtin_amdgcn_readfirstlane((hh) * 64u);                      \
+    const uint64_t hp = wptr_u + ho;                                                     \
+    const uint32_t hlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp));      \
+    const uint32_t hhi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp >> 32)); \
+    uint32_t hn; /* nr - min(ho, nr) on the scalar unit (no VALU temp; see above) */     \
+    asm("s_min_u32 %0, %1, %2\n\ts_sub_u32 %0, %2, %0" : "=&s"(hn) : "s"(ho), "s"(nr));   \
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(                 \
+        reinterpret_cast<uint8_t*>((static_cast<uint64_t>(hhi) << 32) | hlo),            \
+        static_cast<short>(0), static_cast<int>(hn), 0x00020000);                        \
+    H[0] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa0, 0, JRQ_CRC_LOAD_AUX);                         \
+    H[1] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa1, 0, JRQ_CRC_LOAD_AUX);                         \
+    H[2] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa2, 0, JRQ_CRC_LOAD_AUX);                         \
+    H[3] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa3, 0, JRQ_CRC_LOAD_AUX);                         \
+    asm volatile("" ::: "memory");                                                       \
+  } while (0)
+    // the ring's first two half-rounds go out before the segment setup: the setup's dependent
+    // lookups (entry search, boundary window) then overlap the payload fetch instead of
+    // leaving HBM idle at the start of every chunk (short segments: C1, V2)
+    JRQ_LOAD_HALF(h0, 0u);
+    JRQ_LOAD_HALF(h1, 1u);
+
+    // ---- segment setup ----
     SegWalk sw;
     RState r{0u, 0u};
     sw.flags = SegWalk::kStarted | (k + 1 == nseg ? SegWalk::kLastSeg : 0u) |
@@ -549,48 +597,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
       }
     };
 
-    // buffer descriptor: from the wave's first segment to the data end (loads past it
-    // return zero).  Its words pass through readfirstlane: the compiler then keeps it in
-    // SGPRs (otherwise it may hold it in VGPRs and wrap each load in a waterfall loop).
-    const uint64_t nrec = span - wbase;
-    const uintptr_t wptr = reinterpret_cast<uintptr_t>(A + wbase);
-    const uint32_t wlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wptr));
-    const uint32_t whi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wptr >> 32));
-    const uint32_t nr = __builtin_amdgcn_readfirstlane(
-        static_cast<uint32_t>(nrec > 0x7FFFFFFFull ? 0x7FFFFFFFull : nrec));
-
-    // Ring of three half-rounds (64 B per lane each, 16 VGPRs): two in flight while one is
-    // hashed.  Half-round h: load q reads 16 B of owner lane 16q + c at segment offset
-    // 64h + 16*row, so each row group reads 64 contiguous bytes of one owner per instruction.
-#if JRQ_CRC_RING == 4
-    u32x4 h0[4], h1[4], h2[4], h3[4];
-#else
-    u32x4 h0[4], h1[4], h2[4];
-#endif
-    // Each half-round's loads use a descriptor whose base is advanced by the half's offset
-    // (scalar adds), so the per-lane voffsets stay loop-invariant: no VALU address temps
-    // that the register allocator could place on a ring slot still being loaded (such a
-    // write-after-write made the compiler wait for the whole ring, vmcnt(0)).
-    const uint32_t qa0 = qbase, qa1 = qbase + 16u * WS, qa2 = qbase + 32u * WS,
-                   qa3 = qbase + 48u * WS;
-    const uint64_t wptr_u = (static_cast<uint64_t>(whi) << 32) | wlo;
-#define JRQ_LOAD_HALF(H, hh)                                                             \
-  do {                                                                                   \
-    const uint32_t ho = __builtin_amdgcn_readfirstlane((hh) * 64u);                      \
-    const uint64_t hp = wptr_u + ho;                                                     \
-    const uint32_t hlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp));      \
-    const uint32_t hhi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp >> 32)); \
-    uint32_t hn; /* nr - min(ho, nr) on the scalar unit (no VALU temp; see above) */     \
-    asm("s_min_u32 %0, %1, %2\n\ts_sub_u32 %0, %2, %0" : "=&s"(hn) : "s"(ho), "s"(nr));   \
-    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(                 \
-        reinterpret_cast<uint8_t*>((static_cast<uint64_t>(hhi) << 32) | hlo),            \
-        static_cast<short>(0), static_cast<int>(hn), 0x00020000);                        \
-    H[0] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa0, 0, JRQ_CRC_LOAD_AUX);                         \
-    H[1] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa1, 0, JRQ_CRC_LOAD_AUX);                         \
-    H[2] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa2, 0, JRQ_CRC_LOAD_AUX);                         \
-    H[3] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa3, 0, JRQ_CRC_LOAD_AUX);                         \
-    asm volatile("" ::: "memory");                                                       \
-  } while (0)
     const uint32_t halves = __builtin_amdgcn_readfirstlane(rounds * 2);
     const uint32_t prog0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(j * halves));
     // prefetches past the chunk's last half-round re-read that half (L2-hot): the half
@@ -601,8 +607,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     // compiler still counts as in flight when the ring starts costs a vmcnt(0) at the top
     // of every ring iteration
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    JRQ_LOAD_HALF(h0, 0u);
-    JRQ_LOAD_HALF(h1, 1u);
 
     auto process = [&](uint32_t hh, const u32x4 (&v)[4]) {
       if (sw.flags & SegWalk::kDone) return;
