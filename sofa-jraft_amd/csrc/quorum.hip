@@ -216,30 +216,42 @@ __global__ __launch_bounds__(64 * W) void quorum_epochs_kernel(JrqQuorumArgs a, 
   const uint32_t gl = lane & (T - 1u);
   const uint32_t chunk = (threadIdx.x >> 6) * kPerWave + lane / T;  // this lane's chunk
   const uint32_t nchunks = (blockDim.x >> 6) * kPerWave;
-  const uint32_t g = blockIdx.x * T + gl;
+  // tiles in XCD-contiguous order: workgroups are dealt round-robin to the 8 XCDs, so block b
+  // takes tile (b % 8)'s run position b / 8 -- the tiles that share DRAM pages (8 per 2 KiB of
+  // a row) then go out from one XCD back to back (-4 %, tools/epochs_probe.hip mode 4)
+  const uint32_t nb = gridDim.x, xq = nb / 8, xr = nb % 8, xcd = blockIdx.x % 8;
+  const uint32_t tile = xcd * xq + (xcd < xr ? xcd : xr) + blockIdx.x / 8;
+  const uint32_t g = tile * T + gl;
   const bool live = g < a.G;
-  const int64_t pi0 = live ? a.pending_index[g] : 0;
-  const int64_t lc0 = live ? a.last_committed[g] : 0;
-  const uint64_t cw = live ? a.conf[g] : 0;
-  const bool runs = a.run_off != nullptr && (cw & kConfRuns);
-  const uint32_t r0 = runs ? a.run_off[g] : 0, r1 = runs ? a.run_off[g + 1] : 0;
+  // Every load is unconditional (a dead lane reads group 0, an epoch past K reads epoch K-1;
+  // both results are discarded): per-lane conditions around them made the compiler wait for
+  // each epoch's loads before issuing the next epoch's -- C round trips instead of one.
+  const uint32_t gs = live ? g : 0u;
+  const int64_t pi0 = live ? a.pending_index[gs] : 0;
+  const int64_t lc0 = live ? a.last_committed[gs] : 0;
+  const uint64_t cw = live ? a.conf[gs] : 0;
   int64_t carry = kI64Min;  // max v over the epochs of earlier super-chunks
   for (uint32_t base = 0; base < K; base += nchunks * C) {
     const uint32_t k0 = base + chunk * C;
     int64_t la[C], pre[C];
     uint8_t st[C];
+    bool runs;
+    uint32_t r0, r1;
     {
       int64_t m[C][P];
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const size_t k = k0 + c;
-        if (!live || k >= K) continue;
-        la[c] = __builtin_nontemporal_load(a.last_appended + k * la_eld + g);
+        const size_t k = k0 + c < K ? k0 + c : K - 1;
+        la[c] = __builtin_nontemporal_load(a.last_appended + k * la_eld + gs);
 #pragma unroll
         for (int p = 0; p < P; ++p)
           m[c][p] = __builtin_nontemporal_load(a.match + k * match_eld +
-                                               static_cast<size_t>(p) * a.match_ld + g);
+                                               static_cast<size_t>(p) * a.match_ld + gs);
       }
+      // conf runs of a flagged group: its CSR bounds, after the epoch loads are out
+      runs = a.run_off != nullptr && (cw & kConfRuns);
+      r0 = runs ? a.run_off[g] : 0;
+      r1 = runs ? a.run_off[g + 1] : 0;
       int64_t run_max = kI64Min;
 #pragma unroll
       for (int c = 0; c < C; ++c) {
@@ -268,7 +280,7 @@ __global__ __launch_bounds__(64 * W) void quorum_epochs_kernel(JrqQuorumArgs a, 
       if (u < chunk) excl = t > excl ? t : excl;
       all = t > all ? t : all;
     }
-    __syncthreads();  // chunk_max is rewritten by the next super-chunk
+    if (base + nchunks * C < K) __syncthreads();  // the next super-chunk rewrites chunk_max
     carry = all;
     if (!live) continue;
 #pragma unroll

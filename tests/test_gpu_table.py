@@ -62,9 +62,13 @@ def committed_from(changed, pi_before, lc_before):
     return out, g
 
 
-@pytest.mark.parametrize("P,G", [(5, 4096), (3, 3001), (16, 777), (1, 64)])
-def test_one_epoch_vs_replay(engine, oracle, P, G):
-    b = random_batch(1000 + P, G, P, run_prob=0.4)
+@pytest.mark.parametrize("P,G,runs", [(5, 4096, 0.4), (3, 3001, 0.4), (16, 777, 0.4), (1, 64, 0.4),
+                                      (5, 70001, 0.95)])
+def test_one_epoch_vs_replay(engine, oracle, P, G, runs):
+    """One epoch vs the BallotBox replay.  The last case has 35 workgroups (several per list
+    segment, a pad group) and nearly every group walking conf runs (many quad-walk passes
+    per workgroup)."""
+    b = random_batch(1000 + P, G, P, run_prob=runs)
     ce, se, _ = oracle.quorum_epoch_replay(b["match"], b["pending_index"], b["last_appended"],
                                            b["last_committed"], b["conf"], b["run_off"],
                                            b["run_start"], b["run_conf"], chunk=7)

@@ -45,7 +45,7 @@ def main():
     import bench
     tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
     os.makedirs(PROF, exist_ok=True)
-    res = {"tag": tag, "csrc_sha": bench.csrc_sha(), "correction": "2*FETCH_SIZE+WRITE_SIZE, KiB->B",
+    res = {"tag": tag, "csrc_sha": bench.csrc_sha(), "correction": "2*FETCH_SIZE+WRITE_SIZE (CRC rounds kernels: calibration factor*FETCH_SIZE), KiB->B",
            "kernel_stats": {}, "legs": collections.defaultdict(lambda: collections.defaultdict(dict))}
     st = os.path.join(OUT, "prof", "run_kernel_stats.csv")
     if os.path.exists(st):
