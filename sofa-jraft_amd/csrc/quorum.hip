@@ -101,12 +101,11 @@ __device__ __forceinline__ i64x2 ld2nt(const int64_t* p) {
 // the run walk then shares no registers with the fast path (occupancy of the common case).
 template <int P>
 __global__ __launch_bounds__(256) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
-  __shared__ uint32_t n_deferred;
-  __shared__ uint32_t deferred[512];
+  __shared__ uint32_t wave_def[4];
+  __shared__ uint32_t deferred[4][128];
   const uint32_t pairs = a.G >> 1;
   const uint32_t t = blockIdx.x * 256u + threadIdx.x;
-  if (threadIdx.x == 0) n_deferred = 0;
-  __syncthreads();
+  bool f0 = false, f1 = false;
   if (t < pairs) {
     const uint32_t g = t << 1;
     const i64x2 pi = ld2nt(a.pending_index + g);
@@ -117,8 +116,8 @@ __global__ __launch_bounds__(256) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel
 #pragma unroll
     for (int p = 0; p < P; ++p) m[p] = ld2nt(a.match + static_cast<size_t>(p) * a.match_ld + g);
     const bool runs = a.run_off != nullptr;
-    const bool f0 = runs && (static_cast<uint64_t>(cw.x) & kConfRuns);
-    const bool f1 = runs && (static_cast<uint64_t>(cw.y) & kConfRuns);
+    f0 = runs && (static_cast<uint64_t>(cw.x) & kConfRuns);
+    f1 = runs && (static_cast<uint64_t>(cw.y) & kConfRuns);
     int64_t m0[P], m1[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -140,28 +139,37 @@ __global__ __launch_bounds__(256) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel
       if (!f0) {
         a.committed[g] = o0;
         a.status[g] = s0;
-      } else {
-        deferred[atomicAdd(&n_deferred, 1u)] = g;
       }
       if (!f1) {
         a.committed[g + 1] = o1;
         a.status[g + 1] = s1;
-      } else {
-        deferred[atomicAdd(&n_deferred, 1u)] = g + 1;
       }
     }
   }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n_deferred; i += 256u) {  // up to 2 per lane
-    const uint32_t g = deferred[i];
-    int64_t m[P];
+  if (a.run_off != nullptr) {  // kernel-uniform: no LDS list and no barrier without run tables
+    // flagged groups -> the wave's slice of the list (ballot prefixes, no atomics, no
+    // initialising barrier in front of the loads)
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
+    if (f0) deferred[w][__popcll(b0 & below)] = t << 1;
+    if (f1) deferred[w][__popcll(b0) + __popcll(b1 & below)] = (t << 1) + 1;
+    if (lane == 0) wave_def[w] = __popcll(b0) + __popcll(b1);
+    __syncthreads();
+    const uint32_t nd = wave_def[0] + wave_def[1] + wave_def[2] + wave_def[3];
+    for (uint32_t i = threadIdx.x; i < nd; i += 256u) {  // up to 2 per lane
+      uint32_t k = i, u = 0;
+      while (k >= wave_def[u]) k -= wave_def[u++];
+      const uint32_t g = deferred[u][k];
+      int64_t m[P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
-    int64_t out;
-    uint8_t st;
-    decide_runs<P>(a, g, a.pending_index[g], a.last_appended[g], a.last_committed[g], m, out, st);
-    a.committed[g] = out;
-    a.status[g] = st;
+      for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
+      int64_t out;
+      uint8_t st;
+      decide_runs<P>(a, g, a.pending_index[g], a.last_appended[g], a.last_committed[g], m, out, st);
+      a.committed[g] = out;
+      a.status[g] = st;
+    }
   }
   // odd G: the last group goes through the scalar decision
   if ((a.G & 1u) && t == 0) {
