@@ -57,6 +57,7 @@ struct jrq_engine {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   uint64_t* slice = nullptr;  // [kSliceTables][256]
+  uint64_t* xinv = nullptr;   // [8][256] TI[i][b] = b * x^(8i - 64) mod P (v2_decode.hip)
   uint64_t* shift = nullptr;  // [kShiftTables][8][256]
   uint64_t* acc = nullptr;    // straddler accumulators
   uint32_t* cnt = nullptr;    // straddler counters
@@ -73,7 +74,7 @@ struct jrq_engine {
   uint32_t crc_seg_map = 1;  // JRQ_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
-  DevBuf stage[24];  // 0-13 host-variant staging, 14 stream-update chunk CRCs, 16-19 AppendEntries scratch, 21-23 V2 decode scratch
+  DevBuf stage[25];  // 0-13 host-variant staging, 14 stream-update chunk CRCs, 16-19 AppendEntries scratch, 21-24 V2 decode scratch
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = -1;
   std::string err;
@@ -128,7 +129,9 @@ uint64_t mulmod(uint64_t a, uint64_t b) {
 //   T1[i]  = T0[i] advanced by one zero byte
 //   slice  = { bswap(T0) .. bswap(T7) }  (reversed-domain slice-by-8)
 //   shift[t][k][i] = (i * x^(8k)) * x^(8 * 2^t) mod G
-void build_tables(std::vector<uint64_t>& slice, std::vector<uint64_t>& shift) {
+//   xinv[k][i]     = i * x^(8k - 64) mod G   (x^-1 = x^63 + (p + 1) / x for G = x^64 + p)
+void build_tables(std::vector<uint64_t>& slice, std::vector<uint64_t>& shift,
+                  std::vector<uint64_t>& xinv) {
   uint64_t t[jrq::kSliceTables][256];
   for (int i = 0; i < 256; ++i) {
     uint64_t c = static_cast<uint64_t>(i) << 56;
@@ -148,6 +151,14 @@ void build_tables(std::vector<uint64_t>& slice, std::vector<uint64_t>& shift) {
         shift[(static_cast<size_t>(t) * 8 + k) * 256 + i] = mulmod(static_cast<uint64_t>(i) << (8 * k), K);
     K = mulmod(K, K);  // x^(8 * 2^(t+1))
   }
+  const uint64_t xm1 = (1ull << 63) | ((jrq::kCrcPoly ^ 1ull) >> 1);
+  xinv.resize(8 * 256);
+  for (int k = 0; k < 8; ++k)
+    for (int i = 0; i < 256; ++i) {
+      uint64_t v = static_cast<uint64_t>(i);
+      for (int b = 0; b < 64 - 8 * k; ++b) v = (v >> 1) ^ ((v & 1ull) ? xm1 : 0ull);
+      xinv[k * 256 + i] = v;
+    }
 }
 
 int ensure_stage(jrq_engine* e, int slot, size_t bytes, void** out) {
@@ -265,8 +276,8 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
     e->crc_seg_bytes = std::strtoull(v, nullptr, 10);
   e->scratch_len = static_cast<uint32_t>(2ull * e->crc_grid * jrq::kCrcBlock + 2);
   int rc = JRQ_OK;
-  std::vector<uint64_t> slice, shift;
-  build_tables(slice, shift);
+  std::vector<uint64_t> slice, shift, xinv;
+  build_tables(slice, shift, xinv);
   auto try_hip = [&](hipError_t s, const char* what) {
     if (s != hipSuccess && rc == JRQ_OK) rc = fail(nullptr, JRQ_E_HIP, "%s: %s", what, hipGetErrorString(s));
   };
@@ -274,6 +285,7 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   e->stream = e->own_stream;
   try_hip(hipMalloc(&e->slice, slice.size() * 8), "hipMalloc(slice)");
   try_hip(hipMalloc(&e->shift, shift.size() * 8), "hipMalloc(shift)");
+  try_hip(hipMalloc(&e->xinv, xinv.size() * 8), "hipMalloc(xinv)");
   // acc/cnt: [scratch_len] entry slots + [2 * (scratch_len / 64 + 2)] 64-segment group slots
   // + [2 * (scratch_len / 4096 + 2)] 64-group supergroup slots (crc64.hip straddle_piece)
   const size_t slots = e->scratch_len + 2 * (e->scratch_len / 64 + 2) + 2 * (e->scratch_len / 4096 + 2);
@@ -285,6 +297,7 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
     try_hip(hipMemset(e->fan_ctr, 0, 16), "zero fan_ctr");
     try_hip(hipMemcpy(e->slice, slice.data(), slice.size() * 8, hipMemcpyHostToDevice), "upload slice");
     try_hip(hipMemcpy(e->shift, shift.data(), shift.size() * 8, hipMemcpyHostToDevice), "upload shift");
+    try_hip(hipMemcpy(e->xinv, xinv.data(), xinv.size() * 8, hipMemcpyHostToDevice), "upload xinv");
     try_hip(hipMemset(e->acc, 0, slots * 8), "zero acc");
     try_hip(hipMemset(e->cnt, 0, slots * 4), "zero cnt");
   }
@@ -306,6 +319,7 @@ void jrq_destroy(jrq_engine* e) {
     if (b.p) (void)hipFree(b.p);
   if (e->slice) (void)hipFree(e->slice);
   if (e->shift) (void)hipFree(e->shift);
+  if (e->xinv) (void)hipFree(e->xinv);
   if (e->acc) (void)hipFree(e->acc);
   if (e->cnt) (void)hipFree(e->cnt);
   if (e->pieces) (void)hipFree(e->pieces);
@@ -878,13 +892,16 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
   int rc;
   void *partial, *off2, *crc2;
   if ((rc = ensure_stage(e, 21, static_cast<size_t>(N) * 8, &partial))) return rc;
-  if ((rc = ensure_stage(e, 22, (2 * static_cast<size_t>(N) + 2) * 8, &off2))) return rc;
-  if ((rc = ensure_stage(e, 23, (2 * static_cast<size_t>(N) + 1) * 8, &crc2))) return rc;
+  if ((rc = ensure_stage(e, 22, (static_cast<size_t>(N) + 2) * 8, &off2))) return rc;
+  if ((rc = ensure_stage(e, 23, (static_cast<size_t>(N) + 1) * 8, &crc2))) return rc;
+  void* edges;  // per record: header CRC, trailer CRC, lengths
+  if ((rc = ensure_stage(e, 24, static_cast<size_t>(N) * 24, &edges))) return rc;
   JrqV2Args v{};
   v.rec = rec;
   v.off = off;
   v.n = N;
   v.slice = e->slice;
+  v.xinv = e->xinv;
   v.status = status;
   v.type = type;
   v.index = index;
@@ -899,14 +916,18 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
   v.partial = static_cast<uint64_t*>(partial);
   v.off2 = static_cast<uint64_t*>(off2);
   v.crc2 = static_cast<const uint64_t*>(crc2);
+  v.hcrc = static_cast<uint64_t*>(edges);
+  v.tcrc = v.hcrc + N;
+  v.lens = v.tcrc + N;
   JRQ_HIP(e, jrq_launch_v2_parse(&v, e->stream));
-  // data ranges interleaved with the gaps between them: one streaming pass over the records
+  // one range per record from its data start (the leading header first): one streaming pass
+  // over the records, one entry boundary per record (v2_finish recovers the data CRCs)
   JrqCrcArgs a{};
   a.payload = rec;
   a.offsets = v.off2;
-  a.n = 2 * N + 1;
+  a.n = N + 1;
   a.out = static_cast<uint64_t*>(crc2);
-  a.regs_slowpath = 1;  // two unaligned boundaries per record
+  a.regs_slowpath = 1;  // an unaligned boundary per record
   if ((rc = crc_dispatch(e, a, 0))) return rc;
   JRQ_HIP(e, jrq_launch_v2_finish(&v, e->num_cus, e->stream));
   return JRQ_OK;

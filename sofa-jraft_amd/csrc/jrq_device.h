@@ -152,7 +152,8 @@ struct JrqV2Args {
   const uint8_t* rec;
   const uint64_t* off;     // [n+1]
   uint32_t n;
-  const uint64_t* slice;   // engine slice tables (R0 = bswap of the CRC64 byte table)
+  const uint64_t* slice;   // engine slice tables (R_j = bswap of T_j = i * x^(64 + 8j))
+  const uint64_t* xinv;    // engine [8][256]: i * x^(8k - 64) mod P
   uint8_t* status;
   uint8_t* type;
   int64_t* index;
@@ -165,8 +166,11 @@ struct JrqV2Args {
   uint64_t* computed;
   uint8_t* corrupt;
   uint64_t* partial;       // scratch [n]
-  uint64_t* off2;          // scratch [2n+2]
-  const uint64_t* crc2;    // scratch [2n+1] (CRC of the interleaved ranges)
+  uint64_t* off2;          // scratch [n+2]: record i's range = [off2[i+1], off2[i+2])
+  const uint64_t* crc2;    // scratch [n+1] (CRC of the ranges; range 0 = the leading header)
+  uint64_t* hcrc;          // scratch [n] CRC of each record's bytes before its data
+  uint64_t* tcrc;          // scratch [n] CRC of each record's bytes after its data
+  uint64_t* lens;          // scratch [n] header length << 32 | trailer length
 };
 
 struct JrqQuorumArgs {

@@ -24,7 +24,8 @@
 //   crc64      the batched CRC kernels (crc64.hip) over those 2N+1 ranges: one pass over the
 //              record bytes at streaming bandwidth (gap ranges -- headers -- are hashed too and
 //              dropped; they are a few dozen bytes per record).
-//   v2_finish  computed = partial ^ crc(data range), corrupt = has_checksum && stored != computed.
+//   v2_finish  computed = partial ^ crc(data), the data CRC recovered from its range's CRC by
+//              linearity (see v2_finish), corrupt = has_checksum && stored != computed.
 //
 // A peer string is hashed as stored when it is already what PeerId.toString() would render
 // from it (V2Encoder always writes toString(), so this is every record it produced).  A
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r == 0) {
     a.off2[0] = a.off[0];
-    a.off2[2ull * a.n + 1] = a.off[a.n];
+    a.off2[a.n + 1] = a.off[a.n];
   }
   if (r >= a.n) return;
   const uint64_t b0 = a.off[r];
@@ -311,15 +312,67 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
   a.data_off[r] = b0 + static_cast<uint64_t>(doff);
   a.data_len[r] = static_cast<uint64_t>(dlen);
   if (a.peer_counts) a.peer_counts[r] = counts;
-  a.off2[2ull * r + 1] = b0 + static_cast<uint64_t>(doff);
-  a.off2[2ull * r + 2] = b0 + static_cast<uint64_t>(doff + dlen);
+  a.off2[r + 1] = b0 + static_cast<uint64_t>(doff);  // a failed record: its start
+  // CRCs of the bytes around the data (v2_finish removes them from the range CRCs)
+  uint64_t hc = 0, tc = 0;
+  uint64_t hl = 0, tl = 0;
+  if (st == kV2Ok) {
+    ChunkReader rd(rec, L);
+    hl = static_cast<uint64_t>(doff);
+    tl = static_cast<uint64_t>(L - doff - dlen);
+    for (int64_t p = 0; p < doff; ++p) hc = T[((hc >> 56) ^ rd.at(p)) & 0xFFu] ^ (hc << 8);
+    for (int64_t p = doff + dlen; p < L; ++p) tc = T[((tc >> 56) ^ rd.at(p)) & 0xFFu] ^ (tc << 8);
+  }
+  a.hcrc[r] = hc;
+  a.tcrc[r] = tc;
+  a.lens[r] = (hl << 32) | tl;
 }
 
+// The CRC pass hashes one range per record, [data start, next record's data start): the data,
+// then a suffix of k bytes -- the record's trailer (checksum / learner fields) and the next
+// record's header.  CRC64 here is linear (init 0, xorout 0) and x is invertible mod P
+// (P(0) = 1), so
+//   crc(suffix) = crc(trailer) * x^(8 |next header|) ^ crc(next header)
+//   crc(data)   = (crc(range) ^ crc(suffix)) * x^(-8k)
+// with the trailer / header CRCs from v2_parse (it reads those bytes anyway).  A multiply by
+// x^(+-64) is one lookup per register byte: T_i[b] = b x^(64 + 8i) (the engine's slice tables,
+// un-swapped), TI_i[b] = b x^(8i - 64) (engine xinv); single bytes use T_0 / TI_7.  One entry
+// boundary per record instead of two: the CRC pass takes 310 instead of 330 us on 64k x 16 KiB
+// records (tools/v2_boundary_probe.py).
 __global__ __launch_bounds__(256) void v2_finish(JrqV2Args a) {
+  __shared__ uint64_t Tf[8][256], Ti[8][256];
+  for (uint32_t e = threadIdx.x; e < 8 * 256; e += blockDim.x) {
+    Tf[e >> 8][e & 255u] = bswap64(a.slice[e]);
+    Ti[e >> 8][e & 255u] = a.xinv[e];
+  }
+  __syncthreads();
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
     const bool ok = a.status[r] == kV2Ok;
-    const uint64_t c = ok ? (a.partial[r] ^ a.crc2[2ull * r + 1]) : 0;
+    uint64_t c = 0;
+    if (ok) {
+      const bool more = r + 1 < a.n;
+      uint64_t h = more ? a.lens[r + 1] >> 32 : 0;  // next record's header (0 if it failed)
+      const uint64_t k = (a.lens[r] & 0xFFFFFFFFull) + h;
+      uint64_t s = a.tcrc[r];
+      for (; h >= 8; h -= 8) {  // s * x^64
+        uint64_t t = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t ^= Tf[i][(s >> (8 * i)) & 0xFFu];
+        s = t;
+      }
+      for (; h > 0; --h) s = (s << 8) ^ Tf[0][s >> 56];
+      s ^= more ? a.hcrc[r + 1] : 0;
+      uint64_t d = a.crc2[r + 1] ^ s, m = k;
+      for (; m >= 8; m -= 8) {  // d * x^-64
+        uint64_t t = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t ^= Ti[i][(d >> (8 * i)) & 0xFFu];
+        d = t;
+      }
+      for (; m > 0; --m) d = (d >> 8) ^ Ti[7][d & 0xFFu];
+      c = a.partial[r] ^ d;  // d = crc(data)
+    }
     a.computed[r] = c;
     a.corrupt[r] = (ok && a.has_checksum[r] && a.stored[r] != c) ? 1 : 0;
   }
@@ -336,8 +389,10 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_v2_parse(
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_v2_finish(
     const JrqV2Args* a, int num_cus, hipStream_t stream) {
+  // each workgroup stages 32 KiB of tables in LDS: one record per lane, at most 2 workgroups
+  // per CU (a grid of 8 per CU re-read 64 MiB of tables from L2 for 64k records)
   uint32_t blocks = (a->n + 255) / 256;
-  const uint32_t cap = static_cast<uint32_t>(num_cus) * 8u;
+  const uint32_t cap = static_cast<uint32_t>(num_cus) * 2u;
   if (blocks > cap) blocks = cap;
   hipLaunchKernelGGL(jrq::v2_finish, dim3(blocks ? blocks : 1), dim3(256), 0, stream, *a);
   return hipGetLastError();

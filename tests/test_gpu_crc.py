@@ -304,3 +304,23 @@ def test_stream_update_errors_and_empty(engine):
     with pytest.raises(ValueError):
         engine.crc64_stream_update(np.zeros(3, np.uint64), np.zeros(4, np.uint8),
                                    np.array([0, 4], np.uint64))
+
+
+@pytest.mark.parametrize("offs", [[0, 9, 4, 16], [5, 2, 16], [4, 9, 12, 3]])
+def test_batch_offsets_must_be_monotone(engine, offs):
+    """jrq_crc64_batch / jrq_logentry_checksum_batch reject offsets that go backwards (or
+    below offsets[0]) with JRQ_E_INVALID before staging anything: the kernels' segment walk
+    and boundary search assume sorted offsets (include/jrq.h)."""
+    from jraft_amd._lib import JrqError
+    offs = np.array(offs, np.uint64)
+    n = len(offs) - 1
+    payload = np.arange(32, dtype=np.uint8)
+    with pytest.raises(JrqError, match="monotone"):
+        engine.crc64_batch(payload, offs)
+    with pytest.raises(JrqError, match="monotone"):
+        engine.logentry_checksum_batch(np.ones(n, np.uint8), np.arange(n), np.ones(n), None,
+                                       payload, offs)
+    # the engine stays usable after a refused call
+    ok = engine.crc64_batch(payload, np.array([0, 9, 16], np.uint64))
+    assert ok.shape == (2,)
+

@@ -228,3 +228,24 @@ def test_gpu_quorum_epochs_with_runs(engine, oracle, P, G, K):
     engine.synchronize()
     np.testing.assert_array_equal(c.cpu().numpy(), ce)
     np.testing.assert_array_equal(st.cpu().numpy(), se)
+
+
+def test_host_variant_rejects_bad_run_csr(engine):
+    """jrq_quorum_epoch checks the run table CSR on the host before staging it (run_off[0] =
+    0, monotone, run_off[G] = the number of runs): a bad one is JRQ_E_INVALID, not a device
+    read past the staged runs."""
+    from jraft_amd import JrqError
+    b = random_batch(5, 64, 3, run_prob=0.5)
+    args = (b["match"], b["pending_index"], b["last_appended"], b["last_committed"], b["conf"])
+    bad = b["run_off"].copy()
+    bad[10], bad[11] = bad[11] + 1, bad[10]          # not monotone
+    with pytest.raises(JrqError):
+        engine.quorum_epoch(*args, run_off=bad, run_start=b["run_start"], run_conf=b["run_conf"])
+    short = b["run_off"].copy()
+    short[-1] += 3                                   # past the runs given
+    with pytest.raises(JrqError):
+        engine.quorum_epoch(*args, run_off=short, run_start=b["run_start"], run_conf=b["run_conf"])
+    c, _ = engine.quorum_epoch(*args, run_off=b["run_off"], run_start=b["run_start"],
+                               run_conf=b["run_conf"])
+    assert c.shape == (64,)
+
