@@ -367,17 +367,16 @@ struct SegWalk {
 constexpr uint32_t kOffWin = 512;
 static_assert(kCrcLdsBytes + (kCrcBlock / 64) * kOffWin * 4 <= 160 * 1024, "LDS budget");
 
-// Workgroup size: 1024 threads (16 waves, 128 VGPRs each: the ring and the step trees spill a
-// few).  The register boundary path keeps more live state: at 768 threads (12 waves, ~160
-// VGPRs) it runs without spills, 6 % faster on V2 records (350 -> 333 us) -- the
-// boundary-free path stays at 1024, where 768 measured slower on C5 and C1.
-template <bool kRegs>
-constexpr uint32_t rounds_block() { return kRegs ? 768u : static_cast<uint32_t>(kCrcBlock); }
-
-template <bool kRegs>
-__global__ __launch_bounds__(rounds_block<kRegs>()) void crc64_rounds_kernel(JrqCrcArgs a) {
+// Workgroup size kBlock (one workgroup per CU: the LDS tables fill it).  At 1024 threads (16
+// waves) the 128-VGPR budget makes the ring and the step trees spill a few registers; fewer
+// waves run spill-free (512: ~155 VGPRs, 768: ~160) at the cost of half / three quarters of the
+// lanes, i.e. longer segments.  Measured (tools/ab_run.sh): the register boundary path at 768
+// (V2 records 350 -> 336 us); the boundary-free path at 512 when a batch has fewer entries than
+// lanes (C5 264 -> 255 us) and at 1024 otherwise (C1's 1 KiB segments: 512 is 3.5 % slower).
+template <uint32_t kBlock, bool kRegs>
+__global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
-  __shared__ uint32_t offwin[rounds_block<kRegs>() / 64][kOffWin];
+  __shared__ uint32_t offwin[kBlock / 64][kOffWin];
   const char* lds = reinterpret_cast<const char*>(lds_tab);
 
   // Build the replicated LDS image of the slice tables (a.slice = R0, R1, R2, R3).
@@ -782,14 +781,17 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64(
     JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {
+  const uint64_t full = static_cast<uint64_t>(grid) * jrq::kCrcBlock;
   if (args->regs_slowpath) {
-    constexpr uint32_t b = jrq::rounds_block<true>();
-    args->lanes = static_cast<uint32_t>(grid) * b;
-    hipLaunchKernelGGL(jrq::crc64_rounds_kernel<true>, dim3(grid), dim3(b), 0, stream, *args);
+    args->lanes = static_cast<uint32_t>(grid) * 768u;
+    hipLaunchKernelGGL((jrq::crc64_rounds_kernel<768, true>), dim3(grid), dim3(768), 0, stream, *args);
+  } else if (args->n < full) {  // fewer entries than lanes: long entries, few boundaries
+    args->lanes = static_cast<uint32_t>(grid) * 512u;
+    hipLaunchKernelGGL((jrq::crc64_rounds_kernel<512, false>), dim3(grid), dim3(512), 0, stream, *args);
   } else {
-    constexpr uint32_t b = jrq::rounds_block<false>();
-    args->lanes = static_cast<uint32_t>(grid) * b;
-    hipLaunchKernelGGL(jrq::crc64_rounds_kernel<false>, dim3(grid), dim3(b), 0, stream, *args);
+    args->lanes = static_cast<uint32_t>(full);
+    hipLaunchKernelGGL((jrq::crc64_rounds_kernel<jrq::kCrcBlock, false>), dim3(grid),
+                       dim3(jrq::kCrcBlock), 0, stream, *args);
   }
   const uint32_t blocks = (args->n + 255) / 256;
   const uint32_t cap = static_cast<uint32_t>(grid) * 8;
