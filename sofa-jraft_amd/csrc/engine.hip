@@ -75,6 +75,11 @@ struct jrq_engine {
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
   DevBuf stage[25];  // 0-13 host-variant staging, 14 stream-update chunk CRCs, 16-19 AppendEntries scratch, 21-24 V2 decode scratch
+  // pinned bounce buffers for the host variants' uploads (stage_in): two chunks, each
+  // reusable once the copy recorded after it has run
+  uint8_t* bounce[2] = {nullptr, nullptr};
+  hipEvent_t bounce_done[2] = {nullptr, nullptr};
+  bool bounce_busy[2] = {false, false};
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = -1;
   std::string err;
@@ -179,6 +184,51 @@ int ensure_stage(jrq_engine* e, int slot, size_t bytes, void** out) {
   return JRQ_OK;
 }
 
+// Host -> device upload of caller memory through the engine's pinned bounce chunks: a CPU
+// copy into a pinned chunk, then an async DMA from it on the engine stream, two chunks in
+// flight.  HIP's own pageable-copy path for >1 MiB uploads failed intermittently ("illegal
+// memory access" from the copy itself, read-only numpy views over Python bytes), so the host
+// variants never hand it caller pages.
+constexpr size_t kBounceChunk = size_t(8) << 20;
+
+int upload(jrq_engine* e, void* dst, const void* src, size_t bytes) {
+  for (int i = 0; i < 2; ++i)
+    if (!e->bounce[i]) {
+      JRQ_HIP(e, hipHostMalloc(reinterpret_cast<void**>(&e->bounce[i]), kBounceChunk, hipHostMallocDefault));
+      JRQ_HIP(e, hipEventCreateWithFlags(&e->bounce_done[i], hipEventDisableTiming));
+    }
+  int i = 0;
+  for (size_t off = 0; off < bytes; off += kBounceChunk, i ^= 1) {
+    const size_t n = bytes - off < kBounceChunk ? bytes - off : kBounceChunk;
+    if (e->bounce_busy[i]) JRQ_HIP(e, hipEventSynchronize(e->bounce_done[i]));
+    std::memcpy(e->bounce[i], static_cast<const uint8_t*>(src) + off, n);
+    JRQ_HIP(e, hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, e->bounce[i], n,
+                              hipMemcpyHostToDevice, e->stream));
+    JRQ_HIP(e, hipEventRecord(e->bounce_done[i], e->stream));
+    e->bounce_busy[i] = true;
+  }
+  return JRQ_OK;
+}
+
+// Caller memory registered with HIP (jrq_host_register, hipHostMalloc) goes straight to the
+// DMA engine; anything else through the bounce chunks.
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // an unregistered pointer reports an error: not sticky
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
+int upload_any(jrq_engine* e, void* dst, const void* src, size_t bytes) {
+  if (host_pinned(src)) {
+    JRQ_HIP(e, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream));
+    return JRQ_OK;
+  }
+  return upload(e, dst, src, bytes);
+}
+
 template <typename T>
 int stage_in(jrq_engine* e, int slot, const T* host, size_t count, const T** dev) {
   if (host == nullptr) {
@@ -188,7 +238,7 @@ int stage_in(jrq_engine* e, int slot, const T* host, size_t count, const T** dev
   void* p = nullptr;
   int rc = ensure_stage(e, slot, count * sizeof(T), &p);
   if (rc) return rc;
-  if (count) JRQ_HIP(e, hipMemcpyAsync(p, host, count * sizeof(T), hipMemcpyHostToDevice, e->stream));
+  if (count && (rc = upload_any(e, p, host, count * sizeof(T)))) return rc;
   *dev = static_cast<const T*>(p);
   return JRQ_OK;
 }
@@ -317,6 +367,10 @@ void jrq_destroy(jrq_engine* e) {
   if (e->comm) (void)ncclCommDestroy(e->comm);
   for (auto& b : e->stage)
     if (b.p) (void)hipFree(b.p);
+  for (int i = 0; i < 2; ++i) {
+    if (e->bounce[i]) (void)hipHostFree(e->bounce[i]);
+    if (e->bounce_done[i]) (void)hipEventDestroy(e->bounce_done[i]);
+  }
   if (e->slice) (void)hipFree(e->slice);
   if (e->shift) (void)hipFree(e->shift);
   if (e->xinv) (void)hipFree(e->xinv);
@@ -1105,12 +1159,11 @@ int jrq_table_update(jrq_table* t, const jrq_group_state* states, uint32_t n_sta
   void *ds = nullptr, *dr = nullptr;
   if (n_states) {
     if ((rc = stage_buf(e, t->st_stage, static_cast<size_t>(n_states) * sizeof(jrq_group_state), &ds))) return rc;
-    JRQ_HIP(e, hipMemcpyAsync(ds, states, static_cast<size_t>(n_states) * sizeof(jrq_group_state),
-                              hipMemcpyHostToDevice, e->stream));
+    if ((rc = upload_any(e, ds, states, static_cast<size_t>(n_states) * sizeof(jrq_group_state)))) return rc;
   }
   if (n_recs) {
     if ((rc = stage_buf(e, t->rec_stage, static_cast<size_t>(n_recs) * 8, &dr))) return rc;
-    JRQ_HIP(e, hipMemcpyAsync(dr, recs, static_cast<size_t>(n_recs) * 8, hipMemcpyHostToDevice, e->stream));
+    if ((rc = upload_any(e, dr, recs, static_cast<size_t>(n_recs) * 8))) return rc;
   }
   return jrq_table_update_dev(t, static_cast<const jrq_group_state*>(ds), n_states,
                               static_cast<const uint64_t*>(dr), n_recs);
