@@ -660,7 +660,7 @@ def leg_c2(ctx, args):
             "batched_epochs": {"epochs_per_launch": KE, "kernel_ms": k_ms,
                                "decisions_per_s": G2 * KE / (k_ms * 1e-3),
                                "roofline": roofline(alg, k_ms, kernel="quorum_epochs_kernel<3>",
-                                                    **pmc_traffic("C2", "quorum_epochs_kernel<3>")),
+                                                    **pmc_traffic("C2", "quorum_epochs_kernel<3,")),
                                "bit_exact_vs_oracle_256_groups": ok}}
 
 
