@@ -130,7 +130,10 @@ const char *jrq_last_error(const jrq_engine *e);
 void *jrq_get_stream(jrq_engine *e);
 int jrq_set_stream(jrq_engine *e, void *hip_stream);
 int jrq_synchronize(jrq_engine *e);
-/* Page-lock a host buffer (e.g. a DirectByteBuffer's address) for fast staging. */
+/* Page-lock a host buffer (e.g. a DirectByteBuffer's address) for fast staging.  Host
+ * variants (the functions without _dev) DMA registered input memory straight to the device;
+ * other input memory goes through the engine's two pinned 8 MiB bounce chunks (a CPU copy
+ * overlapped with the previous chunk's DMA). */
 int jrq_host_register(void *ptr, size_t bytes);
 int jrq_host_unregister(void *ptr);
 
