@@ -99,12 +99,16 @@ __device__ __forceinline__ i64x2 ld2nt(const int64_t* p) {
 // one 16-bit word.  A group flagged JRQ_CONF_RUNS (a conf change inside its pending window) is
 // deferred to the workgroup's second phase, where one lane per deferred group walks its runs:
 // the run walk then shares no registers with the fast path (occupancy of the common case).
+// 512-thread workgroups: 256 and 1024 measured 6-8 % slower on C3 (tools/table_probe.hip).
+constexpr uint32_t kPairBlock = 512;
+
 template <int P>
-__global__ __launch_bounds__(256) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
-  __shared__ uint32_t wave_def[4];
-  __shared__ uint32_t deferred[4][128];
+__global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
+  constexpr uint32_t kWaves = kPairBlock / 64;
+  __shared__ uint32_t wave_def[kWaves];
+  __shared__ uint32_t deferred[kWaves][128];
   const uint32_t pairs = a.G >> 1;
-  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t t = blockIdx.x * kPairBlock + threadIdx.x;
   bool f0 = false, f1 = false;
   if (t < pairs) {
     const uint32_t g = t << 1;
@@ -156,8 +160,10 @@ __global__ __launch_bounds__(256) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel
     if (f1) deferred[w][__popcll(b0) + __popcll(b1 & below)] = (t << 1) + 1;
     if (lane == 0) wave_def[w] = __popcll(b0) + __popcll(b1);
     __syncthreads();
-    const uint32_t nd = wave_def[0] + wave_def[1] + wave_def[2] + wave_def[3];
-    for (uint32_t i = threadIdx.x; i < nd; i += 256u) {  // up to 2 per lane
+    uint32_t nd = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < kWaves; ++u) nd += wave_def[u];
+    for (uint32_t i = threadIdx.x; i < nd; i += kPairBlock) {  // up to 2 per lane
       uint32_t k = i, u = 0;
       while (k >= wave_def[u]) k -= wave_def[u++];
       const uint32_t g = deferred[u][k];
@@ -407,7 +413,6 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_lease(
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
     const JrqQuorumArgs* args, int num_cus, hipStream_t stream) {
-  const dim3 blk(256);
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
   const JrqQuorumArgs& a = *args;
   const bool pair = (a.match_ld & 1u) == 0 && al16(a.match) && al16(a.pending_index) &&
@@ -417,7 +422,9 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
   // pair kernel: one lane per two groups, the whole grid at once; scalar kernel: one lane per
   // group, at most 8 workgroups per CU, grid-stride beyond
   const uint64_t lanes = pair ? (a.G >> 1) : a.G;
-  const uint64_t need = (lanes + 255) / 256;
+  const uint32_t bs = pair ? jrq::kPairBlock : 256u;
+  const dim3 blk(bs);
+  const uint64_t need = (lanes + bs - 1) / bs;
   const uint64_t cap = pair ? need : static_cast<uint64_t>(num_cus) * 8;
   const dim3 grid(static_cast<unsigned>(need < cap ? (need ? need : 1) : cap));
   switch (args->num_peers) {

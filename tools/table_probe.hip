@@ -89,6 +89,50 @@ __global__ __launch_bounds__(kTableBlock) void variant(JrqTableArgs t) {
   if (c1) t.changed[pos] = e1;
 }
 
+
+// the headline pair kernel's fast path (no run tables) with other launch shapes: kBlock threads
+// per workgroup, kU pairs per lane (kU pairs kBlock*gridDim apart, all loads issued first)
+template <int P, int kBlock, int kU>
+__global__ __launch_bounds__(kBlock) JRQ_SGPRS_8WAVES void pair_variant(JrqQuorumArgs a) {
+  const uint32_t pairs = a.G >> 1;
+  const uint32_t stride = gridDim.x * kBlock;
+  const uint32_t t0 = blockIdx.x * kBlock + threadIdx.x;
+  i64x2 pi[kU], lc[kU], la[kU], cw[kU], m[kU][P];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const uint32_t t = t0 + u * stride;
+    const uint32_t g = (t < pairs ? t : 0u) << 1;
+    pi[u] = ld2nt(a.pending_index + g);
+    lc[u] = ld2nt(a.last_committed + g);
+    la[u] = ld2nt(a.last_appended + g);
+    cw[u] = ld2nt(reinterpret_cast<const int64_t*>(a.conf) + g);
+#pragma unroll
+    for (int p = 0; p < P; ++p) m[u][p] = ld2nt(a.match + static_cast<size_t>(p) * a.match_ld + g);
+  }
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const uint32_t t = t0 + u * stride;
+    if (t >= pairs) continue;
+    const uint32_t g = t << 1;
+    int64_t m0[P], m1[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      m0[p] = m[u][p].x;
+      m1[p] = m[u][p].y;
+    }
+    int64_t o0, o1;
+    uint8_t s0, s1;
+    decide_single<P>(pi[u].x, la[u].x, lc[u].x, static_cast<uint64_t>(cw[u].x), m0, o0, s0);
+    decide_single<P>(pi[u].y, la[u].y, lc[u].y, static_cast<uint64_t>(cw[u].y), m1, o1, s1);
+    i64x2 out;
+    out.x = o0;
+    out.y = o1;
+    __builtin_nontemporal_store(out, reinterpret_cast<i64x2*>(a.committed + g));
+    __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
+                                reinterpret_cast<uint16_t*>(a.status + g));
+  }
+}
+
 __global__ void init(JrqTableArgs t, uint64_t seed) {
   const uint32_t g = blockIdx.x * 256 + threadIdx.x;
   if (g >= t.G) return;
@@ -181,8 +225,16 @@ int main() {
   q.committed = committed;
   q.status = status;
   q.G = G;
-  const dim3 pgrid(G / 2 / 256), pblk(256);
+  const dim3 pgrid(G / 2 / jrq::kPairBlock), pblk(jrq::kPairBlock);
   run("pair", [&] { hipLaunchKernelGGL(jrq::quorum_epoch_pair_kernel<5>, pgrid, pblk, 0, 0, q); });
+  const uint32_t np = G / 2;
+  run("pv_256_u1", [&] { hipLaunchKernelGGL((probe::pair_variant<5, 256, 1>), dim3(np / 256), dim3(256), 0, 0, q); });
+  run("pv_512_u1", [&] { hipLaunchKernelGGL((probe::pair_variant<5, 512, 1>), dim3(np / 512), dim3(512), 0, 0, q); });
+  run("pv_1024_u1", [&] { hipLaunchKernelGGL((probe::pair_variant<5, 1024, 1>), dim3(np / 1024), dim3(1024), 0, 0, q); });
+  run("pv_256_u2", [&] { hipLaunchKernelGGL((probe::pair_variant<5, 256, 2>), dim3(np / 512), dim3(256), 0, 0, q); });
+  run("pv_256_u4", [&] { hipLaunchKernelGGL((probe::pair_variant<5, 256, 4>), dim3(np / 1024), dim3(256), 0, 0, q); });
+  run("pv_512_u2", [&] { hipLaunchKernelGGL((probe::pair_variant<5, 512, 2>), dim3(np / 1024), dim3(512), 0, 0, q); });
+  run("pair_again", [&] { hipLaunchKernelGGL(jrq::quorum_epoch_pair_kernel<5>, pgrid, pblk, 0, 0, q); });
   run("product2", [&] { hipLaunchKernelGGL(jrq::table_epoch_kernel<5>, grid, blk, 0, 0, a); });
   CK(hipDeviceSynchronize());
   return 0;
