@@ -114,15 +114,50 @@ def roofline(alg_bytes: float, ms: float, **extra) -> dict:
 
 # ------------------------------------------------------------------ timing --
 
-def timed_launches(fn, steps, warmup, stream, sync):
-    """`warmup` untimed calls, then `steps` calls back to back between ONE pair of HIP events on
-    `stream` (the engine's stream): the per-launch time is that span / steps.  This is the only
-    timing method used for `roofline` (rocprofv3's per-kernel averages in profiles/ agree with
-    it; per-launch event pairs stretch a ~17 us kernel by 2-3 us)."""
+# Untimed warm-up: besides the --warmup calls, each timed series first runs its own work for
+# at least this much GPU time.  A GPU coming out of idle (every leg starts after seconds of
+# host-side input generation) runs its first few ms of streaming kernels up to 15 % slower
+# (C5 verify: 0.255 ms/launch over 20 launches after 3 warm-up calls, 0.222 ms in steady
+# state, same box, tools/ab_inproc.py); the timed region should see the steady state.
+WARM_MS = 200.0
+
+
+def warm_until(fn, stream, sync, warm_ms=None, calls=None):
+    """Call fn(i) back to back until `warm_ms` of its GPU time has run (at most 4096 calls) --
+    or exactly `calls` times: a function holding a collective must make the same number of
+    calls on every rank."""
+    import torch
+    if calls is not None:
+        for i in range(calls):
+            fn(i)
+        sync()
+        return calls
+    warm_ms = WARM_MS if warm_ms is None else warm_ms
+    done, n, batch = 0.0, 0, 4
+    while done < warm_ms and n < 4096:
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for j in range(batch):
+            fn(n + j)
+        z.record(stream)
+        sync()
+        done += a.elapsed_time(z)
+        n += batch
+        batch = min(batch * 2, 256)
+    return n
+
+
+def timed_launches(fn, steps, warmup, stream, sync, warm_calls=None):
+    """`warmup` untimed calls plus WARM_MS of untimed calls (warm_until), then `steps` calls
+    back to back between ONE pair of HIP events on `stream` (the engine's stream): the
+    per-launch time is that span / steps.  This is the only timing method used for `roofline`
+    (rocprofv3's per-kernel averages in profiles/ agree with it; per-launch event pairs stretch
+    a ~17 us kernel by 2-3 us)."""
     import torch
     for i in range(warmup):
         fn(i)
     sync()
+    warm_until(fn, stream, sync, calls=warm_calls)
     b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     b0.record(stream)
@@ -328,10 +363,11 @@ class Ctx:
         import torch
         torch.cuda.synchronize(self.dev)
 
-    def timed(self, fn, steps=None, warmup=None):
+    def timed(self, fn, steps=None, warmup=None, warm_calls=None):
         a = self.args
         return timed_launches(fn, a.steps if steps is None else steps,
-                              a.warmup if warmup is None else warmup, self.stream, self.sync)
+                              a.warmup if warmup is None else warmup, self.stream, self.sync,
+                              warm_calls)
 
 
 def leg_quorum(ctx, args, barrier, max_over_ranks):
@@ -377,12 +413,17 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
     # kernel only (HIP events on the engine's stream)
     k_ms, _ = ctx.timed(lambda i: epoch_fn(i, local))
     pub_ms = None
+    k_ms_max = max_over_ranks(k_ms)
+    # the same number of warm-up steps on every rank (they hold the all-gather)
+    warm_steps = int(min(4096, max(1, WARM_MS / max(k_ms_max, 1e-3))))
     if world > 1:
-        pub_ms, _ = ctx.timed(lambda i: se.publish())
-    # the contract's timed region: K steps between barrier + sync on both sides
+        pub_ms, _ = ctx.timed(lambda i: se.publish(), warm_calls=64)
+    # the contract's timed region: K steps between barrier + sync on both sides (after the
+    # --warmup steps and WARM_MS of untimed steps)
     for _ in range(args.warmup):
         se.step()
     ctx.sync()
+    warm_until(lambda i: se.step(), ctx.stream, ctx.sync, calls=warm_steps)
     barrier()
     ctx.sync()
     t0 = time.perf_counter()
@@ -392,7 +433,6 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
     barrier()
     ctx.sync()
     elapsed = max_over_ranks(time.perf_counter() - t0)
-    k_ms_max = max_over_ranks(k_ms)
     value = Gtot * args.steps / elapsed
     ok = None
     if ctx.oracle_checks:  # 4096 groups of the last epoch against the oracle replay
@@ -475,9 +515,12 @@ def leg_table(ctx, args, G, pair_ms):
     steps = max(10, args.steps)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
-    for i in range(args.warmup):
+    def table_epoch(i):
         work.copy_from(pristine[i % nb])
         work.epoch_dev(changed, n)
+    for i in range(args.warmup):
+        table_epoch(i)
+    warm_until(table_epoch, ctx.stream, ctx.sync)
     for i in range(steps):
         work.copy_from(pristine[i % nb])
         ev[i][0].record(ctx.stream)
@@ -511,6 +554,7 @@ def leg_table(ctx, args, G, pair_ms):
     def per_launch(fn):
         for i in range(args.warmup):
             fn(i)
+        warm_until(fn, ctx.stream, ctx.sync)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(steps)]
         for i in range(steps):
@@ -1066,7 +1110,7 @@ def main():
     ctx = Ctx(eng, stream, dev, world, rank, args)
 
     line = {"metric": "quorum commit decisions/sec", "value": None, "unit": "decisions/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "warm_ms": WARM_MS, "ms_per_step": None,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
             "data": "synthetic (seeded splitmix64, SURVEY.md §8d)", "legs": sorted(legs),
             "csrc_sha": csrc_sha()}

@@ -242,6 +242,10 @@ __device__ __forceinline__ bool arrive_xor(uint64_t* acc, uint32_t* cnt, uint32_
   // read-and-zero in one memory-side RMW (an xor-with-0 would be folded into a load)
   *v = __hip_atomic_exchange(acc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // settle the exchange here: its result is consumed on some paths only, and a returning
+  // load still pending where those paths join the ring loop made the compiler guard every
+  // later write of its register (a step temp) with a vmcnt wait on the payload ring
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   return true;
 }
 
@@ -379,10 +383,30 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
   __shared__ uint32_t offwin[kBlock / 64][kOffWin];
   const char* lds = reinterpret_cast<const char*>(lds_tab);
 
-  // Build the replicated LDS image of the slice tables (a.slice = R0, R1, R2, R3).
-  for (uint32_t w = threadIdx.x; w < kCrcLdsBytes / 8; w += blockDim.x)
-    lds_tab[w] = a.slice[CrcTab::src_index(w)];
-  __syncthreads();
+  // The replicated LDS image of the slice tables: its L2 reads go out first, the LDS writes
+  // and the barrier follow once the first chunk's ring loads are out too, so the first
+  // payload round trip overlaps the table build instead of waiting behind it (a wave
+  // without a first chunk writes its share before leaving; every wave meets the one barrier).
+  // Only the 512-thread shape has the registers to hold its share (32 words) over the first
+  // loads; the wider shapes (128 / 168 VGPRs) build the image up front.
+  constexpr bool kTabEarly = kBlock <= 512;
+  constexpr uint32_t kTabWords = kCrcLdsBytes / 8, kTabPer = kTabEarly ? kTabWords / kBlock : 1;
+  static_assert(!kTabEarly || kTabWords % kBlock == 0, "table share");
+  uint64_t tab_v[kTabPer];
+  if (kTabEarly) {
+#pragma unroll
+    for (uint32_t i = 0; i < kTabPer; ++i)
+      tab_v[i] = a.slice[CrcTab::src_index(threadIdx.x + i * kBlock)];
+  } else {
+    for (uint32_t w = threadIdx.x; w < kTabWords; w += kBlock) lds_tab[w] = a.slice[CrcTab::src_index(w)];
+    __syncthreads();
+  }
+  auto build_tables = [&]() {
+    if (!kTabEarly) return;
+#pragma unroll
+    for (uint32_t i = 0; i < kTabPer; ++i) lds_tab[threadIdx.x + i * kBlock] = tab_v[i];
+    __syncthreads();
+  };
 
   const CrcTab tb(threadIdx.x & 63u);
   const uint32_t n = a.n;
@@ -435,7 +459,10 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
   for (uint64_t j = 0;; ++j) {
     const uint64_t kw = a.seg_map ? ((j * grid + blockIdx.x) * waves + (L0 >> 6)) * 64
                                   : ((j * waves + (L0 >> 6)) * grid + blockIdx.x) * 64;
-    if (kw >= nseg) break;  // wave-uniform
+    if (kw >= nseg) {  // wave-uniform
+      if (j == 0) build_tables();
+      break;
+    }
     const uint64_t wbase = kw * S;  // the wave's window starts at its first segment
     const uint64_t k = kw + (L - L0);
     const uint64_t s0 = wbase + lane_off;
@@ -511,6 +538,7 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     // leaving HBM idle at the start of every chunk (short segments: C1, V2)
     JRQ_LOAD_HALF(h0, 0u);
     JRQ_LOAD_HALF(h1, 1u);
+    if (j == 0) build_tables();
 
     // ---- segment setup ----
     SegWalk sw;
@@ -607,7 +635,11 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     const uint32_t prog0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(j * halves));
     // prefetches past the chunk's last half-round re-read that half (L2-hot): the half
     // index stays wave-uniform and the descriptor a single SGPR quad -- selecting an empty
-    // descriptor instead put it in VGPRs and wrapped every load in a waterfall loop
+    // descriptor instead put it in VGPRs and wrapped every load in a waterfall loop.
+    // The ring loop has no exit but its header: the last iteration's surplus stages load and
+    // transpose (L2-hot) and skip process().  A `break` between stages joined ring states
+    // with different halves in flight at the loop header, and the compiler then waited for
+    // two halves (vmcnt(4)) before hashing the oldest one: the ring ran one half deep.
     auto last_half = [&](uint32_t h) -> uint32_t { return h < halves ? h : halves - 1u; };
     // settle the setup's loads first (e.g. an unused interpolation probe): a load the
     // compiler still counts as in flight when the ring starts costs a vmcnt(0) at the top
@@ -675,18 +707,15 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
       JRQ_LOAD_HALF(h3, last_half(hh + 3));
       transpose_half(h0);
       process(hh, h0);
-      if (hh + 1 >= halves) break;  // wave-uniform
       JRQ_LOAD_HALF(h0, last_half(hh + 4));
       transpose_half(h1);
-      process(hh + 1, h1);
-      if (hh + 2 >= halves) break;
+      if (hh + 1 < halves) process(hh + 1, h1);  // wave-uniform
       JRQ_LOAD_HALF(h1, last_half(hh + 5));
       transpose_half(h2);
-      process(hh + 2, h2);
-      if (hh + 3 >= halves) break;
+      if (hh + 2 < halves) process(hh + 2, h2);
       JRQ_LOAD_HALF(h2, last_half(hh + 6));
       transpose_half(h3);
-      process(hh + 3, h3);
+      if (hh + 3 < halves) process(hh + 3, h3);
     }
 #else
     for (uint32_t hh0 = 0; hh0 < halves; hh0 += 3) {
@@ -705,14 +734,12 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
       JRQ_LOAD_HALF(h2, last_half(hh + 2));
       transpose_half(h0);
       process(hh, h0);
-      if (hh + 1 >= halves) break;  // wave-uniform
       JRQ_LOAD_HALF(h0, last_half(hh + 3));
       transpose_half(h1);
-      process(hh + 1, h1);
-      if (hh + 2 >= halves) break;
+      if (hh + 1 < halves) process(hh + 1, h1);  // wave-uniform
       JRQ_LOAD_HALF(h1, last_half(hh + 4));
       transpose_half(h2);
-      process(hh + 2, h2);
+      if (hh + 2 < halves) process(hh + 2, h2);
     }
 #endif
 #undef JRQ_LOAD_HALF

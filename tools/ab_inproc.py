@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""A/B of libjrq builds in ONE process (tools only): every variant library is loaded side by
+side (ctypes, its own engine on the shared stream), and the legs run interleaved round by
+round, so box-to-box and warm-up drift fall on every variant alike.
+
+  python tools/ab_inproc.py NAME=PATH.so[:ENV=V,...] [...]   (ENV: engine knobs, e.g. JRQ_CRC_SEG_BYTES)
+
+Per leg and variant: the median over rounds of (one event pair around `reps` back-to-back
+launches) / reps, and whether the outputs equal the first variant's.  A torch int64 sum over
+the C5 payload is timed alongside as the plain-read reference."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sofa-jraft_amd"))
+
+
+def load_variant(path):
+    from jraft_amd import _lib
+    from jraft_amd import Engine
+    lib = C.CDLL(os.path.abspath(path), mode=C.RTLD_LOCAL)
+    for name, res, args in _lib.SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    e = Engine.__new__(Engine)
+    e._L = lib
+    err = C.c_int(0)
+    h = lib.jrq_create(0, 1 << 20, 16, C.byref(err))
+    if not h:
+        raise RuntimeError(f"{path}: jrq_create failed {err.value}")
+    e._h = C.c_void_p(h)
+    e.device = 0
+    return e
+
+
+def main():
+    import torch
+
+    from jraft_amd import Engine
+    from jraft_amd import workloads as W
+    specs = sys.argv[1:] or ["lib=sofa-jraft_amd/lib/libjrq.so"]
+    legs_env = os.environ.get("AB_LEGS", "C5,C1,archive,v2")
+    rounds = int(os.environ.get("AB_ROUNDS", "8"))
+    reps = int(os.environ.get("AB_REPS", "10"))
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(s)
+    import jraft_amd._lib as L
+    L.load()  # the in-tree lib first: torch's HIP runtime is already the process runtime
+    variants = []
+    for sp in specs:
+        name, _, rest = sp.partition("=")
+        path, _, envs = rest.partition(":")
+        saved = {}
+        for kv in filter(None, envs.split(",")):  # engine knobs read at jrq_create
+            k, _, v = kv.partition("=")
+            saved[k] = os.environ.get(k)
+            os.environ[k] = v
+        e = load_variant(path)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        e._L.jrq_set_stream(e._h, C.c_void_p(s.cuda_stream))
+        variants.append((name, e))
+
+    def dev_t(a):
+        return torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(dev)
+
+    legs = {}
+    eb5 = W.entry_batch(64 << 10, 16 << 10, seed=3)
+    d5 = {k: dev_t(v) for k, v in eb5.items() if isinstance(v, np.ndarray)}
+    n5 = 64 << 10
+    exp5 = torch.zeros(n5, dtype=torch.int64, device=dev)
+    outs = {}
+
+    def mk_c5(e, o):
+        cor = torch.empty(n5, dtype=torch.uint8, device=dev)
+        return lambda: e.logentry_checksum_batch_dev(d5["etype"], d5["index"], d5["term"], None,
+                                                     d5["payload"], d5["offsets"], o,
+                                                     expected=exp5, corrupt=cor)
+    if "C5" in legs_env:
+        legs["C5"] = (mk_c5, lambda: torch.empty(n5, dtype=torch.int64, device=dev))
+    if "C1" in legs_env:
+        eb1 = W.entry_batch(1 << 20, 256, seed=5)
+        d1 = {k: dev_t(v) for k, v in eb1.items() if isinstance(v, np.ndarray)}
+        legs["C1"] = (lambda e, o: (lambda: e.logentry_checksum_batch_dev(
+            d1["etype"], d1["index"], d1["term"], None, d1["payload"], d1["offsets"], o)),
+            lambda: torch.empty(1 << 20, dtype=torch.int64, device=dev))
+    if "archive" in legs_env:
+        tot = int(d5["payload"].numel())
+        one = torch.tensor([0, tot], dtype=torch.int64, device=dev)
+
+        def mk_arch(e, o):
+            def f():
+                o.zero_()
+                e.crc64_stream_update_dev(o, d5["payload"], one)
+            return f
+        legs["archive"] = (mk_arch, lambda: torch.zeros(1, dtype=torch.int64, device=dev))
+    if "v2" in legs_env:
+        rec_np, lens = W.v2_records(eb5["etype"], eb5["index"], eb5["term"], eb5["payload"],
+                                    eb5["offsets"], np.zeros(n5, np.uint64))
+        d_rec = torch.from_numpy(rec_np).to(dev)
+        d_roff = dev_t(lens)
+
+        def mk_v2(e, o):
+            return lambda: e.v2_decode_verify_dev(d_rec, d_roff, o)
+
+        def new_v2():
+            return {k: torch.empty(n5, dtype={np.uint8: torch.uint8, np.uint32: torch.int32}.get(t, torch.int64),
+                                   device=dev) for k, t in Engine.V2_FIELDS}
+        legs["v2"] = (mk_v2, new_v2)
+
+    pay64 = d5["payload"].view(torch.int64)
+    acc = torch.empty((), dtype=torch.int64, device=dev)
+    fns = {}
+    for leg, (mk, new_out) in legs.items():
+        for name, e in variants:
+            o = new_out()
+            outs[(leg, name)] = o
+            fns[(leg, name)] = mk(e, o)
+    fns[("read", "torch_sum")] = lambda: torch.sum(pay64, dim=0, out=acc)
+    times = {k: [] for k in fns}
+    for r in range(rounds + 1):
+        for k, f in fns.items():
+            f()
+            a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            for _ in range(reps):
+                f()
+            z.record(s)
+            z.synchronize()
+            if r > 0:
+                times[k].append(a.elapsed_time(z) / reps)
+    res = {}
+    for (leg, name), t in times.items():
+        o = outs.get((leg, name))
+        first = outs.get((leg, variants[0][0]))
+        same = None
+        if o is not None:
+            if isinstance(o, dict):
+                same = all(torch.equal(o[k], first[k]) for k in o)
+            else:
+                same = bool(torch.equal(o, first))
+        res.setdefault(leg, {})[name] = {"ms_median": float(np.median(t)), "ms_min": float(np.min(t)),
+                                         "same_as_first": same}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

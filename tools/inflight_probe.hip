@@ -74,7 +74,7 @@ __global__ __launch_bounds__(BLOCK) void ring(const uint8_t* __restrict__ p, uin
   out[(uint64_t)blockIdx.x * BLOCK + L] = acc;
 }
 
-int main() {
+int main(int argc, char** argv) {
   const uint64_t total = 1ull << 30;
   uint8_t* d;
   uint32_t* out;
@@ -119,6 +119,11 @@ int main() {
     time("D=" #D " W=" #W " block=" #BLOCK, [&] {                                              \
       hipLaunchKernelGGL((ring<D, W, BLOCK>), dim3(256), dim3(BLOCK), 0, 0, d, S, out);        \
     });                                                                                        \
+  }
+  if (argc > 1) {  // block-size sweep at W = 0: the rounds kernel's load shape per workgroup size
+    RUN(3, 0, 1024) RUN(3, 0, 768) RUN(3, 0, 512) RUN(4, 0, 512) RUN(6, 0, 512) RUN(8, 0, 512)
+    RUN(3, 0, 256) RUN(6, 0, 256) RUN(3, 192, 512) RUN(6, 192, 512)
+    return 0;
   }
   RUN(3, 0, 1024) RUNS(3, 0, 1) RUNS(4, 0, 1) RUNS(3, 192, 2) RUNS(3, 192, 4) RUNS(3, 160, 2)
   RUN(3, 192, 1024)
