@@ -774,9 +774,9 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
            "value": pay * world / (v_max * 1e-3) / 1e9, "unit": "GB/s (payload)",
            "workload": "C5: 64k x 16 KiB DATA LogEntries per GPU, checksum + isCorrupted verify",
            "ms_per_launch": v_ms, "bit_exact_vs_oracle": ok,
-           "roofline": roofline(alg_v, v_ms, kernel="crc64_rounds_kernel<512, false> + "
+           "roofline": roofline(alg_v, v_ms, kernel="crc64_rounds_kernel<512u, false> + "
                                 "crc64_finish_kernel<true>",
-                                **pmc_traffic("C5", "crc64_rounds_kernel<512",
+                                **pmc_traffic("C5", "crc64_rounds_kernel<512u, false>",
                                               "crc64_finish_kernel<true>"))}
     c5_step = {"workload": "C5 as BASELINE states it: 64k regions x 3 replicas x 16 KiB entries; "
                            "one step = CRC64 verify of the 64k entries + commit of the 64k groups",
@@ -856,7 +856,7 @@ def leg_v2(ctx, args, c5state):
                         f"field), decode + isCorrupted",
             "GBps_records": tot / (ms * 1e-3) / 1e9, "ms_per_batch": ms,
             "bit_exact_vs_oracle": ok, "oracle_decoder_sample_ok": sample_ok,
-            "roofline": roofline(alg, ms, **pmc_traffic("v2", "v2_parse", "crc64_rounds_kernel<768",
+            "roofline": roofline(alg, ms, **pmc_traffic("v2", "v2_parse", "crc64_rounds_kernel<768u, true>",
                                                         "crc64_finish_kernel<false>", "v2_finish"))}
 
 
@@ -901,7 +901,7 @@ def leg_snapshot(ctx, args, c5state):
             "regions_GBps": tot_b / (sS_ms * 1e-3) / 1e9, "regions_ms": sS_ms,
             "bit_exact_vs_oracle": ok,
             "roofline": roofline(tot_b + 24, s1_ms, kernel="archive leg (one 1 GiB chunk)",
-                                 **pmc_traffic("snapshot", "crc64_rounds_kernel<512",
+                                 **pmc_traffic("snapshot", "crc64_rounds_kernel<512u, false>",
                                                "crc64_finish_kernel<false>"))}
 
 
@@ -948,7 +948,7 @@ def leg_c1(ctx, args):
             "GBps_payload": n1 * c1["entry_bytes"] / (ms * 1e-3) / 1e9,
             "bit_exact_vs_oracle": ok,
             "roofline": roofline(alg, crc_ms, kernel="LogEntry checksum of the 1M x 256 B entries",
-                                 **pmc_traffic("C1", "crc64_rounds_kernel<1024",
+                                 **pmc_traffic("C1", "crc64_rounds_kernel<512u, false>",
                                                "crc64_finish_kernel<true>"))}
 
 

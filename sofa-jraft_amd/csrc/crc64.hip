@@ -361,7 +361,7 @@ struct SegWalk {
 // kRegs: a half-round holding an entry boundary hashes its bytes from the ring registers
 // (hash_regs) instead of re-reading them from L2 (hash_global).  Faster when boundaries are
 // frequent and unaligned (V2 records, ragged batches), but the extra live ranges spill a few
-// VGPRs at the 128-VGPR budget, which costs ~9 % on boundary-free aligned batches.
+// VGPRs at a 128-VGPR budget (1024-thread workgroups), ~9 % on boundary-free aligned batches.
 // Entry boundaries of a wave's window, cached in LDS (the rest of the 160 KiB next to the
 // 128 KiB of tables): offsets[eb .. eb + kOffWin) of the window's first entry eb, as u32
 // bytes from the window start (0xFFFFFFFF: 4 GiB or more past it).  An event then looks its
@@ -369,14 +369,13 @@ struct SegWalk {
 // wait for the wave's whole in-flight prefetch ring (vmcnt is in order) -- small entries
 // (C1, V2 ranges) are all events.
 constexpr uint32_t kOffWin = 512;
-static_assert(kCrcLdsBytes + (kCrcBlock / 64) * kOffWin * 4 <= 160 * 1024, "LDS budget");
+static_assert(kCrcLdsBytes + (kCrcRegsBlock / 64) * kOffWin * 4 <= 160 * 1024, "LDS budget");
 
-// Workgroup size kBlock (one workgroup per CU: the LDS tables fill it).  At 1024 threads (16
-// waves) the 128-VGPR budget makes the ring and the step trees spill a few registers; fewer
-// waves run spill-free (512: ~155 VGPRs, 768: ~160) at the cost of half / three quarters of the
-// lanes, i.e. longer segments.  Measured (tools/ab_run.sh): the register boundary path at 768
-// (V2 records 350 -> 336 us); the boundary-free path at 512 when a batch has fewer entries than
-// lanes (C5 264 -> 255 us) and at 1024 otherwise (C1's 1 KiB segments: 512 is 3.5 % slower).
+// Workgroup size kBlock (one workgroup per CU: the LDS tables fill it).  The boundary-free
+// path runs kCrcBlock = 512 (2 waves per SIMD, 256 VGPRs each), which also holds its share of
+// the table image over the first loads (below); 1024 threads (128 VGPRs) spilled the ring and
+// the step trees: C1 0.087 -> 0.080 ms at 512 (tools/ab_inproc.py).  The register boundary path
+// (V2 records) runs 768 threads (168 VGPRs, no spill; 512 measured 2-3 % slower there).
 template <uint32_t kBlock, bool kRegs>
 __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
@@ -387,9 +386,9 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
   // and the barrier follow once the first chunk's ring loads are out too, so the first
   // payload round trip overlaps the table build instead of waiting behind it (a wave
   // without a first chunk writes its share before leaving; every wave meets the one barrier).
-  // Only the 512-thread shape has the registers to hold its share (32 words) over the first
-  // loads; the wider shapes (128 / 168 VGPRs) build the image up front.
-  constexpr bool kTabEarly = kBlock <= 512;
+  // (512 threads: 32 words per thread, held in registers over the first loads; the 768-thread
+  // shape has no registers to spare and builds the image up front)
+  constexpr bool kTabEarly = kBlock == 512;
   constexpr uint32_t kTabWords = kCrcLdsBytes / 8, kTabPer = kTabEarly ? kTabWords / kBlock : 1;
   static_assert(!kTabEarly || kTabWords % kBlock == 0, "table share");
   uint64_t tab_v[kTabPer];
@@ -572,9 +571,17 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     if (!(sw.flags & SegWalk::kDone))
       e0 = interp_lower_bound(off, n, base, total, s0 + sw.pos - D + base);
     // fill the wave's LDS window from its first lane's entry (lane 0 is never done here: the
-    // chunk's first segment exists), one coalesced pass of up to kOffWin offsets
+    // chunk's first segment exists), one coalesced pass of up to kOffWin offsets -- as many as
+    // the window's 64 segments hold at the batch's mean entry size, plus a wave of margin
+    // (boundaries past the window fall back to global loads: slower, same result)
     eb = __builtin_amdgcn_readfirstlane(e0);  // wave-uniform (SGPRs): every lane is active
-    wcnt = __builtin_amdgcn_readfirstlane(n + 1 - eb < kOffWin ? n + 1 - eb : kOffWin);
+    {
+      const double est = static_cast<double>(64 * S) / static_cast<double>(total ? total : 1) *
+                         static_cast<double>(n) + 65.0;
+      uint32_t c = n + 1 - eb < kOffWin ? n + 1 - eb : kOffWin;
+      if (est < static_cast<double>(c)) c = static_cast<uint32_t>(est);
+      wcnt = __builtin_amdgcn_readfirstlane(c);
+    }
     for (uint32_t i = L - L0; i < wcnt; i += 64) {
       const uint64_t d = E(eb + i) - wbase;
       win[i] = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(d);
@@ -808,15 +815,12 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64(
     JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {
-  const uint64_t full = static_cast<uint64_t>(grid) * jrq::kCrcBlock;
   if (args->regs_slowpath) {
-    args->lanes = static_cast<uint32_t>(grid) * 768u;
-    hipLaunchKernelGGL((jrq::crc64_rounds_kernel<768, true>), dim3(grid), dim3(768), 0, stream, *args);
-  } else if (args->n < full) {  // fewer entries than lanes: long entries, few boundaries
-    args->lanes = static_cast<uint32_t>(grid) * 512u;
-    hipLaunchKernelGGL((jrq::crc64_rounds_kernel<512, false>), dim3(grid), dim3(512), 0, stream, *args);
+    args->lanes = static_cast<uint32_t>(grid) * jrq::kCrcRegsBlock;
+    hipLaunchKernelGGL((jrq::crc64_rounds_kernel<jrq::kCrcRegsBlock, true>), dim3(grid),
+                       dim3(jrq::kCrcRegsBlock), 0, stream, *args);
   } else {
-    args->lanes = static_cast<uint32_t>(full);
+    args->lanes = static_cast<uint32_t>(grid) * jrq::kCrcBlock;
     hipLaunchKernelGGL((jrq::crc64_rounds_kernel<jrq::kCrcBlock, false>), dim3(grid),
                        dim3(jrq::kCrcBlock), 0, stream, *args);
   }

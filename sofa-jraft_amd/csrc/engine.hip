@@ -324,7 +324,7 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   if (const char* v = std::getenv("JRQ_CRC_SEG_MAP")) e->crc_seg_map = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("JRQ_CRC_SEG_BYTES"))  // rounded up to 256 B by the kernel
     e->crc_seg_bytes = std::strtoull(v, nullptr, 10);
-  e->scratch_len = static_cast<uint32_t>(2ull * e->crc_grid * jrq::kCrcBlock + 2);
+  e->scratch_len = static_cast<uint32_t>(2ull * e->crc_grid * jrq::kCrcRegsBlock + 2);  // >= 2 slots per lane
   int rc = JRQ_OK;
   std::vector<uint64_t> slice, shift, xinv;
   build_tables(slice, shift, xinv);

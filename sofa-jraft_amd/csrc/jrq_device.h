@@ -27,7 +27,8 @@ constexpr int kShiftTables = 48;  // shifts up to 2^48 - 1 bytes
 // LDS image of the slice tables (128 KiB): 8 tables x 8 replicas (crc64.hip Tab8).
 constexpr int kSliceTables = 8;
 constexpr int kCrcLdsBytes = 8 * 256 * 8 * 8;
-constexpr int kCrcBlock = 1024;  // threads per workgroup (16 waves, 1 workgroup / CU)
+constexpr int kCrcBlock = 512;       // threads per workgroup (8 waves, 1 workgroup / CU)
+constexpr int kCrcRegsBlock = 768;   // the register boundary path's workgroup (crc64.hip)
 
 // Status flags, identical to include/jrq.h jrq_group_status.
 constexpr uint8_t kStNotLeader = 1, kStOutOfRange = 2, kStEmptyConf = 4;
