@@ -50,9 +50,10 @@ def quorum_bytes_per_group(P: int) -> int:
     return 8 * P + 41
 
 
-def crc_bytes(n_entries: int, payload_bytes: int, verify: bool = True) -> int:
-    # payload + offsets (N+1)*8 + per entry type 1, index 8, term 8, out 8 (+ expected 8, corrupt 1)
-    b = payload_bytes + 8 * (n_entries + 1) + n_entries * (1 + 8 + 8 + 8)
+def crc_bytes(n_entries: int, payload_bytes: int, verify: bool = True, offsets: bool = True) -> int:
+    # payload + offsets (N+1)*8 (not for fixed-size entries) + per entry type 1, index 8, term 8,
+    # out 8 (+ expected 8, corrupt 1)
+    b = payload_bytes + (8 * (n_entries + 1) if offsets else 0) + n_entries * (1 + 8 + 8 + 8)
     if verify:
         b += n_entries * (8 + 1)
     return b
@@ -923,9 +924,9 @@ def leg_c1(ctx, args):
     c1c = torch.empty(1, dtype=torch.int64, device=dev)
     c1s = torch.empty(1, dtype=torch.uint8, device=dev)
 
-    def crc(i):
-        eng.logentry_checksum_batch_dev(d1["etype"], d1["index"], d1["term"], None,
-                                        d1["payload"], d1["offsets"], out1)
+    def crc(i):  # 256-B entries back to back: the fixed-size entry point (no offsets array)
+        eng.logentry_checksum_fixed_dev(d1["etype"], d1["index"], d1["term"], None,
+                                        d1["payload"], c1["entry_bytes"], out1)
 
     def step(i):
         crc(i)
@@ -942,14 +943,14 @@ def leg_c1(ctx, args):
                                           q1["last_committed"], q1["conf"], chunk=1024)
         ok = bool(np.array_equal(out1.cpu().numpy().view(np.uint64), exp1)) and \
             bool(np.array_equal(c1c.cpu().numpy(), ce))
-    alg = crc_bytes(n1, n1 * c1["entry_bytes"], verify=False)
+    alg = crc_bytes(n1, n1 * c1["entry_bytes"], verify=False, offsets=False)
     return {"workload": "C1: 1 group x 3 peers, 1M appended 256-B LogEntries: checksum + commitAt",
             "ms_per_step": ms, "entries_per_s": n1 / (ms * 1e-3),
             "GBps_payload": n1 * c1["entry_bytes"] / (ms * 1e-3) / 1e9,
             "bit_exact_vs_oracle": ok,
-            "roofline": roofline(alg, crc_ms, kernel="LogEntry checksum of the 1M x 256 B entries",
-                                 **pmc_traffic("C1", "crc64_rounds_kernel<512u, false>",
-                                               "crc64_finish_kernel<true>"))}
+            "roofline": roofline(alg, crc_ms, kernel="crc64_fixed_kernel<true> (1M x 256 B LogEntries, "
+                                                    "jrq_logentry_checksum_fixed_dev)",
+                                 **pmc_traffic("C1", "crc64_fixed_kernel<true>"))}
 
 
 def leg_lease(ctx, args, quorum_conf_dev, G, P):

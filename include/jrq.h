@@ -282,6 +282,14 @@ int jrq_crc64_batch_dev(jrq_engine *e, const uint8_t *payload_dev, const uint64_
                         uint32_t N, uint64_t *crc_out_dev);
 int jrq_crc64_batch(jrq_engine *e, const uint8_t *payload, const uint64_t *offsets, uint32_t N,
                     uint64_t *crc_out);
+/* Fixed-size entries: N entries of entry_bytes each, back to back from payload_dev (no offsets
+ * array).  The batch jrq_crc64_batch_dev would see with offsets[i] = i * entry_bytes -- same
+ * results.  Whole 256-B multiples on a 16-B aligned payload, with at least one entry per lane
+ * of the engine's grid, run the one-launch fixed-size kernel (crc64.hip crc64_fixed_kernel);
+ * anything else goes through the offsets path.  The host variants route batches of equal
+ * entries there by themselves. */
+int jrq_crc64_fixed_dev(jrq_engine *e, const uint8_t *payload_dev, uint64_t entry_bytes, uint32_t N,
+                        uint64_t *crc_out_dev);
 
 /* Streaming CRC64 as a java.util.zip.Checksum (JC/util/CRC64.java:26,106-126), batched over S
  * independent streams: the RheaKV snapshot archive checksum, fed by CheckedOutputStream /
@@ -315,6 +323,12 @@ int jrq_logentry_checksum_batch(jrq_engine *e, const uint8_t *type, const int64_
                                 const uint8_t *payload, const uint64_t *offsets, uint32_t N,
                                 uint64_t *out, const uint64_t *expected, const uint8_t *has,
                                 uint8_t *corrupt_out);
+/* Fixed-size entries (see jrq_crc64_fixed_dev): entry i = payload_dev[i*entry_bytes, +entry_bytes). */
+int jrq_logentry_checksum_fixed_dev(jrq_engine *e, const uint8_t *type_dev, const int64_t *index_dev,
+                                    const int64_t *term_dev, const uint64_t *peer_xor_dev,
+                                    const uint8_t *payload_dev, uint64_t entry_bytes, uint32_t N,
+                                    uint64_t *out_dev, const uint64_t *expected_dev,
+                                    const uint8_t *has_dev, uint8_t *corrupt_out_dev);
 
 /* ------------------------------------------- follower verify on receive -- */
 

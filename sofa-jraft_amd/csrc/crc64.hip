@@ -166,6 +166,13 @@ __device__ __forceinline__ void row_transpose(u32x4& a0, u32x4& a1, u32x4& a2, u
   swap32(a1, a3);
 }
 
+// The same, pinned below the loads issued before it (the asm keeps the scheduler from
+// hoisting the memory-free swaps and draining the prefetch with vmcnt(0)).
+__device__ __forceinline__ void transpose_ring(u32x4 (&v)[4]) {
+  asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+  row_transpose(v[0], v[1], v[2], v[3]);
+}
+
 // --------------------------------------------------------------- helpers ---
 
 // Continue r over virtual bytes [p, q) read from global memory (A = address of virtual byte
@@ -811,7 +818,146 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
   }
 }
 
+// ------------------------------------------------------ fixed-size entries ---
+// N entries of EL bytes each, back to back (EL a multiple of 256): no segments, no offsets.
+// Lane c of a wave hashes entry 64r + c of each of its rows r, so every entry ends in the same
+// half-round on all lanes, the wave's 64 results leave as one coalesced 512-B row, and the
+// LogEntry fields (coalesced, loaded when the row starts) are applied right there: one
+// launch, no finish kernel.  The loads are the rounds kernel's transposed row-group shape with
+// lane stride EL; a ring of four half-rounds turns 4 halves per step, an entry = EL / 256 turns,
+// so the field loads of a row sit at least 16 ring loads before their use (the compiler never
+// waits for the ring on their account).  C1 (1M x 256 B): the segment walk wrote 6.5x its 8 MB
+// of results as scattered 8-B stores and re-read them in the finish kernel.
+template <bool kLogEntry>
+__global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
+  __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
+  const char* lds = reinterpret_cast<const char*>(lds_tab);
+  constexpr uint32_t kTabPer = kCrcLdsBytes / 8 / kCrcBlock;
+  uint64_t tab_v[kTabPer];  // this thread's share of the table image (written after the first loads)
+#pragma unroll
+  for (uint32_t i = 0; i < kTabPer; ++i)
+    tab_v[i] = a.slice[CrcTab::src_index(threadIdx.x + i * kCrcBlock)];
+  auto build_tables = [&]() {
+#pragma unroll
+    for (uint32_t i = 0; i < kTabPer; ++i) lds_tab[threadIdx.x + i * kCrcBlock] = tab_v[i];
+    __syncthreads();
+  };
+  const CrcTab tb(threadIdx.x & 63u);
+  const uint32_t L = threadIdx.x;
+  const uint32_t L0 = __builtin_amdgcn_readfirstlane(L & ~63u);
+  const uint32_t lane = L - L0;
+  const uint32_t n = a.n;
+  const uint64_t EL = a.entry_bytes;
+  const uint32_t rows = (n + 63) / 64;
+  // contiguous rows per wave (a wave streams 64 * EL * rows bytes in order)
+  const uint32_t W = gridDim.x * (kCrcBlock / 64);
+  const uint32_t w = blockIdx.x * (kCrcBlock / 64) + (L0 >> 6);
+  const uint32_t per = rows / W, extra = rows % W;
+  const uint32_t r0 = __builtin_amdgcn_readfirstlane(w * per + (w < extra ? w : extra));
+  const uint32_t r1 = __builtin_amdgcn_readfirstlane(r0 + per + (w < extra ? 1u : 0u));
+  if (r0 >= r1) {  // no rows: write the table share (every wave meets the one barrier)
+    build_tables();
+    return;
+  }
+  const uint32_t HE = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(EL >> 6));  // halves per entry
+  const uint32_t turns = HE >> 2;
+  const uint64_t total = static_cast<uint64_t>(n) * EL;
+  const uint32_t WS = static_cast<uint32_t>(EL);  // lane-to-lane stride (64 * EL < 2^32)
+  const uint32_t qb = (L & 15u) * WS + 16u * ((L >> 4) & 3u);
+  const uint32_t qa0 = qb, qa1 = qb + 16u * WS, qa2 = qb + 32u * WS, qa3 = qb + 48u * WS;
+  const uintptr_t pbase = reinterpret_cast<uintptr_t>(a.payload);
+  // load cursor (row, half of the entry) of the next half-round to issue, scalar; past the
+  // wave's last row it keeps re-reading that row's last half (L2-hot, results unused)
+  uint32_t crow = r0, chalf = 0;
+  auto load_half = [&](u32x4 (&H)[4]) {
+    const uint64_t o = static_cast<uint64_t>(crow) * 64u * EL + static_cast<uint64_t>(chalf) * 64u;
+    const uint64_t hp = pbase + o;
+    const uint32_t hlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp));
+    const uint32_t hhi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp >> 32));
+    const uint64_t left = total - o;  // lanes past entry n-1 read zeros
+    const uint32_t hn = __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left));
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<uint8_t*>((static_cast<uint64_t>(hhi) << 32) | hlo),
+        static_cast<short>(0), static_cast<int>(hn), 0x00020000);
+    H[0] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa0, 0, JRQ_CRC_LOAD_AUX);
+    H[1] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa1, 0, JRQ_CRC_LOAD_AUX);
+    H[2] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa2, 0, JRQ_CRC_LOAD_AUX);
+    H[3] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa3, 0, JRQ_CRC_LOAD_AUX);
+    asm volatile("" ::: "memory");
+    if (chalf + 1 < HE) {
+      ++chalf;
+    } else if (crow + 1 < r1) {
+      ++crow;
+      chalf = 0;
+    }
+  };
+  u32x4 h0[4], h1[4], h2[4], h3[4];
+  load_half(h0);
+  load_half(h1);
+  load_half(h2);
+  build_tables();
+  // LogEntry fields: absent arrays read word 0 of the slice table (R0[0] = 0), masked below
+  const uint64_t* const z = a.slice;
+  const bool ver = kLogEntry && a.expected != nullptr && a.corrupt != nullptr;
+  const uint64_t* const p_peer = kLogEntry && a.peer_xor ? a.peer_xor : z;
+  const uint64_t* const p_exp = ver ? a.expected : z;
+  const uint8_t* const p_has = ver && a.has ? a.has : reinterpret_cast<const uint8_t*>(z);
+  const uint32_t m_peer = a.peer_xor ? ~0u : 0u, m_exp = ver ? ~0u : 0u, m_has = ver && a.has ? ~0u : 0u;
+  for (uint32_t r = r0; r < r1; ++r) {
+    const uint32_t e0 = r * 64u + lane;
+    const bool live = e0 < n;
+    const uint32_t e = live ? e0 : n - 1u;
+    uint32_t f_type = 0, f_has = 0;
+    uint64_t f_index = 0, f_term = 0, f_peer = 0, f_exp = 0;
+    if (kLogEntry) {
+      f_type = a.type[e];
+      f_index = static_cast<uint64_t>(a.index[e]);
+      f_term = static_cast<uint64_t>(a.term[e]);
+      f_peer = p_peer[e & m_peer];
+      f_exp = p_exp[e & m_exp];
+      f_has = p_has[e & m_has];
+    }
+    RState s{0u, 0u};
+    uint32_t q = 0;
+    do {
+      load_half(h3);
+      transpose_ring(h0);
+      tb.step64(s, h0, lds);
+      load_half(h0);
+      transpose_ring(h1);
+      tb.step64(s, h1, lds);
+      load_half(h1);
+      transpose_ring(h2);
+      tb.step64(s, h2, lds);
+      load_half(h2);
+      transpose_ring(h3);
+      tb.step64(s, h3, lds);
+    } while (++q < turns);
+    uint64_t c = crc_value(s);
+    if (kLogEntry) {  // LogEntry.checksum(): type ^ LogId.checksum() ^ peers ^ crc64(data)
+      RState lid{0u, 0u};
+      const uint64_t bi = bswap64(f_index), bt = bswap64(f_term);
+      tb.step8(lid, static_cast<uint32_t>(bi), static_cast<uint32_t>(bi >> 32), lds);
+      tb.step8(lid, static_cast<uint32_t>(bt), static_cast<uint32_t>(bt >> 32), lds);
+      c ^= static_cast<uint64_t>(f_type) ^ crc_value(lid) ^ f_peer;
+      if (ver && live) a.corrupt[e] = static_cast<uint8_t>((m_has ? f_has != 0 : true) && f_exp != c);
+    }
+    if (live) a.out[e] = c;
+  }
+}
+
 }  // namespace jrq
+
+// Fixed-size entries (crc64_fixed_kernel): 64 * entry_bytes < 2^32, entry_bytes % 256 == 0.
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64_fixed(
+    JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {
+  if (log_entry)
+    hipLaunchKernelGGL(jrq::crc64_fixed_kernel<true>, dim3(grid), dim3(jrq::kCrcBlock), 0, stream, *args);
+  else
+    hipLaunchKernelGGL(jrq::crc64_fixed_kernel<false>, dim3(grid), dim3(jrq::kCrcBlock), 0, stream, *args);
+  return hipGetLastError();
+}
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64(
     JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {

@@ -20,6 +20,8 @@
 
 extern "C" hipError_t jrq_launch_crc64(JrqCrcArgs* args, int log_entry, int grid,
                                        hipStream_t stream);
+extern "C" hipError_t jrq_launch_crc64_fixed(JrqCrcArgs* args, int log_entry, int grid,
+                                             hipStream_t stream);
 extern "C" hipError_t jrq_launch_quorum(const JrqQuorumArgs* args, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_quorum_epochs(const JrqQuorumArgs* args, uint32_t K,
                                                uint64_t match_eld, uint64_t la_eld,
@@ -74,7 +76,7 @@ struct jrq_engine {
   uint32_t crc_seg_map = 1;  // JRQ_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
-  DevBuf stage[25];  // 0-13 host-variant staging, 14 stream-update chunk CRCs, 16-19 AppendEntries scratch, 21-24 V2 decode scratch
+  DevBuf stage[25];  // 0-13 host-variant staging, 14 stream-update chunk CRCs, 15 fixed-size offsets, 16-19 AppendEntries scratch, 21-24 V2 decode scratch
   // pinned bounce buffers for the host variants' uploads (stage_in): two chunks, each
   // reusable once the copy recorded after it has run
   uint8_t* bounce[2] = {nullptr, nullptr};
@@ -249,6 +251,37 @@ int stage_in(jrq_engine* e, int slot, const T* host, size_t count, const T** dev
 int check_monotone(jrq_engine* e, const uint64_t* off, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i)
     if (off[i + 1] < off[i]) return fail(e, JRQ_E_INVALID, "offsets not monotone at entry %u", i);
+  return JRQ_OK;
+}
+
+// offsets[i] = i * entry_bytes: the segment walk's view of a fixed-size batch the fixed kernel
+// cannot take (crc_fixed_ok)
+__global__ void iota_offsets_kernel(uint64_t* off, uint32_t n, uint64_t entry_bytes) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += gridDim.x * blockDim.x)
+    off[i] = static_cast<uint64_t>(i) * entry_bytes;
+}
+
+// crc64_fixed_kernel (crc64.hip) takes a batch of N entries of entry_bytes each when the
+// entries are whole 256-B multiples (4-half-round turns), 64 of them fit the u32 lane offsets,
+// the payload is 16-B aligned, and there is at least one entry per lane of the grid (fewer,
+// longer entries -- C5's 64k x 16 KiB -- keep every lane busy in the segment walk instead).
+bool crc_fixed_ok(const jrq_engine* e, const void* payload, uint64_t entry_bytes, uint32_t N) {
+  return entry_bytes >= 256 && entry_bytes % 256 == 0 && entry_bytes < (1ull << 26) &&
+         (reinterpret_cast<uintptr_t>(payload) & 15u) == 0 &&
+         static_cast<uint64_t>(N) >= static_cast<uint64_t>(e->crc_grid) * jrq::kCrcBlock;
+}
+
+// All N ranges of a host offsets array the same length (0 if not).
+uint64_t uniform_length(const uint64_t* off, uint32_t n) {
+  const uint64_t L = off[1] - off[0];
+  for (uint32_t i = 1; i < n; ++i)
+    if (off[i + 1] - off[i] != L) return 0;
+  return L;
+}
+
+int crc_fixed_dispatch(jrq_engine* e, JrqCrcArgs& a, int log_entry) {
+  a.slice = e->slice;
+  JRQ_HIP(e, jrq_launch_crc64_fixed(&a, log_entry, e->crc_grid, e->stream));
   return JRQ_OK;
 }
 
@@ -538,6 +571,40 @@ int jrq_crc64_batch_dev(jrq_engine* e, const uint8_t* payload, const uint64_t* o
   return crc_dispatch(e, a, 0);
 }
 
+// The segment walk over generated offsets (stage 15), for fixed-size batches the fixed kernel
+// cannot take.
+int fixed_offsets(jrq_engine* e, uint64_t entry_bytes, uint32_t N, const uint64_t** off) {
+  void* d = nullptr;
+  int rc;
+  if ((rc = ensure_stage(e, 15, (static_cast<size_t>(N) + 1) * 8, &d))) return rc;
+  const uint32_t blocks = (N + 1 + 255) / 256;
+  hipLaunchKernelGGL(iota_offsets_kernel, dim3(blocks < 1024 ? blocks : 1024), dim3(256), 0,
+                     e->stream, static_cast<uint64_t*>(d), N, entry_bytes);
+  JRQ_HIP(e, hipGetLastError());
+  *off = static_cast<const uint64_t*>(d);
+  return JRQ_OK;
+}
+
+int jrq_crc64_fixed_dev(jrq_engine* e, const uint8_t* payload, uint64_t entry_bytes, uint32_t N,
+                        uint64_t* crc_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (N == 0) return JRQ_OK;
+  if (!payload || !crc_out) return fail(e, JRQ_E_INVALID, "null pointer");
+  DeviceGuard guard(e->device);
+  if (!crc_fixed_ok(e, payload, entry_bytes, N)) {
+    const uint64_t* off;
+    int rc;
+    if ((rc = fixed_offsets(e, entry_bytes, N, &off))) return rc;
+    return jrq_crc64_batch_dev(e, payload, off, N, crc_out);
+  }
+  JrqCrcArgs a{};
+  a.payload = payload;
+  a.n = N;
+  a.out = crc_out;
+  a.entry_bytes = entry_bytes;
+  return crc_fixed_dispatch(e, a, 0);
+}
+
 int jrq_crc64_batch(jrq_engine* e, const uint8_t* payload, const uint64_t* offsets, uint32_t N,
                     uint64_t* crc_out) {
   if (!e) return JRQ_E_INVALID;
@@ -562,7 +629,14 @@ int jrq_crc64_batch(jrq_engine* e, const uint8_t* payload, const uint64_t* offse
   a.n = N;
   a.out = static_cast<uint64_t*>(dout);
   a.regs_slowpath = unaligned_bounds(offsets, N);
-  if ((rc = crc_dispatch(e, a, 0))) return rc;
+  const uint64_t ul = uniform_length(offsets, N);
+  if (crc_fixed_ok(e, dp, ul, N)) {
+    a.entry_bytes = ul;
+    rc = crc_fixed_dispatch(e, a, 0);
+  } else {
+    rc = crc_dispatch(e, a, 0);
+  }
+  if (rc) return rc;
   JRQ_HIP(e, hipMemcpyAsync(crc_out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
@@ -640,6 +714,40 @@ int jrq_logentry_checksum_batch_dev(jrq_engine* e, const uint8_t* type, const in
   return crc_dispatch(e, a, 1);
 }
 
+int jrq_logentry_checksum_fixed_dev(jrq_engine* e, const uint8_t* type, const int64_t* index,
+                                    const int64_t* term, const uint64_t* peer_xor,
+                                    const uint8_t* payload, uint64_t entry_bytes, uint32_t N,
+                                    uint64_t* out, const uint64_t* expected, const uint8_t* has,
+                                    uint8_t* corrupt_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (N == 0) return JRQ_OK;
+  if (!type || !index || !term || !payload || !out)
+    return fail(e, JRQ_E_INVALID, "null pointer");
+  if ((expected == nullptr) != (corrupt_out == nullptr))
+    return fail(e, JRQ_E_INVALID, "expected and corrupt_out go together");
+  DeviceGuard guard(e->device);
+  if (!crc_fixed_ok(e, payload, entry_bytes, N)) {
+    const uint64_t* off;
+    int rc;
+    if ((rc = fixed_offsets(e, entry_bytes, N, &off))) return rc;
+    return jrq_logentry_checksum_batch_dev(e, type, index, term, peer_xor, payload, off, N, out,
+                                           expected, has, corrupt_out);
+  }
+  JrqCrcArgs a{};
+  a.payload = payload;
+  a.n = N;
+  a.out = out;
+  a.type = type;
+  a.index = index;
+  a.term = term;
+  a.peer_xor = peer_xor;
+  a.expected = expected;
+  a.has = has;
+  a.corrupt = corrupt_out;
+  a.entry_bytes = entry_bytes;
+  return crc_fixed_dispatch(e, a, 1);
+}
+
 int jrq_logentry_checksum_batch(jrq_engine* e, const uint8_t* type, const int64_t* index,
                                 const int64_t* term, const uint64_t* peer_xor,
                                 const uint8_t* payload, const uint64_t* offsets, uint32_t N,
@@ -671,10 +779,16 @@ int jrq_logentry_checksum_batch(jrq_engine* e, const uint8_t* type, const int64_
   void *dout = nullptr, *dcor = nullptr;
   if ((rc = ensure_stage(e, 12, static_cast<size_t>(N) * 8, &dout))) return rc;
   if (corrupt_out && (rc = ensure_stage(e, 13, N, &dcor))) return rc;
-  e->regs_hint = unaligned_bounds(offsets, N);
-  rc = jrq_logentry_checksum_batch_dev(e, dt, di, dtm, dpx, dp, doff, N, static_cast<uint64_t*>(dout),
-                                       dex, dh, static_cast<uint8_t*>(dcor));
-  e->regs_hint = 0;
+  const uint64_t ul = uniform_length(offsets, N);
+  if (crc_fixed_ok(e, dp, ul, N)) {  // equal entries: the fixed-size kernel (one launch)
+    rc = jrq_logentry_checksum_fixed_dev(e, dt, di, dtm, dpx, dp, ul, N, static_cast<uint64_t*>(dout),
+                                         dex, dh, static_cast<uint8_t*>(dcor));
+  } else {
+    e->regs_hint = unaligned_bounds(offsets, N);
+    rc = jrq_logentry_checksum_batch_dev(e, dt, di, dtm, dpx, dp, doff, N, static_cast<uint64_t*>(dout),
+                                         dex, dh, static_cast<uint8_t*>(dcor));
+    e->regs_hint = 0;
+  }
   if (rc) return rc;
   JRQ_HIP(e, hipMemcpyAsync(out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
   if (corrupt_out) JRQ_HIP(e, hipMemcpyAsync(corrupt_out, dcor, N, hipMemcpyDeviceToHost, e->stream));

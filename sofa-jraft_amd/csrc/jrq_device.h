@@ -99,6 +99,7 @@ struct JrqCrcArgs {
   uint32_t prio_steps;     // 1: waves lower their priority as they progress (crc64.hip)
   uint32_t regs_slowpath;  // 1: boundary half-rounds hash from registers (crc64_rounds_kernel<true>)
   uint64_t* stream_state;  // nullable: streaming Checksum registers folded by the finish kernel
+  uint64_t entry_bytes;    // crc64_fixed_kernel: every entry this long, back to back (no offsets)
 };
 
 // Leader lease / alive-quorum check (quorum.hip, lease kernel).

@@ -100,12 +100,15 @@ SIGNATURES = [
      [_V, C.POINTER(GroupBatch), C.c_uint32, C.c_uint64, C.c_uint64, _V, _V, C.c_uint32]),
     ("jrq_crc64_batch_dev", C.c_int, [_V, _V, _V, C.c_uint32, _V]),
     ("jrq_crc64_batch", C.c_int, [_V, _V, _V, C.c_uint32, _V]),
+    ("jrq_crc64_fixed_dev", C.c_int, [_V, _V, C.c_uint64, C.c_uint32, _V]),
     ("jrq_crc64_stream_update_dev", C.c_int, [_V, _V, _V, _V, C.c_uint32]),
     ("jrq_crc64_stream_update", C.c_int, [_V, _V, _V, _V, C.c_uint32]),
     ("jrq_logentry_checksum_batch_dev", C.c_int,
      [_V, _V, _V, _V, _V, _V, _V, C.c_uint32, _V, _V, _V, _V]),
     ("jrq_logentry_checksum_batch", C.c_int,
      [_V, _V, _V, _V, _V, _V, _V, C.c_uint32, _V, _V, _V, _V]),
+    ("jrq_logentry_checksum_fixed_dev", C.c_int,
+     [_V, _V, _V, _V, _V, _V, C.c_uint64, C.c_uint32, _V, _V, _V, _V]),
     ("jrq_append_entries_verify_dev", C.c_int,
      [_V, C.c_uint32, _V, _V, C.c_uint32, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
     ("jrq_append_entries_verify", C.c_int,

@@ -200,6 +200,20 @@ class Engine:
                 _np_ptr(has), _np_ptr(corrupt)), self._h)
         return out if corrupt is None else (out, corrupt)
 
+    def crc64_fixed_dev(self, payload, entry_bytes, out, n=None):
+        """Device variant over N entries of `entry_bytes` each, back to back (no offsets)."""
+        n = out.shape[0] if n is None else n
+        check(self._L.jrq_crc64_fixed_dev(self._h, _dev_ptr(payload), entry_bytes, n,
+                                          _dev_ptr(out)), self._h)
+
+    def logentry_checksum_fixed_dev(self, etype, index, term, peer_xor, payload, entry_bytes, out,
+                                    expected=None, has=None, corrupt=None, n=None):
+        n = out.shape[0] if n is None else n
+        check(self._L.jrq_logentry_checksum_fixed_dev(
+            self._h, _dev_ptr(etype), _dev_ptr(index), _dev_ptr(term), _dev_ptr(peer_xor),
+            _dev_ptr(payload), entry_bytes, n, _dev_ptr(out), _dev_ptr(expected),
+            _dev_ptr(has), _dev_ptr(corrupt)), self._h)
+
     def logentry_checksum_batch_dev(self, etype, index, term, peer_xor, payload, offsets, out,
                                     expected=None, has=None, corrupt=None, n=None):
         n = offsets.shape[0] - 1 if n is None else n

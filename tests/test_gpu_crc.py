@@ -176,8 +176,81 @@ def test_logentry_verify(engine, oracle):
     np.testing.assert_array_equal(corrupt2, bad.astype(np.uint8))
 
 
+def _entry_fields(N, seed):
+    rng = np.random.default_rng(seed)
+    et = rng.integers(0, 4, N).astype(np.uint8)
+    idx = rng.integers(-2**62, 2**62, N).astype(np.int64)
+    term = rng.integers(0, 2**40, N).astype(np.int64)
+    px = rng.integers(0, 2**63, N).astype(np.uint64) * (et == 3)
+    return rng, et, idx, term, px
+
+
+LANES = 256 * 512  # the CRC grid's lanes on MI355X: the fixed-size kernel wants >= 1 entry each
+
+
+@pytest.mark.parametrize("el,n,tail", [(256, 140000, []), (512, LANES + 5, []), (1024, LANES, [77]),
+                                       (256, LANES, [0]), (768, 140000, []), (256, 4000, [])])
+def test_fixed_size_batches(engine, oracle, el, n, tail):
+    """Host variants route batches of equal entries (256-B multiples, >= one per lane) to the
+    one-launch fixed-size kernel (crc64.hip crc64_fixed_kernel: fields, verify and the store
+    there); a ragged / zero-length tail, other lengths and small batches take the segment walk.
+    Every result vs the oracle: LogEntry (verify, has, peers) and plain CRC."""
+    lens = [el] * n + tail
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    N = len(lens)
+    payload = W.random_bytes(el + n, int(offs[-1]) or 1)
+    rng, et, idx, term, px = _entry_fields(N, el + n)
+    exp = oracle.logentry_checksum_batch(et, idx, term, px, payload, offs)
+    expected = exp.copy()
+    bad = rng.random(N) < 0.02
+    expected[bad] ^= np.uint64(1 << 40)
+    has = (rng.random(N) < 0.8).astype(np.uint8)
+    out, corrupt = engine.logentry_checksum_batch(et, idx, term, px, payload, offs, expected, has)
+    np.testing.assert_array_equal(out, exp)
+    np.testing.assert_array_equal(corrupt, (bad & (has == 1)).astype(np.uint8))
+    out2 = engine.logentry_checksum_batch(et, idx, term, None, payload, offs)
+    np.testing.assert_array_equal(out2, oracle.logentry_checksum_batch(et, idx, term, None, payload, offs))
+    np.testing.assert_array_equal(engine.crc64_batch(payload, offs), oracle.crc64_batch(payload, offs))
+
+
+@pytest.mark.parametrize("el,n", [(256, 140000), (512, LANES + 7), (100, 5000), (256, 3000)])
+def test_fixed_dev_api(engine, oracle, el, n):
+    """jrq_logentry_checksum_fixed_dev / jrq_crc64_fixed_dev (device buffers, no offsets): the
+    fixed-size kernel, or the offsets path over generated offsets (100-B entries, few entries)."""
+    import torch
+    dev = torch.device("cuda:0")
+    payload = W.random_bytes(el * 7 + n, el * n)
+    offs = (np.arange(n + 1, dtype=np.uint64) * np.uint64(el))
+    rng, et, idx, term, px = _entry_fields(n, el + 3 * n)
+    exp = oracle.logentry_checksum_batch(et, idx, term, px, payload, offs)
+    expected = exp.copy()
+    bad = rng.random(n) < 0.05
+    expected[bad] ^= np.uint64(3)
+
+    def t(a):
+        return torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(dev)
+    # a non-default torch stream shared with the engine: torch's default stream handle is 0,
+    # which selects the engine's own stream (no ordering with the uploads)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        ins = [t(x) for x in (et, idx, term, px, payload, expected)]
+        out = torch.zeros(n, dtype=torch.int64, device=dev)
+        cor = torch.zeros(n, dtype=torch.uint8, device=dev)
+        crc = torch.zeros(n, dtype=torch.int64, device=dev)
+    engine.use_stream(s.cuda_stream)
+    try:
+        engine.logentry_checksum_fixed_dev(*ins[:5], el, out, expected=ins[5], corrupt=cor)
+        engine.crc64_fixed_dev(ins[4], el, crc)
+        s.synchronize()
+    finally:
+        engine.use_stream(None)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), exp)
+    np.testing.assert_array_equal(cor.cpu().numpy(), bad.astype(np.uint8))
+    np.testing.assert_array_equal(crc.cpu().numpy().view(np.uint64), oracle.crc64_batch(payload, offs))
+
+
 def test_device_path_c1_shape(engine, oracle):
-    """Device-resident variant (torch tensors, engine on torch's stream), C1-shaped slice."""
+    """Device-resident variant (torch tensors, engine on its own stream), C1-shaped slice."""
     import torch
     n = 1 << 16
     b = W.entry_batch(n, 256, seed=11)
@@ -185,13 +258,10 @@ def test_device_path_c1_shape(engine, oracle):
     t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v).to(dev)
          for k, v in b.items() if isinstance(v, np.ndarray)}
     out = torch.zeros(n, dtype=torch.int64, device=dev)
-    engine.use_stream(torch.cuda.current_stream().cuda_stream)
-    try:
-        engine.logentry_checksum_batch_dev(t["etype"], t["index"], t["term"], None, t["payload"],
-                                           t["offsets"], out)
-        torch.cuda.synchronize()
-    finally:
-        engine.use_stream(None)
+    torch.cuda.synchronize()  # the uploads went to torch's default stream; the engine uses its own
+    engine.logentry_checksum_batch_dev(t["etype"], t["index"], t["term"], None, t["payload"],
+                                       t["offsets"], out)
+    engine.synchronize()
     exp = oracle.logentry_checksum_batch(b["etype"], b["index"], b["term"], None, b["payload"],
                                          b["offsets"])
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), exp)

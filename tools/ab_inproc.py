@@ -24,7 +24,9 @@ def load_variant(path):
     from jraft_amd import Engine
     lib = C.CDLL(os.path.abspath(path), mode=C.RTLD_LOCAL)
     for name, res, args in _lib.SIGNATURES:
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:  # an older build without this entry point
+            continue
         fn.restype = res
         fn.argtypes = args
     e = Engine.__new__(Engine)
@@ -44,7 +46,7 @@ def main():
     from jraft_amd import Engine
     from jraft_amd import workloads as W
     specs = sys.argv[1:] or ["lib=sofa-jraft_amd/lib/libjrq.so"]
-    legs_env = os.environ.get("AB_LEGS", "C5,C1,archive,v2")
+    legs_env = os.environ.get("AB_LEGS", "C5,C1,archive,v2").split(",")
     rounds = int(os.environ.get("AB_ROUNDS", "8"))
     reps = int(os.environ.get("AB_REPS", "10"))
     dev = torch.device("cuda:0")
@@ -93,6 +95,13 @@ def main():
         legs["C1"] = (lambda e, o: (lambda: e.logentry_checksum_batch_dev(
             d1["etype"], d1["index"], d1["term"], None, d1["payload"], d1["offsets"], o)),
             lambda: torch.empty(1 << 20, dtype=torch.int64, device=dev))
+    if "C1f" in legs_env:  # the same 256-B entries through the fixed-size entry point
+        if "C1" not in legs_env:
+            eb1 = W.entry_batch(1 << 20, 256, seed=5)
+            d1 = {k: dev_t(v) for k, v in eb1.items() if isinstance(v, np.ndarray)}
+        legs["C1f"] = (lambda e, o: (lambda: e.logentry_checksum_fixed_dev(
+            d1["etype"], d1["index"], d1["term"], None, d1["payload"], 256, o)),
+            lambda: torch.empty(1 << 20, dtype=torch.int64, device=dev))
     if "archive" in legs_env:
         tot = int(d5["payload"].numel())
         one = torch.tensor([0, tot], dtype=torch.int64, device=dev)
@@ -120,8 +129,11 @@ def main():
     pay64 = d5["payload"].view(torch.int64)
     acc = torch.empty((), dtype=torch.int64, device=dev)
     fns = {}
+    needs = {"C1f": "jrq_logentry_checksum_fixed_dev"}
     for leg, (mk, new_out) in legs.items():
         for name, e in variants:
+            if leg in needs and not hasattr(e._L, needs[leg]):
+                continue  # an older build without that entry point
             o = new_out()
             outs[(leg, name)] = o
             fns[(leg, name)] = mk(e, o)
@@ -141,7 +153,7 @@ def main():
     res = {}
     for (leg, name), t in times.items():
         o = outs.get((leg, name))
-        first = outs.get((leg, variants[0][0]))
+        first = next((outs[(leg, v)] for v, _ in variants if (leg, v) in outs), None)
         same = None
         if o is not None:
             if isinstance(o, dict):
