@@ -401,7 +401,16 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
         eng.rccl_init(world, rank, uid[0])
         nranks = eng.rccl_nranks()
 
+    # one prepared launch per epoch buffer (arguments resolved once, as a C / JNI host keeps
+    # its jrq_group_batch): the step loop then costs the GPU epoch, not Python marshalling
+    launchers = [eng.quorum_epoch_launcher(t["match"], t["pending_index"], t["last_appended"],
+                                           t["last_committed"], t["conf"], local, status)
+                 for t in epochs]
+
     def epoch_fn(i, out):
+        if out is local:
+            launchers[i % QUORUM_EPOCH_BUFFERS]()
+            return
         t = epochs[i % QUORUM_EPOCH_BUFFERS]
         eng.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
                              t["last_committed"], t["conf"], out, status)
@@ -667,9 +676,13 @@ def leg_c2(ctx, args):
     c2c = torch.empty(G2, dtype=torch.int64, device=dev)
     c2s = torch.empty(G2, dtype=torch.uint8, device=dev)
 
+    # prepared launches (arguments resolved once, as a C / JNI host would): Python's per-call
+    # marshalling (~10 us) otherwise outlasts these 6-9 us kernels in the timed loop
+    c2_launch = eng.quorum_epoch_launcher(c2d["match"], c2d["pending_index"], c2d["last_appended"],
+                                          c2d["last_committed"], c2d["conf"], c2c, c2s)
+
     def c2_step(i):
-        eng.quorum_epoch_dev(c2d["match"], c2d["pending_index"], c2d["last_appended"],
-                             c2d["last_committed"], c2d["conf"], c2c, c2s)
+        c2_launch()
     one_ms, one_wall = ctx.timed(c2_step)
     KE = 64
     ser = W.quorum_epoch_series("C2", KE)
@@ -677,9 +690,12 @@ def leg_c2(ctx, args):
     kc = torch.empty((KE, G2), dtype=torch.int64, device=dev)
     ks = torch.empty((KE, G2), dtype=torch.uint8, device=dev)
 
+    c2k_launch = eng.quorum_epochs_launcher(ser_d["match"], ser_d["pending_index"],
+                                            ser_d["last_appended"], ser_d["last_committed"],
+                                            ser_d["conf"], kc, ks)
+
     def c2k_step(i):
-        eng.quorum_epochs_dev(ser_d["match"], ser_d["pending_index"], ser_d["last_appended"],
-                              ser_d["last_committed"], ser_d["conf"], kc, ks)
+        c2k_launch()
     k_ms, _ = ctx.timed(c2k_step)
     ok = None
     if ctx.oracle_checks:  # the oracle on 256 groups, all KE epochs, state carried
@@ -738,7 +754,11 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
     qc = torch.empty(n, dtype=torch.int64, device=dev)
     qs = torch.empty(n, dtype=torch.uint8, device=dev)
 
-    def verify(i):
+    def verify(i):  # 16 KiB entries back to back: the fixed-size entry point (no offsets array)
+        eng.logentry_checksum_fixed_dev(d["etype"], d["index"], d["term"], None, d["payload"],
+                                        c5["entry_bytes"], out, expected=d_exp, corrupt=corrupt)
+
+    def verify_offsets(i):  # the same batch through the general offsets entry point
         eng.logentry_checksum_batch_dev(d["etype"], d["index"], d["term"], None, d["payload"],
                                         d["offsets"], out, expected=d_exp, corrupt=corrupt)
 
@@ -754,6 +774,11 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
         ctx.sync()
         return None, None, (d, eb, expected, flip, out)
     steps = max(10, args.steps)
+    vo_ms, _ = ctx.timed(verify_offsets, steps, 2)
+    ok_off = None
+    if ctx.oracle_checks:
+        ok_off = bool(np.array_equal(out.cpu().numpy().view(np.uint64), expected)) and \
+            bool(np.array_equal(corrupt.cpu().numpy().astype(bool), flip))
     v_ms, _ = ctx.timed(verify, steps, 2)
     c_ms, _ = ctx.timed(commit, steps, 2)
     s_ms, _ = ctx.timed(step, steps, 2)
@@ -769,16 +794,18 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
                                           qb["last_committed"], qb["conf"], chunk=1024)
         step_ok = ok and bool(np.array_equal(qc.cpu().numpy(), ce)) and \
             bool(np.array_equal(qs.cpu().numpy(), se))
-    alg_v = crc_bytes(n, pay, verify=True)
+    alg_v = crc_bytes(n, pay, verify=True, offsets=False)
     alg_c = quorum_bytes_per_group(3) * n
     crc = {"metric": "LogEntry CRC64 verify GB/s",
            "value": pay * world / (v_max * 1e-3) / 1e9, "unit": "GB/s (payload)",
-           "workload": "C5: 64k x 16 KiB DATA LogEntries per GPU, checksum + isCorrupted verify",
+           "workload": "C5: 64k x 16 KiB DATA LogEntries per GPU, checksum + isCorrupted verify "
+                       "(jrq_logentry_checksum_fixed_dev: 2 lanes per entry)",
            "ms_per_launch": v_ms, "bit_exact_vs_oracle": ok,
-           "roofline": roofline(alg_v, v_ms, kernel="crc64_rounds_kernel<512u, false> + "
-                                "crc64_finish_kernel<true>",
-                                **pmc_traffic("C5", "crc64_rounds_kernel<512u, false>",
-                                              "crc64_finish_kernel<true>"))}
+           "offsets_path": {"ms_per_launch": vo_ms, "bit_exact_vs_oracle": ok_off,
+                            "GBps_payload": pay / (vo_ms * 1e-3) / 1e9,
+                            "how": "jrq_logentry_checksum_batch_dev (segment walk + finish kernel)"},
+           "roofline": roofline(alg_v, v_ms, kernel="crc64_fixed_kernel<true>",
+                                **pmc_traffic("C5", "crc64_fixed_kernel<true>"))}
     c5_step = {"workload": "C5 as BASELINE states it: 64k regions x 3 replicas x 16 KiB entries; "
                            "one step = CRC64 verify of the 64k entries + commit of the 64k groups",
                "ms_per_step": s_ms, "verify_ms": v_ms, "commit_ms": c_ms,
@@ -786,8 +813,7 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
                "GBps_payload": pay * world / (s_max * 1e-3) / 1e9,
                "bit_exact_vs_oracle": step_ok,
                "roofline": roofline(alg_v + alg_c, s_ms,
-                                    bytes_note="verify (payload + 34 B/entry + offsets) + "
-                                               "commit 65 B/group")}
+                                    bytes_note="verify (payload + 34 B/entry) + commit 65 B/group")}
     return crc, c5_step, (d, eb, expected, flip, out)
 
 

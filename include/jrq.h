@@ -284,10 +284,10 @@ int jrq_crc64_batch(jrq_engine *e, const uint8_t *payload, const uint64_t *offse
                     uint64_t *crc_out);
 /* Fixed-size entries: N entries of entry_bytes each, back to back from payload_dev (no offsets
  * array).  The batch jrq_crc64_batch_dev would see with offsets[i] = i * entry_bytes -- same
- * results.  Whole 256-B multiples on a 16-B aligned payload, with at least one entry per lane
- * of the engine's grid, run the one-launch fixed-size kernel (crc64.hip crc64_fixed_kernel);
- * anything else goes through the offsets path.  The host variants route batches of equal
- * entries there by themselves. */
+ * results.  Entries that split into k = 1, 2, 4 .. 64 pieces of whole 256-B multiples, one
+ * piece per lane of the engine's grid, on a 16-B aligned payload, run the one-launch
+ * fixed-size kernel (crc64.hip crc64_fixed_kernel); anything else goes through the offsets
+ * path.  The host variants route batches of equal entries there by themselves. */
 int jrq_crc64_fixed_dev(jrq_engine *e, const uint8_t *payload_dev, uint64_t entry_bytes, uint32_t N,
                         uint64_t *crc_out_dev);
 

@@ -819,11 +819,13 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
 }
 
 // ------------------------------------------------------ fixed-size entries ---
-// N entries of EL bytes each, back to back (EL a multiple of 256): no segments, no offsets.
-// Lane c of a wave hashes entry 64r + c of each of its rows r, so every entry ends in the same
-// half-round on all lanes, the wave's 64 results leave as one coalesced 512-B row, and the
-// LogEntry fields (coalesced, loaded when the row starts) are applied right there: one
-// launch, no finish kernel.  The loads are the rounds kernel's transposed row-group shape with
+// N entries of EL bytes each, back to back: no segments, no offsets.  An entry is hashed by
+// k = fixed_k consecutive lanes (a power of two, k pieces of PS = EL / k bytes, PS a multiple of
+// 256; k > 1 only when N < lanes, e.g. C5's 64k x 16 KiB on 128k lanes), lane c of a wave takes
+// piece c of row r (64 pieces), so every piece ends in the same half-round on all lanes.  The k
+// piece CRCs meet by linearity in log2(k) butterfly levels, crc(A || B) = crc(A) x^(8|B|) ^
+// crc(B), and the last lane of the entry applies the LogEntry fields (coalesced, loaded when
+// the row starts) and stores the result: one launch, no finish kernel.  The loads are the rounds kernel's transposed row-group shape with
 // lane stride EL; a ring of four half-rounds turns 4 halves per step, an entry = EL / 256 turns,
 // so the field loads of a row sit at least 16 ring loads before their use (the compiler never
 // waits for the ring on their account).  C1 (1M x 256 B): the segment walk wrote 6.5x its 8 MB
@@ -847,8 +849,10 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   const uint32_t L0 = __builtin_amdgcn_readfirstlane(L & ~63u);
   const uint32_t lane = L - L0;
   const uint32_t n = a.n;
-  const uint64_t EL = a.entry_bytes;
-  const uint32_t rows = (n + 63) / 64;
+  const uint32_t K = a.fixed_k, kl = 31u - __builtin_clz(K);  // lanes per entry, log2
+  const uint64_t PS = a.entry_bytes >> kl;                    // piece bytes
+  const uint32_t EPR = 64u >> kl;                              // entries per row
+  const uint32_t rows = (n + EPR - 1) / EPR;
   // contiguous rows per wave (a wave streams 64 * EL * rows bytes in order)
   const uint32_t W = gridDim.x * (kCrcBlock / 64);
   const uint32_t w = blockIdx.x * (kCrcBlock / 64) + (L0 >> 6);
@@ -859,10 +863,10 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     build_tables();
     return;
   }
-  const uint32_t HE = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(EL >> 6));  // halves per entry
+  const uint32_t HE = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(PS >> 6));  // halves per piece
   const uint32_t turns = HE >> 2;
-  const uint64_t total = static_cast<uint64_t>(n) * EL;
-  const uint32_t WS = static_cast<uint32_t>(EL);  // lane-to-lane stride (64 * EL < 2^32)
+  const uint64_t total = static_cast<uint64_t>(n) * a.entry_bytes;
+  const uint32_t WS = static_cast<uint32_t>(PS);  // lane-to-lane stride (64 * PS < 2^32)
   const uint32_t qb = (L & 15u) * WS + 16u * ((L >> 4) & 3u);
   const uint32_t qa0 = qb, qa1 = qb + 16u * WS, qa2 = qb + 32u * WS, qa3 = qb + 48u * WS;
   const uintptr_t pbase = reinterpret_cast<uintptr_t>(a.payload);
@@ -870,7 +874,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   // wave's last row it keeps re-reading that row's last half (L2-hot, results unused)
   uint32_t crow = r0, chalf = 0;
   auto load_half = [&](u32x4 (&H)[4]) {
-    const uint64_t o = static_cast<uint64_t>(crow) * 64u * EL + static_cast<uint64_t>(chalf) * 64u;
+    const uint64_t o = static_cast<uint64_t>(crow) * 64u * PS + static_cast<uint64_t>(chalf) * 64u;
     const uint64_t hp = pbase + o;
     const uint32_t hlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp));
     const uint32_t hhi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp >> 32));
@@ -904,8 +908,9 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   const uint64_t* const p_exp = ver ? a.expected : z;
   const uint8_t* const p_has = ver && a.has ? a.has : reinterpret_cast<const uint8_t*>(z);
   const uint32_t m_peer = a.peer_xor ? ~0u : 0u, m_exp = ver ? ~0u : 0u, m_has = ver && a.has ? ~0u : 0u;
+  const uint32_t piece = lane & (K - 1u);
   for (uint32_t r = r0; r < r1; ++r) {
-    const uint32_t e0 = r * 64u + lane;
+    const uint32_t e0 = r * EPR + (lane >> kl);
     const bool live = e0 < n;
     const uint32_t e = live ? e0 : n - 1u;
     uint32_t f_type = 0, f_has = 0;
@@ -935,21 +940,32 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
       tb.step64(s, h3, lds);
     } while (++q < turns);
     uint64_t c = crc_value(s);
+    // pieces -> entry: at level l, the group of 2^l lanes holding the earlier bytes is shifted
+    // past the 2^l * PS bytes of its partner group (x^(8 * 2^l * PS), global power tables)
+    for (uint32_t l = 0; l < kl; ++l) {
+      const uint64_t sh = (piece >> l) & 1u ? c : crc_shift(c, PS << l, a.shift);
+      const uint32_t lo = __shfl_xor(static_cast<uint32_t>(sh), 1 << l);
+      const uint32_t hi = __shfl_xor(static_cast<uint32_t>(sh >> 32), 1 << l);
+      const uint64_t other = (static_cast<uint64_t>(hi) << 32) | lo;
+      if ((piece >> l) & 1u) c ^= other;  // the later group accumulates
+    }
+    const bool last = piece == K - 1u;  // the lane holding the entry's CRC
     if (kLogEntry) {  // LogEntry.checksum(): type ^ LogId.checksum() ^ peers ^ crc64(data)
       RState lid{0u, 0u};
       const uint64_t bi = bswap64(f_index), bt = bswap64(f_term);
       tb.step8(lid, static_cast<uint32_t>(bi), static_cast<uint32_t>(bi >> 32), lds);
       tb.step8(lid, static_cast<uint32_t>(bt), static_cast<uint32_t>(bt >> 32), lds);
       c ^= static_cast<uint64_t>(f_type) ^ crc_value(lid) ^ f_peer;
-      if (ver && live) a.corrupt[e] = static_cast<uint8_t>((m_has ? f_has != 0 : true) && f_exp != c);
+      if (ver && live && last) a.corrupt[e] = static_cast<uint8_t>((m_has ? f_has != 0 : true) && f_exp != c);
     }
-    if (live) a.out[e] = c;
+    if (live && last) a.out[e] = c;
   }
 }
 
 }  // namespace jrq
 
-// Fixed-size entries (crc64_fixed_kernel): 64 * entry_bytes < 2^32, entry_bytes % 256 == 0.
+// Fixed-size entries (crc64_fixed_kernel): fixed_k lanes per entry, 64 * (entry_bytes / fixed_k)
+// < 2^32, (entry_bytes / fixed_k) % 256 == 0.
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64_fixed(
     JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {
   if (log_entry)

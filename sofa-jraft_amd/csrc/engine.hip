@@ -91,11 +91,16 @@ namespace {
 
 // --------------------------------------------------------------- helpers ---
 
-struct DeviceGuard {
-  int prev = -1;
+struct DeviceGuard {  // (no set / restore when the caller is on the engine's device already:
+  int prev = -1;       //  a launch-sized call should cost the launch, ~17 us epochs are host-bound)
   bool ok = false;
   explicit DeviceGuard(int dev) {
     if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev == dev) {
+      prev = -1;
+      ok = true;
+      return;
+    }
     ok = hipSetDevice(dev) == hipSuccess;
   }
   ~DeviceGuard() {
@@ -255,20 +260,25 @@ int check_monotone(jrq_engine* e, const uint64_t* off, uint32_t n) {
 }
 
 // offsets[i] = i * entry_bytes: the segment walk's view of a fixed-size batch the fixed kernel
-// cannot take (crc_fixed_ok)
+// cannot take (crc_fixed_k)
 __global__ void iota_offsets_kernel(uint64_t* off, uint32_t n, uint64_t entry_bytes) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += gridDim.x * blockDim.x)
     off[i] = static_cast<uint64_t>(i) * entry_bytes;
 }
 
-// crc64_fixed_kernel (crc64.hip) takes a batch of N entries of entry_bytes each when the
-// entries are whole 256-B multiples (4-half-round turns), 64 of them fit the u32 lane offsets,
-// the payload is 16-B aligned, and there is at least one entry per lane of the grid (fewer,
-// longer entries -- C5's 64k x 16 KiB -- keep every lane busy in the segment walk instead).
-bool crc_fixed_ok(const jrq_engine* e, const void* payload, uint64_t entry_bytes, uint32_t N) {
-  return entry_bytes >= 256 && entry_bytes % 256 == 0 && entry_bytes < (1ull << 26) &&
-         (reinterpret_cast<uintptr_t>(payload) & 15u) == 0 &&
-         static_cast<uint64_t>(N) >= static_cast<uint64_t>(e->crc_grid) * jrq::kCrcBlock;
+// crc64_fixed_kernel (crc64.hip) takes a batch of N entries of entry_bytes each, k lanes per
+// entry (k pieces): the fewest k (a power of two <= 64) that gives every lane of the grid a
+// piece, with pieces of whole 256-B multiples (4-half-round turns) whose 64-lane rows fit the
+// u32 lane offsets, on a 16-B aligned payload.  0 = not applicable (the offsets path).
+// C1: 1M x 256 B -> k = 1; C5: 64k x 16 KiB -> k = 2.
+uint32_t crc_fixed_k(const jrq_engine* e, const void* payload, uint64_t entry_bytes, uint32_t N) {
+  if (entry_bytes < 256 || entry_bytes % 256 != 0 || (reinterpret_cast<uintptr_t>(payload) & 15u))
+    return 0;
+  const uint64_t lanes = static_cast<uint64_t>(e->crc_grid) * jrq::kCrcBlock;
+  uint32_t k = 1;
+  while (static_cast<uint64_t>(N) * k < lanes && k < 64 && (entry_bytes / (2 * k)) % 256 == 0) k *= 2;
+  if (static_cast<uint64_t>(N) * k < lanes || entry_bytes / k >= (1ull << 26)) return 0;
+  return k;
 }
 
 // All N ranges of a host offsets array the same length (0 if not).
@@ -281,6 +291,7 @@ uint64_t uniform_length(const uint64_t* off, uint32_t n) {
 
 int crc_fixed_dispatch(jrq_engine* e, JrqCrcArgs& a, int log_entry) {
   a.slice = e->slice;
+  a.shift = e->shift;
   JRQ_HIP(e, jrq_launch_crc64_fixed(&a, log_entry, e->crc_grid, e->stream));
   return JRQ_OK;
 }
@@ -591,7 +602,8 @@ int jrq_crc64_fixed_dev(jrq_engine* e, const uint8_t* payload, uint64_t entry_by
   if (N == 0) return JRQ_OK;
   if (!payload || !crc_out) return fail(e, JRQ_E_INVALID, "null pointer");
   DeviceGuard guard(e->device);
-  if (!crc_fixed_ok(e, payload, entry_bytes, N)) {
+  const uint32_t k = crc_fixed_k(e, payload, entry_bytes, N);
+  if (k == 0) {
     const uint64_t* off;
     int rc;
     if ((rc = fixed_offsets(e, entry_bytes, N, &off))) return rc;
@@ -602,6 +614,7 @@ int jrq_crc64_fixed_dev(jrq_engine* e, const uint8_t* payload, uint64_t entry_by
   a.n = N;
   a.out = crc_out;
   a.entry_bytes = entry_bytes;
+  a.fixed_k = k;
   return crc_fixed_dispatch(e, a, 0);
 }
 
@@ -630,8 +643,9 @@ int jrq_crc64_batch(jrq_engine* e, const uint8_t* payload, const uint64_t* offse
   a.out = static_cast<uint64_t*>(dout);
   a.regs_slowpath = unaligned_bounds(offsets, N);
   const uint64_t ul = uniform_length(offsets, N);
-  if (crc_fixed_ok(e, dp, ul, N)) {
+  if (const uint32_t k = crc_fixed_k(e, dp, ul, N)) {
     a.entry_bytes = ul;
+    a.fixed_k = k;
     rc = crc_fixed_dispatch(e, a, 0);
   } else {
     rc = crc_dispatch(e, a, 0);
@@ -726,7 +740,8 @@ int jrq_logentry_checksum_fixed_dev(jrq_engine* e, const uint8_t* type, const in
   if ((expected == nullptr) != (corrupt_out == nullptr))
     return fail(e, JRQ_E_INVALID, "expected and corrupt_out go together");
   DeviceGuard guard(e->device);
-  if (!crc_fixed_ok(e, payload, entry_bytes, N)) {
+  const uint32_t k = crc_fixed_k(e, payload, entry_bytes, N);
+  if (k == 0) {
     const uint64_t* off;
     int rc;
     if ((rc = fixed_offsets(e, entry_bytes, N, &off))) return rc;
@@ -745,6 +760,7 @@ int jrq_logentry_checksum_fixed_dev(jrq_engine* e, const uint8_t* type, const in
   a.has = has;
   a.corrupt = corrupt_out;
   a.entry_bytes = entry_bytes;
+  a.fixed_k = k;
   return crc_fixed_dispatch(e, a, 1);
 }
 
@@ -780,7 +796,7 @@ int jrq_logentry_checksum_batch(jrq_engine* e, const uint8_t* type, const int64_
   if ((rc = ensure_stage(e, 12, static_cast<size_t>(N) * 8, &dout))) return rc;
   if (corrupt_out && (rc = ensure_stage(e, 13, N, &dcor))) return rc;
   const uint64_t ul = uniform_length(offsets, N);
-  if (crc_fixed_ok(e, dp, ul, N)) {  // equal entries: the fixed-size kernel (one launch)
+  if (crc_fixed_k(e, dp, ul, N)) {  // equal entries: the fixed-size kernel (one launch)
     rc = jrq_logentry_checksum_fixed_dev(e, dt, di, dtm, dpx, dp, ul, N, static_cast<uint64_t*>(dout),
                                          dex, dh, static_cast<uint8_t*>(dcor));
   } else {

@@ -100,6 +100,7 @@ struct JrqCrcArgs {
   uint32_t regs_slowpath;  // 1: boundary half-rounds hash from registers (crc64_rounds_kernel<true>)
   uint64_t* stream_state;  // nullable: streaming Checksum registers folded by the finish kernel
   uint64_t entry_bytes;    // crc64_fixed_kernel: every entry this long, back to back (no offsets)
+  uint32_t fixed_k;        // crc64_fixed_kernel: lanes per entry (power of two, 1..64)
 };
 
 // Leader lease / alive-quorum check (quorum.hip, lease kernel).

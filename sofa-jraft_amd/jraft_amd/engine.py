@@ -125,6 +125,52 @@ class Engine:
         check(self._L.jrq_quorum_epoch_dev(self._h, C.byref(b), _dev_ptr(committed_out),
                                            _dev_ptr(status_out), G), self._h)
 
+    def quorum_epoch_launcher(self, match, pending_index, last_appended, last_committed, conf,
+                              committed_out, status_out, run_off=None, run_start=None,
+                              run_conf=None):
+        """quorum_epoch_dev with its arguments resolved once: returns a zero-argument callable
+        that only makes the C call -- the per-epoch host cost of a C / JNI host that keeps its
+        jrq_group_batch (bench.py's epoch loop; Python's per-call argument marshalling would
+        otherwise outlast a 17 us epoch)."""
+        P = match.shape[0]
+        G = pending_index.shape[0]
+        b = self._batch(_dev_ptr, match, pending_index, last_appended, last_committed, conf,
+                        run_off, run_start, run_conf, num_peers=P, match_ld=match.stride(0),
+                        num_runs=0 if run_start is None else run_start.shape[0])
+        fn, h, ref = self._L.jrq_quorum_epoch_dev, self._h, C.byref(b)
+        co, so = _dev_ptr(committed_out), _dev_ptr(status_out)
+        keep = (b, match, pending_index, last_appended, last_committed, conf, committed_out,
+                status_out, run_off, run_start, run_conf)
+
+        def launch():
+            rc = fn(h, ref, co, so, G)
+            if rc:
+                check(rc, h)
+        launch.keep = keep
+        return launch
+
+    def quorum_epochs_launcher(self, match, pending_index, last_appended, last_committed, conf,
+                               committed_out, status_out, run_off=None, run_start=None,
+                               run_conf=None):
+        """quorum_epochs_dev with its arguments resolved once (see quorum_epoch_launcher)."""
+        K, P = match.shape[0], match.shape[1]
+        G = pending_index.shape[0]
+        b = self._batch(_dev_ptr, match, pending_index, last_appended, last_committed, conf,
+                        run_off, run_start, run_conf, num_peers=P, match_ld=match.stride(1),
+                        num_runs=0 if run_start is None else run_start.shape[0])
+        fn, h, ref = self._L.jrq_quorum_epochs_dev, self._h, C.byref(b)
+        me, le = match.stride(0), last_appended.stride(0)
+        co, so = _dev_ptr(committed_out), _dev_ptr(status_out)
+        keep = (b, match, pending_index, last_appended, last_committed, conf, committed_out,
+                status_out, run_off, run_start, run_conf)
+
+        def launch():
+            rc = fn(h, ref, K, me, le, co, so, G)
+            if rc:
+                check(rc, h)
+        launch.keep = keep
+        return launch
+
     def quorum_epochs_dev(self, match, pending_index, last_appended, last_committed, conf,
                           committed_out, status_out, run_off=None, run_start=None, run_conf=None):
         """K epochs in one launch: match [K, P, ld], last_appended [K, G] (torch tensors);

@@ -189,11 +189,14 @@ LANES = 256 * 512  # the CRC grid's lanes on MI355X: the fixed-size kernel wants
 
 
 @pytest.mark.parametrize("el,n,tail", [(256, 140000, []), (512, LANES + 5, []), (1024, LANES, [77]),
-                                       (256, LANES, [0]), (768, 140000, []), (256, 4000, [])])
+                                       (256, LANES, [0]), (768, 140000, []), (256, 4000, []),
+                                       (512, 70001, []), (1024, 40000, []), (16384, 2100, []),
+                                       (4096, 33000, [])])
 def test_fixed_size_batches(engine, oracle, el, n, tail):
-    """Host variants route batches of equal entries (256-B multiples, >= one per lane) to the
-    one-launch fixed-size kernel (crc64.hip crc64_fixed_kernel: fields, verify and the store
-    there); a ragged / zero-length tail, other lengths and small batches take the segment walk.
+    """Host variants route batches of equal entries to the one-launch fixed-size kernel
+    (crc64.hip crc64_fixed_kernel: k = 1, 2, 4 .. 64 lanes per entry combined by linearity,
+    fields, verify and the store there); a ragged / zero-length tail, other lengths and small
+    batches take the segment walk.
     Every result vs the oracle: LogEntry (verify, has, peers) and plain CRC."""
     lens = [el] * n + tail
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
@@ -213,7 +216,8 @@ def test_fixed_size_batches(engine, oracle, el, n, tail):
     np.testing.assert_array_equal(engine.crc64_batch(payload, offs), oracle.crc64_batch(payload, offs))
 
 
-@pytest.mark.parametrize("el,n", [(256, 140000), (512, LANES + 7), (100, 5000), (256, 3000)])
+@pytest.mark.parametrize("el,n", [(256, 140000), (512, LANES + 7), (100, 5000), (256, 3000),
+                                  (16384, 8192), (16384, 8191)])
 def test_fixed_dev_api(engine, oracle, el, n):
     """jrq_logentry_checksum_fixed_dev / jrq_crc64_fixed_dev (device buffers, no offsets): the
     fixed-size kernel, or the offsets path over generated offsets (100-B entries, few entries)."""

@@ -95,6 +95,13 @@ def main():
         legs["C1"] = (lambda e, o: (lambda: e.logentry_checksum_batch_dev(
             d1["etype"], d1["index"], d1["term"], None, d1["payload"], d1["offsets"], o)),
             lambda: torch.empty(1 << 20, dtype=torch.int64, device=dev))
+    if "C5f" in legs_env:  # the C5 entries (16 KiB each) through the fixed-size entry point
+        def mk_c5f(e, o):
+            cor = torch.empty(n5, dtype=torch.uint8, device=dev)
+            return lambda: e.logentry_checksum_fixed_dev(d5["etype"], d5["index"], d5["term"], None,
+                                                         d5["payload"], 16 << 10, o,
+                                                         expected=exp5, corrupt=cor)
+        legs["C5f"] = (mk_c5f, lambda: torch.empty(n5, dtype=torch.int64, device=dev))
     if "C1f" in legs_env:  # the same 256-B entries through the fixed-size entry point
         if "C1" not in legs_env:
             eb1 = W.entry_batch(1 << 20, 256, seed=5)
@@ -129,7 +136,7 @@ def main():
     pay64 = d5["payload"].view(torch.int64)
     acc = torch.empty((), dtype=torch.int64, device=dev)
     fns = {}
-    needs = {"C1f": "jrq_logentry_checksum_fixed_dev"}
+    needs = {"C1f": "jrq_logentry_checksum_fixed_dev", "C5f": "jrq_logentry_checksum_fixed_dev"}
     for leg, (mk, new_out) in legs.items():
         for name, e in variants:
             if leg in needs and not hasattr(e._L, needs[leg]):

@@ -81,7 +81,7 @@ def main():
         f = res["calibration"]["bytes_per_FETCH_byte"]
         for leg, ks in res["legs"].items():
             for k, v in ks.items():
-                if "crc64_rounds_kernel" in k and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+                if ("crc64_rounds_kernel" in k or "crc64_fixed_kernel" in k) and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
                     v["hbm_bytes_per_launch"] = (f * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
                     v["fetch_factor"] = f
     res["legs"] = {k: dict(v) for k, v in res["legs"].items()}
