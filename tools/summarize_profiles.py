@@ -61,6 +61,19 @@ def main():
                 continue
             for c, v in vals.items():
                 res["legs"][leg][k][c] = v
+    # per-leg kernel durations from the same passes' kernel traces (one workload per kernel name
+    # per pass, unlike the full-bench kernel stats where e.g. C1 and C5 share a kernel name)
+    for f in sorted(glob.glob(os.path.join(OUT, "pmc_*_FETCH_SIZE", "*kernel_trace.csv"))):
+        leg = os.path.basename(os.path.dirname(f))[4:].rsplit("_FETCH_SIZE", 1)[0]
+        durs = collections.defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            k = kernel_key(r["Kernel_Name"])
+            if "jrq" in k:
+                durs[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        for k, v in durs.items():
+            v.sort()
+            res["legs"][leg][k]["duration_ns_median"] = float(v[len(v) // 2])
+            res["legs"][leg][k]["dispatches"] = len(v)
     for leg, ks in res["legs"].items():
         for k, v in ks.items():
             if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
