@@ -958,13 +958,22 @@ def leg_c1(ctx, args):
         crc(i)
         eng.quorum_epoch_dev(q1d["match"], q1d["pending_index"], q1d["last_appended"],
                              q1d["last_committed"], q1d["conf"], c1c, c1s)
-    crc_ms, _ = ctx.timed(crc, max(10, args.steps), 2)
-    ms, _ = ctx.timed(step, max(10, args.steps), 2)
-    ok = None
+
+    def crc_offsets(i):  # the same entries through the general offsets entry point
+        eng.logentry_checksum_batch_dev(d1["etype"], d1["index"], d1["term"], None,
+                                        d1["payload"], d1["offsets"], out1)
+    off_ms, _ = ctx.timed(crc_offsets, max(10, args.steps), 2)
+    ok_off = None
+    exp1 = None
     if ctx.oracle_checks:
         import jraft_oracle as O
         exp1 = O.logentry_checksum_batch(e1["etype"], e1["index"], e1["term"], None,
                                          e1["payload"], e1["offsets"])
+        ok_off = bool(np.array_equal(out1.cpu().numpy().view(np.uint64), exp1))
+    crc_ms, _ = ctx.timed(crc, max(10, args.steps), 2)
+    ms, _ = ctx.timed(step, max(10, args.steps), 2)
+    ok = None
+    if ctx.oracle_checks:
         ce, se, _ = O.quorum_epoch_replay(q1["match"], q1["pending_index"], q1["last_appended"],
                                           q1["last_committed"], q1["conf"], chunk=1024)
         ok = bool(np.array_equal(out1.cpu().numpy().view(np.uint64), exp1)) and \
@@ -974,6 +983,10 @@ def leg_c1(ctx, args):
             "ms_per_step": ms, "entries_per_s": n1 / (ms * 1e-3),
             "GBps_payload": n1 * c1["entry_bytes"] / (ms * 1e-3) / 1e9,
             "bit_exact_vs_oracle": ok,
+            "offsets_path": {"ms_per_launch": off_ms, "bit_exact_vs_oracle": ok_off,
+                             "how": "jrq_logentry_checksum_batch_dev (segment walk + finish kernel)",
+                             "frac": crc_bytes(n1, n1 * c1["entry_bytes"], verify=False) /
+                             (off_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS},
             "roofline": roofline(alg, crc_ms, kernel="crc64_fixed_kernel<true> (1M x 256 B LogEntries, "
                                                     "jrq_logentry_checksum_fixed_dev)",
                                  **pmc_traffic("C1", "crc64_fixed_kernel<true>"))}
