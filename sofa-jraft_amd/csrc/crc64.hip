@@ -216,6 +216,22 @@ __device__ __forceinline__ void hash_regs(const CrcTab& tb, RState& r, const u32
   }
 }
 
+// CRC of the first b (< 64) bytes of a 64-B line held in registers (each step is kept or
+// dropped: no per-lane loop bound).
+__device__ __forceinline__ uint64_t prefix_crc(const CrcTab& tb, const uint4 (&w)[4], uint32_t b,
+                                               const char* lds) {
+  RState r{0u, 0u};
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    const uint4 q = w[t >> 4];
+    const uint32_t word = (t & 15) < 4 ? q.x : (t & 15) < 8 ? q.y : (t & 15) < 12 ? q.z : q.w;
+    RState n = r;
+    tb.step1(n, (word >> (8 * (t & 3))) & 0xFFu, lds);
+    if (static_cast<uint32_t>(t) < b) r = n;
+  }
+  return crc_value(r);
+}
+
 // c * x^(8n) mod P via the global power tables: one 8-lookup pass per set bit of n.
 __device__ __forceinline__ uint64_t crc_shift(uint64_t c, uint64_t n,
                                               const uint64_t* __restrict__ shift) {
@@ -387,6 +403,7 @@ template <uint32_t kBlock, bool kRegs>
 __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
   __shared__ uint32_t offwin[kBlock / 64][kOffWin];
+  if (a.gate != nullptr && a.gate[0] != 0) return;  // V2: the fixed-size path took the batch
   const char* lds = reinterpret_cast<const char*>(lds_tab);
 
   // The replicated LDS image of the slice tables: its L2 reads go out first, the LDS writes
@@ -772,6 +789,7 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
 template <bool kLogEntry>
 __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
   __shared__ uint64_t r0[256];
+  if (a.gate != nullptr && a.gate[0] != 0) return;  // V2: the fixed-size path took the batch
   if (kLogEntry) r0[threadIdx.x] = a.slice[threadIdx.x];  // R0 = bswap(T0) (blockDim == 256)
   __syncthreads();
   const uint64_t* __restrict__ off = a.offsets;
@@ -830,9 +848,14 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
 // so the field loads of a row sit at least 16 ring loads before their use (the compiler never
 // waits for the ring on their account).  C1 (1M x 256 B): the segment walk wrote 6.5x its 8 MB
 // of results as scattered 8-B stores and re-read them in the finish kernel.
-template <bool kLogEntry>
+// kStarts (V2 decode): entry i starts at payload + starts[i] (non-decreasing, any byte
+// alignment: buffer loads take unaligned offsets), k and EL come from the device words
+// gate[0..1] written by v2_uniform (gate[3]: the payload's end offset); k == 0 means the
+// segment walk takes the batch instead.
+template <bool kLogEntry, bool kStarts>
 __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
+  if (kStarts && a.gate[0] == 0) return;
   const char* lds = reinterpret_cast<const char*>(lds_tab);
   constexpr uint32_t kTabPer = kCrcLdsBytes / 8 / kCrcBlock;
   uint64_t tab_v[kTabPer];  // this thread's share of the table image (written after the first loads)
@@ -849,8 +872,10 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   const uint32_t L0 = __builtin_amdgcn_readfirstlane(L & ~63u);
   const uint32_t lane = L - L0;
   const uint32_t n = a.n;
-  const uint32_t K = a.fixed_k, kl = 31u - __builtin_clz(K);  // lanes per entry, log2
-  const uint64_t PS = a.entry_bytes >> kl;                    // piece bytes
+  const uint32_t K = kStarts ? static_cast<uint32_t>(a.gate[0]) : a.fixed_k;
+  const uint64_t EL = kStarts ? a.gate[1] : a.entry_bytes;
+  const uint32_t kl = 31u - __builtin_clz(K);  // lanes per entry, log2
+  const uint64_t PS = EL >> kl;                // piece bytes
   const uint32_t EPR = 64u >> kl;                              // entries per row
   const uint32_t rows = (n + EPR - 1) / EPR;
   // contiguous rows per wave (a wave streams 64 * EL * rows bytes in order)
@@ -865,20 +890,46 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   }
   const uint32_t HE = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(PS >> 6));  // halves per piece
   const uint32_t turns = HE >> 2;
-  const uint64_t total = static_cast<uint64_t>(n) * a.entry_bytes;
+  // load window end (read once: the loads' memory clobber would re-read it in the ring)
+  const uint64_t total = kStarts ? a.gate[3] : static_cast<uint64_t>(n) * EL;
   const uint32_t WS = static_cast<uint32_t>(PS);  // lane-to-lane stride (64 * PS < 2^32)
   const uint32_t qb = (L & 15u) * WS + 16u * ((L >> 4) & 3u);
-  const uint32_t qa0 = qb, qa1 = qb + 16u * WS, qa2 = qb + 32u * WS, qa3 = qb + 48u * WS;
+  uint32_t qa0 = qb, qa1 = qb + 16u * WS, qa2 = qb + 32u * WS, qa3 = qb + 48u * WS;
   const uintptr_t pbase = reinterpret_cast<uintptr_t>(a.payload);
+  // kStarts: the row's base (its first piece) and each owner's offset from it, through
+  // __shfl (the load of lane 16q + c reads owner 16q + c's piece); a new row costs a load
+  // Byte-misaligned 16-B loads stream at ~60 % of the aligned rate (tools/unal_probe.hip) and
+  // 64-B halves across two lines double the L2 requests: a piece starting at byte b of a 64-B
+  // line is hashed over [start - b, start - b + PS) (same ring, aligned loads) and corrected
+  // after the loop (the b bytes before it and the b bytes it missed, by linearity); the
+  // payload is 64-B aligned (the host checks)
+  uint64_t row_base = 0;
+  auto set_row = [&](uint32_t row) {
+    const uint32_t er = row * EPR + (lane >> kl);
+    const uint64_t ps = (a.starts[er < n ? er : n - 1u] + static_cast<uint64_t>(lane & (K - 1u)) * PS) & ~63ull;
+    const uint32_t rb_lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ps));
+    const uint32_t rb_hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ps >> 32));
+    row_base = (static_cast<uint64_t>(rb_hi) << 32) | rb_lo;
+    const uint32_t rel = static_cast<uint32_t>(ps - row_base);
+    const uint32_t c = L & 15u, ro = 16u * ((L >> 4) & 3u);
+    qa0 = __shfl(rel, static_cast<int>(c)) + ro;
+    qa1 = __shfl(rel, static_cast<int>(16u + c)) + ro;
+    qa2 = __shfl(rel, static_cast<int>(32u + c)) + ro;
+    qa3 = __shfl(rel, static_cast<int>(48u + c)) + ro;
+  };
+  if (kStarts) set_row(r0);
   // load cursor (row, half of the entry) of the next half-round to issue, scalar; past the
   // wave's last row it keeps re-reading that row's last half (L2-hot, results unused)
   uint32_t crow = r0, chalf = 0;
   auto load_half = [&](u32x4 (&H)[4]) {
-    const uint64_t o = static_cast<uint64_t>(crow) * 64u * PS + static_cast<uint64_t>(chalf) * 64u;
+    const uint64_t o = kStarts ? row_base + static_cast<uint64_t>(chalf) * 64u
+                               : static_cast<uint64_t>(crow) * 64u * PS + static_cast<uint64_t>(chalf) * 64u;
     const uint64_t hp = pbase + o;
     const uint32_t hlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp));
     const uint32_t hhi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp >> 32));
-    const uint64_t left = total - o;  // lanes past entry n-1 read zeros
+    // lanes past entry n-1 read zeros; kStarts: the dword past the last chunk of the batch may
+    // lie past the payload (gate[3] = its end): zeros too
+    const uint64_t left = total - o;
     const uint32_t hn = __builtin_amdgcn_readfirstlane(
         static_cast<uint32_t>(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left));
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
@@ -894,6 +945,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     } else if (crow + 1 < r1) {
       ++crow;
       chalf = 0;
+      if (kStarts) set_row(crow);
     }
   };
   u32x4 h0[4], h1[4], h2[4], h3[4];
@@ -940,6 +992,32 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
       tb.step64(s, h3, lds);
     } while (++q < turns);
     uint64_t c = crc_value(s);
+    if (kStarts) {  // hashed [ps - b, ps - b + PS): drop the b bytes before, add the b missed
+      const uint64_t ps = a.starts[e] + static_cast<uint64_t>(piece) * PS;
+      const uint32_t b = static_cast<uint32_t>(ps & 63u);
+      // both are the first b bytes of a 64-B line: J before the piece, T its tail (the line
+      // past T may run past the records' end: then bytes)
+      const uint64_t jl = ps - b, tl = ps - b + PS;
+      uint4 jw[4], tw[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) jw[i] = reinterpret_cast<const uint4*>(a.payload + jl)[i];
+      const bool tail_lines = tl + 64u <= total;
+      if (tail_lines) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tw[i] = reinterpret_cast<const uint4*>(a.payload + tl)[i];
+      }
+      const uint64_t cj = prefix_crc(tb, jw, b, lds);
+      uint64_t ct;
+      if (tail_lines) {
+        ct = prefix_crc(tb, tw, b, lds);
+      } else {
+        RState r{0u, 0u};
+        for (uint32_t t = 0; t < b; ++t) tb.step1(r, a.payload[tl + t], lds);
+        ct = crc_value(r);
+      }
+      c ^= crc_shift(cj, PS - b, a.shift);   // crc(piece minus its last b bytes)
+      c = crc_shift(c, b, a.shift) ^ ct;     // ... then those b bytes
+    }
     // pieces -> entry: at level l, the group of 2^l lanes holding the earlier bytes is shifted
     // past the 2^l * PS bytes of its partner group (x^(8 * 2^l * PS), global power tables)
     for (uint32_t l = 0; l < kl; ++l) {
@@ -968,10 +1046,15 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
 // < 2^32, (entry_bytes / fixed_k) % 256 == 0.
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64_fixed(
     JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {
-  if (log_entry)
-    hipLaunchKernelGGL(jrq::crc64_fixed_kernel<true>, dim3(grid), dim3(jrq::kCrcBlock), 0, stream, *args);
+  if (args->starts != nullptr)  // plain CRCs at given starts, gated on the device (V2 decode)
+    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<false, true>), dim3(grid), dim3(jrq::kCrcBlock), 0,
+                       stream, *args);
+  else if (log_entry)
+    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<true, false>), dim3(grid), dim3(jrq::kCrcBlock), 0,
+                       stream, *args);
   else
-    hipLaunchKernelGGL(jrq::crc64_fixed_kernel<false>, dim3(grid), dim3(jrq::kCrcBlock), 0, stream, *args);
+    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<false, false>), dim3(grid), dim3(jrq::kCrcBlock), 0,
+                       stream, *args);
   return hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ extern "C" hipError_t jrq_launch_ae_meta(const JrqAeArgs* a, hipStream_t stream)
 extern "C" hipError_t jrq_launch_lease(const JrqLeaseArgs* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_fanout(const JrqFanoutArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_v2_parse(const JrqV2Args* a, hipStream_t stream);
+extern "C" hipError_t jrq_launch_v2_gate(const JrqV2Args* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_v2_finish(const JrqV2Args* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_first_corrupt(const JrqAeArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_table_update(const JrqTableArgs* a, const JrqGroupState* states,
@@ -76,7 +77,7 @@ struct jrq_engine {
   uint32_t crc_seg_map = 1;  // JRQ_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
-  DevBuf stage[25];  // 0-13 host-variant staging, 14 stream-update chunk CRCs, 15 fixed-size offsets, 16-19 AppendEntries scratch, 21-24 V2 decode scratch
+  DevBuf stage[27];  // 0-13 host-variant staging, 14 stream-update chunk CRCs, 15 fixed-size offsets, 16-19 AppendEntries scratch, 21-26 V2 decode scratch
   // pinned bounce buffers for the host variants' uploads (stage_in): two chunks, each
   // reusable once the copy recorded after it has run
   uint8_t* bounce[2] = {nullptr, nullptr};
@@ -1080,6 +1081,9 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
   if ((rc = ensure_stage(e, 23, (static_cast<size_t>(N) + 1) * 8, &crc2))) return rc;
   void* edges;  // per record: header CRC, trailer CRC, lengths
   if ((rc = ensure_stage(e, 24, static_cast<size_t>(N) * 24, &edges))) return rc;
+  void *gate, *crcd;  // the fixed-size data CRC path: {k, L, bad, end, count}, per-record data CRCs
+  if ((rc = ensure_stage(e, 25, 40, &gate))) return rc;
+  if ((rc = ensure_stage(e, 26, static_cast<size_t>(N) * 8, &crcd))) return rc;
   JrqV2Args v{};
   v.rec = rec;
   v.off = off;
@@ -1103,10 +1107,30 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
   v.hcrc = static_cast<uint64_t*>(edges);
   v.tcrc = v.hcrc + N;
   v.lens = v.tcrc + N;
+  v.gate = static_cast<uint64_t*>(gate);
+  v.crc_data = static_cast<const uint64_t*>(crcd);
+  // (the fixed-size path hashes from the 64-B line of each data start: records 64-B aligned)
+  v.lanes = (reinterpret_cast<uintptr_t>(rec) & 63u) ? ~0ull
+                                                     : static_cast<uint64_t>(e->crc_grid) * jrq::kCrcBlock;
   JRQ_HIP(e, jrq_launch_v2_parse(&v, e->stream));
-  // one range per record from its data start (the leading header first): one streaming pass
-  // over the records, one entry boundary per record (v2_finish recovers the data CRCs)
+  JRQ_HIP(e, jrq_launch_v2_gate(&v, e->num_cus, e->stream));
+  // every record with the same data length (the common case: fixed-size commands): the data
+  // ranges alone, k lanes per record (crc64_fixed_kernel at the data starts); the gate words
+  // on the device pick this or the segment walk below, each kernel of the other path returns
+  {
+    JrqCrcArgs f{};
+    f.payload = rec;
+    f.starts = v.data_off;
+    f.gate = v.gate;
+    f.n = N;
+    f.out = static_cast<uint64_t*>(crcd);
+    if ((rc = crc_fixed_dispatch(e, f, 0))) return rc;
+  }
+  // otherwise one range per record from its data start (the leading header first): one
+  // streaming pass over the records, one entry boundary per record (v2_finish recovers the
+  // data CRCs)
   JrqCrcArgs a{};
+  a.gate = v.gate;
   a.payload = rec;
   a.offsets = v.off2;
   a.n = N + 1;

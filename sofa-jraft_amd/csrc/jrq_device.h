@@ -101,6 +101,9 @@ struct JrqCrcArgs {
   uint64_t* stream_state;  // nullable: streaming Checksum registers folded by the finish kernel
   uint64_t entry_bytes;    // crc64_fixed_kernel: every entry this long, back to back (no offsets)
   uint32_t fixed_k;        // crc64_fixed_kernel: lanes per entry (power of two, 1..64)
+  const uint64_t* starts;  // crc64_fixed_kernel<., true>: entry i starts at payload + starts[i]
+  const uint64_t* gate;    // nullable device words {k, entry_bytes} (V2 decode): the starts
+                           // kernel runs iff k != 0, the segment walk (rounds + finish) iff k == 0
 };
 
 // Leader lease / alive-quorum check (quorum.hip, lease kernel).
@@ -174,7 +177,21 @@ struct JrqV2Args {
   uint64_t* hcrc;          // scratch [n] CRC of each record's bytes before its data
   uint64_t* tcrc;          // scratch [n] CRC of each record's bytes after its data
   uint64_t* lens;          // scratch [n] header length << 32 | trailer length
+  uint64_t* gate;          // scratch [5]: {k, L, bad, end, count} -- the data CRCs by crc64_fixed_kernel
+                           // (k lanes per record) when every record decoded with data length L
+  const uint64_t* crc_data;  // scratch [n]: the data CRCs of that path
+  uint64_t lanes;          // lanes of the CRC grid (crc64_fixed_kernel)
 };
+
+// Lanes per entry of crc64_fixed_kernel for N entries of L bytes on `lanes` lanes: the fewest
+// power of two (<= 64) giving every lane a piece of whole 256-B multiples; 0 = not applicable.
+__host__ __device__ inline uint32_t jrq_fixed_k(uint64_t L, uint32_t n, uint64_t lanes) {
+  if (L < 256 || L % 256 != 0) return 0;
+  uint32_t k = 1;
+  while (static_cast<uint64_t>(n) * k < lanes && k < 64 && (L / (2 * k)) % 256 == 0) k *= 2;
+  if (static_cast<uint64_t>(n) * k < lanes || L / k > (1ull << 25)) return 0;
+  return k;
+}
 
 struct JrqQuorumArgs {
   const int64_t* match;

@@ -200,6 +200,10 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r == 0) {
+    if (a.gate != nullptr) {  // v2_uniform's flag and arrival count (it runs next)
+      a.gate[2] = 0;
+      a.gate[4] = 0;
+    }
     a.off2[0] = a.off[0];
     a.off2[a.n + 1] = a.off[a.n];
   }
@@ -328,6 +332,33 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
   a.lens[r] = (hl << 32) | tl;
 }
 
+// Every record decoded, all with the data length L of record 0, data ranges in order and each
+// 64 consecutive ones within 1 GiB (the fixed-size CRC path's conditions: crc64_fixed_kernel
+// reads a row of records through one buffer descriptor at u32 offsets from its first start).
+// Any block that finds one broken sets gate[2]; the last block to arrive (gate[4], zeroed by
+// v2_parse) writes gate = {k, L, bad, end}: k lanes per record for crc64_fixed_kernel, 0 = the
+// segment walk.
+__global__ __launch_bounds__(256) void v2_uniform(JrqV2Args a) {
+  const uint64_t L0 = a.data_len[0];
+  bool bad = false;
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += gridDim.x * blockDim.x) {
+    const uint64_t d = a.data_off[r];
+    bad = bad || a.status[r] != kV2Ok || a.data_len[r] != L0;
+    if (r > 0) bad = bad || d < a.data_off[r - 1] + L0;
+    if (r >= 63) bad = bad || d + L0 - a.data_off[r - 63] >= (1ull << 30);
+  }
+  if (__syncthreads_or(bad) && threadIdx.x == 0) a.gate[2] = 1;
+  if (threadIdx.x != 0) return;
+  __threadfence();
+  if (atomicAdd(reinterpret_cast<unsigned long long*>(a.gate + 4), 1ull) != gridDim.x - 1u) return;
+  __threadfence();
+  const uint64_t L = L0;
+  const uint32_t k = __atomic_load_n(a.gate + 2, __ATOMIC_RELAXED) ? 0u : jrq_fixed_k(L, a.n, a.lanes);
+  a.gate[0] = L / (k ? k : 1u) <= (1ull << 23) ? k : 0u;
+  a.gate[1] = L;
+  a.gate[3] = a.off[a.n];  // the records' end: crc64_fixed_kernel's load window
+}
+
 // The CRC pass hashes one range per record, [data start, next record's data start): the data,
 // then a suffix of k bytes -- the record's trailer (checksum / learner fields) and the next
 // record's header.  CRC64 here is linear (init 0, xorout 0) and x is invertible mod P
@@ -347,10 +378,13 @@ __global__ __launch_bounds__(256) void v2_finish(JrqV2Args a) {
   }
   __syncthreads();
   const uint32_t stride = gridDim.x * blockDim.x;
+  const bool fixed = a.gate != nullptr && a.gate[0] != 0;  // data CRCs by crc64_fixed_kernel
   for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
     const bool ok = a.status[r] == kV2Ok;
     uint64_t c = 0;
-    if (ok) {
+    if (ok && fixed) {
+      c = a.partial[r] ^ a.crc_data[r];
+    } else if (ok) {
       const bool more = r + 1 < a.n;
       uint64_t h = more ? a.lens[r + 1] >> 32 : 0;  // next record's header (0 if it failed)
       const uint64_t k = (a.lens[r] & 0xFFFFFFFFull) + h;
@@ -384,6 +418,15 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_v2_parse(
     const JrqV2Args* a, hipStream_t stream) {
   const uint32_t blocks = (a->n + 255) / 256;
   hipLaunchKernelGGL(jrq::v2_parse, dim3(blocks ? blocks : 1), dim3(256), 0, stream, *a);
+  return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_v2_gate(
+    const JrqV2Args* a, int num_cus, hipStream_t stream) {
+  uint32_t blocks = (a->n + 255) / 256;
+  const uint32_t cap = static_cast<uint32_t>(num_cus) * 2u;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(jrq::v2_uniform, dim3(blocks ? blocks : 1), dim3(256), 0, stream, *a);
   return hipGetLastError();
 }
 

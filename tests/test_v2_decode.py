@@ -327,3 +327,51 @@ def test_gpu_mutated_corpus(engine, seed):
     for k in ("status", "type", "index", "term", "stored", "has_checksum", "data_off",
               "data_len", "peer_counts", "computed", "corrupt"):
         assert np.array_equal(g[k][keep], o[k][keep]), k
+
+
+def uniform_batch(seed, n, L, bump=None):
+    """n DATA records of L data bytes each (record `bump` 256 B longer), varint-ragged headers
+    (random index / term) so the data starts sit at every byte alignment, random stored
+    checksums: the fixed-size data CRC path's batch (crc64_fixed_kernel at the data starts)."""
+    from jraft_amd import workloads as W
+    rng = np.random.default_rng(seed)
+    lens = np.full(n, L, np.uint64)
+    if bump is not None:
+        lens[bump] += 256
+    offsets = np.zeros(n + 1, np.uint64)
+    offsets[1:] = np.cumsum(lens)
+    payload = rng.integers(0, 256, int(offsets[-1]), dtype=np.uint8)
+    index = rng.integers(1, 1 << 50, n)
+    term = rng.integers(1, 1 << 20, n)
+    ck = rng.integers(0, 1 << 63, n, dtype=np.uint64)
+    return W.v2_records(np.ones(n, np.int64), index, term, payload, offsets, ck)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,L,bump", [
+    (4096, 16384, None),   # k = 32 lanes per record
+    (16384, 4096, None),   # k = 8
+    (65536, 1024, None),   # k = 2
+    (4096, 16384, 1000),   # one longer record: the segment walk
+    (300, 16384, None),    # too few records to fill the grid: the segment walk
+    (4096, 16000, None),   # L off the 256-B grid: the segment walk
+])
+def test_gpu_uniform_data_len(engine, n, L, bump):
+    buf, off = uniform_batch(n + L, n, L, bump)
+    o = O.v2_decode_batch(buf, off)
+    assert (o["status"] == O.V2_OK).all()
+    # half of the stored checksums right: the corrupt flags take both values
+    rng = np.random.default_rng(n)
+    right = rng.random(n) < 0.5
+    from jraft_amd import workloads as W
+    lens = o["data_len"].astype(np.uint64)
+    doff = o["data_off"].astype(np.uint64)
+    offsets = np.zeros(n + 1, np.uint64)
+    offsets[1:] = np.cumsum(lens)
+    payload = np.concatenate([buf[int(a):int(a + b)] for a, b in zip(doff, lens)])
+    ck = np.where(right, o["computed"], o["computed"] ^ np.uint64(0x9E3779B97F4A7C15))
+    buf, off = W.v2_records(o["type"].astype(np.int64), o["index"], o["term"], payload, offsets, ck)
+    o = O.v2_decode_batch(buf, off)
+    g = engine.v2_decode_verify(buf, off)
+    check_gpu_vs_oracle(g, o)
+    assert np.array_equal(g["corrupt"].astype(bool), ~right)
