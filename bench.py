@@ -804,8 +804,8 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
            "offsets_path": {"ms_per_launch": vo_ms, "bit_exact_vs_oracle": ok_off,
                             "GBps_payload": pay / (vo_ms * 1e-3) / 1e9,
                             "how": "jrq_logentry_checksum_batch_dev (segment walk + finish kernel)"},
-           "roofline": roofline(alg_v, v_ms, kernel="crc64_fixed_kernel<true>",
-                                **pmc_traffic("C5", "crc64_fixed_kernel<true>"))}
+           "roofline": roofline(alg_v, v_ms, kernel="crc64_fixed_kernel<true, false>",
+                                **pmc_traffic("C5", "crc64_fixed_kernel<true, false>"))}
     c5_step = {"workload": "C5 as BASELINE states it: 64k regions x 3 replicas x 16 KiB entries; "
                            "one step = CRC64 verify of the 64k entries + commit of the 64k groups",
                "ms_per_step": s_ms, "verify_ms": v_ms, "commit_ms": c_ms,
@@ -989,9 +989,9 @@ def leg_c1(ctx, args):
                              "how": "jrq_logentry_checksum_batch_dev (segment walk + finish kernel)",
                              "frac": crc_bytes(n1, n1 * c1["entry_bytes"], verify=False) /
                              (off_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS},
-            "roofline": roofline(alg, crc_ms, kernel="crc64_fixed_kernel<true> (1M x 256 B LogEntries, "
+            "roofline": roofline(alg, crc_ms, kernel="crc64_fixed_kernel<true, false> (1M x 256 B LogEntries, "
                                                     "jrq_logentry_checksum_fixed_dev)",
-                                 **pmc_traffic("C1", "crc64_fixed_kernel<true>"))}
+                                 **pmc_traffic("C1", "crc64_fixed_kernel<true, false>"))}
 
 
 def leg_lease(ctx, args, quorum_conf_dev, G, P):
