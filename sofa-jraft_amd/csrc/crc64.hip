@@ -219,8 +219,7 @@ __device__ __forceinline__ void hash_regs(const CrcTab& tb, RState& r, const u32
 // CRC of the first b (< 64) bytes of a 64-B line held in registers (each step is kept or
 // dropped: no per-lane loop bound).
 __device__ __forceinline__ uint64_t prefix_crc(const CrcTab& tb, const uint4 (&w)[4], uint32_t b,
-                                               const char* lds) {
-  RState r{0u, 0u};
+                                               const char* lds, RState r = RState{0u, 0u}) {
 #pragma unroll
   for (int t = 0; t < 64; ++t) {
     const uint4 q = w[t >> 4];
@@ -1006,17 +1005,17 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) tw[i] = reinterpret_cast<const uint4*>(a.payload + tl)[i];
       }
+      // crc(J ‖ piece) = crc(J) · x^(8 PS) ⊕ crc(piece), and J ‖ piece = (what the ring hashed)
+      // ‖ T: continue the ring's state over T (one power-table pass for x^(8 PS) when PS is a
+      // power of two, instead of one per set bit of PS - b)
       const uint64_t cj = prefix_crc(tb, jw, b, lds);
-      uint64_t ct;
       if (tail_lines) {
-        ct = prefix_crc(tb, tw, b, lds);
+        c = prefix_crc(tb, tw, b, lds, s);
       } else {
-        RState r{0u, 0u};
-        for (uint32_t t = 0; t < b; ++t) tb.step1(r, a.payload[tl + t], lds);
-        ct = crc_value(r);
+        for (uint32_t t = 0; t < b; ++t) tb.step1(s, a.payload[tl + t], lds);
+        c = crc_value(s);
       }
-      c ^= crc_shift(cj, PS - b, a.shift);   // crc(piece minus its last b bytes)
-      c = crc_shift(c, b, a.shift) ^ ct;     // ... then those b bytes
+      c ^= crc_shift(cj, PS, a.shift);
     }
     // pieces -> entry: at level l, the group of 2^l lanes holding the earlier bytes is shifted
     // past the 2^l * PS bytes of its partner group (x^(8 * 2^l * PS), global power tables)
