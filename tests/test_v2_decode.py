@@ -375,3 +375,26 @@ def test_gpu_uniform_data_len(engine, n, L, bump):
     g = engine.v2_decode_verify(buf, off)
     check_gpu_vs_oracle(g, o)
     assert np.array_equal(g["corrupt"].astype(bool), ~right)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pad", [64, 13])
+def test_gpu_uniform_data_len_device_variant(engine, pad):
+    """The _dev entry point on a uniform batch: records 64-B aligned take the fixed-size data
+    path, records at pad 13 the segment walk (the host's alignment check); same results."""
+    import torch
+    n, L = 4096, 16384
+    buf, off = uniform_batch(7, n, L)
+    o = O.v2_decode_batch(buf, off)
+    dev = torch.device("cuda", 0)
+    store = torch.zeros(len(buf) + pad + 64, dtype=torch.uint8, device=dev)
+    store[pad:pad + len(buf)] = torch.from_numpy(buf).to(dev)
+    d_rec = store[pad:pad + len(buf)]
+    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    tdt = {np.uint8: torch.uint8, np.int64: torch.int64, np.uint64: torch.int64, np.uint32: torch.int32}
+    out = {k: torch.empty(n, dtype=tdt[t], device=dev) for k, t in engine.V2_FIELDS}
+    torch.cuda.synchronize()
+    engine.v2_decode_verify_dev(d_rec, d_off, out)
+    engine.synchronize()
+    g = {k: out[k].cpu().numpy().view(t) for k, t in engine.V2_FIELDS}
+    check_gpu_vs_oracle(g, o)
