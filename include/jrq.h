@@ -137,6 +137,19 @@ int jrq_synchronize(jrq_engine *e);
 int jrq_host_register(void *ptr, size_t bytes);
 int jrq_host_unregister(void *ptr);
 
+/* Test and A/B hooks: per-engine overrides of kernel and staging choices.  A host never needs
+ * them, and the library reads nothing from the environment (a JVM that loads libjrq gets the
+ * defaults).  No reference counterpart. */
+typedef enum {
+    JRQ_DBG_CRC_SEG_BYTES = 1,   /* fixed segment size of the CRC segment walk, 0 = automatic */
+    JRQ_DBG_CRC_REGS = 2,        /* boundary path: -1 per call site (default), 0 global, 1 registers */
+    JRQ_DBG_CRC_PRIO = 3,        /* progress-stepped wave priority steps, 0..3 (default 1) */
+    JRQ_DBG_CRC_SEG_MAP = 4,     /* 1 contiguous chunks per workgroup (default), 0 interleaved */
+    JRQ_DBG_UPLOAD_PAGEABLE = 5  /* 1: host variants hand unregistered caller memory to HIP's
+                                    pageable copy instead of the pinned bounce chunks */
+} jrq_debug_option;
+int jrq_debug_set(jrq_engine *e, int option, int64_t value);
+
 /* ---------------------------------------------------------------- quorum -- */
 
 /* One quorum epoch for G groups: committed_out[g] = the lastCommittedIndex that
@@ -229,6 +242,13 @@ int jrq_table_update(jrq_table *t, const jrq_group_state *states, uint32_t n_sta
                      const uint64_t *recs, uint32_t n_recs);
 int jrq_table_update_dev(jrq_table *t, const jrq_group_state *states_dev, uint32_t n_states,
                          const uint64_t *recs_dev, uint32_t n_recs);
+/* Host variant gathering `parts` pieces (e.g. one per packing thread, each its own registered
+ * buffer): the same as one jrq_table_update with every part's headers back to back, then every
+ * part's records back to back.  A group's header and its records must sit in the same part
+ * (records are relative to the pendingIndex its header sets). */
+int jrq_table_update_gather(jrq_table *t, uint32_t parts, const jrq_group_state *const *states,
+                            const uint32_t *n_states, const uint64_t *const *recs,
+                            const uint32_t *n_recs);
 
 /* One quorum epoch over every group of the table, state updated in place as BallotBox.commitAt
  * leaves it (BallotBox.java:96-139; commit -> lastCommittedIndex, pendingIndex = commit + 1).

@@ -68,13 +68,15 @@ struct jrq_engine {
   uint32_t* fan_ctr = nullptr; // commit fan-out {listed sum, blocks done}, zero between launches
   uint32_t scratch_len = 0;
   int crc_grid = 0;
-  // JRQ_CRC_SEG_BYTES: fixed CRC segment size (0 = automatic, ~payload / lanes); tests use it
-  // to force many straddling entries
+  // Test / A-B overrides, set only through jrq_debug_set (never from the environment):
+  // JRQ_DBG_CRC_SEG_BYTES: fixed CRC segment size (0 = automatic, ~payload / lanes); tests use
+  // it to force many straddling entries
   uint64_t crc_seg_bytes = 0;
-  int crc_regs = -1;         // JRQ_CRC_REGS: force the boundary path (-1: per call site)
+  int crc_regs = -1;         // JRQ_DBG_CRC_REGS: force the boundary path (-1: per call site)
   uint32_t regs_hint = 0;    // set by host variants around their _dev call (unaligned_bounds)
-  uint32_t crc_prio = 1;     // JRQ_CRC_PRIO: progress-stepped wave priority (A/B knob)
-  uint32_t crc_seg_map = 1;  // JRQ_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
+  uint32_t crc_prio = 1;     // JRQ_DBG_CRC_PRIO: progress-stepped wave priority (A/B knob)
+  uint32_t crc_seg_map = 1;  // JRQ_DBG_CRC_SEG_MAP: 1 = per-workgroup contiguous chunks (faster on C5), 0 = interleaved
+  bool upload_pageable = false;  // JRQ_DBG_UPLOAD_PAGEABLE: hand caller pages to HIP's own copy
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
   DevBuf stage[27];  // 0-13 host-variant staging, 14 stream-update chunk CRCs, 15 fixed-size offsets, 16-19 AppendEntries scratch, 21-26 V2 decode scratch
@@ -230,7 +232,7 @@ bool host_pinned(const void* p) {
 }
 
 int upload_any(jrq_engine* e, void* dst, const void* src, size_t bytes) {
-  if (host_pinned(src)) {
+  if (e->upload_pageable || host_pinned(src)) {
     JRQ_HIP(e, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream));
     return JRQ_OK;
   }
@@ -364,11 +366,6 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   e->max_groups = max_groups;
   e->max_peers = max_peers;
   e->crc_grid = e->num_cus;  // persistent: one 1024-thread workgroup per CU (128 KiB LDS)
-  if (const char* v = std::getenv("JRQ_CRC_PRIO")) e->crc_prio = (uint32_t)std::atoi(v);
-  if (const char* v = std::getenv("JRQ_CRC_REGS")) e->crc_regs = std::atoi(v);
-  if (const char* v = std::getenv("JRQ_CRC_SEG_MAP")) e->crc_seg_map = (uint32_t)std::atoi(v);
-  if (const char* v = std::getenv("JRQ_CRC_SEG_BYTES"))  // rounded up to 256 B by the kernel
-    e->crc_seg_bytes = std::strtoull(v, nullptr, 10);
   e->scratch_len = static_cast<uint32_t>(2ull * e->crc_grid * jrq::kCrcRegsBlock + 2);  // >= 2 slots per lane
   int rc = JRQ_OK;
   std::vector<uint64_t> slice, shift, xinv;
@@ -440,6 +437,36 @@ int jrq_synchronize(jrq_engine* e) {
   DeviceGuard guard(e->device);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
+}
+
+int jrq_debug_set(jrq_engine* e, int option, int64_t value) {
+  if (!e) return JRQ_E_INVALID;
+  switch (option) {
+    case JRQ_DBG_CRC_SEG_BYTES:  // rounded up to 256 B by the kernel
+      if (value < 0) break;
+      e->crc_seg_bytes = static_cast<uint64_t>(value);
+      return JRQ_OK;
+    case JRQ_DBG_CRC_REGS:
+      if (value < -1 || value > 1) break;
+      e->crc_regs = static_cast<int>(value);
+      return JRQ_OK;
+    case JRQ_DBG_CRC_PRIO:
+      if (value < 0 || value > 3) break;
+      e->crc_prio = static_cast<uint32_t>(value);
+      return JRQ_OK;
+    case JRQ_DBG_CRC_SEG_MAP:
+      if (value < 0 || value > 1) break;
+      e->crc_seg_map = static_cast<uint32_t>(value);
+      return JRQ_OK;
+    case JRQ_DBG_UPLOAD_PAGEABLE:
+      if (value < 0 || value > 1) break;
+      e->upload_pageable = value != 0;
+      return JRQ_OK;
+    default:
+      return fail(e, JRQ_E_INVALID, "unknown debug option %d", option);
+  }
+  return fail(e, JRQ_E_INVALID, "debug option %d: value %lld out of range", option,
+              static_cast<long long>(value));
 }
 
 int jrq_host_register(void* ptr, size_t bytes) {
@@ -1321,6 +1348,39 @@ int jrq_table_update(jrq_table* t, const jrq_group_state* states, uint32_t n_sta
   }
   return jrq_table_update_dev(t, static_cast<const jrq_group_state*>(ds), n_states,
                               static_cast<const uint64_t*>(dr), n_recs);
+}
+
+int jrq_table_update_gather(jrq_table* t, uint32_t parts, const jrq_group_state* const* states,
+                            const uint32_t* n_states, const uint64_t* const* recs,
+                            const uint32_t* n_recs) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if (parts && (!states || !n_states || !recs || !n_recs)) return fail(e, JRQ_E_INVALID, "null part arrays");
+  uint64_t ns = 0, nr = 0;
+  for (uint32_t i = 0; i < parts; ++i) {
+    if ((n_states[i] && !states[i]) || (n_recs[i] && !recs[i])) return fail(e, JRQ_E_INVALID, "null part %u", i);
+    ns += n_states[i];
+    nr += n_recs[i];
+  }
+  if (ns > UINT32_MAX || nr > UINT32_MAX) return fail(e, JRQ_E_INVALID, "update larger than 2^32 items");
+  DeviceGuard guard(e->device);
+  int rc;
+  void *ds = nullptr, *dr = nullptr;
+  if (ns && (rc = stage_buf(e, t->st_stage, ns * sizeof(jrq_group_state), &ds))) return rc;
+  if (nr && (rc = stage_buf(e, t->rec_stage, nr * 8, &dr))) return rc;
+  uint64_t os = 0, orr = 0;
+  for (uint32_t i = 0; i < parts; ++i) {  // the parts back to back: headers, then records
+    if (n_states[i] && (rc = upload_any(e, static_cast<jrq_group_state*>(ds) + os, states[i],
+                                        static_cast<size_t>(n_states[i]) * sizeof(jrq_group_state))))
+      return rc;
+    if (n_recs[i] && (rc = upload_any(e, static_cast<uint64_t*>(dr) + orr, recs[i],
+                                      static_cast<size_t>(n_recs[i]) * 8)))
+      return rc;
+    os += n_states[i];
+    orr += n_recs[i];
+  }
+  return jrq_table_update_dev(t, static_cast<const jrq_group_state*>(ds), static_cast<uint32_t>(ns),
+                              static_cast<const uint64_t*>(dr), static_cast<uint32_t>(nr));
 }
 
 int jrq_table_epoch_dev(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, uint8_t* status_out) {

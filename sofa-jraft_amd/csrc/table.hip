@@ -221,11 +221,15 @@ __global__ __launch_bounds__(256) void table_states_kernel(JrqTableArgs t, const
   if (i >= n) return;
   const JrqGroupState st = s[i];
   const uint32_t g = st.group;
-  if (g >= t.G || st.num_runs > kTableMaxRuns) {  // counted, reported by jrq_table_check
+  const uint32_t nr = st.num_runs;
+  // pendingIndex resolved (JRQ_PI_FOLLOWS_LC = lastCommitted + 1)
+  const int64_t pi = st.pending_index == kPiFollowsLc ? st.last_committed + 1 : st.pending_index;
+  // counted, reported by jrq_table_check: out-of-range group or run count, and a leader with
+  // pending entries but no conf run (conf word 0 = quorum 0, which would grant every entry)
+  if (g >= t.G || nr > kTableMaxRuns || (nr == 0 && pi != 0 && st.last_appended >= pi)) {
     atomicAdd(t.invalid, 1u);
     return;
   }
-  const uint32_t nr = st.num_runs;
   t.pi[g] = st.pending_index;
   t.la[g] = st.last_appended;
   t.lc[g] = st.last_committed;
@@ -238,7 +242,7 @@ __global__ __launch_bounds__(256) void table_states_kernel(JrqTableArgs t, const
     t.xconf[o] = static_cast<uint32_t>(k) < nr ? (st.run_conf[k] & ~kConfRuns) : 0ull;
   }
   if (st.flags & 1u)  // JRQ_STATE_RESET_MATCH: a new leader's replicators start over
-    for (uint32_t p = 0; p < t.P; ++p) t.match[static_cast<size_t>(p) * t.ld + g] = st.pending_index - 1;
+    for (uint32_t p = 0; p < t.P; ++p) t.match[static_cast<size_t>(p) * t.ld + g] = pi - 1;
 }
 
 // 8-byte update records (include/jrq.h JRQ_REC): value relative to the group's pendingIndex.
@@ -255,9 +259,19 @@ __global__ __launch_bounds__(256) void table_recs_kernel(JrqTableArgs t, const u
     return;
   }
   const int64_t pr = t.pi[g], lc = t.lc[g];
-  const int64_t val = (pr == kPiFollowsLc ? lc + 1 : pr) - 1 + static_cast<int64_t>(v);
-  if (f == 16u) t.la[g] = val;
-  else t.match[static_cast<size_t>(f) * t.ld + g] = val;
+  const int64_t pi = pr == kPiFollowsLc ? lc + 1 : pr;
+  const int64_t val = pi - 1 + static_cast<int64_t>(v);
+  if (f == 16u) {
+    // entries pending on a group without a conf run (conf word 0: no header named one) could
+    // never be decided as the reference decides them: refused and counted like any bad record
+    if (t.conf[g] == 0 && pi != 0 && val >= pi) {
+      atomicAdd(t.invalid, 1u);
+      return;
+    }
+    t.la[g] = val;
+  } else {
+    t.match[static_cast<size_t>(f) * t.ld + g] = val;
+  }
 }
 
 }  // namespace jrq

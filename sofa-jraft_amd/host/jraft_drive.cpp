@@ -4,7 +4,7 @@
 // to end (API calls -> changed records from page-locked buffers -> resident device table ->
 // changed commits -> closures / onCommitted).
 //
-// Per group g and epoch k (arrays from the caller, e.g. jraft_amd.workloads):
+// jraft_drive_epochs -- per group g and epoch k (arrays from the caller, e.g. jraft_amd.workloads):
 //   epoch 0: setLastCommittedIndex(lc0) as a follower, resetPendingIndex(pi0) as the new
 //            leader (NodeImpl.becomeLeader), then appendPendingTask for [pi0, la[0]]
 //   epoch k: appendPendingTask for (la[k-1], la[k]] (NodeImpl.executeApplyingTasks,
@@ -14,11 +14,23 @@
 //   every peer slot p whose match moved: commitAt(prev + 1, match[k][p][g], peer p) -- the
 //   Replicator's contiguous ack (Replicator.java:1387-1392); p = 0 is the leader's own
 //   LeaderStableClosure ack (NodeImpl.java:1147-1163)
-//   then GroupBatch::flush(): one epoch on the GPU
+//   then GroupBatch::flush(): one epoch on the GPU.
+//   The calls of an epoch come from `threads` threads, each owning a contiguous slice of the
+//   groups (the reference's callers are concurrent: NodeImpl disruptor, LogManager thread, one
+//   Bolt callback thread per replicator).
+// jraft_drive_latency -- steady load with the background flusher (GroupBatch::startFlusher):
+//   `threads` producers loop over their groups, one entry per group per pass
+//   (appendPendingTask, then every peer's commitAt of it); onCommitted(c) measures the time
+//   from the quorum-completing ack of entry c to the callback.
 // Peer p of every group is PeerId("127.0.0.1", 8001 + p); conf words name peer slots by bit.
+#include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -40,6 +52,87 @@ jraft::Configuration confOfMask(uint32_t mask) {
   return c;
 }
 
+Confs confsOfWord(uint64_t cw) {
+  Confs c;
+  c.cur = confOfMask(static_cast<uint32_t>(cw & 0xFFFFu));
+  c.hasOld = ((cw >> 40) & 0xFFu) != 0;
+  if (c.hasOld) c.old = confOfMask(static_cast<uint32_t>((cw >> 16) & 0xFFFFu));
+  return c;
+}
+
+int64_t nowNs() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// T persistent workers: run(f) calls f(t) for t in [0, T) (t = 0 on the caller) and waits.
+class Workers {
+ public:
+  explicit Workers(unsigned n) {
+    for (unsigned i = 1; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+  }
+  ~Workers() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void run(const std::function<void(unsigned)>& f) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      job_ = &f;
+      pending_ = static_cast<unsigned>(th_.size());
+      err_ = nullptr;
+      ++gen_;
+    }
+    cv_.notify_all();
+    std::exception_ptr mine;
+    try {
+      f(0);
+    } catch (...) {
+      mine = std::current_exception();
+    }
+    std::unique_lock<std::mutex> l(mu_);
+    done_.wait(l, [this] { return pending_ == 0; });
+    if (mine) std::rethrow_exception(mine);
+    if (err_) std::rethrow_exception(err_);
+  }
+
+ private:
+  void loop(unsigned i) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(unsigned)>* f;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = job_;
+      }
+      std::exception_ptr e;
+      try {
+        (*f)(i);
+      } catch (...) {
+        e = std::current_exception();
+      }
+      std::lock_guard<std::mutex> l(mu_);
+      if (e && !err_) err_ = e;
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(unsigned)>* job_ = nullptr;
+  std::exception_ptr err_;
+  uint64_t gen_ = 0;
+  unsigned pending_ = 0;
+  bool stop_ = false;
+};
+
 }  // namespace
 
 extern "C" {
@@ -48,36 +141,34 @@ const char* jraft_drive_last_error(void) { return g_err.c_str(); }
 
 // stats_out[k * 11 + i]: 0 api_ms, 1 pack_ms, 2 device_ms, 3 deliver_ms, 4 flush_ms,
 // 5 h2d_bytes, 6 d2h_bytes, 7 states, 8 records, 9 changed, 10 api_calls
-int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, const int64_t* pi0,
-                       const int64_t* lc0, const uint64_t* conf_a, const uint64_t* conf_b,
-                       const int64_t* switch_at, const int64_t* la, const int64_t* match,
-                       int64_t* committed_out, double* stats_out) {
+int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t threads,
+                       const int64_t* pi0, const int64_t* lc0, const uint64_t* conf_a,
+                       const uint64_t* conf_b, const int64_t* switch_at, const int64_t* la,
+                       const int64_t* match, int64_t* committed_out, double* stats_out) {
   using clk = std::chrono::steady_clock;
   auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
   try {
+    const unsigned T = std::max(1u, std::min(threads, G));
     jraft::Engine eng(device, G, static_cast<uint8_t>(P));
     auto batch = std::make_shared<jraft::GroupBatch>(&eng, G, P);
     std::vector<jraft::BallotBox> boxes;
     boxes.reserve(G);
+    for (uint32_t g = 0; g < G; ++g) boxes.emplace_back(batch, g);
     std::vector<jraft::PeerId> peers;
     for (uint32_t p = 0; p < P; ++p) peers.emplace_back("127.0.0.1", 8001 + static_cast<int>(p));
+    // every distinct conf word's Configurations, built before the threads start (read-only)
     std::unordered_map<uint64_t, Confs> confs;
-    auto confsOf = [&](uint64_t cw) -> const Confs& {
-      auto it = confs.find(cw);
-      if (it != confs.end()) return it->second;
-      Confs c;
-      c.cur = confOfMask(static_cast<uint32_t>(cw & 0xFFFFu));
-      c.hasOld = ((cw >> 40) & 0xFFu) != 0;
-      if (c.hasOld) c.old = confOfMask(static_cast<uint32_t>((cw >> 16) & 0xFFFFu));
-      return confs.emplace(cw, std::move(c)).first->second;
-    };
+    for (uint32_t g = 0; g < G; ++g) {
+      if (!confs.count(conf_a[g])) confs.emplace(conf_a[g], confsOfWord(conf_a[g]));
+      if (switch_at && switch_at[g] > 0 && !confs.count(conf_b[g])) confs.emplace(conf_b[g], confsOfWord(conf_b[g]));
+    }
     std::vector<int64_t> prev(static_cast<size_t>(P) * G, 0);
     auto append = [&](uint32_t g, int64_t from, int64_t to) -> uint64_t {  // entries [from, to]
       uint64_t calls = 0;
       const int64_t sw = switch_at ? switch_at[g] : 0;
       auto run = [&](uint64_t cw, int64_t a, int64_t b) {
         if (b < a) return;
-        const Confs& c = confsOf(cw);
+        const Confs& c = confs.at(cw);
         if (!boxes[g].appendPendingTasks(c.cur, c.hasOld ? &c.old : nullptr, b - a + 1))
           throw std::runtime_error("appendPendingTasks refused");
         ++calls;
@@ -90,33 +181,39 @@ int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, const int
       }
       return calls;
     };
+    Workers workers(T);
+    std::vector<uint64_t> calls(T);
     for (uint32_t k = 0; k < K; ++k) {
       const auto t0 = clk::now();
-      uint64_t calls = 0;
       const int64_t* lak = la + static_cast<size_t>(k) * G;
       const int64_t* mk = match + static_cast<size_t>(k) * P * G;
-      for (uint32_t g = 0; g < G; ++g) {
-        if (k == 0) {
-          boxes.emplace_back(batch, g);
-          boxes[g].init({[](int64_t) {}});
-          boxes[g].setLastCommittedIndex(lc0[g]);
-          if (!boxes[g].resetPendingIndex(pi0[g])) throw std::runtime_error("resetPendingIndex refused");
-          calls += 3 + append(g, pi0[g], lak[g]);
-        } else {
-          const int64_t lp = la[static_cast<size_t>(k - 1) * G + g];
-          if (lak[g] > lp) calls += append(g, lp + 1, lak[g]);
-        }
-        for (uint32_t p = 0; p < P; ++p) {
-          const int64_t m = mk[static_cast<size_t>(p) * G + g];
-          int64_t& pv = prev[static_cast<size_t>(p) * G + g];
-          if (k == 0) pv = m < pi0[g] ? m : pi0[g] - 1;
-          if (m > pv) {
-            boxes[g].commitAt(pv + 1, m, peers[p]);
-            pv = m;
-            ++calls;
+      workers.run([&](unsigned t) {
+        uint64_t n = 0;
+        const uint32_t g0 = static_cast<uint32_t>(static_cast<uint64_t>(G) * t / T);
+        const uint32_t g1 = static_cast<uint32_t>(static_cast<uint64_t>(G) * (t + 1) / T);
+        for (uint32_t g = g0; g < g1; ++g) {
+          if (k == 0) {
+            boxes[g].init({[](int64_t) {}});
+            boxes[g].setLastCommittedIndex(lc0[g]);
+            if (!boxes[g].resetPendingIndex(pi0[g])) throw std::runtime_error("resetPendingIndex refused");
+            n += 3 + append(g, pi0[g], lak[g]);
+          } else {
+            const int64_t lp = la[static_cast<size_t>(k - 1) * G + g];
+            if (lak[g] > lp) n += append(g, lp + 1, lak[g]);
+          }
+          for (uint32_t p = 0; p < P; ++p) {
+            const int64_t m = mk[static_cast<size_t>(p) * G + g];
+            int64_t& pv = prev[static_cast<size_t>(p) * G + g];
+            if (k == 0) pv = m < pi0[g] ? m : pi0[g] - 1;
+            if (m > pv) {
+              boxes[g].commitAt(pv + 1, m, peers[p]);
+              pv = m;
+              ++n;
+            }
           }
         }
-      }
+        calls[t] = n;
+      });
       const auto t1 = clk::now();
       batch->flush();
       const auto t2 = clk::now();
@@ -134,8 +231,111 @@ int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, const int
       o[7] = s.states;
       o[8] = s.records;
       o[9] = s.changed;
-      o[10] = static_cast<double>(calls);
+      uint64_t nc = 0;
+      for (uint64_t c : calls) nc += c;
+      o[10] = static_cast<double>(nc);
     }
+    return 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+// out[0] commits (onCommitted calls), 1 entries appended, 2 commitAt calls, 3 seconds,
+// 4 flushes, 5 p50 latency us, 6 p90, 7 p99, 8 p99.9, 9 max, 10 latency samples
+int jraft_drive_latency(int device, uint32_t G, uint32_t P, uint32_t threads, double seconds,
+                        uint32_t max_delay_us, uint32_t max_dirty, double* out) {
+  try {
+    const unsigned T = std::max(1u, std::min(threads, G));
+    jraft::Engine eng(device, G, static_cast<uint8_t>(P));
+    auto batch = std::make_shared<jraft::GroupBatch>(&eng, G, P);
+    std::vector<jraft::BallotBox> boxes;
+    boxes.reserve(G);
+    std::vector<jraft::PeerId> peers;
+    for (uint32_t p = 0; p < P; ++p) peers.emplace_back("127.0.0.1", 8001 + static_cast<int>(p));
+    const jraft::Configuration conf = confOfMask((1u << P) - 1u);
+    // per group: the entry whose quorum-completing ack was recorded last, and when
+    std::unique_ptr<std::atomic<int64_t>[]> ackIdx(new std::atomic<int64_t>[G]);
+    std::unique_ptr<std::atomic<int64_t>[]> ackNs(new std::atomic<int64_t>[G]);
+    std::mutex latMu;
+    std::vector<std::vector<float>*> latLists;
+    std::atomic<uint64_t> commits{0};
+    static std::atomic<uint64_t> runs{0};
+    const uint64_t run = ++runs;
+    auto latList = [&]() -> std::vector<float>& {  // one list per callback thread and run
+      thread_local std::vector<float>* mine = nullptr;
+      thread_local uint64_t owner = 0;
+      if (owner != run) {
+        mine = new std::vector<float>();
+        owner = run;
+        std::lock_guard<std::mutex> l(latMu);
+        latLists.push_back(mine);
+      }
+      return *mine;
+    };
+    for (uint32_t g = 0; g < G; ++g) {
+      ackIdx[g].store(-1);
+      ackNs[g].store(0);
+      boxes.emplace_back(batch, g);
+      boxes[g].init({[&, g](int64_t c) {
+        commits.fetch_add(1, std::memory_order_relaxed);
+        if (ackIdx[g].load(std::memory_order_acquire) == c)
+          latList().push_back(static_cast<float>((nowNs() - ackNs[g].load(std::memory_order_relaxed)) * 1e-3));
+      }});
+      if (!boxes[g].resetPendingIndex(1)) throw std::runtime_error("resetPendingIndex refused");
+    }
+    batch->flush();  // the first flush ships every group's header
+    std::atomic<bool> stop{false};
+    std::vector<uint64_t> entries(T, 0);
+    batch->startFlusher(jraft::FlushPolicy{max_delay_us, max_dirty});
+    const int64_t t0 = nowNs();
+    {
+      Workers workers(T);
+      std::thread timer([&] {
+        std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+        stop.store(true);
+      });
+      workers.run([&](unsigned t) {
+        const uint32_t g0 = static_cast<uint32_t>(static_cast<uint64_t>(G) * t / T);
+        const uint32_t g1 = static_cast<uint32_t>(static_cast<uint64_t>(G) * (t + 1) / T);
+        uint64_t n = 0;
+        for (int64_t idx = 1; !stop.load(std::memory_order_relaxed); ++idx) {
+          for (uint32_t g = g0; g < g1; ++g) {
+            if (!boxes[g].appendPendingTasks(conf, nullptr, 1)) throw std::runtime_error("append refused");
+            for (uint32_t p = 0; p < P; ++p) boxes[g].commitAt(idx, idx, peers[p]);
+            ackNs[g].store(nowNs(), std::memory_order_relaxed);
+            ackIdx[g].store(idx, std::memory_order_release);
+            ++n;
+          }
+        }
+        entries[t] = n;
+      });
+      timer.join();
+    }
+    batch->stopFlusher();
+    batch->flush();
+    const double secs = (nowNs() - t0) * 1e-9;
+    std::vector<float> all;
+    for (auto* l : latLists) {
+      all.insert(all.end(), l->begin(), l->end());
+      delete l;
+    }
+    std::sort(all.begin(), all.end());
+    auto q = [&](double f) { return all.empty() ? 0.0 : static_cast<double>(all[std::min(all.size() - 1, static_cast<size_t>(f * all.size()))]); };
+    uint64_t ne = 0;
+    for (uint64_t e : entries) ne += e;
+    out[0] = static_cast<double>(commits.load());
+    out[1] = static_cast<double>(ne);
+    out[2] = static_cast<double>(ne) * P;
+    out[3] = secs;
+    out[4] = static_cast<double>(batch->flushCount());
+    out[5] = q(0.5);
+    out[6] = q(0.9);
+    out[7] = q(0.99);
+    out[8] = q(0.999);
+    out[9] = all.empty() ? 0.0 : all.back();
+    out[10] = static_cast<double>(all.size());
     return 0;
   } catch (const std::exception& ex) {
     g_err = ex.what();

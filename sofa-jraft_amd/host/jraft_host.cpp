@@ -188,7 +188,119 @@ uint64_t CRC64::getValue() {
   return crc_;
 }
 
+// ------------------------------------------------------------ peer interning
+
+namespace {
+
+// Process-wide PeerId -> id table (ids from 1; PeerId::internId 0 = not looked up).  Entries
+// sit in fixed chunks that never move, so a caller holding an id reads its entry without a
+// lock: the id was published (release) after the entry was written.  Java compares PeerIds
+// by value (PeerId.equals -> Endpoint.equals -> String.equals, PeerId.java:180-199); the
+// cached id is checked against the entry, so a PeerId changed after caching is re-interned.
+class PeerRegistry {
+ public:
+  static PeerRegistry& get() {
+    static PeerRegistry r;
+    return r;
+  }
+  uint32_t id(const PeerId& p) {
+    const uint32_t c = p.internId.load(std::memory_order_acquire);
+    if (c != 0 && matches(c, p)) return c;
+    uint32_t i;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      auto it = map_.find(p);
+      if (it != map_.end()) {
+        i = it->second;
+      } else {
+        i = next_;
+        if (i >= kChunks * kChunkSize) throw std::length_error("more than 2^24 distinct PeerIds");
+        std::atomic<Entry*>& ch = chunks_[i / kChunkSize];
+        if (!ch.load(std::memory_order_relaxed)) ch.store(new Entry[kChunkSize], std::memory_order_release);
+        Entry& e = ch.load(std::memory_order_relaxed)[i % kChunkSize];
+        e.ip = p.ip;
+        e.port = p.port;
+        e.idx = p.idx;
+        map_.emplace(p, i);
+        ++next_;
+      }
+    }
+    p.internId.store(i, std::memory_order_release);
+    return i;
+  }
+
+ private:
+  static constexpr uint32_t kChunkSize = 4096, kChunks = 4096;
+  struct Entry {
+    std::string ip;
+    int32_t port = 0, idx = 0;
+  };
+  struct Hash {
+    size_t operator()(const PeerId& p) const {
+      return std::hash<std::string>()(p.ip) ^ (static_cast<size_t>(p.port) << 20) ^
+             (static_cast<size_t>(p.idx) << 40);
+    }
+  };
+  bool matches(uint32_t i, const PeerId& p) const {
+    const Entry& e = chunks_[i / kChunkSize].load(std::memory_order_acquire)[i % kChunkSize];
+    return e.port == p.port && e.idx == p.idx && e.ip == p.ip;
+  }
+  PeerRegistry() {
+    for (auto& c : chunks_) c.store(nullptr, std::memory_order_relaxed);
+  }
+  ~PeerRegistry() {
+    for (auto& c : chunks_) delete[] c.load(std::memory_order_relaxed);
+  }
+  std::mutex mu_;
+  std::unordered_map<PeerId, uint32_t, Hash> map_;
+  uint32_t next_ = 1;
+  std::atomic<Entry*> chunks_[kChunks];
+};
+
+inline uint32_t peerId(const PeerId& p) { return PeerRegistry::get().id(p); }
+
+std::atomic<uint64_t> g_batchSerial{1};
+// the batch whose commits this thread is delivering (flush / clearPendingTasks must not re-enter)
+thread_local const GroupBatch* tl_delivering = nullptr;
+
+int64_t nowNs() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// a one-byte spin lock (calls hold it for a few hundred ns at most)
+inline void spinLock(std::atomic<uint8_t>& l) {
+  for (unsigned n = 0; l.exchange(1, std::memory_order_acquire) != 0; ++n) {
+    if (n < 64) {
+      __builtin_ia32_pause();
+    } else {
+      std::this_thread::yield();
+    }
+  }
+}
+
+}  // namespace
+
 // --------------------------------------------------------------- ballot box
+
+struct GroupBatch::DirtyList {  // the groups one calling thread changed since the last swap
+  std::atomic<uint8_t> mu{0};
+  std::vector<uint32_t> v;
+  std::atomic<size_t> n{0};          // v.size(), for the flusher's policy
+  std::atomic<int64_t> firstNs{0};   // when v got its first group
+};
+
+struct GroupBatch::Part {  // one pack worker's headers and records (page-locked)
+  PinnedBuf<jrq_group_state> st;
+  PinnedBuf<uint64_t> rec;
+  uint32_t ns = 0, nr = 0;
+};
+
+struct GroupBatch::Flusher {
+  std::thread th;
+  std::atomic<bool> stop{false};
+  std::string error;
+};
 
 // Persistent workers for flush()'s pack and deliver passes (spawning threads per flush cost
 // ~2 ms on the GPU box): run(f) calls f(part, parts) on every worker and on the caller, and
@@ -258,11 +370,11 @@ struct GroupBatch::Pool {
   bool stop = false;
 };
 
-// f(begin, end) over [0, n) on the pool, only when each part gets at least `grain` items.
+// f(part, begin, end) over [0, n) on the pool, only when each part gets at least `grain` items.
 template <class F>
 void GroupBatch::parallelFor(size_t n, size_t grain, F&& f) {
   if (n < 2 * grain) {
-    f(size_t(0), n);
+    f(0u, size_t(0), n);
     return;
   }
   if (!pool_) {
@@ -271,7 +383,7 @@ void GroupBatch::parallelFor(size_t n, size_t grain, F&& f) {
   }
   const size_t parts = std::min<size_t>(pool_->size(), n / grain);
   pool_->run([&](unsigned i, unsigned) {
-    if (i < parts) f(n * i / parts, n * (i + 1) / parts);
+    if (i < parts) f(i, n * i / parts, n * (i + 1) / parts);
   });
 }
 
@@ -299,10 +411,12 @@ void GroupBatch::PinnedBuf<T>::release() {
 }
 
 GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
-    : eng_(eng), G_(groups), P_(peers) {
+    : eng_(eng), G_(groups), P_(peers), serial_(g_batchSerial.fetch_add(1)) {
   if (peers == 0 || peers > JRQ_MAX_PEERS) throw std::invalid_argument("peers must be 1..16");
   if (groups == 0 || groups > JRQ_TABLE_MAX_GROUPS) throw std::invalid_argument("groups must be 1..2^27");
   const size_t GP = static_cast<size_t>(G_) * P_;
+  lock_.reset(new std::atomic<uint8_t>[G_]);
+  for (uint32_t g = 0; g < G_; ++g) lock_[g].store(0, std::memory_order_relaxed);
   pi_.assign(G_, 0);
   lc_.assign(G_, 0);
   la_.assign(G_, -1);
@@ -318,15 +432,47 @@ GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
 }
 
 GroupBatch::~GroupBatch() {
+  try {
+    stopFlusher();
+  } catch (...) {
+  }
   if (table_) jrq_table_destroy(table_);
 }
 
-uint32_t GroupBatch::internPeer(const PeerId& p) {
-  auto it = peerIds_.find(p);
-  if (it != peerIds_.end()) return it->second;
-  const uint32_t id = static_cast<uint32_t>(peerIds_.size());
-  peerIds_.emplace(p, id);
-  return id;
+void GroupBatch::lock(uint32_t g) const { spinLock(lock_[g]); }
+
+GroupBatch::DirtyList* GroupBatch::myDirtyList() {
+  struct Slot {
+    const GroupBatch* b;
+    uint64_t serial;
+    DirtyList* l;
+  };
+  static thread_local Slot cache[4] = {};
+  static thread_local unsigned next = 0;
+  for (const Slot& s : cache)
+    if (s.b == this && s.serial == serial_) return s.l;
+  DirtyList* l;
+  {
+    std::lock_guard<std::mutex> g(listsMu_);
+    lists_.emplace_back(new DirtyList());
+    l = lists_.back().get();
+  }
+  cache[next++ & 3u] = Slot{this, serial_, l};
+  return l;
+}
+
+// Under the group's lock: the first change since the group was last packed puts it on this
+// thread's dirty list; the bits say what to pack.
+void GroupBatch::markDirty(uint32_t g, uint32_t bits) {
+  if (dirty_[g] == 0) {
+    DirtyList* l = myDirtyList();
+    spinLock(l->mu);
+    if (l->v.empty()) l->firstNs.store(nowNs(), std::memory_order_relaxed);
+    l->v.push_back(g);
+    l->n.store(l->v.size(), std::memory_order_relaxed);
+    l->mu.store(0, std::memory_order_release);
+  }
+  dirty_[g] |= bits;
 }
 
 // Slots named by the masks of the group's live conf runs: their peers vote on pending entries.
@@ -341,7 +487,7 @@ uint32_t GroupBatch::liveMask(uint32_t g) const {
 
 // The slot of `peer` in group g.  create: a free slot, else the least recently acked slot that
 // no live conf run names (and that is not in `reserved`), its match reset (its peer's acks no
-// longer matter to any pending ballot).  Throws std::length_error when every slot is live.
+// longer matter to any pending ballot).  -1 when there is none (every slot is live).
 int GroupBatch::slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved) {
   const size_t base = static_cast<size_t>(g) * P_;
   int victim = -1;
@@ -355,12 +501,10 @@ int GroupBatch::slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved
     for (uint32_t s = 0; s < P_; ++s)
       if (!((busy >> s) & 1u) && (victim < 0 || slotUse_[base + s] < slotUse_[base + victim]))
         victim = static_cast<int>(s);
-    if (victim < 0)
-      throw std::length_error("more distinct live peers in group " + std::to_string(g) +
-                              " than the " + std::to_string(P_) + " peer slots");
+    if (victim < 0) return -1;
   }
   slotPeer_[base + victim] = peer;
-  slotUse_[base + victim] = flushes_;
+  slotUse_[base + victim] = static_cast<uint32_t>(flushes_.load(std::memory_order_relaxed));
   if (match_[base + victim] != 0) {
     match_[base + victim] = 0;
     markDirty(g, 1u << victim);
@@ -368,16 +512,17 @@ int GroupBatch::slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved
   return victim;
 }
 
-uint64_t GroupBatch::confWord(uint32_t g, const Configuration& conf, const Configuration* old) {
+uint64_t GroupBatch::confWord(uint32_t g, const uint32_t* ids, uint32_t nn, uint32_t no, bool hasOld) {
   // Ballot.init (Ballot.java:63-85): peers only, quorum = size/2+1, oldQuorum 0 if null
   uint32_t nm = 0, om = 0;
-  for (auto& p : conf.peers) nm |= 1u << slotOf(g, internPeer(p), true, nm | om);
-  uint32_t nq = static_cast<uint32_t>(conf.peers.size()) / 2 + 1, oq = 0;
-  if (old) {
-    for (auto& p : old->peers) om |= 1u << slotOf(g, internPeer(p), true, nm | om);
-    oq = static_cast<uint32_t>(old->peers.size()) / 2 + 1;
+  for (uint32_t i = 0; i < nn + no; ++i) {
+    const int s = slotOf(g, ids[i], true, nm | om);
+    if (s < 0)
+      throw std::length_error("more distinct live peers in group " + std::to_string(g) +
+                              " than the " + std::to_string(P_) + " peer slots");
+    (i < nn ? nm : om) |= 1u << s;
   }
-  return JRQ_CONF(nm, om, nq, oq);
+  return JRQ_CONF(nm, om, nn / 2 + 1, hasOld ? no / 2 + 1 : 0);
 }
 
 // Would a gap [lo, hi] in `slot`'s acks skip a pending entry whose ballot counts that slot?
@@ -405,32 +550,64 @@ void GroupBatch::dropDeadRuns(uint32_t g) {
   }
 }
 
-// BallotBox.commitAt's commit, after the epoch (:130-137): drop the ballots up to c, run their
-// closures (ClosureQueue.popClosureUntil -> done.run(OK)), then waiter.onCommitted(c).
-void GroupBatch::commitTo(uint32_t g, int64_t c) {
-  if (auto& q = closures_[g]) {
-    while (!q->empty() && q->front().first <= c) {
-      auto done = std::move(q->front().second);
-      q->pop_front();
-      done(true);
+// Append groups[0..n) to `part` (reserved for them): per group, under its lock, the dirty bits
+// are taken and the header or records written from the group's current state.
+void GroupBatch::packRange(Part& part, const uint32_t* groups, size_t n) {
+  uint32_t si = part.ns, ri = part.nr;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t g = groups[i];
+    Guard lk(*this, g);
+    const uint32_t d = dirty_[g];
+    dirty_[g] = 0;
+    const int64_t pi = pi_[g], base = pi - 1;
+    if (d & kDirtyHeader) {
+      jrq_group_state& st = part.st.p[si++];
+      std::memset(&st, 0, sizeof st);
+      st.group = g;
+      st.num_runs = nruns_[g];
+      st.flags = (d & kDirtyReset) ? JRQ_STATE_RESET_MATCH : 0;
+      // the table's steady-state encoding of pendingIndex = lastCommittedIndex + 1: the
+      // group's next commit then writes lastCommitted only
+      st.pending_index = (pi != 0 && pi == lc_[g] + 1) ? JRQ_PI_FOLLOWS_LC : pi;
+      st.last_appended = la_[g];
+      st.last_committed = lc_[g];
+      const Run* R = &runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS];
+      for (uint32_t r = 0; r < nruns_[g]; ++r) {
+        st.run_conf[r] = R[r].conf;
+        st.run_start[r] = R[r].start;
+      }
+    } else if ((d & kDirtyLa) && pi != 0) {
+      part.rec.p[ri++] = JRQ_REC(g, JRQ_REC_LAST_APPENDED, la_[g] - base);
+    }
+    if (pi == 0) continue;  // not the leader: its acks are refused (commitAt returns false)
+    for (uint32_t m = d & 0xFFFFu; m; m &= m - 1) {
+      const uint32_t s = static_cast<uint32_t>(__builtin_ctz(m));
+      const int64_t v = match_[static_cast<size_t>(g) * P_ + s] - base;
+      part.rec.p[ri++] = JRQ_REC(g, s, v > 0 ? v : 0);
     }
   }
-  pi_[g] = c + 1;
-  lc_[g] = c;
-  dropDeadRuns(g);
-  if (waiter_[g]) waiter_[g](c);
+  part.ns = si;
+  part.nr = ri;
 }
 
 uint32_t GroupBatch::flush() {
+  if (tl_delivering == this)
+    throw std::logic_error("GroupBatch::flush from inside a commit callback of the same batch");
+  std::lock_guard<std::mutex> fl(flushMu_);
+  return flushLocked();
+}
+
+uint32_t GroupBatch::flushLocked() {
   if (!eng_) throw std::logic_error("GroupBatch::flush needs an Engine");
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
-  stats_ = FlushStats{};
+  FlushStats stats;
   if (!table_) {  // first flush: the device table starts empty, ship every group's state
     int err = 0;
     table_ = jrq_table_create(eng_->raw(), G_, P_, &err);
     if (!table_) throwIfError(err ? err : JRQ_E_NOMEM, eng_->raw(), "jrq_table_create");
     for (uint32_t g = 0; g < G_; ++g) {
+      Guard lk(*this, g);
       uint32_t bits = 0;
       if (pi_[g] != 0 || lc_[g] != 0 || nruns_[g] != 0) bits |= kDirtyHeader;
       for (uint32_t s = 0; s < P_; ++s)
@@ -438,82 +615,79 @@ uint32_t GroupBatch::flush() {
       if (bits) markDirty(g, bits);
     }
   }
-  // pack the changes: one header per group whose header changed, else 8-B records -- two
-  // passes over the dirty groups (count, then fill at per-chunk offsets), split across threads
-  const size_t nd = dirtyList_.size();
-  const size_t kChunk = 1u << 12;
-  const size_t nchunks = (nd + kChunk - 1) / kChunk;
-  std::vector<uint32_t> cs(nchunks + 1, 0), cr(nchunks + 1, 0);
-  parallelFor(nchunks, 1, [&](size_t c0, size_t c1) {
-    for (size_t c = c0; c < c1; ++c) {
-      uint32_t ns = 0, nr = 0;
-      for (size_t i = c * kChunk, e = std::min(nd, (c + 1) * kChunk); i < e; ++i) {
-        const uint32_t g = dirtyList_[i], d = dirty_[g];
-        if (d & kDirtyHeader) ++ns;
-        else if ((d & kDirtyLa) && pi_[g] != 0) ++nr;
-        if (pi_[g] != 0) nr += static_cast<uint32_t>(__builtin_popcount(d & 0xFFFFu));
-      }
-      cs[c + 1] = ns;
-      cr[c + 1] = nr;
+  // swap out every thread's dirty list: callers go on marking groups for the next epoch
+  size_t nl;
+  {
+    std::lock_guard<std::mutex> g(listsMu_);
+    nl = lists_.size();
+    if (work_.size() < nl) work_.resize(nl);
+    for (size_t i = 0; i < nl; ++i) {
+      DirtyList& l = *lists_[i];
+      work_[i].clear();
+      spinLock(l.mu);
+      std::swap(l.v, work_[i]);
+      l.n.store(0, std::memory_order_relaxed);
+      l.mu.store(0, std::memory_order_release);
     }
-  });
-  for (size_t c = 0; c < nchunks; ++c) {
-    cs[c + 1] += cs[c];
-    cr[c + 1] += cr[c];
   }
-  const uint32_t ns = cs[nchunks], nr = cr[nchunks];
-  states_.reserve(ns + 1);
-  recs_.reserve(nr + 1);
-  parallelFor(nchunks, 1, [&](size_t c0, size_t c1) {
-    for (size_t c = c0; c < c1; ++c) {
-      uint32_t si = cs[c], ri = cr[c];
-      for (size_t i = c * kChunk, e = std::min(nd, (c + 1) * kChunk); i < e; ++i) {
-        const uint32_t g = dirtyList_[i], d = dirty_[g];
-        dirty_[g] = 0;
-        const int64_t pi = pi_[g], base = pi - 1;
-        if (d & kDirtyHeader) {
-          jrq_group_state& st = states_.p[si++];
-          std::memset(&st, 0, sizeof st);
-          st.group = g;
-          st.num_runs = nruns_[g];
-          st.flags = (d & kDirtyReset) ? JRQ_STATE_RESET_MATCH : 0;
-          // the table's steady-state encoding of pendingIndex = lastCommittedIndex + 1: the
-          // group's next commit then writes lastCommitted only
-          st.pending_index = (pi != 0 && pi == lc_[g] + 1) ? JRQ_PI_FOLLOWS_LC : pi;
-          st.last_appended = la_[g];
-          st.last_committed = lc_[g];
-          const Run* R = &runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS];
-          for (uint32_t r = 0; r < nruns_[g]; ++r) {
-            st.run_conf[r] = R[r].conf;
-            st.run_start[r] = R[r].start;
-          }
-        } else if ((d & kDirtyLa) && pi != 0) {
-          recs_.p[ri++] = JRQ_REC(g, JRQ_REC_LAST_APPENDED, la_[g] - base);
-        }
-        if (pi == 0) continue;  // not the leader: its acks are refused (commitAt returns false)
-        for (uint32_t m = d & 0xFFFFu; m; m &= m - 1) {
-          const uint32_t s = static_cast<uint32_t>(__builtin_ctz(m));
-          const int64_t v = match_[static_cast<size_t>(g) * P_ + s] - base;
-          recs_.p[ri++] = JRQ_REC(g, s, v > 0 ? v : 0);
-        }
-      }
+  std::vector<size_t> pre(nl + 1, 0);
+  for (size_t i = 0; i < nl; ++i) pre[i + 1] = pre[i] + work_[i].size();
+  const size_t nd = pre[nl];
+  // pack: the dirty groups split into contiguous ranges of the concatenated lists
+  const size_t kGrain = 1u << 12;
+  const size_t nparts = std::max<size_t>(1, std::min<size_t>(16, nd / kGrain));
+  if (parts_.size() < nparts) parts_.resize(nparts);
+  for (auto& p : parts_) p.ns = p.nr = 0;
+  parallelFor(nd, kGrain, [&](unsigned part, size_t b, size_t e) {
+    Part& P = parts_[part];
+    P.st.reserve(e - b + 1);
+    P.rec.reserve((e - b) * (P_ + 1) + 1);
+    // the pieces of the lists inside [b, e)
+    size_t li = static_cast<size_t>(std::upper_bound(pre.begin(), pre.end(), b) - pre.begin()) - 1;
+    for (size_t pos = b; pos < e; ++li) {
+      const size_t lo = pos - pre[li], hi = std::min(e, pre[li + 1]) - pre[li];
+      if (hi <= lo) continue;
+      packRange(P, work_[li].data() + lo, hi - lo);
+      pos = pre[li] + hi;
     }
   });
-  dirtyList_.clear();
+  std::vector<const jrq_group_state*> sp(nparts);
+  std::vector<const uint64_t*> rp(nparts);
+  std::vector<uint32_t> sn(nparts), rn(nparts);
+  for (size_t i = 0; i < nparts; ++i) {
+    sp[i] = parts_[i].st.p;
+    rp[i] = parts_[i].rec.p;
+    sn[i] = parts_[i].ns;
+    rn[i] = parts_[i].nr;
+    stats.states += sn[i];
+    stats.records += rn[i];
+  }
   changed_.reserve(G_);
   const auto t1 = clk::now();
-  throwIfError(jrq_table_update(table_, states_.p, ns, recs_.p, nr), eng_->raw(), "jrq_table_update");
+  throwIfError(jrq_table_update_gather(table_, static_cast<uint32_t>(nparts), sp.data(), sn.data(),
+                                       rp.data(), rn.data()),
+               eng_->raw(), "jrq_table_update_gather");
   uint32_t n = 0;
   throwIfError(jrq_table_epoch(table_, changed_.p, &n, nullptr), eng_->raw(), "jrq_table_epoch");
   const auto t2 = clk::now();
-  // deliver: groups are independent, so their commits (closures, then onCommitted) run split
-  // across threads; one group's callbacks run on one thread, in order.  A commit touches the
-  // group in several host arrays at random places: prefetch a few groups ahead.
-  parallelFor(n, 1u << 12, [&](size_t i0, size_t i1) {
+  // deliver: per changed group, under its lock, the commit BallotBox.commitAt makes
+  // (:130-134: drop ballots up to c, pendingIndex = c + 1, lastCommittedIndex = c); then,
+  // without the lock, its closures (ClosureQueue.popClosureUntil -> done.run(OK)) and
+  // waiter.onCommitted(c) (:137).  Groups are independent: split across threads, one group's
+  // callbacks on one thread, in order.  A commit touches several host arrays at random
+  // places: prefetch a few groups ahead.
+  parallelFor(n, 1u << 12, [&](unsigned, size_t i0, size_t i1) {
+    struct Scope {
+      const GroupBatch* prev;
+      explicit Scope(const GroupBatch* b) : prev(tl_delivering) { tl_delivering = b; }
+      ~Scope() { tl_delivering = prev; }
+    } scope(this);
+    std::vector<std::function<void(bool)>> done;
     constexpr size_t kAhead = 8;
     for (size_t i = i0; i < i1; ++i) {
       if (i + kAhead < i1) {
         const uint32_t h = static_cast<uint32_t>(changed_.p[i + kAhead]);
+        __builtin_prefetch(&lock_[h], 1);
         __builtin_prefetch(&pi_[h], 1);
         __builtin_prefetch(&lc_[h], 1);
         __builtin_prefetch(&nruns_[h], 0);
@@ -522,21 +696,81 @@ uint32_t GroupBatch::flush() {
       }
       const uint64_t w = changed_.p[i];
       const uint32_t g = static_cast<uint32_t>(w);
-      commitTo(g, pi_[g] - 1 + static_cast<int64_t>(w >> 32));
+      int64_t c;
+      CommitWaiter waiter;
+      {
+        Guard lk(*this, g);
+        c = pi_[g] - 1 + static_cast<int64_t>(w >> 32);
+        if (auto& q = closures_[g]) {
+          while (!q->empty() && q->front().first <= c) {
+            done.push_back(std::move(q->front().second));
+            q->pop_front();
+          }
+        }
+        pi_[g] = c + 1;
+        lc_[g] = c;
+        dropDeadRuns(g);
+        if (waiter_[g]) waiter = waiter_[g];
+      }
+      for (auto& f : done) f(true);
+      done.clear();
+      if (waiter) waiter(c);
     }
   });
-  ++flushes_;
+  flushes_.fetch_add(1, std::memory_order_relaxed);
   const auto t3 = clk::now();
   auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
-  stats_.states = ns;
-  stats_.records = nr;
-  stats_.changed = n;
-  stats_.h2d_bytes = static_cast<uint64_t>(ns) * sizeof(jrq_group_state) + static_cast<uint64_t>(nr) * 8;
-  stats_.d2h_bytes = 4 * JRQ_TABLE_SEGMENTS + static_cast<uint64_t>(n) * 8;
-  stats_.pack_ms = ms(t1 - t0);
-  stats_.device_ms = ms(t2 - t1);
-  stats_.deliver_ms = ms(t3 - t2);
+  stats.changed = n;
+  stats.h2d_bytes = static_cast<uint64_t>(stats.states) * sizeof(jrq_group_state) +
+                    static_cast<uint64_t>(stats.records) * 8;
+  stats.d2h_bytes = 4 * JRQ_TABLE_SEGMENTS + static_cast<uint64_t>(n) * 8;
+  stats.pack_ms = ms(t1 - t0);
+  stats.device_ms = ms(t2 - t1);
+  stats.deliver_ms = ms(t3 - t2);
+  stats_ = stats;
   return n;
+}
+
+void GroupBatch::startFlusher(const FlushPolicy& policy) {
+  stopFlusher();
+  flusher_.reset(new Flusher());
+  Flusher* f = flusher_.get();
+  f->th = std::thread([this, f, policy] {
+    const int64_t delayNs = static_cast<int64_t>(policy.maxDelayUs) * 1000;
+    const auto nap = std::chrono::microseconds(std::max<uint32_t>(10, std::min<uint32_t>(100, policy.maxDelayUs / 8)));
+    try {
+      while (!f->stop.load(std::memory_order_acquire)) {
+        size_t pending = 0;
+        int64_t oldest = INT64_MAX;
+        {
+          std::lock_guard<std::mutex> g(listsMu_);
+          for (auto& l : lists_) {
+            const size_t k = l->n.load(std::memory_order_relaxed);
+            if (k) {
+              pending += k;
+              oldest = std::min(oldest, l->firstNs.load(std::memory_order_relaxed));
+            }
+          }
+        }
+        if (pending && (pending >= policy.maxDirtyGroups || nowNs() - oldest >= delayNs)) {
+          flush();
+        } else {
+          std::this_thread::sleep_for(nap);
+        }
+      }
+    } catch (const std::exception& ex) {
+      f->error = ex.what();
+    }
+  });
+}
+
+void GroupBatch::stopFlusher() {
+  if (!flusher_) return;
+  flusher_->stop.store(true, std::memory_order_release);
+  if (flusher_->th.joinable()) flusher_->th.join();
+  const std::string err = flusher_->error;
+  flusher_.reset();
+  if (!err.empty()) throw std::runtime_error("GroupBatch flusher: " + err);
 }
 
 BallotBox::BallotBox(std::shared_ptr<GroupBatch> batch, uint32_t group) : batch_(std::move(batch)), g_(group) {
@@ -545,18 +779,25 @@ BallotBox::BallotBox(std::shared_ptr<GroupBatch> batch, uint32_t group) : batch_
 
 bool BallotBox::init(const BallotBoxOptions& opts) {
   if (!opts.waiter || !opts.closureQueue) return false;  // "waiter or closure queue is null."
-  batch_->waiter_[g_] = opts.waiter;
-  batch_->inited_[g_] = 1;
+  GroupBatch& b = *batch_;
+  GroupBatch::Guard lk(b, g_);
+  b.waiter_[g_] = opts.waiter;
+  b.inited_[g_] = 1;
   return true;
 }
 
 bool BallotBox::commitAt(int64_t first, int64_t last, const PeerId& peer) {
   GroupBatch& b = *batch_;
+  const uint32_t id = peerId(peer);
+  GroupBatch::Guard lk(b, g_);
   const int64_t pi = b.pi_[g_];
   if (pi == 0) return false;                                     // :101-103
   if (last < pi) return true;                                    // :104-106
   if (last > b.la_[g_]) throw std::out_of_range("ArrayIndexOutOfBoundsException");  // :107-109
-  const int s = b.slotOf(g_, b.internPeer(peer), true);
+  const int s = b.slotOf(g_, id, true);
+  // every slot is named by a live conf run and this peer by none: no pending ballot counts
+  // it, so Ballot.grant finds nothing (Ballot.java:100-127) and commitAt returns true
+  if (s < 0) return true;
   const size_t k = static_cast<size_t>(g_) * b.P_ + s;
   int64_t& m = b.match_[k];
   const int64_t lo = std::max(m + 1, pi);
@@ -566,27 +807,40 @@ bool BallotBox::commitAt(int64_t first, int64_t last, const PeerId& peer) {
     m = last;
     b.markDirty(g_, 1u << s);
   }
-  b.slotUse_[k] = b.flushes_;
+  b.slotUse_[k] = static_cast<uint32_t>(b.flushes_.load(std::memory_order_relaxed));
   return true;
 }
 
 void BallotBox::clearPendingTasks() {
   GroupBatch& b = *batch_;
+  if (tl_delivering == batch_.get())
+    throw std::logic_error("BallotBox.clearPendingTasks from inside a commit callback of its batch");
+  // waits for a flush in progress (it may hold this group's acks)
+  std::lock_guard<std::mutex> fl(b.flushMu_);
   // Acks recorded since the last epoch would have committed at once in the reference
   // (BallotBox.commitAt decides synchronously): decide them before the queue is dropped.
-  if ((b.dirty_[g_] & 0xFFFFu) && b.pi_[g_] != 0 && b.eng_) b.flush();
-  if (auto& q = b.closures_[g_]) {
-    for (auto& c : *q) c.second(false);  // ClosureQueue.clear runs closures with EPERM
-    q->clear();
+  bool decide;
+  {
+    GroupBatch::Guard lk(b, g_);
+    decide = (b.dirty_[g_] & 0xFFFFu) && b.pi_[g_] != 0 && b.eng_;
   }
-  b.nruns_[g_] = 0;
-  b.pi_[g_] = 0;
-  b.la_[g_] = -1;
-  b.markDirty(g_, GroupBatch::kDirtyHeader);
+  if (decide) b.flushLocked();
+  std::unique_ptr<std::deque<std::pair<int64_t, std::function<void(bool)>>>> q;
+  {
+    GroupBatch::Guard lk(b, g_);
+    q = std::move(b.closures_[g_]);
+    b.nruns_[g_] = 0;
+    b.pi_[g_] = 0;
+    b.la_[g_] = -1;
+    b.markDirty(g_, GroupBatch::kDirtyHeader);
+  }
+  if (q)
+    for (auto& c : *q) c.second(false);  // ClosureQueue.clear runs closures with EPERM
 }
 
 bool BallotBox::resetPendingIndex(int64_t n) {
   GroupBatch& b = *batch_;
+  GroupBatch::Guard lk(b, g_);
   if (!(b.pi_[g_] == 0 && b.la_[g_] < b.pi_[g_])) return false;
   if (n <= b.lc_[g_]) return false;
   b.pi_[g_] = n;
@@ -601,12 +855,36 @@ bool BallotBox::resetPendingIndex(int64_t n) {
 
 bool BallotBox::appendPendingTasks(const Configuration& conf, const Configuration* oldConf,
                                    int64_t count) {
+  return append(conf, oldConf, count, nullptr);
+}
+
+bool BallotBox::appendPendingTask(const Configuration& conf, const Configuration* oldConf,
+                                  std::function<void(bool)> done) {
+  return append(conf, oldConf, 1, done ? &done : nullptr);
+}
+
+// The ballots and (for one entry) the closure under one hold of the group's lock, as the
+// reference appends both under its write lock (BallotBox.java:203-214).
+bool BallotBox::append(const Configuration& conf, const Configuration* oldConf, int64_t count,
+                       std::function<void(bool)>* done) {
   GroupBatch& b = *batch_;
+  // the peers' ids, interned outside the group's lock
+  const size_t nn = conf.peers.size(), no = oldConf ? oldConf->peers.size() : 0;
+  uint32_t small[32];
+  std::vector<uint32_t> big;
+  uint32_t* ids = small;
+  if (nn + no > 32) {
+    big.resize(nn + no);
+    ids = big.data();
+  }
+  for (size_t i = 0; i < nn; ++i) ids[i] = peerId(conf.peers[i]);
+  for (size_t i = 0; i < no; ++i) ids[nn + i] = peerId(oldConf->peers[i]);
+  GroupBatch::Guard lk(b, g_);
   if (b.pi_[g_] <= 0) return false;  // :204-207
   if (count <= 0) return true;
   if (b.la_[g_] + count - b.pi_[g_] + 1 > INT32_MAX)  // pendingMetaQueue is a Java ArrayList
     throw std::length_error("pending queue larger than an ArrayList");
-  const uint64_t cw = b.confWord(g_, conf, oldConf);
+  const uint64_t cw = b.confWord(g_, ids, static_cast<uint32_t>(nn), static_cast<uint32_t>(no), oldConf != nullptr);
   GroupBatch::Run* R = &b.runs_[static_cast<size_t>(g_) * JRQ_TABLE_MAX_RUNS];
   uint8_t& n = b.nruns_[g_];
   const int64_t idx = b.la_[g_] + 1;
@@ -622,52 +900,63 @@ bool BallotBox::appendPendingTasks(const Configuration& conf, const Configuratio
   }
   b.la_[g_] = idx + count - 1;
   b.markDirty(g_, GroupBatch::kDirtyLa);
-  return true;
-}
-
-bool BallotBox::appendPendingTask(const Configuration& conf, const Configuration* oldConf,
-                                  std::function<void(bool)> done) {
-  GroupBatch& b = *batch_;
-  if (b.pi_[g_] <= 0) return false;  // :204-207
-  if (!appendPendingTasks(conf, oldConf, 1)) return false;
-  if (done) {
+  if (done) {  // ClosureQueue.appendPendingClosure (ClosureQueueImpl.java:98-105)
     auto& q = b.closures_[g_];
     if (!q) q.reset(new std::deque<std::pair<int64_t, std::function<void(bool)>>>());
-    q->emplace_back(b.la_[g_], std::move(done));
+    q->emplace_back(b.la_[g_], std::move(*done));
   }
   return true;
 }
 
 bool BallotBox::setLastCommittedIndex(int64_t c) {
   GroupBatch& b = *batch_;
-  if (b.pi_[g_] != 0 || b.la_[g_] >= b.pi_[g_]) {
-    if (!(c < b.pi_[g_]))  // Requires.requireTrue (:229-231)
-      throw std::invalid_argument("Node changes to leader, pendingIndex=" +
-                                  std::to_string(b.pi_[g_]) +
-                                  ", param lastCommittedIndex=" + std::to_string(c));
-    return false;
-  }
-  if (c < b.lc_[g_]) return false;
-  if (c > b.lc_[g_]) {
+  CommitWaiter w;
+  {
+    GroupBatch::Guard lk(b, g_);
+    if (b.pi_[g_] != 0 || b.la_[g_] >= b.pi_[g_]) {
+      if (!(c < b.pi_[g_]))  // Requires.requireTrue (:229-231)
+        throw std::invalid_argument("Node changes to leader, pendingIndex=" +
+                                    std::to_string(b.pi_[g_]) +
+                                    ", param lastCommittedIndex=" + std::to_string(c));
+      return false;
+    }
+    if (c < b.lc_[g_]) return false;
+    if (c == b.lc_[g_]) return true;
     b.lc_[g_] = c;
     b.markDirty(g_, GroupBatch::kDirtyHeader);
-    if (b.waiter_[g_]) b.waiter_[g_](c);
+    w = b.waiter_[g_];
   }
+  if (w) w(c);  // onCommitted after unlocking (:244-246)
   return true;
 }
 
-int64_t BallotBox::getLastCommittedIndex() const { return batch_->lc_[g_]; }
-int64_t BallotBox::getPendingIndex() const { return batch_->pi_[g_]; }
+int64_t BallotBox::getLastCommittedIndex() const {
+  GroupBatch::Guard lk(*batch_, g_);
+  return batch_->lc_[g_];
+}
+int64_t BallotBox::getPendingIndex() const {
+  GroupBatch::Guard lk(*batch_, g_);
+  return batch_->pi_[g_];
+}
 int64_t BallotBox::getPendingMetaQueueSize() const {
   const GroupBatch& b = *batch_;
+  GroupBatch::Guard lk(b, g_);
   return b.pi_[g_] == 0 ? 0 : b.la_[g_] - b.pi_[g_] + 1;
 }
 
 std::string BallotBox::describe() const {
+  int64_t lc, pi, q;
+  {
+    const GroupBatch& b = *batch_;
+    GroupBatch::Guard lk(b, g_);
+    lc = b.lc_[g_];
+    pi = b.pi_[g_];
+    q = pi == 0 ? 0 : b.la_[g_] - pi + 1;
+  }
   std::ostringstream o;
-  o << "  lastCommittedIndex: " << getLastCommittedIndex() << "\n"
-    << "  pendingIndex: " << getPendingIndex() << "\n"
-    << "  pendingMetaQueueSize: " << getPendingMetaQueueSize() << "\n";
+  o << "  lastCommittedIndex: " << lc << "\n"
+    << "  pendingIndex: " << pi << "\n"
+    << "  pendingMetaQueueSize: " << q << "\n";
   return o.str();
 }
 

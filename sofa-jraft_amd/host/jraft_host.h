@@ -19,11 +19,13 @@
 // which the FSMCaller waiter sees onCommitted(index) exactly as the reference calls it.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <deque>
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -39,8 +41,22 @@ struct PeerId {
   std::string ip;
   int32_t port = 0;
   int32_t idx = 0;
+  // Interning cache: the process-wide id of this peer (0 = not looked up yet), like the hash a
+  // Java String caches.  Checked against the interned value on use, so changing ip/port/idx
+  // afterwards is safe; written with atomics, so one PeerId may be shared by threads.
+  mutable std::atomic<uint32_t> internId{0};
   PeerId() = default;
   PeerId(std::string ip_, int32_t port_, int32_t idx_ = 0) : ip(std::move(ip_)), port(port_), idx(idx_) {}
+  PeerId(const PeerId& o) : ip(o.ip), port(o.port), idx(o.idx), internId(o.internId.load(std::memory_order_relaxed)) {}
+  PeerId(PeerId&& o) noexcept
+      : ip(std::move(o.ip)), port(o.port), idx(o.idx), internId(o.internId.load(std::memory_order_relaxed)) {}
+  PeerId& operator=(const PeerId& o) {
+    ip = o.ip;
+    port = o.port;
+    idx = o.idx;
+    internId.store(o.internId.load(std::memory_order_relaxed), std::memory_order_relaxed);
+    return *this;
+  }
   // PeerId.toString (PeerId.java:135-144): ip:port[:idx]
   std::string toString() const;
   // PeerId.parse (PeerId.java:150-170): "ip:port" or "ip:port:idx"
@@ -151,7 +167,9 @@ struct BallotBoxOptions {
 
 class GroupBatch;
 
-// One Raft group's BallotBox (BallotBox.java), backed by a shared GroupBatch.
+// One Raft group's BallotBox (BallotBox.java), backed by a shared GroupBatch.  Thread-safe as
+// the reference's @ThreadSafe BallotBox is (BallotBox.java:45, a StampedLock per box): every
+// call takes the group's lock, and onCommitted / closures run after it is released.
 class BallotBox {
  public:
   BallotBox(std::shared_ptr<GroupBatch> batch, uint32_t group);
@@ -163,8 +181,9 @@ class BallotBox {
   // contiguous over the entries whose ballots count it (the Replicator invariant,
   // Replicator.java:1387-1401): a gap over such an entry throws std::logic_error.
   bool commitAt(int64_t firstLogIndex, int64_t lastLogIndex, const PeerId& peer);
-  // :147-156 -- acks recorded since the last epoch are decided first (one flush of the
-  // batch), as the reference has already committed them when the leader steps down
+  // :147-156 -- acks recorded since the last epoch are decided first (it waits for a flush in
+  // progress and flushes once more), as the reference has already committed them when the
+  // leader steps down.  Not from inside a commit callback of the same batch (logic_error).
   void clearPendingTasks();
   bool resetPendingIndex(int64_t newPendingIndex);                             // :167-186
   // :197-215 -- oldConf == nullptr means a stable configuration
@@ -181,6 +200,8 @@ class BallotBox {
   void shutdown() { clearPendingTasks(); }
 
  private:
+  bool append(const Configuration& conf, const Configuration* oldConf, int64_t count,
+              std::function<void(bool)>* done);
   std::shared_ptr<GroupBatch> batch_;
   uint32_t g_;
 };
@@ -194,14 +215,32 @@ struct FlushStats {
   double pack_ms = 0, device_ms = 0, deliver_ms = 0;
 };
 
+// When the background flusher (GroupBatch::startFlusher) runs an epoch: as soon as the oldest
+// change not yet flushed is maxDelayUs old, or maxDirtyGroups groups have changed, whichever
+// comes first (the reference decides inside commitAt; the batch trades that for one GPU epoch
+// per flush, and this bounds the ack -> onCommitted delay it adds).
+struct FlushPolicy {
+  uint32_t maxDelayUs = 1000;
+  uint32_t maxDirtyGroups = 1u << 16;
+};
+
 // BallotBox state of G groups, resident on the GPU (include/jrq.h jrq_table): the host keeps
 // a shadow of what Java's BallotBox holds, records what the API calls change, and flush()
 // ships only those changes (from page-locked buffers), runs one epoch and delivers the
 // commits -- closures, then waiter.onCommitted(index), as BallotBox.commitAt does after
-// unlocking (BallotBox.java:131-137).  The batch is driven from one host thread; flush()
-// packs and delivers on up to 16 threads, so the callbacks of different groups may run
-// concurrently (as the reference's replicator threads call commitAt concurrently) and must
-// not call back into the batch.
+// unlocking (BallotBox.java:131-137).
+//
+// Threading (the reference's callers: Bolt callback threads per replicator -> commitAt,
+// Replicator.java:1391; the LogManager thread's self-ack, NodeImpl.java:1156; the NodeImpl
+// disruptor -> appendPendingTask, NodeImpl.java:1195-1196; Bolt server threads ->
+// setLastCommittedIndex): every BallotBox call may come from any thread, concurrently with
+// other calls and with flush().  Each group has its own lock (a one-byte spin lock: calls
+// are short), peers are interned in a lock-free-read process-wide table, and each calling
+// thread marks the groups it changes in its own dirty list, which flush() swaps out, so
+// callers keep recording acks for the next epoch while one is packed, decided and delivered.
+// Flushes are serialised.  flush() packs and delivers on up to 16 threads; callbacks run
+// without the group's lock and may call commitAt / appendPendingTask* (on any group), but not
+// flush() or clearPendingTasks() of this batch (std::logic_error).
 class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
  public:
   // eng may be null until the first flush() (host-only state checks need no GPU)
@@ -215,19 +254,18 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   // pendingIndex / lastCommittedIndex, drop committed ballots, run closures, call waiters.
   // Returns the number of groups whose commit index advanced.
   uint32_t flush();
+  // Stats of the last flush (read them from the thread that flushed, or after stopFlusher).
   const FlushStats& lastFlush() const { return stats_; }
+  // A background thread flushing under `policy` until stopFlusher() (or destruction).
+  void startFlusher(const FlushPolicy& policy);
+  void stopFlusher();
+  uint64_t flushCount() const { return flushes_.load(std::memory_order_relaxed); }
 
  private:
   friend class BallotBox;
   struct Run {
     int64_t start;
     uint64_t conf;
-  };
-  struct PeerHash {
-    size_t operator()(const PeerId& p) const {
-      return std::hash<std::string>()(p.ip) ^ (static_cast<size_t>(p.port) << 20) ^
-             (static_cast<size_t>(p.idx) << 40);
-    }
   };
   template <class T>
   struct PinnedBuf {  // page-locked host staging (pageable when registration fails)
@@ -236,28 +274,44 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
     bool registered = false;
     void reserve(size_t n);
     void release();
+    PinnedBuf() = default;
+    PinnedBuf(PinnedBuf&& o) noexcept : p(o.p), cap(o.cap), registered(o.registered) { o.p = nullptr; o.cap = 0; }
     ~PinnedBuf() { release(); }
   };
+  struct DirtyList;  // one per calling thread
+  struct Pool;
+  struct Flusher;
+  struct Part;       // one pack worker's share of a flush
   static constexpr uint32_t kNoPeer = 0xFFFFFFFFu;
   static constexpr uint32_t kDirtyLa = 1u << 16, kDirtyHeader = 1u << 17, kDirtyReset = 1u << 18;
 
-  uint32_t internPeer(const PeerId& p);
+  void lock(uint32_t g) const;
+  void unlock(uint32_t g) const { lock_[g].store(0, std::memory_order_release); }
+  struct Guard {  // the group's lock for a scope
+    const GroupBatch& b;
+    uint32_t g;
+    Guard(const GroupBatch& b_, uint32_t g_) : b(b_), g(g_) { b.lock(g); }
+    ~Guard() { b.unlock(g); }
+  };
+  // all of these run under the group's lock
   int slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved = 0);
   uint32_t liveMask(uint32_t g) const;
-  uint64_t confWord(uint32_t g, const Configuration& conf, const Configuration* old);
+  // conf word of a Configuration pair given its peers' ids (new conf's nn, then old conf's no)
+  uint64_t confWord(uint32_t g, const uint32_t* ids, uint32_t nn, uint32_t no, bool hasOld);
   bool gapCountsPeer(uint32_t g, int slot, int64_t lo, int64_t hi) const;
-  void markDirty(uint32_t g, uint32_t bits) {
-    if (dirty_[g] == 0) dirtyList_.push_back(g);
-    dirty_[g] |= bits;
-  }
-  void commitTo(uint32_t g, int64_t c);
+  void markDirty(uint32_t g, uint32_t bits);
   void dropDeadRuns(uint32_t g);
-  struct Pool;
+
+  DirtyList* myDirtyList();
+  uint32_t flushLocked();
+  void packRange(Part& part, const uint32_t* groups, size_t n);
   template <class F>
   void parallelFor(size_t n, size_t grain, F&& f);
 
   Engine* eng_;
   uint32_t G_, P_;
+  const uint64_t serial_;                 // process-unique id (thread-local list caches)
+  std::unique_ptr<std::atomic<uint8_t>[]> lock_;  // [G] group locks
   std::vector<int64_t> pi_, lc_, la_;     // pendingIndex, lastCommittedIndex, lastAppended
   std::vector<Run> runs_;                 // [G][JRQ_TABLE_MAX_RUNS] conf runs of the queue
   std::vector<uint8_t> nruns_;
@@ -265,18 +319,23 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   std::vector<uint32_t> slotUse_;         // [G][P] flush count of the slot's last ack
   std::vector<int64_t> match_;            // [G][P] highest acked index per slot
   std::vector<uint32_t> dirty_;           // [G] slots / lastAppended / header changed
-  std::vector<uint32_t> dirtyList_;
   std::vector<CommitWaiter> waiter_;
   std::vector<uint8_t> inited_;
   // ClosureQueue (ClosureQueueImpl.java): only non-null closures, per group, in index order
   std::vector<std::unique_ptr<std::deque<std::pair<int64_t, std::function<void(bool)>>>>> closures_;
-  std::unordered_map<PeerId, uint32_t, PeerHash> peerIds_;
+  std::mutex listsMu_;                    // the per-thread dirty lists
+  std::vector<std::unique_ptr<DirtyList>> lists_;
+  std::atomic<uint64_t> dirtyCount_{0};   // groups marked since the last swap (flusher policy)
+  std::atomic<int64_t> oldestDirtyNs_{0}; // steady_clock time of the first mark since the swap
+  std::mutex flushMu_;                    // one flush at a time
+  std::vector<std::vector<uint32_t>> work_;  // swapped-out dirty lists (buffers kept)
+  std::vector<Part> parts_;
   jrq_table* table_ = nullptr;
-  PinnedBuf<jrq_group_state> states_;
-  PinnedBuf<uint64_t> recs_, changed_;
-  uint32_t flushes_ = 0;
+  PinnedBuf<uint64_t> changed_;
+  std::atomic<uint64_t> flushes_{0};
   FlushStats stats_;
   std::unique_ptr<Pool> pool_;
+  std::unique_ptr<Flusher> flusher_;
 };
 
 }  // namespace jraft

@@ -52,6 +52,8 @@ PI_FOLLOWS_LC = -(1 << 63)             # JRQ_PI_FOLLOWS_LC
 REC_LAST_APPENDED = 16                 # JRQ_REC_LAST_APPENDED
 TABLE_SEGMENTS = 16                    # JRQ_TABLE_SEGMENTS
 STATE_RESET_MATCH = 1                  # JRQ_STATE_RESET_MATCH
+# jrq_debug_option (test / A-B hooks)
+DBG_CRC_SEG_BYTES, DBG_CRC_REGS, DBG_CRC_PRIO, DBG_CRC_SEG_MAP, DBG_UPLOAD_PAGEABLE = 1, 2, 3, 4, 5
 
 try:
     import numpy as _np
@@ -94,6 +96,7 @@ SIGNATURES = [
     ("jrq_synchronize", C.c_int, [_V]),
     ("jrq_host_register", C.c_int, [_V, C.c_size_t]),
     ("jrq_host_unregister", C.c_int, [_V]),
+    ("jrq_debug_set", C.c_int, [_V, C.c_int, C.c_int64]),
     ("jrq_quorum_epoch_dev", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
     ("jrq_quorum_epoch", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
     ("jrq_quorum_epochs_dev", C.c_int,
@@ -125,6 +128,7 @@ SIGNATURES = [
     ("jrq_table_destroy", None, [_V]),
     ("jrq_table_update", C.c_int, [_V, _V, C.c_uint32, _V, C.c_uint32]),
     ("jrq_table_update_dev", C.c_int, [_V, _V, C.c_uint32, _V, C.c_uint32]),
+    ("jrq_table_update_gather", C.c_int, [_V, C.c_uint32, _V, _V, _V, _V]),
     ("jrq_table_epoch_dev", C.c_int, [_V, _V, _V, _V]),
     ("jrq_table_epoch", C.c_int, [_V, _V, _V, _V]),
     ("jrq_table_segment_capacity", C.c_uint32, [_V]),

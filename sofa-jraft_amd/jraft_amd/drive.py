@@ -26,14 +26,19 @@ def load():
         d = C.CDLL(DRIVE_PATH)
         d.jraft_drive_last_error.restype = C.c_char_p
         d.jraft_drive_epochs.restype = C.c_int
-        d.jraft_drive_epochs.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32] + [C.c_void_p] * 9
+        d.jraft_drive_epochs.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.c_uint32] + [C.c_void_p] * 9
+        d.jraft_drive_latency.restype = C.c_int
+        d.jraft_drive_latency.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double,
+                                          C.c_uint32, C.c_uint32, C.c_void_p]
         _drv = d
     return _drv
 
 
-def drive_epochs(device: int, s: dict):
-    """Replay series `s` (workloads.host_series) through BallotBox; returns (committed [K][G]
-    after each flush, stats dict of per-epoch arrays named by STATS)."""
+def drive_epochs(device: int, s: dict, threads: int = 1):
+    """Replay series `s` (workloads.host_series) through BallotBox, each epoch's calls made by
+    `threads` threads (contiguous group slices); returns (committed [K][G] after each flush,
+    stats dict of per-epoch arrays named by STATS)."""
     d = load()
     K, P, G = s["match"].shape
     arrs = {k: np.ascontiguousarray(s[k]) for k in ("pending_index", "last_committed", "conf_a",
@@ -42,9 +47,27 @@ def drive_epochs(device: int, s: dict):
     out = np.zeros((K, G), np.int64)
     stats = np.zeros((K, len(STATS)), np.float64)
     ptr = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
-    rc = d.jraft_drive_epochs(device, G, P, K, ptr(arrs["pending_index"]), ptr(arrs["last_committed"]),
+    rc = d.jraft_drive_epochs(device, G, P, K, threads, ptr(arrs["pending_index"]), ptr(arrs["last_committed"]),
                               ptr(arrs["conf_a"]), ptr(arrs["conf_b"]), ptr(arrs["switch_at"]),
                               ptr(arrs["last_appended"]), ptr(arrs["match"]), ptr(out), ptr(stats))
     if rc != 0:
         raise RuntimeError("jraft_drive_epochs: " + (d.jraft_drive_last_error() or b"").decode())
     return out, {k: stats[:, i] for i, k in enumerate(STATS)}
+
+
+LATENCY = ("commits", "entries", "acks", "seconds", "flushes", "p50_us", "p90_us", "p99_us",
+           "p999_us", "max_us", "samples")
+
+
+def drive_latency(device: int, groups: int, peers: int, threads: int, seconds: float,
+                  max_delay_us: int, max_dirty: int) -> dict:
+    """Steady load through BallotBox with the background flusher (GroupBatch::startFlusher,
+    FlushPolicy{max_delay_us, max_dirty}): `threads` producers append one entry per group and
+    every peer acks it; returns counts and the ack -> onCommitted latency quantiles (us)."""
+    d = load()
+    out = np.zeros(len(LATENCY), np.float64)
+    rc = d.jraft_drive_latency(device, groups, peers, threads, seconds, max_delay_us, max_dirty,
+                               C.c_void_p(out.ctypes.data))
+    if rc != 0:
+        raise RuntimeError("jraft_drive_latency: " + (d.jraft_drive_last_error() or b"").decode())
+    return dict(zip(LATENCY, out.tolist()))

@@ -78,6 +78,10 @@ class Engine:
     def synchronize(self):
         check(self._L.jrq_synchronize(self._h), self._h)
 
+    def debug_set(self, option: int, value: int):
+        """jrq_debug_set: a test / A-B override (_lib.DBG_*) on this engine only."""
+        check(self._L.jrq_debug_set(self._h, option, value), self._h)
+
     # -------------------------------------------------------------- quorum --
     @staticmethod
     def _batch(ptr, match, pending_index, last_appended, last_committed, conf, run_off, run_start,

@@ -1,3 +1,4 @@
+import ctypes
 import os
 import sys
 
@@ -27,3 +28,41 @@ def engine():
     e = Engine(0)
     yield e
     e.close()
+
+
+_hip = None
+
+
+def _hip_runtime():
+    """The HIP runtime libjrq and torch share in this process (loaded by jraft_amd._lib)."""
+    global _hip
+    if _hip is None:
+        from jraft_amd import _lib
+        _lib.load()
+        # already loaded (torch's copy, SONAME libamdhip64.so.7): NOLOAD binds that one
+        _hip = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
+        _hip.hipDeviceSynchronize.restype = ctypes.c_int
+        _hip.hipGetLastError.restype = ctypes.c_int
+        _hip.hipGetErrorString.restype = ctypes.c_char_p
+        _hip.hipGetErrorString.argtypes = [ctypes.c_int]
+    return _hip
+
+
+@pytest.fixture(autouse=True)
+def _device_fault_check(request):
+    """After every GPU test: synchronise the whole device and check for an error.  A kernel
+    fault is asynchronous -- on its own it surfaces at the next HIP call, possibly in another
+    test (round 2 saw an "illegal memory access" reported by a later copy).  Synchronising
+    here charges it to the test whose kernels caused it."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    hip = _hip_runtime()
+    rc = hip.hipDeviceSynchronize()
+    # (hipGetLastError alone also holds expected API refusals, e.g. the engine's probe of an
+    # unregistered pointer; only a failing device-wide synchronisation is a fault)
+    hip.hipGetLastError()
+    if rc:
+        pytest.fail("device error after %s: %s (hipDeviceSynchronize -> %d)"
+                    % (request.node.nodeid, hip.hipGetErrorString(rc).decode(), rc),
+                    pytrace=False)

@@ -1,0 +1,169 @@
+// fake_jrq.cpp -- TEST DOUBLE of libjrq.so for CPU-only sanitizer builds of the host mirror.
+//
+// TEST INFRASTRUCTURE ONLY.  ThreadSanitizer and AddressSanitizer cannot instrument the GPU
+// side, and this container has no GPU, so the sanitizer binaries (tests/cpp/Makefile:
+// host_test_tsan, host_test_asan) link the host mirror (sofa-jraft_amd/host/jraft_host.cpp)
+// against this stand-in instead of libjrq.so.  It implements the few entry points the mirror
+// calls with the CPU oracle (oracle/jraft_oracle.c: the Java-faithful BallotBox replay and the
+// byte-at-a-time CRC), so that every concurrent host-side path -- locks, dirty lists, packing,
+// gathering, delivery, the flusher -- runs under the sanitizers with real epoch results.  It is
+// never built into libjrq.so, libjraft_host.so or anything bench.py or smoke() loads; the GPU
+// build of the same tests (tests/_build/host_test) links the real library.
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/jrq.h"
+#include "../../oracle/jraft_oracle.h"
+
+struct jrq_engine {
+  std::string err;
+};
+
+namespace {
+thread_local std::string g_err;
+}
+
+struct jrq_table {
+  jrq_engine* e;
+  uint32_t G, P;
+  std::vector<int64_t> pi, la, lc, match;  // pi resolved (never JRQ_PI_FOLLOWS_LC)
+  std::vector<uint8_t> nr;
+  std::vector<int64_t> start;   // [G][JRQ_TABLE_MAX_RUNS]
+  std::vector<uint64_t> conf;   // [G][JRQ_TABLE_MAX_RUNS]
+  uint32_t invalid = 0;
+  std::mutex mu;  // the real table orders calls on the engine stream
+};
+
+extern "C" {
+
+jrq_engine* jrq_create(int, uint32_t, uint8_t, int* err) {
+  if (err) *err = JRQ_OK;
+  return new jrq_engine();
+}
+void jrq_destroy(jrq_engine* e) { delete e; }
+const char* jrq_last_error(const jrq_engine* e) { return e ? e->err.c_str() : g_err.c_str(); }
+int jrq_host_register(void* p, size_t n) { return p && n ? JRQ_OK : JRQ_E_INVALID; }
+int jrq_host_unregister(void* p) { return p ? JRQ_OK : JRQ_E_INVALID; }
+
+int jrq_crc64_batch(jrq_engine*, const uint8_t* payload, const uint64_t* offsets, uint32_t N,
+                    uint64_t* crc_out) {
+  std::vector<uint64_t> off(offsets, offsets + N + 1);
+  for (auto& o : off) o -= offsets[0];
+  jo_crc64_batch(payload + offsets[0], off.data(), N, crc_out);
+  return JRQ_OK;
+}
+
+int jrq_crc64_stream_update(jrq_engine*, uint64_t* state, const uint8_t* payload,
+                            const uint64_t* offsets, uint32_t S) {
+  for (uint32_t s = 0; s < S; ++s)
+    state[s] = jo_crc64_update(state[s], payload + offsets[s], offsets[s + 1] - offsets[s]);
+  return JRQ_OK;
+}
+
+int jrq_logentry_checksum_batch(jrq_engine*, const uint8_t* type, const int64_t* index,
+                                const int64_t* term, const uint64_t* peer_xor,
+                                const uint8_t* payload, const uint64_t* offsets, uint32_t N,
+                                uint64_t* out, const uint64_t* expected, const uint8_t* has,
+                                uint8_t* corrupt_out) {
+  std::vector<uint64_t> off(offsets, offsets + N + 1);
+  for (auto& o : off) o -= offsets[0];
+  jo_logentry_checksum_batch(type, index, term, peer_xor, payload + offsets[0], off.data(), N, out,
+                             expected, has, corrupt_out);
+  return JRQ_OK;
+}
+
+jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
+  auto* t = new jrq_table();
+  t->e = e;
+  t->G = G;
+  t->P = P;
+  t->pi.assign(G, 0);
+  t->la.assign(G, 0);
+  t->lc.assign(G, 0);
+  t->match.assign(static_cast<size_t>(G) * P, 0);
+  t->nr.assign(G, 0);
+  t->start.assign(static_cast<size_t>(G) * JRQ_TABLE_MAX_RUNS, 0);
+  t->conf.assign(static_cast<size_t>(G) * JRQ_TABLE_MAX_RUNS, 0);
+  if (err) *err = JRQ_OK;
+  return t;
+}
+void jrq_table_destroy(jrq_table* t) { delete t; }
+
+int jrq_table_update_gather(jrq_table* t, uint32_t parts, const jrq_group_state* const* states,
+                            const uint32_t* n_states, const uint64_t* const* recs,
+                            const uint32_t* n_recs) {
+  std::lock_guard<std::mutex> l(t->mu);
+  for (uint32_t i = 0; i < parts; ++i)  // headers of every part first (include/jrq.h)
+    for (uint32_t k = 0; k < n_states[i]; ++k) {
+      const jrq_group_state& s = states[i][k];
+      const int64_t pi = s.pending_index == JRQ_PI_FOLLOWS_LC ? s.last_committed + 1 : s.pending_index;
+      if (s.group >= t->G || s.num_runs > JRQ_TABLE_MAX_RUNS ||
+          (s.num_runs == 0 && pi != 0 && s.last_appended >= pi)) {
+        ++t->invalid;
+        continue;
+      }
+      const uint32_t g = s.group;
+      t->pi[g] = pi;
+      t->la[g] = s.last_appended;
+      t->lc[g] = s.last_committed;
+      t->nr[g] = static_cast<uint8_t>(s.num_runs);
+      for (uint32_t r = 0; r < JRQ_TABLE_MAX_RUNS; ++r) {
+        t->start[g * JRQ_TABLE_MAX_RUNS + r] = s.run_start[r];
+        t->conf[g * JRQ_TABLE_MAX_RUNS + r] = s.run_conf[r] & ~JRQ_CONF_RUNS;
+      }
+      if (s.flags & JRQ_STATE_RESET_MATCH)
+        for (uint32_t p = 0; p < t->P; ++p) t->match[static_cast<size_t>(g) * t->P + p] = pi - 1;
+    }
+  for (uint32_t i = 0; i < parts; ++i)
+    for (uint32_t k = 0; k < n_recs[i]; ++k) {
+      const uint64_t r = recs[i][k];
+      const uint32_t f = static_cast<uint32_t>(r & 31u), g = static_cast<uint32_t>(r >> 5) & ((1u << 27) - 1u);
+      const int64_t v = static_cast<int64_t>(static_cast<uint32_t>(r >> 32));
+      if (g >= t->G || f > 16u || (f < 16u && f >= t->P)) {
+        ++t->invalid;
+        continue;
+      }
+      const int64_t val = t->pi[g] - 1 + v;
+      if (f == 16u) {
+        if (t->nr[g] == 0 && t->pi[g] != 0 && val >= t->pi[g]) {
+          ++t->invalid;
+          continue;
+        }
+        t->la[g] = val;
+      } else {
+        t->match[static_cast<size_t>(g) * t->P + f] = val;
+      }
+    }
+  return JRQ_OK;
+}
+
+// One epoch, group by group through the oracle's BallotBox replay (jo_quorum_epoch_replay).
+int jrq_table_epoch(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, uint8_t* status_out) {
+  std::lock_guard<std::mutex> l(t->mu);
+  uint32_t n = 0;
+  std::vector<int64_t> m(t->P);
+  for (uint32_t g = 0; g < t->G; ++g) {
+    if (status_out) status_out[g] = JO_ST_NOT_LEADER;
+    if (t->pi[g] == 0 || t->nr[g] == 0) continue;
+    for (uint32_t p = 0; p < t->P; ++p) m[p] = t->match[static_cast<size_t>(g) * t->P + p];
+    const uint32_t ro[2] = {0, t->nr[g]};
+    int64_t c = 0;
+    uint8_t st = 0;
+    jo_quorum_epoch_replay(1, t->P, m.data(), &t->pi[g], &t->la[g], &t->lc[g],
+                           &t->conf[g * JRQ_TABLE_MAX_RUNS], ro, &t->start[g * JRQ_TABLE_MAX_RUNS],
+                           &t->conf[g * JRQ_TABLE_MAX_RUNS], 64, &c, &st);
+    if (status_out) status_out[g] = st;
+    if (c > t->lc[g]) {
+      changed_out[n++] = (static_cast<uint64_t>(c - t->pi[g] + 1) << 32) | g;
+      t->lc[g] = c;
+      t->pi[g] = c + 1;
+    }
+  }
+  *n_changed = n;
+  return JRQ_OK;
+}
+
+}  // extern "C"

@@ -8,7 +8,9 @@
 //   core/BallotBoxTest.java:62-154, entity/BallotTest.java:37-50,
 //   entity/LogEntryTest.java:95-125, util/CrcUtilTest.java:27-42
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
+#include <thread>
 #include <cstring>
 #include <functional>
 #include <string>
@@ -471,7 +473,226 @@ static void testRandomDifferentialOnGpu(Engine& eng) {
   CHECK(flushes > 10);
 }
 
+// ------------------------------------------------------- concurrent callers
+
+// The reference's callers of one BallotBox run concurrently (BallotBox is @ThreadSafe,
+// BallotBox.java:45, a StampedLock per call, :98): the NodeImpl disruptor appends
+// (NodeImpl.java:1195-1196), the LogManager thread self-acks (NodeImpl.java:1156), one Bolt
+// callback thread per replicator acks its peer (Replicator.java:1391).  Here one thread per
+// role works over every group of the batch while a background flusher decides epochs, and a
+// second stage steps down a quarter of the groups from several threads at once.  The final
+// state of every group must equal the oracle's BallotBox fed the same calls in one order (the
+// post-epoch state is order-independent, BallotBox.java:96-139), every closure must run
+// exactly once, and onCommitted must see increasing indices ending at lastCommittedIndex.
+static void testConcurrentCallers(Engine& eng, uint32_t G, int64_t kEntries) {
+  const uint32_t P = 5, kAcks = 4;  // peers 0 (leader) .. 4
+  auto batch = std::make_shared<GroupBatch>(&eng, G, 8);
+  std::vector<BallotBox> boxes;
+  boxes.reserve(G);
+  struct Obs {
+    std::atomic<int64_t> last{-1};
+    std::atomic<int64_t> calls{0};
+    std::atomic<bool> monotone{true};
+    std::atomic<int64_t> closuresOk{0}, closuresFailed{0};
+  };
+  std::vector<Obs> obs(G);
+  std::vector<int64_t> pi0(G);
+  std::vector<int64_t> jointAt(G, 0);  // index of the joint conf entry (0: stays stable)
+  std::vector<std::atomic<int64_t>> published(G);  // highest appended index, for the ackers
+  std::mt19937_64 rng(77);
+  for (uint32_t g = 0; g < G; ++g) {
+    boxes.emplace_back(batch, g);
+    Obs* o = &obs[g];
+    boxes[g].init({[o](int64_t c) {
+      const int64_t prev = o->last.exchange(c);
+      if (c <= prev) o->monotone = false;
+      o->calls.fetch_add(1);
+    }});
+    pi0[g] = 1 + static_cast<int64_t>(rng() % 1000);
+    CHECK(boxes[g].resetPendingIndex(pi0[g]));
+    published[g].store(pi0[g] - 1);
+    if (g % 4 == 1) jointAt[g] = pi0[g] + kEntries / 3 + static_cast<int64_t>(rng() % (kEntries / 4));
+  }
+  auto confOf = [](int n) {
+    Configuration c;
+    for (int p = 0; p < n; ++p) c.peers.emplace_back("10.0.0.1", 9000 + p);
+    return c;
+  };
+  const Configuration c3 = confOf(3), c5 = confOf(5);
+  std::vector<PeerId> peers;
+  for (int p = 0; p < 5; ++p) peers.emplace_back("10.0.0.1", 9000 + p);
+  batch->startFlusher(FlushPolicy{200, 4096});
+  std::atomic<bool> failed{false};
+  std::vector<std::thread> th;
+  // the NodeImpl disruptor: batches of appends per group, every 3rd entry with a closure
+  th.emplace_back([&] {
+    try {
+      for (int64_t k = 0; k < kEntries; k += 8)
+        for (uint32_t g = 0; g < G; ++g) {
+          for (int64_t i = 0; i < 8; ++i) {
+            const int64_t idx = pi0[g] + k + i;
+            const bool joint = jointAt[g] && idx >= jointAt[g];
+            const Configuration& c = joint ? c5 : c3;
+            const Configuration* old = joint ? &c3 : nullptr;
+            Obs* o = &obs[g];
+            const bool ok = idx % 3 == 0
+                                ? boxes[g].appendPendingTask(c, old, [o](bool st) {
+                                    (st ? o->closuresOk : o->closuresFailed).fetch_add(1);
+                                  })
+                                : boxes[g].appendPendingTask(c, old);
+            if (!ok) failed = true;
+          }
+          published[g].store(pi0[g] + k + 7, std::memory_order_release);
+        }
+    } catch (...) {
+      failed = true;
+    }
+  });
+  // the LogManager self-ack (peer 0) and one replicator thread per follower: contiguous acks
+  // up to what has been appended, peer p lagging p entries behind; peers 3 and 4 (named only
+  // by the joint conf) ack every group, as catch-up replicators would
+  for (uint32_t p = 0; p < P; ++p)
+    th.emplace_back([&, p] {
+      try {
+        std::vector<int64_t> m(G);
+        for (uint32_t g = 0; g < G; ++g) m[g] = pi0[g] - 1;
+        for (;;) {
+          bool more = false;
+          for (uint32_t g = 0; g < G; ++g) {
+            const int64_t top = std::min(published[g].load(std::memory_order_acquire) - static_cast<int64_t>(p),
+                                         pi0[g] + kEntries - 1 - static_cast<int64_t>(p));
+            if (m[g] < pi0[g] + kEntries - 1 - static_cast<int64_t>(p)) more = true;
+            if (top > m[g]) {
+              const int64_t last = std::min(top, m[g] + static_cast<int64_t>(kAcks));
+              boxes[g].commitAt(m[g] + 1, last, peers[p]);
+              m[g] = last;
+            }
+          }
+          if (!more) break;
+        }
+      } catch (...) {
+        failed = true;
+      }
+    });
+  // readers: getLastCommittedIndex never goes backwards
+  th.emplace_back([&] {
+    std::vector<int64_t> seen(G, 0);
+    for (int r = 0; r < 200; ++r)
+      for (uint32_t g = 0; g < G; ++g) {
+        const int64_t c = boxes[g].getLastCommittedIndex();
+        if (c < seen[g]) failed = true;
+        seen[g] = c;
+      }
+  });
+  for (auto& t : th) t.join();
+  batch->stopFlusher();
+  batch->flush();
+  CHECK(!failed);
+  std::vector<jo_ballot_box*> ob(G);
+  auto same = [&](uint32_t g) {
+    const int64_t lc = jo_bb_last_committed_index(ob[g]);
+    if (boxes[g].getLastCommittedIndex() == lc && boxes[g].getPendingIndex() == jo_bb_pending_index(ob[g]) &&
+        boxes[g].getPendingMetaQueueSize() == jo_bb_queue_size(ob[g]))
+      return true;
+    std::fprintf(stderr, "  group %u: mirror lc %lld pi %lld q %lld, oracle lc %lld pi %lld q %lld\n", g,
+                 (long long)boxes[g].getLastCommittedIndex(), (long long)boxes[g].getPendingIndex(),
+                 (long long)boxes[g].getPendingMetaQueueSize(), (long long)lc,
+                 (long long)jo_bb_pending_index(ob[g]), (long long)jo_bb_queue_size(ob[g]));
+    return false;
+  };
+  for (uint32_t g = 0; g < G; ++g) {
+    jo_ballot_box* bb = ob[g] = jo_bb_new();
+    CHECK(jo_bb_reset_pending_index(bb, pi0[g]) == JO_TRUE);
+    const int32_t i3[] = {0, 1, 2}, i5[] = {0, 1, 2, 3, 4};
+    for (int64_t idx = pi0[g]; idx < pi0[g] + kEntries; ++idx) {
+      const bool joint = jointAt[g] && idx >= jointAt[g];
+      jo_bb_append_pending_task(bb, joint ? i5 : i3, joint ? 5 : 3, joint ? i3 : nullptr, joint ? 3 : -1);
+    }
+    for (int32_t p = 0; p < static_cast<int32_t>(P); ++p) jo_bb_commit_at(bb, pi0[g], pi0[g] + kEntries - 1 - p, p);
+    CHECK(same(g));
+    const int64_t lc = jo_bb_last_committed_index(bb);
+    CHECK(obs[g].monotone && obs[g].last == lc);
+    // closures of entries <= lc ran once with OK; the rest are still queued
+    int64_t exp = 0;
+    for (int64_t idx = pi0[g]; idx <= lc; ++idx) exp += idx % 3 == 0;
+    CHECK(obs[g].closuresOk == exp && obs[g].closuresFailed == 0);
+  }
+  CHECK(batch->flushCount() >= 3);
+  // step-downs from several threads at once (groups g % 16 < 4), concurrent with acks of the
+  // other groups by peer 4 up to the last entry
+  std::vector<std::thread> th2;
+  for (uint32_t t = 0; t < 4; ++t)
+    th2.emplace_back([&, t] {
+      for (uint32_t g = t; g < G; g += 16) boxes[g].clearPendingTasks();
+    });
+  th2.emplace_back([&] {
+    for (uint32_t g = 0; g < G; ++g)
+      if (g % 16 >= 4) boxes[g].commitAt(pi0[g], pi0[g] + kEntries - 1, peers[4]);
+  });
+  for (auto& t : th2) t.join();
+  batch->flush();
+  for (uint32_t g = 0; g < G; ++g) {
+    if (g % 16 < 4) {
+      jo_bb_clear_pending_tasks(ob[g]);
+      int64_t queued = 0;  // entries above lc with closures: failed by the step-down
+      for (int64_t idx = boxes[g].getLastCommittedIndex() + 1; idx < pi0[g] + kEntries; ++idx) queued += idx % 3 == 0;
+      CHECK(obs[g].closuresFailed == queued);
+    } else {
+      jo_bb_commit_at(ob[g], pi0[g], pi0[g] + kEntries - 1, 4);
+    }
+    CHECK(same(g));
+    CHECK(obs[g].last == jo_bb_last_committed_index(ob[g]));
+  }
+  for (auto* bb : ob) jo_bb_free(bb);
+}
+
+// Every slot of the group named by a live conf run, and a peer in none of them acks: no pending
+// ballot counts it (Ballot.grant finds nothing, Ballot.java:100-127), commitAt returns true.
+static void testAckFromPeerWithoutSlot() {
+  auto batch = std::make_shared<GroupBatch>(nullptr, 1, 3);
+  BallotBox box(batch, 0);
+  Waiter w;
+  CHECK(box.init({w.fn()}));
+  CHECK(box.resetPendingIndex(5));
+  CHECK(box.appendPendingTask(conf("a:1,b:2,c:3"), nullptr));
+  CHECK(box.commitAt(5, 5, PeerId("d", 4)));
+  CHECK(box.commitAt(5, 5, PeerId("a", 1)));
+  CHECK(box.getPendingMetaQueueSize() == 1);
+}
+
+// flush() and clearPendingTasks() from inside a commit callback of the same batch are refused.
+static void testReentrantFlushRefused(Engine& eng) {
+  auto batch = std::make_shared<GroupBatch>(&eng, 2, 3);
+  BallotBox a(batch, 0), b(batch, 1);
+  bool refusedFlush = false, refusedClear = false, appended = false;
+  CHECK(a.init({[&](int64_t) {
+    try {
+      batch->flush();
+    } catch (const std::logic_error&) {
+      refusedFlush = true;
+    }
+    try {
+      b.clearPendingTasks();
+    } catch (const std::logic_error&) {
+      refusedClear = true;
+    }
+    appended = b.appendPendingTask(conf("a:1,b:2,c:3"), nullptr);  // recording calls are fine
+  }}));
+  Waiter w;
+  CHECK(b.init({w.fn()}));
+  CHECK(a.resetPendingIndex(1) && b.resetPendingIndex(1));
+  CHECK(a.appendPendingTask(conf("a:1,b:2,c:3"), nullptr));
+  a.commitAt(1, 1, PeerId("a", 1));
+  a.commitAt(1, 1, PeerId("b", 2));
+  batch->flush();
+  CHECK(a.getLastCommittedIndex() == 1);
+  CHECK(refusedFlush && refusedClear && appended);
+  CHECK(b.getPendingMetaQueueSize() == 1);
+}
+
 int main(int argc, char** argv) {
+  // "gpu": with an engine (the real libjrq.so on the GPU box; the sanitizer builds link the
+  // test double tests/cpp/fake_jrq.cpp instead and run the same list on the CPU)
   const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
   struct T {
     const char* name;
@@ -487,6 +708,7 @@ int main(int argc, char** argv) {
       {"testSetLastCommittedIndex", testSetLastCommittedIndex},
       {"testInitRequiresWaiter", testInitRequiresWaiter},
       {"testNonContiguousAckRejected", testNonContiguousAckRejected},
+      {"testAckFromPeerWithoutSlot", testAckFromPeerWithoutSlot},
   };
   std::unique_ptr<Engine> eng;
   if (gpu) {
@@ -500,6 +722,10 @@ int main(int argc, char** argv) {
     tests.push_back({"testLogEntryChecksumOnGpu", [&] { testLogEntryChecksumOnGpu(e); }});
     tests.push_back({"testCrcUtilOnGpu", [&] { testCrcUtilOnGpu(e); }});
     tests.push_back({"testCRC64ChecksumOnGpu", [&] { testCRC64ChecksumOnGpu(e); }});
+    tests.push_back({"testConcurrentCallers", [&] { testConcurrentCallers(e, 384, 400); }});
+    // > 8192 changed groups per epoch: flush() packs and delivers on several threads
+    tests.push_back({"testConcurrentCallersWide", [&] { testConcurrentCallers(e, 20000, 48); }});
+    tests.push_back({"testReentrantFlushRefused", [&] { testReentrantFlushRefused(e); }});
   }
   for (auto& t : tests) {
     const int before = g_fail;

@@ -10,6 +10,7 @@ import os
 import numpy as np
 import pytest
 
+from jraft_amd import _lib
 from jraft_amd import workloads as W
 
 pytestmark = pytest.mark.gpu
@@ -71,12 +72,12 @@ def test_mixed_huge_and_tiny(engine, oracle):
 
 
 @pytest.mark.parametrize("seg", ["64", "100", "1000"])
-def test_tiny_segments_stress_straddlers(oracle, seg, monkeypatch):
+def test_tiny_segments_stress_straddlers(oracle, seg):
     """Forced tiny segments: nearly every entry spans many segments, so every result goes
     through the x^(8n) shifts and the atomic last-arriver hand-off (all lanes, all XCDs)."""
     from jraft_amd import Engine
-    monkeypatch.setenv("JRQ_CRC_SEG_BYTES", seg)
     with Engine(0) as e:
+        e.debug_set(_lib.DBG_CRC_SEG_BYTES, int(seg))
         offs = W.ragged_offsets(int(seg), 20000, 3000, start=3)
         payload = W.random_bytes(int(seg), int(offs[-1]) + 1)
         exp = oracle.crc64_batch(payload, offs)
@@ -86,31 +87,30 @@ def test_tiny_segments_stress_straddlers(oracle, seg, monkeypatch):
 
 @pytest.mark.parametrize("seg,seg_map", [("0", "0"), ("0", "1"), ("256", "1"), ("768", "0"),
                                          ("4096", "1"), (str(1 << 20), "0")])
-def test_segment_sizes_and_maps(oracle, seg, seg_map, monkeypatch):
+def test_segment_sizes_and_maps(oracle, seg, seg_map):
     """Every segment size (rounded to 256 B) and chunk-to-workgroup map is bit-exact on
     ragged, unaligned and long entries: pieces land in per-segment slots (finish kernel)
     or go through the atomic hand-off when an entry spans more than 64 segments."""
     from jraft_amd import Engine
-    monkeypatch.setenv("JRQ_CRC_SEG_BYTES", seg)
-    monkeypatch.setenv("JRQ_CRC_SEG_MAP", seg_map)
     lens = [0, 1, 15, 16, 17, 63, 64, 65, 255, 256, 257, 1023, 4099, 16384, 100000, 3 << 20, 7]
     offs = np.concatenate([[5], 5 + np.cumsum(lens)]).astype(np.uint64)
     payload = W.random_bytes(11, int(offs[-1]) + 2)
     rag = W.ragged_offsets(12, 5000, 9000, start=1)
     payload2 = W.random_bytes(13, int(rag[-1]) + 1)
     with Engine(0) as e:
+        e.debug_set(_lib.DBG_CRC_SEG_BYTES, int(seg))
+        e.debug_set(_lib.DBG_CRC_SEG_MAP, int(seg_map))
         np.testing.assert_array_equal(e.crc64_batch(payload, offs), oracle.crc64_batch(payload, offs))
         np.testing.assert_array_equal(e.crc64_batch(payload2, rag), oracle.crc64_batch(payload2, rag))
 
 
 @pytest.mark.parametrize("seg,n,lo,hi", [("256", 600, 65, 400), ("512", 600, 65, 400),
                                          ("256", 24, 4097, 12000)])
-def test_adjacent_long_entries_group_slots(oracle, seg, n, lo, hi, monkeypatch):
+def test_adjacent_long_entries_group_slots(oracle, seg, n, lo, hi):
     """Back-to-back entries of lo..hi segments: every 64-segment group slot (and, past 4096
     segments, every 64-group supergroup slot) is shared by one long entry ending in it and
     one starting in it (multi-level hand-off keys)."""
     from jraft_amd import Engine
-    monkeypatch.setenv("JRQ_CRC_SEG_BYTES", seg)
     S = int(seg)
     lens = W.uniform(31, n, lo * S, hi * S, stream=5)
     lens[::7] = (lo - 1) * S + 1   # exactly lo parts when aligned
@@ -119,17 +119,18 @@ def test_adjacent_long_entries_group_slots(oracle, seg, n, lo, hi, monkeypatch):
     payload = W.random_bytes(31, int(offs[-1]) + 1)
     exp = oracle.crc64_batch(payload, offs)
     with Engine(0) as e:
+        e.debug_set(_lib.DBG_CRC_SEG_BYTES, S)
         for _ in range(2):
             np.testing.assert_array_equal(e.crc64_batch(payload, offs), exp)
 
 
-def test_more_segments_than_lanes(oracle, monkeypatch):
+def test_more_segments_than_lanes(oracle):
     """256-B segments over ~90 MB: each wave loops over several chunks."""
     from jraft_amd import Engine
-    monkeypatch.setenv("JRQ_CRC_SEG_BYTES", "256")
     offs = W.ragged_offsets(21, 40000, 4000, start=9)
     payload = W.random_bytes(21, int(offs[-1]) + 3)
     with Engine(0) as e:
+        e.debug_set(_lib.DBG_CRC_SEG_BYTES, 256)
         np.testing.assert_array_equal(e.crc64_batch(payload, offs), oracle.crc64_batch(payload, offs))
 
 

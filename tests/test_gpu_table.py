@@ -197,3 +197,63 @@ def test_device_variant_and_view(engine, oracle):
     assert v.G == G and v.num_peers == P and v.ld >= G and v.last_committed
     np.testing.assert_array_equal(t.read()["last_committed"], ce)
     t.close()
+
+
+def test_reset_header_in_follows_lc_encoding(engine):
+    """A new leader's header in the steady-state encoding (pendingIndex = lastCommitted + 1 sent
+    as JRQ_PI_FOLLOWS_LC, as GroupBatch::flush sends it after setLastCommittedIndex +
+    resetPendingIndex(lc + 1)) with RESET_MATCH: every slot's match becomes pendingIndex - 1,
+    nothing reports OUT_OF_RANGE, and later acks commit as usual."""
+    from jraft_amd import conf_word
+    G, P = 130, 3
+    t = Table(engine, G, P)
+    st = Table.states(G)
+    st["group"] = np.arange(G)
+    st["num_runs"] = 1
+    st["flags"] = _lib.STATE_RESET_MATCH
+    lc = 1000 + np.arange(G, dtype=np.int64) * 7
+    st["pending_index"] = _lib.PI_FOLLOWS_LC
+    st["last_committed"] = lc
+    st["last_appended"] = lc + 10
+    st["run_conf"][:, 0] = conf_word(0b111)
+    t.update(st)
+    r = t.read()
+    np.testing.assert_array_equal(r["pending_index"], lc + 1)
+    np.testing.assert_array_equal(r["match"], np.broadcast_to(lc, (P, G)))
+    changed, stt = t.epoch(status=True)
+    assert len(changed) == 0 and (stt == 0).all()
+    gs = np.arange(G)
+    t.update(None, np.concatenate([_lib.rec(gs, 0, 4), _lib.rec(gs, 2, 6)]))
+    changed, stt = t.epoch(status=True)
+    g, d = decode_changed(changed)
+    assert sorted(g.tolist()) == list(range(G)) and (d == 4).all() and (stt == 0).all()
+    t.check()
+    t.close()
+
+
+def test_pending_entries_without_conf_run_are_invalid(engine):
+    """A leader header with entries pending but no conf run (conf word 0 = quorum 0, which would
+    grant everything), or a queue-size record growing such a group's queue, is refused and
+    reported; the group then commits nothing whatever it is acked."""
+    t = Table(engine, 8, 3)
+    st = Table.states(1)
+    st["group"] = 2
+    st["num_runs"] = 0
+    st["pending_index"] = 10
+    st["last_committed"] = 9
+    st["last_appended"] = 12
+    t.update(st)
+    with pytest.raises(JrqError):
+        t.check()
+    st["last_appended"] = 9   # nothing pending (what resetPendingIndex leaves): valid
+    t.update(st)
+    t.check()
+    t.update(None, np.atleast_1d(_lib.rec(2, _lib.REC_LAST_APPENDED, 3)))
+    with pytest.raises(JrqError):
+        t.check()
+    t.update(None, np.concatenate([np.atleast_1d(_lib.rec(2, p, 3)) for p in range(3)]))
+    changed, _ = t.epoch()
+    assert len(changed) == 0
+    assert t.read()["last_appended"][2] == 9
+    t.check()
+    t.close()

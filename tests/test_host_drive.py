@@ -38,13 +38,17 @@ def _expected_counts(s, committed):
     return recs, changed
 
 
-@pytest.mark.parametrize("G,K,joint,active", [(20000, 5, 0.05, 0.5), (4096, 4, 0.3, 1.0)])
-def test_host_mirror_drives_series(engine, oracle, G, K, joint, active):
+@pytest.mark.parametrize("G,K,joint,active,threads", [(20000, 5, 0.05, 0.5, 1),
+                                                      (4096, 4, 0.3, 1.0, 1),
+                                                      (50000, 4, 0.1, 0.8, 16)])
+def test_host_mirror_drives_series(engine, oracle, G, K, joint, active, threads):
+    """threads = 16: each epoch's calls come from 16 threads at once (group slices); the
+    flush packs and delivers on its own worker threads (> 8192 changed groups)."""
     import torch
 
     from jraft_amd import drive
     s = W.host_series("C3", K, groups=G, joint_frac=joint, active=active)
-    committed, st = drive.drive_epochs(0, s)
+    committed, st = drive.drive_epochs(0, s, threads=threads)
     # (b) every group against the stateless K-epoch kernel with the same conf runs
     dev = torch.device("cuda:0")
     t = {k: torch.from_numpy(np.ascontiguousarray(s[k].view(np.int64) if s[k].dtype == np.uint64
@@ -82,3 +86,15 @@ def test_host_mirror_drives_series(engine, oracle, G, K, joint, active):
     assert st["states"][0] == G and (st["states"][1:] == 0).all()
     np.testing.assert_array_equal(st["h2d_bytes"], st["states"] * 96 + st["records"] * 8)
     np.testing.assert_array_equal(st["d2h_bytes"], 4 * 16 + st["changed"] * 8)  # segment counts + entries
+
+
+def test_flusher_latency_small():
+    """The background flusher under steady load (GroupBatch::startFlusher): every entry is
+    acked by all peers and then committed; onCommitted follows the quorum-completing ack
+    within the policy's delay plus one epoch."""
+    from jraft_amd import drive
+    r = drive.drive_latency(0, groups=4096, peers=3, threads=4, seconds=1.0, max_delay_us=500,
+                            max_dirty=1 << 14)
+    assert r["entries"] > 4096 and r["commits"] > 0 and r["samples"] > 0
+    assert r["flushes"] > 10
+    assert r["p50_us"] < 50_000, r
