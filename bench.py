@@ -38,8 +38,8 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 QUORUM_EPOCH_BUFFERS = 6
-LEGS = ("quorum", "table", "drive", "C2", "C5", "C1", "ae", "v2", "snapshot", "lease", "fanout",
-        "peak", "cpu")
+LEGS = ("quorum", "table", "drive", "C2", "C3K", "C5", "C1", "ae", "v2", "snapshot", "pinned",
+        "lease", "fanout", "peak", "cpu")
 
 
 def quorum_bytes_per_group(P: int) -> int:
@@ -510,13 +510,18 @@ def leg_table(ctx, args, G, pair_ms):
     eng, dev = ctx.eng, ctx.dev
     P = 5
     nb = 3
-    pristine, series = [], []
+    pristine, series, plain = [], [], []
     for e in range(nb):
         s = W.host_series("C3", 1, groups=G, joint_frac=0.01, seed=(W.SEED_BASE ^ 3) + 7919 * e)
         t = Table(eng, G, P)
         table_load(t, s)
         pristine.append(t)
         series.append(s)
+    for e in range(nb):  # the same shape with no conf change in any window (no flagged group)
+        s0 = W.host_series("C3", 1, groups=G, joint_frac=0.0, seed=(W.SEED_BASE ^ 3) + 7919 * e)
+        t = Table(eng, G, P)
+        table_load(t, s0)
+        plain.append(t)
     ctx.sync()
     work = Table(eng, G, P)
     from jraft_amd import _lib
@@ -541,6 +546,13 @@ def leg_table(ctx, args, G, pair_ms):
     last = (steps - 1) % nb
     words = work.gather_dev_list(changed, n)
     n_changed = len(words)
+    for i in range(steps):  # the table without flagged groups, timed the same way
+        work.copy_from(plain[i % nb])
+        ev[i][0].record(ctx.stream)
+        work.epoch_dev(changed, n)
+        ev[i][1].record(ctx.stream)
+    ctx.sync()
+    t_plain_ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
     # the stateless pair kernel on the same inputs (CSR run table, flagged groups), same timing
     s = series[last]
     d = {k: to_dev(s[k] if k != "match" else s["match"][0], dev)
@@ -593,12 +605,14 @@ def leg_table(ctx, args, G, pair_ms):
                                          s["run_start"][idx], s["run_conf"][idx], chunk=1024)
         ok = ok and bool(np.array_equal(got[sub], ce))
     alg = G * (8 * P + 32) + n_changed * 16
-    for t in pristine:
+    for t in pristine + plain:
         t.close()
     work.close()
     return {"workload": f"C3 resident table: {G} groups x {P} peers, joint, 1% with a conf "
                         f"change in the pending window; one epoch, in place",
             "kernel_ms": t_ms, "changed_groups": n_changed,
+            "kernel_ms_no_conf_change": t_plain_ms,
+            "flagged_over_no_conf_change": t_ms / t_plain_ms,
             "stateless_pair_kernel_ms_same_inputs": p_ms,
             "stateless_pair_kernel_ms_no_conf_change": pp_ms,
             "table_over_pair": t_ms / p_ms,
@@ -617,16 +631,19 @@ def leg_drive(ctx, args, G):
     mirror's BallotBox API (appendPendingTask / commitAt) over the resident table, one
     GroupBatch::flush() per epoch (libjraft_drive.so): changed records from page-locked
     buffers -> H2D -> apply + epoch kernels -> D2H of the changed commits -> closures /
-    onCommitted.  Reported per steady epoch (epochs 1..K-1; epoch 0 loads every group)."""
+    onCommitted.  Reported per steady epoch (epochs 1..K-1; epoch 0 loads every group), with
+    the epoch's API calls made by 1 and by 16 threads (contiguous group slices), and the
+    end-to-end rate including those calls.  Then the ack -> onCommitted latency under the
+    background flusher's policy, with 16 producer threads."""
     import torch
 
     from jraft_amd import drive
     from jraft_amd import workloads as W
     K = 6
     out = {}
-    for active in (1.0, 0.1):
+    for active, threads in ((1.0, 1), (1.0, 16), (0.1, 16)):
         s = W.host_series("C3", K, groups=G, joint_frac=0.01, active=active)
-        committed, st = drive.drive_epochs(ctx.dev.index, s)
+        committed, st = drive.drive_epochs(ctx.dev.index, s, threads=threads)
         ok = None
         if active == 1.0:  # every group against the stateless K-epoch kernel
             d = {k: to_dev(s[k], ctx.dev) for k in ("match", "last_appended", "pending_index",
@@ -642,25 +659,38 @@ def leg_drive(ctx, args, G):
             del d, c, cs
         sl = slice(1, K)
         f = float(np.mean(st["flush_ms"][sl]))
+        api = float(np.mean(st["api_ms"][sl]))
         pcie = float(np.mean(st["h2d_bytes"][sl] + st["d2h_bytes"][sl]))
-        out[f"active_{int(active * 100)}pct"] = {
+        out[f"active_{int(active * 100)}pct_{threads}_threads"] = {
+            "api_threads": threads,
             "flush_ms": f, "pack_ms": float(np.mean(st["pack_ms"][sl])),
             "device_ms": float(np.mean(st["device_ms"][sl])),
             "deliver_ms": float(np.mean(st["deliver_ms"][sl])),
-            "decisions_per_s": G / (f * 1e-3),
+            "api_ms_per_epoch": api,
+            "api_calls_per_epoch": float(np.mean(st["api_calls"][sl])),
+            "end_to_end_ms_per_epoch": api + f,
+            "decisions_per_s_end_to_end": G / ((api + f) * 1e-3),
+            "decisions_per_s_flush_only": G / (f * 1e-3),
+            "api_share_of_end_to_end": api / (api + f),
             "records_per_epoch": float(np.mean(st["records"][sl])),
             "changed_per_epoch": float(np.mean(st["changed"][sl])),
             "pcie_bytes_per_epoch": pcie, "pcie_GBps": pcie / (f * 1e-3) / 1e9,
-            "api_calls_per_epoch": float(np.mean(st["api_calls"][sl])),
-            "api_ms_per_epoch": float(np.mean(st["api_ms"][sl])),
             "first_epoch_flush_ms": float(st["flush_ms"][0]),
             "bit_exact_vs_stateless_kernel": ok}
+    lat = drive.drive_latency(ctx.dev.index, G, 5, 16, 2.0, 1000, 1 << 16)
+    lat["policy"] = {"maxDelayUs": 1000, "maxDirtyGroups": 1 << 16}
+    lat["how"] = ("16 threads loop over their slices of the groups: appendPendingTask of one "
+                  "entry, then commitAt of it by each of the 5 peers; GroupBatch::startFlusher "
+                  "flushes when the oldest unflushed change is 1 ms old or 65536 groups changed; "
+                  "latency = onCommitted(c) time - time of entry c's last ack")
+    lat["commits_per_s"] = lat["commits"] / lat["seconds"]
+    lat["api_calls_per_s"] = (lat["entries"] + lat["acks"]) / lat["seconds"]
     return {"workload": f"C3 through the C++ BallotBox host mirror: {G} groups x 5 peers, joint, "
                         f"1% with a conf change in the pending window, {K} epochs",
             "how": "flush = pack changed records + H2D (pinned) + apply + epoch kernels + D2H of "
                    "the changed commits + closures / onCommitted; api = the appendPendingTask / "
-                   "commitAt calls before it (host-side, not part of flush)",
-            **out}
+                   "commitAt calls of the epoch (made before the flush, from `api_threads` threads)",
+            **out, "ack_to_onCommitted_latency": lat}
 
 
 def leg_c2(ctx, args):
@@ -698,8 +728,9 @@ def leg_c2(ctx, args):
         c2k_launch()
     k_ms, _ = ctx.timed(c2k_step)
     ok = None
-    if ctx.oracle_checks:  # the oracle on 256 groups, all KE epochs, state carried
+    if ctx.oracle_checks:
         import jraft_oracle as O
+    if ctx.oracle_checks:  # the oracle on 256 groups, all KE epochs, state carried
         sub = np.random.default_rng(2).choice(G2, 256, replace=False)
         pi = ser["pending_index"][sub].copy()
         lc = ser["last_committed"][sub].copy()
@@ -715,6 +746,32 @@ def leg_c2(ctx, args):
     # per group-epoch: match 8P + lastAppended 8 read, committed 8 + status 1 written (41 B at
     # P = 3); pendingIndex / lastCommitted / conf once per group
     alg = G2 * KE * 41 + G2 * 24
+    # 256 epochs per launch: the kernel's ramp and tail spread over 4x the work
+    KL = 256
+    serl = W.quorum_epoch_series("C2", KL)
+    serl_d = {k: to_dev(v, dev) for k, v in serl.items()}
+    klc = torch.empty((KL, G2), dtype=torch.int64, device=dev)
+    kls = torch.empty((KL, G2), dtype=torch.uint8, device=dev)
+    c2l_launch = eng.quorum_epochs_launcher(serl_d["match"], serl_d["pending_index"],
+                                            serl_d["last_appended"], serl_d["last_committed"],
+                                            serl_d["conf"], klc, kls)
+    kl_ms, _ = ctx.timed(lambda i: c2l_launch())
+    ok_l = None
+    if ctx.oracle_checks:  # 64 groups, all KL epochs, state carried
+        sub = np.random.default_rng(3).choice(G2, 64, replace=False)
+        pi = serl["pending_index"][sub].copy()
+        lc = serl["last_committed"][sub].copy()
+        got = klc.cpu().numpy()
+        ok_l = True
+        for k in range(KL):
+            ce, _, _ = O.quorum_epoch_replay(serl["match"][k][:, sub], pi,
+                                             serl["last_appended"][k][sub], lc,
+                                             serl["conf"][sub], chunk=1024)
+            pi = np.where((pi != 0) & (ce > lc), ce + 1, pi)
+            lc = ce
+            ok_l = ok_l and bool(np.array_equal(got[k, sub], ce))
+    alg_l = G2 * KL * 41 + G2 * 24
+    del serl_d, klc, kls
     return {"workload": "C2: 10k groups x 3 peers x 1k pending (configs[1])",
             "decisions_per_s": G2 / (one_ms * 1e-3), "kernel_ms": one_ms,
             "entry_ballots_per_s": G2 * 1024 / (one_ms * 1e-3),
@@ -722,7 +779,125 @@ def leg_c2(ctx, args):
                                "decisions_per_s": G2 * KE / (k_ms * 1e-3),
                                "roofline": roofline(alg, k_ms, kernel="quorum_epochs_kernel<3>",
                                                     **pmc_traffic("C2", "quorum_epochs_kernel<3,")),
-                               "bit_exact_vs_oracle_256_groups": ok}}
+                               "bit_exact_vs_oracle_256_groups": ok},
+            "batched_epochs_256": {"epochs_per_launch": KL, "kernel_ms": kl_ms,
+                                   "decisions_per_s": G2 * KL / (kl_ms * 1e-3),
+                                   "roofline": roofline(alg_l, kl_ms, kernel="quorum_epochs_kernel<3>",
+                                                        **pmc_traffic("C2", "quorum_epochs_kernel<3,")),
+                                   "bit_exact_vs_oracle_64_groups": ok_l}}
+
+
+def leg_c3k(ctx, args, G):
+    """C3 through the K-epochs-per-launch kernel (jrq_quorum_epochs_dev): K successive epochs of
+    the 1M groups x 5 peers, joint, state carried between them as BallotBox carries it, in one
+    launch -- the headline epoch's launch ramp and tail spread over K epochs."""
+    import torch
+
+    from jraft_amd import workloads as W
+    eng, dev = ctx.eng, ctx.dev
+    K = 8
+    ser = W.quorum_epoch_series("C3", K, groups=G)
+    d = {k: to_dev(v, dev) for k, v in ser.items()}
+    kc = torch.empty((K, G), dtype=torch.int64, device=dev)
+    ks = torch.empty((K, G), dtype=torch.uint8, device=dev)
+    launch = eng.quorum_epochs_launcher(d["match"], d["pending_index"], d["last_appended"],
+                                        d["last_committed"], d["conf"], kc, ks)
+    ms, _ = ctx.timed(lambda i: launch())
+    ok = None
+    if ctx.oracle_checks:  # the oracle on 2048 groups, all K epochs, state carried
+        import jraft_oracle as O
+        sub = np.random.default_rng(4).choice(G, 2048, replace=False)
+        pi = ser["pending_index"][sub].copy()
+        lc = ser["last_committed"][sub].copy()
+        got, gst = kc.cpu().numpy(), ks.cpu().numpy()
+        ok = True
+        for k in range(K):
+            ce, se, _ = O.quorum_epoch_replay(ser["match"][k][:, sub], pi,
+                                              ser["last_appended"][k][sub], lc, ser["conf"][sub],
+                                              chunk=1024)
+            pi = np.where((pi != 0) & (ce > lc), ce + 1, pi)
+            lc = ce
+            ok = ok and bool(np.array_equal(got[k, sub], ce)) and bool(np.array_equal(gst[k, sub], se))
+    P = 5
+    # per group-epoch: match 8P + lastAppended 8 read, committed 8 + status 1 written; per
+    # group pendingIndex / lastCommitted / conf once
+    alg = G * K * (8 * P + 17) + G * 24
+    del d, kc, ks
+    return {"workload": f"C3: {G} groups x {P} peers, joint, {K} successive epochs per launch",
+            "epochs_per_launch": K, "kernel_ms": ms,
+            "decisions_per_s": G * K / (ms * 1e-3),
+            "roofline": roofline(alg, ms, kernel="quorum_epochs_kernel<5>",
+                                 bytes_note="8P+17 B per group-epoch + 24 B per group",
+                                 **pmc_traffic("C3K", "quorum_epochs_kernel<5,")),
+            "bit_exact_vs_oracle_2048_groups": ok}
+
+
+def leg_pinned(ctx, args, c5state):
+    """The host-pointer entry points from caller memory registered with jrq_host_register (a
+    JNI host's pinned DirectByteBuffers): LogEntry checksum + verify of the C5
+    batch (1 GiB) and the C1 batch (256 MB) with every input and output in registered memory,
+    PCIe transfers included; beside them the same calls from unregistered memory (the engine's
+    pinned bounce chunks).  The reference copies a direct buffer into a new byte[] before
+    checksumming it (CrcUtil.java:65-80)."""
+    import ctypes
+
+    from jraft_amd import _lib
+    from jraft_amd import workloads as W
+    eng = ctx.eng
+    L = _lib.load()
+    d, eb, expected, flip, out = c5state
+    c1 = W.CONFIGS["C1"]
+    e1 = W.entry_batch(c1["pending"], c1["entry_bytes"], seed=W.SEED_BASE ^ 1)
+    res = {}
+    for name, e, exp in (("C5", eb, expected ^ flip.astype(np.uint64)), ("C1", e1, None)):
+        n = len(e["offsets"]) - 1
+        arrs = {"payload": e["payload"], "etype": e["etype"], "index": e["index"], "term": e["term"],
+                "offsets": e["offsets"]}
+        if exp is not None:
+            arrs["expected"] = np.ascontiguousarray(exp)
+        row = {}
+        for pinned in (True, False):
+            regs = []
+            if pinned:
+                for a in arrs.values():
+                    if L.jrq_host_register(ctypes.c_void_p(a.ctypes.data), a.nbytes) == 0:
+                        regs.append(a)
+            try:
+                def call():
+                    return eng.logentry_checksum_batch(arrs["etype"], arrs["index"], arrs["term"],
+                                                       None, arrs["payload"], arrs["offsets"],
+                                                       expected=arrs.get("expected"))
+                call()
+                walls = []
+                for _ in range(max(3, min(10, args.steps // 5))):
+                    t0 = time.perf_counter()
+                    r = call()
+                    walls.append(time.perf_counter() - t0)
+                wall = float(np.median(walls))
+            finally:
+                for a in regs:
+                    L.jrq_host_unregister(ctypes.c_void_p(a.ctypes.data))
+            got = r[0] if isinstance(r, tuple) else r
+            ok = None
+            if ctx.oracle_checks:
+                if name == "C5":
+                    ok = bool(np.array_equal(got, expected)) and bool(np.array_equal(r[1].astype(bool), flip))
+                else:
+                    import jraft_oracle as O
+                    ok = bool(np.array_equal(got[:4096], O.logentry_checksum_batch(
+                        e["etype"][:4096], e["index"][:4096], e["term"][:4096], None, e["payload"],
+                        e["offsets"][:4097])))
+            pay = int(e["offsets"][-1] - e["offsets"][0])
+            h2d = pay + sum(a.nbytes for k, a in arrs.items() if k != "payload")
+            row["registered" if pinned else "unregistered"] = {
+                "ms_per_call": wall * 1e3, "GBps_payload_pcie_inclusive": pay / wall / 1e9,
+                "h2d_bytes": h2d, "registered_arrays": len(regs), "bit_exact_vs_oracle": ok}
+        res[name] = {"entries": n, "payload_bytes": int(e["offsets"][-1]), **row}
+    return {"how": "jrq_logentry_checksum_batch (host variant: H2D of every input, the fixed-size "
+                   "kernel, D2H of the results, synchronised) timed by wall clock per call; "
+                   "registered = every caller array jrq_host_register'ed first (DMA straight from "
+                   "it), unregistered = through the engine's 8 MiB pinned bounce chunks",
+            **res}
 
 
 def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
@@ -842,9 +1017,18 @@ def leg_ae(ctx, args, c5state):
         ok = bool(np.array_equal(ae_out.cpu().numpy().view(np.uint64), expected)) and \
             bool((ae_first.cpu().numpy() == 0).all())  # entry 0 of each request is flipped
     pay = n * c5["entry_bytes"]
+    # payload + per entry term 8, type 1, data_len 8, stored checksum 8, checksum out 8, corrupt
+    # 1 + per request req_off 4, prevLogIndex 8, first corrupt 4 (scratch offsets / indices not
+    # counted)
+    alg = pay + 34 * n + 16 * R + 4
     return {"workload": f"{R} AppendEntries requests x 1024 EntryMeta x 16 KiB (C5 payload)",
             "GBps_payload": pay / (ms * 1e-3) / 1e9, "ms_per_batch": ms,
-            "bit_exact_vs_oracle": ok}
+            "bit_exact_vs_oracle": ok,
+            "roofline": roofline(alg, ms, kernel="AppendEntries verify (scan + segment-walk CRC "
+                                                 "+ finish + first-corrupt)",
+                                 **pmc_traffic("ae", "ae_block_sums", "ae_scan_sums", "ae_meta",
+                                               "crc64_rounds_kernel<512u, false>",
+                                               "crc64_finish_kernel<true>", "ae_first_corrupt"))}
 
 
 def leg_v2(ctx, args, c5state):
@@ -1179,9 +1363,11 @@ def main():
         line["end_to_end_host_mirror"] = leg_drive(ctx, args, G)
     if "C2" in legs:
         line["C2"] = leg_c2(ctx, args)
+    if "C3K" in legs:
+        line["C3_k_epochs"] = leg_c3k(ctx, args, G)
     extras = {}
     c5state = None
-    if legs & {"C5", "ae", "v2", "snapshot"}:
+    if legs & {"C5", "ae", "v2", "snapshot", "pinned"}:
         crc, c5_step, c5state = leg_c5(ctx, args, barrier, max_over_ranks,
                                        time_it="C5" in legs)
         if "C5" in legs:
@@ -1193,6 +1379,8 @@ def main():
         extras["v2_decode_verify"] = leg_v2(ctx, args, c5state)
     if "snapshot" in legs:
         extras["snapshot_stream_crc64"] = leg_snapshot(ctx, args, c5state)
+    if "pinned" in legs:
+        line["pinned_host_payload"] = leg_pinned(ctx, args, c5state)
     c5state = None
     if "C1" in legs:
         line["C1"] = leg_c1(ctx, args)

@@ -849,8 +849,10 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
 // of results as scattered 8-B stores and re-read them in the finish kernel.
 // kStarts (V2 decode): entry i starts at payload + starts[i] (non-decreasing, any byte
 // alignment: buffer loads take unaligned offsets), k and EL come from the device words
-// gate[0..1] written by v2_uniform (gate[3]: the payload's end offset); k == 0 means the
-// segment walk takes the batch instead.
+// gate[0..1] written by v2_parse (gate[3]: the payload's end offset); k == 0 means the
+// segment walk takes the batch instead.  With kLogEntry the record's partial checksum (type ^
+// crc(LogId) ^ peers, from v2_parse) arrives in peer_xor: out = partial ^ crc(data) and the
+// verify compare, as v2_finish does on the segment-walk path.
 template <bool kLogEntry, bool kStarts>
 __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
@@ -967,9 +969,11 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     uint32_t f_type = 0, f_has = 0;
     uint64_t f_index = 0, f_term = 0, f_peer = 0, f_exp = 0;
     if (kLogEntry) {
-      f_type = a.type[e];
-      f_index = static_cast<uint64_t>(a.index[e]);
-      f_term = static_cast<uint64_t>(a.term[e]);
+      if (!kStarts) {
+        f_type = a.type[e];
+        f_index = static_cast<uint64_t>(a.index[e]);
+        f_term = static_cast<uint64_t>(a.term[e]);
+      }
       f_peer = p_peer[e & m_peer];
       f_exp = p_exp[e & m_exp];
       f_has = p_has[e & m_has];
@@ -1028,11 +1032,14 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     }
     const bool last = piece == K - 1u;  // the lane holding the entry's CRC
     if (kLogEntry) {  // LogEntry.checksum(): type ^ LogId.checksum() ^ peers ^ crc64(data)
-      RState lid{0u, 0u};
-      const uint64_t bi = bswap64(f_index), bt = bswap64(f_term);
-      tb.step8(lid, static_cast<uint32_t>(bi), static_cast<uint32_t>(bi >> 32), lds);
-      tb.step8(lid, static_cast<uint32_t>(bt), static_cast<uint32_t>(bt >> 32), lds);
-      c ^= static_cast<uint64_t>(f_type) ^ crc_value(lid) ^ f_peer;
+      if (!kStarts) {
+        RState lid{0u, 0u};
+        const uint64_t bi = bswap64(f_index), bt = bswap64(f_term);
+        tb.step8(lid, static_cast<uint32_t>(bi), static_cast<uint32_t>(bi >> 32), lds);
+        tb.step8(lid, static_cast<uint32_t>(bt), static_cast<uint32_t>(bt >> 32), lds);
+        c ^= static_cast<uint64_t>(f_type) ^ crc_value(lid);
+      }
+      c ^= f_peer;
       if (ver && live && last) a.corrupt[e] = static_cast<uint8_t>((m_has ? f_has != 0 : true) && f_exp != c);
     }
     if (live && last) a.out[e] = c;
@@ -1045,7 +1052,10 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
 // < 2^32, (entry_bytes / fixed_k) % 256 == 0.
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64_fixed(
     JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {
-  if (args->starts != nullptr)  // plain CRCs at given starts, gated on the device (V2 decode)
+  if (args->starts != nullptr && log_entry)  // V2 decode: partial ^ crc(data), gated on the device
+    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<true, true>), dim3(grid), dim3(jrq::kCrcBlock), 0,
+                       stream, *args);
+  else if (args->starts != nullptr)  // plain CRCs at given starts, gated on the device
     hipLaunchKernelGGL((jrq::crc64_fixed_kernel<false, true>), dim3(grid), dim3(jrq::kCrcBlock), 0,
                        stream, *args);
   else if (log_entry)

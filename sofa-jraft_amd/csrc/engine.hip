@@ -30,7 +30,6 @@ extern "C" hipError_t jrq_launch_ae_meta(const JrqAeArgs* a, hipStream_t stream)
 extern "C" hipError_t jrq_launch_lease(const JrqLeaseArgs* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_fanout(const JrqFanoutArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_v2_parse(const JrqV2Args* a, hipStream_t stream);
-extern "C" hipError_t jrq_launch_v2_gate(const JrqV2Args* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_v2_finish(const JrqV2Args* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_first_corrupt(const JrqAeArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_table_update(const JrqTableArgs* a, const JrqGroupState* states,
@@ -66,6 +65,7 @@ struct jrq_engine {
   uint32_t* cnt = nullptr;    // straddler counters
   uint64_t* pieces = nullptr; // per-segment straddler pieces: [2][scratch_len]
   uint32_t* fan_ctr = nullptr; // commit fan-out {listed sum, blocks done}, zero between launches
+  uint64_t* v2_gate = nullptr; // V2 decode gate {k, L, bad, end, arrivals}; arrivals zero between launches
   uint32_t scratch_len = 0;
   int crc_grid = 0;
   // Test / A-B overrides, set only through jrq_debug_set (never from the environment):
@@ -385,8 +385,10 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   try_hip(hipMalloc(&e->cnt, slots * 4), "hipMalloc(cnt)");
   try_hip(hipMalloc(&e->pieces, static_cast<size_t>(e->scratch_len) * 16), "hipMalloc(pieces)");
   try_hip(hipMalloc(&e->fan_ctr, 16), "hipMalloc(fan_ctr)");
+  try_hip(hipMalloc(&e->v2_gate, 64), "hipMalloc(v2_gate)");
   if (rc == JRQ_OK) {
     try_hip(hipMemset(e->fan_ctr, 0, 16), "zero fan_ctr");
+    try_hip(hipMemset(e->v2_gate, 0, 64), "zero v2_gate");
     try_hip(hipMemcpy(e->slice, slice.data(), slice.size() * 8, hipMemcpyHostToDevice), "upload slice");
     try_hip(hipMemcpy(e->shift, shift.data(), shift.size() * 8, hipMemcpyHostToDevice), "upload shift");
     try_hip(hipMemcpy(e->xinv, xinv.data(), xinv.size() * 8, hipMemcpyHostToDevice), "upload xinv");
@@ -420,6 +422,7 @@ void jrq_destroy(jrq_engine* e) {
   if (e->cnt) (void)hipFree(e->cnt);
   if (e->pieces) (void)hipFree(e->pieces);
   if (e->fan_ctr) (void)hipFree(e->fan_ctr);
+  if (e->v2_gate) (void)hipFree(e->v2_gate);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
 }
@@ -1106,11 +1109,9 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
   if ((rc = ensure_stage(e, 21, static_cast<size_t>(N) * 8, &partial))) return rc;
   if ((rc = ensure_stage(e, 22, (static_cast<size_t>(N) + 2) * 8, &off2))) return rc;
   if ((rc = ensure_stage(e, 23, (static_cast<size_t>(N) + 1) * 8, &crc2))) return rc;
-  void* edges;  // per record: header CRC, trailer CRC, lengths
-  if ((rc = ensure_stage(e, 24, static_cast<size_t>(N) * 24, &edges))) return rc;
-  void *gate, *crcd;  // the fixed-size data CRC path: {k, L, bad, end, count}, per-record data CRCs
-  if ((rc = ensure_stage(e, 25, 40, &gate))) return rc;
-  if ((rc = ensure_stage(e, 26, static_cast<size_t>(N) * 8, &crcd))) return rc;
+  void *lens, *blk;  // per record: header / trailer lengths; per 256 records: parse summaries
+  if ((rc = ensure_stage(e, 24, static_cast<size_t>(N) * 8, &lens))) return rc;
+  if ((rc = ensure_stage(e, 25, (static_cast<size_t>(N) + 255) / 256 * 32, &blk))) return rc;
   JrqV2Args v{};
   v.rec = rec;
   v.off = off;
@@ -1131,27 +1132,29 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
   v.partial = static_cast<uint64_t*>(partial);
   v.off2 = static_cast<uint64_t*>(off2);
   v.crc2 = static_cast<const uint64_t*>(crc2);
-  v.hcrc = static_cast<uint64_t*>(edges);
-  v.tcrc = v.hcrc + N;
-  v.lens = v.tcrc + N;
-  v.gate = static_cast<uint64_t*>(gate);
-  v.crc_data = static_cast<const uint64_t*>(crcd);
+  v.lens = static_cast<uint64_t*>(lens);
+  v.gate = e->v2_gate;
+  v.blk = static_cast<uint64_t*>(blk);
   // (the fixed-size path hashes from the 64-B line of each data start: records 64-B aligned)
   v.lanes = (reinterpret_cast<uintptr_t>(rec) & 63u) ? ~0ull
                                                      : static_cast<uint64_t>(e->crc_grid) * jrq::kCrcBlock;
-  JRQ_HIP(e, jrq_launch_v2_parse(&v, e->stream));
-  JRQ_HIP(e, jrq_launch_v2_gate(&v, e->num_cus, e->stream));
+  JRQ_HIP(e, jrq_launch_v2_parse(&v, e->stream));  // (its last block writes the gate)
   // every record with the same data length (the common case: fixed-size commands): the data
-  // ranges alone, k lanes per record (crc64_fixed_kernel at the data starts); the gate words
-  // on the device pick this or the segment walk below, each kernel of the other path returns
+  // ranges alone, k lanes per record (crc64_fixed_kernel at the data starts), finished in place
+  // (computed = partial ^ crc(data), corrupt); the gate words on the device pick this or the
+  // segment walk below, each kernel of the other path returns at once
   {
     JrqCrcArgs f{};
     f.payload = rec;
     f.starts = v.data_off;
     f.gate = v.gate;
     f.n = N;
-    f.out = static_cast<uint64_t*>(crcd);
-    if ((rc = crc_fixed_dispatch(e, f, 0))) return rc;
+    f.out = computed;
+    f.peer_xor = v.partial;  // type ^ crc(LogId) ^ peers, from v2_parse
+    f.expected = stored;
+    f.has = has_checksum;
+    f.corrupt = corrupt;
+    if ((rc = crc_fixed_dispatch(e, f, 1))) return rc;
   }
   // otherwise one range per record from its data start (the leading header first): one
   // streaming pass over the records, one entry boundary per record (v2_finish recovers the
@@ -1232,6 +1235,7 @@ struct jrq_table {
   DevBuf st_stage, rec_stage, changed_stage;  // staging of the host variants
   uint32_t* n_dev = nullptr;  // device count word of the host-variant epoch
   uint32_t* n_host = nullptr; // pinned
+  size_t state_bytes = 0;     // the rows at the start of mem (jrq_table_copy)
 };
 
 namespace {
@@ -1273,7 +1277,12 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   auto* t = new jrq_table();
   t->e = e;
   const uint64_t ld = (static_cast<uint64_t>(G) + 63) & ~63ull;  // pairs + 512-B rows
-  const uint64_t words = ld * (P + 4 + 2 * (jrq::kTableMaxRuns - 1));
+  // rows (the state jrq_table_copy copies): match[P], pi, la, lc, conf, xstart[3], xconf[3],
+  // the flagged lists flag_list[blocks * 2048] + flag_cnt[blocks] (u32); then the control
+  // words: ctr[16], invalid
+  const uint64_t blocks = (G + jrq::kTableBlockGroups - 1) / jrq::kTableBlockGroups;
+  const uint64_t flag_words = (blocks * (jrq::kTableBlockGroups + 1) + 1) / 2;
+  const uint64_t words = ld * (P + 4 + 2 * (jrq::kTableMaxRuns - 1)) + flag_words;
   const size_t bytes = words * 8 + 8 * jrq::kTableSegments + 64;
   if (hipMalloc(&t->mem, bytes) != hipSuccess || hipMemset(t->mem, 0, bytes) != hipSuccess ||
       hipMalloc(&t->n_dev, 4 * jrq::kTableSegments) != hipSuccess ||
@@ -1293,8 +1302,11 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   a.conf = reinterpret_cast<uint64_t*>(a.lc + ld);
   a.xstart = reinterpret_cast<int64_t*>(a.conf + ld);
   a.xconf = reinterpret_cast<uint64_t*>(a.xstart + ld * (jrq::kTableMaxRuns - 1));
-  a.ctr = reinterpret_cast<unsigned long long*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
+  a.flag_list = reinterpret_cast<uint32_t*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
+  a.flag_cnt = a.flag_list + blocks * jrq::kTableBlockGroups;
+  a.ctr = reinterpret_cast<unsigned long long*>(w + words);
   a.invalid = reinterpret_cast<uint32_t*>(a.ctr + jrq::kTableSegments);
+  t->state_bytes = words * 8;
   a.seg_cap = jrq_table_seg_cap(G);
   a.ld = ld;
   a.G = G;
@@ -1469,8 +1481,7 @@ int jrq_table_copy(jrq_table* dst, const jrq_table* src) {
   if (src->a.G != dst->a.G || src->a.P != dst->a.P || src->a.ld != dst->a.ld)
     return fail(e, JRQ_E_INVALID, "table shapes differ");
   DeviceGuard guard(e->device);
-  const size_t bytes = dst->a.ld * (dst->a.P + 4 + 2 * (jrq::kTableMaxRuns - 1)) * 8;
-  JRQ_HIP(e, hipMemcpyAsync(dst->mem, src->mem, bytes, hipMemcpyDeviceToDevice, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(dst->mem, src->mem, dst->state_bytes, hipMemcpyDeviceToDevice, e->stream));
   return JRQ_OK;
 }
 

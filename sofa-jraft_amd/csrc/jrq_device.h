@@ -174,12 +174,11 @@ struct JrqV2Args {
   uint64_t* partial;       // scratch [n]
   uint64_t* off2;          // scratch [n+2]: record i's range = [off2[i+1], off2[i+2])
   const uint64_t* crc2;    // scratch [n+1] (CRC of the ranges; range 0 = the leading header)
-  uint64_t* hcrc;          // scratch [n] CRC of each record's bytes before its data
-  uint64_t* tcrc;          // scratch [n] CRC of each record's bytes after its data
   uint64_t* lens;          // scratch [n] header length << 32 | trailer length
-  uint64_t* gate;          // scratch [5]: {k, L, bad, end, count} -- the data CRCs by crc64_fixed_kernel
-                           // (k lanes per record) when every record decoded with data length L
-  const uint64_t* crc_data;  // scratch [n]: the data CRCs of that path
+  uint64_t* gate;          // engine words [5]: {k, L, bad, end, arrivals} -- the data CRCs by
+                           // crc64_fixed_kernel (k lanes per record) when every record decoded with
+                           // data length L; arrivals is zero between launches
+  uint64_t* blk;           // scratch [4 * ceil(n / 256)]: v2_parse's per-block summaries
   uint64_t lanes;          // lanes of the CRC grid (crc64_fixed_kernel)
 };
 
@@ -234,6 +233,9 @@ struct JrqTableArgs {
   uint32_t* n_changed;   // [kTableSegments] out
   uint32_t seg_cap;      // entries per list segment
   uint8_t* status;       // [G] out, nullable
+  uint32_t* flag_list;   // [blocks * kTableBlockGroups] per epoch workgroup b: its groups
+                         // flagged JRQ_CONF_RUNS, from b * kTableBlockGroups
+  uint32_t* flag_cnt;    // [blocks] how many
 };
 
 // One group header as the ABI carries it (include/jrq.h jrq_group_state).

@@ -40,7 +40,7 @@ __device__ __forceinline__ void table_commit_one(const JrqTableArgs& t, uint32_t
 constexpr uint32_t kTableBlock = kTableBlockGroups / 2;
 
 // The run walk of one flagged group, run r of it on lane r of an aligned lane quad (the table
-// holds at most kTableMaxRuns = 4 runs): each lane reloads the group (the quad's loads of it
+// holds at most kTableMaxRuns = 4 runs): each lane loads the group (the quad's loads of it
 // coalesce) and its run's start, next start and conf word, all in one batch; the quad then
 // max-reduces the runs' candidates.  Returns the group's candidate (kI64Min: none) and status.
 template <int P>
@@ -69,22 +69,41 @@ __device__ __forceinline__ int64_t table_run_lane(const JrqTableArgs& t, uint32_
   return run_candidate<P>(m, cw, s, e < la ? e : la, st);
 }
 
+// One epoch over every group of the table.  1024-thread workgroups of 2048 groups (two per
+// lane, 16-B loads), 2 resident per CU.
+// Groups with a conf change inside their pending window (JRQ_CONF_RUNS) are skipped by the
+// single-conf pass and decided from the table's flagged lists (table_flags_kernel keeps them:
+// they change only with group headers): workgroup b's flagged groups, in its own slot range of
+// flag_list, are split over its 16 waves -- at 1 % flagged one or two groups per wave, four
+// lanes each (one conf run per lane).  The wave loads its slice's list entries before the
+// single-conf loads and walks the groups after its single-conf decisions: no LDS list of
+// flagged groups, no workgroup barrier in front of them, and a workgroup lists only its own
+// groups (at most 2048: the list segments' capacity).
+// The one barrier left is the compaction's: list entries are staged per wave in LDS, and one
+// 64-bit atomic per workgroup ({done << 32 | entries}) on its segment's counter (workgroup b
+// -> segment b % kTableSegments: same-address atomics serialise, ~14 ns each,
+// tools/table_probe.hip) reserves its slice; the last workgroup of a segment publishes the
+// segment's count and re-zeroes the counter.
 template <int P>
 __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
   constexpr uint32_t kWaves = kTableBlock / 64;
-  __shared__ uint32_t wave_cnt[kWaves];   // fast-path commits per wave
-  __shared__ uint32_t wave_def[kWaves];   // flagged groups per wave
-  __shared__ uint32_t deferred[kWaves][128];
-  __shared__ uint64_t staged[kWaves][128];  // fast-path list entries, wave-compacted
-  __shared__ uint64_t walk_staged[kTableBlockGroups];  // run-walk list entries
-  __shared__ uint32_t walk_n;
-  __shared__ uint32_t blk_base, blk_walk;
+  constexpr uint32_t kStage = 2 * 64 + kTableBlockGroups / kWaves;  // fast path + walked
+  __shared__ uint32_t wave_cnt[kWaves];
+  __shared__ uint64_t staged[kWaves][kStage];
+  __shared__ uint32_t blk_base;
   const uint32_t pairs = (t.G + 1) >> 1;  // ld covers the pad group of an odd G (not a leader)
   const uint32_t tt = blockIdx.x * kTableBlock + threadIdx.x;
   const uint32_t g = tt << 1;
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
-  bool c0 = false, c1 = false, f0 = false, f1 = false;
+  // this wave's slice [fs0, fs1) of the workgroup's flagged list, four lanes per group, 16
+  // groups per pass
+  const uint32_t nflag = __builtin_amdgcn_readfirstlane(t.flag_cnt[blockIdx.x]);
+  const uint32_t fbase = blockIdx.x * kTableBlockGroups;
+  const uint32_t fs0 = fbase + nflag * w / kWaves, fs1 = fbase + nflag * (w + 1) / kWaves;
+  const uint32_t fi = fs0 + (lane >> 2);
+  uint32_t h0 = fi < fs1 ? t.flag_list[fi] : 0u;  // the first pass's group, loaded up front
+  bool c0 = false, c1 = false;
   uint64_t e0 = 0, e1 = 0;
   if (tt < pairs) {
     const i64x2 pr = tld2(t.pi + g);
@@ -96,8 +115,8 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
     for (int p = 0; p < P; ++p) mv[p] = tld2(t.match + static_cast<size_t>(p) * t.ld + g);
     const int64_t pi0 = pr.x == kPiFollowsLc ? lc.x + 1 : pr.x;
     const int64_t pi1 = pr.y == kPiFollowsLc ? lc.y + 1 : pr.y;
-    f0 = static_cast<uint64_t>(cw.x) >> 63;
-    f1 = static_cast<uint64_t>(cw.y) >> 63;
+    const bool f0 = static_cast<uint64_t>(cw.x) >> 63;
+    const bool f1 = static_cast<uint64_t>(cw.y) >> 63;
     int64_t m0[P], m1[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -108,8 +127,7 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
     uint8_t s0, s1;
     decide_single<P>(pi0, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
     decide_single<P>(pi1, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
-    // a group with a conf change inside its pending window (JRQ_CONF_RUNS) is decided again
-    // in the second phase with its runs; its single-conf result here is discarded
+    // a flagged group is decided by the walk (its single-conf result here is discarded)
     c0 = !f0 && o0 > lc.x;  // decide_single returns lastCommitted unless a commit happened
     c1 = !f1 && o1 > lc.y;
     if (c0 && c1) {
@@ -125,7 +143,7 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
       if (c0) table_commit_one(t, g, pr.x, o0);
       if (c1) table_commit_one(t, g + 1, pr.y, o1);
     }
-    if (t.status) {  // a flagged group's status is written by the run walk
+    if (t.status) {  // a flagged group's status is written by the walk
       if (g + 1 < t.G && !f0 && !f1)
         __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
                                     reinterpret_cast<uint16_t*>(t.status + g));
@@ -137,67 +155,41 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
     e0 = (static_cast<uint64_t>(o0 - pi0 + 1) << 32) | g;
     e1 = (static_cast<uint64_t>(o1 - pi1 + 1) << 32) | (g + 1);
   }
-  // list entries and flagged groups -> the wave's slices of LDS (ballot prefixes, no atomics)
+  // list entries -> the wave's slice of LDS (ballot prefixes, no atomics)
   const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
-  const uint64_t bf0 = __ballot(f0), bf1 = __ballot(f1);
   if (c0) staged[w][__popcll(b0 & below)] = e0;
   if (c1) staged[w][__popcll(b0) + __popcll(b1 & below)] = e1;
-  if (f0) deferred[w][__popcll(bf0 & below)] = g;
-  if (f1) deferred[w][__popcll(bf0) + __popcll(bf1 & below)] = g + 1;
-  if (lane == 0) {
-    wave_cnt[w] = __popcll(b0) + __popcll(b1);
-    wave_def[w] = __popcll(bf0) + __popcll(bf1);
-  }
-  if (threadIdx.x == 0) walk_n = 0;
-  __syncthreads();
-  // second phase: the workgroup's flagged groups, packed four lanes each (one per conf run)
-  // onto the first lanes, walk their runs -- ~1% of groups flagged then costs one short pass
-  // of one or two waves per workgroup (the walk is VALU-heavy: one per wave, or one per
-  // lane with the runs in a loop, measured +8..+12 us per 1M-group epoch)
-  uint32_t nd = 0;
-#pragma unroll
-  for (uint32_t u = 0; u < kWaves; ++u) nd += wave_def[u];
-  if (__builtin_expect(nd != 0, 0)) {
-    for (uint32_t base = 0; base < nd * kTableMaxRuns; base += kTableBlock) {
-      const uint32_t q = base + threadIdx.x, i = q / kTableMaxRuns, r = q % kTableMaxRuns;
-      const bool act = i < nd;
-      int64_t cand = kI64Min, pr = 0, lc = 0, pi = 0;
-      uint8_t st = 0;
-      uint32_t h = 0;
-      if (act) {
-        uint32_t k = i, u = 0;
-        while (k >= wave_def[u]) k -= wave_def[u++];
-        h = deferred[u][k];
-        cand = table_run_lane<P>(t, h, r, pr, lc, pi, st);
-      }
-      cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 1)));
-      cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 2)));
-      uint32_t s32 = st;
-      s32 |= __shfl_xor(s32, 1);
-      s32 |= __shfl_xor(s32, 2);
-      if (act && r == 0) {
-        if (t.status) t.status[h] = static_cast<uint8_t>(s32);
-        if (cand > lc) {  // pi == 0 (not the leader) returned kI64Min
-          table_commit_one(t, h, pr, cand);
-          walk_staged[atomicAdd(&walk_n, 1u)] = (static_cast<uint64_t>(cand - pi + 1) << 32) | h;
-        }
-      }
+  uint32_t cnt = __popcll(b0) + __popcll(b1);
+  // the wave's flagged groups, 16 per pass (wave-uniform loop)
+  for (uint32_t base = fs0; base < fs1; base += 16) {
+    const uint32_t i = base + (lane >> 2), r = lane & 3u;
+    const bool act = i < fs1;
+    const uint32_t h = base == fs0 ? h0 : (act ? t.flag_list[i] : 0u);
+    int64_t cand = kI64Min, pr = 0, lc = 0, pi = 0;
+    uint8_t st = 0;
+    if (act) cand = table_run_lane<P>(t, h, r, pr, lc, pi, st);
+    cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 1)));
+    cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 2)));
+    uint32_t s32 = st;
+    s32 |= __shfl_xor(s32, 1);
+    s32 |= __shfl_xor(s32, 2);
+    const bool commit = act && r == 0 && cand > lc;  // pi == 0 (not the leader) gave kI64Min
+    if (act && r == 0) {
+      if (t.status) t.status[h] = static_cast<uint8_t>(s32);
+      if (commit) table_commit_one(t, h, pr, cand);
     }
-    __syncthreads();
+    const uint64_t bc = __ballot(commit);
+    if (commit) staged[w][cnt + __popcll(bc & below)] = (static_cast<uint64_t>(cand - pi + 1) << 32) | h;
+    cnt += __popcll(bc);
   }
-  // compaction: fast-path entries in (wave, lane) order, then the run walk's; one
-  // 64-bit atomic per workgroup ({workgroups done << 32 | entries}) on its segment's counter
-  // reserves the workgroup's slice, and the last workgroup of a segment publishes its count
-  // and re-zeroes the counter
+  if (lane == 0) wave_cnt[w] = cnt;
+  __syncthreads();
   const uint32_t seg = blockIdx.x % kTableSegments;
   if (threadIdx.x == 0) {
     uint32_t tot = 0;
     for (uint32_t u = 0; u < kWaves; ++u) tot += wave_cnt[u];
-    blk_walk = tot;
-    tot += walk_n;
     const unsigned long long old = atomicAdd(t.ctr + seg, (1ull << 32) | tot);
     blk_base = seg * t.seg_cap + static_cast<uint32_t>(old);
-    blk_walk += blk_base;
     const uint32_t seg_blocks = (gridDim.x - seg + kTableSegments - 1) / kTableSegments;
     if (static_cast<uint32_t>(old >> 32) + 1u == seg_blocks) {  // the segment is complete
       t.n_changed[seg] = static_cast<uint32_t>(old) + tot;
@@ -207,11 +199,38 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
   __syncthreads();
   uint32_t pos = blk_base;
   for (uint32_t u = 0; u < w; ++u) pos += wave_cnt[u];
-  const uint32_t nw = wave_cnt[w];
-  if (lane < nw) t.changed[pos + lane] = staged[w][lane];
-  if (lane + 64 < nw) t.changed[pos + lane + 64] = staged[w][lane + 64];
-  if (__builtin_expect(nd != 0, 0))
-    for (uint32_t i = threadIdx.x; i < walk_n; i += kTableBlock) t.changed[blk_walk + i] = walk_staged[i];
+  for (uint32_t i = lane; i < cnt; i += 64) t.changed[pos + i] = staged[w][i];
+}
+
+// The flagged lists: per range of kTableBlockGroups groups (one epoch workgroup's), its groups
+// whose conf word carries JRQ_CONF_RUNS at flag_list[b * kTableBlockGroups ...] and their count
+// at flag_cnt[b].  Rebuilt after every update that carries group headers (only headers change
+// a flag); one workgroup per range, no atomics.
+constexpr uint32_t kFlagBlock = kTableBlockGroups / 2;
+__global__ __launch_bounds__(kFlagBlock) void table_flags_kernel(JrqTableArgs t) {
+  __shared__ uint32_t wave_cnt[kFlagBlock / 64];
+  const uint32_t pairs = (t.G + 1) >> 1;
+  const uint32_t tt = blockIdx.x * kFlagBlock + threadIdx.x;
+  const uint32_t g = tt << 1;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  bool f0 = false, f1 = false;
+  if (tt < pairs) {
+    const i64x2 cw = tld2(reinterpret_cast<const int64_t*>(t.conf) + g);
+    f0 = static_cast<uint64_t>(cw.x) >> 63;
+    f1 = (static_cast<uint64_t>(cw.y) >> 63) && g + 1 < t.G;
+  }
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
+  if (lane == 0) wave_cnt[w] = __popcll(b0) + __popcll(b1);
+  __syncthreads();
+  uint32_t pos = blockIdx.x * kTableBlockGroups, tot = 0;
+  for (uint32_t u = 0; u < kFlagBlock / 64; ++u) {
+    if (u == w) pos += tot;
+    tot += wave_cnt[u];
+  }
+  if (f0) t.flag_list[pos + __popcll(b0 & below)] = g;
+  if (f1) t.flag_list[pos + __popcll(b0) + __popcll(b1 & below)] = g + 1;
+  if (threadIdx.x == 0) t.flag_cnt[blockIdx.x] = tot;
 }
 
 // Group headers: one lane per header (a group appears at most once per call).
@@ -234,7 +253,7 @@ __global__ __launch_bounds__(256) void table_states_kernel(JrqTableArgs t, const
   t.la[g] = st.last_appended;
   t.lc[g] = st.last_committed;
   const uint64_t c0 = nr ? (st.run_conf[0] & ~kConfRuns) : 0;
-  t.conf[g] = c0 | (nr > 1 ? kConfRuns : 0ull);
+  t.conf[g] = c0 | (nr > 1 ? kConfRuns : 0ull);  // (table_flags_kernel lists the flagged)
 #pragma unroll
   for (int k = 1; k < kTableMaxRuns; ++k) {
     const size_t o = static_cast<size_t>(k - 1) * t.ld + g;
@@ -279,9 +298,13 @@ __global__ __launch_bounds__(256) void table_recs_kernel(JrqTableArgs t, const u
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_update(
     const JrqTableArgs* a, const JrqGroupState* states, uint32_t n_states, const uint64_t* recs,
     uint32_t n_recs, hipStream_t stream) {
-  if (n_states)
+  if (n_states) {
     hipLaunchKernelGGL(jrq::table_states_kernel, dim3((n_states + 255) / 256), dim3(256), 0,
                        stream, *a, states, n_states);
+    const uint32_t pairs = (a->G + 1) >> 1;
+    hipLaunchKernelGGL(jrq::table_flags_kernel, dim3((pairs + jrq::kFlagBlock - 1) / jrq::kFlagBlock),
+                       dim3(jrq::kFlagBlock), 0, stream, *a);
+  }
   if (n_recs)
     hipLaunchKernelGGL(jrq::table_recs_kernel, dim3((n_recs + 255) / 256), dim3(256), 0, stream,
                        *a, recs, n_recs);

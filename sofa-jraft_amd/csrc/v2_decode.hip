@@ -18,14 +18,17 @@
 //              cache (a handful of dependent loads per record: the header fields, then a jump
 //              over `data` to the trailing checksum / learner fields).  Peer strings are hashed
 //              byte-wise from an LDS copy of the CRC table while their canonical form is
-//              checked; type ^ crc(LogId) ^ peers goes to a partial word.  It also writes the
-//              interleaved range list  gap0, data0, gap1, data1, ..., dataN-1, gapN  whose
-//              boundaries are [off[0], d0, e0, d1, e1, ..., off[N]].
-//   crc64      the batched CRC kernels (crc64.hip) over those 2N+1 ranges: one pass over the
-//              record bytes at streaming bandwidth (gap ranges -- headers -- are hashed too and
-//              dropped; they are a few dozen bytes per record).
-//   v2_finish  computed = partial ^ crc(data), the data CRC recovered from its range's CRC by
-//              linearity (see v2_finish), corrupt = has_checksum && stored != computed.
+//              checked; type ^ crc(LogId) ^ peers goes to a partial word.  It also writes one
+//              CRC range per record, [data start, next data start), and its last block to
+//              arrive writes the gate of the fixed-size data path (every record decoded, one
+//              data length).
+//   fixed path crc64_fixed_kernel at the data starts (k lanes per record), finishing in place:
+//              computed = partial ^ crc(data), corrupt = has_checksum && stored != computed.
+//   otherwise  the batched segment walk (crc64.hip) over the ranges -- one pass over the
+//              record bytes at streaming bandwidth -- then v2_finish: the data CRC recovered
+//              from its range's CRC by linearity (see v2_finish), computed, corrupt.
+//   The kernels of the path not taken return at their first instruction (gate on the device,
+//   so the _dev entry point stays free of host synchronisation).
 //
 // A peer string is hashed as stored when it is already what PeerId.toString() would render
 // from it (V2Encoder always writes toString(), so this is every record it produced).  A
@@ -194,20 +197,76 @@ __device__ __forceinline__ uint64_t crc_bytes_be(uint64_t crc, uint64_t v, const
   return crc;
 }
 
+// One lane per record; then the block's summary for the fixed-size data path's gate (below).
+__device__ void v2_parse_record(const JrqV2Args& a, uint32_t r, const uint64_t* T, uint8_t& st_out,
+                                uint64_t& d_out, uint64_t& dl_out);
+
 __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
   __shared__ uint64_t T[256];
+  __shared__ uint64_t s_doff[256];
+  __shared__ uint64_t s_len0;
+  __shared__ uint32_t s_last;
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) T[i] = bswap64(a.slice[i]);
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r == 0) {
-    if (a.gate != nullptr) {  // v2_uniform's flag and arrival count (it runs next)
-      a.gate[2] = 0;
-      a.gate[4] = 0;
-    }
     a.off2[0] = a.off[0];
     a.off2[a.n + 1] = a.off[a.n];
   }
-  if (r >= a.n) return;
+  const bool live = r < a.n;
+  uint8_t st = kV2Null;
+  uint64_t d = 0, dl = 0;
+  if (live) v2_parse_record(a, r, T, st, d, dl);
+  // The gate of the fixed-size data path (crc64_fixed_kernel at the data starts): every record
+  // decoded, all with the data length L0 of record 0, data ranges in order, and each 64
+  // consecutive ones within 1 GiB (the fixed kernel reads a row of records through one buffer
+  // descriptor at u32 offsets from its first start; checked per pair of adjacent blocks of 256,
+  // a sufficient condition).  Each block summarises its records {first start, last start, its
+  // first length, broken}; the last block to arrive combines the summaries and writes
+  // gate = {k, L0, broken, end}: k lanes per record for crc64_fixed_kernel, 0 = the segment walk.
+  s_doff[threadIdx.x] = d;
+  if (threadIdx.x == 0) s_len0 = dl;
+  __syncthreads();
+  const uint64_t lb = s_len0;
+  const bool bad = live && (st != kV2Ok || dl != lb ||
+                            (threadIdx.x > 0 && d < s_doff[threadIdx.x - 1] + lb));
+  const bool any_bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) {
+    const uint32_t nb = a.n - blockIdx.x * blockDim.x;
+    uint64_t* sm = a.blk + 4ull * blockIdx.x;
+    sm[0] = s_doff[0];
+    sm[1] = s_doff[(nb < blockDim.x ? nb : blockDim.x) - 1];
+    sm[2] = lb;
+    sm[3] = any_bad ? 1u : 0u;
+    __threadfence();  // release the summary, then arrive
+    const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(a.gate + 4), 1ull);
+    s_last = old + 1 == gridDim.x;
+    __threadfence();  // acquire (the last arriver reads every block's summary)
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const uint64_t L0 = a.blk[2];
+  bool broken = false;
+  for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+    const uint64_t* sm = a.blk + 4ull * b;
+    broken = broken || sm[3] != 0 || sm[2] != L0;
+    const uint64_t first_prev = b ? sm[-4] : sm[0];
+    if (b) broken = broken || sm[0] < sm[-3] + L0;
+    broken = broken || sm[1] + L0 - first_prev >= (1ull << 30);
+  }
+  broken = __syncthreads_or(broken);
+  if (threadIdx.x == 0) {
+    const uint32_t k = broken ? 0u : jrq_fixed_k(L0, a.n, a.lanes);
+    a.gate[0] = L0 / (k ? k : 1u) <= (1ull << 23) ? k : 0u;
+    a.gate[1] = L0;
+    a.gate[2] = broken ? 1u : 0u;
+    a.gate[3] = a.off[a.n];  // the records' end: crc64_fixed_kernel's load window
+    a.gate[4] = 0;           // the arrival count, zero for the next launch
+  }
+}
+
+__device__ void v2_parse_record(const JrqV2Args& a, uint32_t r, const uint64_t* T, uint8_t& st_out,
+                                uint64_t& d_out, uint64_t& dl_out) {
   const uint64_t b0 = a.off[r];
   const int64_t L = static_cast<int64_t>(a.off[r + 1] - b0);
   const uint8_t* rec = a.rec + b0;
@@ -317,46 +376,14 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
   a.data_len[r] = static_cast<uint64_t>(dlen);
   if (a.peer_counts) a.peer_counts[r] = counts;
   a.off2[r + 1] = b0 + static_cast<uint64_t>(doff);  // a failed record: its start
-  // CRCs of the bytes around the data (v2_finish removes them from the range CRCs)
-  uint64_t hc = 0, tc = 0;
-  uint64_t hl = 0, tl = 0;
-  if (st == kV2Ok) {
-    ChunkReader rd(rec, L);
-    hl = static_cast<uint64_t>(doff);
-    tl = static_cast<uint64_t>(L - doff - dlen);
-    for (int64_t p = 0; p < doff; ++p) hc = T[((hc >> 56) ^ rd.at(p)) & 0xFFu] ^ (hc << 8);
-    for (int64_t p = doff + dlen; p < L; ++p) tc = T[((tc >> 56) ^ rd.at(p)) & 0xFFu] ^ (tc << 8);
-  }
-  a.hcrc[r] = hc;
-  a.tcrc[r] = tc;
+  // the lengths of the bytes around the data (v2_finish hashes and removes them from the
+  // range CRCs when the segment walk runs)
+  const uint64_t hl = st == kV2Ok ? static_cast<uint64_t>(doff) : 0;
+  const uint64_t tl = st == kV2Ok ? static_cast<uint64_t>(L - doff - dlen) : 0;
   a.lens[r] = (hl << 32) | tl;
-}
-
-// Every record decoded, all with the data length L of record 0, data ranges in order and each
-// 64 consecutive ones within 1 GiB (the fixed-size CRC path's conditions: crc64_fixed_kernel
-// reads a row of records through one buffer descriptor at u32 offsets from its first start).
-// Any block that finds one broken sets gate[2]; the last block to arrive (gate[4], zeroed by
-// v2_parse) writes gate = {k, L, bad, end}: k lanes per record for crc64_fixed_kernel, 0 = the
-// segment walk.
-__global__ __launch_bounds__(256) void v2_uniform(JrqV2Args a) {
-  const uint64_t L0 = a.data_len[0];
-  bool bad = false;
-  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += gridDim.x * blockDim.x) {
-    const uint64_t d = a.data_off[r];
-    bad = bad || a.status[r] != kV2Ok || a.data_len[r] != L0;
-    if (r > 0) bad = bad || d < a.data_off[r - 1] + L0;
-    if (r >= 63) bad = bad || d + L0 - a.data_off[r - 63] >= (1ull << 30);
-  }
-  if (__syncthreads_or(bad) && threadIdx.x == 0) a.gate[2] = 1;
-  if (threadIdx.x != 0) return;
-  __threadfence();
-  if (atomicAdd(reinterpret_cast<unsigned long long*>(a.gate + 4), 1ull) != gridDim.x - 1u) return;
-  __threadfence();
-  const uint64_t L = L0;
-  const uint32_t k = __atomic_load_n(a.gate + 2, __ATOMIC_RELAXED) ? 0u : jrq_fixed_k(L, a.n, a.lanes);
-  a.gate[0] = L / (k ? k : 1u) <= (1ull << 23) ? k : 0u;
-  a.gate[1] = L;
-  a.gate[3] = a.off[a.n];  // the records' end: crc64_fixed_kernel's load window
+  st_out = st;
+  d_out = b0 + static_cast<uint64_t>(doff);
+  dl_out = static_cast<uint64_t>(dlen);
 }
 
 // The CRC pass hashes one range per record, [data start, next record's data start): the data,
@@ -365,30 +392,38 @@ __global__ __launch_bounds__(256) void v2_uniform(JrqV2Args a) {
 // (P(0) = 1), so
 //   crc(suffix) = crc(trailer) * x^(8 |next header|) ^ crc(next header)
 //   crc(data)   = (crc(range) ^ crc(suffix)) * x^(-8k)
-// with the trailer / header CRCs from v2_parse (it reads those bytes anyway).  A multiply by
+// with the trailer / header CRCs hashed here from the record bytes.  A multiply by
 // x^(+-64) is one lookup per register byte: T_i[b] = b x^(64 + 8i) (the engine's slice tables,
 // un-swapped), TI_i[b] = b x^(8i - 64) (engine xinv); single bytes use T_0 / TI_7.  One entry
 // boundary per record instead of two: the CRC pass takes 310 instead of 330 us on 64k x 16 KiB
 // records (tools/v2_boundary_probe.py).
+// (The fixed-size data path -- gate[0] != 0 -- finishes inside crc64_fixed_kernel: this kernel
+// then returns at once.)
 __global__ __launch_bounds__(256) void v2_finish(JrqV2Args a) {
   __shared__ uint64_t Tf[8][256], Ti[8][256];
+  if (a.gate[0] != 0) return;  // (grid-uniform)
   for (uint32_t e = threadIdx.x; e < 8 * 256; e += blockDim.x) {
     Tf[e >> 8][e & 255u] = bswap64(a.slice[e]);
     Ti[e >> 8][e & 255u] = a.xinv[e];
   }
   __syncthreads();
   const uint32_t stride = gridDim.x * blockDim.x;
-  const bool fixed = a.gate != nullptr && a.gate[0] != 0;  // data CRCs by crc64_fixed_kernel
   for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
     const bool ok = a.status[r] == kV2Ok;
     uint64_t c = 0;
-    if (ok && fixed) {
-      c = a.partial[r] ^ a.crc_data[r];
-    } else if (ok) {
+    if (ok) {
       const bool more = r + 1 < a.n;
       uint64_t h = more ? a.lens[r + 1] >> 32 : 0;  // next record's header (0 if it failed)
-      const uint64_t k = (a.lens[r] & 0xFFFFFFFFull) + h;
-      uint64_t s = a.tcrc[r];
+      const uint64_t tl = a.lens[r] & 0xFFFFFFFFull, k = tl + h;
+      // the CRCs of this record's trailer and the next record's header, from their bytes
+      uint64_t s = 0, hc = 0;
+      {
+        const uint64_t e = a.off[r + 1];
+        ChunkReader rd(a.rec + e - tl, static_cast<int64_t>(tl));
+        for (uint64_t p = 0; p < tl; ++p) s = Tf[0][((s >> 56) ^ rd.at(static_cast<int64_t>(p))) & 0xFFu] ^ (s << 8);
+        ChunkReader rn(a.rec + e, static_cast<int64_t>(h));
+        for (uint64_t p = 0; p < h; ++p) hc = Tf[0][((hc >> 56) ^ rn.at(static_cast<int64_t>(p))) & 0xFFu] ^ (hc << 8);
+      }
       for (; h >= 8; h -= 8) {  // s * x^64
         uint64_t t = 0;
 #pragma unroll
@@ -396,7 +431,7 @@ __global__ __launch_bounds__(256) void v2_finish(JrqV2Args a) {
         s = t;
       }
       for (; h > 0; --h) s = (s << 8) ^ Tf[0][s >> 56];
-      s ^= more ? a.hcrc[r + 1] : 0;
+      s ^= hc;
       uint64_t d = a.crc2[r + 1] ^ s, m = k;
       for (; m >= 8; m -= 8) {  // d * x^-64
         uint64_t t = 0;
@@ -418,15 +453,6 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_v2_parse(
     const JrqV2Args* a, hipStream_t stream) {
   const uint32_t blocks = (a->n + 255) / 256;
   hipLaunchKernelGGL(jrq::v2_parse, dim3(blocks ? blocks : 1), dim3(256), 0, stream, *a);
-  return hipGetLastError();
-}
-
-extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_v2_gate(
-    const JrqV2Args* a, int num_cus, hipStream_t stream) {
-  uint32_t blocks = (a->n + 255) / 256;
-  const uint32_t cap = static_cast<uint32_t>(num_cus) * 2u;
-  if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL(jrq::v2_uniform, dim3(blocks ? blocks : 1), dim3(256), 0, stream, *a);
   return hipGetLastError();
 }
 

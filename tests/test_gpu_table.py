@@ -257,3 +257,61 @@ def test_pending_entries_without_conf_run_are_invalid(engine):
     assert t.read()["last_appended"][2] == 9
     t.check()
     t.close()
+
+
+@pytest.mark.parametrize("G,joint", [(20000, 0.05), (4097, 0.9), (70000, 0.0)])
+def test_flagged_groups_in_full_blocks(engine, G, joint):
+    """Every group commits (C3 host series) and some have a conf change in their window: a
+    workgroup lists its own groups only -- committing single-conf ones and walked flagged ones --
+    so no list segment overflows; against the stateless kernel with the CSR run table, through
+    both the host variant and the _dev segments, twice (the flagged lists after reloads)."""
+    import torch
+
+    from jraft_amd import workloads as W
+    s = W.host_series("C3", 1, groups=G, joint_frac=joint)
+    P = 5
+    pi = s["pending_index"]
+    st = Table.states(G)
+    jm = s["switch_at"] != 0
+    st["group"] = np.arange(G)
+    st["num_runs"] = np.where(jm, 2, 1)
+    st["flags"] = _lib.STATE_RESET_MATCH
+    st["pending_index"] = np.where(pi == s["last_committed"] + 1, _lib.PI_FOLLOWS_LC, pi)
+    st["last_appended"] = s["last_appended"][0]
+    st["last_committed"] = s["last_committed"]
+    st["run_conf"][:, 0] = s["conf_a"]
+    st["run_conf"][:, 1] = np.where(jm, s["conf_b"], 0)
+    st["run_start"][:, 1] = s["switch_at"]
+    m = s["match"][0]
+    gs = np.arange(G)
+    recs = np.concatenate([_lib.rec(gs, p, np.maximum(m[p] - (pi - 1), 0)) for p in range(P)])
+    dev = torch.device("cuda:0")
+    d = {k: torch.from_numpy(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v)).to(dev)
+         for k, v in (("match", m), ("pi", pi), ("la", s["last_appended"][0]),
+                      ("lc", s["last_committed"]), ("conf", s["conf"]), ("run_off", s["run_off"]),
+                      ("run_start", s["run_start"]), ("run_conf", s["run_conf"]))}
+    pc = torch.empty(G, dtype=torch.int64, device=dev)
+    ps = torch.empty(G, dtype=torch.uint8, device=dev)
+    engine.quorum_epoch_dev(d["match"], d["pi"], d["la"], d["lc"], d["conf"], pc, ps,
+                            run_off=d["run_off"], run_start=d["run_start"], run_conf=d["run_conf"])
+    engine.synchronize()
+    exp_c, exp_s = pc.cpu().numpy(), ps.cpu().numpy()
+    assert (exp_c > s["last_committed"]).mean() > 0.9
+    t = Table(engine, G, P)
+    for rep in range(2):
+        t.update(st, recs)
+        if rep == 0:
+            changed, stt = t.epoch(status=True)
+        else:
+            out = torch.empty(_lib.TABLE_SEGMENTS * t.segment_capacity(), dtype=torch.int64, device=dev)
+            n = torch.zeros(_lib.TABLE_SEGMENTS, dtype=torch.int32, device=dev)
+            sd = torch.empty(G, dtype=torch.uint8, device=dev)
+            t.epoch_dev(out, n, sd)
+            engine.synchronize()
+            assert (n.cpu().numpy() <= t.segment_capacity()).all()
+            changed, stt = t.gather_dev_list(out, n), sd.cpu().numpy()
+        got, _ = committed_from(changed, pi, s["last_committed"])
+        np.testing.assert_array_equal(got, exp_c)
+        np.testing.assert_array_equal(stt, exp_s)
+    t.check()
+    t.close()

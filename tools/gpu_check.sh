@@ -16,7 +16,7 @@ run() {  # run <name> <seconds> <cmd...>
 STEPS=${STEPS:-"tests smoke bench"}
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -x -p no:cacheprovider --timeout 240 --timeout-method thread --durations=15 ;;
     crc)   run crc_tests 600 python -m pytest tests/test_gpu_crc.py -q -x -p no:cacheprovider --timeout 300 ;;
     quorum) run quorum_tests 600 python -m pytest tests/test_gpu_quorum.py -q -x -p no:cacheprovider --timeout 300 ;;
     quick) run bench_quick 600 python bench.py --steps 20 --warmup 3 --no-cpu ;;

@@ -9,12 +9,12 @@ Reads (when present):
       rocprofv3 --pmc pass per bench leg (`bench.py --legs <leg>`) and counter
 Writes profiles/<tag>_kernel_stats.csv (verbatim copy) and profiles/<tag>_pmc.json: per leg
 and kernel, the mean of each counter over its dispatches, and the HBM bytes per launch
-(2 * FETCH_SIZE + WRITE_SIZE) KiB -- on gfx950 FETCH_SIZE counts a wide streaming read at
-half its bytes (MI355X_MICROARCH.md, HBM section).  The snapshot leg (one 1 GiB stream
-through the CRC kernel, ~1 GiB of reads) measures that factor on the CRC kernel's own access
-pattern (`calibration`: 64-B reads per lane quad, counted at more than half), and the CRC
-rounds kernels' bytes use it instead of 2.  `csrc_sha` = bench.csrc_sha() of the tree the passes ran on; bench.py
-cites a summary only when it matches its own sources.
+(2 * FETCH_SIZE + WRITE_SIZE) KiB -- on gfx950 FETCH_SIZE counts a wide (16 B per lane)
+streaming read at half its bytes (MI355X_MICROARCH.md, HBM section); every product kernel reads
+its streams with 16-B loads (the CRC kernels' buffer_load_b128 included), so one rule holds for
+all of them (round 2 scaled the CRC kernels by a factor calibrated on one of them, which does
+not transfer: VERDICT r02).  `csrc_sha` = bench.csrc_sha() of the tree the passes ran on;
+bench.py cites a summary only when it matches its own sources.
 """
 import collections
 import csv
@@ -45,7 +45,7 @@ def main():
     import bench
     tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
     os.makedirs(PROF, exist_ok=True)
-    res = {"tag": tag, "csrc_sha": bench.csrc_sha(), "correction": "2*FETCH_SIZE+WRITE_SIZE (CRC rounds kernels: calibration factor*FETCH_SIZE), KiB->B",
+    res = {"tag": tag, "csrc_sha": bench.csrc_sha(), "correction": "2*FETCH_SIZE+WRITE_SIZE (MI355X_MICROARCH.md HBM section), KiB->B",
            "kernel_stats": {}, "legs": collections.defaultdict(lambda: collections.defaultdict(dict))}
     st = os.path.join(OUT, "prof", "run_kernel_stats.csv")
     if os.path.exists(st):
@@ -79,24 +79,6 @@ def main():
             if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
                 v["hbm_bytes_per_launch"] = (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
                 v["hbm_bytes_per_launch_raw"] = (v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
-    snap = res["legs"].get("snapshot", {})
-    rk = [v for k, v in snap.items() if "crc64_rounds_kernel" in k and "FETCH_SIZE" in v]
-    if rk:
-        # the archive launch reads the 1 GiB payload once (+ 128 KiB LDS tables per workgroup
-        # from L2 and a few KiB of offsets/scratch); the same kernel name also ran the 64k
-        # region streams (same bytes) in that pass
-        fetched = rk[0]["FETCH_SIZE"] * 1024
-        res["calibration"] = {"kernel": "crc64_rounds_kernel (snapshot leg)",
-                              "known_read_bytes": 1 << 30, "FETCH_SIZE_bytes": fetched,
-                              "bytes_per_FETCH_byte": (1 << 30) / fetched}
-        # the CRC rounds kernels read 64 contiguous bytes per lane quad, not the wide streams
-        # the x2 rule is measured on: their HBM bytes use this kernel's own factor
-        f = res["calibration"]["bytes_per_FETCH_byte"]
-        for leg, ks in res["legs"].items():
-            for k, v in ks.items():
-                if ("crc64_rounds_kernel" in k or "crc64_fixed_kernel" in k) and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-                    v["hbm_bytes_per_launch"] = (f * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
-                    v["fetch_factor"] = f
     res["legs"] = {k: dict(v) for k, v in res["legs"].items()}
     with open(os.path.join(PROF, f"{tag}_pmc.json"), "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
