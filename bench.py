@@ -456,11 +456,11 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
                                          b["conf"][idx], chunk=1024)
         ok = bool(np.array_equal(local.cpu().numpy()[idx], ce))
     bpg = quorum_bytes_per_group(P)
-    rl = roofline(bpg * G, k_ms, kernel="quorum_epoch_pair_kernel<5>", bytes_per_group=bpg,
+    rl = roofline(bpg * G, k_ms, kernel="quorum_epoch_pair_kernel<5, false>", bytes_per_group=bpg,
                   survey_bytes_per_group=8 * P + 38,
                   frac_survey_bytes=(8 * P + 38) * G / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                   timing="one HIP event pair around --steps back-to-back launches / steps",
-                  **pmc_traffic("quorum", "quorum_epoch_pair_kernel<5>"))
+                  **pmc_traffic("quorum", "quorum_epoch_pair_kernel<5, false>"))
     return {
         "value": value, "elapsed": elapsed, "cfg": cfg, "G": G, "P": P, "roofline": rl,
         "multi_gpu": {"rccl_nranks": nranks, "publish_every": args.publish_every,
@@ -677,20 +677,31 @@ def leg_drive(ctx, args, G):
             "pcie_bytes_per_epoch": pcie, "pcie_GBps": pcie / (f * 1e-3) / 1e9,
             "first_epoch_flush_ms": float(st["flush_ms"][0]),
             "bit_exact_vs_stateless_kernel": ok}
-    lat = drive.drive_latency(ctx.dev.index, G, 5, 16, 2.0, 1000, 1 << 16)
-    lat["policy"] = {"maxDelayUs": 1000, "maxDirtyGroups": 1 << 16}
-    lat["how"] = ("16 threads loop over their slices of the groups: appendPendingTask of one "
-                  "entry, then commitAt of it by each of the 5 peers; GroupBatch::startFlusher "
-                  "flushes when the oldest unflushed change is 1 ms old or 65536 groups changed; "
-                  "latency = onCommitted(c) time - time of entry c's last ack")
-    lat["commits_per_s"] = lat["commits"] / lat["seconds"]
-    lat["api_calls_per_s"] = (lat["entries"] + lat["acks"]) / lat["seconds"]
+    lats = {}
+    for lg, prod, fl, delay, pace in ((G, 8, 8, 1000, 100_000), (1 << 16, 4, 4, 500, 10_000)):
+        lat = drive.drive_latency(ctx.dev.index, lg, 5, prod, 2.0, delay, 1 << 16, flush_threads=fl,
+                                  pass_us=pace)
+        lat.update({"groups": lg, "producer_threads": prod, "flush_threads": fl,
+                    "producer_pass_us": pace,
+                    "policy": {"maxDelayUs": delay, "maxDirtyGroups": 1 << 16},
+                    "commits_per_s": lat["commits"] / lat["seconds"],
+                    "api_calls_per_s": (lat["entries"] + lat["acks"]) / lat["seconds"],
+                    "flushes_per_s": lat["flushes"] / lat["seconds"]})
+        lats[f"{lg}_groups"] = lat
+    lats["how"] = ("producer threads loop over their slices of the groups -- one pass per "
+                   "producer_pass_us (paced: acks arrive with the network; spinning producers also "
+                   "hit the box's cgroup CPU quota, whose throttling then sets the latency) -- "
+                   "appendPendingTask of one entry, then commitAt of it by each of the 5 peers; GroupBatch::"
+                   "startFlusher flushes when the oldest unflushed change is maxDelayUs old or "
+                   "65536 groups changed, packing and delivering on flush_threads threads (producers "
+                   "+ flush threads = the 16-CPU share of the box); latency = onCommitted(c) time "
+                   "- time of entry c's last ack")
     return {"workload": f"C3 through the C++ BallotBox host mirror: {G} groups x 5 peers, joint, "
                         f"1% with a conf change in the pending window, {K} epochs",
             "how": "flush = pack changed records + H2D (pinned) + apply + epoch kernels + D2H of "
                    "the changed commits + closures / onCommitted; api = the appendPendingTask / "
                    "commitAt calls of the epoch (made before the flush, from `api_threads` threads)",
-            **out, "ack_to_onCommitted_latency": lat}
+            **out, "ack_to_onCommitted_latency": lats}
 
 
 def leg_c2(ctx, args):

@@ -1278,10 +1278,11 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   t->e = e;
   const uint64_t ld = (static_cast<uint64_t>(G) + 63) & ~63ull;  // pairs + 512-B rows
   // rows (the state jrq_table_copy copies): match[P], pi, la, lc, conf, xstart[3], xconf[3],
-  // the flagged lists flag_list[blocks * 2048] + flag_cnt[blocks] (u32); then the control
-  // words: ctr[16], invalid
+  // the flagged-entry slots flag_ent[waves][128][8] + flag_wcnt[waves] (u32); then the
+  // control words: ctr[16], invalid
   const uint64_t blocks = (G + jrq::kTableBlockGroups - 1) / jrq::kTableBlockGroups;
-  const uint64_t flag_words = (blocks * (jrq::kTableBlockGroups + 1) + 1) / 2;
+  const uint64_t waves = blocks * (jrq::kTableBlockGroups / 128);
+  const uint64_t flag_words = waves * jrq::kFlagSlots * 8 + (waves + 1) / 2;
   const uint64_t words = ld * (P + 4 + 2 * (jrq::kTableMaxRuns - 1)) + flag_words;
   const size_t bytes = words * 8 + 8 * jrq::kTableSegments + 64;
   if (hipMalloc(&t->mem, bytes) != hipSuccess || hipMemset(t->mem, 0, bytes) != hipSuccess ||
@@ -1302,8 +1303,8 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   a.conf = reinterpret_cast<uint64_t*>(a.lc + ld);
   a.xstart = reinterpret_cast<int64_t*>(a.conf + ld);
   a.xconf = reinterpret_cast<uint64_t*>(a.xstart + ld * (jrq::kTableMaxRuns - 1));
-  a.flag_list = reinterpret_cast<uint32_t*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
-  a.flag_cnt = a.flag_list + blocks * jrq::kTableBlockGroups;
+  a.flag_ent = reinterpret_cast<uint64_t*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
+  a.flag_wcnt = reinterpret_cast<uint32_t*>(a.flag_ent + waves * jrq::kFlagSlots * 8);
   a.ctr = reinterpret_cast<unsigned long long*>(w + words);
   a.invalid = reinterpret_cast<uint32_t*>(a.ctr + jrq::kTableSegments);
   t->state_bytes = words * 8;

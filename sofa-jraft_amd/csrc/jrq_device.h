@@ -39,6 +39,14 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 
 __device__ __forceinline__ uint64_t bswap64(uint64_t v) { return __builtin_bswap64(v); }
 
+// Workgroup barrier for a hand-off through LDS only: waits for the wave's own LDS operations,
+// not for its global stores.  __syncthreads() also waits vmcnt(0) -- on gfx9 stores count there
+// too -- so a wave that has just stored its results would sit out their round trip to memory
+// before the barrier (the memory clobber keeps the compiler from moving memory accesses across).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Block-wide exclusive scan of one value per thread (wave shuffles + LDS).
 __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* lds_warp,
                                                          uint64_t* total) {
@@ -214,6 +222,7 @@ constexpr int kTableMaxRuns = 4;                   // JRQ_TABLE_MAX_RUNS
 constexpr uint32_t kTableSegments = 16;            // JRQ_TABLE_SEGMENTS
 constexpr uint32_t kTableBlockGroups = 2048;       // groups per epoch workgroup
 constexpr int64_t kPiFollowsLc = INT64_MIN;        // JRQ_PI_FOLLOWS_LC
+constexpr uint32_t kFlagSlots = 128;               // flagged-entry slots per 128-group wave
 }  // namespace jrq
 struct JrqTableArgs {
   int64_t* match;        // [P][ld]
@@ -233,9 +242,9 @@ struct JrqTableArgs {
   uint32_t* n_changed;   // [kTableSegments] out
   uint32_t seg_cap;      // entries per list segment
   uint8_t* status;       // [G] out, nullable
-  uint32_t* flag_list;   // [blocks * kTableBlockGroups] per epoch workgroup b: its groups
-                         // flagged JRQ_CONF_RUNS, from b * kTableBlockGroups
-  uint32_t* flag_cnt;    // [blocks] how many
+  uint64_t* flag_ent;    // [waves][kFlagSlots][8] per 128-group epoch wave: its groups flagged
+                         // JRQ_CONF_RUNS as 64-B entries {group, run starts 1-3, conf words 0-3}
+  uint32_t* flag_wcnt;   // [waves] how many
 };
 
 // One group header as the ABI carries it (include/jrq.h jrq_group_state).

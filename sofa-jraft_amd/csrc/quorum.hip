@@ -96,19 +96,29 @@ __device__ __forceinline__ i64x2 ld2nt(const int64_t* p) {
 // Fast path (16-B aligned arrays, even match_ld): one lane decides two adjacent groups; every
 // stream is read with 16-byte non-temporal loads (1 KiB per wave instruction; each input is
 // read once per epoch, so it is not kept in L2 / MALL) and the two status bytes are stored as
-// one 16-bit word.  A group flagged JRQ_CONF_RUNS (a conf change inside its pending window) is
-// deferred to the workgroup's second phase, where one lane per deferred group walks its runs:
-// the run walk then shares no registers with the fast path (occupancy of the common case).
-// 512-thread workgroups: 256 and 1024 measured 6-8 % slower on C3 (tools/table_probe.hip).
+// one 16-bit word.  512-thread workgroups: 256 and 1024 measured 6-8 % slower on C3
+// (tools/table_probe.hip).
+// kRuns (run tables given): a group flagged JRQ_CONF_RUNS (a conf change inside its pending
+// window) is skipped by the single-conf decision and walked by its own wave afterwards, four
+// lanes per group (runs r, r + 4, ... on lane r of the quad, candidates max-reduced over the
+// quad); its state (pendingIndex, lastCommitted, lastAppended, match) comes from the owner lane
+// through the wave's slice of LDS (the first 16 flagged groups of a wave; a wave-local hand-off),
+// so the walk costs the run table's two dependent loads and no workgroup barrier.  Round 2
+// deferred flagged groups to a workgroup list behind __syncthreads() -- which also waits for
+// every store of the fast path -- and reloaded them.  Without run tables the kernel is the
+// kRuns = false instantiation: no LDS, no walk.
 constexpr uint32_t kPairBlock = 512;
 
-template <int P>
+template <int P, bool kRuns>
 __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
   constexpr uint32_t kWaves = kPairBlock / 64;
-  __shared__ uint32_t wave_def[kWaves];
-  __shared__ uint32_t deferred[kWaves][128];
+  constexpr uint32_t kHand = 16;
+  __shared__ int64_t hand[kRuns ? kWaves : 1][kHand][P + 3];  // {pi, lc, la, match[P]}
+  __shared__ uint32_t flagged[kRuns ? kWaves : 1][128];
   const uint32_t pairs = a.G >> 1;
   const uint32_t t = blockIdx.x * kPairBlock + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
   bool f0 = false, f1 = false;
   if (t < pairs) {
     const uint32_t g = t << 1;
@@ -119,14 +129,30 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
     i64x2 m[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) m[p] = ld2nt(a.match + static_cast<size_t>(p) * a.match_ld + g);
-    const bool runs = a.run_off != nullptr;
-    f0 = runs && (static_cast<uint64_t>(cw.x) & kConfRuns);
-    f1 = runs && (static_cast<uint64_t>(cw.y) & kConfRuns);
+    f0 = kRuns && (static_cast<uint64_t>(cw.x) & kConfRuns);
+    f1 = kRuns && (static_cast<uint64_t>(cw.y) & kConfRuns);
     int64_t m0[P], m1[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) {
       m0[p] = m[p].x;
       m1[p] = m[p].y;
+    }
+    if (kRuns) {  // flagged groups -> the wave's list and hand-off slots (ballot ranks)
+      const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
+      const uint32_t k0 = __popcll(b0 & below), k1 = __popcll(b0) + __popcll(b1 & below);
+      auto put = [&](uint32_t k, uint32_t h, int64_t p_, int64_t c_, int64_t l_, const int64_t(&mm)[P]) {
+        flagged[w][k] = h;
+        if (k < kHand) {
+          int64_t* hs = hand[w][k];
+          hs[0] = p_;
+          hs[1] = c_;
+          hs[2] = l_;
+#pragma unroll
+          for (int q = 0; q < P; ++q) hs[3 + q] = mm[q];
+        }
+      };
+      if (f0) put(k0, g, pi.x, lc.x, la.x, m0);
+      if (f1) put(k1, g + 1, pi.y, lc.y, la.y, m1);
     }
     int64_t o0, o1;
     uint8_t s0, s1;
@@ -139,7 +165,7 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
       __builtin_nontemporal_store(out, reinterpret_cast<i64x2*>(a.committed + g));
       __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
                                   reinterpret_cast<uint16_t*>(a.status + g));
-    } else {  // rare: a deferred group's outputs are written by the second phase only
+    } else {  // rare: a flagged group's outputs are written by the walk only
       if (!f0) {
         a.committed[g] = o0;
         a.status[g] = s0;
@@ -150,31 +176,53 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
       }
     }
   }
-  if (a.run_off != nullptr) {  // kernel-uniform: no LDS list and no barrier without run tables
-    // flagged groups -> the wave's slice of the list (ballot prefixes, no atomics, no
-    // initialising barrier in front of the loads)
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t below = (1ull << lane) - 1ull;
-    const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
-    if (f0) deferred[w][__popcll(b0 & below)] = t << 1;
-    if (f1) deferred[w][__popcll(b0) + __popcll(b1 & below)] = (t << 1) + 1;
-    if (lane == 0) wave_def[w] = __popcll(b0) + __popcll(b1);
-    __syncthreads();
-    uint32_t nd = 0;
+  if (kRuns) {
+    const uint32_t nflag = __popcll(__ballot(f0)) + __popcll(__ballot(f1));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (this wave's slots only)
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t q = lane >> 2, r = lane & 3u;
+    for (uint32_t base = 0; base < nflag; base += 16) {  // (wave-uniform)
+      const uint32_t i = base + q;
+      const bool act = i < nflag;
+      const uint32_t h = act ? flagged[w][i] : 0u;
+      int64_t hpi = 0, hlc = 0, hla = 0, hm[P];
+      if (act && i < kHand) {
+        const int64_t* hs = hand[w][i];
+        hpi = hs[0];
+        hlc = hs[1];
+        hla = hs[2];
 #pragma unroll
-    for (uint32_t u = 0; u < kWaves; ++u) nd += wave_def[u];
-    for (uint32_t i = threadIdx.x; i < nd; i += kPairBlock) {  // up to 2 per lane
-      uint32_t k = i, u = 0;
-      while (k >= wave_def[u]) k -= wave_def[u++];
-      const uint32_t g = deferred[u][k];
-      int64_t m[P];
+        for (int p = 0; p < P; ++p) hm[p] = hs[3 + p];
+      } else if (act) {  // more flagged groups than hand-off slots: reload (rare)
+        hpi = a.pending_index[h];
+        hlc = a.last_committed[h];
+        hla = a.last_appended[h];
 #pragma unroll
-      for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
-      int64_t out;
-      uint8_t st;
-      decide_runs<P>(a, g, a.pending_index[g], a.last_appended[g], a.last_committed[g], m, out, st);
-      a.committed[g] = out;
-      a.status[g] = st;
+        for (int p = 0; p < P; ++p) hm[p] = a.match[static_cast<size_t>(p) * a.match_ld + h];
+      }
+      int64_t cand = kI64Min;
+      uint8_t st = 0;
+      if (act && hpi != 0) {
+        st = mask_out_of_range<P>(hm, hla);
+        const uint32_t r0 = a.run_off[h], nr = a.run_off[h + 1] - r0;
+        for (uint32_t rr = r; rr < nr; rr += 4) {  // runs_best (quorum_core.h), spread over the quad
+          const int64_t rs = a.run_start[r0 + rr];
+          const int64_t s = (rr == 0) ? hpi : (rs > hpi ? rs : hpi);
+          const int64_t e = (rr + 1 < nr) ? a.run_start[r0 + rr + 1] - 1 : hla;
+          const int64_t c = run_candidate<P>(hm, a.run_conf[r0 + rr], s, e < hla ? e : hla, st);
+          cand = c > cand ? c : cand;
+        }
+      }
+      cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 1)));
+      cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 2)));
+      uint32_t s32 = st;
+      s32 |= __shfl_xor(s32, 1);
+      s32 |= __shfl_xor(s32, 2);
+      if (act && r == 0) {
+        // decide_runs: not the leader -> unchanged (BallotBox.java:101-103)
+        a.committed[h] = hpi == 0 ? hlc : (cand > hlc ? cand : hlc);
+        a.status[h] = hpi == 0 ? kStNotLeader : static_cast<uint8_t>(s32);
+      }
     }
   }
   // odd G: the last group goes through the scalar decision
@@ -430,8 +478,10 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
   switch (args->num_peers) {
 #define JRQ_CASE(P)                                                                      \
   case P:                                                                                \
-    if (pair)                                                                            \
-      hipLaunchKernelGGL(jrq::quorum_epoch_pair_kernel<P>, grid, blk, 0, stream, *args); \
+    if (pair && a.run_off)                                                               \
+      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, true>), grid, blk, 0, stream, *args); \
+    else if (pair)                                                                       \
+      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, false>), grid, blk, 0, stream, *args); \
     else                                                                                 \
       hipLaunchKernelGGL(jrq::quorum_epoch_kernel<P>, grid, blk, 0, stream, *args);      \
     break;

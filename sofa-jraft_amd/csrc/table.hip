@@ -71,14 +71,17 @@ __device__ __forceinline__ int64_t table_run_lane(const JrqTableArgs& t, uint32_
 
 // One epoch over every group of the table.  1024-thread workgroups of 2048 groups (two per
 // lane, 16-B loads), 2 resident per CU.
-// Groups with a conf change inside their pending window (JRQ_CONF_RUNS) are skipped by the
-// single-conf pass and decided from the table's flagged lists (table_flags_kernel keeps them:
-// they change only with group headers): workgroup b's flagged groups, in its own slot range of
-// flag_list, are split over its 16 waves -- at 1 % flagged one or two groups per wave, four
-// lanes each (one conf run per lane).  The wave loads its slice's list entries before the
-// single-conf loads and walks the groups after its single-conf decisions: no LDS list of
-// flagged groups, no workgroup barrier in front of them, and a workgroup lists only its own
-// groups (at most 2048: the list segments' capacity).
+// A group with a conf change inside its pending window (JRQ_CONF_RUNS) is skipped by the
+// single-conf decision and walked by its own wave afterwards: its dynamic state (pendingIndex,
+// lastCommitted, lastAppended, match) is what its owner lane loaded, left in the wave's slice of
+// LDS (the first 16 flagged groups of a wave; a wave-local hand-off, no barrier), and its runs
+// come from the wave's flagged-entry slots (table_flags_kernel writes them with every header
+// update: only headers change runs), spread over a lane quad by shuffles, one conf run per lane
+// (the table holds at most 4).  The wave loads its count and its first two entries together
+// with its single-conf loads, so a flagged group costs no dependent round trip to memory and no
+// workgroup barrier (round 2 deferred flagged groups to an LDS list behind a barrier and
+// reloaded them: +25 % on C3 with 1 % flagged, tools/flag_probe.hip).  Beyond 16 flagged
+// groups in one wave the walk reloads the group from memory.
 // The one barrier left is the compaction's: list entries are staged per wave in LDS, and one
 // 64-bit atomic per workgroup ({done << 32 | entries}) on its segment's counter (workgroup b
 // -> segment b % kTableSegments: same-address atomics serialise, ~14 ns each,
@@ -87,23 +90,25 @@ __device__ __forceinline__ int64_t table_run_lane(const JrqTableArgs& t, uint32_
 template <int P>
 __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
   constexpr uint32_t kWaves = kTableBlock / 64;
-  constexpr uint32_t kStage = 2 * 64 + kTableBlockGroups / kWaves;  // fast path + walked
+  constexpr uint32_t kHand = 16;  // flagged groups per wave handed over through LDS
   __shared__ uint32_t wave_cnt[kWaves];
-  __shared__ uint64_t staged[kWaves][kStage];
+  __shared__ uint64_t staged[kWaves][128];
+  __shared__ int64_t hand[kWaves][kHand][P + 3];  // {pendingIndex word, lc, la, match[P]}
+  __shared__ __attribute__((aligned(16))) int64_t ent2[kWaves][2][8];  // entries 0 and 1
   __shared__ uint32_t blk_base;
-  const uint32_t pairs = (t.G + 1) >> 1;  // ld covers the pad group of an odd G (not a leader)
+  const uint32_t pairs = (t.G + 1) >> 1;
   const uint32_t tt = blockIdx.x * kTableBlock + threadIdx.x;
   const uint32_t g = tt << 1;
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
-  // this wave's slice [fs0, fs1) of the workgroup's flagged list, four lanes per group, 16
-  // groups per pass
-  const uint32_t nflag = __builtin_amdgcn_readfirstlane(t.flag_cnt[blockIdx.x]);
-  const uint32_t fbase = blockIdx.x * kTableBlockGroups;
-  const uint32_t fs0 = fbase + nflag * w / kWaves, fs1 = fbase + nflag * (w + 1) / kWaves;
-  const uint32_t fi = fs0 + (lane >> 2);
-  uint32_t h0 = fi < fs1 ? t.flag_list[fi] : 0u;  // the first pass's group, loaded up front
-  bool c0 = false, c1 = false;
+  // the wave's flagged groups: their count, and entries 0 and 1 copied straight to the wave's
+  // LDS slice (an LDS-DMA load: no registers held across the single-conf path)
+  const uint32_t wid = blockIdx.x * kWaves + w;
+  const uint32_t nflag = __builtin_amdgcn_readfirstlane(t.flag_wcnt[wid]);
+  const int64_t* const ent = reinterpret_cast<const int64_t*>(t.flag_ent) + static_cast<size_t>(wid) * kFlagSlots * 8;
+  if (nflag != 0 && lane < 8)  // lane l: bytes 16 l .. 16 l + 15 of entries 0-1
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ent + lane * 2), &ent2[w][0][0], 16, 0, 0);
+  bool c0 = false, c1 = false, f0 = false, f1 = false;
   uint64_t e0 = 0, e1 = 0;
   if (tt < pairs) {
     const i64x2 pr = tld2(t.pi + g);
@@ -115,13 +120,33 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
     for (int p = 0; p < P; ++p) mv[p] = tld2(t.match + static_cast<size_t>(p) * t.ld + g);
     const int64_t pi0 = pr.x == kPiFollowsLc ? lc.x + 1 : pr.x;
     const int64_t pi1 = pr.y == kPiFollowsLc ? lc.y + 1 : pr.y;
-    const bool f0 = static_cast<uint64_t>(cw.x) >> 63;
-    const bool f1 = static_cast<uint64_t>(cw.y) >> 63;
+    f0 = static_cast<uint64_t>(cw.x) >> 63;
+    f1 = static_cast<uint64_t>(cw.y) >> 63;
     int64_t m0[P], m1[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) {
       m0[p] = mv[p].x;
       m1[p] = mv[p].y;
+    }
+    // a flagged group's state -> the wave's hand-off slot of its rank (the flags kernel's
+    // entry order: the first groups of the pairs, then the second ones)
+    const uint64_t bf0 = __ballot(f0), bf1 = __ballot(f1);
+    const uint32_t k0 = __popcll(bf0 & below), k1 = __popcll(bf0) + __popcll(bf1 & below);
+    if (f0 && k0 < kHand) {
+      int64_t* hs = hand[w][k0];
+      hs[0] = pr.x;
+      hs[1] = lc.x;
+      hs[2] = la.x;
+#pragma unroll
+      for (int p = 0; p < P; ++p) hs[3 + p] = m0[p];
+    }
+    if (f1 && k1 < kHand) {
+      int64_t* hs = hand[w][k1];
+      hs[0] = pr.y;
+      hs[1] = lc.y;
+      hs[2] = la.y;
+#pragma unroll
+      for (int p = 0; p < P; ++p) hs[3 + p] = m1[p];
     }
     int64_t o0, o1;
     uint8_t s0, s1;
@@ -160,30 +185,64 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
   if (c0) staged[w][__popcll(b0 & below)] = e0;
   if (c1) staged[w][__popcll(b0) + __popcll(b1 & below)] = e1;
   uint32_t cnt = __popcll(b0) + __popcll(b1);
-  // the wave's flagged groups, 16 per pass (wave-uniform loop)
-  for (uint32_t base = fs0; base < fs1; base += 16) {
-    const uint32_t i = base + (lane >> 2), r = lane & 3u;
-    const bool act = i < fs1;
-    const uint32_t h = base == fs0 ? h0 : (act ? t.flag_list[i] : 0u);
-    int64_t cand = kI64Min, pr = 0, lc = 0, pi = 0;
+  // the walk: flagged group i of the wave on quad i % 16, one conf run per lane
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the hand-off slots: this wave's)
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t q = lane >> 2, r = lane & 3u;
+  for (uint32_t base = 0; base < nflag; base += 16) {  // (wave-uniform)
+    const uint32_t i = base + q;
+    const bool act = i < nflag;
+    // the entry {group, start1, start2, start3, conf0 .. conf3}: run r's start, the next run's
+    // start and run r's conf word (entries 0-1 from LDS, later ones from memory)
+    const int64_t* e = i < 2 ? &ent2[w][i][0] : ent + (act ? i : 0u) * 8;
+    const uint32_t h = act ? static_cast<uint32_t>(e[0]) : 0u;
+    const int64_t rs = r == 0 || !act ? kI64Min : e[r];
+    const int64_t nx = r == 3 || !act ? kI64Max : e[r + 1];
+    const uint64_t rc = act ? static_cast<uint64_t>(e[4 + r]) : 0ull;
+    int64_t cand = kI64Min, hpr = 0, hlc = 0, hla = 0, pi = 0;
     uint8_t st = 0;
-    if (act) cand = table_run_lane<P>(t, h, r, pr, lc, pi, st);
+    if (act) {
+      int64_t hm[P];
+      if (i < kHand) {  // from the owner lane, through LDS
+        const int64_t* hs = hand[w][i];
+        hpr = hs[0];
+        hlc = hs[1];
+        hla = hs[2];
+#pragma unroll
+        for (int p = 0; p < P; ++p) hm[p] = hs[3 + p];
+      } else {  // more flagged groups than hand-off slots: reload (rare)
+        hpr = t.pi[h];
+        hlc = t.lc[h];
+        hla = t.la[h];
+#pragma unroll
+        for (int p = 0; p < P; ++p) hm[p] = t.match[static_cast<size_t>(p) * t.ld + h];
+      }
+      pi = hpr == kPiFollowsLc ? hlc + 1 : hpr;
+      if (pi == 0) {
+        st = kStNotLeader;
+      } else {
+        st = mask_out_of_range<P>(hm, hla);
+        const int64_t s = rs > pi ? rs : pi;
+        const int64_t e = nx == kI64Max ? hla : nx - 1;
+        cand = run_candidate<P>(hm, rc, s, e < hla ? e : hla, st);
+      }
+    }
     cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 1)));
     cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 2)));
     uint32_t s32 = st;
     s32 |= __shfl_xor(s32, 1);
     s32 |= __shfl_xor(s32, 2);
-    const bool commit = act && r == 0 && cand > lc;  // pi == 0 (not the leader) gave kI64Min
+    const bool commit = act && r == 0 && cand > hlc;  // pi == 0 (not the leader): kI64Min
     if (act && r == 0) {
       if (t.status) t.status[h] = static_cast<uint8_t>(s32);
-      if (commit) table_commit_one(t, h, pr, cand);
+      if (commit) table_commit_one(t, h, hpr, cand);
     }
     const uint64_t bc = __ballot(commit);
     if (commit) staged[w][cnt + __popcll(bc & below)] = (static_cast<uint64_t>(cand - pi + 1) << 32) | h;
     cnt += __popcll(bc);
   }
   if (lane == 0) wave_cnt[w] = cnt;
-  __syncthreads();
+  lds_barrier();  // (the results' stores stay in flight)
   const uint32_t seg = blockIdx.x % kTableSegments;
   if (threadIdx.x == 0) {
     uint32_t tot = 0;
@@ -196,23 +255,25 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
       atomicExch(t.ctr + seg, 0ull);
     }
   }
-  __syncthreads();
+  lds_barrier();
   uint32_t pos = blk_base;
   for (uint32_t u = 0; u < w; ++u) pos += wave_cnt[u];
   for (uint32_t i = lane; i < cnt; i += 64) t.changed[pos + i] = staged[w][i];
 }
 
-// The flagged lists: per range of kTableBlockGroups groups (one epoch workgroup's), its groups
-// whose conf word carries JRQ_CONF_RUNS at flag_list[b * kTableBlockGroups ...] and their count
-// at flag_cnt[b].  Rebuilt after every update that carries group headers (only headers change
-// a flag); one workgroup per range, no atomics.
+// The flagged-entry slots: per 128-group wave range of the epoch kernel, its groups flagged
+// JRQ_CONF_RUNS, each as a 64-B entry {group, start1 | start2, start3 | conf0, conf1 | conf2,
+// conf3} (run starts and conf words; unused runs: start INT64_MAX, conf 0), and their count.
+// Rebuilt after every update that carries group headers (only headers change runs and flags);
+// the waves map exactly as the epoch kernel's (1024-thread workgroups, two groups per lane),
+// no barrier, no atomics.
 constexpr uint32_t kFlagBlock = kTableBlockGroups / 2;
 __global__ __launch_bounds__(kFlagBlock) void table_flags_kernel(JrqTableArgs t) {
-  __shared__ uint32_t wave_cnt[kFlagBlock / 64];
   const uint32_t pairs = (t.G + 1) >> 1;
   const uint32_t tt = blockIdx.x * kFlagBlock + threadIdx.x;
   const uint32_t g = tt << 1;
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wid = blockIdx.x * (kFlagBlock / 64) + (threadIdx.x >> 6);
   bool f0 = false, f1 = false;
   if (tt < pairs) {
     const i64x2 cw = tld2(reinterpret_cast<const int64_t*>(t.conf) + g);
@@ -221,16 +282,18 @@ __global__ __launch_bounds__(kFlagBlock) void table_flags_kernel(JrqTableArgs t)
   }
   const uint64_t below = (1ull << lane) - 1ull;
   const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
-  if (lane == 0) wave_cnt[w] = __popcll(b0) + __popcll(b1);
-  __syncthreads();
-  uint32_t pos = blockIdx.x * kTableBlockGroups, tot = 0;
-  for (uint32_t u = 0; u < kFlagBlock / 64; ++u) {
-    if (u == w) pos += tot;
-    tot += wave_cnt[u];
-  }
-  if (f0) t.flag_list[pos + __popcll(b0 & below)] = g;
-  if (f1) t.flag_list[pos + __popcll(b0) + __popcll(b1 & below)] = g + 1;
-  if (threadIdx.x == 0) t.flag_cnt[blockIdx.x] = tot;
+  int64_t* const ent = reinterpret_cast<int64_t*>(t.flag_ent) + static_cast<size_t>(wid) * kFlagSlots * 8;
+  auto put = [&](uint32_t k, uint32_t h) {
+    int64_t* e = ent + k * 8;
+    e[0] = h;
+    for (int r = 1; r < kTableMaxRuns; ++r) e[r] = t.xstart[static_cast<size_t>(r - 1) * t.ld + h];
+    e[4] = static_cast<int64_t>(t.conf[h] & ~kConfRuns);
+    for (int r = 1; r < kTableMaxRuns; ++r)
+      e[4 + r] = static_cast<int64_t>(t.xconf[static_cast<size_t>(r - 1) * t.ld + h]);
+  };
+  if (f0) put(__popcll(b0 & below), g);
+  if (f1) put(__popcll(b0) + __popcll(b1 & below), g + 1);
+  if (lane == 0) t.flag_wcnt[wid] = __popcll(b0) + __popcll(b1);
 }
 
 // Group headers: one lane per header (a group appears at most once per call).

@@ -44,25 +44,35 @@ typedef uint32_t v2u32x4 __attribute__((ext_vector_type(4)));
 // include/jrq.h jrq_v2_status
 constexpr uint8_t kV2Ok = 0, kV2Null = 1, kV2V1 = 2, kV2Host = 3;
 
+// A record's bytes through a one-line cache: a miss loads the whole aligned 64-B line (four
+// independent 16-B loads, one round trip) -- a V2 header (magic, type, term, index, the data
+// tag and length) mostly fits one line, where 16-B chunks cost one dependent round trip each.
 struct ChunkReader {
   const uint8_t* rec;  // record start
   int64_t limit;       // record length
-  uintptr_t chunk_addr;
-  v2u32x4 chunk;
+  uintptr_t line_addr;
+  v2u32x4 c0, c1, c2, c3;
   bool err;
   __device__ explicit ChunkReader(const uint8_t* r, int64_t len)
-      : rec(r), limit(len), chunk_addr(~static_cast<uintptr_t>(0)), err(false) {}
-  // byte at record position pos (< limit): its 16-B granule holds a valid byte, so the
-  // aligned load never leaves the mapped buffer
+      : rec(r), limit(len), line_addr(~static_cast<uintptr_t>(0)), err(false) {}
+  // byte at record position pos (< limit): its 64-B line holds a valid byte and lies in one
+  // 4 KiB page with it, so the aligned loads never leave the mapped buffer
   __device__ __forceinline__ uint32_t at(int64_t pos) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(rec) + static_cast<uintptr_t>(pos);
-    const uintptr_t ca = a & ~static_cast<uintptr_t>(15);
-    if (ca != chunk_addr) {
-      chunk = *reinterpret_cast<const v2u32x4*>(ca);
-      chunk_addr = ca;
+    const uintptr_t la = a & ~static_cast<uintptr_t>(63);
+    if (la != line_addr) {
+      const v2u32x4* p = reinterpret_cast<const v2u32x4*>(la);
+      c0 = p[0];
+      c1 = p[1];
+      c2 = p[2];
+      c3 = p[3];
+      line_addr = la;
     }
-    const uint32_t o = static_cast<uint32_t>(a & 15u);
-    const uint32_t w = o < 8 ? (o < 4 ? chunk[0] : chunk[1]) : (o < 12 ? chunk[2] : chunk[3]);
+    // (selects on scalars: a dynamically indexed vector would live in scratch memory)
+    const uint32_t o = static_cast<uint32_t>(a & 63u), d = o >> 2, q = d & 3u, h = d >> 2;
+    auto sel4 = [q](v2u32x4 v) { return q < 2 ? (q == 0 ? v.x : v.y) : (q == 2 ? v.z : v.w); };
+    const uint32_t w0 = sel4(c0), w1 = sel4(c1), w2 = sel4(c2), w3 = sel4(c3);
+    const uint32_t w = h < 2 ? (h == 0 ? w0 : w1) : (h == 2 ? w2 : w3);
     return (w >> (8 * (o & 3u))) & 0xFFu;
   }
 };

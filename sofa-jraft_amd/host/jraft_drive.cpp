@@ -21,7 +21,8 @@
 // jraft_drive_latency -- steady load with the background flusher (GroupBatch::startFlusher):
 //   `threads` producers loop over their groups, one entry per group per pass
 //   (appendPendingTask, then every peer's commitAt of it); onCommitted(c) measures the time
-//   from the quorum-completing ack of entry c to the callback.
+//   from the quorum-completing ack of entry c to the callback.  flush() packs and delivers on
+//   `flush_threads` threads (0: its default), beside the producers.
 // Peer p of every group is PeerId("127.0.0.1", 8001 + p); conf words name peer slots by bit.
 #include <algorithm>
 #include <atomic>
@@ -243,13 +244,16 @@ int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t 
 }
 
 // out[0] commits (onCommitted calls), 1 entries appended, 2 commitAt calls, 3 seconds,
-// 4 flushes, 5 p50 latency us, 6 p90, 7 p99, 8 p99.9, 9 max, 10 latency samples
-int jraft_drive_latency(int device, uint32_t G, uint32_t P, uint32_t threads, double seconds,
-                        uint32_t max_delay_us, uint32_t max_dirty, double* out) {
+// 4 flushes, 5 p50 latency us, 6 p90, 7 p99, 8 p99.9, 9 max, 10 latency samples, 11 producer
+// duty cycle (busy / wall)
+int jraft_drive_latency(int device, uint32_t G, uint32_t P, uint32_t threads, uint32_t flush_threads,
+                        double seconds, uint32_t max_delay_us, uint32_t max_dirty, uint32_t pass_us,
+                        double* out) {
   try {
     const unsigned T = std::max(1u, std::min(threads, G));
     jraft::Engine eng(device, G, static_cast<uint8_t>(P));
     auto batch = std::make_shared<jraft::GroupBatch>(&eng, G, P);
+    if (flush_threads) batch->setFlushThreads(flush_threads);
     std::vector<jraft::BallotBox> boxes;
     boxes.reserve(G);
     std::vector<jraft::PeerId> peers;
@@ -288,6 +292,7 @@ int jraft_drive_latency(int device, uint32_t G, uint32_t P, uint32_t threads, do
     batch->flush();  // the first flush ships every group's header
     std::atomic<bool> stop{false};
     std::vector<uint64_t> entries(T, 0);
+    std::vector<int64_t> busyNs(T, 0);
     batch->startFlusher(jraft::FlushPolicy{max_delay_us, max_dirty});
     const int64_t t0 = nowNs();
     {
@@ -300,7 +305,9 @@ int jraft_drive_latency(int device, uint32_t G, uint32_t P, uint32_t threads, do
         const uint32_t g0 = static_cast<uint32_t>(static_cast<uint64_t>(G) * t / T);
         const uint32_t g1 = static_cast<uint32_t>(static_cast<uint64_t>(G) * (t + 1) / T);
         uint64_t n = 0;
+        int64_t busy = 0;
         for (int64_t idx = 1; !stop.load(std::memory_order_relaxed); ++idx) {
+          const int64_t p0 = nowNs();
           for (uint32_t g = g0; g < g1; ++g) {
             if (!boxes[g].appendPendingTasks(conf, nullptr, 1)) throw std::runtime_error("append refused");
             for (uint32_t p = 0; p < P; ++p) boxes[g].commitAt(idx, idx, peers[p]);
@@ -308,8 +315,15 @@ int jraft_drive_latency(int device, uint32_t G, uint32_t P, uint32_t threads, do
             ackIdx[g].store(idx, std::memory_order_release);
             ++n;
           }
+          const int64_t spent = nowNs() - p0;
+          busy += spent;
+          // paced producers: one pass per pass_us (the replicators' acks arrive with the network,
+          // they do not spin); a busy loop would also hit the box's cgroup CPU quota
+          if (pass_us && spent < static_cast<int64_t>(pass_us) * 1000)
+            std::this_thread::sleep_for(std::chrono::nanoseconds(static_cast<int64_t>(pass_us) * 1000 - spent));
         }
         entries[t] = n;
+        busyNs[t] = busy;
       });
       timer.join();
     }
@@ -336,6 +350,9 @@ int jraft_drive_latency(int device, uint32_t G, uint32_t P, uint32_t threads, do
     out[8] = q(0.999);
     out[9] = all.empty() ? 0.0 : all.back();
     out[10] = static_cast<double>(all.size());
+    double busy = 0;
+    for (int64_t b : busyNs) busy += static_cast<double>(b);
+    out[11] = busy * 1e-9 / (secs * T);  // the producers' duty cycle
     return 0;
   } catch (const std::exception& ex) {
     g_err = ex.what();

@@ -13,6 +13,8 @@
 #include <sstream>
 #include <thread>
 
+#include <sched.h>
+
 namespace jraft {
 
 namespace {
@@ -370,6 +372,28 @@ struct GroupBatch::Pool {
   bool stop = false;
 };
 
+// CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota (a container
+// sees every CPU of the host in hardware_concurrency()).
+static unsigned usableCpus() {
+  unsigned n = std::max(1u, std::thread::hardware_concurrency());
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = std::max(1, CPU_COUNT(&set));
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long period = 0;
+    if (std::fscanf(f, "%31s %lld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+      n = std::min<unsigned>(n, std::max<long long>(1, std::atoll(q) / period));
+    std::fclose(f);
+  }
+  return n;
+}
+
+void GroupBatch::setFlushThreads(unsigned n) {
+  std::lock_guard<std::mutex> fl(flushMu_);
+  pool_.reset();
+  poolSize_ = std::max(1u, std::min(n, 64u));
+}
+
 // f(part, begin, end) over [0, n) on the pool, only when each part gets at least `grain` items.
 template <class F>
 void GroupBatch::parallelFor(size_t n, size_t grain, F&& f) {
@@ -377,9 +401,8 @@ void GroupBatch::parallelFor(size_t n, size_t grain, F&& f) {
     f(0u, size_t(0), n);
     return;
   }
-  if (!pool_) {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    pool_.reset(new Pool(std::min(16u, hw)));  // the box's CPU share per GPU
+  if (!pool_) {  // default: the box's CPU share per GPU, at most 16
+    pool_.reset(new Pool(poolSize_ ? poolSize_ : std::min(16u, usableCpus())));
   }
   const size_t parts = std::min<size_t>(pool_->size(), n / grain);
   pool_->run([&](unsigned i, unsigned) {
@@ -635,7 +658,7 @@ uint32_t GroupBatch::flushLocked() {
   const size_t nd = pre[nl];
   // pack: the dirty groups split into contiguous ranges of the concatenated lists
   const size_t kGrain = 1u << 12;
-  const size_t nparts = std::max<size_t>(1, std::min<size_t>(16, nd / kGrain));
+  const size_t nparts = std::max<size_t>(1, std::min<size_t>(64, nd / kGrain));
   if (parts_.size() < nparts) parts_.resize(nparts);
   for (auto& p : parts_) p.ns = p.nr = 0;
   parallelFor(nd, kGrain, [&](unsigned part, size_t b, size_t e) {

@@ -260,6 +260,9 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   void startFlusher(const FlushPolicy& policy);
   void stopFlusher();
   uint64_t flushCount() const { return flushes_.load(std::memory_order_relaxed); }
+  // Threads flush() packs and delivers on (default: the CPUs this process may use, cgroup
+  // quota included, at most 16).
+  void setFlushThreads(unsigned n);
 
  private:
   friend class BallotBox;
@@ -335,6 +338,7 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   std::atomic<uint64_t> flushes_{0};
   FlushStats stats_;
   std::unique_ptr<Pool> pool_;
+  unsigned poolSize_ = 0;
   std::unique_ptr<Flusher> flusher_;
 };
 

@@ -29,8 +29,9 @@ def load():
         d.jraft_drive_epochs.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.c_uint32] + [C.c_void_p] * 9
         d.jraft_drive_latency.restype = C.c_int
-        d.jraft_drive_latency.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double,
-                                          C.c_uint32, C.c_uint32, C.c_void_p]
+        d.jraft_drive_latency.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                          C.c_double, C.c_uint32, C.c_uint32, C.c_uint32,
+                                          C.c_void_p]
         _drv = d
     return _drv
 
@@ -56,18 +57,20 @@ def drive_epochs(device: int, s: dict, threads: int = 1):
 
 
 LATENCY = ("commits", "entries", "acks", "seconds", "flushes", "p50_us", "p90_us", "p99_us",
-           "p999_us", "max_us", "samples")
+           "p999_us", "max_us", "samples", "producer_duty")
 
 
 def drive_latency(device: int, groups: int, peers: int, threads: int, seconds: float,
-                  max_delay_us: int, max_dirty: int) -> dict:
+                  max_delay_us: int, max_dirty: int, flush_threads: int = 0, pass_us: int = 0) -> dict:
     """Steady load through BallotBox with the background flusher (GroupBatch::startFlusher,
     FlushPolicy{max_delay_us, max_dirty}): `threads` producers append one entry per group and
-    every peer acks it; returns counts and the ack -> onCommitted latency quantiles (us)."""
+    every peer acks it, flush() runs on `flush_threads` threads (0 = its default); returns
+    counts and the ack -> onCommitted latency quantiles (us).  pass_us > 0 paces each producer
+    to one pass over its groups per pass_us."""
     d = load()
     out = np.zeros(len(LATENCY), np.float64)
-    rc = d.jraft_drive_latency(device, groups, peers, threads, seconds, max_delay_us, max_dirty,
-                               C.c_void_p(out.ctypes.data))
+    rc = d.jraft_drive_latency(device, groups, peers, threads, flush_threads, seconds,
+                               max_delay_us, max_dirty, pass_us, C.c_void_p(out.ctypes.data))
     if rc != 0:
         raise RuntimeError("jraft_drive_latency: " + (d.jraft_drive_last_error() or b"").decode())
     return dict(zip(LATENCY, out.tolist()))

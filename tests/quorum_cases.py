@@ -28,7 +28,7 @@ def random_conf(rng, P, allow_empty=True):
     return conf_word(new, random_mask(rng, P, no))
 
 
-def random_batch(seed, G, P, pend_max=64, run_prob=0.5, edge=True):
+def random_batch(seed, G, P, pend_max=64, run_prob=0.5, edge=True, max_runs=4):
     rng = np.random.default_rng(seed)
     pi = rng.integers(1, 1 << 20, G).astype(np.int64)
     npend = rng.integers(0, pend_max + 1, G)
@@ -49,12 +49,12 @@ def random_batch(seed, G, P, pend_max=64, run_prob=0.5, edge=True):
         oor = rng.random(G) < 0.03  # an ack past lastAppended
         rows = np.where(oor)[0]
         match[rng.integers(0, P, len(rows)), rows] = la[rows] + 1 + rng.integers(0, 5, len(rows))
-    # conf runs: 1..4 runs per group over the pending window
+    # conf runs: 2..max_runs runs per flagged group over the pending window
     run_off = [0]
     run_start, run_conf = [], []
     use_runs = rng.random(G) < run_prob
     for g in range(G):
-        nr = int(rng.integers(2, 5)) if use_runs[g] else 1
+        nr = int(rng.integers(2, max_runs + 1)) if use_runs[g] else 1
         starts = sorted(set(int(x) for x in rng.integers(pi[g], max(pi[g] + 1, la[g] + 2), nr - 1)))
         run_start.append(int(pi[g]) - int(rng.integers(0, 5)))  # first start <= pendingIndex
         run_conf.append(int(conf[g]))

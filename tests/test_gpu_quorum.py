@@ -188,15 +188,18 @@ def _to_dev(b, keys):
                                                      else b[k])).to(dev) for k in keys}
 
 
-@pytest.mark.parametrize("P,run_prob", [(5, 0.01), (3, 0.3), (8, 0.05)])
-def test_dev_fast_path_with_flagged_runs(engine, oracle, P, run_prob):
+@pytest.mark.parametrize("P,run_prob,max_runs,G", [(5, 0.01, 4, 4096), (3, 0.3, 4, 4096),
+                                                   (8, 0.05, 4, 4096), (5, 0.9, 9, 4098),
+                                                   (16, 0.5, 6, 1030), (1, 0.2, 3, 2048)])
+def test_dev_fast_path_with_flagged_runs(engine, oracle, P, run_prob, max_runs, G):
     """Device batch with aligned arrays (pair kernel) where only JRQ_CONF_RUNS groups walk the
     run table: a conf-changing group no longer demotes the launch, and every group -- flagged
-    or not -- matches the replay through real BallotBoxes."""
+    or not -- matches the replay through real BallotBoxes.  Each wave walks its own flagged
+    groups, four lanes per group: 90 % flagged puts more than the 16 LDS hand-off slots'
+    worth in a wave (the reload path), up to 9 runs loops a lane over runs r, r + 4, r + 8."""
     import torch
     from quorum_cases import flag_runs
-    G = 4096
-    b = random_batch(500 + P, G, P, run_prob=run_prob)
+    b = random_batch(500 + P, G, P, run_prob=run_prob, max_runs=max_runs)
     b["conf"] = flag_runs(b)
     ce, se = _replay(oracle, b)
     t = _to_dev(b, ["match", "pending_index", "last_appended", "last_committed", "conf",

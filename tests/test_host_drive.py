@@ -94,7 +94,7 @@ def test_flusher_latency_small():
     within the policy's delay plus one epoch."""
     from jraft_amd import drive
     r = drive.drive_latency(0, groups=4096, peers=3, threads=4, seconds=1.0, max_delay_us=500,
-                            max_dirty=1 << 14)
+                            max_dirty=1 << 14, flush_threads=2, pass_us=2000)
     assert r["entries"] > 4096 and r["commits"] > 0 and r["samples"] > 0
     assert r["flushes"] > 10
     assert r["p50_us"] < 50_000, r

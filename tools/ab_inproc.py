@@ -3,7 +3,8 @@
 side (ctypes, its own engine on the shared stream), and the legs run interleaved round by
 round, so box-to-box and warm-up drift fall on every variant alike.
 
-  python tools/ab_inproc.py NAME=PATH.so[:ENV=V,...] [...]   (ENV: engine knobs, e.g. JRQ_CRC_SEG_BYTES)
+  python tools/ab_inproc.py NAME=PATH.so[:OPT=V,...] [...]   (OPT: jrq_debug_set options by
+  name, e.g. CRC_SEG_BYTES=4096 -> jrq_debug_set(e, JRQ_DBG_CRC_SEG_BYTES, 4096))
 
 Per leg and variant: the median over rounds of (one event pair around `reps` back-to-back
 launches) / reps, and whether the outputs equal the first variant's.  A torch int64 sum over
@@ -58,17 +59,11 @@ def main():
     for sp in specs:
         name, _, rest = sp.partition("=")
         path, _, envs = rest.partition(":")
-        saved = {}
-        for kv in filter(None, envs.split(",")):  # engine knobs read at jrq_create
-            k, _, v = kv.partition("=")
-            saved[k] = os.environ.get(k)
-            os.environ[k] = v
         e = load_variant(path)
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        for kv in filter(None, envs.split(",")):  # per-engine overrides (jrq_debug_set)
+            k, _, v = kv.partition("=")
+            if e._L.jrq_debug_set(e._h, getattr(L, "DBG_" + k), int(v)) != 0:
+                raise RuntimeError(f"{name}: jrq_debug_set {k}={v} refused")
         e._L.jrq_set_stream(e._h, C.c_void_p(s.cuda_stream))
         variants.append((name, e))
 

@@ -33,9 +33,8 @@ for s in $STEPS; do
              done
            done ;;
     host)  run host_test 300 ./tests/_build/host_test gpu ;;
-    probe) run mem_probe 300 ./tools/mem_probe ;;
     tprobe) run table_probe 120 ./tools/table_probe ;;
+    fprobe) run flag_probe 120 ./tools/flag_probe ;;
     eprobe) run epochs_probe 120 ./tools/epochs_probe ;;
-    sweep) run crc_sweep 600 python tools/crc_sweep.py ${SWEEP_VARIANTS:-} ;;
   esac
 done

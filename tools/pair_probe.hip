@@ -137,7 +137,7 @@ int main() {
   };
   const uint32_t pairs = G / 2;
   time("product", [&](const JrqQuorumArgs& a) {
-    hipLaunchKernelGGL(jrq::quorum_epoch_pair_kernel<5>, dim3((pairs + 511) / 512), dim3(512), 0, 0, a);
+    hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<5, false>), dim3((pairs + 511) / 512), dim3(512), 0, 0, a);
   });
   for (int n : {2, 4, 8}) {
     char nm[16];
@@ -150,7 +150,7 @@ int main() {
     hipLaunchKernelGGL(probe::quad_kernel<5>, dim3((G / 4 + 511) / 512), dim3(512), 0, 0, a);
   });
   time("product2", [&](const JrqQuorumArgs& a) {
-    hipLaunchKernelGGL(jrq::quorum_epoch_pair_kernel<5>, dim3((pairs + 511) / 512), dim3(512), 0, 0, a);
+    hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<5, false>), dim3((pairs + 511) / 512), dim3(512), 0, 0, a);
   });
   return 0;
 }

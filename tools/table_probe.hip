@@ -226,7 +226,7 @@ int main() {
   q.status = status;
   q.G = G;
   const dim3 pgrid(G / 2 / jrq::kPairBlock), pblk(jrq::kPairBlock);
-  run("pair", [&] { hipLaunchKernelGGL(jrq::quorum_epoch_pair_kernel<5>, pgrid, pblk, 0, 0, q); });
+  run("pair", [&] { hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<5, false>), pgrid, pblk, 0, 0, q); });
   const uint32_t np = G / 2;
   run("pv_256_u1", [&] { hipLaunchKernelGGL((probe::pair_variant<5, 256, 1>), dim3(np / 256), dim3(256), 0, 0, q); });
   run("pv_512_u1", [&] { hipLaunchKernelGGL((probe::pair_variant<5, 512, 1>), dim3(np / 512), dim3(512), 0, 0, q); });
@@ -234,7 +234,7 @@ int main() {
   run("pv_256_u2", [&] { hipLaunchKernelGGL((probe::pair_variant<5, 256, 2>), dim3(np / 512), dim3(256), 0, 0, q); });
   run("pv_256_u4", [&] { hipLaunchKernelGGL((probe::pair_variant<5, 256, 4>), dim3(np / 1024), dim3(256), 0, 0, q); });
   run("pv_512_u2", [&] { hipLaunchKernelGGL((probe::pair_variant<5, 512, 2>), dim3(np / 1024), dim3(512), 0, 0, q); });
-  run("pair_again", [&] { hipLaunchKernelGGL(jrq::quorum_epoch_pair_kernel<5>, pgrid, pblk, 0, 0, q); });
+  run("pair_again", [&] { hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<5, false>), pgrid, pblk, 0, 0, q); });
   run("product2", [&] { hipLaunchKernelGGL(jrq::table_epoch_kernel<5>, grid, blk, 0, 0, a); });
   CK(hipDeviceSynchronize());
   return 0;
