@@ -678,8 +678,11 @@ def leg_drive(ctx, args, G):
             "first_epoch_flush_ms": float(st["flush_ms"][0]),
             "bit_exact_vs_stateless_kernel": ok}
     lats = {}
-    for lg, prod, fl, delay, pace in ((G, 8, 8, 1000, 100_000), (1 << 16, 4, 4, 500, 10_000)):
-        lat = drive.drive_latency(ctx.dev.index, lg, 5, prod, 2.0, delay, 1 << 16, flush_threads=fl,
+    # (1M groups at one entry per group per second -- 1M entries/s, 5M acks/s -- and at ten:
+    # the producers then run at ~90 % duty and contend with the flush for every group's lines)
+    for lg, prod, fl, delay, pace, secs in ((G, 8, 8, 1000, 1_000_000, 3.0), (G, 8, 8, 1000, 100_000, 2.0),
+                                            (1 << 16, 4, 4, 500, 10_000, 2.0)):
+        lat = drive.drive_latency(ctx.dev.index, lg, 5, prod, secs, delay, 1 << 16, flush_threads=fl,
                                   pass_us=pace)
         lat.update({"groups": lg, "producer_threads": prod, "flush_threads": fl,
                     "producer_pass_us": pace,
@@ -687,7 +690,8 @@ def leg_drive(ctx, args, G):
                     "commits_per_s": lat["commits"] / lat["seconds"],
                     "api_calls_per_s": (lat["entries"] + lat["acks"]) / lat["seconds"],
                     "flushes_per_s": lat["flushes"] / lat["seconds"]})
-        lats[f"{lg}_groups"] = lat
+        lat["entries_per_s"] = lat["entries"] / lat["seconds"]
+        lats[f"{lg}_groups_pass_{pace // 1000}ms"] = lat
     lats["how"] = ("producer threads loop over their slices of the groups -- one pass per "
                    "producer_pass_us (paced: acks arrive with the network; spinning producers also "
                    "hit the box's cgroup CPU quota, whose throttling then sets the latency) -- "

@@ -107,6 +107,9 @@ __device__ __forceinline__ i64x2 ld2nt(const int64_t* p) {
 // deferred flagged groups to a workgroup list behind __syncthreads() -- which also waits for
 // every store of the fast path -- and reloaded them.  Without run tables the kernel is the
 // kRuns = false instantiation: no LDS, no walk.
+// The single-conf decision runs in 32-bit arithmetic relative to pendingIndex
+// (decide_single_rel, quorum_core.h: C3 16.4 -> 15.6 us per epoch in tools/pair_probe.hip,
+// against 15.1 us for the loads and stores alone).
 constexpr uint32_t kPairBlock = 512;
 
 template <int P, bool kRuns>
@@ -120,6 +123,7 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
   bool f0 = false, f1 = false;
+  bool slow = false;  // a group outside decide_single_rel's domain (never in a real batch)
   if (t < pairs) {
     const uint32_t g = t << 1;
     const i64x2 pi = ld2nt(a.pending_index + g);
@@ -156,8 +160,9 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
     }
     int64_t o0, o1;
     uint8_t s0, s1;
-    decide_single<P>(pi.x, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
-    decide_single<P>(pi.y, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
+    decide_single_rel<P>(pi.x, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
+    decide_single_rel<P>(pi.y, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
+    slow = !(rel_domain(pi.x, la.x) && rel_domain(pi.y, la.y));
     if (!f0 && !f1) {
       i64x2 out;
       out.x = o0;
@@ -223,6 +228,24 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
         a.committed[h] = hpi == 0 ? hlc : (cand > hlc ? cand : hlc);
         a.status[h] = hpi == 0 ? kStNotLeader : static_cast<uint8_t>(s32);
       }
+    }
+  }
+  // groups outside the 32-bit domain: decided again with 64-bit arithmetic from reloaded
+  // words, after (and over) the fast path's stores -- a wave-uniform branch, never taken by a
+  // real batch, kept out of the fast path's registers
+  if (__builtin_expect(__ballot(slow) != 0, 0) && slow) {
+#pragma unroll 1
+    for (uint32_t g = t << 1; g < (t << 1) + 2; ++g) {
+      if (kRuns && (a.conf[g] & kConfRuns)) continue;  // (the walk decided it, exactly)
+      int64_t m[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
+      int64_t out;
+      uint8_t st;
+      decide_single<P>(a.pending_index[g], a.last_appended[g], a.last_committed[g], a.conf[g], m,
+                       out, st);
+      a.committed[g] = out;
+      a.status[g] = st;
     }
   }
   // odd G: the last group goes through the scalar decision

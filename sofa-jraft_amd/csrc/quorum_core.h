@@ -68,6 +68,96 @@ __device__ __forceinline__ void decide_single(int64_t pi, int64_t la, int64_t lc
   st_out = pi == 0 ? kStNotLeader : st;
 }
 
+// The same decision in 32-bit arithmetic relative to pendingIndex, for every group whose
+// pending window [pi, la] holds fewer than 2^32 - 1 entries (every real group).  Only match
+// values inside the window can grant a pending entry, so each peer maps to r = m - pi + 1 in
+// [1, W] (W = la - pi + 1, 0 when nothing is pending) or to 0 (below the window, or past
+// lastAppended: out of range).  The map is monotone, so it commutes with the q-th-largest and
+// the min of the conf words' bounds, and "candidate >= pendingIndex" becomes r >= 1.  The q-th
+// largest member: the members' r (others 0) sorted by an odd-even transposition network of u32
+// max / min, then element q - 1 (0 when fewer than q members: nothing granted).  Per pair of
+// groups ~300 VALU instead of ~540 for kth_largest's P^2 64-bit compares (tools/pair_probe.hip).
+template <int P>
+__device__ __forceinline__ uint32_t kth_largest_rel(const uint32_t (&r)[P], uint32_t mask, uint32_t q) {
+  uint32_t s[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) s[p] = ((mask >> p) & 1u) ? r[p] : 0u;
+#pragma unroll
+  for (int round = 0; round < P; ++round) {
+#pragma unroll
+    for (int i = round & 1; i + 1 < P; i += 2) {
+      const uint32_t hi = s[i] > s[i + 1] ? s[i] : s[i + 1];
+      const uint32_t lo = s[i] > s[i + 1] ? s[i + 1] : s[i];
+      s[i] = hi;
+      s[i + 1] = lo;
+    }
+  }
+  uint32_t out = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) out = q == static_cast<uint32_t>(p + 1) ? s[p] : out;
+  return out;
+}
+
+// decide_single inside rel_domain (pi = 0: not the leader; la < pi: nothing pending, W = 0).
+// With pi < 2^62 a match below the window (negative ones included) wraps to d >= 2^62 > W:
+// no false grant from any int64 match value.  Two steps, so a caller deciding several groups
+// can map all of them first and let their 64-bit match words die before the sorting networks.
+template <int P>
+struct RelGroup {
+  uint32_t r[P];  // per slot: m - pi + 1 inside the window, else 0
+  uint32_t W;     // pending entries
+  uint8_t st;     // out-of-range flags
+};
+
+template <int P>
+__device__ __forceinline__ void rel_map(int64_t pi, int64_t la, const int64_t (&m)[P], RelGroup<P>& g) {
+  g.W = la >= pi ? static_cast<uint32_t>(la - pi) + 1u : 0u;
+  g.st = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const uint64_t d = static_cast<uint64_t>(m[p]) - static_cast<uint64_t>(pi);
+    g.st |= m[p] > la ? kStOutOfRange : 0;
+    g.r[p] = d < g.W ? static_cast<uint32_t>(d) + 1u : 0u;
+  }
+}
+
+template <int P>
+__device__ __forceinline__ void rel_decide(int64_t pi, int64_t lc, uint64_t cw, const RelGroup<P>& g,
+                                           int64_t& out, uint8_t& st_out) {
+  uint8_t st = g.st;
+  if ((cw & 0xFFFFu) == 0 && g.W != 0) st |= kStEmptyConf;
+  const uint32_t nmask = static_cast<uint32_t>(cw & 0xFFFFu);
+  const uint32_t omask = static_cast<uint32_t>((cw >> 16) & 0xFFFFu);
+  const uint32_t nq = static_cast<uint32_t>((cw >> 32) & 0xFFu);
+  const uint32_t oq = static_cast<uint32_t>((cw >> 40) & 0xFFu);
+  const uint32_t kn = nq == 0 ? g.W : kth_largest_rel<P>(g.r, nmask, nq);
+  const uint32_t ko = oq == 0 ? g.W : kth_largest_rel<P>(g.r, omask, oq);
+  uint32_t cand = kn < ko ? kn : ko;
+  cand = cand < g.W ? cand : g.W;
+  const int64_t c = pi - 1 + static_cast<int64_t>(cand);
+  // commitAt returns false when not the leader (BallotBox.java:101-103): state unchanged
+  out = (pi != 0 && cand >= 1u && c > lc) ? c : lc;
+  st_out = pi == 0 ? kStNotLeader : st;
+}
+
+template <int P>
+__device__ __forceinline__ void decide_single_rel(int64_t pi, int64_t la, int64_t lc, uint64_t cw,
+                                                  const int64_t (&m)[P], int64_t& out, uint8_t& st_out) {
+  RelGroup<P> g;
+  rel_map<P>(pi, la, m, g);
+  rel_decide<P>(pi, lc, cw, g, out, st_out);
+}
+
+// The domain of decide_single_rel: not the leader (pi = 0), or a leader with pendingIndex
+// below 2^62 and a window of at most 2^32 - 1 entries -- every real group.  Callers route the rest (negative
+// or huge indexes, 4-billion-entry windows) through the 64-bit decide_single, outside their
+// fast path: the pair kernel in a second pass, the table by flagging them for its run walk.
+__device__ __forceinline__ bool rel_domain(int64_t pi, int64_t la) {
+  return pi == 0 ||  // not the leader: lastCommitted, whatever the window
+         (pi > 0 && pi < (int64_t{1} << 62) &&
+          (la < pi || static_cast<uint64_t>(la - pi) <= 0xFFFFFFFEull));
+}
+
 // Runs of one group, in order: run r covers [start(r), start(r+1)) (the last run ends at
 // lastAppended, the first starts at or before pendingIndex; a start past lastAppended makes a
 // run empty).  best is max(lc, the largest granted index over the runs); each run is

@@ -25,6 +25,19 @@ __device__ __forceinline__ i64x2 tld2(const int64_t* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(p));
 }
 
+// 16 B at byte offset `off` of a wave-uniform row base: the scalar-base form of the load (one
+// 32-bit offset VGPR shared by every row instead of a 64-bit address per row; with 64-bit
+// addresses the epoch kernel ran out of its 64 VGPRs and spilled loaded words mid-issue).  The
+// empty asm pins the base in SGPRs, so the compiler cannot fold a row's p * ld into a per-lane
+// 64-bit address again.
+typedef __attribute__((address_space(1))) const i64x2 gi64x2;
+typedef __attribute__((address_space(1))) const char gchar;
+__device__ __forceinline__ i64x2 tld2o(const int64_t* base, uint32_t off) {
+  gchar* b = (gchar*)base;
+  asm volatile("" : "+s"(b));
+  return __builtin_nontemporal_load(reinterpret_cast<const gi64x2*>(b + off));
+}
+
 // Writes of a committing group: lastCommitted, and pendingIndex -> JRQ_PI_FOLLOWS_LC once.
 __device__ __forceinline__ void table_commit_one(const JrqTableArgs& t, uint32_t g, int64_t pr,
                                                  int64_t out) {
@@ -111,13 +124,14 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
   bool c0 = false, c1 = false, f0 = false, f1 = false;
   uint64_t e0 = 0, e1 = 0;
   if (tt < pairs) {
-    const i64x2 pr = tld2(t.pi + g);
-    const i64x2 lc = tld2(t.lc + g);
-    const i64x2 la = tld2(t.la + g);
-    const i64x2 cw = tld2(reinterpret_cast<const int64_t*>(t.conf) + g);
+    const uint32_t go = g * 8u;  // (g < 2^27)
+    const i64x2 pr = tld2o(t.pi, go);
+    const i64x2 lc = tld2o(t.lc, go);
+    const i64x2 la = tld2o(t.la, go);
+    const i64x2 cw = tld2o(reinterpret_cast<const int64_t*>(t.conf), go);
     i64x2 mv[P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) mv[p] = tld2(t.match + static_cast<size_t>(p) * t.ld + g);
+    for (int p = 0; p < P; ++p) mv[p] = tld2o(t.match + static_cast<size_t>(p) * t.ld, go);
     const int64_t pi0 = pr.x == kPiFollowsLc ? lc.x + 1 : pr.x;
     const int64_t pi1 = pr.y == kPiFollowsLc ? lc.y + 1 : pr.y;
     f0 = static_cast<uint64_t>(cw.x) >> 63;
@@ -150,6 +164,8 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
     }
     int64_t o0, o1;
     uint8_t s0, s1;
+    // (the 64-bit decision: the 32-bit one of the pair kernel, decide_single_rel, took this
+    // kernel past its 64 VGPRs -- 10 spills at P = 5)
     decide_single<P>(pi0, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
     decide_single<P>(pi1, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
     // a flagged group is decided by the walk (its single-conf result here is discarded)

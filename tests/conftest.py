@@ -48,6 +48,17 @@ def _hip_runtime():
     return _hip
 
 
+def device_checkpoint(where):
+    """Synchronise the device now and fail naming `where` if it reports an error: inside a test
+    with several GPU steps, it charges an asynchronous fault to the step that caused it."""
+    hip = _hip_runtime()
+    rc = hip.hipDeviceSynchronize()
+    hip.hipGetLastError()
+    if rc:
+        pytest.fail("device error at %s: %s (hipDeviceSynchronize -> %d)"
+                    % (where, hip.hipGetErrorString(rc).decode(), rc), pytrace=False)
+
+
 @pytest.fixture(autouse=True)
 def _device_fault_check(request):
     """After every GPU test: synchronise the whole device and check for an error.  A kernel

@@ -252,3 +252,78 @@ def test_host_variant_rejects_bad_run_csr(engine):
                                run_conf=b["run_conf"])
     assert c.shape == (64,)
 
+
+
+def _decide_single_ref(pi, la, lc, cw, m):
+    """The single-conf decision in plain int64 arithmetic (quorum_core.h decide_single; the
+    formulation test_quorum_model.py checks against BallotBox replays): committed, status."""
+    from jraft_amd import ST_EMPTY_CONF, ST_NOT_LEADER, ST_OUT_OF_RANGE
+    P = len(m)
+    if pi == 0:
+        return lc, ST_NOT_LEADER
+    st = 0
+    v = []
+    for p in range(P):
+        if m[p] > la:
+            st |= ST_OUT_OF_RANGE
+            v.append(None)
+        else:
+            v.append(int(m[p]))
+    if (cw & 0xFFFF) == 0 and la >= pi:
+        st |= ST_EMPTY_CONF
+
+    def kth(mask, q):
+        if q == 0:
+            return float("inf")
+        vals = sorted((x for p, x in enumerate(v) if (mask >> p) & 1 and x is not None), reverse=True)
+        return vals[q - 1] if q <= len(vals) else float("-inf")
+    cand = min(kth(cw & 0xFFFF, (cw >> 32) & 0xFF), kth((cw >> 16) & 0xFFFF, (cw >> 40) & 0xFF), la)
+    return (int(cand) if cand >= pi and cand > lc else lc), st
+
+
+def test_pair_kernel_32bit_domain_edges(engine):
+    """The pair kernel decides in 32-bit arithmetic relative to pendingIndex (decide_single_rel)
+    and sends groups outside that domain -- negative or huge pendingIndex, windows of 2^32 - 1
+    entries and more -- through a 64-bit second pass.  Edge groups of every kind, mixed into
+    waves with ordinary ones, against the decision in Python integers."""
+    import torch
+    rng = np.random.default_rng(77)
+    P, G = 5, 4096
+    I64 = np.iinfo(np.int64)
+    pis = [0, 1, 2, 1 << 31, (1 << 32) + 7, (1 << 62) - 5, 1 << 62, (1 << 62) + 3, -5, I64.max - 10]
+    wins = [0, 1, 2, 1000, (1 << 32) - 2, (1 << 32) - 1, 1 << 32, (1 << 32) + 1, 1 << 40]
+    pi = np.zeros(G, np.int64)
+    la = np.zeros(G, np.int64)
+    lc = np.zeros(G, np.int64)
+    m = np.zeros((P, G), np.int64)
+    conf = np.zeros(G, np.uint64)
+    for g in range(G):
+        p0 = int(rng.choice(pis)) if rng.random() < 0.6 else int(rng.integers(1, 1 << 40))
+        w = int(rng.choice(wins))
+        l = max(min(p0 - 1 + w, int(I64.max)), int(I64.min))
+        pi[g], la[g] = p0, l
+        lc[g] = p0 - 1 - int(rng.integers(0, 3)) if p0 > I64.min + 3 else p0
+        for p in range(P):
+            c = rng.integers(0, 8)
+            val = [p0 - 1, p0, l, l + 1 if l < I64.max else l, p0 + w // 2, -1, int(I64.min),
+                   int(I64.max)][c]
+            m[p, g] = max(min(val, int(I64.max)), int(I64.min))
+        from quorum_cases import random_conf
+        conf[g] = random_conf(rng, P)
+    ce = np.zeros(G, np.int64)
+    se = np.zeros(G, np.uint8)
+    for g in range(G):
+        c, s = _decide_single_ref(int(pi[g]), int(la[g]), int(lc[g]), int(conf[g]),
+                                  [int(x) for x in m[:, g]])
+        ce[g], se[g] = c, s
+    dev = torch.device("cuda:0")
+    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v).to(dev)
+         for k, v in dict(match=m, pending_index=pi, last_appended=la, last_committed=lc,
+                          conf=conf).items()}
+    out = torch.empty(G, dtype=torch.int64, device=dev)
+    st = torch.empty(G, dtype=torch.uint8, device=dev)
+    engine.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
+                            t["last_committed"], t["conf"], out, st)
+    engine.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), ce)
+    np.testing.assert_array_equal(st.cpu().numpy(), se)

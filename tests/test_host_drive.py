@@ -45,22 +45,27 @@ def test_host_mirror_drives_series(engine, oracle, G, K, joint, active, threads)
     """threads = 16: each epoch's calls come from 16 threads at once (group slices); the
     flush packs and delivers on its own worker threads (> 8192 changed groups)."""
     import torch
+    from conftest import device_checkpoint
 
     from jraft_amd import drive
     s = W.host_series("C3", K, groups=G, joint_frac=joint, active=active)
     committed, st = drive.drive_epochs(0, s, threads=threads)
+    # (round 3 saw one "illegal memory access" in this test: the checkpoints name the step)
+    device_checkpoint("after drive_epochs (the mirror's flushes, its engine destroyed)")
     # (b) every group against the stateless K-epoch kernel with the same conf runs
     dev = torch.device("cuda:0")
-    t = {k: torch.from_numpy(np.ascontiguousarray(s[k].view(np.int64) if s[k].dtype == np.uint64
-                                                  else s[k])).to(dev)
-         for k in ("match", "last_appended", "pending_index", "last_committed", "conf",
-                   "run_off", "run_start", "run_conf")}
+    t = {}
+    for k in ("match", "last_appended", "pending_index", "last_committed", "conf", "run_off",
+              "run_start", "run_conf"):
+        t[k] = torch.from_numpy(np.ascontiguousarray(s[k].view(np.int64) if s[k].dtype == np.uint64
+                                                     else s[k])).to(dev)
+        device_checkpoint(f"after the torch upload of {k} ({s[k].nbytes} B, pageable)")
     c = torch.empty((K, G), dtype=torch.int64, device=dev)
     sst = torch.empty((K, G), dtype=torch.uint8, device=dev)
     engine.quorum_epochs_dev(t["match"], t["pending_index"], t["last_appended"],
                              t["last_committed"], t["conf"], c, sst, run_off=t["run_off"],
                              run_start=t["run_start"], run_conf=t["run_conf"])
-    engine.synchronize()
+    device_checkpoint("after quorum_epochs_dev")
     np.testing.assert_array_equal(committed, c.cpu().numpy())
     # (a) a sample of groups (all the joint ones among them) against the oracle
     rng = np.random.default_rng(1)

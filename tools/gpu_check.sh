@@ -35,6 +35,9 @@ for s in $STEPS; do
     host)  run host_test 300 ./tests/_build/host_test gpu ;;
     tprobe) run table_probe 120 ./tools/table_probe ;;
     fprobe) run flag_probe 120 ./tools/flag_probe ;;
+    pprobe) run pair_probe 120 ./tools/pair_probe ;;
+    trace) run trace_${TRACE_LEGS:-v2} 300 rocprofv3 --kernel-trace -d gpurun_out/trace_${TRACE_LEGS:-v2} -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs ${TRACE_LEGS:-v2} ;;
+    drive) run drive_tests 300 python -u -m pytest tests/test_host_drive.py -v -x -p no:cacheprovider --timeout 240 --timeout-method thread ;;
     eprobe) run epochs_probe 120 ./tools/epochs_probe ;;
   esac
 done

@@ -1,10 +1,12 @@
 // pair_probe.hip -- launch shapes of the headline quorum epoch (tools only; not part of libjrq).
 // C3-shaped stateless epochs (1M groups x 5 peers, joint conf words, no run tables), 6 rotating
 // input buffers (486 MB, past the Infinity Cache, as bench.py's headline leg), back-to-back
-// launches between one event pair after a warm-up.  Variants:
-//   product   quorum_epoch_pair_kernel<5>: one lane per 2 groups, the whole grid at once
-//   gsN       grid-stride: N workgroups of 512 per CU, each lane walks pairs (t, t + stride, ..)
-//   quad      one lane per 4 groups (two 16-B loads per stream)
+// launches between one event pair after a warm-up.  Variants (round 2 also measured grid-stride
+// shapes and 4 groups per lane: DESIGN.md §4.1):
+//   product   quorum_epoch_pair_kernel<5, false>
+//   single64  the product's shape and decision (decide_single: P^2 64-bit compares per conf mask)
+//   rel32     the same with decide_single_rel (32-bit relative values, u32 sorting network)
+//   floor     the same loads and stores, no decision (words XOR-folded): what the loads cost
 //   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/pair_probe tools/pair_probe.hip
 #include <hip/hip_runtime.h>
 
@@ -26,8 +28,13 @@
 namespace probe {
 using jrq::i64x2;
 
-template <int P>
-__device__ __forceinline__ void pair_at(const JrqQuorumArgs& a, uint32_t g) {
+// kMode 0: decide_single (the 64-bit P^2 kth); 1: decide_single_rel (32-bit relative, sorting
+// network); 2: no decision (every loaded word folded into the outputs by XOR: the load floor)
+template <int P, int kMode>
+__global__ __launch_bounds__(512) void variant(JrqQuorumArgs a) {
+  const uint32_t t = blockIdx.x * 512 + threadIdx.x;
+  if (t >= (a.G >> 1)) return;
+  const uint32_t g = t << 1;
   const i64x2 pi = jrq::ld2nt(a.pending_index + g);
   const i64x2 lc = jrq::ld2nt(a.last_committed + g);
   const i64x2 la = jrq::ld2nt(a.last_appended + g);
@@ -43,29 +50,29 @@ __device__ __forceinline__ void pair_at(const JrqQuorumArgs& a, uint32_t g) {
   }
   int64_t o0, o1;
   uint8_t s0, s1;
-  jrq::decide_single<P>(pi.x, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
-  jrq::decide_single<P>(pi.y, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
+  if (kMode == 0) {
+    jrq::decide_single<P>(pi.x, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
+    jrq::decide_single<P>(pi.y, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
+  } else if (kMode == 1) {
+    jrq::decide_single_rel<P>(pi.x, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
+    jrq::decide_single_rel<P>(pi.y, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
+  } else {
+    o0 = pi.x ^ lc.x ^ la.x ^ cw.x;
+    o1 = pi.y ^ lc.y ^ la.y ^ cw.y;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      o0 ^= m0[p];
+      o1 ^= m1[p];
+    }
+    s0 = static_cast<uint8_t>(o0);
+    s1 = static_cast<uint8_t>(o1);
+  }
   i64x2 out;
   out.x = o0;
   out.y = o1;
   __builtin_nontemporal_store(out, reinterpret_cast<i64x2*>(a.committed + g));
   __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
                               reinterpret_cast<uint16_t*>(a.status + g));
-}
-
-template <int P>
-__global__ __launch_bounds__(512) void gs_kernel(JrqQuorumArgs a) {
-  const uint32_t pairs = a.G >> 1, stride = gridDim.x * 512;
-  for (uint32_t t = blockIdx.x * 512 + threadIdx.x; t < pairs; t += stride) pair_at<P>(a, t << 1);
-}
-
-template <int P>
-__global__ __launch_bounds__(512) void quad_kernel(JrqQuorumArgs a) {
-  const uint32_t t = blockIdx.x * 512 + threadIdx.x;
-  if (4 * t + 3 < a.G) {
-    pair_at<P>(a, 4 * t);
-    pair_at<P>(a, 4 * t + 2);
-  }
 }
 }  // namespace probe
 
@@ -139,15 +146,14 @@ int main() {
   time("product", [&](const JrqQuorumArgs& a) {
     hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<5, false>), dim3((pairs + 511) / 512), dim3(512), 0, 0, a);
   });
-  for (int n : {2, 4, 8}) {
-    char nm[16];
-    std::snprintf(nm, sizeof nm, "gs%d", n);
-    time(nm, [&](const JrqQuorumArgs& a) {
-      hipLaunchKernelGGL(probe::gs_kernel<5>, dim3(cus * n), dim3(512), 0, 0, a);
-    });
-  }
-  time("quad", [&](const JrqQuorumArgs& a) {
-    hipLaunchKernelGGL(probe::quad_kernel<5>, dim3((G / 4 + 511) / 512), dim3(512), 0, 0, a);
+  time("single64", [&](const JrqQuorumArgs& a) {
+    hipLaunchKernelGGL((probe::variant<5, 0>), dim3((pairs + 511) / 512), dim3(512), 0, 0, a);
+  });
+  time("rel32", [&](const JrqQuorumArgs& a) {
+    hipLaunchKernelGGL((probe::variant<5, 1>), dim3((pairs + 511) / 512), dim3(512), 0, 0, a);
+  });
+  time("floor", [&](const JrqQuorumArgs& a) {
+    hipLaunchKernelGGL((probe::variant<5, 2>), dim3((pairs + 511) / 512), dim3(512), 0, 0, a);
   });
   time("product2", [&](const JrqQuorumArgs& a) {
     hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<5, false>), dim3((pairs + 511) / 512), dim3(512), 0, 0, a);
