@@ -1158,7 +1158,10 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
   }
   // otherwise one range per record from its data start (the leading header first): one
   // streaming pass over the records, one entry boundary per record (v2_finish recovers the
-  // data CRCs)
+  // data CRCs).  (These launches cost ~5 us each when they return at once, tools/trace_gaps.py;
+  // on a second stream beside the fixed-size kernel they still ran after it -- the rounds
+  // kernel's 160 KiB of LDS waits for the fixed kernel's workgroups to leave -- and the call
+  // took 262 instead of 257 us.)
   JrqCrcArgs a{};
   a.gate = v.gate;
   a.payload = rec;

@@ -77,11 +77,59 @@ struct ChunkReader {
   }
 };
 
+// A record's bytes for the parse, one lane per record: the 128 B from the 64-B line of its first
+// byte and the 128 B ending with the line of its last byte, loaded together (one round trip)
+// and staged into the lane's slice of LDS; any other byte is a single global load.  A V2
+// header (magic, type, term, index, peers, the data tag and length) and its trailer (checksum,
+// learners) fit the two windows.  With a one-line cache per lane instead (ChunkReader), a
+// wave went to memory whenever any of its 64 lanes crossed a line -- nearly every header byte,
+// the lanes' records starting at unrelated offsets: 29-30 us for 64k records.
+constexpr uint32_t kWinSlot = 272;  // LDS bytes per lane (256 + 16: 16-B aligned slots starting in different banks)
+
+struct WindowReader {
+  const uint8_t* rec;
+  int64_t limit;
+  uintptr_t head, tail;  // the windows' 64-B aligned starts
+  const uint8_t* slot;   // the lane's LDS copy: [0, 128) head window, [128, 256) tail window
+  bool err;
+  __device__ WindowReader(const uint8_t* r, int64_t len, uint8_t* lds) : rec(r), limit(len), slot(lds), err(false) {
+    // len >= 1.  A line is loaded only when it holds a byte of the record (so it lies in a
+    // mapped page); the line at `tail` always does (tail >= head, tail <= the last byte's line).
+    const uintptr_t s = reinterpret_cast<uintptr_t>(r), e = s + static_cast<uintptr_t>(len);
+    head = s & ~static_cast<uintptr_t>(63);
+    const uintptr_t last = (e - 1) & ~static_cast<uintptr_t>(63);
+    tail = last >= head + 64 ? last - 64 : head;
+    const uintptr_t lines[4] = {head, head + 64, tail, tail + 64};
+    v2u32x4 v[16];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      if (lines[l] <= e - 1) {
+        const v2u32x4* p = reinterpret_cast<const v2u32x4*>(lines[l]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[4 * l + c] = p[c];
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      if (lines[l] <= e - 1) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) *reinterpret_cast<v2u32x4*>(lds + 64 * l + 16 * c) = v[4 * l + c];
+      }
+    }
+  }
+  __device__ __forceinline__ uint32_t at(int64_t pos) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(rec) + static_cast<uintptr_t>(pos);
+    if (a - head < 128) return slot[a - head];
+    if (a - tail < 128) return slot[128 + (a - tail)];
+    return rec[pos];
+  }
+};
+
 struct PbIn {
-  ChunkReader rd;
+  WindowReader rd;
   int64_t pos;
   uint32_t last_tag;
-  __device__ PbIn(const uint8_t* r, int64_t len) : rd(r, len), pos(6), last_tag(0) {}
+  __device__ PbIn(const uint8_t* r, int64_t len, uint8_t* lds) : rd(r, len, lds), pos(6), last_tag(0) {}
   __device__ __forceinline__ uint32_t byte() {
     if (pos >= rd.limit) {
       rd.err = true;  // truncatedMessage
@@ -208,14 +256,15 @@ __device__ __forceinline__ uint64_t crc_bytes_be(uint64_t crc, uint64_t v, const
 }
 
 // One lane per record; then the block's summary for the fixed-size data path's gate (below).
-__device__ void v2_parse_record(const JrqV2Args& a, uint32_t r, const uint64_t* T, uint8_t& st_out,
-                                uint64_t& d_out, uint64_t& dl_out);
+__device__ void v2_parse_record(const JrqV2Args& a, uint32_t r, const uint64_t* T, uint8_t* win,
+                                uint8_t& st_out, uint64_t& d_out, uint64_t& dl_out);
 
 __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
   __shared__ uint64_t T[256];
   __shared__ uint64_t s_doff[256];
   __shared__ uint64_t s_len0;
   __shared__ uint32_t s_last;
+  __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinSlot];
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) T[i] = bswap64(a.slice[i]);
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -226,7 +275,7 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
   const bool live = r < a.n;
   uint8_t st = kV2Null;
   uint64_t d = 0, dl = 0;
-  if (live) v2_parse_record(a, r, T, st, d, dl);
+  if (live) v2_parse_record(a, r, T, win + threadIdx.x * kWinSlot, st, d, dl);
   // The gate of the fixed-size data path (crc64_fixed_kernel at the data starts): every record
   // decoded, all with the data length L0 of record 0, data ranges in order, and each 64
   // consecutive ones within 1 GiB (the fixed kernel reads a row of records through one buffer
@@ -275,8 +324,8 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
   }
 }
 
-__device__ void v2_parse_record(const JrqV2Args& a, uint32_t r, const uint64_t* T, uint8_t& st_out,
-                                uint64_t& d_out, uint64_t& dl_out) {
+__device__ void v2_parse_record(const JrqV2Args& a, uint32_t r, const uint64_t* T, uint8_t* win,
+                                uint8_t& st_out, uint64_t& d_out, uint64_t& dl_out) {
   const uint64_t b0 = a.off[r];
   const int64_t L = static_cast<int64_t>(a.off[r + 1] - b0);
   const uint8_t* rec = a.rec + b0;
@@ -289,7 +338,7 @@ __device__ void v2_parse_record(const JrqV2Args& a, uint32_t r, const uint64_t* 
   if (L < 1) {
     st = kV2Null;
   } else {
-    PbIn in(rec, L);
+    PbIn in(rec, L, win);
     const uint32_t m0 = in.rd.at(0);
     if (m0 != 0xBBu) {
       st = kV2V1;

@@ -306,21 +306,31 @@ int jraft_drive_latency(int device, uint32_t G, uint32_t P, uint32_t threads, ui
         const uint32_t g1 = static_cast<uint32_t>(static_cast<uint64_t>(G) * (t + 1) / T);
         uint64_t n = 0;
         int64_t busy = 0;
+        // paced producers: one pass over the slice per pass_us, spread evenly over it in chunks
+        // of 256 groups (the replicators' acks arrive with the network: neither a spinning loop,
+        // which also hits the box's cgroup CPU quota, nor a burst per pass, which measured the
+        // flush of a burst instead of the steady state)
+        const uint32_t kChunk = 256;
+        const int64_t passNs = static_cast<int64_t>(pass_us) * 1000;
         for (int64_t idx = 1; !stop.load(std::memory_order_relaxed); ++idx) {
           const int64_t p0 = nowNs();
-          for (uint32_t g = g0; g < g1; ++g) {
-            if (!boxes[g].appendPendingTasks(conf, nullptr, 1)) throw std::runtime_error("append refused");
-            for (uint32_t p = 0; p < P; ++p) boxes[g].commitAt(idx, idx, peers[p]);
-            ackNs[g].store(nowNs(), std::memory_order_relaxed);
-            ackIdx[g].store(idx, std::memory_order_release);
-            ++n;
+          for (uint32_t c0 = g0; c0 < g1 && !stop.load(std::memory_order_relaxed); c0 += kChunk) {
+            const uint32_t c1 = std::min(g1, c0 + kChunk);
+            const int64_t b0 = nowNs();
+            for (uint32_t g = c0; g < c1; ++g) {
+              if (!boxes[g].appendPendingTasks(conf, nullptr, 1)) throw std::runtime_error("append refused");
+              for (uint32_t p = 0; p < P; ++p) boxes[g].commitAt(idx, idx, peers[p]);
+              ackNs[g].store(nowNs(), std::memory_order_relaxed);
+              ackIdx[g].store(idx, std::memory_order_release);
+              ++n;
+            }
+            const int64_t b1 = nowNs();
+            busy += b1 - b0;
+            if (passNs) {  // on schedule: this chunk's share of the pass
+              const int64_t due = p0 + passNs * static_cast<int64_t>(c1 - g0) / static_cast<int64_t>(g1 - g0);
+              if (due > b1) std::this_thread::sleep_for(std::chrono::nanoseconds(due - b1));
+            }
           }
-          const int64_t spent = nowNs() - p0;
-          busy += spent;
-          // paced producers: one pass per pass_us (the replicators' acks arrive with the network,
-          // they do not spin); a busy loop would also hit the box's cgroup CPU quota
-          if (pass_us && spent < static_cast<int64_t>(pass_us) * 1000)
-            std::this_thread::sleep_for(std::chrono::nanoseconds(static_cast<int64_t>(pass_us) * 1000 - spent));
         }
         entries[t] = n;
         busyNs[t] = busy;
