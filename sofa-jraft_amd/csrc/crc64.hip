@@ -322,21 +322,6 @@ __device__ __forceinline__ void straddle_piece(const JrqCrcArgs& a, uint32_t e, 
     emit(a, e, v);
 }
 
-// Entries spanning at most this many segments hand their pieces over through per-segment
-// slots (plain stores) combined by crc64_finish_kernel; longer ones through the atomic slot.
-constexpr uint64_t kMaxSlotParts = 64;
-
-// Segment size (bytes; identical in the rounds and finish kernels): a multiple of 256 (two
-// 128-B rounds), ~span / lanes of the rounds grid, never more segments than straddler slots.
-__device__ __forceinline__ uint64_t seg_size(const JrqCrcArgs& a, uint64_t span) {
-  auto up256 = [](uint64_t x) { return (x + 255) & ~255ull; };
-  const uint64_t lanes = a.lanes;
-  uint64_t S = a.seg_bytes ? up256(a.seg_bytes) : up256((span + lanes - 1) / lanes);
-  if (S < 256) S = 256;
-  const uint64_t s_min = up256((span + a.scratch_len - 3) / (a.scratch_len - 2));
-  return S < s_min ? s_min : S;
-}
-
 // First e in [0, n] with off[e] >= x, given off[0] <= x <= off[n].  Probes off[g-1 .. g+1]
 // around the interpolated guess g (one round trip when entries are evenly sized), then
 // bisects the side that holds the answer.
@@ -800,11 +785,7 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < a.n; e += stride) {
     const uint64_t o0 = off[e], o1 = off[e + 1];
     uint64_t v;
-    const uint64_t first = (o0 - base + D) / S, last = o1 > o0 ? (o1 - 1 - base + D) / S : first;
-    if (last != first && last - first + 1 <= kMaxSlotParts) {
-      v = a.piece_tail[last];
-      for (uint64_t g = first; g < last; ++g) v ^= a.piece_cont[g];
-    } else {
+    if (!crc_pieces(a, o0, o1, base, D, S, v)) {
       // whole entry (or atomic hand-off): out[e] is final
       if (!kLogEntry && a.stream_state == nullptr) continue;
       v = a.out[e];
@@ -1078,6 +1059,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64(
     hipLaunchKernelGGL((jrq::crc64_rounds_kernel<jrq::kCrcBlock, false>), dim3(grid),
                        dim3(jrq::kCrcBlock), 0, stream, *args);
   }
+  if (args->no_finish) return hipGetLastError();  // (the caller's own kernel assembles the pieces)
   const uint32_t blocks = (args->n + 255) / 256;
   const uint32_t cap = static_cast<uint32_t>(grid) * 8;
   const dim3 fg(blocks < cap ? blocks : cap);

@@ -30,7 +30,8 @@ extern "C" hipError_t jrq_launch_ae_meta(const JrqAeArgs* a, hipStream_t stream)
 extern "C" hipError_t jrq_launch_lease(const JrqLeaseArgs* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_fanout(const JrqFanoutArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_v2_parse(const JrqV2Args* a, hipStream_t stream);
-extern "C" hipError_t jrq_launch_v2_finish(const JrqV2Args* a, int num_cus, hipStream_t stream);
+extern "C" hipError_t jrq_launch_v2_finish(const JrqV2Args* a, const JrqCrcArgs* walk, int num_cus,
+                                           hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_first_corrupt(const JrqAeArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_table_update(const JrqTableArgs* a, const JrqGroupState* states,
                                               uint32_t n_states, const uint64_t* recs,
@@ -1157,11 +1158,13 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
     if ((rc = crc_fixed_dispatch(e, f, 1))) return rc;
   }
   // otherwise one range per record from its data start (the leading header first): one
-  // streaming pass over the records, one entry boundary per record (v2_finish recovers the
-  // data CRCs).  (These launches cost ~5 us each when they return at once, tools/trace_gaps.py;
-  // on a second stream beside the fixed-size kernel they still ran after it -- the rounds
-  // kernel's 160 KiB of LDS waits for the fixed kernel's workgroups to leave -- and the call
-  // took 262 instead of 257 us.)
+  // streaming pass over the records, one entry boundary per record; v2_finish assembles each
+  // range from its pieces and recovers the data CRCs.  Two launches, which return at once when
+  // the fixed-size path took the batch: ~5 us each then (launch and kernel-boundary cost,
+  // tools/trace_gaps.py), so the walk's own finish kernel was folded into v2_finish.  (On a
+  // second stream beside the fixed-size kernel they still ran after it -- the rounds kernel's
+  // 160 KiB of LDS waits for the fixed kernel's workgroups to leave -- and the call took 262
+  // instead of 257 us.)
   JrqCrcArgs a{};
   a.gate = v.gate;
   a.payload = rec;
@@ -1169,8 +1172,9 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
   a.n = N + 1;
   a.out = static_cast<uint64_t*>(crc2);
   a.regs_slowpath = 1;  // an unaligned boundary per record
-  if ((rc = crc_dispatch(e, a, 0))) return rc;
-  JRQ_HIP(e, jrq_launch_v2_finish(&v, e->num_cus, e->stream));
+  a.no_finish = 1;
+  if ((rc = crc_dispatch(e, a, 0))) return rc;  // (sets a.lanes and the scratch pointers)
+  JRQ_HIP(e, jrq_launch_v2_finish(&v, &a, e->num_cus, e->stream));
   return JRQ_OK;
 }
 

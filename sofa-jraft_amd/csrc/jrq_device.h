@@ -112,7 +112,38 @@ struct JrqCrcArgs {
   const uint64_t* starts;  // crc64_fixed_kernel<., true>: entry i starts at payload + starts[i]
   const uint64_t* gate;    // nullable device words {k, entry_bytes} (V2 decode): the starts
                            // kernel runs iff k != 0, the segment walk (rounds + finish) iff k == 0
+  uint32_t no_finish;      // 1: launch the rounds kernel only; the caller's kernel assembles the
+                           // straddling entries (crc_pieces) -- V2's v2_finish does
 };
+
+// Segment walk geometry shared by crc64_rounds_kernel / crc64_finish_kernel (crc64.hip) and
+// v2_finish (v2_decode.hip).  Entries spanning at most kMaxSlotParts segments hand their pieces
+// over through per-segment slots (plain stores) XOR-ed by whoever finishes the entry; longer
+// ones through the atomic slot (their out[] is final after the rounds kernel).
+constexpr uint64_t kMaxSlotParts = 64;
+
+// Segment size (bytes; identical in every kernel of one walk): a multiple of 256 (two 128-B
+// rounds), ~span / lanes of the rounds grid, never more segments than straddler slots.
+__device__ __forceinline__ uint64_t seg_size(const JrqCrcArgs& a, uint64_t span) {
+  auto up256 = [](uint64_t x) { return (x + 255) & ~255ull; };
+  const uint64_t lanes = a.lanes;
+  uint64_t S = a.seg_bytes ? up256(a.seg_bytes) : up256((span + lanes - 1) / lanes);
+  if (S < 256) S = 256;
+  const uint64_t s_min = up256((span + a.scratch_len - 3) / (a.scratch_len - 2));
+  return S < s_min ? s_min : S;
+}
+
+// An entry [o0, o1) of the walk (stream base, misalignment D, segment size S) that straddles
+// 2..kMaxSlotParts segments: *v = the XOR of its pieces (true); otherwise false and its out[]
+// entry holds the CRC.
+__device__ __forceinline__ bool crc_pieces(const JrqCrcArgs& a, uint64_t o0, uint64_t o1, uint64_t base,
+                                           uint64_t D, uint64_t S, uint64_t& v) {
+  const uint64_t first = (o0 - base + D) / S, last = o1 > o0 ? (o1 - 1 - base + D) / S : first;
+  if (last == first || last - first + 1 > kMaxSlotParts) return false;
+  v = a.piece_tail[last];
+  for (uint64_t g = first; g < last; ++g) v ^= a.piece_cont[g];
+  return true;
+}
 
 // Leader lease / alive-quorum check (quorum.hip, lease kernel).
 struct JrqLeaseArgs {

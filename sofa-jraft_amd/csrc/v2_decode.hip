@@ -458,9 +458,15 @@ __device__ void v2_parse_record(const JrqV2Args& a, uint32_t r, const uint64_t* 
 // records (tools/v2_boundary_probe.py).
 // (The fixed-size data path -- gate[0] != 0 -- finishes inside crc64_fixed_kernel: this kernel
 // then returns at once.)
-__global__ __launch_bounds__(256) void v2_finish(JrqV2Args a) {
+__global__ __launch_bounds__(256) void v2_finish(JrqV2Args a, JrqCrcArgs w) {
   __shared__ uint64_t Tf[8][256], Ti[8][256];
   if (a.gate[0] != 0) return;  // (grid-uniform)
+  // the walk's geometry (w: the rounds kernel's arguments): a range's CRC is its out[] entry
+  // or the XOR of its pieces -- assembled here, so the walk needs no crc64_finish_kernel
+  const uint64_t* const off2 = w.offsets;
+  const uint64_t wbase = off2[0];
+  const uint64_t wD = reinterpret_cast<uintptr_t>(w.payload + wbase) & 15u;
+  const uint64_t wS = seg_size(w, wD + (off2[w.n] - wbase));
   for (uint32_t e = threadIdx.x; e < 8 * 256; e += blockDim.x) {
     Tf[e >> 8][e & 255u] = bswap64(a.slice[e]);
     Ti[e >> 8][e & 255u] = a.xinv[e];
@@ -491,7 +497,9 @@ __global__ __launch_bounds__(256) void v2_finish(JrqV2Args a) {
       }
       for (; h > 0; --h) s = (s << 8) ^ Tf[0][s >> 56];
       s ^= hc;
-      uint64_t d = a.crc2[r + 1] ^ s, m = k;
+      uint64_t range;
+      if (!crc_pieces(w, off2[r + 1], off2[r + 2], wbase, wD, wS, range)) range = a.crc2[r + 1];
+      uint64_t d = range ^ s, m = k;
       for (; m >= 8; m -= 8) {  // d * x^-64
         uint64_t t = 0;
 #pragma unroll
@@ -516,12 +524,12 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_v2_parse(
 }
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_v2_finish(
-    const JrqV2Args* a, int num_cus, hipStream_t stream) {
+    const JrqV2Args* a, const JrqCrcArgs* walk, int num_cus, hipStream_t stream) {
   // each workgroup stages 32 KiB of tables in LDS: one record per lane, at most 2 workgroups
   // per CU (a grid of 8 per CU re-read 64 MiB of tables from L2 for 64k records)
   uint32_t blocks = (a->n + 255) / 256;
   const uint32_t cap = static_cast<uint32_t>(num_cus) * 2u;
   if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL(jrq::v2_finish, dim3(blocks ? blocks : 1), dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL(jrq::v2_finish, dim3(blocks ? blocks : 1), dim3(256), 0, stream, *a, *walk);
   return hipGetLastError();
 }
