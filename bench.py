@@ -1082,10 +1082,10 @@ def leg_v2(ctx, args, c5state):
                         f"field), decode + isCorrupted",
             "GBps_records": tot / (ms * 1e-3) / 1e9, "ms_per_batch": ms,
             "bit_exact_vs_oracle": ok, "oracle_decoder_sample_ok": sample_ok,
-            "roofline": roofline(alg, ms, **pmc_traffic("v2", "v2_parse", "v2_uniform",
-                                                        "crc64_fixed_kernel<false, true>",
-                                                        "crc64_rounds_kernel<768u, true>",
-                                                        "crc64_finish_kernel<false>", "v2_finish"))}
+            "roofline": roofline(alg, ms, kernel="v2_parse + crc64_fixed_kernel<true, true> (+ the "
+                                                 "segment walk's two launches, which return at once)",
+                                 **pmc_traffic("v2", "v2_parse", "crc64_fixed_kernel<true, true>",
+                                               "crc64_rounds_kernel<768u, true>", "v2_finish"))}
 
 
 def leg_snapshot(ctx, args, c5state):
