@@ -66,7 +66,7 @@ struct jrq_engine {
   uint32_t* cnt = nullptr;    // straddler counters
   uint64_t* pieces = nullptr; // per-segment straddler pieces: [2][scratch_len]
   uint32_t* fan_ctr = nullptr; // commit fan-out {listed sum, blocks done}, zero between launches
-  uint64_t* v2_gate = nullptr; // V2 decode gate {k, L, bad, end, arrivals}; arrivals zero between launches
+  uint64_t* v2_gate = nullptr; // V2 decode gate {k, L, bad, end, arrivals, -, -, -, segment arrivals[16]}; arrivals zero between launches
   uint32_t scratch_len = 0;
   int crc_grid = 0;
   // Test / A-B overrides, set only through jrq_debug_set (never from the environment):
@@ -386,10 +386,10 @@ jrq_engine* jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int* 
   try_hip(hipMalloc(&e->cnt, slots * 4), "hipMalloc(cnt)");
   try_hip(hipMalloc(&e->pieces, static_cast<size_t>(e->scratch_len) * 16), "hipMalloc(pieces)");
   try_hip(hipMalloc(&e->fan_ctr, 16), "hipMalloc(fan_ctr)");
-  try_hip(hipMalloc(&e->v2_gate, 64), "hipMalloc(v2_gate)");
+  try_hip(hipMalloc(&e->v2_gate, 8 * (8 + 16)), "hipMalloc(v2_gate)");
   if (rc == JRQ_OK) {
     try_hip(hipMemset(e->fan_ctr, 0, 16), "zero fan_ctr");
-    try_hip(hipMemset(e->v2_gate, 0, 64), "zero v2_gate");
+    try_hip(hipMemset(e->v2_gate, 0, 8 * (8 + 16)), "zero v2_gate");
     try_hip(hipMemcpy(e->slice, slice.data(), slice.size() * 8, hipMemcpyHostToDevice), "upload slice");
     try_hip(hipMemcpy(e->shift, shift.data(), shift.size() * 8, hipMemcpyHostToDevice), "upload shift");
     try_hip(hipMemcpy(e->xinv, xinv.data(), xinv.size() * 8, hipMemcpyHostToDevice), "upload xinv");

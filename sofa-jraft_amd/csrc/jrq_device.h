@@ -214,7 +214,8 @@ struct JrqV2Args {
   uint64_t* off2;          // scratch [n+2]: record i's range = [off2[i+1], off2[i+2])
   const uint64_t* crc2;    // scratch [n+1] (CRC of the ranges; range 0 = the leading header)
   uint64_t* lens;          // scratch [n] header length << 32 | trailer length
-  uint64_t* gate;          // engine words [5]: {k, L, bad, end, arrivals} -- the data CRCs by
+  uint64_t* gate;          // engine words [24]: {k, L, bad, end, arrivals, -, -, -, segment
+                           // arrivals [16]} -- the data CRCs by
                            // crc64_fixed_kernel (k lanes per record) when every record decoded with
                            // data length L; arrivals is zero between launches
   uint64_t* blk;           // scratch [4 * ceil(n / 256)]: v2_parse's per-block summaries

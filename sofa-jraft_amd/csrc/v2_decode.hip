@@ -125,6 +125,82 @@ struct WindowReader {
   }
 };
 
+// A varint from 10 bytes of a window (independent LDS reads, no per-byte branch): its value
+// accumulated as readRawVarint64 does (readRawVarint32 = the low 32 bits: bytes 5..9 only
+// carry bits >= 35), *n = the bytes it takes, 11 if all ten continue (malformed).
+__device__ __forceinline__ uint64_t lds_varint(const uint8_t* w, uint32_t* n) {
+  uint32_t b[10], cont = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    b[i] = w[i];
+    cont |= ((b[i] >> 7) & 1u) << i;
+  }
+  const uint32_t k = static_cast<uint32_t>(__builtin_ctz(~cont)) + 1u;
+  uint64_t v = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) v |= i < static_cast<int>(k) ? static_cast<uint64_t>(b[i] & 0x7Fu) << (7 * i) : 0ull;
+  *n = k;
+  return v;
+}
+
+// The record as V2Encoder writes a data entry (V2Encoder.java:76-130; generated writeTo order,
+// LogOutter.java:518-546): type, term, index, data, an optional checksum, nothing else, each
+// varint inside the LDS windows.  Decodes it with a fixed sequence of window reads (a handful
+// of dependent LDS round trips per record); false on anything else -- peers, learners, unknown
+// fields, other orders, a field outside the windows -- and the general parser decodes the
+// record from its start.  One lane per record runs a wave's records in lockstep: the general
+// parser's per-byte loop and field switch were 29 us for 64k records (tools/v2_parse_probe.hip).
+struct V2Fast {
+  uint32_t etype;
+  int64_t term, index, doff, dlen;
+  uint64_t ck;
+  bool have_ck;
+};
+
+__device__ __forceinline__ bool v2_fast_fields(const WindowReader& rd, int64_t L, V2Fast& f) {
+  const uintptr_t base = reinterpret_cast<uintptr_t>(rd.rec);
+  int64_t p = 6;
+  // the 10 window bytes at record position q (nullptr: not inside a window)
+  auto win = [&](int64_t q) -> const uint8_t* {
+    const uintptr_t a = base + static_cast<uintptr_t>(q);
+    if (a - rd.head <= 118) return rd.slot + (a - rd.head);
+    if (a - rd.tail <= 118) return rd.slot + 128 + (a - rd.tail);
+    return nullptr;
+  };
+  // tag, then a varint value: false unless the tag is `want` and both fit the record
+  auto field = [&](uint32_t want, uint64_t* v) -> bool {
+    const uint8_t* w = win(p);
+    if (!w || w[0] != want || p + 1 >= L) return false;
+    const uint8_t* x = win(p + 1);
+    if (!x) return false;
+    uint32_t n;
+    *v = lds_varint(x, &n);
+    if (n > 10 || p + 1 + static_cast<int64_t>(n) > L) return false;
+    p += 1 + n;
+    return true;
+  };
+  uint64_t v;
+  if (!field(0x08, &v) || static_cast<uint32_t>(v) > 3u) return false;  // type: an EntryType
+  f.etype = static_cast<uint32_t>(v);
+  if (!field(0x10, &v)) return false;
+  f.term = static_cast<int64_t>(v);
+  if (!field(0x18, &v)) return false;
+  f.index = static_cast<int64_t>(v);
+  if (!field(0x32, &v)) return false;  // data: a length-delimited field
+  const int32_t size = static_cast<int32_t>(static_cast<uint32_t>(v));
+  if (size < 0 || size > L - p) return false;
+  f.doff = p;
+  f.dlen = size;
+  p += size;
+  f.have_ck = false;
+  f.ck = 0;
+  if (p == L) return true;
+  if (!field(0x38, &v)) return false;
+  f.ck = v;
+  f.have_ck = true;
+  return p == L;
+}
+
 struct PbIn {
   WindowReader rd;
   int64_t pos;
@@ -255,6 +331,8 @@ __device__ __forceinline__ uint64_t crc_bytes_be(uint64_t crc, uint64_t v, const
   return crc;
 }
 
+constexpr uint32_t kV2Segments = 16;  // first-level arrival counters of v2_parse (gate[8..23])
+
 // One lane per record; then the block's summary for the fixed-size data path's gate (below).
 __device__ void v2_parse_record(const JrqV2Args& a, uint32_t r, const uint64_t* T, uint8_t* win,
                                 uint8_t& st_out, uint64_t& d_out, uint64_t& dl_out);
@@ -298,8 +376,19 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
     sm[2] = lb;
     sm[3] = any_bad ? 1u : 0u;
     __threadfence();  // release the summary, then arrive
-    const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(a.gate + 4), 1ull);
-    s_last = old + 1 == gridDim.x;
+    // in two levels (block b -> segment counter b % 16, the last of each segment -> gate[4]):
+    // same-address atomics serialise, ~14 ns each, and 256 arrivals on one word cost ~3.6 us
+    unsigned long long* const cnt = reinterpret_cast<unsigned long long*>(a.gate);
+    const uint32_t seg = blockIdx.x % kV2Segments;
+    const uint32_t in_seg = (gridDim.x - seg + kV2Segments - 1) / kV2Segments;
+    bool last = false;
+    if (atomicAdd(cnt + 8 + seg, 1ull) + 1 == in_seg) {
+      cnt[8 + seg] = 0;  // (no other arrival on it in this launch)
+      __threadfence();
+      const uint32_t segs = gridDim.x < kV2Segments ? gridDim.x : kV2Segments;
+      last = atomicAdd(cnt + 4, 1ull) + 1 == segs;
+    }
+    s_last = last;
     __threadfence();  // acquire (the last arriver reads every block's summary)
   }
   __syncthreads();
@@ -320,7 +409,8 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
     a.gate[1] = L0;
     a.gate[2] = broken ? 1u : 0u;
     a.gate[3] = a.off[a.n];  // the records' end: crc64_fixed_kernel's load window
-    a.gate[4] = 0;           // the arrival count, zero for the next launch
+    a.gate[4] = 0;           // the arrival count, zero for the next launch (the segment counters
+                             // were re-zeroed by their last arrivers)
   }
 }
 
@@ -344,6 +434,14 @@ __device__ void v2_parse_record(const JrqV2Args& a, uint32_t r, const uint64_t* 
       st = kV2V1;
     } else if (L < 6 || in.rd.at(1) != 0xD2u || in.rd.at(2) != 1u) {
       st = kV2Null;
+    } else if (V2Fast f; v2_fast_fields(in.rd, L, f)) {  // the common encoding
+      etype = f.etype;
+      tm = f.term;
+      idx = f.index;
+      doff = f.doff;
+      dlen = f.dlen;
+      ck = f.ck;
+      have_ck = f.have_ck;
     } else {
       uint32_t grp[2] = {0, 0};  // open unknown-field groups (field numbers)
       int depth = 0;

@@ -398,3 +398,41 @@ def test_gpu_uniform_data_len_device_variant(engine, pad):
     engine.synchronize()
     g = {k: out[k].cpu().numpy().view(t) for k, t in engine.V2_FIELDS}
     check_gpu_vs_oracle(g, o)
+
+
+@pytest.mark.gpu
+def test_gpu_fast_path_near_misses(engine):
+    """The kernel decodes the encoder's data-entry layout (type, term, index, data, optional
+    checksum) with a fixed sequence of window reads and hands anything else to its general
+    parser from the record's start.  Records that look almost like that layout -- each must
+    decode exactly as the oracle decodes it, whichever way the kernel goes."""
+    F, V, H = O.pb_field, O.pb_varint, O.V2_HEADER
+    rng = np.random.default_rng(11)
+    data = bytes(rng.integers(0, 256, 300, dtype=np.uint8))
+    ck = F(7, 0, V(0x1234567890))
+    std = [F(1, 0, V(0)), F(2, 0, V(7)), F(3, 0, V(1 << 40)), F(6, 2, V(len(data)) + data)]
+    recs = [
+        H + b"".join(std),                                           # no checksum
+        H + b"".join(std) + ck,                                      # the common form
+        H + bytes([0x88, 0x00]) + V(0) + b"".join(std[1:]) + ck,    # type tag in two bytes
+        H + F(1, 0, V(4)) + b"".join(std) + ck,                      # unknown enum, then type
+        H + F(1, 0, V(5)) + b"".join(std[1:]) + ck,                  # only an unknown enum
+        H + b"".join(std) + ck + F(20, 0, V(1)),                     # a field after the checksum
+        H + b"".join(std) + ck + ck,                                 # checksum twice
+        H + b"".join(std[:3]) + F(6, 2, bytes([0x83, 0x80, 0x80, 0x80, 0x00]) + b"abc") + ck,
+        H + b"".join(std[:2]) + F(3, 0, bytes([0xFF] * 9 + [0x01])) + std[3] + ck,  # index -1
+        H + b"".join(std[:3]) + F(6, 2, V(0)) + ck,                  # empty data
+        H + b"".join(std[:3]) + F(6, 2, V(len(data) + 1) + data),    # data past the end
+        H + b"".join(std)[:-1],                                      # truncated data
+        H + b"".join(std) + bytes([0x38]),                           # checksum tag, no value
+        H + b"".join(std) + bytes([0x38] + [0x80] * 10 + [0x01]),    # overlong checksum varint
+        H + std[1] + std[0] + b"".join(std[2:]) + ck,                # term before type
+        H + b"".join(std[:3]) + F(6, 2, V(0x7FFFFFFF)),              # length past the record
+        H + b"".join(std[:3]) + F(6, 2, bytes([0xFF, 0xFF, 0xFF, 0xFF, 0x0F])),  # negative length
+        H + F(1, 0, V(3)) + b"".join(std[1:]) + ck,                  # CONFIGURATION type, no peers
+    ]
+    buf, off = batch(recs)
+    g = engine.v2_decode_verify(buf, off)
+    o = O.v2_decode_batch(buf, off)
+    check_gpu_vs_oracle(g, o)
+    assert (o["status"] == O.V2_OK).sum() >= 8 and (o["status"] == O.V2_NULL).sum() >= 4
