@@ -160,17 +160,22 @@ struct V2Fast {
 __device__ __forceinline__ bool v2_fast_fields(const WindowReader& rd, int64_t L, V2Fast& f) {
   const uintptr_t base = reinterpret_cast<uintptr_t>(rd.rec);
   int64_t p = 6;
-  // the 10 window bytes at record position q (nullptr: not inside a window)
+  // the window bytes from record position q on (nullptr: its record bytes up to q + 10 are not
+  // all inside one window).  Reads may run up to 9 bytes past a window: past the head window
+  // that is the tail window's copy (so the record must end first), past the tail window the
+  // lane slot's padding (the tail window ends with the record's last line)
   auto win = [&](int64_t q) -> const uint8_t* {
     const uintptr_t a = base + static_cast<uintptr_t>(q);
-    if (a - rd.head <= 118) return rd.slot + (a - rd.head);
-    if (a - rd.tail <= 118) return rd.slot + 128 + (a - rd.tail);
+    const uintptr_t need = static_cast<uintptr_t>(L - q < 10 ? L - q : 10);
+    if (a - rd.head < 128 && a - rd.head + need <= 128) return rd.slot + (a - rd.head);
+    if (a - rd.tail < 128) return rd.slot + 128 + (a - rd.tail);
     return nullptr;
   };
   // tag, then a varint value: false unless the tag is `want` and both fit the record
   auto field = [&](uint32_t want, uint64_t* v) -> bool {
+    if (p + 1 >= L) return false;
     const uint8_t* w = win(p);
-    if (!w || w[0] != want || p + 1 >= L) return false;
+    if (!w || w[0] != want) return false;
     const uint8_t* x = win(p + 1);
     if (!x) return false;
     uint32_t n;
@@ -371,36 +376,42 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
   if (threadIdx.x == 0) {
     const uint32_t nb = a.n - blockIdx.x * blockDim.x;
     uint64_t* sm = a.blk + 4ull * blockIdx.x;
-    sm[0] = s_doff[0];
-    sm[1] = s_doff[(nb < blockDim.x ? nb : blockDim.x) - 1];
-    sm[2] = lb;
-    sm[3] = any_bad ? 1u : 0u;
-    __threadfence();  // release the summary, then arrive
-    // in two levels (block b -> segment counter b % 16, the last of each segment -> gate[4]):
-    // same-address atomics serialise, ~14 ns each, and 256 arrivals on one word cost ~3.6 us
-    unsigned long long* const cnt = reinterpret_cast<unsigned long long*>(a.gate);
+    // The hand-off to the last block uses agent-scope relaxed atomics (stores and loads that
+    // go to the coherence point, past the XCDs' own L2s) and one explicit wait for the
+    // summary's stores before the arrival: __threadfence() here is buffer_wbl2 + buffer_inv,
+    // an L2 writeback per workgroup (twice), ~10 us for the 256 workgroups of 64k records
+    // (tools/v2_parse_probe.hip "gate").
+    auto st_agent = [](uint64_t* q, uint64_t v) { __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto add_agent = [](uint64_t* q) { return __hip_atomic_fetch_add(q, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    st_agent(sm + 0, s_doff[0]);
+    st_agent(sm + 1, s_doff[(nb < blockDim.x ? nb : blockDim.x) - 1]);
+    st_agent(sm + 2, lb);
+    st_agent(sm + 3, any_bad ? 1u : 0u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the summary is at the coherence point
+    // arrival in two levels (block b -> segment counter b % 16, the last of each segment ->
+    // gate[4]): same-address atomics serialise
     const uint32_t seg = blockIdx.x % kV2Segments;
     const uint32_t in_seg = (gridDim.x - seg + kV2Segments - 1) / kV2Segments;
     bool last = false;
-    if (atomicAdd(cnt + 8 + seg, 1ull) + 1 == in_seg) {
-      cnt[8 + seg] = 0;  // (no other arrival on it in this launch)
-      __threadfence();
+    if (add_agent(a.gate + 8 + seg) + 1 == in_seg) {
+      st_agent(a.gate + 8 + seg, 0);  // (no other arrival on it in this launch)
       const uint32_t segs = gridDim.x < kV2Segments ? gridDim.x : kV2Segments;
-      last = atomicAdd(cnt + 4, 1ull) + 1 == segs;
+      last = add_agent(a.gate + 4) + 1 == segs;
     }
     s_last = last;
-    __threadfence();  // acquire (the last arriver reads every block's summary)
   }
   __syncthreads();
   if (!s_last) return;
-  const uint64_t L0 = a.blk[2];
+  auto ld_agent = [](const uint64_t* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  const uint64_t L0 = ld_agent(a.blk + 2);
   bool broken = false;
   for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
     const uint64_t* sm = a.blk + 4ull * b;
-    broken = broken || sm[3] != 0 || sm[2] != L0;
-    const uint64_t first_prev = b ? sm[-4] : sm[0];
-    if (b) broken = broken || sm[0] < sm[-3] + L0;
-    broken = broken || sm[1] + L0 - first_prev >= (1ull << 30);
+    const uint64_t s0 = ld_agent(sm), s1 = ld_agent(sm + 1), s2 = ld_agent(sm + 2), s3 = ld_agent(sm + 3);
+    broken = broken || s3 != 0 || s2 != L0;
+    const uint64_t first_prev = b ? ld_agent(sm - 4) : s0;
+    if (b) broken = broken || s0 < ld_agent(sm - 3) + L0;
+    broken = broken || s1 + L0 - first_prev >= (1ull << 30);
   }
   broken = __syncthreads_or(broken);
   if (threadIdx.x == 0) {
@@ -409,8 +420,8 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
     a.gate[1] = L0;
     a.gate[2] = broken ? 1u : 0u;
     a.gate[3] = a.off[a.n];  // the records' end: crc64_fixed_kernel's load window
-    a.gate[4] = 0;           // the arrival count, zero for the next launch (the segment counters
-                             // were re-zeroed by their last arrivers)
+    __hip_atomic_store(a.gate + 4, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the arrival
+    // count, zero for the next launch (the segment counters were re-zeroed by their last arrivers)
   }
 }
 
