@@ -135,7 +135,14 @@ int jrq_synchronize(jrq_engine *e);
  * other input memory goes through the engine's two pinned 8 MiB bounce chunks (a CPU copy
  * overlapped with the previous chunk's DMA). */
 int jrq_host_register(void *ptr, size_t bytes);
+/* Call only after the last call that used the buffer has returned, and before the memory is
+ * freed: a registration left over freed pages is a stale device mapping of that address. */
 int jrq_host_unregister(void *ptr);
+/* Page-locked host memory owned by the HIP driver (hipHostMalloc): staging for a host that has
+ * no buffer of its own to register (the C++ mirror's pack buffers).  The pages never return to
+ * the process heap while the device may map them.  *out = NULL on failure. */
+int jrq_host_alloc(size_t bytes, void **out);
+int jrq_host_free(void *ptr);
 
 /* Test and A/B hooks: per-engine overrides of kernel and staging choices.  A host never needs
  * them, and the library reads nothing from the environment (a JVM that loads libjrq gets the

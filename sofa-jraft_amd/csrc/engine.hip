@@ -483,6 +483,23 @@ int jrq_host_unregister(void* ptr) {
   return hipHostUnregister(ptr) == hipSuccess ? JRQ_OK : JRQ_E_HIP;
 }
 
+int jrq_host_alloc(size_t bytes, void** out) {
+  if (!out) return JRQ_E_INVALID;
+  *out = nullptr;
+  if (!bytes) return JRQ_E_INVALID;
+  if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return JRQ_E_NOMEM;
+  }
+  return JRQ_OK;
+}
+
+int jrq_host_free(void* ptr) {
+  if (!ptr) return JRQ_E_INVALID;
+  return hipHostFree(ptr) == hipSuccess ? JRQ_OK : JRQ_E_HIP;
+}
+
 // ----------------------------------------------------------------- quorum ---
 
 int jrq_quorum_epoch_dev(jrq_engine* e, const jrq_group_batch* in, int64_t* committed_out,

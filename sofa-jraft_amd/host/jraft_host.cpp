@@ -395,42 +395,48 @@ void GroupBatch::setFlushThreads(unsigned n) {
 }
 
 // f(part, begin, end) over [0, n) on the pool, only when each part gets at least `grain` items.
-template <class F>
-void GroupBatch::parallelFor(size_t n, size_t grain, F&& f) {
-  if (n < 2 * grain) {
-    f(0u, size_t(0), n);
-    return;
-  }
+// How many parts parallelFor(n, grain, f) cuts [0, n) into; part i is [n i / parts, n (i+1) / parts).
+size_t GroupBatch::partsFor(size_t n, size_t grain) {
+  if (n < 2 * grain) return 1;
   if (!pool_) {  // default: the box's CPU share per GPU, at most 16
     pool_.reset(new Pool(poolSize_ ? poolSize_ : std::min(16u, usableCpus())));
   }
-  const size_t parts = std::min<size_t>(pool_->size(), n / grain);
+  return std::min<size_t>(pool_->size(), n / grain);
+}
+
+template <class F>
+void GroupBatch::parallelFor(size_t n, size_t grain, F&& f) {
+  const size_t parts = partsFor(n, grain);
+  if (parts == 1) {
+    f(0u, size_t(0), n);
+    return;
+  }
   pool_->run([&](unsigned i, unsigned) {
     if (i < parts) f(i, n * i / parts, n * (i + 1) / parts);
   });
 }
 
+// Driver-owned page-locked memory (jrq_host_alloc), not heap pages registered with HIP: a
+// registered heap range that is later freed and reused by the process for other memory is
+// exactly what a device mapping must not outlive ("Staging memory").  Called
+// only from the flushing thread, never from pack workers.
 template <class T>
 void GroupBatch::PinnedBuf<T>::reserve(size_t n) {
   if (n <= cap) return;
   const size_t want = std::max(n, 2 * cap);
   const size_t bytes = ((want * sizeof(T)) + 4095) & ~size_t(4095);
   release();
-  p = static_cast<T*>(std::aligned_alloc(4096, bytes));
-  if (!p) throw std::bad_alloc();
-  registered = jrq_host_register(p, bytes) == JRQ_OK;  // DMA straight from these pages
+  void* q = nullptr;
+  if (jrq_host_alloc(bytes, &q) != JRQ_OK || !q) throw std::bad_alloc();
+  p = static_cast<T*>(q);
   cap = bytes / sizeof(T);
 }
 
 template <class T>
 void GroupBatch::PinnedBuf<T>::release() {
-  if (p) {
-    if (registered) jrq_host_unregister(p);
-    std::free(p);
-  }
+  if (p) jrq_host_free(p);
   p = nullptr;
   cap = 0;
-  registered = false;
 }
 
 GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
@@ -658,13 +664,18 @@ uint32_t GroupBatch::flushLocked() {
   const size_t nd = pre[nl];
   // pack: the dirty groups split into contiguous ranges of the concatenated lists
   const size_t kGrain = 1u << 12;
-  const size_t nparts = std::max<size_t>(1, std::min<size_t>(64, nd / kGrain));
+  const size_t nparts = partsFor(nd, kGrain);
   if (parts_.size() < nparts) parts_.resize(nparts);
   for (auto& p : parts_) p.ns = p.nr = 0;
+  // staging grows here, on this thread: allocation and release of page-locked memory stay
+  // out of the pack workers
+  for (size_t i = 0; i < nparts; ++i) {
+    const size_t len = nd * (i + 1) / nparts - nd * i / nparts;
+    parts_[i].st.reserve(len + 1);
+    parts_[i].rec.reserve(len * (P_ + 1) + 1);
+  }
   parallelFor(nd, kGrain, [&](unsigned part, size_t b, size_t e) {
     Part& P = parts_[part];
-    P.st.reserve(e - b + 1);
-    P.rec.reserve((e - b) * (P_ + 1) + 1);
     // the pieces of the lists inside [b, e)
     size_t li = static_cast<size_t>(std::upper_bound(pre.begin(), pre.end(), b) - pre.begin()) - 1;
     for (size_t pos = b; pos < e; ++li) {

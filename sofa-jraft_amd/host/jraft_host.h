@@ -271,14 +271,13 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
     uint64_t conf;
   };
   template <class T>
-  struct PinnedBuf {  // page-locked host staging (pageable when registration fails)
+  struct PinnedBuf {  // page-locked host staging (jrq_host_alloc)
     T* p = nullptr;
     size_t cap = 0;
-    bool registered = false;
     void reserve(size_t n);
     void release();
     PinnedBuf() = default;
-    PinnedBuf(PinnedBuf&& o) noexcept : p(o.p), cap(o.cap), registered(o.registered) { o.p = nullptr; o.cap = 0; }
+    PinnedBuf(PinnedBuf&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
     ~PinnedBuf() { release(); }
   };
   struct DirtyList;  // one per calling thread
@@ -308,6 +307,7 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   DirtyList* myDirtyList();
   uint32_t flushLocked();
   void packRange(Part& part, const uint32_t* groups, size_t n);
+  size_t partsFor(size_t n, size_t grain);
   template <class F>
   void parallelFor(size_t n, size_t grain, F&& f);
 

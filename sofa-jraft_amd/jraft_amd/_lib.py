@@ -96,6 +96,8 @@ SIGNATURES = [
     ("jrq_synchronize", C.c_int, [_V]),
     ("jrq_host_register", C.c_int, [_V, C.c_size_t]),
     ("jrq_host_unregister", C.c_int, [_V]),
+    ("jrq_host_alloc", C.c_int, [C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("jrq_host_free", C.c_int, [_V]),
     ("jrq_debug_set", C.c_int, [_V, C.c_int, C.c_int64]),
     ("jrq_quorum_epoch_dev", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
     ("jrq_quorum_epoch", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),

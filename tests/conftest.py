@@ -48,6 +48,46 @@ def _hip_runtime():
     return _hip
 
 
+class _PtrAttr(ctypes.Structure):  # hipPointerAttribute_t (hip_runtime_api.h)
+    _fields_ = [("type", ctypes.c_int), ("device", ctypes.c_int),
+                ("devicePointer", ctypes.c_void_p), ("hostPointer", ctypes.c_void_p),
+                ("isManaged", ctypes.c_int), ("allocationFlags", ctypes.c_uint)]
+
+
+def hip_registration(addr):
+    """What HIP knows about host address `addr`: None for plain pageable memory, else the
+    registration it finds there (type, device pointer, and the device range it belongs to)."""
+    hip = _hip_runtime()
+    a = _PtrAttr()
+    rc = hip.hipPointerGetAttributes(ctypes.byref(a), ctypes.c_void_p(addr))
+    hip.hipGetLastError()
+    if rc or a.type == 0:
+        return None
+    base, size = ctypes.c_void_p(), ctypes.c_size_t()
+    rr = hip.hipMemGetAddressRange(ctypes.byref(base), ctypes.byref(size),
+                                   ctypes.c_void_p(a.devicePointer))
+    hip.hipGetLastError()
+    return {"addr": hex(addr), "type": a.type, "devicePointer": hex(a.devicePointer or 0),
+            "hostPointer": hex(a.hostPointer or 0), "flags": a.allocationFlags,
+            "dev_range": None if rr else (hex(base.value or 0), size.value)}
+
+
+def assert_unregistered(arrays, where):
+    """Fail (before any copy) if HIP holds a registration over memory we never registered:
+    a pageable copy from such an address would DMA through that stale mapping."""
+    stale = []
+    for name, a in arrays.items():
+        if not hasattr(a, "ctypes") or a.nbytes == 0:
+            continue
+        for off in sorted({0, a.nbytes // 2, a.nbytes - 1}):
+            r = hip_registration(a.ctypes.data + off)
+            if r is not None:
+                stale.append((name, a.nbytes, off, r))
+    if stale:
+        pytest.fail("HIP reports registrations over unregistered numpy arrays %s: %r"
+                    % (where, stale), pytrace=False)
+
+
 def device_checkpoint(where):
     """Synchronise the device now and fail naming `where` if it reports an error: inside a test
     with several GPU steps, it charges an asynchronous fault to the step that caused it."""

@@ -10,6 +10,7 @@
 // never built into libjrq.so, libjraft_host.so or anything bench.py or smoke() loads; the GPU
 // build of the same tests (tests/_build/host_test) links the real library.
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -47,6 +48,16 @@ void jrq_destroy(jrq_engine* e) { delete e; }
 const char* jrq_last_error(const jrq_engine* e) { return e ? e->err.c_str() : g_err.c_str(); }
 int jrq_host_register(void* p, size_t n) { return p && n ? JRQ_OK : JRQ_E_INVALID; }
 int jrq_host_unregister(void* p) { return p ? JRQ_OK : JRQ_E_INVALID; }
+int jrq_host_alloc(size_t n, void** out) {
+  if (!out) return JRQ_E_INVALID;
+  *out = n ? std::aligned_alloc(4096, (n + 4095) & ~size_t(4095)) : nullptr;
+  return *out ? JRQ_OK : (n ? JRQ_E_NOMEM : JRQ_E_INVALID);
+}
+int jrq_host_free(void* p) {
+  if (!p) return JRQ_E_INVALID;
+  std::free(p);
+  return JRQ_OK;
+}
 
 int jrq_crc64_batch(jrq_engine*, const uint8_t* payload, const uint64_t* offsets, uint32_t N,
                     uint64_t* crc_out) {

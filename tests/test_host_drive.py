@@ -45,13 +45,15 @@ def test_host_mirror_drives_series(engine, oracle, G, K, joint, active, threads)
     """threads = 16: each epoch's calls come from 16 threads at once (group slices); the
     flush packs and delivers on its own worker threads (> 8192 changed groups)."""
     import torch
-    from conftest import device_checkpoint
+    from conftest import assert_unregistered, device_checkpoint
 
     from jraft_amd import drive
     s = W.host_series("C3", K, groups=G, joint_frac=joint, active=active)
+    assert_unregistered(s, "before drive_epochs")
     committed, st = drive.drive_epochs(0, s, threads=threads)
     # (round 3 saw one "illegal memory access" in this test: the checkpoints name the step)
     device_checkpoint("after drive_epochs (the mirror's flushes, its engine destroyed)")
+    assert_unregistered(s, "after drive_epochs")
     # (b) every group against the stateless K-epoch kernel with the same conf runs
     dev = torch.device("cuda:0")
     t = {}
