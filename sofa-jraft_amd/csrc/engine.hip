@@ -197,9 +197,10 @@ int ensure_stage(jrq_engine* e, int slot, size_t bytes, void** out) {
 
 // Host -> device upload of caller memory through the engine's pinned bounce chunks: a CPU
 // copy into a pinned chunk, then an async DMA from it on the engine stream, two chunks in
-// flight.  HIP's own pageable-copy path for >1 MiB uploads failed intermittently ("illegal
-// memory access" from the copy itself, read-only numpy views over Python bytes), so the host
-// variants never hand it caller pages.
+// flight.  (Round 2 moved here from HIP's own pageable copy after that copy failed with
+// "illegal memory access"; round 3 found the trigger elsewhere -- concurrent host
+// registrations, now serialised in jrq_host_register -- and kept the bounce path: it needs no
+// pinning of caller pages at all.  JRQ_DBG_UPLOAD_PAGEABLE selects HIP's copy for A/B runs.)
 constexpr size_t kBounceChunk = size_t(8) << 20;
 
 int upload(jrq_engine* e, void* dst, const void* src, size_t bytes) {
@@ -473,20 +474,42 @@ int jrq_debug_set(jrq_engine* e, int option, int64_t value) {
               static_cast<long long>(value));
 }
 
+// Registration, unregistration and driver-owned page-locked allocations go through one
+// process-wide lock.  Round 3 traced the round-2/3 "illegal memory access" of a later pageable
+// copy to hipHostRegister / hipHostUnregister called from several threads at once (the C++
+// mirror's pack workers each registering their own staging buffer): with the same buffers
+// registered from one thread, or allocated with hipHostMalloc, the failing test passed
+// (DESIGN.md §4.10).  A JNI host may pin DirectByteBuffers from any thread, so the library
+// serialises the calls itself; they are rare (setup, buffer growth), never per epoch.
+namespace {
+std::mutex g_pin_mu;
+}  // namespace
+
 int jrq_host_register(void* ptr, size_t bytes) {
   if (!ptr || !bytes) return JRQ_E_INVALID;
-  return hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess ? JRQ_OK : JRQ_E_HIP;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  if (hipHostRegister(ptr, bytes, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return JRQ_E_HIP;
+  }
+  return JRQ_OK;
 }
 
 int jrq_host_unregister(void* ptr) {
   if (!ptr) return JRQ_E_INVALID;
-  return hipHostUnregister(ptr) == hipSuccess ? JRQ_OK : JRQ_E_HIP;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  if (hipHostUnregister(ptr) != hipSuccess) {
+    (void)hipGetLastError();
+    return JRQ_E_HIP;
+  }
+  return JRQ_OK;
 }
 
 int jrq_host_alloc(size_t bytes, void** out) {
   if (!out) return JRQ_E_INVALID;
   *out = nullptr;
   if (!bytes) return JRQ_E_INVALID;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
   if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
     (void)hipGetLastError();
     *out = nullptr;
@@ -497,7 +520,12 @@ int jrq_host_alloc(size_t bytes, void** out) {
 
 int jrq_host_free(void* ptr) {
   if (!ptr) return JRQ_E_INVALID;
-  return hipHostFree(ptr) == hipSuccess ? JRQ_OK : JRQ_E_HIP;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  if (hipHostFree(ptr) != hipSuccess) {
+    (void)hipGetLastError();
+    return JRQ_E_HIP;
+  }
+  return JRQ_OK;
 }
 
 // ----------------------------------------------------------------- quorum ---

@@ -175,6 +175,27 @@ __device__ __forceinline__ int64_t run_candidate(const int64_t (&m)[P], uint64_t
   return cand >= s ? cand : kI64Min;
 }
 
+// run_candidate inside rel_domain, on a group mapped by rel_map: [s, ee] lies inside the
+// window [pi, la] (s >= pi by construction, ee <= la), so both ends map to [1, W] and the run
+// grants r in [s_rel, e_rel].  Same result and status as run_candidate.
+template <int P>
+__device__ __forceinline__ int64_t run_candidate_rel(const RelGroup<P>& g, uint64_t cw, int64_t pi,
+                                                     int64_t s, int64_t ee, uint8_t& st) {
+  if (ee < s) return kI64Min;
+  if ((cw & 0xFFFFu) == 0) st |= kStEmptyConf;
+  const uint32_t sr = static_cast<uint32_t>(s - pi) + 1u;
+  const uint32_t er = static_cast<uint32_t>(ee - pi) + 1u;
+  const uint32_t nmask = static_cast<uint32_t>(cw & 0xFFFFu);
+  const uint32_t omask = static_cast<uint32_t>((cw >> 16) & 0xFFFFu);
+  const uint32_t nq = static_cast<uint32_t>((cw >> 32) & 0xFFu);
+  const uint32_t oq = static_cast<uint32_t>((cw >> 40) & 0xFFu);
+  const uint32_t kn = nq == 0 ? g.W : kth_largest_rel<P>(g.r, nmask, nq);
+  const uint32_t ko = oq == 0 ? g.W : kth_largest_rel<P>(g.r, omask, oq);
+  uint32_t c = kn < ko ? kn : ko;
+  c = c < er ? c : er;
+  return c >= sr ? pi - 1 + static_cast<int64_t>(c) : kI64Min;
+}
+
 template <int P, class Runs>
 __device__ __forceinline__ int64_t runs_best(const Runs& R, uint32_t nruns, int64_t pi, int64_t la,
                                              int64_t lc, const int64_t (&m)[P], uint8_t& st) {

@@ -237,10 +237,21 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
       if (pi == 0) {
         st = kStNotLeader;
       } else {
-        st = mask_out_of_range<P>(hm, hla);
         const int64_t s = rs > pi ? rs : pi;
         const int64_t e = nx == kI64Max ? hla : nx - 1;
-        cand = run_candidate<P>(hm, rc, s, e < hla ? e : hla, st);
+        const int64_t ee = e < hla ? e : hla;
+        // the walk runs when every load of the wave has landed and the VALU is the busy
+        // unit: 32-bit arithmetic relative to pendingIndex for every real group (half the
+        // VALU of the 64-bit rank count), 64-bit outside rel_domain
+        if (rel_domain(pi, hla)) {
+          RelGroup<P> rg;
+          rel_map<P>(pi, hla, hm, rg);
+          st = rg.st;
+          cand = run_candidate_rel<P>(rg, rc, pi, s, ee, st);
+        } else {
+          st = mask_out_of_range<P>(hm, hla);
+          cand = run_candidate<P>(hm, rc, s, ee, st);
+        }
       }
     }
     cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 1)));

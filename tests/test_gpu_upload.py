@@ -1,12 +1,15 @@
 """GPU: host-variant uploads of caller memory (the DirectByteBuffer path of INTEGRATION.md).
 
-Round 2 saw two "illegal memory access" errors reported by a host variant's upload of a
-read-only > 1 MiB numpy view over a Python bytes object, after a successful stream
-synchronisation; the uploads were then routed through the engine's pinned bounce chunks.
+Rounds 2 and 3 saw "illegal memory access" errors reported by a > 1 MiB pageable upload (a host
+variant's, then torch's) after a successful device synchronisation.  Round 3 traced the trigger
+to hipHostRegister / hipHostUnregister called from several threads at once (the host mirror's
+pack workers registering their staging buffers): the failing drive test passed once the same
+buffers were registered from one thread.  libjrq now serialises its pin calls.
 These tests pin the cases down, each followed by conftest's device-wide synchronisation:
   * the default path (bounce chunks) on read-only views of 1 MiB + 1 .. 64 MiB,
-  * HIP's own pageable copy on the same views (JRQ_DBG_UPLOAD_PAGEABLE), the path that failed,
-  * caller memory registered with jrq_host_register (DMA straight from the caller's pages).
+  * HIP's own pageable copy on the same views (JRQ_DBG_UPLOAD_PAGEABLE),
+  * caller memory registered with jrq_host_register (DMA straight from the caller's pages),
+  * registrations from 16 threads at once, then pageable uploads of fresh arrays.
 """
 import numpy as np
 import pytest
@@ -68,3 +71,51 @@ def test_registered_caller_buffer(oracle):
             np.testing.assert_array_equal(e.crc64_batch(a, offs), oracle.crc64_batch(a, offs))
     finally:
         assert L.jrq_host_unregister(ctypes.c_void_p(a.ctypes.data)) == 0
+
+
+def test_concurrent_registrations_then_pageable_uploads(oracle):
+    """16 threads register, use and unregister their own buffers through jrq_host_register at
+    the same time (as the mirror's pack workers once did, and as a JNI host pinning
+    DirectByteBuffers from its RPC threads may); afterwards fresh > 1 MiB arrays go up through
+    torch's pageable copy and through the host variants, and come back intact."""
+    import ctypes
+    import threading
+
+    import torch
+
+    from jraft_amd import Engine
+    L = _lib.load()
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(t)
+            for _ in range(4):
+                n = int(rng.integers(1, 9)) << 20
+                buf = np.empty(n + 4096, np.uint8)
+                a = buf[(-buf.ctypes.data) % 4096:][:n]
+                a[:] = t
+                if L.jrq_host_register(ctypes.c_void_p(a.ctypes.data), n) != 0:
+                    errors.append(("register", t, n))
+                    continue
+                if L.jrq_host_unregister(ctypes.c_void_p(a.ctypes.data)) != 0:
+                    errors.append(("unregister", t, n))
+                del a, buf
+        except Exception as ex:  # pragma: no cover - reported below
+            errors.append(repr(ex))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    dev = torch.device("cuda:0")
+    for k in range(6):
+        host = np.frombuffer(W.random_bytes(100 + k, (8 << 20) + 8 * k), np.int64).copy()
+        got = torch.from_numpy(host).to(dev).cpu().numpy()
+        np.testing.assert_array_equal(got, host)
+    payload = W.random_bytes(7, 6 << 20)
+    offs = np.arange(0, len(payload) + 1, 4096, dtype=np.uint64)
+    with Engine(0) as e:
+        np.testing.assert_array_equal(e.crc64_batch(payload, offs), oracle.crc64_batch(payload, offs))
