@@ -104,25 +104,29 @@ template <int P>
 __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
   constexpr uint32_t kWaves = kTableBlock / 64;
   constexpr uint32_t kHand = 16;  // flagged groups per wave handed over through LDS
+  constexpr uint32_t kEntLds = 4; // flagged-entry slots per wave copied to LDS up front
   __shared__ uint32_t wave_cnt[kWaves];
   __shared__ uint64_t staged[kWaves][128];
   __shared__ int64_t hand[kWaves][kHand][P + 3];  // {pendingIndex word, lc, la, match[P]}
-  __shared__ __attribute__((aligned(16))) int64_t ent2[kWaves][2][8];  // entries 0 and 1
+  __shared__ __attribute__((aligned(16))) int64_t ent4[kWaves][kEntLds][8];  // entries 0-3
   __shared__ uint32_t blk_base;
   const uint32_t pairs = (t.G + 1) >> 1;
   const uint32_t tt = blockIdx.x * kTableBlock + threadIdx.x;
   const uint32_t g = tt << 1;
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
-  // the wave's flagged groups: their count, and entries 0 and 1 copied straight to the wave's
-  // LDS slice (an LDS-DMA load: no registers held across the single-conf path)
+  // The wave's first four flagged-entry slots go straight to its LDS slice (an LDS-DMA load,
+  // 256 B per wave, ~1 % of the epoch's bytes; no registers held across the single-conf path),
+  // whatever the wave's count: the count is the wave's own ballot of its flagged groups (the
+  // flags kernel's count of the same 128 groups).  Loading the count and branching on it here
+  // put a full memory round trip in front of every wave's single-conf loads.
   const uint32_t wid = blockIdx.x * kWaves + w;
-  const uint32_t nflag = __builtin_amdgcn_readfirstlane(t.flag_wcnt[wid]);
   const int64_t* const ent = reinterpret_cast<const int64_t*>(t.flag_ent) + static_cast<size_t>(wid) * kFlagSlots * 8;
-  if (nflag != 0 && lane < 8)  // lane l: bytes 16 l .. 16 l + 15 of entries 0-1
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ent + lane * 2), &ent2[w][0][0], 16, 0, 0);
-  bool c0 = false, c1 = false, f0 = false, f1 = false;
-  uint64_t e0 = 0, e1 = 0;
+  if (lane < 4 * kEntLds)  // lane l: bytes 16 l .. 16 l + 15 of entries 0-3 (64 B each)
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ent + lane * 2), &ent4[w][0][0], 16, 0, 0);
+  bool c0 = false, c1 = false, f0 = false, f1 = false, w0 = false, w1 = false;
+  int64_t o0 = 0, o1 = 0;
+  uint32_t s01 = 0;
   if (tt < pairs) {
     const uint32_t go = g * 8u;  // (g < 2^27)
     const i64x2 pr = tld2o(t.pi, go);
@@ -162,7 +166,6 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
 #pragma unroll
       for (int p = 0; p < P; ++p) hs[3 + p] = m1[p];
     }
-    int64_t o0, o1;
     uint8_t s0, s1;
     // (the 64-bit decision: the 32-bit one of the pair kernel, decide_single_rel, took this
     // kernel past its 64 VGPRs -- 10 spills at P = 5)
@@ -171,50 +174,50 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
     // a flagged group is decided by the walk (its single-conf result here is discarded)
     c0 = !f0 && o0 > lc.x;  // decide_single returns lastCommitted unless a commit happened
     c1 = !f1 && o1 > lc.y;
-    if (c0 && c1) {
-      i64x2 o;
-      o.x = o0;
-      o.y = o1;
-      __builtin_nontemporal_store(o, reinterpret_cast<i64x2*>(t.lc + g));
-      // pendingIndex = lastCommittedIndex + 1 from now on (BallotBox.java:131-132): one
-      // store per group and leadership, the steady state writes lastCommitted only
-      if (pr.x != kPiFollowsLc) t.pi[g] = kPiFollowsLc;
-      if (pr.y != kPiFollowsLc) t.pi[g + 1] = kPiFollowsLc;
-    } else {
-      if (c0) table_commit_one(t, g, pr.x, o0);
-      if (c1) table_commit_one(t, g + 1, pr.y, o1);
-    }
-    if (t.status) {  // a flagged group's status is written by the walk
-      if (g + 1 < t.G && !f0 && !f1)
-        __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
-                                    reinterpret_cast<uint16_t*>(t.status + g));
-      else {
-        if (!f0) t.status[g] = s0;
-        if (!f1 && g + 1 < t.G) t.status[g + 1] = s1;
-      }
-    }
-    e0 = (static_cast<uint64_t>(o0 - pi0 + 1) << 32) | g;
-    e1 = (static_cast<uint64_t>(o1 - pi1 + 1) << 32) | (g + 1);
+    // pendingIndex = lastCommittedIndex + 1 from now on (BallotBox.java:131-132): one store per
+    // group and leadership, the steady state writes lastCommitted only
+    w0 = pr.x != kPiFollowsLc;
+    w1 = pr.y != kPiFollowsLc;
+    s01 = s0 | (static_cast<uint32_t>(s1) << 8);
+    // list entries -> the wave's slice of LDS (ballot prefixes, no atomics)
+    const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
+    if (c0) staged[w][__popcll(b0 & below)] = (static_cast<uint64_t>(o0 - pi0 + 1) << 32) | g;
+    if (c1) staged[w][__popcll(b0) + __popcll(b1 & below)] = (static_cast<uint64_t>(o1 - pi1 + 1) << 32) | (g + 1);
   }
-  // list entries -> the wave's slice of LDS (ballot prefixes, no atomics)
-  const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
-  if (c0) staged[w][__popcll(b0 & below)] = e0;
-  if (c1) staged[w][__popcll(b0) + __popcll(b1 & below)] = e1;
-  uint32_t cnt = __popcll(b0) + __popcll(b1);
-  // the walk: flagged group i of the wave on quad i % 16, one conf run per lane
+  uint32_t cnt = __popcll(__ballot(c0)) + __popcll(__ballot(c1));
+  // The walk, before any of the wave's stores: its reads (LDS, and the entries past the first
+  // four from memory) then wait for nothing but themselves.  With the single-conf stores issued
+  // first, every wait of the walk (vmcnt counts stores too) drained the wave's stores.
+  // Flagged group i of the wave on quad i % 16, one conf run per lane.
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the hand-off slots: this wave's)
   __builtin_amdgcn_wave_barrier();
   const uint32_t q = lane >> 2, r = lane & 3u;
+  // this wave's flagged groups (f0 / f1 are false on lanes past the table)
+  const uint32_t nflag = __popcll(__ballot(f0)) + __popcll(__ballot(f1));
   for (uint32_t base = 0; base < nflag; base += 16) {  // (wave-uniform)
     const uint32_t i = base + q;
-    const bool act = i < nflag;
+    bool act = i < nflag;
     // the entry {group, start1, start2, start3, conf0 .. conf3}: run r's start, the next run's
-    // start and run r's conf word (entries 0-1 from LDS, later ones from memory)
-    const int64_t* e = i < 2 ? &ent2[w][i][0] : ent + (act ? i : 0u) * 8;
-    const uint32_t h = act ? static_cast<uint32_t>(e[0]) : 0u;
-    const int64_t rs = r == 0 || !act ? kI64Min : e[r];
-    const int64_t nx = r == 3 || !act ? kI64Max : e[r + 1];
-    const uint64_t rc = act ? static_cast<uint64_t>(e[4 + r]) : 0ull;
+    // start and run r's conf word (entries 0-3 from LDS, later ones from memory; values, not a
+    // pointer that could be either: a generic pointer makes flat loads, which wait for every
+    // outstanding memory operation)
+    int64_t eh = 0, ers = kI64Min, enx = kI64Max;
+    uint64_t rc = 0;
+    if (act && i < kEntLds) {
+      eh = ent4[w][i][0];
+      if (r != 0) ers = ent4[w][i][r];
+      if (r != 3) enx = ent4[w][i][r + 1];
+      rc = static_cast<uint64_t>(ent4[w][i][4 + r]);
+    } else if (act) {
+      const int64_t* e = ent + static_cast<size_t>(i) * 8;
+      eh = e[0];
+      if (r != 0) ers = e[r];
+      if (r != 3) enx = e[r + 1];
+      rc = static_cast<uint64_t>(e[4 + r]);
+    }
+    const uint32_t h = static_cast<uint32_t>(eh);
+    const int64_t rs = ers, nx = enx;
+    act = act && h < t.G;  // (the flags kernel writes only table groups: a guard, not a case)
     int64_t cand = kI64Min, hpr = 0, hlc = 0, hla = 0, pi = 0;
     uint8_t st = 0;
     if (act) {
@@ -267,6 +270,34 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
     const uint64_t bc = __ballot(commit);
     if (commit) staged[w][cnt + __popcll(bc & below)] = (static_cast<uint64_t>(cand - pi + 1) << 32) | h;
     cnt += __popcll(bc);
+  }
+  // the single-conf results
+  if (tt < pairs) {
+    if (c0 && c1) {
+      i64x2 o;
+      o.x = o0;
+      o.y = o1;
+      __builtin_nontemporal_store(o, reinterpret_cast<i64x2*>(t.lc + g));
+      if (w0) t.pi[g] = kPiFollowsLc;
+      if (w1) t.pi[g + 1] = kPiFollowsLc;
+    } else {
+      if (c0) {
+        t.lc[g] = o0;
+        if (w0) t.pi[g] = kPiFollowsLc;
+      }
+      if (c1) {
+        t.lc[g + 1] = o1;
+        if (w1) t.pi[g + 1] = kPiFollowsLc;
+      }
+    }
+    if (t.status) {  // a flagged group's status is written by the walk
+      if (g + 1 < t.G && !f0 && !f1)
+        __builtin_nontemporal_store(static_cast<uint16_t>(s01), reinterpret_cast<uint16_t*>(t.status + g));
+      else {
+        if (!f0) t.status[g] = static_cast<uint8_t>(s01);
+        if (!f1 && g + 1 < t.G) t.status[g + 1] = static_cast<uint8_t>(s01 >> 8);
+      }
+    }
   }
   if (lane == 0) wave_cnt[w] = cnt;
   lds_barrier();  // (the results' stores stay in flight)
