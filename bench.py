@@ -38,7 +38,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 QUORUM_EPOCH_BUFFERS = 6
-LEGS = ("quorum", "table", "drive", "C2", "C3K", "C5", "C1", "ae", "v2", "snapshot", "pinned",
+LEGS = ("quorum", "table", "drive", "C2", "C2L", "C3K", "C5", "C1", "ae", "v2", "snapshot", "pinned",
         "lease", "fanout", "peak", "cpu")
 
 
@@ -761,7 +761,25 @@ def leg_c2(ctx, args):
     # per group-epoch: match 8P + lastAppended 8 read, committed 8 + status 1 written (41 B at
     # P = 3); pendingIndex / lastCommitted / conf once per group
     alg = G2 * KE * 41 + G2 * 24
-    # 256 epochs per launch: the kernel's ramp and tail spread over 4x the work
+    return {"workload": "C2: 10k groups x 3 peers x 1k pending (configs[1])",
+            "decisions_per_s": G2 / (one_ms * 1e-3), "kernel_ms": one_ms,
+            "entry_ballots_per_s": G2 * 1024 / (one_ms * 1e-3),
+            "batched_epochs": {"epochs_per_launch": KE, "kernel_ms": k_ms,
+                               "decisions_per_s": G2 * KE / (k_ms * 1e-3),
+                               "roofline": roofline(alg, k_ms, kernel="quorum_epochs_kernel<3>",
+                                                    **pmc_traffic("C2", "quorum_epochs_kernel<3,")),
+                               "bit_exact_vs_oracle_256_groups": ok}}
+
+
+def leg_c2l(ctx, args):
+    """configs[1] with 256 successive epochs per launch (jrq_quorum_epochs_dev): the scan
+    kernel's ramp and tail spread over 4x the work of the 64-epoch launch.  Its own leg, so its
+    PMC pass (one leg per pass) attributes this launch shape's bytes to it alone."""
+    import torch
+
+    from jraft_amd import workloads as W
+    eng, dev = ctx.eng, ctx.dev
+    G2 = W.quorum_batch("C2")["pending_index"].shape[0]
     KL = 256
     serl = W.quorum_epoch_series("C2", KL)
     serl_d = {k: to_dev(v, dev) for k, v in serl.items()}
@@ -773,6 +791,7 @@ def leg_c2(ctx, args):
     kl_ms, _ = ctx.timed(lambda i: c2l_launch())
     ok_l = None
     if ctx.oracle_checks:  # 64 groups, all KL epochs, state carried
+        import jraft_oracle as O
         sub = np.random.default_rng(3).choice(G2, 64, replace=False)
         pi = serl["pending_index"][sub].copy()
         lc = serl["last_committed"][sub].copy()
@@ -787,19 +806,11 @@ def leg_c2(ctx, args):
             ok_l = ok_l and bool(np.array_equal(got[k, sub], ce))
     alg_l = G2 * KL * 41 + G2 * 24
     del serl_d, klc, kls
-    return {"workload": "C2: 10k groups x 3 peers x 1k pending (configs[1])",
-            "decisions_per_s": G2 / (one_ms * 1e-3), "kernel_ms": one_ms,
-            "entry_ballots_per_s": G2 * 1024 / (one_ms * 1e-3),
-            "batched_epochs": {"epochs_per_launch": KE, "kernel_ms": k_ms,
-                               "decisions_per_s": G2 * KE / (k_ms * 1e-3),
-                               "roofline": roofline(alg, k_ms, kernel="quorum_epochs_kernel<3>",
-                                                    **pmc_traffic("C2", "quorum_epochs_kernel<3,")),
-                               "bit_exact_vs_oracle_256_groups": ok},
-            "batched_epochs_256": {"epochs_per_launch": KL, "kernel_ms": kl_ms,
-                                   "decisions_per_s": G2 * KL / (kl_ms * 1e-3),
-                                   "roofline": roofline(alg_l, kl_ms, kernel="quorum_epochs_kernel<3>",
-                                                        **pmc_traffic("C2", "quorum_epochs_kernel<3,")),
-                                   "bit_exact_vs_oracle_64_groups": ok_l}}
+    return {"epochs_per_launch": KL, "kernel_ms": kl_ms,
+            "decisions_per_s": G2 * KL / (kl_ms * 1e-3),
+            "roofline": roofline(alg_l, kl_ms, kernel="quorum_epochs_kernel<3>",
+                                 **pmc_traffic("C2L", "quorum_epochs_kernel<3,")),
+            "bit_exact_vs_oracle_64_groups": ok_l}
 
 
 def leg_c3k(ctx, args, G):
@@ -1233,7 +1244,8 @@ def leg_fanout(ctx, args, G):
         eng.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
                              t["last_committed"], t["conf"], c, status)
         cq_size0 = t["last_appended"] - t["pending_index"] + 1
-        fan_sets.append({"prev": t["last_committed"], "c": c, "la": t["last_committed"],
+        # lastApplied: its own array (FSMCaller's), equal to lastCommitted before the epoch
+        fan_sets.append({"prev": t["last_committed"], "c": c, "la": t["last_committed"].clone(),
                          "cf0": t["pending_index"], "cs0": cq_size0,
                          "cf": torch.empty_like(c), "cs": torch.empty_like(c)})
     fan_fc = torch.empty(G, dtype=torch.int64, device=dev)
@@ -1378,6 +1390,8 @@ def main():
         line["end_to_end_host_mirror"] = leg_drive(ctx, args, G)
     if "C2" in legs:
         line["C2"] = leg_c2(ctx, args)
+    if "C2L" in legs:
+        line.setdefault("C2", {})["batched_epochs_256"] = leg_c2l(ctx, args)
     if "C3K" in legs:
         line["C3_k_epochs"] = leg_c3k(ctx, args, G)
     extras = {}

@@ -90,11 +90,14 @@ __device__ __forceinline__ int64_t table_run_lane(const JrqTableArgs& t, uint32_
 // LDS (the first 16 flagged groups of a wave; a wave-local hand-off, no barrier), and its runs
 // come from the wave's flagged-entry slots (table_flags_kernel writes them with every header
 // update: only headers change runs), spread over a lane quad by shuffles, one conf run per lane
-// (the table holds at most 4).  The wave loads its count and its first two entries together
-// with its single-conf loads, so a flagged group costs no dependent round trip to memory and no
-// workgroup barrier (round 2 deferred flagged groups to an LDS list behind a barrier and
-// reloaded them: +25 % on C3 with 1 % flagged, tools/flag_probe.hip).  Beyond 16 flagged
-// groups in one wave the walk reloads the group from memory.
+// (the table holds at most 4).  The wave copies its first four entries to LDS beside its
+// single-conf loads and counts its flagged groups by ballot, and it walks them before issuing
+// any store, so a flagged group costs no dependent round trip to memory, no wait for the wave's
+// stores and no workgroup barrier (round 2 deferred flagged groups to an LDS list behind a
+// barrier and reloaded them: +25 % on C3 with 1 % flagged, tools/flag_probe.hip; round 3's
+// first walk came after the stores and read entries through a generic pointer, and every flat
+// load drained the wave's stores).  Beyond 4 flagged groups in one wave the walk reads the
+// further entries from memory, beyond 16 it reloads the group too.
 // The one barrier left is the compaction's: list entries are staged per wave in LDS, and one
 // 64-bit atomic per workgroup ({done << 32 | entries}) on its segment's counter (workgroup b
 // -> segment b % kTableSegments: same-address atomics serialise, ~14 ns each,
