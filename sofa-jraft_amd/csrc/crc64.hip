@@ -38,9 +38,6 @@
 #define JRQ_CRC_LOAD_AUX 0  // cache-policy bits of the payload ring loads (2 = nt on gfx950)
 #endif
 
-#ifndef JRQ_CRC_RING
-#define JRQ_CRC_RING 3  // half-round register ring depth of the rounds kernel (3 or 4)
-#endif
 
 namespace jrq {
 
@@ -511,11 +508,11 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     // Ring of three half-rounds (64 B per lane each, 16 VGPRs): two in flight while one is
     // hashed.  Half-round h: load q reads 16 B of owner lane 16q + c at segment offset
     // 64h + 16*row, so each row group reads 64 contiguous bytes of one owner per instruction.
-#if JRQ_CRC_RING == 4
+    // The boundary-free shape (!kRegs, 512 threads) runs a ring of four, the two halves of a
+    // 128-B line loaded back to back (see the loop); the register boundary path (768 threads,
+    // 168 VGPRs) keeps three.
+    constexpr bool kRing4 = !kRegs;
     u32x4 h0[4], h1[4], h2[4], h3[4];
-#else
-    u32x4 h0[4], h1[4], h2[4];
-#endif
     // Each half-round's loads use a descriptor whose base is advanced by the half's offset
     // (scalar adds), so the per-lane voffsets stay loop-invariant: no VALU address temps
     // that the register allocator could place on a ring slot still being loaded (such a
@@ -703,60 +700,65 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
       row_transpose(v[0], v[1], v[2], v[3]);
     };
 
-#if JRQ_CRC_RING == 4
-    // 4-slot ring: three half-rounds in flight while one is hashed
-    JRQ_LOAD_HALF(h2, last_half(2u));
-    for (uint32_t hh0 = 0; hh0 < halves; hh0 += 4) {
-      const uint32_t hh = __builtin_amdgcn_readfirstlane(hh0);  // keep the counter in SGPRs
-      if (a.prio_steps) {  // wave-uniform: lower this wave's priority as it gets ahead
-        const uint32_t prog = prog0 + hh;
-        const uint32_t lvl = __builtin_amdgcn_readfirstlane(
-            static_cast<uint32_t>(prog >= pt0) + (prog >= pt1) + (prog >= pt2));
-        if (lvl != prio_lvl) {
-          prio_lvl = lvl;
-          if (lvl == 1) __builtin_amdgcn_s_setprio(2);
-          else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
-          else __builtin_amdgcn_s_setprio(0);
+    if constexpr (kRing4) {
+      // 4-slot ring, the two halves of a 128-B line loaded back to back: the line's second
+      // half then meets its first half's fill in L2.  With the halves issued one step apart,
+      // 15-19 % of the lines were fetched twice (rocprofv3 TCC_EA0_RDREQ_128B, DESIGN.md
+      // §4.2): the waves of an XCD walk segments 2^k bytes apart in step, so they contend for
+      // the same L2 sets, and a line could be evicted between its two halves.
+      JRQ_LOAD_HALF(h2, last_half(2u));
+      JRQ_LOAD_HALF(h3, last_half(3u));
+      for (uint32_t hh0 = 0; hh0 < halves; hh0 += 4) {
+        const uint32_t hh = __builtin_amdgcn_readfirstlane(hh0);  // keep the counter in SGPRs
+        if (a.prio_steps) {  // wave-uniform: lower this wave's priority as it gets ahead
+          const uint32_t prog = prog0 + hh;
+          const uint32_t lvl = __builtin_amdgcn_readfirstlane(
+              static_cast<uint32_t>(prog >= pt0) + (prog >= pt1) + (prog >= pt2));
+          if (lvl != prio_lvl) {
+            prio_lvl = lvl;
+            if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+            else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+          }
         }
+        transpose_half(h0);
+        process(hh, h0);
+        transpose_half(h1);
+        if (hh + 1 < halves) process(hh + 1, h1);  // wave-uniform
+        JRQ_LOAD_HALF(h0, last_half(hh + 4));
+        JRQ_LOAD_HALF(h1, last_half(hh + 5));
+        transpose_half(h2);
+        if (hh + 2 < halves) process(hh + 2, h2);
+        transpose_half(h3);
+        if (hh + 3 < halves) process(hh + 3, h3);
+        JRQ_LOAD_HALF(h2, last_half(hh + 6));
+        JRQ_LOAD_HALF(h3, last_half(hh + 7));
       }
-      JRQ_LOAD_HALF(h3, last_half(hh + 3));
-      transpose_half(h0);
-      process(hh, h0);
-      JRQ_LOAD_HALF(h0, last_half(hh + 4));
-      transpose_half(h1);
-      if (hh + 1 < halves) process(hh + 1, h1);  // wave-uniform
-      JRQ_LOAD_HALF(h1, last_half(hh + 5));
-      transpose_half(h2);
-      if (hh + 2 < halves) process(hh + 2, h2);
-      JRQ_LOAD_HALF(h2, last_half(hh + 6));
-      transpose_half(h3);
-      if (hh + 3 < halves) process(hh + 3, h3);
-    }
-#else
-    for (uint32_t hh0 = 0; hh0 < halves; hh0 += 3) {
-      const uint32_t hh = __builtin_amdgcn_readfirstlane(hh0);  // keep the counter in SGPRs
-      if (a.prio_steps) {  // wave-uniform: lower this wave's priority as it gets ahead
-        const uint32_t prog = prog0 + hh;
-        const uint32_t lvl = __builtin_amdgcn_readfirstlane(
-            static_cast<uint32_t>(prog >= pt0) + (prog >= pt1) + (prog >= pt2));
-        if (lvl != prio_lvl) {
-          prio_lvl = lvl;
-          if (lvl == 1) __builtin_amdgcn_s_setprio(2);
-          else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
-          else __builtin_amdgcn_s_setprio(0);
+    } else {
+      for (uint32_t hh0 = 0; hh0 < halves; hh0 += 3) {
+        const uint32_t hh = __builtin_amdgcn_readfirstlane(hh0);  // keep the counter in SGPRs
+        if (a.prio_steps) {  // wave-uniform: lower this wave's priority as it gets ahead
+          const uint32_t prog = prog0 + hh;
+          const uint32_t lvl = __builtin_amdgcn_readfirstlane(
+              static_cast<uint32_t>(prog >= pt0) + (prog >= pt1) + (prog >= pt2));
+          if (lvl != prio_lvl) {
+            prio_lvl = lvl;
+            if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+            else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+          }
         }
+        JRQ_LOAD_HALF(h2, last_half(hh + 2));
+        transpose_half(h0);
+        process(hh, h0);
+        JRQ_LOAD_HALF(h0, last_half(hh + 3));
+        transpose_half(h1);
+        if (hh + 1 < halves) process(hh + 1, h1);  // wave-uniform
+        JRQ_LOAD_HALF(h1, last_half(hh + 4));
+        transpose_half(h2);
+        if (hh + 2 < halves) process(hh + 2, h2);
       }
-      JRQ_LOAD_HALF(h2, last_half(hh + 2));
-      transpose_half(h0);
-      process(hh, h0);
-      JRQ_LOAD_HALF(h0, last_half(hh + 3));
-      transpose_half(h1);
-      if (hh + 1 < halves) process(hh + 1, h1);  // wave-uniform
-      JRQ_LOAD_HALF(h1, last_half(hh + 4));
-      transpose_half(h2);
-      if (hh + 2 < halves) process(hh + 2, h2);
     }
-#endif
 #undef JRQ_LOAD_HALF
   }
 }
@@ -934,6 +936,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   load_half(h0);
   load_half(h1);
   load_half(h2);
+  load_half(h3);
   build_tables();
   // LogEntry fields: absent arrays read word 0 of the slice table (R0[0] = 0), masked below
   const uint64_t* const z = a.slice;
@@ -961,19 +964,24 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     }
     RState s{0u, 0u};
     uint32_t q = 0;
+    // the two halves of a 128-B line go out back to back (slots h0 + h1, h2 + h3): the
+    // line's second half then meets its first half's fill in L2.  Issued one step apart,
+    // 15 % of the lines were fetched twice (rocprofv3 TCC_EA0_RDREQ_128B):
+    // the waves of an XCD walk rows 2^k bytes apart in step, so they contend for the same
+    // L2 sets and a line could be evicted between its two halves.
     do {
-      load_half(h3);
       transpose_ring(h0);
       tb.step64(s, h0, lds);
-      load_half(h0);
       transpose_ring(h1);
       tb.step64(s, h1, lds);
+      load_half(h0);
       load_half(h1);
       transpose_ring(h2);
       tb.step64(s, h2, lds);
-      load_half(h2);
       transpose_ring(h3);
       tb.step64(s, h3, lds);
+      load_half(h2);
+      load_half(h3);
     } while (++q < turns);
     uint64_t c = crc_value(s);
     if (kStarts) {  // hashed [ps - b, ps - b + PS): drop the b bytes before, add the b missed

@@ -45,7 +45,8 @@ def main():
     import bench
     tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
     os.makedirs(PROF, exist_ok=True)
-    res = {"tag": tag, "csrc_sha": bench.csrc_sha(), "correction": "2*FETCH_SIZE+WRITE_SIZE (MI355X_MICROARCH.md HBM section), KiB->B",
+    res = {"tag": tag, "csrc_sha": bench.csrc_sha(), "correction": "2*FETCH_SIZE+WRITE_SIZE (MI355X_MICROARCH.md HBM section), KiB->B; "
+           "read_bytes_by_request_size = 32 n32 + 64 n64 + 128 n128 (TCC_EA0_RDREQ_{32,64,128}B) where collected",
            "kernel_stats": {}, "legs": collections.defaultdict(lambda: collections.defaultdict(dict))}
     st = os.path.join(OUT, "prof", "run_kernel_stats.csv")
     if os.path.exists(st):
@@ -74,11 +75,19 @@ def main():
             v.sort()
             res["legs"][leg][k]["duration_ns_median"] = float(v[len(v) // 2])
             res["legs"][leg][k]["dispatches"] = len(v)
+    sizes = ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")
     for leg, ks in res["legs"].items():
         for k, v in ks.items():
             if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
                 v["hbm_bytes_per_launch"] = (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
                 v["hbm_bytes_per_launch_raw"] = (v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
+            # the `rdreq` passes: read requests by size, so read bytes need no width rule
+            if all(c in v for c in sizes):
+                v["read_bytes_by_request_size"] = (32 * v[sizes[0]] + 64 * v[sizes[1]] +
+                                                   128 * v[sizes[2]])
+                if "WRITE_SIZE" in v:
+                    v["hbm_bytes_per_launch_by_request_size"] = (v["read_bytes_by_request_size"] +
+                                                                 v["WRITE_SIZE"] * 1024)
     res["legs"] = {k: dict(v) for k, v in res["legs"].items()}
     with open(os.path.join(PROF, f"{tag}_pmc.json"), "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
