@@ -252,7 +252,10 @@ struct JrqQuorumArgs {
 namespace jrq {
 constexpr int kTableMaxRuns = 4;                   // JRQ_TABLE_MAX_RUNS
 constexpr uint32_t kTableSegments = 16;            // JRQ_TABLE_SEGMENTS
-constexpr uint32_t kTableBlockGroups = 2048;       // groups per epoch workgroup
+#ifndef JRQ_TABLE_BLOCK_GROUPS
+#define JRQ_TABLE_BLOCK_GROUPS 2048
+#endif
+constexpr uint32_t kTableBlockGroups = JRQ_TABLE_BLOCK_GROUPS;  // groups per epoch workgroup
 constexpr int64_t kPiFollowsLc = INT64_MIN;        // JRQ_PI_FOLLOWS_LC
 constexpr uint32_t kFlagSlots = 128;               // flagged-entry slots per 128-group wave
 }  // namespace jrq

@@ -39,6 +39,7 @@ for s in $STEPS; do
     host)  run host_test 300 ./tests/_build/host_test gpu ;;
     tprobe) run table_probe 120 ./tools/table_probe ;;
     fprobe) run flag_probe 120 ./tools/flag_probe ;;
+    fprobe2) run flag_probe_b1024 120 ./tools/flag_probe_b1024 ;;
     pprobe) run pair_probe 120 ./tools/pair_probe ;;
     vprobe) run v2_parse_probe 120 ./tools/v2_parse_probe ;;
     sqpmc) run sqpmc_${TRACE_LEGS:-v2} 120 rocprofv3 --kernel-trace --pmc ${SQ_COUNTERS:-SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_INSTS_SMEM SQ_BUSY_CYCLES} -d gpurun_out/sqpmc_${TRACE_LEGS:-v2} -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs ${TRACE_LEGS:-v2} ;;

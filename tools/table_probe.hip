@@ -176,6 +176,16 @@ int main() {
   CK(hipMalloc(&a.changed, static_cast<size_t>(G) * 8 * 17 + 8 * 65536));
   CK(hipMalloc(&a.n_changed, 64));
   a.seg_cap = jrq_table_seg_cap(G);
+  // the flagged-entry slots the product kernel reads (no group flagged here: all zero), laid
+  // out as jrq_table_create lays them out
+  {
+    const size_t waves = static_cast<size_t>((G + jrq::kTableBlockGroups - 1) / jrq::kTableBlockGroups) *
+                         (jrq::kTableBlockGroups / 128);
+    const size_t fbytes = waves * jrq::kFlagSlots * 64 + waves * 4 + 64;
+    CK(hipMalloc(&a.flag_ent, fbytes));
+    CK(hipMemset(a.flag_ent, 0, fbytes));
+    a.flag_wcnt = reinterpret_cast<uint32_t*>(a.flag_ent + waves * jrq::kFlagSlots * 8);
+  }
   hipLaunchKernelGGL(probe::init, dim3(G / 256), dim3(256), 0, 0, a, 12345ull);
   int64_t *pi0, *lc0;
   CK(hipMalloc(&pi0, G * 8));
