@@ -903,8 +903,9 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   };
   if (kStarts) set_row(r0);
   // load cursor (row, half of the entry) of the next half-round to issue, scalar; past the
-  // wave's last row it keeps re-reading that row's last half (L2-hot, results unused)
-  uint32_t crow = r0, chalf = 0;
+  // wave's last half its loads get an empty descriptor (zeros, no memory request: re-reading
+  // that half cost up to 3 % of the bytes when the line had left L2)
+  uint32_t crow = r0, chalf = 0, cur_live = 1u;
   auto load_half = [&](u32x4 (&H)[4]) {
     const uint64_t o = kStarts ? row_base + static_cast<uint64_t>(chalf) * 64u
                                : static_cast<uint64_t>(crow) * 64u * PS + static_cast<uint64_t>(chalf) * 64u;
@@ -914,8 +915,8 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     // lanes past entry n-1 read zeros; kStarts: the dword past the last chunk of the batch may
     // lie past the payload (gate[3] = its end): zeros too
     const uint64_t left = total - o;
-    const uint32_t hn = __builtin_amdgcn_readfirstlane(
-        static_cast<uint32_t>(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left));
+    const uint32_t hn = cur_live ? __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left)) : 0u;
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<uint8_t*>((static_cast<uint64_t>(hhi) << 32) | hlo),
         static_cast<short>(0), static_cast<int>(hn), 0x00020000);
@@ -930,6 +931,8 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
       ++crow;
       chalf = 0;
       if (kStarts) set_row(crow);
+    } else {
+      cur_live = 0u;
     }
   };
   u32x4 h0[4], h1[4], h2[4], h3[4];
