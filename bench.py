@@ -1335,6 +1335,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.legs == "all":
+        # the scaling runs measure the headline (C4 sharded over the ranks); the other legs are
+        # single-GPU measurements of one rank's work and would only lengthen every N > 1 run
+        legs = {"quorum"}
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
