@@ -1,0 +1,132 @@
+// loadpat_probe.hip -- the CRC kernels' load pattern alone (tools only; not part of libjrq).
+// 1 GiB, 2048 waves (256 workgroups of 512 threads, as crc64_fixed_kernel runs C5), each lane
+// owning one 8 KiB piece and XOR-folding it (no table lookups), through
+//   p16x64  16 owners x 64 B per instruction, 4 instructions per 64-B half, two halves of a line
+//           issued back to back (the product's shape)
+//   p8x128  8 owners x 128 B per instruction (full lines), 8 instructions per 128-B round
+//   contig  each instruction 1 KiB contiguous (64 lanes x 16 B; the plain-read floor)
+// Ring: 256 B per lane in flight in every variant.  Reports the median of 20 launches.
+//   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/loadpat_probe tools/loadpat_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                                \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) {                                                                  \
+      std::printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);     \
+      std::exit(1);                                                                          \
+    }                                                                                        \
+  } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kPS = 8192;     // piece bytes per lane
+constexpr uint32_t kBlock = 512;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* p, uint32_t n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), static_cast<short>(0),
+                                           static_cast<int>(n), 0x00020000);
+}
+
+__device__ __forceinline__ uint32_t fold(const u32x4& v) { return v.x ^ v.y ^ v.z ^ v.w; }
+
+// mode 0: p16x64, 1: p8x128, 2: contig
+template <int kMode>
+__global__ __launch_bounds__(kBlock) void probe(const uint8_t* buf, uint32_t* out) {
+  const uint32_t L = threadIdx.x & 63u;
+  const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  const uint8_t* wb = buf + static_cast<size_t>(wave) * 64u * kPS;  // the wave's 64 pieces
+  const __amdgpu_buffer_rsrc_t r = rsrc(wb, 64u * kPS);
+  uint32_t acc = 0;
+  if (kMode == 0) {
+    const uint32_t qb = (L & 15u) * kPS + 16u * (L >> 4);
+    u32x4 h[4][4];
+    auto ld = [&](u32x4 (&H)[4], uint32_t half) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, qb + j * 16u * kPS + half * 64u, 0, 0);
+    };
+    ld(h[0], 0); ld(h[1], 1); ld(h[2], 2); ld(h[3], 3);
+    for (uint32_t t = 0; t < kPS / 256; ++t) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc ^= fold(h[0][j]) ^ fold(h[1][j]);
+      ld(h[0], 4 * t + 4); ld(h[1], 4 * t + 5);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc ^= fold(h[2][j]) ^ fold(h[3][j]);
+      ld(h[2], 4 * t + 6); ld(h[3], 4 * t + 7);
+    }
+  } else if (kMode == 1) {
+    const uint32_t qb = (L & 7u) * kPS + 16u * (L >> 3);
+    u32x4 h[2][8];
+    auto ld = [&](u32x4 (&H)[8], uint32_t round) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, qb + j * 8u * kPS + round * 128u, 0, 0);
+    };
+    ld(h[0], 0); ld(h[1], 1);
+    for (uint32_t t = 0; t < kPS / 256; ++t) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc ^= fold(h[0][j]);
+      ld(h[0], 2 * t + 2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc ^= fold(h[1][j]);
+      ld(h[1], 2 * t + 3);
+    }
+  } else {
+    // each instruction 1 KiB contiguous: the wave's 512 KiB in order
+    u32x4 h[2][8];
+    auto ld = [&](u32x4 (&H)[8], uint32_t blk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (blk * 8u + j) * 1024u + L * 16u, 0, 0);
+    };
+    ld(h[0], 0); ld(h[1], 1);
+    for (uint32_t t = 0; t < kPS / 256; ++t) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc ^= fold(h[0][j]);
+      ld(h[0], 2 * t + 2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc ^= fold(h[1][j]);
+      ld(h[1], 2 * t + 3);
+    }
+  }
+  out[blockIdx.x * kBlock + threadIdx.x] = acc;
+}
+
+int main() {
+  const size_t bytes = size_t(1) << 30;
+  const uint32_t waves = static_cast<uint32_t>(bytes / (64ull * kPS));  // 2048
+  const uint32_t grid = waves / (kBlock / 64);
+  uint8_t* buf;
+  uint32_t* out;
+  // room for the surplus loads past the last piece (up to two rounds)
+  CK(hipMalloc(&buf, bytes + (1 << 20)));
+  CK(hipMemset(buf, 0x5A, bytes + (1 << 20)));
+  CK(hipMalloc(&out, static_cast<size_t>(grid) * kBlock * 4));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto run = [&](const char* name, auto launch) {
+    std::vector<float> ms;
+    for (int i = 0; i < 25; ++i) {
+      CK(hipEventRecord(e0, 0));
+      launch();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float t = 0;
+      CK(hipEventElapsedTime(&t, e0, e1));
+      if (i >= 5) ms.push_back(t);
+    }
+    std::sort(ms.begin(), ms.end());
+    std::printf("%-8s median %7.1f us  min %7.1f us  %6.2f TB/s\n", name, ms[ms.size() / 2] * 1e3,
+                ms[0] * 1e3, bytes / (ms[ms.size() / 2] * 1e-3) / 1e12);
+  };
+  for (int rep = 0; rep < 2; ++rep) {
+    run("p16x64", [&] { hipLaunchKernelGGL(probe<0>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
+    run("p8x128", [&] { hipLaunchKernelGGL(probe<1>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
+    run("contig", [&] { hipLaunchKernelGGL(probe<2>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
+  }
+  CK(hipDeviceSynchronize());
+  return 0;
+}
