@@ -5,7 +5,8 @@
 //           issued back to back (the product's shape)
 //   p8x128  8 owners x 128 B per instruction (full lines), 8 instructions per 128-B round
 //   contig  each instruction 1 KiB contiguous (64 lanes x 16 B; the plain-read floor)
-// Ring: 256 B per lane in flight in every variant.  Reports the median of 20 launches.
+//   p16x64r8  the product's shape with an 8-slot ring (512 B per lane in flight)
+// Ring: 256 B per lane in flight in the first three.  Reports the median of 20 launches.
 //   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/loadpat_probe tools/loadpat_probe.hip
 #include <hip/hip_runtime.h>
 
@@ -57,6 +58,24 @@ __global__ __launch_bounds__(kBlock) void probe(const uint8_t* buf, uint32_t* ou
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc ^= fold(h[2][j]) ^ fold(h[3][j]);
       ld(h[2], 4 * t + 6); ld(h[3], 4 * t + 7);
+    }
+  } else if (kMode == 3) {  // p16x64 with an 8-slot ring (512 B per lane in flight)
+    const uint32_t qb = (L & 15u) * kPS + 16u * (L >> 4);
+    u32x4 h[8][4];
+    auto ld = [&](u32x4 (&H)[4], uint32_t half) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, qb + j * 16u * kPS + half * 64u, 0, 0);
+    };
+#pragma unroll
+    for (int s = 0; s < 8; ++s) ld(h[s], s);
+    for (uint32_t t = 0; t < kPS / 512; ++t) {
+#pragma unroll
+      for (int s = 0; s < 8; s += 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc ^= fold(h[s][j]) ^ fold(h[s + 1][j]);
+        ld(h[s], 8 * t + 8 + s);
+        ld(h[s + 1], 8 * t + 9 + s);
+      }
     }
   } else if (kMode == 1) {
     const uint32_t qb = (L & 7u) * kPS + 16u * (L >> 3);
@@ -126,6 +145,7 @@ int main() {
     run("p16x64", [&] { hipLaunchKernelGGL(probe<0>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
     run("p8x128", [&] { hipLaunchKernelGGL(probe<1>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
     run("contig", [&] { hipLaunchKernelGGL(probe<2>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
+    run("p16x64r8", [&] { hipLaunchKernelGGL(probe<3>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
   }
   CK(hipDeviceSynchronize());
   return 0;
