@@ -218,11 +218,11 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
           cand = c > cand ? c : cand;
         }
       }
-      cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 1)));
-      cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 2)));
+      cand = max(cand, dpp64<kDppXor1>(cand));
+      cand = max(cand, dpp64<kDppXor2>(cand));
       uint32_t s32 = st;
-      s32 |= __shfl_xor(s32, 1);
-      s32 |= __shfl_xor(s32, 2);
+      s32 |= dpp32<kDppXor1>(s32);
+      s32 |= dpp32<kDppXor2>(s32);
       if (act && r == 0) {
         // decide_runs: not the leader -> unchanged (BallotBox.java:101-103)
         a.committed[h] = hpi == 0 ? hlc : (cand > hlc ? cand : hlc);

@@ -11,6 +11,24 @@ constexpr int64_t kI64Min = INT64_MIN;
 constexpr int64_t kI64Max = INT64_MAX;
 constexpr uint64_t kConfRuns = 1ull << 63;  // include/jrq.h JRQ_CONF_RUNS
 
+// Lane exchanges of the run walks (table.hip, quorum.hip) as DPP moves (a VALU operand
+// modifier, no LDS round trip; __shfl_xor compiles to ds_bpermute, and the walks' reductions
+// were a chain of them):
+//   kDppXor1 / kDppXor2  quad_perm [1,0,3,2] / [2,3,0,1]: the partner lane 1 / 2 apart
+//   kDppHalfMirror       row_half_mirror: lane i of each 8-lane half row gets lane 7 - i, so
+//                        lane 0 of an 8-lane group sees lane 7 (the group's other quad)
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141;
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), kCtrl, 0xF, 0xF, false));
+}
+template <int kCtrl>
+__device__ __forceinline__ int64_t dpp64(int64_t x) {
+  const uint32_t lo = dpp32<kCtrl>(static_cast<uint32_t>(x));
+  const uint32_t hi = dpp32<kCtrl>(static_cast<uint32_t>(static_cast<uint64_t>(x) >> 32));
+  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
 // q-th largest of v[p] over the peers in `mask` (q >= 1); kI64Min if fewer than q members.
 // P <= 16: rank-by-counting, branch-free, P^2 compares on 64-bit values in registers.
 template <int P>

@@ -194,10 +194,14 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
   // Flagged group i of the wave on quad i % 16, one conf run per lane.
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the hand-off slots: this wave's)
   __builtin_amdgcn_wave_barrier();
-  const uint32_t q = lane >> 2, r = lane & 3u;
+  // eight lanes per flagged group: run r = (lane >> 1) & 3 of group slot lane >> 3, the lane
+  // pair splitting the run's two quorum checks (new conf, old conf: one q-th largest each,
+  // joined by one shuffle) -- the walk's VALU is what a flagged wave adds, and the two
+  // sorting networks were most of it
+  const uint32_t q = lane >> 3, r = (lane >> 1) & 3u, mh = lane & 1u;
   // this wave's flagged groups (f0 / f1 are false on lanes past the table)
   const uint32_t nflag = __popcll(__ballot(f0)) + __popcll(__ballot(f1));
-  for (uint32_t base = 0; base < nflag; base += 16) {  // (wave-uniform)
+  for (uint32_t base = 0; base < nflag; base += 8) {  // (wave-uniform)
     const uint32_t i = base + q;
     bool act = i < nflag;
     // the entry {group, start1, start2, start3, conf0 .. conf3}: run r's start, the next run's
@@ -221,8 +225,10 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
     const uint32_t h = static_cast<uint32_t>(eh);
     const int64_t rs = ers, nx = enx;
     act = act && h < t.G;  // (the flags kernel writes only table groups: a guard, not a case)
-    int64_t cand = kI64Min, hpr = 0, hlc = 0, hla = 0, pi = 0;
+    int64_t cand64 = kI64Min, hpr = 0, hlc = 0, hla = 0, pi = 0;
     uint8_t st = 0;
+    bool relp = false;
+    uint32_t kx = 0xFFFFFFFFu, sr = 0, er = 0;
     if (act) {
       int64_t hm[P];
       if (i < kHand) {  // from the owner lane, through LDS
@@ -253,20 +259,39 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
           RelGroup<P> rg;
           rel_map<P>(pi, hla, hm, rg);
           st = rg.st;
-          cand = run_candidate_rel<P>(rg, rc, pi, s, ee, st);
-        } else {
+          if (ee >= s) {  // run_candidate_rel, this lane's half of it
+            if ((rc & 0xFFFFu) == 0) st |= kStEmptyConf;
+            relp = true;
+            sr = static_cast<uint32_t>(s - pi) + 1u;
+            er = static_cast<uint32_t>(ee - pi) + 1u;
+            const uint32_t msk = static_cast<uint32_t>((rc >> (mh ? 16 : 0)) & 0xFFFFu);
+            const uint32_t qq = static_cast<uint32_t>((rc >> (mh ? 40 : 32)) & 0xFFu);
+            kx = qq == 0 ? rg.W : kth_largest_rel<P>(rg.r, msk, qq);
+          }
+        } else {  // both lanes of the pair: the whole 64-bit run_candidate
           st = mask_out_of_range<P>(hm, hla);
-          cand = run_candidate<P>(hm, rc, s, ee, st);
+          cand64 = run_candidate<P>(hm, rc, s, ee, st);
         }
       }
     }
-    cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 1)));
-    cand = max(cand, static_cast<int64_t>(__shfl_xor(static_cast<long long>(cand), 2)));
+    // the pair's two bounds (every lane exchanges: the wave stays converged)
+    const uint32_t kp = dpp32<kDppXor1>(kx);
+    int64_t cand = cand64;
+    if (relp) {
+      uint32_t c = kx < kp ? kx : kp;
+      c = c < er ? c : er;
+      cand = c >= sr ? pi - 1 + static_cast<int64_t>(c) : kI64Min;
+    }
+    // max over the group's 8 lanes, complete on its lead lane (the lane pairs agree already)
+    cand = max(cand, dpp64<kDppXor2>(cand));
+    cand = max(cand, dpp64<kDppHalfMirror>(cand));
     uint32_t s32 = st;
-    s32 |= __shfl_xor(s32, 1);
-    s32 |= __shfl_xor(s32, 2);
-    const bool commit = act && r == 0 && cand > hlc;  // pi == 0 (not the leader): kI64Min
-    if (act && r == 0) {
+    s32 |= dpp32<kDppXor1>(s32);
+    s32 |= dpp32<kDppXor2>(s32);
+    s32 |= dpp32<kDppHalfMirror>(s32);
+    const bool lead = (lane & 7u) == 0;
+    const bool commit = act && lead && cand > hlc;  // pi == 0 (not the leader): kI64Min
+    if (act && lead) {
       if (t.status) t.status[h] = static_cast<uint8_t>(s32);
       if (commit) table_commit_one(t, h, hpr, cand);
     }
