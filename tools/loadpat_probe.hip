@@ -6,6 +6,10 @@
 //   p8x128  8 owners x 128 B per instruction (full lines), 8 instructions per 128-B round
 //   contig  each instruction 1 KiB contiguous (64 lanes x 16 B; the plain-read floor)
 //   p16x64r8  the product's shape with an 8-slot ring (512 B per lane in flight)
+//   ldsdma  contig order through LDS: global_load_lds_dwordx4 into an 8-slot ring of 1 KiB per
+//           wave (8 KiB in flight per wave, 64 KiB per CU), each slot read back with ds_read_b128;
+//           ldsdmant the same with nt loads, ldsdma16[nt] with 16 slots (128 KiB per CU)
+//   contignt, p16x64nt, p8x128nt  those shapes with nt loads (aux 2)
 // Ring: 256 B per lane in flight in the first three.  Reports the median of 20 launches.
 //   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/loadpat_probe tools/loadpat_probe.hip
 #include <hip/hip_runtime.h>
@@ -43,12 +47,15 @@ __global__ __launch_bounds__(kBlock) void probe(const uint8_t* buf, uint32_t* ou
   const uint8_t* wb = buf + static_cast<size_t>(wave) * 64u * kPS;  // the wave's 64 pieces
   const __amdgpu_buffer_rsrc_t r = rsrc(wb, 64u * kPS);
   uint32_t acc = 0;
-  if (kMode == 0) {
+  if constexpr (kMode == 0 || kMode == 9) {
     const uint32_t qb = (L & 15u) * kPS + 16u * (L >> 4);
     u32x4 h[4][4];
     auto ld = [&](u32x4 (&H)[4], uint32_t half) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, qb + j * 16u * kPS + half * 64u, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (kMode == 9) H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, qb + j * 16u * kPS + half * 64u, 0, 2);
+        else H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, qb + j * 16u * kPS + half * 64u, 0, 0);
+      }
     };
     ld(h[0], 0); ld(h[1], 1); ld(h[2], 2); ld(h[3], 3);
     for (uint32_t t = 0; t < kPS / 256; ++t) {
@@ -59,7 +66,7 @@ __global__ __launch_bounds__(kBlock) void probe(const uint8_t* buf, uint32_t* ou
       for (int j = 0; j < 4; ++j) acc ^= fold(h[2][j]) ^ fold(h[3][j]);
       ld(h[2], 4 * t + 6); ld(h[3], 4 * t + 7);
     }
-  } else if (kMode == 3) {  // p16x64 with an 8-slot ring (512 B per lane in flight)
+  } else if constexpr (kMode == 3) {  // p16x64 with an 8-slot ring (512 B per lane in flight)
     const uint32_t qb = (L & 15u) * kPS + 16u * (L >> 4);
     u32x4 h[8][4];
     auto ld = [&](u32x4 (&H)[4], uint32_t half) {
@@ -77,12 +84,15 @@ __global__ __launch_bounds__(kBlock) void probe(const uint8_t* buf, uint32_t* ou
         ld(h[s + 1], 8 * t + 9 + s);
       }
     }
-  } else if (kMode == 1) {
+  } else if constexpr (kMode == 1 || kMode == 10) {
     const uint32_t qb = (L & 7u) * kPS + 16u * (L >> 3);
     u32x4 h[2][8];
     auto ld = [&](u32x4 (&H)[8], uint32_t round) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, qb + j * 8u * kPS + round * 128u, 0, 0);
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (kMode == 10) H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, qb + j * 8u * kPS + round * 128u, 0, 2);
+        else H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, qb + j * 8u * kPS + round * 128u, 0, 0);
+      }
     };
     ld(h[0], 0); ld(h[1], 1);
     for (uint32_t t = 0; t < kPS / 256; ++t) {
@@ -93,12 +103,41 @@ __global__ __launch_bounds__(kBlock) void probe(const uint8_t* buf, uint32_t* ou
       for (int j = 0; j < 8; ++j) acc ^= fold(h[1][j]);
       ld(h[1], 2 * t + 3);
     }
+  } else if constexpr (kMode >= 4 && kMode <= 7) {  // LDS-DMA ring: 4 = 8 slots, 5 = 8 nt, 6 = 16, 7 = 16 nt
+    constexpr int kS = kMode >= 6 ? 16 : 8;
+    // (the aux operand must be a literal: a template-dependent constant drops the kernel)
+    auto dma = [&](const uint8_t* g, uint32_t* l) {
+      if constexpr (kMode & 1) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g), l, 16, 0, 2);
+      else __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g), l, 16, 0, 0);
+    };
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];  // [waves][kS][256]
+    uint32_t(*ring)[kS][256] = reinterpret_cast<uint32_t(*)[kS][256]>(dyn_lds);
+    const uint32_t w = threadIdx.x >> 6;
+    const uint8_t* src = wb + L * 16u;
+#pragma unroll
+    for (int s = 0; s < kS; ++s)
+      dma(src + s * 1024u, &ring[w][s][0]);
+    for (uint32_t t = 0; t < 64u * kPS / 1024u; t += kS) {
+#pragma unroll
+      for (int s = 0; s < kS; ++s) {
+        // slot s landed: the kS - 1 loads issued after it may still be out (the compiler does
+        // not track LDS-DMA landings; the surplus loads of the last round read the slack)
+        if (kS == 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        const u32x4 v = *reinterpret_cast<const u32x4*>(&ring[w][s][L * 4u]);
+        acc ^= fold(v);
+        dma(src + (t + kS + s) * 1024u, &ring[w][s][0]);
+      }
+    }
   } else {
     // each instruction 1 KiB contiguous: the wave's 512 KiB in order
     u32x4 h[2][8];
     auto ld = [&](u32x4 (&H)[8], uint32_t blk) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (blk * 8u + j) * 1024u + L * 16u, 0, 0);
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (kMode == 8) H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (blk * 8u + j) * 1024u + L * 16u, 0, 2);
+        else H[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (blk * 8u + j) * 1024u + L * 16u, 0, 0);
+      }
     };
     ld(h[0], 0); ld(h[1], 1);
     for (uint32_t t = 0; t < kPS / 256; ++t) {
@@ -138,14 +177,23 @@ int main() {
       if (i >= 5) ms.push_back(t);
     }
     std::sort(ms.begin(), ms.end());
-    std::printf("%-8s median %7.1f us  min %7.1f us  %6.2f TB/s\n", name, ms[ms.size() / 2] * 1e3,
+    std::printf("%-10s median %7.1f us  min %7.1f us  %6.2f TB/s\n", name, ms[ms.size() / 2] * 1e3,
                 ms[0] * 1e3, bytes / (ms[ms.size() / 2] * 1e-3) / 1e12);
   };
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(probe<6>), hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(probe<7>), hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
   for (int rep = 0; rep < 2; ++rep) {
     run("p16x64", [&] { hipLaunchKernelGGL(probe<0>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
     run("p8x128", [&] { hipLaunchKernelGGL(probe<1>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
     run("contig", [&] { hipLaunchKernelGGL(probe<2>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
     run("p16x64r8", [&] { hipLaunchKernelGGL(probe<3>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
+    run("ldsdma", [&] { hipLaunchKernelGGL(probe<4>, dim3(grid), dim3(kBlock), 8 * 8 * 1024, 0, buf, out); });
+    run("ldsdmant", [&] { hipLaunchKernelGGL(probe<5>, dim3(grid), dim3(kBlock), 8 * 8 * 1024, 0, buf, out); });
+    run("ldsdma16", [&] { hipLaunchKernelGGL(probe<6>, dim3(grid), dim3(kBlock), 16 * 8 * 1024, 0, buf, out); });
+    run("ldsdma16nt", [&] { hipLaunchKernelGGL(probe<7>, dim3(grid), dim3(kBlock), 16 * 8 * 1024, 0, buf, out); });
+    run("p16x64nt", [&] { hipLaunchKernelGGL(probe<9>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
+    run("p8x128nt", [&] { hipLaunchKernelGGL(probe<10>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
+    run("contignt", [&] { hipLaunchKernelGGL(probe<8>, dim3(grid), dim3(kBlock), 0, 0, buf, out); });
   }
   CK(hipDeviceSynchronize());
   return 0;
