@@ -364,6 +364,17 @@ class Ctx:
         import torch
         torch.cuda.synchronize(self.dev)
 
+    def gather(self, x: float) -> list:
+        """x from every rank, in rank order (a one-float all-reduce per call)."""
+        if self.world == 1:
+            return [x]
+        import torch
+        import torch.distributed as dist
+        t = torch.zeros(self.world, dtype=torch.float64, device=self.dev)
+        t[self.rank] = x
+        dist.all_reduce(t)
+        return [float(v) for v in t.cpu()]
+
     def timed(self, fn, steps=None, warmup=None, warm_calls=None):
         a = self.args
         return timed_launches(fn, a.steps if steps is None else steps,
@@ -939,7 +950,10 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
     eb = W.entry_batch(n, c5["entry_bytes"], seed=W.SEED_BASE ^ 5 ^ rank)
     qb = W.quorum_batch("C5", group_offset=rank * n)
     expected = None
-    if ctx.oracle_checks:
+    # every rank checks its own shard (rank r's regions r*64k .. (r+1)*64k-1 carry their own
+    # payload seed): the oracle's byte-at-a-time pass over 1 GiB takes ~2 s per rank
+    checks = not args.no_cpu
+    if checks:
         import jraft_oracle as O
         expected = O.logentry_checksum_batch(eb["etype"], eb["index"], eb["term"], None,
                                              eb["payload"], eb["offsets"])
@@ -977,7 +991,7 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
     steps = max(10, args.steps)
     vo_ms, _ = ctx.timed(verify_offsets, steps, 2)
     ok_off = None
-    if ctx.oracle_checks:
+    if checks:
         ok_off = bool(np.array_equal(out.cpu().numpy().view(np.uint64), expected)) and \
             bool(np.array_equal(corrupt.cpu().numpy().astype(bool), flip))
     v_ms, _ = ctx.timed(verify, steps, 2)
@@ -987,8 +1001,7 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
     v_max, s_max = max_over_ranks(v_ms), max_over_ranks(s_ms)
     pay = n * c5["entry_bytes"]
     ok = step_ok = None
-    if ctx.oracle_checks:
-        import jraft_oracle as O
+    if checks:
         ok = bool(np.array_equal(out.cpu().numpy().view(np.uint64), expected)) and \
             bool(np.array_equal(corrupt.cpu().numpy().astype(bool), flip))
         ce, se, _ = O.quorum_epoch_replay(qb["match"], qb["pending_index"], qb["last_appended"],
@@ -997,8 +1010,14 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
             bool(np.array_equal(qs.cpu().numpy(), se))
     alg_v = crc_bytes(n, pay, verify=True, offsets=False)
     alg_c = quorum_bytes_per_group(3) * n
+    per_rank_ms = ctx.gather(v_ms)
+    per_rank_ok = ctx.gather(-1.0 if ok is None else float(ok))
     crc = {"metric": "LogEntry CRC64 verify GB/s",
            "value": pay * world / (v_max * 1e-3) / 1e9, "unit": "GB/s (payload)",
+           "per_rank_GBps": [pay / (m * 1e-3) / 1e9 for m in per_rank_ms],
+           "per_rank_bit_exact": [None if x < 0 else bool(x) for x in per_rank_ok],
+           "timing": "max over ranks of each rank's per-launch time (one event pair around "
+                     "the launches on its own stream)",
            "workload": "C5: 64k x 16 KiB DATA LogEntries per GPU, checksum + isCorrupted verify "
                        "(jrq_logentry_checksum_fixed_dev: 2 lanes per entry)",
            "ms_per_launch": v_ms, "bit_exact_vs_oracle": ok,
@@ -1007,8 +1026,12 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
                             "how": "jrq_logentry_checksum_batch_dev (segment walk + finish kernel)"},
            "roofline": roofline(alg_v, v_ms, kernel="crc64_fixed_kernel<true, false>",
                                 **pmc_traffic("C5", "crc64_fixed_kernel<true, false>"))}
-    c5_step = {"workload": "C5 as BASELINE states it: 64k regions x 3 replicas x 16 KiB entries; "
-                           "one step = CRC64 verify of the 64k entries + commit of the 64k groups",
+    per_rank_step_ok = ctx.gather(-1.0 if step_ok is None else float(step_ok))
+    c5_step = {"workload": f"C5 as BASELINE states it: 64k regions x 3 replicas x 16 KiB entries "
+                           f"per GPU ({n * world} regions over {world} GPU(s), region shards by "
+                           f"regionId); one step = CRC64 verify of the GPU's entries + commit of "
+                           f"its groups",
+               "per_rank_bit_exact": [None if x < 0 else bool(x) for x in per_rank_step_ok],
                "ms_per_step": s_ms, "verify_ms": v_ms, "commit_ms": c_ms,
                "regions_per_s": n * world / (s_max * 1e-3),
                "GBps_payload": pay * world / (s_max * 1e-3) / 1e9,
@@ -1305,6 +1328,176 @@ def leg_peak(ctx):
                    "xor into half-size output (2 reads + 1 write) / time"}
 
 
+# ------------------------------------------------------------------ the printed line --
+
+# The driver parses the one stdout line from a bounded tail of the run's output (round 3's
+# 20.8 KB line was not parsed; round 2's 13.2 KB one was).  The printed line keeps the contract
+# keys plus one small summary per leg; everything else goes to the detail file it names.
+LINE_BUDGET = 6000
+DETAIL_FILE = "bench_detail.json"
+
+
+def _r(x, nd=4):
+    """Round a float to `nd` significant digits (None passes through)."""
+    if x is None or isinstance(x, bool) or not isinstance(x, (int, float)):
+        return x
+    if x == 0 or isinstance(x, int):
+        return x
+    return float(f"{x:.{nd}g}")
+
+
+def _roof_summary(rl: dict | None) -> dict | None:
+    """The contract's roofline object (+ kernel name, per-launch ms and bytes)."""
+    if not rl:
+        return None
+    out = {k: _r(rl.get(k)) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic")}
+    out["kernel"] = rl.get("kernel")
+    out["kernel_ms"] = _r(rl.get("kernel_ms"), 5)
+    out["bytes_per_launch"] = rl.get("bytes_per_launch")
+    if rl.get("traffic") and rl.get("bytes_per_launch"):
+        out["traffic_ratio"] = _r(rl["traffic"] / rl["bytes_per_launch"], 3)
+    if rl.get("frac_survey_bytes") is not None:
+        out["frac_survey_bytes"] = _r(rl["frac_survey_bytes"])
+    pm = rl.get("peak_measured")
+    if pm:
+        out["peak_measured"] = {k: _r(v) for k, v in pm.items() if k != "how"}
+    return out
+
+
+def _cpu_summary(cb: dict | None) -> dict | None:
+    if not cb:
+        return None
+    out = {k: _r(cb.get(k)) for k in ("value", "unit", "cores", "kind")}
+    pt = cb.get("per_threads") or {}
+    out["per_threads"] = {k: _r(v["value"] if isinstance(v, dict) else v, 3) for k, v in pt.items()}
+    opt = (cb.get("optimised") or {}).get("per_threads")
+    if opt:
+        out["optimised_per_threads"] = {k: _r(v, 3) for k, v in opt.items()}
+    out["sample"] = cb.get("sample")
+    host = cb.get("host")
+    if host:
+        out["host"] = f"{host.get('model')}, cgroup quota {host.get('cgroup_cpu_quota')} CPUs"
+    return out
+
+
+def _bit_exact(d: dict):
+    """The leg's oracle verdict: every `bit_exact*` / `*_ok` flag it carries AND-ed (None when the
+    oracle did not run)."""
+    flags = [v for k, v in d.items() if (k.startswith("bit_exact") or k.endswith("_ok"))
+             and isinstance(v, bool)]
+    return all(flags) if flags else None
+
+
+def _leg_summary(d: dict, ms_key: str) -> dict:
+    rl = d.get("roofline") or {}
+    s = {"ms": _r(d.get(ms_key, rl.get("kernel_ms")), 5), "frac": _r(rl.get("frac"), 3)}
+    if rl.get("traffic") and rl.get("bytes_per_launch"):
+        s["traffic_ratio"] = _r(rl["traffic"] / rl["bytes_per_launch"], 3)
+    s["bit_exact"] = _bit_exact(d)
+    return s
+
+
+def compact_line(full: dict, detail_path: str | None = DETAIL_FILE) -> dict:
+    """The printed line: the contract keys, the headline's roofline / cpu_baseline / multi_gpu,
+    the second BASELINE metric (`crc64`) and one {ms, frac, traffic_ratio, bit_exact} per leg.
+    `full` is the whole result (written to `detail_path`)."""
+    keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+            "scaling", "vs_baseline", "dtype", "data", "config")
+    line = {k: _r(full.get(k), 6) if k in ("value", "ms_per_step") else full.get(k) for k in keys}
+    line["warm_ms"] = full.get("warm_ms")
+    line["csrc_sha"] = full.get("csrc_sha")
+    line["roofline"] = _roof_summary(full.get("roofline"))
+    line["cpu_baseline"] = _cpu_summary(full.get("cpu_baseline"))
+    mg = full.get("multi_gpu")
+    if mg:
+        line["multi_gpu"] = {k: _r(v) for k, v in mg.items()}
+    if "bit_exact_vs_oracle_4096_groups" in full:
+        line["bit_exact_vs_oracle_4096_groups"] = full["bit_exact_vs_oracle_4096_groups"]
+    crc = full.get("crc64")
+    if crc:
+        c = {k: _r(crc.get(k)) for k in ("metric", "value", "unit")}
+        c["ms_per_launch"] = _r(crc.get("ms_per_launch"), 5)
+        c["frac"] = _r((crc.get("roofline") or {}).get("frac"), 3)
+        c["bit_exact"] = _bit_exact(crc)
+        if crc.get("per_rank_GBps"):
+            c["per_rank_GBps"] = [_r(v) for v in crc["per_rank_GBps"]]
+            c["per_rank_bit_exact"] = crc.get("per_rank_bit_exact")
+        cb = crc.get("cpu_baseline")
+        if cb:
+            c["cpu_baseline"] = {k: _r(cb.get(k)) for k in ("value", "unit", "cores", "kind")}
+        line["crc64"] = c
+    legs = {}
+    if full.get("roofline"):
+        legs["quorum_C3"] = {"ms": _r(full["roofline"].get("kernel_ms"), 5),
+                             "frac": _r(full["roofline"].get("frac"), 3),
+                             "traffic_ratio": (_roof_summary(full["roofline"]) or {}).get("traffic_ratio"),
+                             "bit_exact": full.get("bit_exact_vs_oracle_4096_groups")}
+    t = full.get("resident_table")
+    if t:
+        legs["table"] = _leg_summary(t, "kernel_ms")
+        legs["table"]["over_no_conf"] = _r(t.get("flagged_over_no_conf_change"), 3)
+        legs["table"]["over_pair"] = _r(t.get("table_over_pair"), 3)
+    c2 = full.get("C2") or {}
+    if "kernel_ms" in c2:
+        legs["C2_one_epoch"] = {"ms": _r(c2["kernel_ms"], 5), "bit_exact": None}
+    if c2.get("batched_epochs"):
+        legs["C2_epochs"] = _leg_summary(c2["batched_epochs"], "kernel_ms")
+        legs["C2_epochs"]["epochs"] = c2["batched_epochs"].get("epochs_per_launch")
+    if c2.get("batched_epochs_256"):
+        legs["C2_epochs_256"] = _leg_summary(c2["batched_epochs_256"], "kernel_ms")
+    if full.get("C3_k_epochs"):
+        legs["C3_k_epochs"] = _leg_summary(full["C3_k_epochs"], "kernel_ms")
+    if crc:
+        legs["C5_verify"] = _leg_summary(crc, "ms_per_launch")
+        if crc.get("offsets_path"):
+            legs["C5_verify_offsets"] = {"ms": _r(crc["offsets_path"].get("ms_per_launch"), 5),
+                                         "bit_exact": crc["offsets_path"].get("bit_exact_vs_oracle")}
+    if full.get("C5"):
+        legs["C5_step"] = _leg_summary(full["C5"], "ms_per_step")
+    if full.get("C1"):
+        legs["C1"] = _leg_summary(full["C1"], "ms_per_step")
+        legs["C1"]["crc_ms"] = _r((full["C1"].get("roofline") or {}).get("kernel_ms"), 5)
+    for name, d in (full.get("next_rows") or {}).items():
+        ms_key = next((k for k in ("ms_per_batch", "archive_ms", "ms_per_launch", "kernel_ms") if k in d),
+                      None)
+        legs[name] = _leg_summary(d, ms_key)
+    drv = full.get("end_to_end_host_mirror")
+    if drv:
+        for k, v in drv.items():
+            if k.startswith("active_") and isinstance(v, dict):
+                legs["drive_" + k] = {"ms": _r(v.get("end_to_end_ms_per_epoch"), 4),
+                                      "flush_ms": _r(v.get("flush_ms"), 4),
+                                      "decisions_per_s": _r(v.get("decisions_per_s_end_to_end"), 3),
+                                      "bit_exact": v.get("bit_exact_vs_stateless_kernel")}
+    pin = full.get("pinned_host_payload")
+    if pin:
+        for k in ("C5", "C1"):
+            if k in pin:
+                legs["pinned_" + k] = {
+                    "GBps_pcie": _r(pin[k]["registered"]["GBps_payload_pcie_inclusive"], 3),
+                    "bit_exact": pin[k]["registered"].get("bit_exact_vs_oracle")}
+    line["legs"] = legs
+    line["detail"] = detail_path
+    return line
+
+
+def emit_line(full: dict, path: str) -> str:
+    """Write the whole result to the detail file `path` and return the compact line (checked
+    against the budget: the per-leg summary is dropped first, never the contract keys)."""
+    try:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path, "w") as fh:
+            json.dump(full, fh, indent=1)
+    except OSError as e:  # a read-only tree: the line still prints
+        print(f"warning: cannot write {path}: {e}", file=sys.stderr)
+    line = compact_line(full, os.path.relpath(path, ROOT))
+    s = json.dumps(line, separators=(",", ":"))
+    if len(s) > LINE_BUDGET:
+        line.pop("legs", None)
+        s = json.dumps(line, separators=(",", ":"))
+    return s
+
+
 # ------------------------------------------------------------------ main --
 
 def main():
@@ -1318,6 +1511,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=4.0,
                     help="seconds per CPU baseline leg and thread count")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--detail", default=os.path.join(ROOT, DETAIL_FILE),
+                    help="file for the full per-leg result (the printed line is the summary)")
     ap.add_argument("--legs", default="all",
                     help=f"comma list of {','.join(LEGS)} (the headline quorum leg always runs "
                          "unless the list omits it; PMC passes run one leg each)")
@@ -1336,9 +1531,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.legs == "all":
-        # the scaling runs measure the headline (C4 sharded over the ranks); the other legs are
+        # the scaling runs measure both BASELINE metrics: the headline (C4 sharded over the
+        # ranks) and C5 (64k regions per GPU: CRC64 verify + commit); the other legs are
         # single-GPU measurements of one rank's work and would only lengthen every N > 1 run
-        legs = {"quorum"}
+        legs = {"quorum", "C5"}
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
@@ -1437,7 +1633,9 @@ def main():
         if "crc64" in line:
             line["crc64"]["cpu_baseline"] = cpu["C5_crc"]
     if rank == 0:
-        print(json.dumps(line))
+        s = emit_line(line, os.path.abspath(args.detail))
+        sys.stderr.flush()
+        print(s, flush=True)
     eng.use_stream(None)
     if world > 1:
         dist.destroy_process_group()

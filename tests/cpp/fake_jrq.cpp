@@ -9,6 +9,7 @@
 // gathering, delivery, the flusher -- runs under the sanitizers with real epoch results.  It is
 // never built into libjrq.so, libjraft_host.so or anything bench.py or smoke() loads; the GPU
 // build of the same tests (tests/_build/host_test) links the real library.
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -151,6 +152,22 @@ int jrq_table_update_gather(jrq_table* t, uint32_t parts, const jrq_group_state*
   return JRQ_OK;
 }
 
+#ifdef FAKE_JRQ_CLOSED_FORM
+// The host-API cost probe (tools/api_probe.py) needs 1M-group epochs in milliseconds, not the
+// replay's seconds: the closed form of DESIGN.md §1 (a run [s, e] commits min(e, k_new, k_old)
+// when that is >= max(s, pendingIndex)), status left 0.
+static int64_t kth(const int64_t* m, uint32_t P, uint32_t mask, uint32_t q) {
+  if (q == 0) return INT64_MAX;
+  int64_t v[16];
+  uint32_t n = 0;
+  for (uint32_t p = 0; p < P; ++p)
+    if ((mask >> p) & 1u) v[n++] = m[p];
+  if (n < q) return INT64_MIN;
+  std::partial_sort(v, v + q, v + n, [](int64_t a, int64_t b) { return a > b; });
+  return v[q - 1];
+}
+#endif
+
 // One epoch, group by group through the oracle's BallotBox replay (jo_quorum_epoch_replay).
 int jrq_table_epoch(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, uint8_t* status_out) {
   std::lock_guard<std::mutex> l(t->mu);
@@ -160,12 +177,23 @@ int jrq_table_epoch(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, ui
     if (status_out) status_out[g] = JO_ST_NOT_LEADER;
     if (t->pi[g] == 0 || t->nr[g] == 0) continue;
     for (uint32_t p = 0; p < t->P; ++p) m[p] = t->match[static_cast<size_t>(g) * t->P + p];
-    const uint32_t ro[2] = {0, t->nr[g]};
-    int64_t c = 0;
+    int64_t c = t->lc[g];
     uint8_t st = 0;
+#ifdef FAKE_JRQ_CLOSED_FORM
+    for (uint32_t r = 0; r < t->nr[g]; ++r) {
+      const uint64_t cw = t->conf[g * JRQ_TABLE_MAX_RUNS + r];
+      const int64_t s = std::max(r == 0 ? t->pi[g] : t->start[g * JRQ_TABLE_MAX_RUNS + r], t->pi[g]);
+      const int64_t e = r + 1 < t->nr[g] ? t->start[g * JRQ_TABLE_MAX_RUNS + r + 1] - 1 : t->la[g];
+      const int64_t k = std::min({e, kth(m.data(), t->P, cw & 0xFFFFu, (cw >> 32) & 0xFFu),
+                                  kth(m.data(), t->P, (cw >> 16) & 0xFFFFu, (cw >> 40) & 0xFFu)});
+      if (k >= s && k > c) c = k;
+    }
+#else
+    const uint32_t ro[2] = {0, t->nr[g]};
     jo_quorum_epoch_replay(1, t->P, m.data(), &t->pi[g], &t->la[g], &t->lc[g],
                            &t->conf[g * JRQ_TABLE_MAX_RUNS], ro, &t->start[g * JRQ_TABLE_MAX_RUNS],
                            &t->conf[g * JRQ_TABLE_MAX_RUNS], 64, &c, &st);
+#endif
     if (status_out) status_out[g] = st;
     if (c > t->lc[g]) {
       changed_out[n++] = (static_cast<uint64_t>(c - t->pi[g] + 1) << 32) | g;

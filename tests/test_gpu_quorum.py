@@ -97,11 +97,14 @@ def test_pair_and_scalar_paths(engine, oracle, G):
     np.testing.assert_array_equal(st.cpu().numpy(), se)
 
 
-@pytest.mark.parametrize("cfg", ["C2", "C3"])
-def test_config_shapes_vs_replay(engine, oracle, cfg):
-    """C2 / C3 shaped groups (1k pending each, 1024-entry ack chunks as the Replicator sends,
-    RaftOptions.maxEntriesSize = 1024) replayed through real BallotBoxes."""
-    b = W.quorum_batch(cfg, groups=2000)
+@pytest.mark.parametrize("cfg,G", [("C2", None), ("C3", 2000)])
+def test_config_shapes_vs_replay(engine, oracle, cfg, G):
+    """C2 at its stated size (all 10k groups x 3 peers, configs[1]) and C3-shaped groups (1k
+    pending each, 1024-entry ack chunks as the Replicator sends, RaftOptions.maxEntriesSize =
+    1024) replayed through real BallotBoxes."""
+    b = W.quorum_batch(cfg, groups=G)
+    if G is None:
+        assert b["pending_index"].shape[0] == W.CONFIGS[cfg]["groups"] == 10_000
     c, s = _gpu(engine, b, runs=False)
     ce, se = _replay(oracle, b, runs=False, chunk=1024)
     np.testing.assert_array_equal(c, ce)
@@ -158,7 +161,8 @@ def _series_oracle(s, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,G,K", [("C2", 1000, 7), ("C3", 3000, 9), ("C2", 1, 1)])
+@pytest.mark.parametrize("cfg,G,K", [("C2", 1000, 7), ("C3", 3000, 9), ("C2", 1, 1),
+                                     ("C2", 10_000, 64)])
 def test_gpu_quorum_epochs_series_vs_oracle(engine, cfg, G, K):
     """K epochs in one launch == K sequential BallotBox replays with carried state."""
     import torch
