@@ -536,8 +536,7 @@ def leg_table(ctx, args, G, pair_ms):
     ctx.sync()
     work = Table(eng, G, P)
     from jraft_amd import _lib
-    changed = torch.empty(_lib.TABLE_SEGMENTS * work.segment_capacity(), dtype=torch.int64, device=dev)
-    n = torch.zeros(_lib.TABLE_SEGMENTS, dtype=torch.int32, device=dev)
+    changed, n = work.list_buffers(dev)
     steps = max(10, args.steps)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]

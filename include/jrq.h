@@ -203,7 +203,7 @@ int jrq_quorum_epochs_dev(jrq_engine *e, const jrq_group_batch *in_dev, uint32_t
 #define JRQ_TABLE_MAX_RUNS 4            /* conf runs per pending window (NodeImpl has <= 2) */
 #define JRQ_TABLE_MAX_GROUPS (1u << 27) /* groups per table (27-bit group ids in records) */
 #define JRQ_PI_FOLLOWS_LC INT64_MIN
-#define JRQ_TABLE_SEGMENTS 16           /* segments of an epoch's changed list (_dev) */
+#define JRQ_TABLE_SLICE 256             /* groups per slice of an epoch's changed list (_dev) */
 
 typedef struct jrq_table jrq_table;
 
@@ -264,14 +264,15 @@ int jrq_table_update_gather(jrq_table *t, uint32_t parts, const jrq_group_state 
  * particular order; status_out[g] (nullable) = jrq_group_status.
  * Host variant: changed_out[0 .. *n_changed) (capacity G); synchronises and copies back only
  * the listed entries.
- * _dev: the list comes in JRQ_TABLE_SEGMENTS segments (one atomic counter each, so that the
- * workgroups' reservations do not serialise on one address): segment s holds n_changed_dev[s]
- * entries at changed_out_dev + s * jrq_table_segment_capacity(t). */
-int jrq_table_epoch_dev(jrq_table *t, uint64_t *changed_out_dev,
-                        uint32_t n_changed_dev[JRQ_TABLE_SEGMENTS], uint8_t *status_out_dev);
+ * _dev: the list comes in jrq_table_slices(t) fixed slices, one per JRQ_TABLE_SLICE groups
+ * (no reservation, no atomics: each slice is written by the one wave that decides its groups):
+ * slice s lists n_changed_dev[s] of the groups [256 s, 256 s + 256) at changed_out_dev + 256 s
+ * (capacity JRQ_TABLE_SLICE * jrq_table_slices(t) words). */
+int jrq_table_epoch_dev(jrq_table *t, uint64_t *changed_out_dev, uint32_t *n_changed_dev,
+                        uint8_t *status_out_dev);
 int jrq_table_epoch(jrq_table *t, uint64_t *changed_out, uint32_t *n_changed,
                     uint8_t *status_out);
-uint32_t jrq_table_segment_capacity(const jrq_table *t);
+uint32_t jrq_table_slices(const jrq_table *t);  /* ceil(G / JRQ_TABLE_SLICE) */
 
 /* Copy the table's state to host arrays (each nullable): pendingIndex resolved (never
  * JRQ_PI_FOLLOWS_LC), last_appended, last_committed [G], match [num_peers][G]. */

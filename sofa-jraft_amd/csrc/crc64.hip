@@ -35,7 +35,12 @@
 #include "jrq_device.h"
 
 #ifndef JRQ_CRC_LOAD_AUX
-#define JRQ_CRC_LOAD_AUX 0  // cache-policy bits of the payload ring loads (2 = nt on gfx950)
+#define JRQ_CRC_LOAD_AUX 0  // cache-policy bits of the half-line ring loads (2 = nt on gfx950)
+#endif
+#ifndef JRQ_CRC_LINE_AUX
+// cache-policy bits of the full-line ring loads: every instruction reads whole 128-B lines, so
+// nothing else wants the line afterwards and `nt` streams it (DESIGN.md §4.2 "Cache policy")
+#define JRQ_CRC_LINE_AUX 2
 #endif
 
 
@@ -168,6 +173,51 @@ __device__ __forceinline__ void row_transpose(u32x4& a0, u32x4& a1, u32x4& a2, u
 __device__ __forceinline__ void transpose_ring(u32x4 (&v)[4]) {
   asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
   row_transpose(v[0], v[1], v[2], v[3]);
+}
+
+// ------------------------------------------------------- line transpose ---
+// Full-line shape: load q (0..7) of lane L = 8p + c reads 16-B piece p of the 128-B line of
+// owner lane c + 8q, so each instruction reads 8 owners x 128 B, whole lines (no line is
+// split across instructions; with `nt` loads a line read half by one instruction and half by
+// the next was evicted in between).  Loads 0..3 land in a[0..3], 4..7 in
+// b[0..3].  Three butterfly stages swap lane bit 5 / 4 / 3 with register bit 2 / 1 / 0, after
+// which lane o holds its own line: a = bytes 0..63, b = bytes 64..127.
+//   lane bit 5: v_permlane32_swap   (a[i] <-> b[i])
+//   lane bit 4: v_permlane16_swap   (x[0] <-> x[2], x[1] <-> x[3])
+//   lane bit 3: two DPP row_ror:8 moves with bank masks (x[0] <-> x[1], x[2] <-> x[3]): lanes
+//               with bit 3 clear take their partner's even register into their odd one, lanes
+//               with bit 3 set their partner's odd register into their even one.
+__device__ __forceinline__ void swap8(uint32_t& a, uint32_t& b) {
+  const uint32_t a0 = a, b0 = b;
+  b = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(b0), static_cast<int>(a0),
+                                                        0x128 /* row_ror:8 */, 0xF, 0x3, false));
+  a = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(a0), static_cast<int>(b0),
+                                                        0x128, 0xF, 0xC, false));
+}
+__device__ __forceinline__ void swap8v(u32x4& a, u32x4& b) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    uint32_t x = a[c], y = b[c];
+    swap8(x, y);
+    a[c] = x;
+    b[c] = y;
+  }
+}
+// Must run with the whole wave active.  The asm pin keeps the swaps below the loads issued
+// before them (the scheduler would otherwise hoist them and drain the ring with vmcnt(0)).
+__device__ __forceinline__ void transpose_line(u32x4 (&a)[4], u32x4 (&b)[4]) {
+  asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]),
+               "+v"(b[2]), "+v"(b[3]));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) swap32(a[i], b[i]);
+  swap16(a[0], a[2]);
+  swap16(a[1], a[3]);
+  swap16(b[0], b[2]);
+  swap16(b[1], b[3]);
+  swap8v(a[0], a[1]);
+  swap8v(a[2], a[3]);
+  swap8v(b[0], b[1]);
+  swap8v(b[2], b[3]);
 }
 
 // --------------------------------------------------------------- helpers ---
@@ -519,6 +569,8 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     // write-after-write made the compiler wait for the whole ring, vmcnt(0)).
     const uint32_t qa0 = qbase, qa1 = qbase + 16u * WS, qa2 = qbase + 32u * WS,
                    qa3 = qbase + 48u * WS;
+    // full-line shape (kRing4): load q reads 16-B piece L >> 3 of owner (L & 7) + 8q's line
+    const uint32_t lb = (L & 7u) * WS + 16u * ((L >> 3) & 7u);
     const uint64_t wptr_u = (static_cast<uint64_t>(whi) << 32) | wlo;
 #define JRQ_LOAD_HALF(H, hh)                                                             \
   do {                                                                                   \
@@ -537,11 +589,36 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
     H[3] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa3, 0, JRQ_CRC_LOAD_AUX);                         \
     asm volatile("" ::: "memory");                                                       \
   } while (0)
+#define JRQ_LOAD_LINE(HA, HB, ll)                                                        \
+  do {                                                                                   \
+    const uint32_t ho = __builtin_amdgcn_readfirstlane((ll) * 128u);                     \
+    const uint64_t hp = wptr_u + ho;                                                     \
+    const uint32_t hlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp));      \
+    const uint32_t hhi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp >> 32)); \
+    uint32_t hn;                                                                         \
+    asm("s_min_u32 %0, %1, %2\n\ts_sub_u32 %0, %2, %0" : "=&s"(hn) : "s"(ho), "s"(nr));   \
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(                 \
+        reinterpret_cast<uint8_t*>((static_cast<uint64_t>(hhi) << 32) | hlo),            \
+        static_cast<short>(0), static_cast<int>(hn), 0x00020000);                        \
+    HA[0] = __builtin_amdgcn_raw_buffer_load_b128(rh, lb, 0, JRQ_CRC_LINE_AUX);          \
+    HA[1] = __builtin_amdgcn_raw_buffer_load_b128(rh, lb + 8u * WS, 0, JRQ_CRC_LINE_AUX); \
+    HA[2] = __builtin_amdgcn_raw_buffer_load_b128(rh, lb + 16u * WS, 0, JRQ_CRC_LINE_AUX); \
+    HA[3] = __builtin_amdgcn_raw_buffer_load_b128(rh, lb + 24u * WS, 0, JRQ_CRC_LINE_AUX); \
+    HB[0] = __builtin_amdgcn_raw_buffer_load_b128(rh, lb + 32u * WS, 0, JRQ_CRC_LINE_AUX); \
+    HB[1] = __builtin_amdgcn_raw_buffer_load_b128(rh, lb + 40u * WS, 0, JRQ_CRC_LINE_AUX); \
+    HB[2] = __builtin_amdgcn_raw_buffer_load_b128(rh, lb + 48u * WS, 0, JRQ_CRC_LINE_AUX); \
+    HB[3] = __builtin_amdgcn_raw_buffer_load_b128(rh, lb + 56u * WS, 0, JRQ_CRC_LINE_AUX); \
+    asm volatile("" ::: "memory");                                                       \
+  } while (0)
     // the ring's first two half-rounds go out before the segment setup: the setup's dependent
     // lookups (entry search, boundary window) then overlap the payload fetch instead of
     // leaving HBM idle at the start of every chunk (short segments: C1, V2)
-    JRQ_LOAD_HALF(h0, 0u);
-    JRQ_LOAD_HALF(h1, 1u);
+    if constexpr (kRing4) {
+      JRQ_LOAD_LINE(h0, h1, 0u);
+    } else {
+      JRQ_LOAD_HALF(h0, 0u);
+      JRQ_LOAD_HALF(h1, 1u);
+    }
     if (j == 0) build_tables();
 
     // ---- segment setup ----
@@ -706,8 +783,8 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
       // 15-19 % of the lines were fetched twice (rocprofv3 TCC_EA0_RDREQ_128B, DESIGN.md
       // §4.2): the waves of an XCD walk segments 2^k bytes apart in step, so they contend for
       // the same L2 sets, and a line could be evicted between its two halves.
-      JRQ_LOAD_HALF(h2, last_half(2u));
-      JRQ_LOAD_HALF(h3, last_half(3u));
+      // (lines, not halves: last_half(2 l) / 2 is the clamped line)
+      JRQ_LOAD_LINE(h2, h3, last_half(2u) >> 1);
       for (uint32_t hh0 = 0; hh0 < halves; hh0 += 4) {
         const uint32_t hh = __builtin_amdgcn_readfirstlane(hh0);  // keep the counter in SGPRs
         if (a.prio_steps) {  // wave-uniform: lower this wave's priority as it gets ahead
@@ -721,18 +798,14 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
             else __builtin_amdgcn_s_setprio(0);
           }
         }
-        transpose_half(h0);
+        transpose_line(h0, h1);
         process(hh, h0);
-        transpose_half(h1);
         if (hh + 1 < halves) process(hh + 1, h1);  // wave-uniform
-        JRQ_LOAD_HALF(h0, last_half(hh + 4));
-        JRQ_LOAD_HALF(h1, last_half(hh + 5));
-        transpose_half(h2);
+        JRQ_LOAD_LINE(h0, h1, last_half(hh + 4) >> 1);
+        transpose_line(h2, h3);
         if (hh + 2 < halves) process(hh + 2, h2);
-        transpose_half(h3);
         if (hh + 3 < halves) process(hh + 3, h3);
-        JRQ_LOAD_HALF(h2, last_half(hh + 6));
-        JRQ_LOAD_HALF(h3, last_half(hh + 7));
+        JRQ_LOAD_LINE(h2, h3, last_half(hh + 6) >> 1);
       }
     } else {
       for (uint32_t hh0 = 0; hh0 < halves; hh0 += 3) {
@@ -760,6 +833,7 @@ __global__ __launch_bounds__(kBlock) void crc64_rounds_kernel(JrqCrcArgs a) {
       }
     }
 #undef JRQ_LOAD_HALF
+#undef JRQ_LOAD_LINE
   }
 }
 
@@ -877,8 +951,12 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   // load window end (read once: the loads' memory clobber would re-read it in the ring)
   const uint64_t total = kStarts ? a.gate[3] : static_cast<uint64_t>(n) * EL;
   const uint32_t WS = static_cast<uint32_t>(PS);  // lane-to-lane stride (64 * PS < 2^32)
-  const uint32_t qb = (L & 15u) * WS + 16u * ((L >> 4) & 3u);
-  uint32_t qa0 = qb, qa1 = qb + 16u * WS, qa2 = qb + 32u * WS, qa3 = qb + 48u * WS;
+  // full-line shape: load q reads 16-B piece L >> 3 of owner (L & 7) + 8q's line
+  // (transpose_line); qa[q] = that owner's offset + 16 (L >> 3)
+  const uint32_t qb = (L & 7u) * WS + 16u * ((L >> 3) & 7u);
+  uint32_t qa[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) qa[q] = qb + 8u * static_cast<uint32_t>(q) * WS;
   const uintptr_t pbase = reinterpret_cast<uintptr_t>(a.payload);
   // kStarts: the row's base (its first piece) and each owner's offset from it, through
   // __shfl (the load of lane 16q + c reads owner 16q + c's piece); a new row costs a load
@@ -895,20 +973,19 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     const uint32_t rb_hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ps >> 32));
     row_base = (static_cast<uint64_t>(rb_hi) << 32) | rb_lo;
     const uint32_t rel = static_cast<uint32_t>(ps - row_base);
-    const uint32_t c = L & 15u, ro = 16u * ((L >> 4) & 3u);
-    qa0 = __shfl(rel, static_cast<int>(c)) + ro;
-    qa1 = __shfl(rel, static_cast<int>(16u + c)) + ro;
-    qa2 = __shfl(rel, static_cast<int>(32u + c)) + ro;
-    qa3 = __shfl(rel, static_cast<int>(48u + c)) + ro;
+    const uint32_t c = L & 7u, ro = 16u * ((L >> 3) & 7u);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) qa[q] = __shfl(rel, static_cast<int>(c + 8u * q)) + ro;
   };
   if (kStarts) set_row(r0);
-  // load cursor (row, half of the entry) of the next half-round to issue, scalar; past the
-  // wave's last half its loads get an empty descriptor (zeros, no memory request: re-reading
-  // that half cost up to 3 % of the bytes when the line had left L2)
-  uint32_t crow = r0, chalf = 0, cur_live = 1u;
-  auto load_half = [&](u32x4 (&H)[4]) {
-    const uint64_t o = kStarts ? row_base + static_cast<uint64_t>(chalf) * 64u
-                               : static_cast<uint64_t>(crow) * 64u * PS + static_cast<uint64_t>(chalf) * 64u;
+  // load cursor (row, line of the piece) of the next 128-B line to issue, scalar; past the
+  // wave's last line its loads get an empty descriptor (zeros, no memory request: re-reading
+  // that line cost up to 3 % of the bytes when it had left L2)
+  uint32_t crow = r0, cline = 0, cur_live = 1u;
+  const uint32_t LE = HE >> 1;  // lines per piece
+  auto load_line = [&](u32x4 (&HA)[4], u32x4 (&HB)[4]) {
+    const uint64_t o = kStarts ? row_base + static_cast<uint64_t>(cline) * 128u
+                               : static_cast<uint64_t>(crow) * 64u * PS + static_cast<uint64_t>(cline) * 128u;
     const uint64_t hp = pbase + o;
     const uint32_t hlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp));
     const uint32_t hhi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(hp >> 32));
@@ -920,26 +997,24 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<uint8_t*>((static_cast<uint64_t>(hhi) << 32) | hlo),
         static_cast<short>(0), static_cast<int>(hn), 0x00020000);
-    H[0] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa0, 0, JRQ_CRC_LOAD_AUX);
-    H[1] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa1, 0, JRQ_CRC_LOAD_AUX);
-    H[2] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa2, 0, JRQ_CRC_LOAD_AUX);
-    H[3] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa3, 0, JRQ_CRC_LOAD_AUX);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) HA[q] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa[q], 0, JRQ_CRC_LINE_AUX);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) HB[q] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa[4 + q], 0, JRQ_CRC_LINE_AUX);
     asm volatile("" ::: "memory");
-    if (chalf + 1 < HE) {
-      ++chalf;
+    if (cline + 1 < LE) {
+      ++cline;
     } else if (crow + 1 < r1) {
       ++crow;
-      chalf = 0;
+      cline = 0;
       if (kStarts) set_row(crow);
     } else {
       cur_live = 0u;
     }
   };
   u32x4 h0[4], h1[4], h2[4], h3[4];
-  load_half(h0);
-  load_half(h1);
-  load_half(h2);
-  load_half(h3);
+  load_line(h0, h1);
+  load_line(h2, h3);
   build_tables();
   // LogEntry fields: absent arrays read word 0 of the slice table (R0[0] = 0), masked below
   const uint64_t* const z = a.slice;
@@ -967,24 +1042,18 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     }
     RState s{0u, 0u};
     uint32_t q = 0;
-    // the two halves of a 128-B line go out back to back (slots h0 + h1, h2 + h3): the
-    // line's second half then meets its first half's fill in L2.  Issued one step apart,
-    // 15 % of the lines were fetched twice (rocprofv3 TCC_EA0_RDREQ_128B):
-    // the waves of an XCD walk rows 2^k bytes apart in step, so they contend for the same
-    // L2 sets and a line could be evicted between its two halves.
+    // a ring of two 128-B lines per lane (slots h0 + h1, h2 + h3), each line read whole by
+    // its load instructions (8 owners x 128 B each): with half-lines per instruction 15 % of
+    // the lines were fetched twice, and `nt` loads could not be used
     do {
-      transpose_ring(h0);
+      transpose_line(h0, h1);
       tb.step64(s, h0, lds);
-      transpose_ring(h1);
       tb.step64(s, h1, lds);
-      load_half(h0);
-      load_half(h1);
-      transpose_ring(h2);
+      load_line(h0, h1);
+      transpose_line(h2, h3);
       tb.step64(s, h2, lds);
-      transpose_ring(h3);
       tb.step64(s, h3, lds);
-      load_half(h2);
-      load_half(h3);
+      load_line(h2, h3);
     } while (++q < turns);
     uint64_t c = crc_value(s);
     if (kStarts) {  // hashed [ps - b, ps - b + PS): drop the b bytes before, add the b missed

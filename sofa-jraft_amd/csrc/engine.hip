@@ -37,11 +37,13 @@ extern "C" hipError_t jrq_launch_table_update(const JrqTableArgs* a, const JrqGr
                                               uint32_t n_states, const uint64_t* recs,
                                               uint32_t n_recs, hipStream_t stream);
 extern "C" hipError_t jrq_launch_table_epoch(const JrqTableArgs* a, hipStream_t stream);
-extern "C" uint32_t jrq_table_seg_cap(uint32_t G);
-static_assert(JRQ_TABLE_SEGMENTS == jrq::kTableSegments, "table list segments");
+extern "C" hipError_t jrq_launch_table_list_gather(const uint64_t* changed, const uint32_t* n,
+                                                   uint32_t slices, uint32_t* off, uint32_t* total,
+                                                   uint64_t* out, hipStream_t stream);
 
 static_assert(sizeof(jrq_group_state) == sizeof(JrqGroupState), "jrq_group_state layout");
 static_assert(JRQ_TABLE_MAX_RUNS == jrq::kTableMaxRuns, "table runs");
+static_assert(JRQ_TABLE_SLICE == jrq::kTableSlice, "table list slices");
 
 namespace {
 
@@ -1285,8 +1287,9 @@ struct jrq_table {
   void* mem = nullptr;        // every device array of the table, one allocation
   JrqTableArgs a{};           // device pointers (changed / n_changed / status set per epoch)
   DevBuf st_stage, rec_stage, changed_stage;  // staging of the host variants
-  uint32_t* n_dev = nullptr;  // device count word of the host-variant epoch
-  uint32_t* n_host = nullptr; // pinned
+  uint32_t* n_dev = nullptr;  // host-variant epoch: slice counts [slices], offsets [slices], total
+  uint32_t* n_host = nullptr; // pinned: the total
+  uint32_t slices = 0;        // JRQ_TABLE_SLICE-group slices of the changed list
   size_t state_bytes = 0;     // the rows at the start of mem (jrq_table_copy)
 };
 
@@ -1330,17 +1333,19 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   t->e = e;
   const uint64_t ld = (static_cast<uint64_t>(G) + 63) & ~63ull;  // pairs + 512-B rows
   // rows (the state jrq_table_copy copies): match[P], pi, la, lc, conf, xstart[3], xconf[3],
-  // the flagged-entry slots flag_ent[waves][128][8] + flag_wcnt[waves] (u32); then the
-  // control words: ctr[16], invalid
-  const uint64_t blocks = (G + jrq::kTableBlockGroups - 1) / jrq::kTableBlockGroups;
-  const uint64_t waves = blocks * (jrq::kTableBlockGroups / 128);
+  // the flagged-entry slots flag_ent[waves][256][8] + flag_wcnt[waves] (u32); then the
+  // control word `invalid`
+  // (one 256-group range per epoch wave, rounded up to whole workgroups: every wave of the
+  // grid reads its slots)
+  const uint64_t ranges = (G + jrq::kTableSlice - 1) / jrq::kTableSlice;
+  const uint64_t waves = (ranges + jrq::kTableBlockWaves - 1) / jrq::kTableBlockWaves * jrq::kTableBlockWaves;
   const uint64_t flag_words = waves * jrq::kFlagSlots * 8 + (waves + 1) / 2;
   const uint64_t words = ld * (P + 4 + 2 * (jrq::kTableMaxRuns - 1)) + flag_words;
-  const size_t bytes = words * 8 + 8 * jrq::kTableSegments + 64;
+  const size_t bytes = words * 8 + 64;
+  t->slices = (G + JRQ_TABLE_SLICE - 1) / JRQ_TABLE_SLICE;
   if (hipMalloc(&t->mem, bytes) != hipSuccess || hipMemset(t->mem, 0, bytes) != hipSuccess ||
-      hipMalloc(&t->n_dev, 4 * jrq::kTableSegments) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&t->n_host), 4 * (jrq::kTableSegments + 1),
-                    hipHostMallocDefault) != hipSuccess) {
+      hipMalloc(&t->n_dev, 4 * (2 * static_cast<size_t>(t->slices) + 1)) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&t->n_host), 64, hipHostMallocDefault) != hipSuccess) {
     fail(e, JRQ_E_NOMEM, "table: allocation of %zu bytes failed", bytes);
     jrq_table_destroy(t);
     set(JRQ_E_NOMEM);
@@ -1357,10 +1362,8 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   a.xconf = reinterpret_cast<uint64_t*>(a.xstart + ld * (jrq::kTableMaxRuns - 1));
   a.flag_ent = reinterpret_cast<uint64_t*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
   a.flag_wcnt = reinterpret_cast<uint32_t*>(a.flag_ent + waves * jrq::kFlagSlots * 8);
-  a.ctr = reinterpret_cast<unsigned long long*>(w + words);
-  a.invalid = reinterpret_cast<uint32_t*>(a.ctr + jrq::kTableSegments);
+  a.invalid = reinterpret_cast<uint32_t*>(w + words);
   t->state_bytes = words * 8;
-  a.seg_cap = jrq_table_seg_cap(G);
   a.ld = ld;
   a.G = G;
   a.P = P;
@@ -1467,32 +1470,33 @@ int jrq_table_epoch(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, ui
   if (!changed_out || !n_changed) return fail(e, JRQ_E_INVALID, "null changed output");
   DeviceGuard guard(e->device);
   const uint32_t G = t->a.G;
-  const size_t cap = static_cast<size_t>(t->a.seg_cap) * JRQ_TABLE_SEGMENTS;
+  const size_t cap = static_cast<size_t>(t->slices) * JRQ_TABLE_SLICE;
   int rc;
-  void *dch = nullptr, *dst = nullptr;
-  if ((rc = stage_buf(e, t->changed_stage, cap * 8 + G, &dch))) return rc;
-  if (status_out) dst = static_cast<uint8_t*>(dch) + cap * 8;
-  if ((rc = jrq_table_epoch_dev(t, static_cast<uint64_t*>(dch), t->n_dev, static_cast<uint8_t*>(dst))))
-    return rc;
-  JRQ_HIP(e, hipMemcpyAsync(t->n_host, t->n_dev, 4 * JRQ_TABLE_SEGMENTS, hipMemcpyDeviceToHost, e->stream));
+  void* dch = nullptr;
+  // staging: the slices, the gathered list, the status bytes
+  if ((rc = stage_buf(e, t->changed_stage, 2 * cap * 8 + G, &dch))) return rc;
+  uint64_t* slices = static_cast<uint64_t*>(dch);
+  uint64_t* list = slices + cap;
+  uint8_t* dst = status_out ? reinterpret_cast<uint8_t*>(list + cap) : nullptr;
+  if ((rc = jrq_table_epoch_dev(t, slices, t->n_dev, dst))) return rc;
+  // the slices back to back on the device, then only the entries cross PCIe
+  uint32_t* off = t->n_dev + t->slices;
+  uint32_t* total = off + t->slices;
+  JRQ_HIP(e, jrq_launch_table_list_gather(slices, t->n_dev, t->slices, off, total, list, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(t->n_host, total, 4, hipMemcpyDeviceToHost, e->stream));
   if (status_out) JRQ_HIP(e, hipMemcpyAsync(status_out, dst, G, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
-  // the segments back to back into the caller's buffer: only the entries cross PCIe
-  uint32_t n = 0;
-  for (uint32_t s = 0; s < JRQ_TABLE_SEGMENTS; ++s) {
-    const uint32_t k = t->n_host[s];
-    if (k > t->a.seg_cap || n + k > G) return fail(e, JRQ_E_STATE, "table list segment %u overflow", s);
-    if (k)
-      JRQ_HIP(e, hipMemcpyAsync(changed_out + n, static_cast<uint64_t*>(dch) + s * static_cast<size_t>(t->a.seg_cap),
-                                static_cast<size_t>(k) * 8, hipMemcpyDeviceToHost, e->stream));
-    n += k;
+  const uint32_t n = t->n_host[0];
+  if (n > G) return fail(e, JRQ_E_STATE, "table list overflow (%u entries)", n);
+  if (n) {
+    JRQ_HIP(e, hipMemcpyAsync(changed_out, list, static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, e->stream));
+    JRQ_HIP(e, hipStreamSynchronize(e->stream));
   }
   *n_changed = n;
-  if (n) JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
 
-uint32_t jrq_table_segment_capacity(const jrq_table* t) { return t ? t->a.seg_cap : 0; }
+uint32_t jrq_table_slices(const jrq_table* t) { return t ? t->slices : 0; }
 
 int jrq_table_read(jrq_table* t, int64_t* pending_index, int64_t* last_appended,
                    int64_t* last_committed, int64_t* match) {

@@ -251,13 +251,10 @@ struct JrqQuorumArgs {
 // Resident group table (table.hip; include/jrq.h jrq_table).
 namespace jrq {
 constexpr int kTableMaxRuns = 4;                   // JRQ_TABLE_MAX_RUNS
-constexpr uint32_t kTableSegments = 16;            // JRQ_TABLE_SEGMENTS
-#ifndef JRQ_TABLE_BLOCK_GROUPS
-#define JRQ_TABLE_BLOCK_GROUPS 2048
-#endif
-constexpr uint32_t kTableBlockGroups = JRQ_TABLE_BLOCK_GROUPS;  // groups per epoch workgroup
+constexpr uint32_t kTableSlice = 256;              // JRQ_TABLE_SLICE: groups per epoch wave
+constexpr uint32_t kTableBlockWaves = 4;           // waves per epoch / flags workgroup
 constexpr int64_t kPiFollowsLc = INT64_MIN;        // JRQ_PI_FOLLOWS_LC
-constexpr uint32_t kFlagSlots = 128;               // flagged-entry slots per 128-group wave
+constexpr uint32_t kFlagSlots = 256;               // flagged-entry slots per 256-group epoch wave
 }  // namespace jrq
 struct JrqTableArgs {
   int64_t* match;        // [P][ld]
@@ -270,14 +267,11 @@ struct JrqTableArgs {
   uint64_t ld;
   uint32_t G;            // groups (ld >= G rounded up to pairs; pad groups are not leaders)
   uint32_t P;
-  unsigned long long* ctr;  // [kTableSegments] compaction counters {blocks done << 32 | entries},
-                            // zero between launches
   uint32_t* invalid;     // records / headers skipped as invalid since the last jrq_table_check
-  uint64_t* changed;     // [kTableSegments][seg_cap] out
-  uint32_t* n_changed;   // [kTableSegments] out
-  uint32_t seg_cap;      // entries per list segment
+  uint64_t* changed;     // [slices][JRQ_TABLE_SLICE] out: wave w's entries at changed[128 w ..]
+  uint32_t* n_changed;   // [slices] out
   uint8_t* status;       // [G] out, nullable
-  uint64_t* flag_ent;    // [waves][kFlagSlots][8] per 128-group epoch wave: its groups flagged
+  uint64_t* flag_ent;    // [waves][kFlagSlots][8] per 256-group epoch wave: its groups flagged
                          // JRQ_CONF_RUNS as 64-B entries {group, run starts 1-3, conf words 0-3}
   uint32_t* flag_wcnt;   // [waves] how many
 };

@@ -139,6 +139,23 @@ __device__ __forceinline__ void rel_map(int64_t pi, int64_t la, const int64_t (&
   }
 }
 
+// The single conf word's bound in the relative domain: the largest r in [0, W] every entry up
+// to which is granted (0: none), and the status bits (out-of-range acks, empty conf).  The
+// commit is pi - 1 + r when pi != 0, r >= 1 and that exceeds lastCommitted.
+template <int P>
+__device__ __forceinline__ uint32_t rel_cand(uint64_t cw, const RelGroup<P>& g, uint8_t& st) {
+  st = g.st;
+  if ((cw & 0xFFFFu) == 0 && g.W != 0) st |= kStEmptyConf;
+  const uint32_t nmask = static_cast<uint32_t>(cw & 0xFFFFu);
+  const uint32_t omask = static_cast<uint32_t>((cw >> 16) & 0xFFFFu);
+  const uint32_t nq = static_cast<uint32_t>((cw >> 32) & 0xFFu);
+  const uint32_t oq = static_cast<uint32_t>((cw >> 40) & 0xFFu);
+  const uint32_t kn = nq == 0 ? g.W : kth_largest_rel<P>(g.r, nmask, nq);
+  const uint32_t ko = oq == 0 ? g.W : kth_largest_rel<P>(g.r, omask, oq);
+  const uint32_t cand = kn < ko ? kn : ko;
+  return cand < g.W ? cand : g.W;
+}
+
 template <int P>
 __device__ __forceinline__ void rel_decide(int64_t pi, int64_t lc, uint64_t cw, const RelGroup<P>& g,
                                            int64_t& out, uint8_t& st_out) {

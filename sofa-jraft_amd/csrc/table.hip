@@ -12,7 +12,8 @@
 //   table_recs_kernel    8-B update records: match of one peer slot / queue size of one group
 //   table_epoch_kernel   one epoch over every group, in place; a commit writes lastCommitted
 //                        (pendingIndex becomes JRQ_PI_FOLLOWS_LC once), and the group is
-//                        appended to a compacted list with one 64-bit atomic per workgroup.
+//                        listed in its wave's fixed slice of the changed list.
+//   table_list_*         host variant only: the slices gathered back to back.
 // HBM per group per epoch: reads match 8P + pendingIndex, lastAppended, lastCommitted, conf
 // 32 B; writes 8 B lastCommitted + 8 B list entry per committing group.
 #include "quorum_core.h"
@@ -45,162 +46,159 @@ __device__ __forceinline__ void table_commit_one(const JrqTableArgs& t, uint32_t
   if (pr != kPiFollowsLc) t.pi[g] = kPiFollowsLc;
 }
 
-// 1024-thread workgroups of 2048 groups (63 VGPRs: 2 workgroups per CU resident).  The
-// compacted list is cut into kTableSegments segments, workgroup b appending to segment
-// b % kTableSegments: same-address atomics serialise (~14 ns each, tools/table_probe.hip: one
-// counter for 512 workgroups cost 7 us of a 25 us epoch), so each counter sees 1/16 of them,
-// and the last arriver of each segment publishes its count -- no global arrival counter.
-constexpr uint32_t kTableBlock = kTableBlockGroups / 2;
+// The epoch's changed list comes in fixed slices, one per 256-group wave range: wave w (groups
+// [256 w, 256 w + 256)) writes its entries at changed[256 w ..] and their count at
+// n_changed[w].  No reservation: round 3 staged the entries in LDS and reserved each
+// workgroup's share with one 64-bit atomic on 16 segment counters, whose round trip at the end
+// of every workgroup (plus the barrier in front of it) cost ~1.5 us of a 21 us epoch
+// (round 3's tools/table_probe.hip).
+// Shape: 256-thread workgroups, two group pairs per lane -- pair A = groups (256 w + 2 l,
+// +1), pair B = pair A + 128, each stream read with 16-B loads (1 KiB per wave instruction),
+// every load of both pairs issued before the first decision.  At the 32-bit decision's ~75
+// VGPRs one pair per lane fits 6 waves per SIMD: a 1M-group epoch (8192 waves of 128 groups)
+// then needs 1.33 rounds of the chip's 6144 wave slots; two pairs per lane at <= 128 VGPRs
+// fit 4 waves per SIMD, 4096 waves of 256 groups: one round.
+constexpr uint32_t kTableEpochBlock = 64 * kTableBlockWaves;
 
-// The run walk of one flagged group, run r of it on lane r of an aligned lane quad (the table
-// holds at most kTableMaxRuns = 4 runs): each lane loads the group (the quad's loads of it
-// coalesce) and its run's start, next start and conf word, all in one batch; the quad then
-// max-reduces the runs' candidates.  Returns the group's candidate (kI64Min: none) and status.
-template <int P>
-__device__ __forceinline__ int64_t table_run_lane(const JrqTableArgs& t, uint32_t h, uint32_t r,
-                                                  int64_t& pr, int64_t& lc, int64_t& pi,
-                                                  uint8_t& st) {
-  static_assert(kTableMaxRuns == 4, "one run per lane of a quad");
-  pr = t.pi[h];
-  lc = t.lc[h];
-  const int64_t la = t.la[h];
-  const size_t o = static_cast<size_t>(r) * t.ld + h;  // run r's slot is r - 1; next run's is r
-  const uint64_t cw = r == 0 ? (t.conf[h] & ~kConfRuns) : t.xconf[o - t.ld];
-  const int64_t rs = r == 0 ? kI64Min : t.xstart[o - t.ld];
-  const int64_t nx = r + 1 < kTableMaxRuns ? t.xstart[o] : kI64Max;
-  int64_t m[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) m[p] = t.match[static_cast<size_t>(p) * t.ld + h];
-  pi = pr == kPiFollowsLc ? lc + 1 : pr;
-  if (pi == 0) {
-    st = kStNotLeader;
-    return kI64Min;
-  }
-  st = mask_out_of_range<P>(m, la);
-  const int64_t s = rs > pi ? rs : pi;
-  const int64_t e = nx == kI64Max ? la : nx - 1;
-  return run_candidate<P>(m, cw, s, e < la ? e : la, st);
-}
-
-// One epoch over every group of the table.  1024-thread workgroups of 2048 groups (two per
-// lane, 16-B loads), 2 resident per CU.
+// One epoch over every group of the table, in place.  The single-conf decision runs in 32-bit
+// arithmetic relative to pendingIndex (rel_map / rel_cand, the pair kernel's); groups outside
+// rel_domain (never a real group) are decided again with 64-bit arithmetic in a wave-uniform
+// pass at the end.
 // A group with a conf change inside its pending window (JRQ_CONF_RUNS) is skipped by the
 // single-conf decision and walked by its own wave afterwards: its dynamic state (pendingIndex,
 // lastCommitted, lastAppended, match) is what its owner lane loaded, left in the wave's slice of
 // LDS (the first 16 flagged groups of a wave; a wave-local hand-off, no barrier), and its runs
 // come from the wave's flagged-entry slots (table_flags_kernel writes them with every header
-// update: only headers change runs), spread over a lane quad by shuffles, one conf run per lane
-// (the table holds at most 4).  The wave copies its first four entries to LDS beside its
-// single-conf loads and counts its flagged groups by ballot, and it walks them before issuing
-// any store, so a flagged group costs no dependent round trip to memory, no wait for the wave's
-// stores and no workgroup barrier (round 2 deferred flagged groups to an LDS list behind a
-// barrier and reloaded them: +25 % on C3 with 1 % flagged, tools/flag_probe.hip; round 3's
-// first walk came after the stores and read entries through a generic pointer, and every flat
-// load drained the wave's stores).  Beyond 4 flagged groups in one wave the walk reads the
-// further entries from memory, beyond 16 it reloads the group too.
-// The one barrier left is the compaction's: list entries are staged per wave in LDS, and one
-// 64-bit atomic per workgroup ({done << 32 | entries}) on its segment's counter (workgroup b
-// -> segment b % kTableSegments: same-address atomics serialise, ~14 ns each,
-// tools/table_probe.hip) reserves its slice; the last workgroup of a segment publishes the
-// segment's count and re-zeroes the counter.
+// update: only headers change runs), eight lanes per group (one conf run per lane pair, the
+// pair splitting the run's new-conf and old-conf q-th largest).  The wave copies its first four
+// entries to LDS beside its single-conf loads and counts its flagged groups by ballot.  Beyond 4
+// flagged groups in one wave the walk reads the further entries from memory, beyond 16 it
+// reloads the group.  No workgroup barrier, no atomics: each wave writes its own list slice and
+// count.
 template <int P>
-__global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
-  constexpr uint32_t kWaves = kTableBlock / 64;
+__global__ __launch_bounds__(kTableEpochBlock) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
+  constexpr uint32_t kWaves = kTableEpochBlock / 64;
   constexpr uint32_t kHand = 16;  // flagged groups per wave handed over through LDS
   constexpr uint32_t kEntLds = 4; // flagged-entry slots per wave copied to LDS up front
-  __shared__ uint32_t wave_cnt[kWaves];
-  __shared__ uint64_t staged[kWaves][128];
   __shared__ int64_t hand[kWaves][kHand][P + 3];  // {pendingIndex word, lc, la, match[P]}
   __shared__ __attribute__((aligned(16))) int64_t ent4[kWaves][kEntLds][8];  // entries 0-3
-  __shared__ uint32_t blk_base;
-  const uint32_t pairs = (t.G + 1) >> 1;
-  const uint32_t tt = blockIdx.x * kTableBlock + threadIdx.x;
-  const uint32_t g = tt << 1;
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
-  // The wave's first four flagged-entry slots go straight to its LDS slice (an LDS-DMA load,
-  // 256 B per wave, ~1 % of the epoch's bytes; no registers held across the single-conf path),
-  // whatever the wave's count: the count is the wave's own ballot of its flagged groups (the
-  // flags kernel's count of the same 128 groups).  Loading the count and branching on it here
-  // put a full memory round trip in front of every wave's single-conf loads.
+  // wave wid holds groups [256 wid, 256 wid + 256): its flagged-entry slots, list slice, count
   const uint32_t wid = blockIdx.x * kWaves + w;
+  const uint32_t gA = wid * kTableSlice + 2u * lane;  // pair A = (gA, gA + 1), B = A + 128
+  uint64_t* const slice = t.changed + static_cast<size_t>(wid) * kTableSlice;
+  // The wave's first four flagged-entry slots go straight to its LDS slice (an LDS-DMA load,
+  // 256 B per wave; no registers held across the single-conf path), whatever the wave's count:
+  // the count is the wave's own ballot of its flagged groups (the flags kernel's count of the
+  // same 256 groups).  Loading the count and branching on it here put a full memory round trip
+  // in front of every wave's single-conf loads.
   const int64_t* const ent = reinterpret_cast<const int64_t*>(t.flag_ent) + static_cast<size_t>(wid) * kFlagSlots * 8;
   if (lane < 4 * kEntLds)  // lane l: bytes 16 l .. 16 l + 15 of entries 0-3 (64 B each)
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ent + lane * 2), &ent4[w][0][0], 16, 0, 0);
-  bool c0 = false, c1 = false, f0 = false, f1 = false, w0 = false, w1 = false;
-  int64_t o0 = 0, o1 = 0;
-  uint32_t s01 = 0;
-  if (tt < pairs) {
-    const uint32_t go = g * 8u;  // (g < 2^27)
-    const i64x2 pr = tld2o(t.pi, go);
-    const i64x2 lc = tld2o(t.lc, go);
-    const i64x2 la = tld2o(t.la, go);
-    const i64x2 cw = tld2o(reinterpret_cast<const int64_t*>(t.conf), go);
-    i64x2 mv[P];
+  // per group k = 0..3 (A.x, A.y, B.x, B.y): live (inside the table), flagged, committing,
+  // outside rel_domain; commit value, delta, status
+  bool live[2], f[4], c[4], x[4], wpi[4];
+  int64_t o[4];
+  uint32_t d[4], st4 = 0;
+  {
+    i64x2 pr[2], lc[2], la[2], cw[2], mv[2][P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) mv[p] = tld2o(t.match + static_cast<size_t>(p) * t.ld, go);
-    const int64_t pi0 = pr.x == kPiFollowsLc ? lc.x + 1 : pr.x;
-    const int64_t pi1 = pr.y == kPiFollowsLc ? lc.y + 1 : pr.y;
-    f0 = static_cast<uint64_t>(cw.x) >> 63;
-    f1 = static_cast<uint64_t>(cw.y) >> 63;
-    int64_t m0[P], m1[P];
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t g = gA + 128u * h;
+      live[h] = g < t.G;
+      const uint32_t go = (live[h] ? g : 0u) * 8u;  // (g < 2^27)
+      pr[h] = tld2o(t.pi, go);
+      lc[h] = tld2o(t.lc, go);
+      la[h] = tld2o(t.la, go);
+      cw[h] = tld2o(reinterpret_cast<const int64_t*>(t.conf), go);
 #pragma unroll
-    for (int p = 0; p < P; ++p) {
-      m0[p] = mv[p].x;
-      m1[p] = mv[p].y;
+      for (int p = 0; p < P; ++p) mv[h][p] = tld2o(t.match + static_cast<size_t>(p) * t.ld, go);
     }
-    // a flagged group's state -> the wave's hand-off slot of its rank (the flags kernel's
-    // entry order: the first groups of the pairs, then the second ones)
-    const uint64_t bf0 = __ballot(f0), bf1 = __ballot(f1);
-    const uint32_t k0 = __popcll(bf0 & below), k1 = __popcll(bf0) + __popcll(bf1 & below);
-    if (f0 && k0 < kHand) {
-      int64_t* hs = hand[w][k0];
-      hs[0] = pr.x;
-      hs[1] = lc.x;
-      hs[2] = la.x;
+    uint32_t kbase = 0;  // hand-off ranks: A.x, A.y, B.x, B.y groups in the flags kernel's order
 #pragma unroll
-      for (int p = 0; p < P; ++p) hs[3 + p] = m0[p];
-    }
-    if (f1 && k1 < kHand) {
-      int64_t* hs = hand[w][k1];
-      hs[0] = pr.y;
-      hs[1] = lc.y;
-      hs[2] = la.y;
+    for (int k = 0; k < 4; ++k) {
+      const int h = k >> 1;
+      const bool y = k & 1;
+      const uint32_t g = gA + 128u * h + (y ? 1u : 0u);
+      const int64_t prk = y ? pr[h].y : pr[h].x, lck = y ? lc[h].y : lc[h].x;
+      const int64_t lak = y ? la[h].y : la[h].x;
+      const uint64_t cwk = static_cast<uint64_t>(y ? cw[h].y : cw[h].x);
+      const bool in = live[h] && g < t.G;
+      f[k] = in && (cwk >> 63);
+      const uint64_t bf = __ballot(f[k]);
+      const uint32_t rk = kbase + __popcll(bf & below);
+      kbase += __popcll(bf);
+      int64_t m[P];
 #pragma unroll
-      for (int p = 0; p < P; ++p) hs[3 + p] = m1[p];
+      for (int p = 0; p < P; ++p) m[p] = y ? mv[h][p].y : mv[h][p].x;
+      if (f[k] && rk < kHand) {  // a flagged group's state -> the wave's hand-off slot
+        int64_t* hs = hand[w][rk];
+        hs[0] = prk;
+        hs[1] = lck;
+        hs[2] = lak;
+#pragma unroll
+        for (int p = 0; p < P; ++p) hs[3 + p] = m[p];
+      }
+      const int64_t pi = prk == kPiFollowsLc ? lck + 1 : prk;
+      RelGroup<P> rg;
+      rel_map<P>(pi, lak, m, rg);
+      uint8_t s;
+      const uint32_t r = rel_cand<P>(cwk, rg, s);
+      s = pi == 0 ? kStNotLeader : s;
+      x[k] = in && !f[k] && !rel_domain(pi, lak);
+      o[k] = pi - 1 + static_cast<int64_t>(r);
+      // a flagged group is decided by the walk (its single-conf result here is discarded)
+      c[k] = in && !f[k] && !x[k] && pi != 0 && r >= 1u && o[k] > lck;
+      d[k] = r;
+      // pendingIndex = lastCommittedIndex + 1 from now on (BallotBox.java:131-132): one store
+      // per group and leadership, the steady state writes lastCommitted only
+      wpi[k] = prk != kPiFollowsLc;
+      st4 |= static_cast<uint32_t>(s) << (8 * k);
     }
-    uint8_t s0, s1;
-    // (the 64-bit decision: the 32-bit one of the pair kernel, decide_single_rel, took this
-    // kernel past its 64 VGPRs -- 10 spills at P = 5)
-    decide_single<P>(pi0, la.x, lc.x, static_cast<uint64_t>(cw.x), m0, o0, s0);
-    decide_single<P>(pi1, la.y, lc.y, static_cast<uint64_t>(cw.y), m1, o1, s1);
-    // a flagged group is decided by the walk (its single-conf result here is discarded)
-    c0 = !f0 && o0 > lc.x;  // decide_single returns lastCommitted unless a commit happened
-    c1 = !f1 && o1 > lc.y;
-    // pendingIndex = lastCommittedIndex + 1 from now on (BallotBox.java:131-132): one store per
-    // group and leadership, the steady state writes lastCommitted only
-    w0 = pr.x != kPiFollowsLc;
-    w1 = pr.y != kPiFollowsLc;
-    s01 = s0 | (static_cast<uint32_t>(s1) << 8);
-    // list entries -> the wave's slice of LDS (ballot prefixes, no atomics)
-    const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
-    if (c0) staged[w][__popcll(b0 & below)] = (static_cast<uint64_t>(o0 - pi0 + 1) << 32) | g;
-    if (c1) staged[w][__popcll(b0) + __popcll(b1 & below)] = (static_cast<uint64_t>(o1 - pi1 + 1) << 32) | (g + 1);
   }
-  uint32_t cnt = __popcll(__ballot(c0)) + __popcll(__ballot(c1));
-  // The walk, before any of the wave's stores: its reads (LDS, and the entries past the first
-  // four from memory) then wait for nothing but themselves.  With the single-conf stores issued
-  // first, every wait of the walk (vmcnt counts stores too) drained the wave's stores.
-  // Flagged group i of the wave on quad i % 16, one conf run per lane.
+  // the single-conf results and their list entries (ballot ranks: one contiguous run per store)
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t g = gA + 128u * h;
+    const bool ca = c[2 * h], cb = c[2 * h + 1];
+    if (ca && cb) {
+      i64x2 v;
+      v.x = o[2 * h];
+      v.y = o[2 * h + 1];
+      __builtin_nontemporal_store(v, reinterpret_cast<i64x2*>(t.lc + g));
+    } else {
+      if (ca) t.lc[g] = o[2 * h];
+      if (cb) t.lc[g + 1] = o[2 * h + 1];
+    }
+    if (ca && wpi[2 * h]) t.pi[g] = kPiFollowsLc;
+    if (cb && wpi[2 * h + 1]) t.pi[g + 1] = kPiFollowsLc;
+    const uint64_t ba = __ballot(ca), bb = __ballot(cb);
+    if (ca) slice[cnt + __popcll(ba & below)] = (static_cast<uint64_t>(d[2 * h]) << 32) | g;
+    if (cb) slice[cnt + __popcll(ba) + __popcll(bb & below)] = (static_cast<uint64_t>(d[2 * h + 1]) << 32) | (g + 1);
+    cnt += __popcll(ba) + __popcll(bb);
+    if (t.status && live[h]) {  // a flagged (or 64-bit) group's status is written by its own pass
+      const uint32_t s2 = (st4 >> (16 * h)) & 0xFFFFu;
+      const bool ka = !f[2 * h] && !x[2 * h], kb = !f[2 * h + 1] && !x[2 * h + 1] && g + 1 < t.G;
+      if (ka && kb)
+        __builtin_nontemporal_store(static_cast<uint16_t>(s2), reinterpret_cast<uint16_t*>(t.status + g));
+      else {
+        if (ka) t.status[g] = static_cast<uint8_t>(s2);
+        if (kb) t.status[g + 1] = static_cast<uint8_t>(s2 >> 8);
+      }
+    }
+  }
+  // The walk.  Its reads are LDS (the hand-off slots and entries 0-3) except in waves with
+  // more than 4 / 16 flagged groups.
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the hand-off slots: this wave's)
   __builtin_amdgcn_wave_barrier();
   // eight lanes per flagged group: run r = (lane >> 1) & 3 of group slot lane >> 3, the lane
   // pair splitting the run's two quorum checks (new conf, old conf: one q-th largest each,
-  // joined by one shuffle) -- the walk's VALU is what a flagged wave adds, and the two
-  // sorting networks were most of it
+  // joined by one exchange)
   const uint32_t q = lane >> 3, r = (lane >> 1) & 3u, mh = lane & 1u;
-  // this wave's flagged groups (f0 / f1 are false on lanes past the table)
-  const uint32_t nflag = __popcll(__ballot(f0)) + __popcll(__ballot(f1));
+  const uint32_t nflag = __popcll(__ballot(f[0])) + __popcll(__ballot(f[1])) +
+                         __popcll(__ballot(f[2])) + __popcll(__ballot(f[3]));
   for (uint32_t base = 0; base < nflag; base += 8) {  // (wave-uniform)
     const uint32_t i = base + q;
     bool act = i < nflag;
@@ -252,9 +250,8 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
         const int64_t s = rs > pi ? rs : pi;
         const int64_t e = nx == kI64Max ? hla : nx - 1;
         const int64_t ee = e < hla ? e : hla;
-        // the walk runs when every load of the wave has landed and the VALU is the busy
-        // unit: 32-bit arithmetic relative to pendingIndex for every real group (half the
-        // VALU of the 64-bit rank count), 64-bit outside rel_domain
+        // 32-bit arithmetic relative to pendingIndex for every real group, 64-bit outside
+        // rel_domain
         if (rel_domain(pi, hla)) {
           RelGroup<P> rg;
           rel_map<P>(pi, hla, hm, rg);
@@ -278,9 +275,9 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
     const uint32_t kp = dpp32<kDppXor1>(kx);
     int64_t cand = cand64;
     if (relp) {
-      uint32_t c = kx < kp ? kx : kp;
-      c = c < er ? c : er;
-      cand = c >= sr ? pi - 1 + static_cast<int64_t>(c) : kI64Min;
+      uint32_t cc = kx < kp ? kx : kp;
+      cc = cc < er ? cc : er;
+      cand = cc >= sr ? pi - 1 + static_cast<int64_t>(cc) : kI64Min;
     }
     // max over the group's 8 lanes, complete on its lead lane (the lane pairs agree already)
     cand = max(cand, dpp64<kDppXor2>(cand));
@@ -296,78 +293,97 @@ __global__ __launch_bounds__(kTableBlock, 8) JRQ_SGPRS_8WAVES void table_epoch_k
       if (commit) table_commit_one(t, h, hpr, cand);
     }
     const uint64_t bc = __ballot(commit);
-    if (commit) staged[w][cnt + __popcll(bc & below)] = (static_cast<uint64_t>(cand - pi + 1) << 32) | h;
+    if (commit) slice[cnt + __popcll(bc & below)] = (static_cast<uint64_t>(cand - pi + 1) << 32) | h;
     cnt += __popcll(bc);
   }
-  // the single-conf results
-  if (tt < pairs) {
-    if (c0 && c1) {
-      i64x2 o;
-      o.x = o0;
-      o.y = o1;
-      __builtin_nontemporal_store(o, reinterpret_cast<i64x2*>(t.lc + g));
-      if (w0) t.pi[g] = kPiFollowsLc;
-      if (w1) t.pi[g + 1] = kPiFollowsLc;
-    } else {
-      if (c0) {
-        t.lc[g] = o0;
-        if (w0) t.pi[g] = kPiFollowsLc;
+  // groups outside rel_domain (negative or huge indexes, 4-billion-entry windows; never a real
+  // group): the 64-bit decision from reloaded words, in a wave-uniform branch kept out of the
+  // fast path's registers
+  if (__builtin_expect(__ballot(x[0] || x[1] || x[2] || x[3]) != 0, 0)) {
+#pragma unroll 1
+    for (uint32_t k = 0; k < 4; ++k) {
+      const bool mine = k == 0 ? x[0] : k == 1 ? x[1] : k == 2 ? x[2] : x[3];
+      const uint32_t h = gA + 128u * (k >> 1) + (k & 1u);
+      int64_t out = 0, pr = 0, pi = 0, lc = 0;
+      uint8_t st = 0;
+      if (mine) {
+        pr = t.pi[h];
+        lc = t.lc[h];
+        const int64_t la = t.la[h];
+        int64_t m[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) m[p] = t.match[static_cast<size_t>(p) * t.ld + h];
+        pi = pr == kPiFollowsLc ? lc + 1 : pr;
+        decide_single<P>(pi, la, lc, t.conf[h], m, out, st);
+        if (t.status) t.status[h] = st;
       }
-      if (c1) {
-        t.lc[g + 1] = o1;
-        if (w1) t.pi[g + 1] = kPiFollowsLc;
-      }
-    }
-    if (t.status) {  // a flagged group's status is written by the walk
-      if (g + 1 < t.G && !f0 && !f1)
-        __builtin_nontemporal_store(static_cast<uint16_t>(s01), reinterpret_cast<uint16_t*>(t.status + g));
-      else {
-        if (!f0) t.status[g] = static_cast<uint8_t>(s01);
-        if (!f1 && g + 1 < t.G) t.status[g + 1] = static_cast<uint8_t>(s01 >> 8);
-      }
-    }
-  }
-  if (lane == 0) wave_cnt[w] = cnt;
-  lds_barrier();  // (the results' stores stay in flight)
-  const uint32_t seg = blockIdx.x % kTableSegments;
-  if (threadIdx.x == 0) {
-    uint32_t tot = 0;
-    for (uint32_t u = 0; u < kWaves; ++u) tot += wave_cnt[u];
-    const unsigned long long old = atomicAdd(t.ctr + seg, (1ull << 32) | tot);
-    blk_base = seg * t.seg_cap + static_cast<uint32_t>(old);
-    const uint32_t seg_blocks = (gridDim.x - seg + kTableSegments - 1) / kTableSegments;
-    if (static_cast<uint32_t>(old >> 32) + 1u == seg_blocks) {  // the segment is complete
-      t.n_changed[seg] = static_cast<uint32_t>(old) + tot;
-      atomicExch(t.ctr + seg, 0ull);
+      const bool commit = mine && out > lc;
+      if (commit) table_commit_one(t, h, pr, out);
+      const uint64_t bc = __ballot(commit);
+      if (commit) slice[cnt + __popcll(bc & below)] = (static_cast<uint64_t>(out - pi + 1) << 32) | h;
+      cnt += __popcll(bc);
     }
   }
-  lds_barrier();
-  uint32_t pos = blk_base;
-  for (uint32_t u = 0; u < w; ++u) pos += wave_cnt[u];
-  for (uint32_t i = lane; i < cnt; i += 64) t.changed[pos + i] = staged[w][i];
+  if (lane == 0 && static_cast<uint64_t>(wid) * kTableSlice < t.G) t.n_changed[wid] = cnt;
 }
 
-// The flagged-entry slots: per 128-group wave range of the epoch kernel, its groups flagged
+// Host variant of the epoch: the slices' counts scanned into offsets (one workgroup; a
+// 1M-group table has 8192 slices) and the slices gathered back to back (one wave per slice),
+// so that only the entries cross PCIe.  total_out[0] = the number of entries.
+constexpr uint32_t kScanBlock = 1024;
+__global__ __launch_bounds__(kScanBlock) void table_list_scan_kernel(const uint32_t* __restrict__ n,
+                                                                     uint32_t slices,
+                                                                     uint32_t* __restrict__ off,
+                                                                     uint32_t* __restrict__ total_out) {
+  __shared__ uint32_t wsum[kScanBlock / 64];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  for (uint32_t b = 0; b < slices; b += kScanBlock) {
+    const uint32_t i = b + threadIdx.x;
+    const uint32_t v = i < slices ? n[i] : 0u;
+    uint32_t x = v;  // inclusive scan over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= static_cast<uint32_t>(o)) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t before = carry;
+    for (uint32_t u = 0; u < w; ++u) before += wsum[u];
+    if (i < slices) off[i] = before + x - v;
+    __syncthreads();
+    if (threadIdx.x == kScanBlock - 1) carry = before + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) total_out[0] = carry;
+}
+
+__global__ __launch_bounds__(512) void table_list_gather_kernel(const uint64_t* __restrict__ changed,
+                                                                const uint32_t* __restrict__ n,
+                                                                const uint32_t* __restrict__ off,
+                                                                uint32_t slices,
+                                                                uint64_t* __restrict__ out) {
+  const uint32_t s = blockIdx.x * 8u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (s >= slices) return;
+  const uint32_t k = n[s], o = off[s];
+  for (uint32_t i = lane; i < k; i += 64) out[o + i] = changed[static_cast<size_t>(s) * kTableSlice + i];
+}
+
+// The flagged-entry slots: per 256-group wave range of the epoch kernel, its groups flagged
 // JRQ_CONF_RUNS, each as a 64-B entry {group, start1 | start2, start3 | conf0, conf1 | conf2,
 // conf3} (run starts and conf words; unused runs: start INT64_MAX, conf 0), and their count.
 // Rebuilt after every update that carries group headers (only headers change runs and flags);
-// the waves map exactly as the epoch kernel's (1024-thread workgroups, two groups per lane),
-// no barrier, no atomics.
-constexpr uint32_t kFlagBlock = kTableBlockGroups / 2;
+// the waves map exactly as the epoch kernel's (lane l: pairs A = 256 w + 2 l and B = A + 128,
+// entries in the order A.x, A.y, B.x, B.y groups by ballot rank), no barrier, no atomics.
+constexpr uint32_t kFlagBlock = 64 * kTableBlockWaves;
 __global__ __launch_bounds__(kFlagBlock) void table_flags_kernel(JrqTableArgs t) {
-  const uint32_t pairs = (t.G + 1) >> 1;
-  const uint32_t tt = blockIdx.x * kFlagBlock + threadIdx.x;
-  const uint32_t g = tt << 1;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wid = blockIdx.x * (kFlagBlock / 64) + (threadIdx.x >> 6);
-  bool f0 = false, f1 = false;
-  if (tt < pairs) {
-    const i64x2 cw = tld2(reinterpret_cast<const int64_t*>(t.conf) + g);
-    f0 = static_cast<uint64_t>(cw.x) >> 63;
-    f1 = (static_cast<uint64_t>(cw.y) >> 63) && g + 1 < t.G;
-  }
+  const uint32_t gA = wid * kTableSlice + 2u * lane;
   const uint64_t below = (1ull << lane) - 1ull;
-  const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
   int64_t* const ent = reinterpret_cast<int64_t*>(t.flag_ent) + static_cast<size_t>(wid) * kFlagSlots * 8;
   auto put = [&](uint32_t k, uint32_t h) {
     int64_t* e = ent + k * 8;
@@ -377,9 +393,22 @@ __global__ __launch_bounds__(kFlagBlock) void table_flags_kernel(JrqTableArgs t)
     for (int r = 1; r < kTableMaxRuns; ++r)
       e[4 + r] = static_cast<int64_t>(t.xconf[static_cast<size_t>(r - 1) * t.ld + h]);
   };
-  if (f0) put(__popcll(b0 & below), g);
-  if (f1) put(__popcll(b0) + __popcll(b1 & below), g + 1);
-  if (lane == 0) t.flag_wcnt[wid] = __popcll(b0) + __popcll(b1);
+  uint32_t base = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t g = gA + 128u * h;
+    bool f0 = false, f1 = false;
+    if (g < t.G) {
+      const i64x2 cw = tld2(reinterpret_cast<const int64_t*>(t.conf) + g);
+      f0 = static_cast<uint64_t>(cw.x) >> 63;
+      f1 = (static_cast<uint64_t>(cw.y) >> 63) && g + 1 < t.G;
+    }
+    const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
+    if (f0) put(base + __popcll(b0 & below), g);
+    if (f1) put(base + __popcll(b0) + __popcll(b1 & below), g + 1);
+    base += __popcll(b0) + __popcll(b1);
+  }
+  if (lane == 0) t.flag_wcnt[wid] = base;
 }
 
 // Group headers: one lane per header (a group appears at most once per call).
@@ -450,8 +479,8 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_upd
   if (n_states) {
     hipLaunchKernelGGL(jrq::table_states_kernel, dim3((n_states + 255) / 256), dim3(256), 0,
                        stream, *a, states, n_states);
-    const uint32_t pairs = (a->G + 1) >> 1;
-    hipLaunchKernelGGL(jrq::table_flags_kernel, dim3((pairs + jrq::kFlagBlock - 1) / jrq::kFlagBlock),
+    const uint32_t waves = (a->G + jrq::kTableSlice - 1) / jrq::kTableSlice;
+    hipLaunchKernelGGL(jrq::table_flags_kernel, dim3((waves + jrq::kFlagBlock / 64 - 1) / (jrq::kFlagBlock / 64)),
                        dim3(jrq::kFlagBlock), 0, stream, *a);
   }
   if (n_recs)
@@ -460,17 +489,20 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_upd
   return hipGetLastError();
 }
 
-extern "C" __attribute__((visibility("hidden"))) uint32_t jrq_table_seg_cap(uint32_t G) {
-  const uint32_t blocks = (G + jrq::kTableBlockGroups - 1) / jrq::kTableBlockGroups;
-  return (blocks + jrq::kTableSegments - 1) / jrq::kTableSegments * jrq::kTableBlockGroups;
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_list_gather(
+    const uint64_t* changed, const uint32_t* n, uint32_t slices, uint32_t* off, uint32_t* total,
+    uint64_t* out, hipStream_t stream) {
+  hipLaunchKernelGGL(jrq::table_list_scan_kernel, dim3(1), dim3(jrq::kScanBlock), 0, stream, n, slices,
+                     off, total);
+  hipLaunchKernelGGL(jrq::table_list_gather_kernel, dim3((slices + 7) / 8), dim3(512), 0, stream,
+                     changed, n, off, slices, out);
+  return hipGetLastError();
 }
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_epoch(
     const JrqTableArgs* a, hipStream_t stream) {
-  const uint32_t pairs = (a->G + 1) >> 1;
-  const dim3 grid((pairs + jrq::kTableBlock - 1) / jrq::kTableBlock), blk(jrq::kTableBlock);
-  if (grid.x < jrq::kTableSegments)  // segments no workgroup appends to: count 0
-    (void)hipMemsetAsync(a->n_changed + grid.x, 0, 4 * (jrq::kTableSegments - grid.x), stream);
+  const uint32_t waves = (a->G + jrq::kTableSlice - 1) / jrq::kTableSlice;
+  const dim3 grid((waves + jrq::kTableEpochBlock / 64 - 1) / (jrq::kTableEpochBlock / 64)), blk(jrq::kTableEpochBlock);
   switch (a->P) {
 #define JRQ_CASE(P)                                                                   \
   case P:                                                                             \

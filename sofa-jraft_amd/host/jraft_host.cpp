@@ -757,7 +757,7 @@ uint32_t GroupBatch::flushLocked() {
   stats.changed = n;
   stats.h2d_bytes = static_cast<uint64_t>(stats.states) * sizeof(jrq_group_state) +
                     static_cast<uint64_t>(stats.records) * 8;
-  stats.d2h_bytes = 4 * JRQ_TABLE_SEGMENTS + static_cast<uint64_t>(n) * 8;
+  stats.d2h_bytes = 4 + static_cast<uint64_t>(n) * 8;
   stats.pack_ms = ms(t1 - t0);
   stats.device_ms = ms(t2 - t1);
   stats.deliver_ms = ms(t3 - t2);

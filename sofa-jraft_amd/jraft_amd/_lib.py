@@ -50,7 +50,7 @@ TABLE_MAX_RUNS = 4                     # JRQ_TABLE_MAX_RUNS
 TABLE_MAX_GROUPS = 1 << 27             # JRQ_TABLE_MAX_GROUPS
 PI_FOLLOWS_LC = -(1 << 63)             # JRQ_PI_FOLLOWS_LC
 REC_LAST_APPENDED = 16                 # JRQ_REC_LAST_APPENDED
-TABLE_SEGMENTS = 16                    # JRQ_TABLE_SEGMENTS
+TABLE_SLICE = 256                      # JRQ_TABLE_SLICE
 STATE_RESET_MATCH = 1                  # JRQ_STATE_RESET_MATCH
 # jrq_debug_option (test / A-B hooks)
 DBG_CRC_SEG_BYTES, DBG_CRC_REGS, DBG_CRC_PRIO, DBG_CRC_SEG_MAP, DBG_UPLOAD_PAGEABLE = 1, 2, 3, 4, 5
@@ -133,7 +133,7 @@ SIGNATURES = [
     ("jrq_table_update_gather", C.c_int, [_V, C.c_uint32, _V, _V, _V, _V]),
     ("jrq_table_epoch_dev", C.c_int, [_V, _V, _V, _V]),
     ("jrq_table_epoch", C.c_int, [_V, _V, _V, _V]),
-    ("jrq_table_segment_capacity", C.c_uint32, [_V]),
+    ("jrq_table_slices", C.c_uint32, [_V]),
     ("jrq_table_read", C.c_int, [_V, _V, _V, _V, _V]),
     ("jrq_table_check", C.c_int, [_V]),
     ("jrq_table_copy", C.c_int, [_V, _V]),

@@ -466,21 +466,30 @@ class Table:
         self._keep = None
         return out[: n.value].copy(), st
 
-    def segment_capacity(self) -> int:
-        return int(self._L.jrq_table_segment_capacity(self._h))
+    def slices(self) -> int:
+        """Slices of the device variant's changed list (one per TABLE_SLICE groups)."""
+        return int(self._L.jrq_table_slices(self._h))
+
+    def list_buffers(self, device):
+        """(changed_out, n_changed_out) device tensors sized for epoch_dev."""
+        import torch
+        s = self.slices()
+        return (torch.empty(s * _lib.TABLE_SLICE, dtype=torch.int64, device=device),
+                torch.zeros(s, dtype=torch.int32, device=device))
 
     def epoch_dev(self, changed_out, n_changed_out, status_out=None):
-        """Device variant: changed_out capacity TABLE_SEGMENTS * segment_capacity() words,
-        n_changed_out int32[TABLE_SEGMENTS] per-segment counts (see include/jrq.h)."""
+        """Device variant: changed_out capacity TABLE_SLICE * slices() words, n_changed_out
+        int32[slices()] per-slice counts (slice s lists groups [256 s, 256 s + 256) at
+        changed_out[256 s ..], see include/jrq.h)."""
         check(self._L.jrq_table_epoch_dev(self._h, _dev_ptr(changed_out), _dev_ptr(n_changed_out),
                                           _dev_ptr(status_out)), self._eng.handle)
 
     def gather_dev_list(self, changed_out, n_changed_out) -> np.ndarray:
-        """Host copy of a device-variant list (segments back to back), as JRQ words."""
-        cap = self.segment_capacity()
+        """Host copy of a device-variant list (slices back to back), as JRQ words."""
         counts = n_changed_out.cpu().numpy().astype(np.int64)
-        words = changed_out.cpu().numpy().view(np.uint64)
-        return np.concatenate([words[s * cap: s * cap + counts[s]] for s in range(len(counts))])
+        words = changed_out.cpu().numpy().view(np.uint64).reshape(-1, _lib.TABLE_SLICE)
+        keep = np.arange(_lib.TABLE_SLICE)[None, :] < counts[:, None]
+        return words[keep]
 
     def read(self) -> dict:
         G, P = self.G, self.P

@@ -187,8 +187,7 @@ def test_device_variant_and_view(engine, oracle):
     st = torch.from_numpy(states_of(b).view(np.uint8)).to(dev)
     rc = torch.from_numpy(match_recs(b["match"], b["pending_index"]).view(np.int64)).to(dev)
     t.update_dev(st, rc)
-    out = torch.empty(_lib.TABLE_SEGMENTS * t.segment_capacity(), dtype=torch.int64, device=dev)
-    n = torch.zeros(_lib.TABLE_SEGMENTS, dtype=torch.int32, device=dev)
+    out, n = t.list_buffers(dev)
     t.epoch_dev(out, n)
     engine.synchronize()
     got, _ = committed_from(t.gather_dev_list(out, n), b["pending_index"], b["last_committed"])
@@ -303,12 +302,11 @@ def test_flagged_groups_in_full_blocks(engine, G, joint):
         if rep == 0:
             changed, stt = t.epoch(status=True)
         else:
-            out = torch.empty(_lib.TABLE_SEGMENTS * t.segment_capacity(), dtype=torch.int64, device=dev)
-            n = torch.zeros(_lib.TABLE_SEGMENTS, dtype=torch.int32, device=dev)
+            out, n = t.list_buffers(dev)
             sd = torch.empty(G, dtype=torch.uint8, device=dev)
             t.epoch_dev(out, n, sd)
             engine.synchronize()
-            assert (n.cpu().numpy() <= t.segment_capacity()).all()
+            assert (n.cpu().numpy() <= _lib.TABLE_SLICE).all()
             changed, stt = t.gather_dev_list(out, n), sd.cpu().numpy()
         got, _ = committed_from(changed, pi, s["last_committed"])
         np.testing.assert_array_equal(got, exp_c)

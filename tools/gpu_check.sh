@@ -37,6 +37,8 @@ for s in $STEPS; do
              run pmc_${leg}_RDREQ 180 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum -d gpurun_out/pmc_${leg}_RDREQ -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs $leg
            done ;;
     host)  run host_test 300 ./tests/_build/host_test gpu ;;
+    tsel)  run tests_${TAG:-sel} 900 python -u -m pytest ${TESTS:-tests/test_gpu_table.py} -x -q -p no:cacheprovider --timeout 240 --timeout-method thread ;;
+    bsel)  run bench_${TAG:-sel} 600 python bench.py --steps 20 --warmup 5 --no-cpu --legs ${BENCH_LEGS:-quorum} --detail gpurun_out/bench_${TAG:-sel}_detail.json ;;
     tprobe) run table_probe 120 ./tools/table_probe ;;
     fprobe) run flag_probe 120 ./tools/flag_probe ;;
     fprobe2) run flag_probe_b1024 120 ./tools/flag_probe_b1024 ;;
