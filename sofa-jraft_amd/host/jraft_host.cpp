@@ -48,8 +48,8 @@ std::vector<std::string> split(const std::string& s, char sep) {
 // ------------------------------------------------------------------ entities
 
 std::string PeerId::toString() const {
-  std::string s = ip + ":" + std::to_string(port);  // Endpoint.toString (Endpoint.java:60-65)
-  if (idx != 0) s += ":" + std::to_string(idx);    // PeerId.toString (PeerId.java:135-144)
+  std::string s = ip_ + ":" + std::to_string(port_);  // Endpoint.toString (Endpoint.java:60-65)
+  if (idx_ != 0) s += ":" + std::to_string(idx_);    // PeerId.toString (PeerId.java:135-144)
   return s;
 }
 
@@ -57,12 +57,15 @@ bool PeerId::parse(const std::string& s, PeerId* out) {
   auto t = split(s, ':');
   if (t.size() != 2 && t.size() != 3) return false;
   try {
-    out->ip = t[0];
-    out->port = std::stoi(t[1]);
-    out->idx = t.size() == 3 ? std::stoi(t[2]) : 0;
+    const int32_t port = std::stoi(t[1]);
+    const int32_t idx = t.size() == 3 ? std::stoi(t[2]) : 0;
+    out->ip_ = t[0];
+    out->port_ = port;
+    out->idx_ = idx;
   } catch (...) {
     return false;
   }
+  out->internId.store(0, std::memory_order_relaxed);  // new contents: look the id up again
   return true;
 }
 
@@ -194,11 +197,10 @@ uint64_t CRC64::getValue() {
 
 namespace {
 
-// Process-wide PeerId -> id table (ids from 1; PeerId::internId 0 = not looked up).  Entries
-// sit in fixed chunks that never move, so a caller holding an id reads its entry without a
-// lock: the id was published (release) after the entry was written.  Java compares PeerIds
-// by value (PeerId.equals -> Endpoint.equals -> String.equals, PeerId.java:180-199); the
-// cached id is checked against the entry, so a PeerId changed after caching is re-interned.
+// Process-wide PeerId -> id table (ids from 1; PeerId::internId 0 = not looked up).  A PeerId
+// only changes through PeerId::parse, which clears its cached id, so a cached id is current
+// and a lookup is one load; Java compares PeerIds by value (PeerId.equals -> Endpoint.equals ->
+// String.equals, PeerId.java:180-199), and equal PeerIds intern to the same id.
 class PeerRegistry {
  public:
   static PeerRegistry& get() {
@@ -206,8 +208,8 @@ class PeerRegistry {
     return r;
   }
   uint32_t id(const PeerId& p) {
-    const uint32_t c = p.internId.load(std::memory_order_acquire);
-    if (c != 0 && matches(c, p)) return c;
+    const uint32_t c = p.internId.load(std::memory_order_relaxed);
+    if (c != 0) return c;
     uint32_t i;
     {
       std::lock_guard<std::mutex> l(mu_);
@@ -215,48 +217,25 @@ class PeerRegistry {
       if (it != map_.end()) {
         i = it->second;
       } else {
-        i = next_;
-        if (i >= kChunks * kChunkSize) throw std::length_error("more than 2^24 distinct PeerIds");
-        std::atomic<Entry*>& ch = chunks_[i / kChunkSize];
-        if (!ch.load(std::memory_order_relaxed)) ch.store(new Entry[kChunkSize], std::memory_order_release);
-        Entry& e = ch.load(std::memory_order_relaxed)[i % kChunkSize];
-        e.ip = p.ip;
-        e.port = p.port;
-        e.idx = p.idx;
+        if (next_ >= (1u << 24)) throw std::length_error("more than 2^24 distinct PeerIds");
+        i = next_++;
         map_.emplace(p, i);
-        ++next_;
       }
     }
-    p.internId.store(i, std::memory_order_release);
+    p.internId.store(i, std::memory_order_relaxed);
     return i;
   }
 
  private:
-  static constexpr uint32_t kChunkSize = 4096, kChunks = 4096;
-  struct Entry {
-    std::string ip;
-    int32_t port = 0, idx = 0;
-  };
   struct Hash {
     size_t operator()(const PeerId& p) const {
-      return std::hash<std::string>()(p.ip) ^ (static_cast<size_t>(p.port) << 20) ^
-             (static_cast<size_t>(p.idx) << 40);
+      return std::hash<std::string>()(p.getIp()) ^ (static_cast<size_t>(p.getPort()) << 20) ^
+             (static_cast<size_t>(p.getIdx()) << 40);
     }
   };
-  bool matches(uint32_t i, const PeerId& p) const {
-    const Entry& e = chunks_[i / kChunkSize].load(std::memory_order_acquire)[i % kChunkSize];
-    return e.port == p.port && e.idx == p.idx && e.ip == p.ip;
-  }
-  PeerRegistry() {
-    for (auto& c : chunks_) c.store(nullptr, std::memory_order_relaxed);
-  }
-  ~PeerRegistry() {
-    for (auto& c : chunks_) delete[] c.load(std::memory_order_relaxed);
-  }
   std::mutex mu_;
   std::unordered_map<PeerId, uint32_t, Hash> map_;
   uint32_t next_ = 1;
-  std::atomic<Entry*> chunks_[kChunks];
 };
 
 inline uint32_t peerId(const PeerId& p) { return PeerRegistry::get().id(p); }
@@ -298,10 +277,21 @@ struct GroupBatch::Part {  // one pack worker's headers and records (page-locked
   uint32_t ns = 0, nr = 0;
 };
 
+// One deliver worker's share of an epoch: the commits it applied (group, index, waiter) and
+// the closures it popped, run after every group of the share has moved.
+struct GroupBatch::Delivery {
+  struct Commit {
+    int64_t c;
+    const CommitWaiter* waiter;  // the group's (set once by BallotBox::init, before its first ack)
+  };
+  std::vector<Commit> commits;
+  std::vector<std::function<void(bool)>> done;  // in commit order
+  std::vector<uint32_t> ndone;                  // closures per commit
+};
+
 struct GroupBatch::Flusher {
   std::thread th;
   std::atomic<bool> stop{false};
-  std::string error;
 };
 
 // Persistent workers for flush()'s pack and deliver passes (spawning threads per flush cost
@@ -443,20 +433,26 @@ GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
     : eng_(eng), G_(groups), P_(peers), serial_(g_batchSerial.fetch_add(1)) {
   if (peers == 0 || peers > JRQ_MAX_PEERS) throw std::invalid_argument("peers must be 1..16");
   if (groups == 0 || groups > JRQ_TABLE_MAX_GROUPS) throw std::invalid_argument("groups must be 1..2^27");
-  const size_t GP = static_cast<size_t>(G_) * P_;
-  lock_.reset(new std::atomic<uint8_t>[G_]);
-  for (uint32_t g = 0; g < G_; ++g) lock_[g].store(0, std::memory_order_relaxed);
-  pi_.assign(G_, 0);
-  lc_.assign(G_, 0);
-  la_.assign(G_, -1);
+  stride_ = (sizeof(Hot) + 16 * static_cast<size_t>(P_) + 63) & ~size_t(63);
+  const size_t bytes = stride_ * G_;
+  rec_ = static_cast<unsigned char*>(std::aligned_alloc(64, bytes));
+  if (!rec_) throw std::bad_alloc();
+  std::memset(rec_, 0, bytes);
+  for (uint32_t g = 0; g < G_; ++g) {
+    Hot* h = new (rec_ + static_cast<size_t>(g) * stride_) Hot();
+    h->lock.store(0, std::memory_order_relaxed);
+    h->nruns = 0;
+    h->inited = 0;
+    h->dirty = 0;
+    h->pi = 0;
+    h->lc = 0;
+    h->la = -1;
+    h->lastConf = 0;
+    uint32_t* sp = slotPeerOf(g);
+    for (uint32_t s = 0; s < P_; ++s) sp[s] = kNoPeer;
+  }
   runs_.assign(static_cast<size_t>(G_) * JRQ_TABLE_MAX_RUNS, Run{0, 0});
-  nruns_.assign(G_, 0);
-  slotPeer_.assign(GP, kNoPeer);
-  slotUse_.assign(GP, 0);
-  match_.assign(GP, 0);
-  dirty_.assign(G_, 0);
   waiter_.resize(G_);
-  inited_.assign(G_, 0);
   closures_.resize(G_);
 }
 
@@ -466,10 +462,14 @@ GroupBatch::~GroupBatch() {
   } catch (...) {
   }
   if (table_) jrq_table_destroy(table_);
+  std::free(rec_);
 }
 
-void GroupBatch::lock(uint32_t g) const { spinLock(lock_[g]); }
+void GroupBatch::lock(uint32_t g) const { spinLock(hot(g).lock); }
 
+// This thread's dirty list for this batch: a thread-local cache of 4 (batch, list) pairs, and on
+// a miss the batch's own per-thread map -- one list per (thread, batch) however many batches a
+// thread alternates between (a miss costs a mutex, never a new list).
 GroupBatch::DirtyList* GroupBatch::myDirtyList() {
   struct Slot {
     const GroupBatch* b;
@@ -483,8 +483,12 @@ GroupBatch::DirtyList* GroupBatch::myDirtyList() {
   DirtyList* l;
   {
     std::lock_guard<std::mutex> g(listsMu_);
-    lists_.emplace_back(new DirtyList());
-    l = lists_.back().get();
+    DirtyList*& mine = byThread_[std::this_thread::get_id()];
+    if (!mine) {
+      lists_.emplace_back(new DirtyList());
+      mine = lists_.back().get();
+    }
+    l = mine;
   }
   cache[next++ & 3u] = Slot{this, serial_, l};
   return l;
@@ -493,7 +497,8 @@ GroupBatch::DirtyList* GroupBatch::myDirtyList() {
 // Under the group's lock: the first change since the group was last packed puts it on this
 // thread's dirty list; the bits say what to pack.
 void GroupBatch::markDirty(uint32_t g, uint32_t bits) {
-  if (dirty_[g] == 0) {
+  Hot& h = hot(g);
+  if (h.dirty == 0) {
     DirtyList* l = myDirtyList();
     spinLock(l->mu);
     if (l->v.empty()) l->firstNs.store(nowNs(), std::memory_order_relaxed);
@@ -501,13 +506,14 @@ void GroupBatch::markDirty(uint32_t g, uint32_t bits) {
     l->n.store(l->v.size(), std::memory_order_relaxed);
     l->mu.store(0, std::memory_order_release);
   }
-  dirty_[g] |= bits;
+  h.dirty |= bits;
 }
 
 // Slots named by the masks of the group's live conf runs: their peers vote on pending entries.
 uint32_t GroupBatch::liveMask(uint32_t g) const {
   uint32_t m = 0;
-  for (uint32_t r = 0; r < nruns_[g]; ++r) {
+  const uint32_t n = hot(g).nruns;
+  for (uint32_t r = 0; r < n; ++r) {
     const uint64_t cw = runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS + r].conf;
     m |= static_cast<uint32_t>(cw & 0xFFFFu) | static_cast<uint32_t>((cw >> 16) & 0xFFFFu);
   }
@@ -518,24 +524,25 @@ uint32_t GroupBatch::liveMask(uint32_t g) const {
 // no live conf run names (and that is not in `reserved`), its match reset (its peer's acks no
 // longer matter to any pending ballot).  -1 when there is none (every slot is live).
 int GroupBatch::slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved) {
-  const size_t base = static_cast<size_t>(g) * P_;
+  uint32_t* sp = slotPeerOf(g);
   int victim = -1;
   for (uint32_t s = 0; s < P_; ++s) {
-    if (slotPeer_[base + s] == peer) return static_cast<int>(s);
-    if (victim < 0 && slotPeer_[base + s] == kNoPeer) victim = static_cast<int>(s);
+    if (sp[s] == peer) return static_cast<int>(s);
+    if (victim < 0 && sp[s] == kNoPeer) victim = static_cast<int>(s);
   }
   if (!create) return -1;
+  uint32_t* su = slotUseOf(g);
   if (victim < 0) {
     const uint32_t busy = liveMask(g) | reserved;
     for (uint32_t s = 0; s < P_; ++s)
-      if (!((busy >> s) & 1u) && (victim < 0 || slotUse_[base + s] < slotUse_[base + victim]))
-        victim = static_cast<int>(s);
+      if (!((busy >> s) & 1u) && (victim < 0 || su[s] < su[victim])) victim = static_cast<int>(s);
     if (victim < 0) return -1;
   }
-  slotPeer_[base + victim] = peer;
-  slotUse_[base + victim] = static_cast<uint32_t>(flushes_.load(std::memory_order_relaxed));
-  if (match_[base + victim] != 0) {
-    match_[base + victim] = 0;
+  sp[victim] = peer;
+  su[victim] = static_cast<uint32_t>(flushes_.load(std::memory_order_relaxed));
+  int64_t* m = matchOf(g);
+  if (m[victim] != 0) {
+    m[victim] = 0;
     markDirty(g, 1u << victim);
   }
   return victim;
@@ -557,10 +564,11 @@ uint64_t GroupBatch::confWord(uint32_t g, const uint32_t* ids, uint32_t nn, uint
 // Would a gap [lo, hi] in `slot`'s acks skip a pending entry whose ballot counts that slot?
 bool GroupBatch::gapCountsPeer(uint32_t g, int slot, int64_t lo, int64_t hi) const {
   const Run* R = &runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS];
-  const uint32_t n = nruns_[g];
+  const Hot& h = hot(g);
+  const uint32_t n = h.nruns;
   for (uint32_t r = 0; r < n; ++r) {
-    const int64_t s = r == 0 ? pi_[g] : R[r].start;
-    const int64_t e = r + 1 < n ? R[r + 1].start - 1 : la_[g];
+    const int64_t s = r == 0 ? h.pi : R[r].start;
+    const int64_t e = r + 1 < n ? R[r + 1].start - 1 : h.la;
     const uint64_t cw = R[r].conf;
     const uint32_t m = static_cast<uint32_t>(cw & 0xFFFFu) | static_cast<uint32_t>((cw >> 16) & 0xFFFFu);
     if (std::max(s, lo) <= std::min(e, hi) && ((m >> slot) & 1u)) return true;
@@ -570,12 +578,15 @@ bool GroupBatch::gapCountsPeer(uint32_t g, int slot, int64_t lo, int64_t hi) con
 
 // Drop runs wholly below pendingIndex (pendingMetaQueue.removeRange, BallotBox.java:130).
 void GroupBatch::dropDeadRuns(uint32_t g) {
+  Hot& h = hot(g);
+  const uint32_t n = h.nruns;
+  if (n < 2) return;
   Run* R = &runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS];
-  uint32_t n = nruns_[g], k = 0;
-  while (k + 1 < n && R[k + 1].start <= pi_[g]) ++k;
+  uint32_t k = 0;
+  while (k + 1 < n && R[k + 1].start <= h.pi) ++k;
   if (k) {
     for (uint32_t r = k; r < n; ++r) R[r - k] = R[r];
-    nruns_[g] = static_cast<uint8_t>(n - k);
+    h.nruns = static_cast<uint8_t>(n - k);
   }
 }
 
@@ -583,35 +594,39 @@ void GroupBatch::dropDeadRuns(uint32_t g) {
 // are taken and the header or records written from the group's current state.
 void GroupBatch::packRange(Part& part, const uint32_t* groups, size_t n) {
   uint32_t si = part.ns, ri = part.nr;
+  constexpr size_t kAhead = 4;
   for (size_t i = 0; i < n; ++i) {
+    if (i + kAhead < n) __builtin_prefetch(rec_ + static_cast<size_t>(groups[i + kAhead]) * stride_, 1);
     const uint32_t g = groups[i];
     Guard lk(*this, g);
-    const uint32_t d = dirty_[g];
-    dirty_[g] = 0;
-    const int64_t pi = pi_[g], base = pi - 1;
+    Hot& h = hot(g);
+    const uint32_t d = h.dirty;
+    h.dirty = 0;
+    const int64_t pi = h.pi, base = pi - 1;
     if (d & kDirtyHeader) {
       jrq_group_state& st = part.st.p[si++];
       std::memset(&st, 0, sizeof st);
       st.group = g;
-      st.num_runs = nruns_[g];
+      st.num_runs = h.nruns;
       st.flags = (d & kDirtyReset) ? JRQ_STATE_RESET_MATCH : 0;
       // the table's steady-state encoding of pendingIndex = lastCommittedIndex + 1: the
       // group's next commit then writes lastCommitted only
-      st.pending_index = (pi != 0 && pi == lc_[g] + 1) ? JRQ_PI_FOLLOWS_LC : pi;
-      st.last_appended = la_[g];
-      st.last_committed = lc_[g];
+      st.pending_index = (pi != 0 && pi == h.lc + 1) ? JRQ_PI_FOLLOWS_LC : pi;
+      st.last_appended = h.la;
+      st.last_committed = h.lc;
       const Run* R = &runs_[static_cast<size_t>(g) * JRQ_TABLE_MAX_RUNS];
-      for (uint32_t r = 0; r < nruns_[g]; ++r) {
+      for (uint32_t r = 0; r < h.nruns; ++r) {
         st.run_conf[r] = R[r].conf;
         st.run_start[r] = R[r].start;
       }
     } else if ((d & kDirtyLa) && pi != 0) {
-      part.rec.p[ri++] = JRQ_REC(g, JRQ_REC_LAST_APPENDED, la_[g] - base);
+      part.rec.p[ri++] = JRQ_REC(g, JRQ_REC_LAST_APPENDED, h.la - base);
     }
     if (pi == 0) continue;  // not the leader: its acks are refused (commitAt returns false)
-    for (uint32_t m = d & 0xFFFFu; m; m &= m - 1) {
-      const uint32_t s = static_cast<uint32_t>(__builtin_ctz(m));
-      const int64_t v = match_[static_cast<size_t>(g) * P_ + s] - base;
+    const int64_t* m = matchOf(g);
+    for (uint32_t b = d & 0xFFFFu; b; b &= b - 1) {
+      const uint32_t s = static_cast<uint32_t>(__builtin_ctz(b));
+      const int64_t v = m[s] - base;
       part.rec.p[ri++] = JRQ_REC(g, s, v > 0 ? v : 0);
     }
   }
@@ -619,9 +634,36 @@ void GroupBatch::packRange(Part& part, const uint32_t* groups, size_t n) {
   part.nr = ri;
 }
 
+// After a failed upload or epoch: every group this flush swapped out goes back on a live list
+// with its whole state marked (header, every slot, queue size), so the next flush re-syncs the
+// device's copy -- whatever part of this one reached it -- from the host's.  The pack cleared
+// the dirty bits of the groups it had packed; without this they were listed nowhere and never
+// shipped again.
+void GroupBatch::relistAfterFailure() {
+  const uint32_t all = kDirtyHeader | kDirtyLa | ((1u << P_) - 1u);
+  for (auto& v : work_) {
+    for (uint32_t g : v) {
+      Guard lk(*this, g);
+      Hot& h = hot(g);
+      const uint32_t d = h.dirty & kDirtyReset;
+      h.dirty = 0;  // not on any list: markDirty lists it again
+      markDirty(g, all | d);
+    }
+    v.clear();
+  }
+}
+
 uint32_t GroupBatch::flush() {
   if (tl_delivering == this)
     throw std::logic_error("GroupBatch::flush from inside a commit callback of the same batch");
+  {
+    std::lock_guard<std::mutex> el(errMu_);
+    if (!flusherError_.empty()) {
+      const std::string err = flusherError_;
+      flusherError_.clear();
+      throw std::runtime_error("GroupBatch flusher: " + err);
+    }
+  }
   std::lock_guard<std::mutex> fl(flushMu_);
   return flushLocked();
 }
@@ -637,10 +679,12 @@ uint32_t GroupBatch::flushLocked() {
     if (!table_) throwIfError(err ? err : JRQ_E_NOMEM, eng_->raw(), "jrq_table_create");
     for (uint32_t g = 0; g < G_; ++g) {
       Guard lk(*this, g);
+      const Hot& h = hot(g);
       uint32_t bits = 0;
-      if (pi_[g] != 0 || lc_[g] != 0 || nruns_[g] != 0) bits |= kDirtyHeader;
+      if (h.pi != 0 || h.lc != 0 || h.nruns != 0) bits |= kDirtyHeader;
+      const int64_t* m = matchOf(g);
       for (uint32_t s = 0; s < P_; ++s)
-        if (match_[static_cast<size_t>(g) * P_ + s] != 0) bits |= 1u << s;
+        if (m[s] != 0) bits |= 1u << s;
       if (bits) markDirty(g, bits);
     }
   }
@@ -662,94 +706,119 @@ uint32_t GroupBatch::flushLocked() {
   std::vector<size_t> pre(nl + 1, 0);
   for (size_t i = 0; i < nl; ++i) pre[i + 1] = pre[i] + work_[i].size();
   const size_t nd = pre[nl];
-  // pack: the dirty groups split into contiguous ranges of the concatenated lists
-  const size_t kGrain = 1u << 12;
-  const size_t nparts = partsFor(nd, kGrain);
-  if (parts_.size() < nparts) parts_.resize(nparts);
-  for (auto& p : parts_) p.ns = p.nr = 0;
-  // staging grows here, on this thread: allocation and release of page-locked memory stay
-  // out of the pack workers
-  for (size_t i = 0; i < nparts; ++i) {
-    const size_t len = nd * (i + 1) / nparts - nd * i / nparts;
-    parts_[i].st.reserve(len + 1);
-    parts_[i].rec.reserve(len * (P_ + 1) + 1);
-  }
-  parallelFor(nd, kGrain, [&](unsigned part, size_t b, size_t e) {
-    Part& P = parts_[part];
-    // the pieces of the lists inside [b, e)
-    size_t li = static_cast<size_t>(std::upper_bound(pre.begin(), pre.end(), b) - pre.begin()) - 1;
-    for (size_t pos = b; pos < e; ++li) {
-      const size_t lo = pos - pre[li], hi = std::min(e, pre[li + 1]) - pre[li];
-      if (hi <= lo) continue;
-      packRange(P, work_[li].data() + lo, hi - lo);
-      pos = pre[li] + hi;
-    }
-  });
-  std::vector<const jrq_group_state*> sp(nparts);
-  std::vector<const uint64_t*> rp(nparts);
-  std::vector<uint32_t> sn(nparts), rn(nparts);
-  for (size_t i = 0; i < nparts; ++i) {
-    sp[i] = parts_[i].st.p;
-    rp[i] = parts_[i].rec.p;
-    sn[i] = parts_[i].ns;
-    rn[i] = parts_[i].nr;
-    stats.states += sn[i];
-    stats.records += rn[i];
-  }
-  changed_.reserve(G_);
-  const auto t1 = clk::now();
-  throwIfError(jrq_table_update_gather(table_, static_cast<uint32_t>(nparts), sp.data(), sn.data(),
-                                       rp.data(), rn.data()),
-               eng_->raw(), "jrq_table_update_gather");
   uint32_t n = 0;
-  throwIfError(jrq_table_epoch(table_, changed_.p, &n, nullptr), eng_->raw(), "jrq_table_epoch");
+  auto t1 = t0;
+  try {
+    // pack: the dirty groups split into contiguous ranges of the concatenated lists
+    const size_t kGrain = 1u << 12;
+    const size_t nparts = partsFor(nd, kGrain);
+    if (parts_.size() < nparts) parts_.resize(nparts);
+    for (auto& p : parts_) p.ns = p.nr = 0;
+    // staging grows here, on this thread: allocation and release of page-locked memory stay
+    // out of the pack workers
+    for (size_t i = 0; i < nparts; ++i) {
+      const size_t len = nd * (i + 1) / nparts - nd * i / nparts;
+      parts_[i].st.reserve(len + 1);
+      parts_[i].rec.reserve(len * (P_ + 1) + 1);
+    }
+    parallelFor(nd, kGrain, [&](unsigned part, size_t b, size_t e) {
+      Part& P = parts_[part];
+      // the pieces of the lists inside [b, e)
+      size_t li = static_cast<size_t>(std::upper_bound(pre.begin(), pre.end(), b) - pre.begin()) - 1;
+      for (size_t pos = b; pos < e; ++li) {
+        const size_t lo = pos - pre[li], hi = std::min(e, pre[li + 1]) - pre[li];
+        if (hi <= lo) continue;
+        packRange(P, work_[li].data() + lo, hi - lo);
+        pos = pre[li] + hi;
+      }
+    });
+    std::vector<const jrq_group_state*> sp(nparts);
+    std::vector<const uint64_t*> rp(nparts);
+    std::vector<uint32_t> sn(nparts), rn(nparts);
+    for (size_t i = 0; i < nparts; ++i) {
+      sp[i] = parts_[i].st.p;
+      rp[i] = parts_[i].rec.p;
+      sn[i] = parts_[i].ns;
+      rn[i] = parts_[i].nr;
+      stats.states += sn[i];
+      stats.records += rn[i];
+    }
+    changed_.reserve(G_);
+    t1 = clk::now();
+    throwIfError(jrq_table_update_gather(table_, static_cast<uint32_t>(nparts), sp.data(), sn.data(),
+                                         rp.data(), rn.data()),
+                 eng_->raw(), "jrq_table_update_gather");
+    throwIfError(jrq_table_epoch(table_, changed_.p, &n, nullptr), eng_->raw(), "jrq_table_epoch");
+  } catch (...) {
+    relistAfterFailure();
+    throw;
+  }
   const auto t2 = clk::now();
   // deliver: per changed group, under its lock, the commit BallotBox.commitAt makes
-  // (:130-134: drop ballots up to c, pendingIndex = c + 1, lastCommittedIndex = c); then,
-  // without the lock, its closures (ClosureQueue.popClosureUntil -> done.run(OK)) and
-  // waiter.onCommitted(c) (:137).  Groups are independent: split across threads, one group's
-  // callbacks on one thread, in order.  A commit touches several host arrays at random
-  // places: prefetch a few groups ahead.
-  parallelFor(n, 1u << 12, [&](unsigned, size_t i0, size_t i1) {
+  // (:130-134: drop ballots up to c, pendingIndex = c + 1, lastCommittedIndex = c) -- for
+  // every group of a worker's share first -- then, without the locks, its closures
+  // (ClosureQueue.popClosureUntil -> done.run(OK)) and waiter.onCommitted(c) (:137), group by
+  // group in order.  A callback that throws cannot leave a group half-applied: the host state
+  // then stays what the device table already holds (its pendingIndex follows lastCommitted),
+  // and the first exception is rethrown after every callback ran.  A commit touches one group
+  // record at a random place: prefetch a few groups ahead.
+  const size_t dparts = partsFor(n, 1u << 12);
+  if (deliveries_.size() < dparts) deliveries_.resize(dparts);
+  std::vector<std::exception_ptr> errs(dparts);
+  parallelFor(n, 1u << 12, [&](unsigned part, size_t i0, size_t i1) {
+    Delivery& D = deliveries_[part];
+    D.commits.clear();
+    D.done.clear();
+    D.ndone.clear();
+    constexpr size_t kAhead = 8;
+    for (size_t i = i0; i < i1; ++i) {
+      if (i + kAhead < i1) {
+        const uint32_t a = static_cast<uint32_t>(changed_.p[i + kAhead]);
+        __builtin_prefetch(rec_ + static_cast<size_t>(a) * stride_, 1);
+        __builtin_prefetch(&closures_[a], 0);
+        __builtin_prefetch(&waiter_[a], 0);
+      }
+      const uint64_t w = changed_.p[i];
+      const uint32_t g = static_cast<uint32_t>(w);
+      Guard lk(*this, g);
+      Hot& h = hot(g);
+      const int64_t c = h.pi - 1 + static_cast<int64_t>(w >> 32);
+      uint32_t nd0 = 0;
+      if (auto& q = closures_[g]) {
+        while (!q->empty() && q->front().first <= c) {
+          D.done.push_back(std::move(q->front().second));
+          q->pop_front();
+          ++nd0;
+        }
+      }
+      h.pi = c + 1;
+      h.lc = c;
+      dropDeadRuns(g);
+      D.commits.push_back(Delivery::Commit{c, &waiter_[g]});
+      D.ndone.push_back(nd0);
+    }
     struct Scope {
       const GroupBatch* prev;
       explicit Scope(const GroupBatch* b) : prev(tl_delivering) { tl_delivering = b; }
       ~Scope() { tl_delivering = prev; }
     } scope(this);
-    std::vector<std::function<void(bool)>> done;
-    constexpr size_t kAhead = 8;
-    for (size_t i = i0; i < i1; ++i) {
-      if (i + kAhead < i1) {
-        const uint32_t h = static_cast<uint32_t>(changed_.p[i + kAhead]);
-        __builtin_prefetch(&lock_[h], 1);
-        __builtin_prefetch(&pi_[h], 1);
-        __builtin_prefetch(&lc_[h], 1);
-        __builtin_prefetch(&nruns_[h], 0);
-        __builtin_prefetch(&closures_[h], 0);
-        __builtin_prefetch(&waiter_[h], 0);
-      }
-      const uint64_t w = changed_.p[i];
-      const uint32_t g = static_cast<uint32_t>(w);
-      int64_t c;
-      CommitWaiter waiter;
-      {
-        Guard lk(*this, g);
-        c = pi_[g] - 1 + static_cast<int64_t>(w >> 32);
-        if (auto& q = closures_[g]) {
-          while (!q->empty() && q->front().first <= c) {
-            done.push_back(std::move(q->front().second));
-            q->pop_front();
-          }
+    size_t k = 0;
+    for (size_t j = 0; j < D.commits.size(); ++j) {
+      for (uint32_t u = 0; u < D.ndone[j]; ++u, ++k) {
+        try {
+          D.done[k](true);
+        } catch (...) {
+          if (!errs[part]) errs[part] = std::current_exception();
         }
-        pi_[g] = c + 1;
-        lc_[g] = c;
-        dropDeadRuns(g);
-        if (waiter_[g]) waiter = waiter_[g];
       }
-      for (auto& f : done) f(true);
-      done.clear();
-      if (waiter) waiter(c);
+      try {
+        if (*D.commits[j].waiter) (*D.commits[j].waiter)(D.commits[j].c);
+      } catch (...) {
+        if (!errs[part]) errs[part] = std::current_exception();
+      }
     }
+    D.commits.clear();
+    D.done.clear();
   });
   flushes_.fetch_add(1, std::memory_order_relaxed);
   const auto t3 = clk::now();
@@ -762,6 +831,8 @@ uint32_t GroupBatch::flushLocked() {
   stats.device_ms = ms(t2 - t1);
   stats.deliver_ms = ms(t3 - t2);
   stats_ = stats;
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
   return n;
 }
 
@@ -787,23 +858,31 @@ void GroupBatch::startFlusher(const FlushPolicy& policy) {
           }
         }
         if (pending && (pending >= policy.maxDirtyGroups || nowNs() - oldest >= delayNs)) {
-          flush();
+          std::lock_guard<std::mutex> fl(flushMu_);
+          flushLocked();
         } else {
           std::this_thread::sleep_for(nap);
         }
       }
     } catch (const std::exception& ex) {
-      f->error = ex.what();
+      // the flusher stops; the error is rethrown by the next flush() or stopFlusher()
+      std::lock_guard<std::mutex> el(errMu_);
+      if (flusherError_.empty()) flusherError_ = ex.what();
     }
   });
 }
 
 void GroupBatch::stopFlusher() {
-  if (!flusher_) return;
-  flusher_->stop.store(true, std::memory_order_release);
-  if (flusher_->th.joinable()) flusher_->th.join();
-  const std::string err = flusher_->error;
-  flusher_.reset();
+  if (flusher_) {
+    flusher_->stop.store(true, std::memory_order_release);
+    if (flusher_->th.joinable()) flusher_->th.join();
+    flusher_.reset();
+  }
+  std::string err;
+  {
+    std::lock_guard<std::mutex> el(errMu_);
+    std::swap(err, flusherError_);
+  }
   if (!err.empty()) throw std::runtime_error("GroupBatch flusher: " + err);
 }
 
@@ -816,7 +895,7 @@ bool BallotBox::init(const BallotBoxOptions& opts) {
   GroupBatch& b = *batch_;
   GroupBatch::Guard lk(b, g_);
   b.waiter_[g_] = opts.waiter;
-  b.inited_[g_] = 1;
+  b.hot(g_).inited = 1;
   return true;
 }
 
@@ -824,16 +903,16 @@ bool BallotBox::commitAt(int64_t first, int64_t last, const PeerId& peer) {
   GroupBatch& b = *batch_;
   const uint32_t id = peerId(peer);
   GroupBatch::Guard lk(b, g_);
-  const int64_t pi = b.pi_[g_];
+  GroupBatch::Hot& h = b.hot(g_);
+  const int64_t pi = h.pi;
   if (pi == 0) return false;                                     // :101-103
   if (last < pi) return true;                                    // :104-106
-  if (last > b.la_[g_]) throw std::out_of_range("ArrayIndexOutOfBoundsException");  // :107-109
+  if (last > h.la) throw std::out_of_range("ArrayIndexOutOfBoundsException");  // :107-109
   const int s = b.slotOf(g_, id, true);
   // every slot is named by a live conf run and this peer by none: no pending ballot counts
   // it, so Ballot.grant finds nothing (Ballot.java:100-127) and commitAt returns true
   if (s < 0) return true;
-  const size_t k = static_cast<size_t>(g_) * b.P_ + s;
-  int64_t& m = b.match_[k];
+  int64_t& m = b.matchOf(g_)[s];
   const int64_t lo = std::max(m + 1, pi);
   if (first > lo && b.gapCountsPeer(g_, s, lo, first - 1))
     throw std::logic_error("non-contiguous ack: the Replicator never skips entries");
@@ -841,7 +920,7 @@ bool BallotBox::commitAt(int64_t first, int64_t last, const PeerId& peer) {
     m = last;
     b.markDirty(g_, 1u << s);
   }
-  b.slotUse_[k] = static_cast<uint32_t>(b.flushes_.load(std::memory_order_relaxed));
+  b.slotUseOf(g_)[s] = static_cast<uint32_t>(b.flushes_.load(std::memory_order_relaxed));
   return true;
 }
 
@@ -856,16 +935,19 @@ void BallotBox::clearPendingTasks() {
   bool decide;
   {
     GroupBatch::Guard lk(b, g_);
-    decide = (b.dirty_[g_] & 0xFFFFu) && b.pi_[g_] != 0 && b.eng_;
+    const GroupBatch::Hot& h = b.hot(g_);
+    decide = (h.dirty & 0xFFFFu) && h.pi != 0 && b.eng_;
   }
   if (decide) b.flushLocked();
   std::unique_ptr<std::deque<std::pair<int64_t, std::function<void(bool)>>>> q;
   {
     GroupBatch::Guard lk(b, g_);
+    GroupBatch::Hot& h = b.hot(g_);
     q = std::move(b.closures_[g_]);
-    b.nruns_[g_] = 0;
-    b.pi_[g_] = 0;
-    b.la_[g_] = -1;
+    h.nruns = 0;
+    h.lastConf = 0;
+    h.pi = 0;
+    h.la = -1;
     b.markDirty(g_, GroupBatch::kDirtyHeader);
   }
   if (q)
@@ -875,14 +957,15 @@ void BallotBox::clearPendingTasks() {
 bool BallotBox::resetPendingIndex(int64_t n) {
   GroupBatch& b = *batch_;
   GroupBatch::Guard lk(b, g_);
-  if (!(b.pi_[g_] == 0 && b.la_[g_] < b.pi_[g_])) return false;
-  if (n <= b.lc_[g_]) return false;
-  b.pi_[g_] = n;
-  b.la_[g_] = n - 1;
-  b.nruns_[g_] = 0;
+  GroupBatch::Hot& h = b.hot(g_);
+  if (!(h.pi == 0 && h.la < h.pi)) return false;
+  if (n <= h.lc) return false;
+  h.pi = n;
+  h.la = n - 1;
+  h.nruns = 0;
+  h.lastConf = 0;
   // a new leader's replicators start over
-  std::fill(b.match_.begin() + static_cast<size_t>(g_) * b.P_,
-            b.match_.begin() + static_cast<size_t>(g_ + 1) * b.P_, 0);
+  std::fill(b.matchOf(g_), b.matchOf(g_) + b.P_, 0);
   b.markDirty(g_, GroupBatch::kDirtyHeader | GroupBatch::kDirtyReset);
   return true;
 }
@@ -914,30 +997,32 @@ bool BallotBox::append(const Configuration& conf, const Configuration* oldConf, 
   for (size_t i = 0; i < nn; ++i) ids[i] = peerId(conf.peers[i]);
   for (size_t i = 0; i < no; ++i) ids[nn + i] = peerId(oldConf->peers[i]);
   GroupBatch::Guard lk(b, g_);
-  if (b.pi_[g_] <= 0) return false;  // :204-207
+  GroupBatch::Hot& h = b.hot(g_);
+  if (h.pi <= 0) return false;  // :204-207
   if (count <= 0) return true;
-  if (b.la_[g_] + count - b.pi_[g_] + 1 > INT32_MAX)  // pendingMetaQueue is a Java ArrayList
+  if (h.la + count - h.pi + 1 > INT32_MAX)  // pendingMetaQueue is a Java ArrayList
     throw std::length_error("pending queue larger than an ArrayList");
   const uint64_t cw = b.confWord(g_, ids, static_cast<uint32_t>(nn), static_cast<uint32_t>(no), oldConf != nullptr);
-  GroupBatch::Run* R = &b.runs_[static_cast<size_t>(g_) * JRQ_TABLE_MAX_RUNS];
-  uint8_t& n = b.nruns_[g_];
-  const int64_t idx = b.la_[g_] + 1;
-  if (n == 0 || R[n - 1].conf != cw) {  // Ballot.init with a new conf: a new conf run
+  const int64_t idx = h.la + 1;
+  if (h.nruns == 0 || h.lastConf != cw) {  // Ballot.init with a new conf: a new conf run
+    GroupBatch::Run* R = &b.runs_[static_cast<size_t>(g_) * JRQ_TABLE_MAX_RUNS];
+    uint8_t& n = h.nruns;
     if (n == JRQ_TABLE_MAX_RUNS) {
-      if (idx > b.pi_[g_])  // NodeImpl never has more than 2 (joint, then stable) pending
+      if (idx > h.pi)  // NodeImpl never has more than 2 (joint, then stable) pending
         throw std::length_error("more conf runs pending than JRQ_TABLE_MAX_RUNS");
       n = 0;  // the queue is empty: every earlier run is dead
     }
     R[n++] = GroupBatch::Run{idx, cw};
+    h.lastConf = cw;
     b.dropDeadRuns(g_);
     b.markDirty(g_, GroupBatch::kDirtyHeader);
   }
-  b.la_[g_] = idx + count - 1;
+  h.la = idx + count - 1;
   b.markDirty(g_, GroupBatch::kDirtyLa);
   if (done) {  // ClosureQueue.appendPendingClosure (ClosureQueueImpl.java:98-105)
     auto& q = b.closures_[g_];
     if (!q) q.reset(new std::deque<std::pair<int64_t, std::function<void(bool)>>>());
-    q->emplace_back(b.la_[g_], std::move(*done));
+    q->emplace_back(h.la, std::move(*done));
   }
   return true;
 }
@@ -947,16 +1032,17 @@ bool BallotBox::setLastCommittedIndex(int64_t c) {
   CommitWaiter w;
   {
     GroupBatch::Guard lk(b, g_);
-    if (b.pi_[g_] != 0 || b.la_[g_] >= b.pi_[g_]) {
-      if (!(c < b.pi_[g_]))  // Requires.requireTrue (:229-231)
+    GroupBatch::Hot& h = b.hot(g_);
+    if (h.pi != 0 || h.la >= h.pi) {
+      if (!(c < h.pi))  // Requires.requireTrue (:229-231)
         throw std::invalid_argument("Node changes to leader, pendingIndex=" +
-                                    std::to_string(b.pi_[g_]) +
+                                    std::to_string(h.pi) +
                                     ", param lastCommittedIndex=" + std::to_string(c));
       return false;
     }
-    if (c < b.lc_[g_]) return false;
-    if (c == b.lc_[g_]) return true;
-    b.lc_[g_] = c;
+    if (c < h.lc) return false;
+    if (c == h.lc) return true;
+    h.lc = c;
     b.markDirty(g_, GroupBatch::kDirtyHeader);
     w = b.waiter_[g_];
   }
@@ -966,16 +1052,17 @@ bool BallotBox::setLastCommittedIndex(int64_t c) {
 
 int64_t BallotBox::getLastCommittedIndex() const {
   GroupBatch::Guard lk(*batch_, g_);
-  return batch_->lc_[g_];
+  return batch_->hot(g_).lc;
 }
 int64_t BallotBox::getPendingIndex() const {
   GroupBatch::Guard lk(*batch_, g_);
-  return batch_->pi_[g_];
+  return batch_->hot(g_).pi;
 }
 int64_t BallotBox::getPendingMetaQueueSize() const {
   const GroupBatch& b = *batch_;
   GroupBatch::Guard lk(b, g_);
-  return b.pi_[g_] == 0 ? 0 : b.la_[g_] - b.pi_[g_] + 1;
+  const GroupBatch::Hot& h = b.hot(g_);
+  return h.pi == 0 ? 0 : h.la - h.pi + 1;
 }
 
 std::string BallotBox::describe() const {
@@ -983,9 +1070,10 @@ std::string BallotBox::describe() const {
   {
     const GroupBatch& b = *batch_;
     GroupBatch::Guard lk(b, g_);
-    lc = b.lc_[g_];
-    pi = b.pi_[g_];
-    q = pi == 0 ? 0 : b.la_[g_] - pi + 1;
+    const GroupBatch::Hot& h = b.hot(g_);
+    lc = h.lc;
+    pi = h.pi;
+    q = pi == 0 ? 0 : h.la - pi + 1;
   }
   std::ostringstream o;
   o << "  lastCommittedIndex: " << lc << "\n"

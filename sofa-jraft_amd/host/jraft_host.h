@@ -28,6 +28,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -37,34 +38,41 @@ namespace jraft {
 
 // ------------------------------------------------------------------ entities
 
-struct PeerId {
-  std::string ip;
-  int32_t port = 0;
-  int32_t idx = 0;
-  // Interning cache: the process-wide id of this peer (0 = not looked up yet), like the hash a
-  // Java String caches.  Checked against the interned value on use, so changing ip/port/idx
-  // afterwards is safe; written with atomics, so one PeerId may be shared by threads.
-  mutable std::atomic<uint32_t> internId{0};
+// Immutable once built, as the reference's PeerId is in use (its fields are private and only
+// parse() sets them, PeerId.java:150-170): the interned id cached in it then never goes stale,
+// and a BallotBox call resolves its peer with one load.
+class PeerId {
+  std::string ip_;
+  int32_t port_ = 0;
+  int32_t idx_ = 0;
+
+ public:
   PeerId() = default;
-  PeerId(std::string ip_, int32_t port_, int32_t idx_ = 0) : ip(std::move(ip_)), port(port_), idx(idx_) {}
-  PeerId(const PeerId& o) : ip(o.ip), port(o.port), idx(o.idx), internId(o.internId.load(std::memory_order_relaxed)) {}
+  PeerId(std::string ip, int32_t port, int32_t idx = 0) : ip_(std::move(ip)), port_(port), idx_(idx) {}
+  PeerId(const PeerId& o) : ip_(o.ip_), port_(o.port_), idx_(o.idx_), internId(o.internId.load(std::memory_order_relaxed)) {}
   PeerId(PeerId&& o) noexcept
-      : ip(std::move(o.ip)), port(o.port), idx(o.idx), internId(o.internId.load(std::memory_order_relaxed)) {}
+      : ip_(std::move(o.ip_)), port_(o.port_), idx_(o.idx_), internId(o.internId.load(std::memory_order_relaxed)) {}
   PeerId& operator=(const PeerId& o) {
-    ip = o.ip;
-    port = o.port;
-    idx = o.idx;
+    ip_ = o.ip_;
+    port_ = o.port_;
+    idx_ = o.idx_;
     internId.store(o.internId.load(std::memory_order_relaxed), std::memory_order_relaxed);
     return *this;
   }
+  const std::string& getIp() const { return ip_; }
+  int32_t getPort() const { return port_; }
+  int32_t getIdx() const { return idx_; }
   // PeerId.toString (PeerId.java:135-144): ip:port[:idx]
   std::string toString() const;
-  // PeerId.parse (PeerId.java:150-170): "ip:port" or "ip:port:idx"
+  // PeerId.parse (PeerId.java:150-170): "ip:port" or "ip:port:idx"; resets the interned id
   static bool parse(const std::string& s, PeerId* out);
-  bool operator==(const PeerId& o) const { return ip == o.ip && port == o.port && idx == o.idx; }
+  bool operator==(const PeerId& o) const { return ip_ == o.ip_ && port_ == o.port_ && idx_ == o.idx_; }
   bool operator<(const PeerId& o) const {
-    return ip != o.ip ? ip < o.ip : (port != o.port ? port < o.port : idx < o.idx);
+    return ip_ != o.ip_ ? ip_ < o.ip_ : (port_ != o.port_ ? port_ < o.port_ : idx_ < o.idx_);
   }
+  // The process-wide id of this peer (0 = not looked up yet), like the hash a Java String
+  // caches; written with atomics, so one PeerId may be shared by threads.
+  mutable std::atomic<uint32_t> internId{0};
 };
 
 struct Configuration {
@@ -173,7 +181,8 @@ class GroupBatch;
 class BallotBox {
  public:
   BallotBox(std::shared_ptr<GroupBatch> batch, uint32_t group);
-  bool init(const BallotBoxOptions& opts);                                     // :82-90
+  // :82-90 -- once, before the group's first ack (the reference's waiter is final)
+  bool init(const BallotBoxOptions& opts);
   // :96-139 -- false if not leader; true if last < pendingIndex (stale); throws
   // std::out_of_range when last >= pendingIndex + queue size; otherwise records the ack,
   // decided at the next GroupBatch::flush().  Any peer may ack (a catch-up replicator of a
@@ -252,7 +261,10 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   uint32_t peers() const { return P_; }
   // One epoch: upload what changed, evaluate every group on the GPU, advance
   // pendingIndex / lastCommittedIndex, drop committed ballots, run closures, call waiters.
-  // Returns the number of groups whose commit index advanced.
+  // Returns the number of groups whose commit index advanced.  Every changed group's state
+  // moves before any callback runs; an exception a callback throws is rethrown after all of
+  // them ran.  If the upload or the epoch fails, the groups it carried are shipped again (in
+  // full) by the next flush.  Rethrows, once, the error that stopped the background flusher.
   uint32_t flush();
   // Stats of the last flush (read them from the thread that flushed, or after stopFlusher).
   const FlushStats& lastFlush() const { return stats_; }
@@ -260,6 +272,11 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   void startFlusher(const FlushPolicy& policy);
   void stopFlusher();
   uint64_t flushCount() const { return flushes_.load(std::memory_order_relaxed); }
+  // Dirty lists of this batch (one per thread that ever changed one of its groups).
+  size_t dirtyLists() {
+    std::lock_guard<std::mutex> l(listsMu_);
+    return lists_.size();
+  }
   // Threads flush() packs and delivers on (default: the CPUs this process may use, cgroup
   // quota included, at most 16).
   void setFlushThreads(unsigned n);
@@ -284,11 +301,37 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   struct Pool;
   struct Flusher;
   struct Part;       // one pack worker's share of a flush
+  struct Delivery;   // one deliver worker's commits and callbacks
   static constexpr uint32_t kNoPeer = 0xFFFFFFFFu;
   static constexpr uint32_t kDirtyLa = 1u << 16, kDirtyHeader = 1u << 17, kDirtyReset = 1u << 18;
 
+  // One group's record: what every API call and the flush touch, in one or two adjacent cache
+  // lines (128 B at P = 5) instead of a word in each of nine arrays: the hot header, then
+  // match[P] (int64, highest index acked per slot), slotPeer[P] (u32, interned PeerId of the
+  // slot), slotUse[P] (u32, flush count of the slot's last ack).  Its conf runs live apart
+  // (runs_: read when a conf changes or a run dies).
+  struct Hot {
+    std::atomic<uint8_t> lock;  // the group's one-byte spin lock
+    uint8_t nruns;              // conf runs of the pending queue
+    uint8_t inited;
+    uint8_t pad;
+    uint32_t dirty;             // slots / lastAppended / header changed since the last pack
+    int64_t pi, lc, la;         // pendingIndex, lastCommittedIndex, lastAppended
+    uint64_t lastConf;          // conf word of the last run (appends compare against it)
+  };
+  Hot& hot(uint32_t g) const { return *reinterpret_cast<Hot*>(rec_ + static_cast<size_t>(g) * stride_); }
+  int64_t* matchOf(uint32_t g) const {
+    return reinterpret_cast<int64_t*>(rec_ + static_cast<size_t>(g) * stride_ + sizeof(Hot));
+  }
+  uint32_t* slotPeerOf(uint32_t g) const {
+    return reinterpret_cast<uint32_t*>(rec_ + static_cast<size_t>(g) * stride_ + sizeof(Hot) + 8 * P_);
+  }
+  uint32_t* slotUseOf(uint32_t g) const {
+    return reinterpret_cast<uint32_t*>(rec_ + static_cast<size_t>(g) * stride_ + sizeof(Hot) + 12 * P_);
+  }
+
   void lock(uint32_t g) const;
-  void unlock(uint32_t g) const { lock_[g].store(0, std::memory_order_release); }
+  void unlock(uint32_t g) const { hot(g).lock.store(0, std::memory_order_release); }
   struct Guard {  // the group's lock for a scope
     const GroupBatch& b;
     uint32_t g;
@@ -307,32 +350,27 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   DirtyList* myDirtyList();
   uint32_t flushLocked();
   void packRange(Part& part, const uint32_t* groups, size_t n);
+  void relistAfterFailure();
   size_t partsFor(size_t n, size_t grain);
   template <class F>
   void parallelFor(size_t n, size_t grain, F&& f);
 
   Engine* eng_;
   uint32_t G_, P_;
+  size_t stride_;                         // bytes per group record (a multiple of 64)
+  unsigned char* rec_ = nullptr;          // [G] group records (64-B aligned)
   const uint64_t serial_;                 // process-unique id (thread-local list caches)
-  std::unique_ptr<std::atomic<uint8_t>[]> lock_;  // [G] group locks
-  std::vector<int64_t> pi_, lc_, la_;     // pendingIndex, lastCommittedIndex, lastAppended
   std::vector<Run> runs_;                 // [G][JRQ_TABLE_MAX_RUNS] conf runs of the queue
-  std::vector<uint8_t> nruns_;
-  std::vector<uint32_t> slotPeer_;        // [G][P] interned PeerId of each slot
-  std::vector<uint32_t> slotUse_;         // [G][P] flush count of the slot's last ack
-  std::vector<int64_t> match_;            // [G][P] highest acked index per slot
-  std::vector<uint32_t> dirty_;           // [G] slots / lastAppended / header changed
   std::vector<CommitWaiter> waiter_;
-  std::vector<uint8_t> inited_;
   // ClosureQueue (ClosureQueueImpl.java): only non-null closures, per group, in index order
   std::vector<std::unique_ptr<std::deque<std::pair<int64_t, std::function<void(bool)>>>>> closures_;
   std::mutex listsMu_;                    // the per-thread dirty lists
   std::vector<std::unique_ptr<DirtyList>> lists_;
-  std::atomic<uint64_t> dirtyCount_{0};   // groups marked since the last swap (flusher policy)
-  std::atomic<int64_t> oldestDirtyNs_{0}; // steady_clock time of the first mark since the swap
+  std::unordered_map<std::thread::id, DirtyList*> byThread_;  // one list per calling thread
   std::mutex flushMu_;                    // one flush at a time
   std::vector<std::vector<uint32_t>> work_;  // swapped-out dirty lists (buffers kept)
   std::vector<Part> parts_;
+  std::vector<Delivery> deliveries_;
   jrq_table* table_ = nullptr;
   PinnedBuf<uint64_t> changed_;
   std::atomic<uint64_t> flushes_{0};
@@ -340,6 +378,8 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   std::unique_ptr<Pool> pool_;
   unsigned poolSize_ = 0;
   std::unique_ptr<Flusher> flusher_;
+  std::mutex errMu_;
+  std::string flusherError_;              // what stopped the background flusher (rethrown once)
 };
 
 }  // namespace jraft

@@ -10,6 +10,7 @@
 // never built into libjrq.so, libjraft_host.so or anything bench.py or smoke() loads; the GPU
 // build of the same tests (tests/_build/host_test) links the real library.
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -104,9 +105,19 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
 }
 void jrq_table_destroy(jrq_table* t) { delete t; }
 
+// Failure injection for the host tests (tests/cpp/host_test.cpp testFlushFailureRelists): the
+// next `n` update calls fail as a lost device would, after applying nothing.
+static std::atomic<int> g_fail_updates{0};
+void fake_jrq_fail_updates(int n) { g_fail_updates.store(n); }
+
 int jrq_table_update_gather(jrq_table* t, uint32_t parts, const jrq_group_state* const* states,
                             const uint32_t* n_states, const uint64_t* const* recs,
                             const uint32_t* n_recs) {
+  if (g_fail_updates.load() > 0) {
+    g_fail_updates.fetch_sub(1);
+    t->e->err = "injected update failure";
+    return JRQ_E_HIP;
+  }
   std::lock_guard<std::mutex> l(t->mu);
   for (uint32_t i = 0; i < parts; ++i)  // headers of every part first (include/jrq.h)
     for (uint32_t k = 0; k < n_states[i]; ++k) {

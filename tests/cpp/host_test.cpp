@@ -24,6 +24,10 @@
 
 using namespace jraft;
 
+// Failure injection, present only in the sanitizer builds' test double (tests/cpp/fake_jrq.cpp):
+// the next n jrq_table_update_gather calls fail.  Null against the real libjrq.so.
+extern "C" void fake_jrq_fail_updates(int n) __attribute__((weak));
+
 static int g_fail = 0, g_pass = 0;
 #define CHECK(c)                                                               \
   do {                                                                         \
@@ -690,6 +694,112 @@ static void testReentrantFlushRefused(Engine& eng) {
   CHECK(b.getPendingMetaQueueSize() == 1);
 }
 
+// an upload that fails after flush() swapped the dirty lists out must not strand
+// the groups it carried -- the pack had cleared their dirty bits.  The next flush ships them
+// again and every group commits.
+static void testFlushFailureRelists(Engine& eng) {
+  if (!fake_jrq_fail_updates) return;  // (the real library has no failure injection)
+  const uint32_t G = 300;
+  auto batch = std::make_shared<GroupBatch>(&eng, G, 3);
+  std::vector<BallotBox> boxes;
+  std::vector<Waiter> ws(G);
+  for (uint32_t g = 0; g < G; ++g) {
+    boxes.emplace_back(batch, g);
+    CHECK(boxes[g].init({ws[g].fn()}));
+    CHECK(boxes[g].resetPendingIndex(1));
+    CHECK(boxes[g].appendPendingTasks(conf("a:1,b:2,c:3"), nullptr, 4));
+  }
+  batch->flush();  // the headers
+  for (uint32_t g = 0; g < G; ++g) {
+    boxes[g].commitAt(1, 3, PeerId("a", 1));
+    boxes[g].commitAt(1, 2 + g % 2, PeerId("b", 2));
+  }
+  fake_jrq_fail_updates(1);
+  CHECK(throws<std::runtime_error>([&] { batch->flush(); }));
+  for (uint32_t g = 0; g < G; ++g) CHECK(boxes[g].getLastCommittedIndex() == 0);
+  CHECK(batch->flush() == G);  // re-shipped in full: every group commits
+  for (uint32_t g = 0; g < G; ++g) {
+    CHECK(boxes[g].getLastCommittedIndex() == 2 + g % 2);
+    CHECK(ws[g].calls.size() == 1 && ws[g].calls[0] == 2 + g % 2);
+  }
+  // and the state stays in step: a further ack commits exactly once more
+  for (uint32_t g = 0; g < G; ++g) boxes[g].commitAt(3 + g % 2, 4, PeerId("b", 2));
+  boxes[0].commitAt(4, 4, PeerId("a", 1));
+  batch->flush();
+  CHECK(boxes[0].getLastCommittedIndex() == 4);
+  for (uint32_t g = 1; g < G; ++g) CHECK(boxes[g].getLastCommittedIndex() == 3);
+}
+
+// a callback that throws must not leave the other groups of the epoch half
+// delivered.  Every group's commit is applied before any callback runs, the exception comes
+// back from flush() after all of them ran, and the next epoch decides from the right state
+// (no false commit from a stale pendingIndex).
+static void testThrowingCallback(Engine& eng) {
+  const uint32_t G = 64;
+  auto batch = std::make_shared<GroupBatch>(&eng, G, 3);
+  std::vector<BallotBox> boxes;
+  std::vector<Waiter> ws(G);
+  for (uint32_t g = 0; g < G; ++g) {
+    boxes.emplace_back(batch, g);
+    if (g == 7)
+      CHECK(boxes[g].init({[](int64_t) { throw std::runtime_error("callback failed"); }}));
+    else
+      CHECK(boxes[g].init({ws[g].fn()}));
+    CHECK(boxes[g].resetPendingIndex(1));
+    CHECK(boxes[g].appendPendingTasks(conf("a:1,b:2,c:3"), nullptr, 10));
+  }
+  int closures = 0;
+  CHECK(boxes[9].appendPendingTask(conf("a:1,b:2,c:3"), nullptr, [&](bool ok) {
+    if (ok) ++closures;
+    throw std::logic_error("closure failed");
+  }));
+  for (uint32_t g = 0; g < G; ++g) {
+    boxes[g].commitAt(1, 5, PeerId("a", 1));
+    boxes[g].commitAt(1, 5, PeerId("b", 2));
+  }
+  bool threw = false;
+  try {
+    batch->flush();
+  } catch (const std::exception&) {
+    threw = true;  // the first of the callbacks' exceptions, after all of them ran
+  }
+  CHECK(threw);
+  for (uint32_t g = 0; g < G; ++g) {
+    CHECK(boxes[g].getLastCommittedIndex() == 5);
+    CHECK(boxes[g].getPendingIndex() == 6);
+    if (g != 7) CHECK(ws[g].calls.size() == 1 && ws[g].calls[0] == 5);
+  }
+  // entry 11 of group 9 (its closure) is not committed yet: nothing popped
+  CHECK(closures == 0);
+  for (uint32_t g = 0; g < G; ++g) boxes[g].commitAt(6, 7, PeerId("a", 1));
+  boxes[3].commitAt(6, 6, PeerId("c", 3));
+  try {
+    batch->flush();
+  } catch (const std::exception&) {
+  }
+  CHECK(boxes[3].getLastCommittedIndex() == 6);
+  for (uint32_t g = 0; g < G; ++g)
+    if (g != 3) CHECK(boxes[g].getLastCommittedIndex() == 5);
+}
+
+// a thread alternating between many batches keeps one dirty list per batch.
+static void testManyBatchesOneThread(Engine& eng) {
+  std::vector<std::shared_ptr<GroupBatch>> batches;
+  std::vector<BallotBox> boxes;
+  for (int i = 0; i < 9; ++i) {
+    batches.push_back(std::make_shared<GroupBatch>(&eng, 4, 3));
+    for (uint32_t g = 0; g < 4; ++g) {
+      boxes.emplace_back(batches.back(), g);
+      Waiter w;
+      CHECK(boxes.back().init({[](int64_t) {}}));
+      CHECK(boxes.back().resetPendingIndex(1));
+    }
+  }
+  for (int round = 0; round < 50; ++round)
+    for (auto& b : boxes) CHECK(b.appendPendingTasks(conf("a:1,b:2,c:3"), nullptr, 1));
+  for (auto& b : batches) CHECK(b->dirtyLists() == 1);
+}
+
 int main(int argc, char** argv) {
   // "gpu": with an engine (the real libjrq.so on the GPU box; the sanitizer builds link the
   // test double tests/cpp/fake_jrq.cpp instead and run the same list on the CPU)
@@ -726,6 +836,9 @@ int main(int argc, char** argv) {
     // > 8192 changed groups per epoch: flush() packs and delivers on several threads
     tests.push_back({"testConcurrentCallersWide", [&] { testConcurrentCallers(e, 20000, 48); }});
     tests.push_back({"testReentrantFlushRefused", [&] { testReentrantFlushRefused(e); }});
+    tests.push_back({"testFlushFailureRelists", [&] { testFlushFailureRelists(e); }});
+    tests.push_back({"testThrowingCallback", [&] { testThrowingCallback(e); }});
+    tests.push_back({"testManyBatchesOneThread", [&] { testManyBatchesOneThread(e); }});
   }
   for (auto& t : tests) {
     const int before = g_fail;
