@@ -31,6 +31,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <exception>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -163,7 +164,15 @@ int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t 
       if (!confs.count(conf_a[g])) confs.emplace(conf_a[g], confsOfWord(conf_a[g]));
       if (switch_at && switch_at[g] > 0 && !confs.count(conf_b[g])) confs.emplace(conf_b[g], confsOfWord(conf_b[g]));
     }
+    // the callers' own state, group-major (a Replicator keeps its peer's matchIndex; here one
+    // row per group of the P peers' acks per epoch and of their previous acks), laid out before
+    // the timed calls so that the timing is the API's, not a strided walk of the input series
     std::vector<int64_t> prev(static_cast<size_t>(P) * G, 0);
+    std::vector<int64_t> acks(static_cast<size_t>(K) * G * P);
+    for (uint32_t k = 0; k < K; ++k)
+      for (uint32_t p = 0; p < P; ++p)
+        for (uint32_t g = 0; g < G; ++g)
+          acks[(static_cast<size_t>(k) * G + g) * P + p] = match[(static_cast<size_t>(k) * P + p) * G + g];
     auto append = [&](uint32_t g, int64_t from, int64_t to) -> uint64_t {  // entries [from, to]
       uint64_t calls = 0;
       const int64_t sw = switch_at ? switch_at[g] : 0;
@@ -187,7 +196,7 @@ int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t 
     for (uint32_t k = 0; k < K; ++k) {
       const auto t0 = clk::now();
       const int64_t* lak = la + static_cast<size_t>(k) * G;
-      const int64_t* mk = match + static_cast<size_t>(k) * P * G;
+      const int64_t* ak = acks.data() + static_cast<size_t>(k) * G * P;
       workers.run([&](unsigned t) {
         uint64_t n = 0;
         const uint32_t g0 = static_cast<uint32_t>(static_cast<uint64_t>(G) * t / T);
@@ -203,8 +212,8 @@ int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t 
             if (lak[g] > lp) n += append(g, lp + 1, lak[g]);
           }
           for (uint32_t p = 0; p < P; ++p) {
-            const int64_t m = mk[static_cast<size_t>(p) * G + g];
-            int64_t& pv = prev[static_cast<size_t>(p) * G + g];
+            const int64_t m = ak[static_cast<size_t>(g) * P + p];
+            int64_t& pv = prev[static_cast<size_t>(g) * P + p];
             if (k == 0) pv = m < pi0[g] ? m : pi0[g] - 1;
             if (m > pv) {
               boxes[g].commitAt(pv + 1, m, peers[p]);
@@ -301,6 +310,23 @@ int jraft_drive_latency(int device, uint32_t G, uint32_t P, uint32_t threads, ui
         std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
         stop.store(true);
       });
+      // a producer's exception (rethrown by workers.run) must still stop and join the timer and
+      // the flusher before it leaves: a joinable std::thread destroyed would call terminate
+      struct Join {
+        std::atomic<bool>& stop;
+        std::thread& timer;
+        jraft::GroupBatch& batch;
+        ~Join() {
+          stop.store(true);
+          if (timer.joinable()) timer.join();
+          if (std::uncaught_exceptions() > 0) {  // (the normal path stops it below, rethrowing)
+            try {
+              batch.stopFlusher();
+            } catch (...) {
+            }
+          }
+        }
+      } join{stop, timer, *batch};
       workers.run([&](unsigned t) {
         const uint32_t g0 = static_cast<uint32_t>(static_cast<uint64_t>(G) * t / T);
         const uint32_t g1 = static_cast<uint32_t>(static_cast<uint64_t>(G) * (t + 1) / T);
@@ -337,7 +363,7 @@ int jraft_drive_latency(int device, uint32_t G, uint32_t P, uint32_t threads, ui
       });
       timer.join();
     }
-    batch->stopFlusher();
+    batch->stopFlusher();  // rethrows an error that stopped the flusher
     batch->flush();
     const double secs = (nowNs() - t0) * 1e-9;
     std::vector<float> all;
