@@ -739,7 +739,10 @@ def leg_c2(ctx, args):
     def c2_step(i):
         c2_launch()
     one_ms, one_wall = ctx.timed(c2_step)
-    KE = 64
+    # the product default for a batch this small (< ~50k groups): 256 epochs per launch, which
+    # spreads the scan kernel's launch ramp and tail over 256 epochs; 64 epochs
+    # per launch are the C2L leg
+    KE = 256
     ser = W.quorum_epoch_series("C2", KE)
     ser_d = {k: to_dev(v, dev) for k, v in ser.items()}
     kc = torch.empty((KE, G2), dtype=torch.int64, device=dev)
@@ -755,8 +758,8 @@ def leg_c2(ctx, args):
     ok = None
     if ctx.oracle_checks:
         import jraft_oracle as O
-    if ctx.oracle_checks:  # the oracle on 256 groups, all KE epochs, state carried
-        sub = np.random.default_rng(2).choice(G2, 256, replace=False)
+    if ctx.oracle_checks:  # the oracle on 128 groups, all KE epochs, state carried
+        sub = np.random.default_rng(2).choice(G2, 128, replace=False)
         pi = ser["pending_index"][sub].copy()
         lc = ser["last_committed"][sub].copy()
         got = kc.cpu().numpy()
@@ -778,19 +781,20 @@ def leg_c2(ctx, args):
                                "decisions_per_s": G2 * KE / (k_ms * 1e-3),
                                "roofline": roofline(alg, k_ms, kernel="quorum_epochs_kernel<3>",
                                                     **pmc_traffic("C2", "quorum_epochs_kernel<3,")),
-                               "bit_exact_vs_oracle_256_groups": ok}}
+                               "bit_exact_vs_oracle_128_groups": ok}}
 
 
 def leg_c2l(ctx, args):
-    """configs[1] with 256 successive epochs per launch (jrq_quorum_epochs_dev): the scan
-    kernel's ramp and tail spread over 4x the work of the 64-epoch launch.  Its own leg, so its
-    PMC pass (one leg per pass) attributes this launch shape's bytes to it alone."""
+    """configs[1] with 64 successive epochs per launch (jrq_quorum_epochs_dev), beside the C2
+    leg's 256 (the product default): the scan kernel's ramp and tail over a quarter of the work.
+    Its own leg, so its PMC pass (one leg per pass) attributes this launch shape's bytes to it
+    alone."""
     import torch
 
     from jraft_amd import workloads as W
     eng, dev = ctx.eng, ctx.dev
     G2 = W.quorum_batch("C2")["pending_index"].shape[0]
-    KL = 256
+    KL = 64
     serl = W.quorum_epoch_series("C2", KL)
     serl_d = {k: to_dev(v, dev) for k, v in serl.items()}
     klc = torch.empty((KL, G2), dtype=torch.int64, device=dev)
@@ -1442,8 +1446,8 @@ def compact_line(full: dict, detail_path: str | None = DETAIL_FILE) -> dict:
     if c2.get("batched_epochs"):
         legs["C2_epochs"] = _leg_summary(c2["batched_epochs"], "kernel_ms")
         legs["C2_epochs"]["epochs"] = c2["batched_epochs"].get("epochs_per_launch")
-    if c2.get("batched_epochs_256"):
-        legs["C2_epochs_256"] = _leg_summary(c2["batched_epochs_256"], "kernel_ms")
+    if c2.get("batched_epochs_64"):
+        legs["C2_epochs_64"] = _leg_summary(c2["batched_epochs_64"], "kernel_ms")
     if full.get("C3_k_epochs"):
         legs["C3_k_epochs"] = _leg_summary(full["C3_k_epochs"], "kernel_ms")
     if crc:
@@ -1590,7 +1594,7 @@ def main():
     if "C2" in legs:
         line["C2"] = leg_c2(ctx, args)
     if "C2L" in legs:
-        line.setdefault("C2", {})["batched_epochs_256"] = leg_c2l(ctx, args)
+        line.setdefault("C2", {})["batched_epochs_64"] = leg_c2l(ctx, args)
     if "C3K" in legs:
         line["C3_k_epochs"] = leg_c3k(ctx, args, G)
     extras = {}

@@ -37,6 +37,10 @@ for s in $STEPS; do
              run pmc_${leg}_RDREQ 180 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum -d gpurun_out/pmc_${leg}_RDREQ -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs $leg
            done ;;
     host)  run host_test 300 ./tests/_build/host_test gpu ;;
+    legtrace) # one kernel trace per bench leg (tools/leg_traces.py -> profiles/<tag>_leg_kernels.json)
+           for leg in ${TRACE_LEGS:-quorum table C2 C2L C3K C5 C1 ae v2 snapshot lease fanout}; do
+             run legtrace_$leg 180 rocprofv3 --kernel-trace -d gpurun_out/legtrace_$leg -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu --legs $leg
+           done ;;
     tsel)  run tests_${TAG:-sel} 900 python -u -m pytest ${TESTS:-tests/test_gpu_table.py} -x -q -p no:cacheprovider --timeout 240 --timeout-method thread ;;
     bsel)  run bench_${TAG:-sel} 600 python bench.py --steps 20 --warmup 5 --no-cpu --legs ${BENCH_LEGS:-quorum} --detail gpurun_out/bench_${TAG:-sel}_detail.json ;;
     tprobe) run table_probe 120 ./tools/table_probe ;;
