@@ -960,7 +960,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   const uintptr_t pbase = reinterpret_cast<uintptr_t>(a.payload);
   // kStarts: the row's base (its first piece) and each owner's offset from it, through
   // __shfl (the load of lane 16q + c reads owner 16q + c's piece); a new row costs a load
-  // Byte-misaligned 16-B loads stream at ~60 % of the aligned rate (tools/unal_probe.hip) and
+  // Byte-misaligned 16-B loads stream at ~60 % of the aligned rate (round 3's tools/unal_probe.hip) and
   // 64-B halves across two lines double the L2 requests: a piece starting at byte b of a 64-B
   // line is hashed over [start - b, start - b + PS) (same ring, aligned loads) and corrected
   // after the loop (the b bytes before it and the b bytes it missed, by linearity); the

@@ -8,7 +8,7 @@
 // + 16)): .sgpr_count <= 80 keeps 8, 82..96 gives 7, while the compiler's occupancy model
 // (and its `Occupancy` remark) still says 8 -- so a 1024-thread workgroup at 96 SGPRs runs 1
 // workgroup per CU, not 2 (table_epoch_kernel<5>: 24.2 -> 20.3 us per 1M groups,
-// tools/table_probe.hip).  amdgpu_num_sgpr(n) yields .sgpr_count = n - 2.
+// round 3's tools/table_probe.hip).  amdgpu_num_sgpr(n) yields .sgpr_count = n - 2.
 #define JRQ_SGPRS(n) __attribute__((amdgpu_num_sgpr(n)))
 #define JRQ_SGPRS_8WAVES JRQ_SGPRS(82)
 

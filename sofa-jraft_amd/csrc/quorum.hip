@@ -97,7 +97,7 @@ __device__ __forceinline__ i64x2 ld2nt(const int64_t* p) {
 // stream is read with 16-byte non-temporal loads (1 KiB per wave instruction; each input is
 // read once per epoch, so it is not kept in L2 / MALL) and the two status bytes are stored as
 // one 16-bit word.  512-thread workgroups: 256 and 1024 measured 6-8 % slower on C3
-// (tools/table_probe.hip).
+// (round 3's round 3's tools/table_probe.hip).
 // kRuns (run tables given): a group flagged JRQ_CONF_RUNS (a conf change inside its pending
 // window) is skipped by the single-conf decision and walked by its own wave afterwards, four
 // lanes per group (runs r, r + 4, ... on lane r of the quad, candidates max-reduced over the
@@ -108,7 +108,7 @@ __device__ __forceinline__ i64x2 ld2nt(const int64_t* p) {
 // every store of the fast path -- and reloaded them.  Without run tables the kernel is the
 // kRuns = false instantiation: no LDS, no walk.
 // The single-conf decision runs in 32-bit arithmetic relative to pendingIndex
-// (decide_single_rel, quorum_core.h: C3 16.4 -> 15.6 us per epoch in tools/pair_probe.hip,
+// (decide_single_rel, quorum_core.h: C3 16.4 -> 15.6 us per epoch in round 3's tools/pair_probe.hip,
 // against 15.1 us for the loads and stores alone).
 constexpr uint32_t kPairBlock = 512;
 
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(64 * W) void quorum_epochs_kernel(JrqQuorumArgs a, 
   const uint32_t nchunks = (blockDim.x >> 6) * kPerWave;
   // tiles in XCD-contiguous order: workgroups are dealt round-robin to the 8 XCDs, so block b
   // takes tile (b % 8)'s run position b / 8 -- the tiles that share DRAM pages (8 per 2 KiB of
-  // a row) then go out from one XCD back to back (-4 %, tools/epochs_probe.hip mode 4)
+  // a row) then go out from one XCD back to back (-4 %, round 3's tools/epochs_probe.hip mode 4)
   const uint32_t nb = gridDim.x, xq = nb / 8, xr = nb % 8, xcd = blockIdx.x % 8;
   const uint32_t tile = xcd * xq + (xcd < xr ? xcd : xr) + blockIdx.x / 8;
   const uint32_t g = tile * T + gl;

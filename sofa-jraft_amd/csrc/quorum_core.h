@@ -94,7 +94,7 @@ __device__ __forceinline__ void decide_single(int64_t pi, int64_t la, int64_t lc
 // the min of the conf words' bounds, and "candidate >= pendingIndex" becomes r >= 1.  The q-th
 // largest member: the members' r (others 0) sorted by an odd-even transposition network of u32
 // max / min, then element q - 1 (0 when fewer than q members: nothing granted).  Per pair of
-// groups ~300 VALU instead of ~540 for kth_largest's P^2 64-bit compares (tools/pair_probe.hip).
+// groups ~300 VALU instead of ~540 for kth_largest's P^2 64-bit compares (round 3's tools/pair_probe.hip).
 template <int P>
 __device__ __forceinline__ uint32_t kth_largest_rel(const uint32_t (&r)[P], uint32_t mask, uint32_t q) {
   uint32_t s[P];

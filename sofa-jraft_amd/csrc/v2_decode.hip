@@ -149,7 +149,7 @@ __device__ __forceinline__ uint64_t lds_varint(const uint8_t* w, uint32_t* n) {
 // of dependent LDS round trips per record); false on anything else -- peers, learners, unknown
 // fields, other orders, a field outside the windows -- and the general parser decodes the
 // record from its start.  One lane per record runs a wave's records in lockstep: the general
-// parser's per-byte loop and field switch were 29 us for 64k records (tools/v2_parse_probe.hip).
+// parser's per-byte loop and field switch were 29 us for 64k records (round 3's tools/v2_parse_probe.hip).
 struct V2Fast {
   uint32_t etype;
   int64_t term, index, doff, dlen;
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(256) void v2_parse(JrqV2Args a) {
     // go to the coherence point, past the XCDs' own L2s) and one explicit wait for the
     // summary's stores before the arrival: __threadfence() here is buffer_wbl2 + buffer_inv,
     // an L2 writeback per workgroup (twice), ~10 us for the 256 workgroups of 64k records
-    // (tools/v2_parse_probe.hip "gate").
+    // (round 3's tools/v2_parse_probe.hip "gate").
     auto st_agent = [](uint64_t* q, uint64_t v) { __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     auto add_agent = [](uint64_t* q) { return __hip_atomic_fetch_add(q, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     st_agent(sm + 0, s_doff[0]);
@@ -564,7 +564,7 @@ __device__ void v2_parse_record(const JrqV2Args& a, uint32_t r, const uint64_t* 
 // x^(+-64) is one lookup per register byte: T_i[b] = b x^(64 + 8i) (the engine's slice tables,
 // un-swapped), TI_i[b] = b x^(8i - 64) (engine xinv); single bytes use T_0 / TI_7.  One entry
 // boundary per record instead of two: the CRC pass takes 310 instead of 330 us on 64k x 16 KiB
-// records (tools/v2_boundary_probe.py).
+// records (round 3's tools/v2_boundary_probe.py).
 // (The fixed-size data path -- gate[0] != 0 -- finishes inside crc64_fixed_kernel: this kernel
 // then returns at once.)
 __global__ __launch_bounds__(256) void v2_finish(JrqV2Args a, JrqCrcArgs w) {

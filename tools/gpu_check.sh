@@ -43,14 +43,8 @@ for s in $STEPS; do
            done ;;
     tsel)  run tests_${TAG:-sel} 900 python -u -m pytest ${TESTS:-tests/test_gpu_table.py} -x -q -p no:cacheprovider --timeout 240 --timeout-method thread ;;
     bsel)  run bench_${TAG:-sel} 600 python bench.py --steps 20 --warmup 5 --no-cpu --legs ${BENCH_LEGS:-quorum} --detail gpurun_out/bench_${TAG:-sel}_detail.json ;;
-    tprobe) run table_probe 120 ./tools/table_probe ;;
-    fprobe) run flag_probe 120 ./tools/flag_probe ;;
-    fprobe2) run flag_probe_b1024 120 ./tools/flag_probe_b1024 ;;
-    pprobe) run pair_probe 120 ./tools/pair_probe ;;
-    vprobe) run v2_parse_probe 120 ./tools/v2_parse_probe ;;
     sqpmc) run sqpmc_${TRACE_LEGS:-v2} 120 rocprofv3 --kernel-trace --pmc ${SQ_COUNTERS:-SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_INSTS_SMEM SQ_BUSY_CYCLES} -d gpurun_out/sqpmc_${TRACE_LEGS:-v2} -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs ${TRACE_LEGS:-v2} ;;
     trace) run trace_${TRACE_LEGS:-v2} 300 rocprofv3 --kernel-trace -d gpurun_out/trace_${TRACE_LEGS:-v2} -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs ${TRACE_LEGS:-v2} ;;
     drive) run drive_tests 300 python -u -m pytest tests/test_host_drive.py -v -x -p no:cacheprovider --timeout 240 --timeout-method thread ;;
-    eprobe) run epochs_probe 120 ./tools/epochs_probe ;;
   esac
 done
