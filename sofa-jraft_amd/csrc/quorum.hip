@@ -111,6 +111,9 @@ __device__ __forceinline__ i64x2 ld2nt(const int64_t* p) {
 // (decide_single_rel, quorum_core.h: C3 16.4 -> 15.6 us per epoch in round 3's tools/pair_probe.hip,
 // against 15.1 us for the loads and stores alone).
 constexpr uint32_t kPairBlock = 512;
+#ifndef JRQ_PAIR_XCD_TILES
+#define JRQ_PAIR_XCD_TILES 0
+#endif
 
 template <int P, bool kRuns>
 __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
@@ -119,7 +122,16 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
   __shared__ int64_t hand[kRuns ? kWaves : 1][kHand][P + 3];  // {pi, lc, la, match[P]}
   __shared__ uint32_t flagged[kRuns ? kWaves : 1][128];
   const uint32_t pairs = a.G >> 1;
+#if JRQ_PAIR_XCD_TILES
+  // A/B knob (tools/ab_build.sh): workgroups in XCD-contiguous order -- block b runs on XCD
+  // b % 8 (round-robin dispatch), so tile = that XCD's run position b / 8 inside its own
+  // contiguous range of tiles, and each XCD streams one region of every row
+  const uint32_t nb = gridDim.x, xq = nb / 8, xr = nb % 8, xcd = blockIdx.x % 8;
+  const uint32_t tile = xcd * xq + (xcd < xr ? xcd : xr) + blockIdx.x / 8;
+  const uint32_t t = tile * kPairBlock + threadIdx.x;
+#else
   const uint32_t t = blockIdx.x * kPairBlock + threadIdx.x;
+#endif
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
   bool f0 = false, f1 = false;

@@ -90,6 +90,22 @@ def main():
         legs["C1"] = (lambda e, o: (lambda: e.logentry_checksum_batch_dev(
             d1["etype"], d1["index"], d1["term"], None, d1["payload"], d1["offsets"], o)),
             lambda: torch.empty(1 << 20, dtype=torch.int64, device=dev))
+    if "C3" in legs_env:  # the headline: C3 epochs (pair kernel) over 6 rotating inputs
+        c3 = []
+        for k in range(6):
+            b = W.quorum_batch("C3", seed=(W.SEED_BASE ^ 3) + 7919 * k)
+            c3.append({kk: dev_t(v) for kk, v in b.items()})
+        c3s = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+        def mk_c3(e, o):
+            cnt = [0]  # per variant: the same buffer sequence for each
+
+            def f():
+                t = c3[cnt[0] % 6]
+                cnt[0] += 1
+                e.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
+                                   t["last_committed"], t["conf"], o, c3s)
+            return f
+        legs["C3"] = (mk_c3, lambda: torch.empty(1 << 20, dtype=torch.int64, device=dev))
     if "C5f" in legs_env:  # the C5 entries (16 KiB each) through the fixed-size entry point
         def mk_c5f(e, o):
             cor = torch.empty(n5, dtype=torch.uint8, device=dev)
