@@ -1247,9 +1247,20 @@ def leg_lease(ctx, args, quorum_conf_dev, G, P):
         eng.lease_check_dev(ts_bufs[i % QUORUM_EPOCH_BUFFERS], quorum_conf_dev, self_slot, now_ms,
                             lease_to, lok, lead, ldead)
     ms, _ = ctx.timed(step)
+    ok = None
+    if ctx.oracle_checks:  # one launch on buffer 0 from fresh lease starts, every group
+        import jraft_oracle as O
+        lead.zero_()
+        step(0)
+        ctx.sync()
+        eok, elead, edead = O.lease_check(ts_bufs[0].cpu().numpy(), quorum_conf_dev.cpu().numpy().view(np.uint64),
+                                          np.zeros(G, np.uint8), now_ms, lease_to, np.zeros(G, np.int64))
+        ok = bool(np.array_equal(lok.cpu().numpy(), eok)) and \
+            bool(np.array_equal(lead.cpu().numpy(), elead)) and \
+            bool(np.array_equal(ldead.cpu().numpy().view(np.uint16), edead))
     lb = (8 * P + 28) * G
     return {"workload": f"{G} leader groups x {P} peers (conf + old conf), checkDeadNodes0",
-            "decisions_per_s": G / (ms * 1e-3), "kernel_ms": ms,
+            "decisions_per_s": G / (ms * 1e-3), "kernel_ms": ms, "bit_exact_vs_oracle": ok,
             "roofline": roofline(lb, ms, **pmc_traffic("lease", f"lease_check_kernel<{P}>"))}
 
 
@@ -1305,12 +1316,28 @@ def leg_fanout(ctx, args, G):
         if rep >= max(1, args.warmup):
             fan_ms.append(e0.elapsed_time(e1) / len(fan_sets))
     ms = float(np.mean(fan_ms))
+    ok = None
+    if ctx.oracle_checks:  # set 0 from fresh queues, every group, call-by-call replay
+        import jraft_oracle as O
+        restore()
+        launch(fan_sets[0])
+        ctx.sync()
+        f = fan_sets[0]
+        prev_c, c = f["prev"].cpu().numpy(), f["c"].cpu().numpy()
+        adv = c > prev_c
+        seq_off = np.zeros(G + 1, np.uint64)
+        seq_off[1:] = np.cumsum(adv)
+        est, efc, _, ecf, ecs, _ = O.commit_fanout_replay(seq_off, c[adv], f["la"].cpu().numpy(),
+                                                          f["cf0"].cpu().numpy(), f["cs0"].cpu().numpy())
+        ok = bool(np.array_equal(fan_st.cpu().numpy(), est)) and \
+            bool(np.array_equal(fan_fc.cpu().numpy(), efc)) and \
+            bool(np.array_equal(f["cf"].cpu().numpy(), ecf)) and bool(np.array_equal(f["cs"].cpu().numpy(), ecs))
     # reads prev/committed/lastApplied/cqFirst/cqSize 40 B, writes firstClosure 8 + status 1
     # + the listed bitmap 1/8; + 16 B queue write-back per popping group
     fb = 49 * G + G // 8 + 16 * n_pop
     return {"workload": f"{G} groups (C3 epoch output) -> doCommitted/popClosureUntil, "
                         f"{n_listed} listed, {n_pop} popping",
-            "groups_per_s": G / (ms * 1e-3), "ms_per_launch": ms,
+            "groups_per_s": G / (ms * 1e-3), "ms_per_launch": ms, "bit_exact_vs_oracle": ok,
             "roofline": roofline(fb, ms, **pmc_traffic("fanout", "fanout_eval"))}
 
 
