@@ -257,6 +257,19 @@ int jrq_table_update_gather(jrq_table *t, uint32_t parts, const jrq_group_state 
                             const uint32_t *n_states, const uint64_t *const *recs,
                             const uint32_t *n_recs);
 
+/* Streamed form of jrq_table_update_gather, for a host that packs its updates in parts on
+ * several threads and wants each part's DMA to overlap the packing of the next:
+ * jrq_table_stage_reserve sizes the device staging for up to max_states headers and max_recs
+ * records (it may synchronise, and drops parts staged but never applied), each jrq_table_stage queues
+ * the H2D copy of one part behind the previous ones (an asynchronous DMA when the memory is
+ * page-locked: jrq_host_alloc / jrq_host_register; the memory must stay unchanged until the
+ * next jrq_table_epoch or jrq_synchronize returns), and jrq_table_stage_apply applies every
+ * staged header, then every staged record, as jrq_table_update_gather does with its parts. */
+int jrq_table_stage_reserve(jrq_table *t, uint32_t max_states, uint32_t max_recs);
+int jrq_table_stage(jrq_table *t, const jrq_group_state *states, uint32_t n_states,
+                    const uint64_t *recs, uint32_t n_recs);
+int jrq_table_stage_apply(jrq_table *t);
+
 /* One quorum epoch over every group of the table, state updated in place as BallotBox.commitAt
  * leaves it (BallotBox.java:96-139; commit -> lastCommittedIndex, pendingIndex = commit + 1).
  * Each group whose lastCommittedIndex advanced is listed once, as the word

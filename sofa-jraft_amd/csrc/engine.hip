@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -226,7 +227,28 @@ int upload(jrq_engine* e, void* dst, const void* src, size_t bytes) {
 
 // Caller memory registered with HIP (jrq_host_register, hipHostMalloc) goes straight to the
 // DMA engine; anything else through the bounce chunks.
+// Page-locked ranges libjrq made itself (jrq_host_alloc / jrq_host_register), base -> bytes:
+// an upload from one of them needs no HIP pointer query (a flush stages ~30 parts).
+std::mutex g_pinned_mu;
+std::map<uintptr_t, size_t> g_pinned;
+
+bool known_pinned(const void* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::lock_guard<std::mutex> lk(g_pinned_mu);
+  auto it = g_pinned.upper_bound(a);
+  if (it == g_pinned.begin()) return false;
+  --it;
+  return a < it->first + it->second;
+}
+
+void note_pinned(const void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_pinned_mu);
+  if (bytes) g_pinned[reinterpret_cast<uintptr_t>(p)] = bytes;
+  else g_pinned.erase(reinterpret_cast<uintptr_t>(p));
+}
+
 bool host_pinned(const void* p) {
+  if (known_pinned(p)) return true;
   hipPointerAttribute_t at;
   if (hipPointerGetAttributes(&at, p) != hipSuccess) {
     (void)hipGetLastError();  // an unregistered pointer reports an error: not sticky
@@ -494,12 +516,14 @@ int jrq_host_register(void* ptr, size_t bytes) {
     (void)hipGetLastError();
     return JRQ_E_HIP;
   }
+  note_pinned(ptr, bytes);
   return JRQ_OK;
 }
 
 int jrq_host_unregister(void* ptr) {
   if (!ptr) return JRQ_E_INVALID;
   std::lock_guard<std::mutex> lk(g_pin_mu);
+  note_pinned(ptr, 0);
   if (hipHostUnregister(ptr) != hipSuccess) {
     (void)hipGetLastError();
     return JRQ_E_HIP;
@@ -517,12 +541,14 @@ int jrq_host_alloc(size_t bytes, void** out) {
     *out = nullptr;
     return JRQ_E_NOMEM;
   }
+  note_pinned(*out, bytes);
   return JRQ_OK;
 }
 
 int jrq_host_free(void* ptr) {
   if (!ptr) return JRQ_E_INVALID;
   std::lock_guard<std::mutex> lk(g_pin_mu);
+  note_pinned(ptr, 0);
   if (hipHostFree(ptr) != hipSuccess) {
     (void)hipGetLastError();
     return JRQ_E_HIP;
@@ -1290,6 +1316,8 @@ struct jrq_table {
   uint32_t* n_dev = nullptr;  // host-variant epoch: slice counts [slices], offsets [slices], total
   uint32_t* n_host = nullptr; // pinned: the total
   uint32_t slices = 0;        // JRQ_TABLE_SLICE-group slices of the changed list
+  uint64_t stage_cap_s = 0, stage_cap_r = 0;  // jrq_table_stage: reserved capacity
+  uint64_t staged_s = 0, staged_r = 0;        // headers / records staged since the last apply
   size_t state_bytes = 0;     // the rows at the start of mem (jrq_table_copy)
 };
 
@@ -1449,6 +1477,49 @@ int jrq_table_update_gather(jrq_table* t, uint32_t parts, const jrq_group_state*
   }
   return jrq_table_update_dev(t, static_cast<const jrq_group_state*>(ds), static_cast<uint32_t>(ns),
                               static_cast<const uint64_t*>(dr), static_cast<uint32_t>(nr));
+}
+
+int jrq_table_stage_reserve(jrq_table* t, uint32_t max_states, uint32_t max_recs) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  t->staged_s = t->staged_r = 0;  // parts staged and never applied (a failed flush) are dropped
+  DeviceGuard guard(e->device);
+  int rc;
+  void* p = nullptr;
+  if ((rc = stage_buf(e, t->st_stage, static_cast<size_t>(max_states) * sizeof(jrq_group_state), &p))) return rc;
+  if ((rc = stage_buf(e, t->rec_stage, static_cast<size_t>(max_recs) * 8, &p))) return rc;
+  t->stage_cap_s = t->st_stage.cap / sizeof(jrq_group_state);
+  t->stage_cap_r = t->rec_stage.cap / 8;
+  return JRQ_OK;
+}
+
+int jrq_table_stage(jrq_table* t, const jrq_group_state* states, uint32_t n_states,
+                    const uint64_t* recs, uint32_t n_recs) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if ((n_states && !states) || (n_recs && !recs)) return fail(e, JRQ_E_INVALID, "null update array");
+  if (t->staged_s + n_states > t->stage_cap_s || t->staged_r + n_recs > t->stage_cap_r)
+    return fail(e, JRQ_E_STATE, "table: staging beyond jrq_table_stage_reserve");
+  DeviceGuard guard(e->device);
+  int rc;
+  if (n_states && (rc = upload_any(e, static_cast<jrq_group_state*>(t->st_stage.p) + t->staged_s, states,
+                                   static_cast<size_t>(n_states) * sizeof(jrq_group_state))))
+    return rc;
+  if (n_recs && (rc = upload_any(e, static_cast<uint64_t*>(t->rec_stage.p) + t->staged_r, recs,
+                                 static_cast<size_t>(n_recs) * 8)))
+    return rc;
+  t->staged_s += n_states;
+  t->staged_r += n_recs;
+  return JRQ_OK;
+}
+
+int jrq_table_stage_apply(jrq_table* t) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  const uint64_t ns = t->staged_s, nr = t->staged_r;
+  t->staged_s = t->staged_r = 0;
+  if (!ns && !nr) return JRQ_OK;
+  return jrq_table_update_dev(t, static_cast<const jrq_group_state*>(t->st_stage.p), static_cast<uint32_t>(ns),
+                              static_cast<const uint64_t*>(t->rec_stage.p), static_cast<uint32_t>(nr));
 }
 
 int jrq_table_epoch_dev(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, uint8_t* status_out) {

@@ -271,7 +271,7 @@ struct GroupBatch::DirtyList {  // the groups one calling thread changed since t
   std::atomic<int64_t> firstNs{0};   // when v got its first group
 };
 
-struct GroupBatch::Part {  // one pack worker's headers and records (page-locked)
+struct alignas(128) GroupBatch::Part {  // one pack part's headers and records (page-locked)
   PinnedBuf<jrq_group_state> st;
   PinnedBuf<uint64_t> rec;
   uint32_t ns = 0, nr = 0;
@@ -279,7 +279,7 @@ struct GroupBatch::Part {  // one pack worker's headers and records (page-locked
 
 // One deliver worker's share of an epoch: the commits it applied (group, index, waiter) and
 // the closures it popped, run after every group of the share has moved.
-struct GroupBatch::Delivery {
+struct alignas(128) GroupBatch::Delivery {  // (one per worker: no false sharing of its vectors)
   struct Commit {
     int64_t c;
     const CommitWaiter* waiter;  // the group's (set once by BallotBox::init, before its first ack)
@@ -709,58 +709,92 @@ uint32_t GroupBatch::flushLocked() {
   uint32_t n = 0;
   auto t1 = t0;
   try {
-    // pack: the dirty groups split into contiguous ranges of the concatenated lists, in up to
-    // four chunks: each chunk's parts are uploaded (an asynchronous DMA from page-locked
-    // memory) as soon as they are packed, so packing chunk c + 1 overlaps the DMA of chunk c
-    // (the update's H2D is the PCIe-bound part of a flush: 36 MB at C3).  A group's header and
-    // records sit in one part; chunks hold disjoint groups.
+    // pack: the dirty groups cut into K contiguous ranges ("parts") of the concatenated
+    // lists, claimed in order by the pool's workers, each packed under the groups' locks into
+    // its own page-locked buffers; the flushing thread stages a part's upload (an asynchronous
+    // DMA, jrq_table_stage) as soon as it is packed, so the DMA of the early parts overlaps the
+    // packing of the later ones -- the update's H2D (36 MB at C3) is the PCIe-bound part of a
+    // flush.  All HIP calls stay on the flushing thread.  A group's header and records sit in
+    // one part.
     const size_t kGrain = 1u << 12;
-    const size_t C = nd >= (size_t{1} << 18) ? 4 : 1;
-    std::vector<size_t> np(C);
-    size_t tot = 0;
-    for (size_t c = 0; c < C; ++c) tot += (np[c] = partsFor(nd * (c + 1) / C - nd * c / C, kGrain));
-    if (parts_.size() < tot) parts_.resize(tot);
+    const size_t workers = partsFor(nd, kGrain);  // (1 below 2 * kGrain groups)
+    const size_t K = workers <= 1 ? 1 : std::min<size_t>(4 * workers, nd / kGrain);
+    if (parts_.size() < K) parts_.resize(K);
     changed_.reserve(G_);
-    size_t pb = 0;
-    for (size_t c = 0; c < C; ++c) {
-      const size_t lo = nd * c / C, len = nd * (c + 1) / C - lo;
-      // staging grows here, on this thread: allocation and release of page-locked memory stay
-      // out of the pack workers
-      for (size_t i = 0; i < np[c]; ++i) {
-        const size_t k = len * (i + 1) / np[c] - len * i / np[c];
-        Part& P = parts_[pb + i];
-        P.ns = P.nr = 0;
-        P.st.reserve(k + 1);
-        P.rec.reserve(k * (P_ + 1) + 1);
+    // staging grows here, on this thread: allocation and release of page-locked memory stay
+    // out of the pack workers
+    for (size_t k = 0; k < K; ++k) {
+      const size_t len = nd * (k + 1) / K - nd * k / K;
+      Part& P = parts_[k];
+      P.ns = P.nr = 0;
+      P.st.reserve(len + 1);
+      P.rec.reserve(len * (P_ + 1) + 1);
+    }
+    throwIfError(jrq_table_stage_reserve(table_, static_cast<uint32_t>(nd + 1),
+                                         static_cast<uint32_t>(nd * (P_ + 1) + 1)),
+                 eng_->raw(), "jrq_table_stage_reserve");
+    auto packPart = [&](size_t k) {
+      Part& P = parts_[k];
+      const size_t b0 = nd * k / K, e0 = nd * (k + 1) / K;
+      size_t li = static_cast<size_t>(std::upper_bound(pre.begin(), pre.end(), b0) - pre.begin()) - 1;
+      for (size_t pos = b0; pos < e0; ++li) {  // the pieces of the lists inside [b0, e0)
+        const size_t l0 = pos - pre[li], hi = std::min(e0, pre[li + 1]) - pre[li];
+        if (hi <= l0) continue;
+        packRange(P, work_[li].data() + l0, hi - l0);
+        pos = pre[li] + hi;
       }
-      parallelFor(len, kGrain, [&](unsigned part, size_t b0, size_t e0) {
-        Part& P = parts_[pb + part];
-        const size_t b = lo + b0, e = lo + e0;
-        // the pieces of the lists inside [b, e)
-        size_t li = static_cast<size_t>(std::upper_bound(pre.begin(), pre.end(), b) - pre.begin()) - 1;
-        for (size_t pos = b; pos < e; ++li) {
-          const size_t l0 = pos - pre[li], hi = std::min(e, pre[li + 1]) - pre[li];
-          if (hi <= l0) continue;
-          packRange(P, work_[li].data() + l0, hi - l0);
-          pos = pre[li] + hi;
+    };
+    auto stagePart = [&](size_t k) {
+      const Part& P = parts_[k];
+      stats.states += P.ns;
+      stats.records += P.nr;
+      throwIfError(jrq_table_stage(table_, P.st.p, P.ns, P.rec.p, P.nr), eng_->raw(), "jrq_table_stage");
+    };
+    if (K == 1) {
+      packPart(0);
+      stagePart(0);
+    } else {
+      std::unique_ptr<std::atomic<uint8_t>[]> done(new std::atomic<uint8_t>[K]);
+      for (size_t k = 0; k < K; ++k) done[k].store(0, std::memory_order_relaxed);
+      std::atomic<size_t> next{0};
+      std::atomic<bool> abort{false};
+      pool_->run([&](unsigned i, unsigned) {
+        if (i == 0) {  // the flushing thread: stage the parts in order as they complete
+          try {
+            for (size_t k = 0; k < K; ++k) {
+              uint8_t st;
+              for (unsigned spin = 0; (st = done[k].load(std::memory_order_acquire)) == 0; ++spin) {
+                if (spin < 256) __builtin_ia32_pause();
+                else std::this_thread::yield();
+              }
+              if (st == 2) return;  // the worker's exception comes back from run()
+              stagePart(k);
+            }
+          } catch (...) {
+            abort.store(true, std::memory_order_relaxed);
+            throw;
+          }
+          return;
+        }
+        for (;;) {
+          const size_t k = next.fetch_add(1, std::memory_order_relaxed);
+          if (k >= K) return;
+          if (abort.load(std::memory_order_relaxed)) {
+            done[k].store(2, std::memory_order_release);
+            continue;
+          }
+          try {
+            packPart(k);
+          } catch (...) {
+            done[k].store(2, std::memory_order_release);
+            abort.store(true, std::memory_order_relaxed);
+            throw;
+          }
+          done[k].store(1, std::memory_order_release);
         }
       });
-      std::vector<const jrq_group_state*> sp(np[c]);
-      std::vector<const uint64_t*> rp(np[c]);
-      std::vector<uint32_t> sn(np[c]), rn(np[c]);
-      for (size_t i = 0; i < np[c]; ++i) {
-        sp[i] = parts_[pb + i].st.p;
-        rp[i] = parts_[pb + i].rec.p;
-        sn[i] = parts_[pb + i].ns;
-        rn[i] = parts_[pb + i].nr;
-        stats.states += sn[i];
-        stats.records += rn[i];
-      }
-      throwIfError(jrq_table_update_gather(table_, static_cast<uint32_t>(np[c]), sp.data(), sn.data(),
-                                           rp.data(), rn.data()),
-                   eng_->raw(), "jrq_table_update_gather");
-      pb += np[c];
     }
+    throwIfError(jrq_table_stage_apply(table_), eng_->raw(), "jrq_table_stage_apply");
     t1 = clk::now();
     throwIfError(jrq_table_epoch(table_, changed_.p, &n, nullptr), eng_->raw(), "jrq_table_epoch");
   } catch (...) {

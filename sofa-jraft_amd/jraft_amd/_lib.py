@@ -131,6 +131,9 @@ SIGNATURES = [
     ("jrq_table_update", C.c_int, [_V, _V, C.c_uint32, _V, C.c_uint32]),
     ("jrq_table_update_dev", C.c_int, [_V, _V, C.c_uint32, _V, C.c_uint32]),
     ("jrq_table_update_gather", C.c_int, [_V, C.c_uint32, _V, _V, _V, _V]),
+    ("jrq_table_stage_reserve", C.c_int, [_V, C.c_uint32, C.c_uint32]),
+    ("jrq_table_stage", C.c_int, [_V, _V, C.c_uint32, _V, C.c_uint32]),
+    ("jrq_table_stage_apply", C.c_int, [_V]),
     ("jrq_table_epoch_dev", C.c_int, [_V, _V, _V, _V]),
     ("jrq_table_epoch", C.c_int, [_V, _V, _V, _V]),
     ("jrq_table_slices", C.c_uint32, [_V]),

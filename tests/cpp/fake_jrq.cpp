@@ -38,6 +38,8 @@ struct jrq_table {
   std::vector<uint64_t> conf;   // [G][JRQ_TABLE_MAX_RUNS]
   uint32_t invalid = 0;
   std::mutex mu;  // the real table orders calls on the engine stream
+  std::vector<jrq_group_state> staged_s;  // jrq_table_stage: copied at once (the real one DMAs)
+  std::vector<uint64_t> staged_r;
 };
 
 extern "C" {
@@ -161,6 +163,35 @@ int jrq_table_update_gather(jrq_table* t, uint32_t parts, const jrq_group_state*
       }
     }
   return JRQ_OK;
+}
+
+int jrq_table_stage_reserve(jrq_table* t, uint32_t, uint32_t) {
+  std::lock_guard<std::mutex> l(t->mu);
+  t->staged_s.clear();
+  t->staged_r.clear();
+  return JRQ_OK;
+}
+
+int jrq_table_stage(jrq_table* t, const jrq_group_state* states, uint32_t n_states,
+                    const uint64_t* recs, uint32_t n_recs) {
+  std::lock_guard<std::mutex> l(t->mu);
+  t->staged_s.insert(t->staged_s.end(), states, states + n_states);
+  t->staged_r.insert(t->staged_r.end(), recs, recs + n_recs);
+  return JRQ_OK;
+}
+
+int jrq_table_stage_apply(jrq_table* t) {
+  std::vector<jrq_group_state> s;
+  std::vector<uint64_t> r;
+  {
+    std::lock_guard<std::mutex> l(t->mu);
+    std::swap(s, t->staged_s);
+    std::swap(r, t->staged_r);
+  }
+  const jrq_group_state* sp = s.data();  // (update_gather carries the failure injection)
+  const uint64_t* rp = r.data();
+  const uint32_t ns = static_cast<uint32_t>(s.size()), nr = static_cast<uint32_t>(r.size());
+  return jrq_table_update_gather(t, 1, &sp, &ns, &rp, &nr);
 }
 
 #ifdef FAKE_JRQ_CLOSED_FORM
