@@ -997,10 +997,14 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<uint8_t*>((static_cast<uint64_t>(hhi) << 32) | hlo),
         static_cast<short>(0), static_cast<int>(hn), 0x00020000);
+    // kStarts: pieces start on 64-B boundaries, so half the "lines" straddle two 128-B lines,
+    // the other half of which the owner's previous or next load reads: nt would evict it in
+    // between (the default policy for those)
+    constexpr int kAux = kStarts ? JRQ_CRC_LOAD_AUX : JRQ_CRC_LINE_AUX;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) HA[q] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa[q], 0, JRQ_CRC_LINE_AUX);
+    for (int q = 0; q < 4; ++q) HA[q] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa[q], 0, kAux);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) HB[q] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa[4 + q], 0, JRQ_CRC_LINE_AUX);
+    for (int q = 0; q < 4; ++q) HB[q] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa[4 + q], 0, kAux);
     asm volatile("" ::: "memory");
     if (cline + 1 < LE) {
       ++cline;
