@@ -89,8 +89,27 @@ __global__ __launch_bounds__(256) JRQ_SGPRS_8WAVES void quorum_epoch_kernel(JrqQ
 
 typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
 
+// A/B knobs (tools/ab_build.sh): the pair kernel's cache policy for its streams
+#ifndef JRQ_PAIR_NT_LOADS
+#define JRQ_PAIR_NT_LOADS 1
+#endif
+#ifndef JRQ_PAIR_NT_STORES
+#define JRQ_PAIR_NT_STORES 1
+#endif
 __device__ __forceinline__ i64x2 ld2nt(const int64_t* p) {
+#if JRQ_PAIR_NT_LOADS
   return __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(p));
+#else
+  return *reinterpret_cast<const i64x2*>(p);
+#endif
+}
+template <class T>
+__device__ __forceinline__ void st_pair(T v, T* p) {
+#if JRQ_PAIR_NT_STORES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
 }
 
 // Fast path (16-B aligned arrays, even match_ld): one lane decides two adjacent groups; every
@@ -179,8 +198,8 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
       i64x2 out;
       out.x = o0;
       out.y = o1;
-      __builtin_nontemporal_store(out, reinterpret_cast<i64x2*>(a.committed + g));
-      __builtin_nontemporal_store(static_cast<uint16_t>(s0 | (s1 << 8)),
+      st_pair(out, reinterpret_cast<i64x2*>(a.committed + g));
+      st_pair(static_cast<uint16_t>(s0 | (s1 << 8)),
                                   reinterpret_cast<uint16_t*>(a.status + g));
     } else {  // rare: a flagged group's outputs are written by the walk only
       if (!f0) {
