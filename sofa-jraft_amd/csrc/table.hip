@@ -39,6 +39,20 @@ __device__ __forceinline__ i64x2 tld2o(const int64_t* base, uint32_t off) {
   return __builtin_nontemporal_load(reinterpret_cast<const gi64x2*>(b + off));
 }
 
+// Plain stores for the epoch's outputs, as the pair kernel (quorum.hip: nt stores measured 7 %
+// slower there); JRQ_TABLE_NT_STORES = 1 is the A/B knob (tools/ab_build.sh)
+#ifndef JRQ_TABLE_NT_STORES
+#define JRQ_TABLE_NT_STORES 0
+#endif
+template <class T>
+__device__ __forceinline__ void st_tab(T v, T* p) {
+#if JRQ_TABLE_NT_STORES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // Writes of a committing group: lastCommitted, and pendingIndex -> JRQ_PI_FOLLOWS_LC once.
 __device__ __forceinline__ void table_commit_one(const JrqTableArgs& t, uint32_t g, int64_t pr,
                                                  int64_t out) {
@@ -167,7 +181,7 @@ __global__ __launch_bounds__(kTableEpochBlock) JRQ_SGPRS_8WAVES void table_epoch
       i64x2 v;
       v.x = o[2 * h];
       v.y = o[2 * h + 1];
-      __builtin_nontemporal_store(v, reinterpret_cast<i64x2*>(t.lc + g));
+      st_tab(v, reinterpret_cast<i64x2*>(t.lc + g));
     } else {
       if (ca) t.lc[g] = o[2 * h];
       if (cb) t.lc[g + 1] = o[2 * h + 1];
@@ -182,7 +196,7 @@ __global__ __launch_bounds__(kTableEpochBlock) JRQ_SGPRS_8WAVES void table_epoch
       const uint32_t s2 = (st4 >> (16 * h)) & 0xFFFFu;
       const bool ka = !f[2 * h] && !x[2 * h], kb = !f[2 * h + 1] && !x[2 * h + 1] && g + 1 < t.G;
       if (ka && kb)
-        __builtin_nontemporal_store(static_cast<uint16_t>(s2), reinterpret_cast<uint16_t*>(t.status + g));
+        st_tab(static_cast<uint16_t>(s2), reinterpret_cast<uint16_t*>(t.status + g));
       else {
         if (ka) t.status[g] = static_cast<uint8_t>(s2);
         if (kb) t.status[g + 1] = static_cast<uint8_t>(s2 >> 8);

@@ -163,10 +163,13 @@ def load() -> C.CDLL:
             import torch  # noqa: F401
         except ImportError:
             pass
-        if not os.path.exists(LIB_PATH):
+        # (tools only: tools/gpu_check.sh's A/B runs point the bench at a variant build,
+        # ab/<name>/libjrq.so; never set by the tests, smoke() or the driver's bench)
+        path = os.environ.get("JRAFT_AMD_AB_LIB") or LIB_PATH
+        if not os.path.exists(path):
             raise FileNotFoundError(
-                f"{LIB_PATH} missing: run `make -C sofa-jraft_amd` (or __graft_entry__.build())")
-        lib = C.CDLL(LIB_PATH)
+                f"{path} missing: run `make -C sofa-jraft_amd` (or __graft_entry__.build())")
+        lib = C.CDLL(path)
         for name, res, args in SIGNATURES:
             fn = getattr(lib, name)
             fn.restype = res

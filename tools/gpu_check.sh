@@ -37,6 +37,10 @@ for s in $STEPS; do
              run pmc_${leg}_RDREQ 180 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum -d gpurun_out/pmc_${leg}_RDREQ -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs $leg
            done ;;
     host)  run host_test 300 ./tests/_build/host_test gpu ;;
+    babl)  # the bench legs once per variant library (A/B of legs ab_inproc.py lacks)
+           for v in ${AB_LIBS:-base}; do
+             run bench_${TAG:-sel}_$v 600 env JRAFT_AMD_AB_LIB=ab/$v/libjrq.so python bench.py --steps 20 --warmup 5 --no-cpu --legs ${BENCH_LEGS:-table} --detail gpurun_out/bench_${TAG:-sel}_${v}_detail.json
+           done ;;
     ab)    run ab_${TAG:-sel} 600 env AB_LEGS=${AB_LEGS:-C3,C5f,C1f,archive} python tools/ab_inproc.py ${AB_VARIANTS:-base=ab/base/libjrq.so} ;;
     legtrace) # one kernel trace per bench leg (tools/leg_traces.py -> profiles/<tag>_leg_kernels.json)
            for leg in ${TRACE_LEGS:-quorum table C2 C2L C3K C5 C1 ae v2 snapshot lease fanout}; do
