@@ -39,10 +39,10 @@ __device__ __forceinline__ i64x2 tld2o(const int64_t* base, uint32_t off) {
   return __builtin_nontemporal_load(reinterpret_cast<const gi64x2*>(b + off));
 }
 
-// Plain stores for the epoch's outputs, as the pair kernel (quorum.hip: nt stores measured 7 %
-// slower there); JRQ_TABLE_NT_STORES = 1 is the A/B knob (tools/ab_build.sh)
+// Cache policy of the epoch's stores (A/B knob, tools/ab_build.sh): nt -- plain stores measured
+// 2 % slower here (21.75 vs 22.14 us), while the pair kernel's are 1.5-7 % faster plain
 #ifndef JRQ_TABLE_NT_STORES
-#define JRQ_TABLE_NT_STORES 0
+#define JRQ_TABLE_NT_STORES 1
 #endif
 template <class T>
 __device__ __forceinline__ void st_tab(T v, T* p) {
@@ -51,6 +51,16 @@ __device__ __forceinline__ void st_tab(T v, T* p) {
 #else
   *p = v;
 #endif
+}
+
+// Word `comp` (0/1) of the 16 B lane `src` holds in v (every lane calls it: two ds_bpermute
+// per word).
+__device__ __forceinline__ int64_t ent_field(const i64x2& v, uint32_t src, uint32_t comp) {
+  const int s = static_cast<int>(src);
+  const uint32_t xl = __shfl(static_cast<uint32_t>(v.x), s), xh = __shfl(static_cast<uint32_t>(static_cast<uint64_t>(v.x) >> 32), s);
+  const uint32_t yl = __shfl(static_cast<uint32_t>(v.y), s), yh = __shfl(static_cast<uint32_t>(static_cast<uint64_t>(v.y) >> 32), s);
+  const uint64_t x = (static_cast<uint64_t>(xh) << 32) | xl, y = (static_cast<uint64_t>(yh) << 32) | yl;
+  return static_cast<int64_t>(comp ? y : x);
 }
 
 // Writes of a committing group: lastCommitted, and pendingIndex -> JRQ_PI_FOLLOWS_LC once.
@@ -95,21 +105,25 @@ __global__ __launch_bounds__(kTableEpochBlock) JRQ_SGPRS_8WAVES void table_epoch
   constexpr uint32_t kHand = 16;  // flagged groups per wave handed over through LDS
   constexpr uint32_t kEntLds = 4; // flagged-entry slots per wave copied to LDS up front
   __shared__ int64_t hand[kWaves][kHand][P + 3];  // {pendingIndex word, lc, la, match[P]}
-  __shared__ __attribute__((aligned(16))) int64_t ent4[kWaves][kEntLds][8];  // entries 0-3
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
   // wave wid holds groups [256 wid, 256 wid + 256): its flagged-entry slots, list slice, count
   const uint32_t wid = blockIdx.x * kWaves + w;
   const uint32_t gA = wid * kTableSlice + 2u * lane;  // pair A = (gA, gA + 1), B = A + 128
   uint64_t* const slice = t.changed + static_cast<size_t>(wid) * kTableSlice;
-  // The wave's first four flagged-entry slots go straight to its LDS slice (an LDS-DMA load,
-  // 256 B per wave; no registers held across the single-conf path), whatever the wave's count:
-  // the count is the wave's own ballot of its flagged groups (the flags kernel's count of the
-  // same 256 groups).  Loading the count and branching on it here put a full memory round trip
-  // in front of every wave's single-conf loads.
+  // The wave's first four flagged-entry slots are loaded up front, beside the single-conf loads,
+  // whatever the wave's count: 16 B per lane on lanes 0-15 (entry i = lanes 4i .. 4i + 3), read
+  // by the walk through lane shuffles.  (The count is the wave's own ballot of its flagged
+  // groups, the flags kernel's count of the same 256 groups: loading the count and branching on
+  // it put a full memory round trip in front of every wave's single-conf loads.  Round 3 copied
+  // the entries into LDS with an LDS-DMA load; with one in flight the compiler waited for every
+  // load of the wave, vmcnt(0), before the first LDS write -- the flagged hand-off -- so pair
+  // B's loads held up pair A's decisions.)
   const int64_t* const ent = reinterpret_cast<const int64_t*>(t.flag_ent) + static_cast<size_t>(wid) * kFlagSlots * 8;
-  if (lane < 4 * kEntLds)  // lane l: bytes 16 l .. 16 l + 15 of entries 0-3 (64 B each)
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ent + lane * 2), &ent4[w][0][0], 16, 0, 0);
+  i64x2 ev;
+  ev.x = 0;
+  ev.y = 0;
+  if (lane < 4 * kEntLds) ev = *reinterpret_cast<const i64x2*>(ent + lane * 2);
   // per group k = 0..3 (A.x, A.y, B.x, B.y): live (inside the table), flagged, committing,
   // outside rel_domain; commit value, delta, status
   bool live[2], f[4], c[4], x[4], wpi[4];
@@ -222,11 +236,17 @@ __global__ __launch_bounds__(kTableEpochBlock) JRQ_SGPRS_8WAVES void table_epoch
     // outstanding memory operation)
     int64_t eh = 0, ers = kI64Min, enx = kI64Max;
     uint64_t rc = 0;
+    // entries 0-3 from the lanes holding them (every lane shuffles: the wave is converged here)
+    const uint32_t ie = i < kEntLds ? i : 0u;
+    const int64_t f0 = ent_field(ev, 4u * ie, 0u);
+    const int64_t fr = ent_field(ev, 4u * ie + (r >> 1), r & 1u);
+    const int64_t fn = ent_field(ev, 4u * ie + ((r + 1) >> 1), (r + 1) & 1u);
+    const int64_t fc = ent_field(ev, 4u * ie + ((4u + r) >> 1), (4u + r) & 1u);
     if (act && i < kEntLds) {
-      eh = ent4[w][i][0];
-      if (r != 0) ers = ent4[w][i][r];
-      if (r != 3) enx = ent4[w][i][r + 1];
-      rc = static_cast<uint64_t>(ent4[w][i][4 + r]);
+      eh = f0;
+      if (r != 0) ers = fr;
+      if (r != 3) enx = fn;
+      rc = static_cast<uint64_t>(fc);
     } else if (act) {
       const int64_t* e = ent + static_cast<size_t>(i) * 8;
       eh = e[0];
