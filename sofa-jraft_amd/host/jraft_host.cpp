@@ -264,7 +264,9 @@ inline void spinLock(std::atomic<uint8_t>& l) {
 
 // --------------------------------------------------------------- ballot box
 
-struct GroupBatch::DirtyList {  // the groups one calling thread changed since the last swap
+// the groups one calling thread changed since the last swap (cache-line aligned: the lists of
+// different threads are written concurrently, each by its own thread)
+struct alignas(128) GroupBatch::DirtyList {
   std::atomic<uint8_t> mu{0};
   std::vector<uint32_t> v;
   std::atomic<size_t> n{0};          // v.size(), for the flusher's policy
