@@ -148,6 +148,21 @@ def warm_until(fn, stream, sync, warm_ms=None, calls=None):
     return n
 
 
+_MARK = {}
+
+
+def mark(stream):
+    """A one-element fill kernel on `stream` right outside a timed series' event pair: in a
+    rocprofv3 kernel trace the launches between two marks are exactly one timed series
+    (tools/leg_traces.py reads them that way).  Costs nothing inside the pair."""
+    import torch
+    t = _MARK.get(stream.device)
+    if t is None:
+        t = _MARK[stream.device] = torch.zeros(1, dtype=torch.int32, device=stream.device)
+    with torch.cuda.stream(stream):
+        t.fill_(7)
+
+
 def timed_launches(fn, steps, warmup, stream, sync, warm_calls=None):
     """`warmup` untimed calls plus WARM_MS of untimed calls (warm_until), then `steps` calls
     back to back between ONE pair of HIP events on `stream` (the engine's stream): the
@@ -160,11 +175,13 @@ def timed_launches(fn, steps, warmup, stream, sync, warm_calls=None):
     sync()
     warm_until(fn, stream, sync, calls=warm_calls)
     b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    mark(stream)
     t0 = time.perf_counter()
     b0.record(stream)
     for i in range(steps):
         fn(i)
     b1.record(stream)
+    mark(stream)
     sync()
     wall = time.perf_counter() - t0
     return b0.elapsed_time(b1) / steps, wall
@@ -545,18 +562,23 @@ def leg_table(ctx, args, G, pair_ms):
         """median over reps of (event pair around NB back-to-back launches) / NB"""
         for w, t in zip(work, src):
             w.copy_from(t)
-        for i in range(NB):  # warm: one untimed series
-            launch(i)
-        warm_until(lambda i: launch(i % NB), ctx.stream, ctx.sync, warm_ms=WARM_MS / 4)
+        def warm(i):  # untimed series, each from fresh tables too
+            if i % NB == 0:
+                for w, t in zip(work, src):
+                    w.copy_from(t)
+            launch(i % NB)
+        warm_until(warm, ctx.stream, ctx.sync, warm_ms=WARM_MS / 4)
         out = []
         for _ in range(reps):
             for w, t in zip(work, src):
                 w.copy_from(t)
             a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            mark(ctx.stream)
             a.record(ctx.stream)
             for i in range(NB):
                 launch(i)
             z.record(ctx.stream)
+            mark(ctx.stream)
             ctx.sync()
             out.append(a.elapsed_time(z) / NB)
         return float(np.median(out))
@@ -1311,10 +1333,12 @@ def leg_fanout(ctx, args, G):
         restore()
         ctx.sync()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        mark(ctx.stream)
         e0.record(ctx.stream)
         for f in fan_sets:
             launch(f)
         e1.record(ctx.stream)
+        mark(ctx.stream)
         ctx.sync()
         if rep >= max(1, args.warmup):
             fan_ms.append(e0.elapsed_time(e1) / len(fan_sets))

@@ -5,10 +5,12 @@ so every kernel name in a trace carries that leg's workload only), and each leg'
 fraction recomputed from them.
 
 For each leg: every kernel name with its launch count and the median / mean / p10 / p90 duration
-(us) over all its launches in the pass (warm-up, timed and check launches alike: the median is
-the steady state).  With --detail (the bench's full result of a run of the same tree), each
-leg's `frac` is recomputed as the leg's algorithmic bytes per launch / the summed medians of its
-kernels / 8 TB/s, beside the frac the bench's HIP-event timing gave.
+(us) over all its launches in the pass; and the timed series of the leg's roofline (the
+launches between two of the bench's marks, `bench.py mark`): its kernels, the kernel time per
+launch (summed medians) and the span per launch (first start to last end / launches: what the
+bench's event pair measures).  With --detail (the bench's full result of a run of the same
+tree), each leg's fraction is recomputed from both, beside the frac the bench's HIP-event
+timing gave.
 
 usage: python tools/leg_traces.py gpurun_out [--detail gpurun_out/bench_detail.json] > profiles/<tag>_leg_kernels.json
 """
@@ -43,20 +45,37 @@ LEG_KERNELS = {
 }
 
 
-def kernel_stats(trace_dir):
+def read_trace(trace_dir):
     files = glob.glob(os.path.join(trace_dir, "**", "*kernel_trace.csv"), recursive=True)
     if not files:
         return None
-    durs = {}
-    for r in csv.DictReader(open(files[0])):
-        name = r["Kernel_Name"]
-        durs.setdefault(name, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    out = {}
-    for name, d in sorted(durs.items()):
-        d.sort()
-        out[name] = {"launches": len(d), "median_us": round(statistics.median(d), 3),
-                     "mean_us": round(statistics.fmean(d), 3),
-                     "p10_us": round(d[len(d) // 10], 3), "p90_us": round(d[(9 * len(d)) // 10], 3)}
+    rows = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+            for r in csv.DictReader(open(files[0]))]
+    rows.sort()
+    return rows
+
+
+def stats(durs):
+    d = sorted(durs)
+    return {"launches": len(d), "median_us": round(statistics.median(d), 3),
+            "mean_us": round(statistics.fmean(d), 3),
+            "p10_us": round(d[len(d) // 10], 3), "p90_us": round(d[(9 * len(d)) // 10], 3)}
+
+
+def timed_series(rows):
+    """The launches between consecutive bench marks (bench.py `mark`: a one-element fill kernel
+    right outside each timed series' event pair), as lists of (start, end, name)."""
+    out, cur = [], None
+    for r in rows:
+        if "FillFunctor" in r[2]:
+            if cur is None:
+                cur = []
+            else:
+                out.append(cur)
+                cur = None
+            continue
+        if cur is not None:
+            cur.append(r)
     return out
 
 
@@ -69,31 +88,47 @@ def main():
     res = {"how": __doc__.split("\n\n")[1].replace("\n", " "), "legs": {}}
     for d in sorted(glob.glob(os.path.join(root, "legtrace_*"))):
         leg = os.path.basename(d)[len("legtrace_"):]
-        ks = kernel_stats(d)
-        if ks is None:
+        rows = read_trace(d)
+        if rows is None:
             continue
-        entry = {"kernels": ks}
+        durs = {}
+        for a, b, n in rows:
+            if "FillFunctor" not in n:
+                durs.setdefault(n, []).append((b - a) / 1e3)
+        entry = {"kernels": {n: stats(v) for n, v in sorted(durs.items())}}
         if leg in LEG_KERNELS:
             path, names = LEG_KERNELS[leg]
-            med = 0.0
-            found = []
-            for n in names:
-                hit = [v for k, v in ks.items() if n in k]
-                if hit:
-                    med += hit[0]["median_us"]
-                    found.append(n)
-            entry["timed_kernels"] = found
-            entry["timed_median_us"] = round(med, 3)
-            if detail is not None:
-                rl = detail
-                for p in path:
-                    rl = (rl or {}).get(p)
-                if rl and med > 0:
-                    frac = rl["bytes_per_launch"] / (med * 1e-6) / 1e9 / PEAK
-                    entry["bytes_per_launch"] = rl["bytes_per_launch"]
-                    entry["frac_from_trace"] = round(frac, 4)
-                    entry["frac_bench_events"] = round(rl["frac"], 4)
-                    entry["trace_over_events"] = round(frac / rl["frac"], 4)
+            # the timed series of this leg's roofline: the first series holding every kernel of
+            # one timed launch and the fewest other names
+            best = None
+            for ser in timed_series(rows):
+                kn = {n for _, _, n in ser}
+                if all(any(x in k for k in kn) for x in names):
+                    if best is None or len(kn) < len({n for _, _, n in best}):
+                        best = ser
+            if best is not None:
+                main = [n for _, _, n in best if names[0] in n]
+                launches = len(main)
+                per = {}
+                for a, b, n in best:
+                    per.setdefault(n, []).append((b - a) / 1e3)
+                kern = sum(statistics.median(v) * len(v) / launches for v in per.values())
+                span = (best[-1][1] - best[0][0]) / 1e3 / launches
+                entry["timed_series"] = {"launches": launches,
+                                         "kernels": {n: stats(v) for n, v in sorted(per.items())},
+                                         "kernel_us_per_launch": round(kern, 3),
+                                         "span_us_per_launch": round(span, 3)}
+                if detail is not None:
+                    rl = detail
+                    for p in path:
+                        rl = (rl or {}).get(p)
+                    if rl:
+                        B = rl["bytes_per_launch"]
+                        entry["bytes_per_launch"] = B
+                        entry["frac_from_trace_kernels"] = round(B / (kern * 1e-6) / 1e9 / PEAK, 4)
+                        entry["frac_from_trace_span"] = round(B / (span * 1e-6) / 1e9 / PEAK, 4)
+                        entry["frac_bench_events"] = round(rl["frac"], 4)
+                        entry["span_over_events"] = round(entry["frac_from_trace_span"] / rl["frac"], 4)
         res["legs"][leg] = entry
     json.dump(res, sys.stdout, indent=1)
     print()
