@@ -151,16 +151,20 @@ def warm_until(fn, stream, sync, warm_ms=None, calls=None):
 _MARK = {}
 
 
-def mark(stream):
-    """A one-element fill kernel on `stream` right outside a timed series' event pair: in a
-    rocprofv3 kernel trace the launches between two marks are exactly one timed series
-    (tools/leg_traces.py reads them that way).  Costs nothing inside the pair."""
+def mark(stream, end=False):
+    """A one-element kernel on `stream` right outside a timed series' event pair -- a
+    bitwise-not before it, a negation after it (ops the legs use nowhere else): in a rocprofv3
+    kernel trace the launches between the two are exactly one timed series (tools/leg_traces.py
+    reads them that way).  Costs nothing inside the pair."""
     import torch
     t = _MARK.get(stream.device)
     if t is None:
         t = _MARK[stream.device] = torch.zeros(1, dtype=torch.int32, device=stream.device)
     with torch.cuda.stream(stream):
-        t.fill_(7)
+        if end:
+            t.neg_()
+        else:
+            t.bitwise_not_()
 
 
 def timed_launches(fn, steps, warmup, stream, sync, warm_calls=None):
@@ -181,7 +185,7 @@ def timed_launches(fn, steps, warmup, stream, sync, warm_calls=None):
     for i in range(steps):
         fn(i)
     b1.record(stream)
-    mark(stream)
+    mark(stream, end=True)
     sync()
     wall = time.perf_counter() - t0
     return b0.elapsed_time(b1) / steps, wall
@@ -578,7 +582,7 @@ def leg_table(ctx, args, G, pair_ms):
             for i in range(NB):
                 launch(i)
             z.record(ctx.stream)
-            mark(ctx.stream)
+            mark(ctx.stream, end=True)
             ctx.sync()
             out.append(a.elapsed_time(z) / NB)
         return float(np.median(out))
@@ -1338,7 +1342,7 @@ def leg_fanout(ctx, args, G):
         for f in fan_sets:
             launch(f)
         e1.record(ctx.stream)
-        mark(ctx.stream)
+        mark(ctx.stream, end=True)
         ctx.sync()
         if rep >= max(1, args.warmup):
             fan_ms.append(e0.elapsed_time(e1) / len(fan_sets))

@@ -6,7 +6,7 @@ fraction recomputed from them.
 
 For each leg: every kernel name with its launch count and the median / mean / p10 / p90 duration
 (us) over all its launches in the pass; and the timed series of the leg's roofline (the
-launches between two of the bench's marks, `bench.py mark`): its kernels, the kernel time per
+launches between the bench's start and end marks, `bench.py mark`): its kernels, the kernel time per
 launch (summed medians) and the span per launch (first start to last end / launches: what the
 bench's event pair measures).  With --detail (the bench's full result of a run of the same
 tree), each leg's fraction is recomputed from both, beside the frac the bench's HIP-event
@@ -62,19 +62,23 @@ def stats(durs):
             "p10_us": round(d[len(d) // 10], 3), "p90_us": round(d[(9 * len(d)) // 10], 3)}
 
 
+def is_mark(name):
+    return "bitwise_not_kernel" in name or "neg_kernel" in name
+
+
 def timed_series(rows):
-    """The launches between consecutive bench marks (bench.py `mark`: a one-element fill kernel
-    right outside each timed series' event pair), as lists of (start, end, name)."""
+    """The launches between a start mark and the next end mark (bench.py `mark`: a one-element
+    bitwise-not right before each timed series' event pair, a negation right after it), as
+    lists of (start, end, name)."""
     out, cur = [], None
     for r in rows:
-        if "FillFunctor" in r[2]:
-            if cur is None:
-                cur = []
-            else:
+        if "bitwise_not_kernel" in r[2]:
+            cur = []
+        elif "neg_kernel" in r[2]:
+            if cur:
                 out.append(cur)
-                cur = None
-            continue
-        if cur is not None:
+            cur = None
+        elif cur is not None:
             cur.append(r)
     return out
 
@@ -93,7 +97,7 @@ def main():
             continue
         durs = {}
         for a, b, n in rows:
-            if "FillFunctor" not in n:
+            if not is_mark(n):
                 durs.setdefault(n, []).append((b - a) / 1e3)
         entry = {"kernels": {n: stats(v) for n, v in sorted(durs.items())}}
         if leg in LEG_KERNELS:
