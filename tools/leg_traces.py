@@ -37,7 +37,7 @@ LEG_KERNELS = {
             "crc64_finish_kernel<true>", "ae_first_corrupt"]),
     "v2": (("next_rows", "v2_decode_verify", "roofline"),
            ["v2_parse", "crc64_fixed_kernel<true, true>", "crc64_rounds_kernel<768u, true>",
-            "crc64_finish_kernel<true>", "v2_finish"]),
+            "v2_finish"]),
     "snapshot": (("next_rows", "snapshot_stream_crc64", "roofline"),
                  ["crc64_rounds_kernel<512u, false>", "crc64_finish_kernel<false>"]),
     "lease": (("next_rows", "lease_check", "roofline"), ["lease_check_kernel<5>"]),
