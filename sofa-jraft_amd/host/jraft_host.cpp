@@ -435,7 +435,8 @@ GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
     : eng_(eng), G_(groups), P_(peers), serial_(g_batchSerial.fetch_add(1)) {
   if (peers == 0 || peers > JRQ_MAX_PEERS) throw std::invalid_argument("peers must be 1..16");
   if (groups == 0 || groups > JRQ_TABLE_MAX_GROUPS) throw std::invalid_argument("groups must be 1..2^27");
-  stride_ = (sizeof(Hot) + 16 * static_cast<size_t>(P_) + 63) & ~size_t(63);
+  static_assert(sizeof(Hot) == 48, "group record header");
+  stride_ = (sizeof(Hot) + 14 * static_cast<size_t>(P_) + 63) & ~size_t(63);
   const size_t bytes = stride_ * G_;
   rec_ = static_cast<unsigned char*>(std::aligned_alloc(64, bytes));
   if (!rec_) throw std::bad_alloc();
@@ -444,12 +445,14 @@ GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
     Hot* h = new (rec_ + static_cast<size_t>(g) * stride_) Hot();
     h->lock.store(0, std::memory_order_relaxed);
     h->nruns = 0;
-    h->inited = 0;
+    h->lastN = 0xFF;
+    h->lastO = 0xFF;
     h->dirty = 0;
     h->pi = 0;
     h->lc = 0;
     h->la = -1;
     h->lastConf = 0;
+    h->lastSlots = 0;
     uint32_t* sp = slotPeerOf(g);
     for (uint32_t s = 0; s < P_; ++s) sp[s] = kNoPeer;
   }
@@ -533,15 +536,17 @@ int GroupBatch::slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved
     if (victim < 0 && sp[s] == kNoPeer) victim = static_cast<int>(s);
   }
   if (!create) return -1;
-  uint32_t* su = slotUseOf(g);
+  uint16_t* su = slotUseOf(g);
   if (victim < 0) {
     const uint32_t busy = liveMask(g) | reserved;
     for (uint32_t s = 0; s < P_; ++s)
-      if (!((busy >> s) & 1u) && (victim < 0 || su[s] < su[victim])) victim = static_cast<int>(s);
+      if (!((busy >> s) & 1u) &&  // least recently acked, in the 16-bit stamps' circular order
+          (victim < 0 || static_cast<int16_t>(static_cast<uint16_t>(su[s] - su[victim])) < 0))
+        victim = static_cast<int>(s);
     if (victim < 0) return -1;
   }
   sp[victim] = peer;
-  su[victim] = static_cast<uint32_t>(flushes_.load(std::memory_order_relaxed));
+  su[victim] = static_cast<uint16_t>(flushes_.load(std::memory_order_relaxed));
   int64_t* m = matchOf(g);
   if (m[victim] != 0) {
     m[victim] = 0;
@@ -550,16 +555,20 @@ int GroupBatch::slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved
   return victim;
 }
 
-uint64_t GroupBatch::confWord(uint32_t g, const uint32_t* ids, uint32_t nn, uint32_t no, bool hasOld) {
+uint64_t GroupBatch::confWord(uint32_t g, const uint32_t* ids, uint32_t nn, uint32_t no, bool hasOld,
+                              uint64_t* slots) {
   // Ballot.init (Ballot.java:63-85): peers only, quorum = size/2+1, oldQuorum 0 if null
   uint32_t nm = 0, om = 0;
+  uint64_t sl = 0;
   for (uint32_t i = 0; i < nn + no; ++i) {
     const int s = slotOf(g, ids[i], true, nm | om);
     if (s < 0)
       throw std::length_error("more distinct live peers in group " + std::to_string(g) +
                               " than the " + std::to_string(P_) + " peer slots");
     (i < nn ? nm : om) |= 1u << s;
+    if (i < 16) sl |= static_cast<uint64_t>(s) << (4 * i);
   }
+  if (slots) *slots = sl;
   return JRQ_CONF(nm, om, nn / 2 + 1, hasOld ? no / 2 + 1 : 0);
 }
 
@@ -945,7 +954,6 @@ bool BallotBox::init(const BallotBoxOptions& opts) {
   GroupBatch& b = *batch_;
   GroupBatch::Guard lk(b, g_);
   b.waiter_[g_] = opts.waiter;
-  b.hot(g_).inited = 1;
   return true;
 }
 
@@ -970,7 +978,7 @@ bool BallotBox::commitAt(int64_t first, int64_t last, const PeerId& peer) {
     m = last;
     b.markDirty(g_, 1u << s);
   }
-  b.slotUseOf(g_)[s] = static_cast<uint32_t>(b.flushes_.load(std::memory_order_relaxed));
+  b.slotUseOf(g_)[s] = static_cast<uint16_t>(b.flushes_.load(std::memory_order_relaxed));
   return true;
 }
 
@@ -1052,7 +1060,22 @@ bool BallotBox::append(const Configuration& conf, const Configuration* oldConf, 
   if (count <= 0) return true;
   if (h.la + count - h.pi + 1 > INT32_MAX)  // pendingMetaQueue is a Java ArrayList
     throw std::length_error("pending queue larger than an ArrayList");
-  const uint64_t cw = b.confWord(g_, ids, static_cast<uint32_t>(nn), static_cast<uint32_t>(no), oldConf != nullptr);
+  // the conf word: the group's last conf again (the common case: NodeImpl passes its current
+  // conf with every task) when the same ids sit in the cached slots, else Ballot.init's walk
+  const uint32_t tot = static_cast<uint32_t>(nn + no);
+  const uint8_t oTag = oldConf ? static_cast<uint8_t>(no) : 0xFF;
+  uint64_t cw;
+  if (h.nruns != 0 && h.lastN == nn && h.lastO == oTag && tot <= 16 && no < 0xFF &&
+      b.sameSlots(g_, ids, tot, h.lastSlots)) {
+    cw = h.lastConf;
+  } else {
+    uint64_t sl = 0;
+    cw = b.confWord(g_, ids, static_cast<uint32_t>(nn), static_cast<uint32_t>(no), oldConf != nullptr, &sl);
+    const bool cache = tot <= 16 && nn < 0xFF && no < 0xFF;
+    h.lastN = cache ? static_cast<uint8_t>(nn) : 0xFF;
+    h.lastO = oTag;
+    h.lastSlots = sl;
+  }
   const int64_t idx = h.la + 1;
   if (h.nruns == 0 || h.lastConf != cw) {  // Ballot.init with a new conf: a new conf run
     GroupBatch::Run* R = &b.runs_[static_cast<size_t>(g_) * JRQ_TABLE_MAX_RUNS];

@@ -308,16 +308,18 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   // One group's record: what every API call and the flush touch, in one or two adjacent cache
   // lines (128 B at P = 5) instead of a word in each of nine arrays: the hot header, then
   // match[P] (int64, highest index acked per slot), slotPeer[P] (u32, interned PeerId of the
-  // slot), slotUse[P] (u32, flush count of the slot's last ack).  Its conf runs live apart
-  // (runs_: read when a conf changes or a run dies).
+  // slot), slotUse[P] (u16, flush count of the slot's last ack, mod 2^16: only orders the
+  // victims of a slot reassignment).  Its conf runs live apart (runs_: read when a conf changes
+  // or a run dies).
   struct Hot {
     std::atomic<uint8_t> lock;  // the group's one-byte spin lock
     uint8_t nruns;              // conf runs of the pending queue
-    uint8_t inited;
-    uint8_t pad;
+    uint8_t lastN, lastO;       // the last appended conf's peer counts (lastO 0xFF: no old
+                                // conf; lastN 0xFF: no cached conf)
     uint32_t dirty;             // slots / lastAppended / header changed since the last pack
     int64_t pi, lc, la;         // pendingIndex, lastCommittedIndex, lastAppended
     uint64_t lastConf;          // conf word of the last run (appends compare against it)
+    uint64_t lastSlots;         // slot of the last conf's i-th peer, 4 bits each (<= 16 peers)
   };
   Hot& hot(uint32_t g) const { return *reinterpret_cast<Hot*>(rec_ + static_cast<size_t>(g) * stride_); }
   int64_t* matchOf(uint32_t g) const {
@@ -326,8 +328,8 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   uint32_t* slotPeerOf(uint32_t g) const {
     return reinterpret_cast<uint32_t*>(rec_ + static_cast<size_t>(g) * stride_ + sizeof(Hot) + 8 * P_);
   }
-  uint32_t* slotUseOf(uint32_t g) const {
-    return reinterpret_cast<uint32_t*>(rec_ + static_cast<size_t>(g) * stride_ + sizeof(Hot) + 12 * P_);
+  uint16_t* slotUseOf(uint32_t g) const {
+    return reinterpret_cast<uint16_t*>(rec_ + static_cast<size_t>(g) * stride_ + sizeof(Hot) + 12 * P_);
   }
 
   void lock(uint32_t g) const;
@@ -342,7 +344,15 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   int slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved = 0);
   uint32_t liveMask(uint32_t g) const;
   // conf word of a Configuration pair given its peers' ids (new conf's nn, then old conf's no)
-  uint64_t confWord(uint32_t g, const uint32_t* ids, uint32_t nn, uint32_t no, bool hasOld);
+  uint64_t confWord(uint32_t g, const uint32_t* ids, uint32_t nn, uint32_t no, bool hasOld,
+                    uint64_t* slots = nullptr);
+  // the ids' slots are the cached ones of the group's last conf (append's fast path)
+  bool sameSlots(uint32_t g, const uint32_t* ids, uint32_t n, uint64_t slots) const {
+    const uint32_t* sp = slotPeerOf(g);
+    for (uint32_t i = 0; i < n; ++i)
+      if (sp[(slots >> (4 * i)) & 15u] != ids[i]) return false;
+    return true;
+  }
   bool gapCountsPeer(uint32_t g, int slot, int64_t lo, int64_t hi) const;
   void markDirty(uint32_t g, uint32_t bits);
   void dropDeadRuns(uint32_t g);

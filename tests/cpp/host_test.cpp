@@ -782,6 +782,30 @@ static void testThrowingCallback(Engine& eng) {
     if (g != 3) CHECK(boxes[g].getLastCommittedIndex() == 5);
 }
 
+// The append fast path reuses the group's last conf word only for the same peers in the same
+// split between conf and old conf: {a,b,c} then {a,b} + old {c} is a new run (Ballot.init with
+// oldQuorum 1), and entry 2 needs c's ack.
+static void testConfCacheSplit(Engine& eng) {
+  auto batch = std::make_shared<GroupBatch>(&eng, 1, 4);
+  BallotBox box(batch, 0);
+  Waiter w;
+  CHECK(box.init({w.fn()}));
+  CHECK(box.resetPendingIndex(1));
+  Configuration abc = conf("a:1,b:2,c:3"), ab = conf("a:1,b:2"), c = conf("c:3");
+  CHECK(box.appendPendingTask(abc, nullptr));
+  CHECK(box.appendPendingTask(abc, nullptr));   // same conf: the cached word, no new run
+  CHECK(box.appendPendingTask(ab, &c));         // same ids, another split: a new run
+  CHECK(box.appendPendingTask(ab, &c));
+  box.commitAt(1, 4, PeerId("a", 1));
+  box.commitAt(1, 4, PeerId("b", 2));
+  batch->flush();
+  CHECK(box.getLastCommittedIndex() == 2);
+  box.commitAt(1, 4, PeerId("c", 3));
+  batch->flush();
+  CHECK(box.getLastCommittedIndex() == 4);
+  CHECK(w.calls.size() == 2 && w.calls[0] == 2 && w.calls[1] == 4);
+}
+
 // a thread alternating between many batches keeps one dirty list per batch.
 static void testManyBatchesOneThread(Engine& eng) {
   std::vector<std::shared_ptr<GroupBatch>> batches;
@@ -839,6 +863,7 @@ int main(int argc, char** argv) {
     tests.push_back({"testFlushFailureRelists", [&] { testFlushFailureRelists(e); }});
     tests.push_back({"testThrowingCallback", [&] { testThrowingCallback(e); }});
     tests.push_back({"testManyBatchesOneThread", [&] { testManyBatchesOneThread(e); }});
+    tests.push_back({"testConfCacheSplit", [&] { testConfCacheSplit(e); }});
   }
   for (auto& t : tests) {
     const int before = g_fail;
