@@ -14,6 +14,7 @@
 #include <thread>
 
 #include <sched.h>
+#include <sys/mman.h>
 
 namespace jraft {
 
@@ -437,9 +438,13 @@ GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
   if (groups == 0 || groups > JRQ_TABLE_MAX_GROUPS) throw std::invalid_argument("groups must be 1..2^27");
   static_assert(sizeof(Hot) == 48, "group record header");
   stride_ = (sizeof(Hot) + 14 * static_cast<size_t>(P_) + 63) & ~size_t(63);
-  const size_t bytes = stride_ * G_;
-  rec_ = static_cast<unsigned char*>(std::aligned_alloc(64, bytes));
+  // 2 MiB-aligned and advised for transparent huge pages: the calls walk 128 MB of records at
+  // C3, 32 records per 4 KiB page
+  const size_t kHuge = size_t(2) << 20;
+  const size_t bytes = (stride_ * G_ + kHuge - 1) & ~(kHuge - 1);
+  rec_ = static_cast<unsigned char*>(std::aligned_alloc(kHuge, bytes));
   if (!rec_) throw std::bad_alloc();
+  (void)madvise(rec_, bytes, MADV_HUGEPAGE);
   std::memset(rec_, 0, bytes);
   for (uint32_t g = 0; g < G_; ++g) {
     Hot* h = new (rec_ + static_cast<size_t>(g) * stride_) Hot();
