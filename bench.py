@@ -149,6 +149,10 @@ def warm_until(fn, stream, sync, warm_ms=None, calls=None):
 
 
 _MARK = {}
+# the leg each timed series belongs to, in mark order (the full result's `timed_series_legs`:
+# tools/leg_traces.py pairs them with the start marks of a trace of the same run)
+_SERIES = []
+_LEG = [None]
 
 
 def mark(stream, end=False):
@@ -164,6 +168,7 @@ def mark(stream, end=False):
         if end:
             t.neg_()
         else:
+            _SERIES.append(_LEG[0])
             t.bitwise_not_()
 
 
@@ -1633,6 +1638,7 @@ def main():
     G = args.groups_per_gpu
     from jraft_amd import workloads as W
     if "quorum" in legs:
+        _LEG[0] = "quorum"
         q = leg_quorum(ctx, args, barrier, max_over_ranks)
         line.update({
             "value": q["value"], "ms_per_step": q["elapsed"] * 1e3 / args.steps,
@@ -1648,42 +1654,56 @@ def main():
             "bit_exact_vs_oracle_4096_groups": q["bit_exact_vs_oracle_4096_groups"]})
     if "table" in legs:
         pair_ms = line.get("roofline", {}).get("kernel_ms")
+        _LEG[0] = "table"
         line["resident_table"] = leg_table(ctx, args, G, pair_ms)
     if "drive" in legs:
+        _LEG[0] = "drive"
         line["end_to_end_host_mirror"] = leg_drive(ctx, args, G)
     if "C2" in legs:
+        _LEG[0] = "C2"
         line["C2"] = leg_c2(ctx, args)
     if "C2L" in legs:
+        _LEG[0] = "C2L"
         line.setdefault("C2", {})["batched_epochs_64"] = leg_c2l(ctx, args)
     if "C3K" in legs:
+        _LEG[0] = "C3K"
         line["C3_k_epochs"] = leg_c3k(ctx, args, G)
     extras = {}
     c5state = None
     if legs & {"C5", "ae", "v2", "snapshot", "pinned"}:
+        _LEG[0] = "C5"
         crc, c5_step, c5state = leg_c5(ctx, args, barrier, max_over_ranks,
                                        time_it="C5" in legs)
         if "C5" in legs:
             line["crc64"] = crc
             line["C5"] = c5_step
     if "ae" in legs:
+        _LEG[0] = "ae"
         extras["append_entries_verify"] = leg_ae(ctx, args, c5state)
     if "v2" in legs:
+        _LEG[0] = "v2"
         extras["v2_decode_verify"] = leg_v2(ctx, args, c5state)
     if "snapshot" in legs:
+        _LEG[0] = "snapshot"
         extras["snapshot_stream_crc64"] = leg_snapshot(ctx, args, c5state)
     if "pinned" in legs:
+        _LEG[0] = "pinned"
         line["pinned_host_payload"] = leg_pinned(ctx, args, c5state)
     c5state = None
     if "C1" in legs:
+        _LEG[0] = "C1"
         line["C1"] = leg_c1(ctx, args)
     if "lease" in legs:
         b = W.quorum_batch("C3", groups=G)
+        _LEG[0] = "lease"
         extras["lease_check"] = leg_lease(ctx, args, to_dev(b["conf"], dev), G, 5)
     if "fanout" in legs:
+        _LEG[0] = "fanout"
         extras["commit_fanout"] = leg_fanout(ctx, args, G)
     if extras:
         line["next_rows"] = extras
     if "peak" in legs and "roofline" in line:
+        _LEG[0] = "peak"
         line["roofline"]["peak_measured"] = leg_peak(ctx)
 
     if "cpu" in legs and rank == 0 and world == 1 and not args.no_cpu:
@@ -1695,6 +1715,7 @@ def main():
         line["cpu_baselines"] = cpu
         if "crc64" in line:
             line["crc64"]["cpu_baseline"] = cpu["C5_crc"]
+    line["timed_series_legs"] = list(_SERIES)
     if rank == 0:
         s = emit_line(line, os.path.abspath(args.detail))
         sys.stderr.flush()

@@ -42,6 +42,11 @@ for s in $STEPS; do
              run bench_${TAG:-sel}_$v 600 env JRAFT_AMD_AB_LIB=ab/$v/libjrq.so python bench.py --steps 20 --warmup 5 --no-cpu --legs ${BENCH_LEGS:-table} --detail gpurun_out/bench_${TAG:-sel}_${v}_detail.json
            done ;;
     ab)    run ab_${TAG:-sel} 600 env AB_LEGS=${AB_LEGS:-C3,C5f,C1f,archive} python tools/ab_inproc.py ${AB_VARIANTS:-base=ab/base/libjrq.so} ;;
+    fulltrace) # the default bench run under the tracer: the printed line, the full result and one
+           # kernel trace of the same launches (tools/leg_traces.py --trace -> <tag>_leg_kernels.json)
+           run fulltrace 900 rocprofv3 --kernel-trace --stats -d gpurun_out/full -o run --output-format csv -- python bench.py --detail gpurun_out/full_detail.json
+           python tools/leg_traces.py --trace gpurun_out/full --detail gpurun_out/full_detail.json > gpurun_out/full_leg_kernels.json
+           rm -f gpurun_out/full/run_kernel_trace.csv ;;
     legtrace) # one kernel trace per bench leg (tools/leg_traces.py -> profiles/<tag>_leg_kernels.json)
            for leg in ${TRACE_LEGS:-quorum table C2 C2L C3K C5 C1 ae v2 snapshot lease fanout}; do
              run legtrace_$leg 180 rocprofv3 --kernel-trace -d gpurun_out/legtrace_$leg -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu --legs $leg

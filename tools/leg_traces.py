@@ -12,7 +12,19 @@ bench's event pair measures).  With --detail (the bench's full result of a run o
 tree), each leg's fraction is recomputed from both, beside the frac the bench's HIP-event
 timing gave.
 
+With --trace DIR (one kernel trace of a whole bench run, `rocprofv3 --kernel-trace -- python
+bench.py --detail D`) and --detail D of that same run, the run's timed series are matched to
+their legs through the result's `timed_series_legs` (the leg of each start mark, in order), so
+the recomputed fractions and the bench's come from the same launches.
+
+With --untraced U (the full result of a run of the same tree on the same box without the
+tracer, as the driver runs the bench), each leg also gets that run's fraction beside the
+trace's: the tracer stretches back-to-back series of short kernels (its per-dispatch completion
+signals), so the traced run's own events under-read those legs while its kernel durations do not.
+--from-json J re-reads an earlier output instead of a trace (to add --untraced to it).
+
 usage: python tools/leg_traces.py gpurun_out [--detail gpurun_out/bench_detail.json] > profiles/<tag>_leg_kernels.json
+       python tools/leg_traces.py --trace gpurun_out/full --detail gpurun_out/full_detail.json [--untraced U]
 """
 import csv
 import glob
@@ -83,18 +95,57 @@ def timed_series(rows):
     return out
 
 
+def traces(argv, detail):
+    """(leg, rows of its launches, its timed series) per leg: one trace per leg (legtrace_<leg>
+    directories), or one trace of a whole run split by the run's `timed_series_legs`."""
+    if "--trace" in argv:
+        rows = read_trace(argv[argv.index("--trace") + 1])
+        labels = (detail or {}).get("timed_series_legs")
+        series = timed_series(rows)
+        if labels is None or len(labels) != len(series):
+            raise SystemExit(f"--trace needs the same run's --detail: {len(series)} series in the "
+                             f"trace, {None if labels is None else len(labels)} labels")
+        for leg in dict.fromkeys(labels):
+            ser = [x for x, l in zip(series, labels) if l == leg]
+            yield leg, [r for x in ser for r in x], ser
+        return
+    for d in sorted(glob.glob(os.path.join(argv[1], "legtrace_*"))):
+        rows = read_trace(d)
+        if rows is not None:
+            yield os.path.basename(d)[len("legtrace_"):], rows, timed_series(rows)
+
+
+def add_untraced(res, plain):
+    """Each leg's roofline fraction from an untraced run's full result, beside the trace's."""
+    res["untraced_run"] = "frac_untraced_events: the same tree's bench without the tracer, same box"
+    for leg, entry in res["legs"].items():
+        if leg not in LEG_KERNELS or "frac_from_trace_kernels" not in entry:
+            continue
+        rl = plain
+        for p in LEG_KERNELS[leg][0]:
+            rl = (rl or {}).get(p)
+        if rl:
+            entry["frac_untraced_events"] = round(rl["frac"], 4)
+            entry["trace_kernels_over_untraced"] = round(entry["frac_from_trace_kernels"] / rl["frac"], 4)
+
+
 def main():
-    root = sys.argv[1]
+    if "--from-json" in sys.argv:
+        with open(sys.argv[sys.argv.index("--from-json") + 1]) as fh:
+            res = json.load(fh)
+        with open(sys.argv[sys.argv.index("--untraced") + 1]) as fh:
+            add_untraced(res, json.load(fh))
+        json.dump(res, sys.stdout, indent=1)
+        print()
+        return
     detail = None
     if "--detail" in sys.argv:
         with open(sys.argv[sys.argv.index("--detail") + 1]) as fh:
             detail = json.load(fh)
-    res = {"how": __doc__.split("\n\n")[1].replace("\n", " "), "legs": {}}
-    for d in sorted(glob.glob(os.path.join(root, "legtrace_*"))):
-        leg = os.path.basename(d)[len("legtrace_"):]
-        rows = read_trace(d)
-        if rows is None:
-            continue
+    res = {"how": "\n\n".join(__doc__.split("\n\n")[1:3]).replace("\n", " "), "legs": {}}
+    if "--trace" in sys.argv:
+        res["trace"] = "one trace of the whole run (the launches of the leg's timed series only)"
+    for leg, rows, series in traces(sys.argv, detail):
         durs = {}
         for a, b, n in rows:
             if not is_mark(n):
@@ -105,7 +156,7 @@ def main():
             # the timed series of this leg's roofline: the first series holding every kernel of
             # one timed launch and the fewest other names
             best = None
-            for ser in timed_series(rows):
+            for ser in series:
                 kn = {n for _, _, n in ser}
                 if all(any(x in k for k in kn) for x in names):
                     if best is None or len(kn) < len({n for _, _, n in best}):
@@ -134,6 +185,9 @@ def main():
                         entry["frac_bench_events"] = round(rl["frac"], 4)
                         entry["span_over_events"] = round(entry["frac_from_trace_span"] / rl["frac"], 4)
         res["legs"][leg] = entry
+    if "--untraced" in sys.argv:
+        with open(sys.argv[sys.argv.index("--untraced") + 1]) as fh:
+            add_untraced(res, json.load(fh))
     json.dump(res, sys.stdout, indent=1)
     print()
 
