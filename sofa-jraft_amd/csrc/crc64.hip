@@ -263,21 +263,6 @@ __device__ __forceinline__ void hash_regs(const CrcTab& tb, RState& r, const u32
   }
 }
 
-// CRC of the first b (< 64) bytes of a 64-B line held in registers (each step is kept or
-// dropped: no per-lane loop bound).
-__device__ __forceinline__ uint64_t prefix_crc(const CrcTab& tb, const uint4 (&w)[4], uint32_t b,
-                                               const char* lds, RState r = RState{0u, 0u}) {
-#pragma unroll
-  for (int t = 0; t < 64; ++t) {
-    const uint4 q = w[t >> 4];
-    const uint32_t word = (t & 15) < 4 ? q.x : (t & 15) < 8 ? q.y : (t & 15) < 12 ? q.z : q.w;
-    RState n = r;
-    tb.step1(n, (word >> (8 * (t & 3))) & 0xFFu, lds);
-    if (static_cast<uint32_t>(t) < b) r = n;
-  }
-  return crc_value(r);
-}
-
 // c * x^(8n) mod P via the global power tables: one 8-lookup pass per set bit of n.
 __device__ __forceinline__ uint64_t crc_shift(uint64_t c, uint64_t n,
                                               const uint64_t* __restrict__ shift) {
@@ -905,7 +890,7 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
 // waits for the ring on their account).  C1 (1M x 256 B): the segment walk wrote 6.5x its 8 MB
 // of results as scattered 8-B stores and re-read them in the finish kernel.
 // kStarts (V2 decode): entry i starts at payload + starts[i] (non-decreasing, any byte
-// alignment: buffer loads take unaligned offsets), k and EL come from the device words
+// alignment: each piece is hashed from its 128-B line, below), k and EL come from the device words
 // gate[0..1] written by v2_parse (gate[3]: the payload's end offset); k == 0 means the
 // segment walk takes the batch instead.  With kLogEntry the record's partial checksum (type ^
 // crc(LogId) ^ peers, from v2_parse) arrives in peer_xor: out = partial ^ crc(data) and the
@@ -960,15 +945,19 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   const uintptr_t pbase = reinterpret_cast<uintptr_t>(a.payload);
   // kStarts: the row's base (its first piece) and each owner's offset from it, through
   // __shfl (the load of lane 16q + c reads owner 16q + c's piece); a new row costs a load
-  // Byte-misaligned 16-B loads stream at ~60 % of the aligned rate (round 3's tools/unal_probe.hip) and
-  // 64-B halves across two lines double the L2 requests: a piece starting at byte b of a 64-B
-  // line is hashed over [start - b, start - b + PS) (same ring, aligned loads) and corrected
-  // after the loop (the b bytes before it and the b bytes it missed, by linearity); the
-  // payload is 64-B aligned (the host checks)
+  // Byte-misaligned 16-B loads stream at ~60 % of the aligned rate (round 3's tools/unal_probe.hip),
+  // and lines split between two loads cannot be `nt`: a piece starting at byte b of a 128-B
+  // line is hashed over [start - b, start - b + PS) -- whole lines, the ring's own loads --
+  // with the b bytes before it zeroed in the row's first line (leading zeros leave the raw CRC
+  // unchanged), and the b bytes it missed are hashed after the loop; the payload is 128-B
+  // aligned (the host checks).  b_next: the b of the row whose first line went out last.
   uint64_t row_base = 0;
+  uint32_t b_next = 0;
   auto set_row = [&](uint32_t row) {
     const uint32_t er = row * EPR + (lane >> kl);
-    const uint64_t ps = (a.starts[er < n ? er : n - 1u] + static_cast<uint64_t>(lane & (K - 1u)) * PS) & ~63ull;
+    const uint64_t psu = a.starts[er < n ? er : n - 1u] + static_cast<uint64_t>(lane & (K - 1u)) * PS;
+    b_next = static_cast<uint32_t>(psu & 127u);
+    const uint64_t ps = psu & ~127ull;
     const uint32_t rb_lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ps));
     const uint32_t rb_hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ps >> 32));
     row_base = (static_cast<uint64_t>(rb_hi) << 32) | rb_lo;
@@ -977,13 +966,15 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) qa[q] = __shfl(rel, static_cast<int>(c + 8u * q)) + ro;
   };
-  if (kStarts) set_row(r0);
   // load cursor (row, line of the piece) of the next 128-B line to issue, scalar; past the
   // wave's last line its loads get an empty descriptor (zeros, no memory request: re-reading
   // that line cost up to 3 % of the bytes when it had left L2)
   uint32_t crow = r0, cline = 0, cur_live = 1u;
   const uint32_t LE = HE >> 1;  // lines per piece
   auto load_line = [&](u32x4 (&HA)[4], u32x4 (&HB)[4]) {
+    // kStarts: a row's offsets are set when its first line goes out, so at the top of row r the
+    // last row set is r (its first line leaves during row r - 1, row r + 1's during row r)
+    if (kStarts && cline == 0 && cur_live) set_row(crow);
     const uint64_t o = kStarts ? row_base + static_cast<uint64_t>(cline) * 128u
                                : static_cast<uint64_t>(crow) * 64u * PS + static_cast<uint64_t>(cline) * 128u;
     const uint64_t hp = pbase + o;
@@ -997,10 +988,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<uint8_t*>((static_cast<uint64_t>(hhi) << 32) | hlo),
         static_cast<short>(0), static_cast<int>(hn), 0x00020000);
-    // kStarts: pieces start on 64-B boundaries, so half the "lines" straddle two 128-B lines,
-    // the other half of which the owner's previous or next load reads: nt would evict it in
-    // between (the default policy for those)
-    constexpr int kAux = kStarts ? JRQ_CRC_LOAD_AUX : JRQ_CRC_LINE_AUX;
+    constexpr int kAux = JRQ_CRC_LINE_AUX;
 #pragma unroll
     for (int q = 0; q < 4; ++q) HA[q] = __builtin_amdgcn_raw_buffer_load_b128(rh, qa[q], 0, kAux);
 #pragma unroll
@@ -1011,7 +999,6 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     } else if (crow + 1 < r1) {
       ++crow;
       cline = 0;
-      if (kStarts) set_row(crow);
     } else {
       cur_live = 0u;
     }
@@ -1046,11 +1033,21 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
     }
     RState s{0u, 0u};
     uint32_t q = 0;
+    const uint32_t bh = kStarts ? b_next : 0u;  // this row's piece offset in its first line
     // a ring of two 128-B lines per lane (slots h0 + h1, h2 + h3), each line read whole by
     // its load instructions (8 owners x 128 B each): with half-lines per instruction 15 % of
     // the lines were fetched twice, and `nt` loads could not be used
     do {
       transpose_line(h0, h1);
+      if (kStarts && q == 0) {  // the bytes before the piece: zeros (wave-uniform branch)
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          const int sh = static_cast<int>(bh) - 4 * j;
+          const uint32_t keep = sh <= 0 ? ~0u : sh >= 4 ? 0u : (~0u << (8 * sh));
+          if (j < 16) h0[j >> 2][j & 3] &= keep;
+          else h1[(j - 16) >> 2][j & 3] &= keep;
+        }
+      }
       tb.step64(s, h0, lds);
       tb.step64(s, h1, lds);
       load_line(h0, h1);
@@ -1060,31 +1057,39 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
       load_line(h2, h3);
     } while (++q < turns);
     uint64_t c = crc_value(s);
-    if (kStarts) {  // hashed [ps - b, ps - b + PS): drop the b bytes before, add the b missed
-      const uint64_t ps = a.starts[e] + static_cast<uint64_t>(piece) * PS;
-      const uint32_t b = static_cast<uint32_t>(ps & 63u);
-      // both are the first b bytes of a 64-B line: J before the piece, T its tail (the line
-      // past T may run past the records' end: then bytes)
-      const uint64_t jl = ps - b, tl = ps - b + PS;
-      uint4 jw[4], tw[4];
+    if (kStarts) {  // hashed [ps - b, ps - b + PS) with its first b bytes zeroed: add the b missed
+      // T = the first b bytes of the 128-B line at tl (the line may run past the records' end:
+      // then byte loads)
+      const uint64_t tl = ((a.starts[e] + static_cast<uint64_t>(piece) * PS) & ~127ull) + PS;
+      const uint32_t b = bh;
+      if (tl + 128u <= total) {
+        uint4 tw[8];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) jw[i] = reinterpret_cast<const uint4*>(a.payload + jl)[i];
-      const bool tail_lines = tl + 64u <= total;
-      if (tail_lines) {
+        for (int i = 0; i < 8; ++i) tw[i] = reinterpret_cast<const uint4*>(a.payload + tl)[i];
+        // whole 8-B words, then the last b & 7 bytes one by one: at most 15 + 7 dependent
+        // table steps (byte by byte it was up to 127)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) tw[i] = reinterpret_cast<const uint4*>(a.payload + tl)[i];
-      }
-      // crc(J ‖ piece) = crc(J) · x^(8 PS) ⊕ crc(piece), and J ‖ piece = (what the ring hashed)
-      // ‖ T: continue the ring's state over T (one power-table pass for x^(8 PS) when PS is a
-      // power of two, instead of one per set bit of PS - b)
-      const uint64_t cj = prefix_crc(tb, jw, b, lds);
-      if (tail_lines) {
-        c = prefix_crc(tb, tw, b, lds, s);
+        for (int w = 0; w < 16; ++w) {
+          if (8u * w + 8u <= b) {
+            const uint4 v = tw[w >> 1];
+            tb.step8(s, (w & 1) ? v.z : v.x, (w & 1) ? v.w : v.y, lds);
+          }
+        }
+        const uint32_t wi = b >> 3, rem = b & 7u;
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+          const uint4 v = tw[w >> 1];
+          lo = wi == static_cast<uint32_t>(w) ? ((w & 1) ? v.z : v.x) : lo;
+          hi = wi == static_cast<uint32_t>(w) ? ((w & 1) ? v.w : v.y) : hi;
+        }
+#pragma unroll
+        for (uint32_t t = 0; t < 7; ++t)
+          if (t < rem) tb.step1(s, ((t < 4 ? lo : hi) >> (8 * (t & 3u))) & 0xFFu, lds);
       } else {
         for (uint32_t t = 0; t < b; ++t) tb.step1(s, a.payload[tl + t], lds);
-        c = crc_value(s);
       }
-      c ^= crc_shift(cj, PS, a.shift);
+      c = crc_value(s);
     }
     // pieces -> entry: at level l, the group of 2^l lanes holding the earlier bytes is shifted
     // past the 2^l * PS bytes of its partner group (x^(8 * 2^l * PS), global power tables)

@@ -1209,8 +1209,8 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
   v.lens = static_cast<uint64_t*>(lens);
   v.gate = e->v2_gate;
   v.blk = static_cast<uint64_t*>(blk);
-  // (the fixed-size path hashes from the 64-B line of each data start: records 64-B aligned)
-  v.lanes = (reinterpret_cast<uintptr_t>(rec) & 63u) ? ~0ull
+  // (the fixed-size path hashes from the 128-B line of each data start: records 128-B aligned)
+  v.lanes = (reinterpret_cast<uintptr_t>(rec) & 127u) ? ~0ull
                                                      : static_cast<uint64_t>(e->crc_grid) * jrq::kCrcBlock;
   JRQ_HIP(e, jrq_launch_v2_parse(&v, e->stream));  // (its last block writes the gate)
   // every record with the same data length (the common case: fixed-size commands): the data

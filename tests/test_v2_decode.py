@@ -378,10 +378,10 @@ def test_gpu_uniform_data_len(engine, n, L, bump):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pad", [64, 13])
+@pytest.mark.parametrize("pad", [128, 64, 13])
 def test_gpu_uniform_data_len_device_variant(engine, pad):
-    """The _dev entry point on a uniform batch: records 64-B aligned take the fixed-size data
-    path, records at pad 13 the segment walk (the host's alignment check); same results."""
+    """The _dev entry point on a uniform batch: records 128-B aligned take the fixed-size data
+    path, records at pad 64 or 13 the segment walk (the host's alignment check); same results."""
     import torch
     n, L = 4096, 16384
     buf, off = uniform_batch(7, n, L)
