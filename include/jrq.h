@@ -465,7 +465,8 @@ int jrq_commit_fanout(jrq_engine *e, uint32_t G, const int64_t *prev_committed,
  * -> V2Decoder.decode (JC/entity/codec/v2/V2Decoder.java:46-110; PBLogEntry, log.proto:10-20,
  * protobuf 3.5.1) -> LogEntry.isCorrupted (JC/entity/LogEntry.java:88-108,156-158), as
  * LogManagerImpl checks every entry it reads (JC/core/LogManagerImpl.java:733-745).
- *   records[offsets[r] .. offsets[r+1])  the stored bytes of entry r (any base/alignment)
+ *   records[offsets[r] .. offsets[r+1])  the stored bytes of entry r (any base/alignment;
+ *   a 128-B aligned base lets a batch of equal data lengths take the one-pass fixed-size path) 
  * Out per record: status_out (jrq_v2_status); for JRQ_V2_OK: type (EntryType number), index,
  * term, stored checksum + has_checksum, data_off (absolute into `records`) / data_len of the
  * data field, peer_counts (nullable: peers | old_peers<<8 | learners<<16 | old_learners<<24,
