@@ -13,10 +13,17 @@
 #include <sstream>
 #include <thread>
 
+#include <linux/membarrier.h>
 #include <sched.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 namespace jraft {
+
+namespace testing {
+void (*fastPathHook)() = nullptr;
+}  // namespace testing
 
 namespace {
 
@@ -250,6 +257,45 @@ int64_t nowNs() {
              std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Relaxed atomic access to record fields that commitAt's fast path reads or writes without
+// the group's lock (plain moves on x86; they keep the concurrent accesses well defined).
+template <class T>
+inline T ald(const T& x) {
+  return __atomic_load_n(&x, __ATOMIC_RELAXED);
+}
+template <class T>
+inline void ast(T& x, T v) {
+  __atomic_store_n(&x, v, __ATOMIC_RELAXED);
+}
+
+// Slot stamps (slotUse): the generation of the slot's last raising ack in 15 bits, bit 15 set
+// when that ack changed the match (the pack ships the slot) -- a slot assignment stamps without
+// it.  older(a, b): a's generation precedes b's (circularly, in 15 bits).
+constexpr uint16_t kStampChanged = 0x8000u;
+inline uint16_t stampOf(uint32_t gen, bool changed) {
+  return static_cast<uint16_t>((gen & 0x7FFFu) | (changed ? kStampChanged : 0u));
+}
+inline bool stampOlder(uint16_t a, uint16_t b) { return ((a - b) & 0x7FFFu) >= 0x4000u; }
+inline bool stampChangedIn(uint16_t u, uint32_t gen) {
+  return (u & kStampChanged) && (u & 0x7FFFu) == (gen & 0x7FFFu);
+}
+
+// The asymmetric barrier pair behind the call regions: a caller's region entry is a plain
+// store and a compiler barrier; the rare side (flush, quiesce) runs membarrier(2), which puts a
+// full barrier on every thread of the process, before it reads the callers' counters.  Without
+// membarrier the callers' entry becomes a full barrier (a locked store) instead.
+bool registerMembarrier() {
+  const long q = syscall(__NR_membarrier, MEMBARRIER_CMD_QUERY, 0, 0);
+  if (q < 0 || !(q & MEMBARRIER_CMD_PRIVATE_EXPEDITED)) return false;
+  return syscall(__NR_membarrier, MEMBARRIER_CMD_REGISTER_PRIVATE_EXPEDITED, 0, 0) == 0;
+}
+const bool g_membarrier = registerMembarrier();
+
+void heavyBarrier() {
+  if (!g_membarrier || syscall(__NR_membarrier, MEMBARRIER_CMD_PRIVATE_EXPEDITED, 0, 0) != 0)
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+}
+
 // a one-byte spin lock (calls hold it for a few hundred ns at most)
 inline void spinLock(std::atomic<uint8_t>& l) {
   for (unsigned n = 0; l.exchange(1, std::memory_order_acquire) != 0; ++n) {
@@ -265,14 +311,35 @@ inline void spinLock(std::atomic<uint8_t>& l) {
 
 // --------------------------------------------------------------- ballot box
 
-// the groups one calling thread changed since the last swap (cache-line aligned: the lists of
-// different threads are written concurrently, each by its own thread)
+// One calling thread's state in a batch (cache-line aligned: the lists of different threads are
+// written concurrently, each by its own thread): the groups it listed in generation t, in
+// v[t & 1] (written only by the thread, inside its call regions; flush() takes v[t & 1] once
+// generation t has ended and its regions have drained), and the region counter (odd inside).
 struct alignas(128) GroupBatch::DirtyList {
-  std::atomic<uint8_t> mu{0};
-  std::vector<uint32_t> v;
-  std::atomic<size_t> n{0};          // v.size(), for the flusher's policy
-  std::atomic<int64_t> firstNs{0};   // when v got its first group
+  std::atomic<uint32_t> seq{0};
+  std::vector<uint32_t> v[2];
+  std::atomic<size_t> n[2] = {};          // v[i].size(), for the flusher's policy
+  std::atomic<int64_t> firstNs[2] = {};   // when v[i] got its first group
 };
+
+namespace {
+// One call region of the calling thread (see GroupBatch's threading note): the accesses between
+// entry and exit that the flush or a quiescing writer must see complete.  No lock is taken and
+// no thread is waited for inside one.
+struct Region {
+  std::atomic<uint32_t>& seq;
+  uint32_t s;
+  explicit Region(std::atomic<uint32_t>& q) : seq(q), s(q.load(std::memory_order_relaxed)) {
+    if (g_membarrier) {
+      seq.store(s + 1, std::memory_order_relaxed);
+      std::atomic_signal_fence(std::memory_order_seq_cst);
+    } else {
+      seq.store(s + 1, std::memory_order_seq_cst);
+    }
+  }
+  ~Region() { seq.store(s + 2, std::memory_order_release); }
+};
+}  // namespace
 
 struct alignas(128) GroupBatch::Part {  // one pack part's headers and records (page-locked)
   PinnedBuf<jrq_group_state> st;
@@ -436,7 +503,7 @@ GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
     : eng_(eng), G_(groups), P_(peers), serial_(g_batchSerial.fetch_add(1)) {
   if (peers == 0 || peers > JRQ_MAX_PEERS) throw std::invalid_argument("peers must be 1..16");
   if (groups == 0 || groups > JRQ_TABLE_MAX_GROUPS) throw std::invalid_argument("groups must be 1..2^27");
-  static_assert(sizeof(Hot) == 48, "group record header");
+  static_assert(sizeof(Hot) == 56, "group record header");
   stride_ = (sizeof(Hot) + 14 * static_cast<size_t>(P_) + 63) & ~size_t(63);
   // 2 MiB-aligned and advised for transparent huge pages: the calls walk 128 MB of records at
   // C3, 32 records per 4 KiB page
@@ -449,6 +516,8 @@ GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
   for (uint32_t g = 0; g < G_; ++g) {
     Hot* h = new (rec_ + static_cast<size_t>(g) * stride_) Hot();
     h->lock.store(0, std::memory_order_relaxed);
+    h->gate.store(0, std::memory_order_relaxed);
+    h->listed = 0;
     h->nruns = 0;
     h->lastN = 0xFF;
     h->lastO = 0xFF;
@@ -480,16 +549,25 @@ void GroupBatch::lock(uint32_t g) const { spinLock(hot(g).lock); }
 // This thread's dirty list for this batch: a thread-local cache of 4 (batch, list) pairs, and on
 // a miss the batch's own per-thread map -- one list per (thread, batch) however many batches a
 // thread alternates between (a miss costs a mutex, never a new list).
-GroupBatch::DirtyList* GroupBatch::myDirtyList() {
-  struct Slot {
-    const GroupBatch* b;
-    uint64_t serial;
-    DirtyList* l;
-  };
-  static thread_local Slot cache[4] = {};
-  static thread_local unsigned next = 0;
-  for (const Slot& s : cache)
-    if (s.b == this && s.serial == serial_) return s.l;
+namespace {
+struct ListSlot {
+  const void* b;
+  uint64_t serial;
+  void* l;
+};
+// initial-exec: one fs-relative load per call (the default model of a shared library calls
+// __tls_get_addr, and commitAt's fast path looks its list up on every call)
+thread_local ListSlot tl_lists[4] __attribute__((tls_model("initial-exec"))) = {};
+thread_local unsigned tl_next __attribute__((tls_model("initial-exec"))) = 0;
+}  // namespace
+
+inline GroupBatch::DirtyList* GroupBatch::myDirtyList() {
+  for (const ListSlot& s : tl_lists)
+    if (s.b == this && s.serial == serial_) return static_cast<DirtyList*>(s.l);
+  return myDirtyListSlow();
+}
+
+GroupBatch::DirtyList* GroupBatch::myDirtyListSlow() {
   DirtyList* l;
   {
     std::lock_guard<std::mutex> g(listsMu_);
@@ -500,23 +578,81 @@ GroupBatch::DirtyList* GroupBatch::myDirtyList() {
     }
     l = mine;
   }
-  cache[next++ & 3u] = Slot{this, serial_, l};
+  tl_lists[tl_next++ & 3u] = ListSlot{this, serial_, l};
   return l;
 }
 
-// Under the group's lock: the first change since the group was last packed puts it on this
-// thread's dirty list; the bits say what to pack.
+// Under the group's lock: the bits say what to pack; the group goes on the calling thread's
+// list of the current generation unless it is on one already.
 void GroupBatch::markDirty(uint32_t g, uint32_t bits) {
   Hot& h = hot(g);
-  if (h.dirty == 0) {
-    DirtyList* l = myDirtyList();
-    spinLock(l->mu);
-    if (l->v.empty()) l->firstNs.store(nowNs(), std::memory_order_relaxed);
-    l->v.push_back(g);
-    l->n.store(l->v.size(), std::memory_order_relaxed);
-    l->mu.store(0, std::memory_order_release);
-  }
   h.dirty |= bits;
+  // on this generation's list already: its pack takes the lock after us and sees the bits
+  if (ald(h.listed) == gen_.load(std::memory_order_acquire)) return;
+  DirtyList* l = myDirtyList();
+  Region rg(l->seq);
+  listIn(l, h, g, gen_.load(std::memory_order_acquire));
+}
+
+// commitAt's common case without the lock (see the threading note in jraft_host.h): a peer
+// with a slot, acks contiguous with its last one.  Everything else -- a peer without a slot, a
+// gap to check against the conf runs, an index past lastAppended (the exception), a group
+// being quiesced -- goes to the locked path, which decides it as before.
+int GroupBatch::ackFast(uint32_t g, int64_t first, int64_t last, uint32_t peer) {
+  DirtyList* l = myDirtyList();
+  Region rg(l->seq);
+  Hot& h = hot(g);
+  if (h.gate.load(std::memory_order_acquire)) return -1;
+  const int64_t pi = ald(h.pi);
+  if (pi == 0) return 0;     // BallotBox.java:101-103
+  if (last < pi) return 1;   // :104-106
+  if (last > ald(h.la)) return -1;
+  const uint32_t* sp = slotPeerOf(g);
+  uint32_t s = 0;
+  while (s < P_ && ald(sp[s]) != peer) ++s;
+  if (s == P_) return -1;
+  int64_t* mp = matchOf(g) + s;
+  const int64_t m = ald(*mp);
+  if (first > std::max(m + 1, pi)) return -1;
+  if (__builtin_expect(testing::fastPathHook != nullptr, 0)) testing::fastPathHook();
+  if (last > m) {
+    const uint32_t t = gen_.load(std::memory_order_acquire);
+    ast(*mp, last);
+    // after the match (the pack reads the stamp, then the match)
+    ast(slotUseOf(g)[s], stampOf(t, true));
+    listIn(l, h, g, t);
+  }
+  return 1;
+}
+
+// In a call region: g on this thread's list of generation t, unless it is on one already.
+void GroupBatch::listIn(DirtyList* l, Hot& h, uint32_t g, uint32_t t) {
+  if (ald(h.listed) == t) return;
+  std::vector<uint32_t>& v = l->v[t & 1u];
+  if (v.empty()) l->firstNs[t & 1u].store(nowNs(), std::memory_order_relaxed);
+  v.push_back(g);
+  l->n[t & 1u].store(v.size(), std::memory_order_relaxed);
+  ast(h.listed, t);
+}
+
+void GroupBatch::waitRegions() {
+  heavyBarrier();
+  std::lock_guard<std::mutex> lg(listsMu_);
+  for (auto& l : lists_) {
+    const uint32_t s = l->seq.load(std::memory_order_acquire);
+    if (!(s & 1u)) continue;
+    for (unsigned n = 0; l->seq.load(std::memory_order_acquire) == s; ++n) {
+      if (n < 256) __builtin_ia32_pause();
+      else std::this_thread::yield();
+    }
+  }
+}
+
+void GroupBatch::quiesce(uint32_t g) {
+  Hot& h = hot(g);
+  if (h.gate.load(std::memory_order_relaxed)) return;
+  h.gate.store(1, std::memory_order_relaxed);
+  waitRegions();
 }
 
 // Slots named by the masks of the group's live conf runs: their peers vote on pending entries.
@@ -546,15 +682,16 @@ int GroupBatch::slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved
     const uint32_t busy = liveMask(g) | reserved;
     for (uint32_t s = 0; s < P_; ++s)
       if (!((busy >> s) & 1u) &&  // least recently acked, in the 16-bit stamps' circular order
-          (victim < 0 || static_cast<int16_t>(static_cast<uint16_t>(su[s] - su[victim])) < 0))
+          (victim < 0 || stampOlder(ald(su[s]), ald(su[victim]))))
         victim = static_cast<int>(s);
     if (victim < 0) return -1;
+    quiesce(g);  // the slot's peer may be acking on the fast path
   }
-  sp[victim] = peer;
-  su[victim] = static_cast<uint16_t>(flushes_.load(std::memory_order_relaxed));
+  ast(sp[victim], peer);
+  ast(su[victim], stampOf(gen_.load(std::memory_order_acquire), false));
   int64_t* m = matchOf(g);
-  if (m[victim] != 0) {
-    m[victim] = 0;
+  if (ald(m[victim]) != 0) {
+    ast(m[victim], int64_t(0));
     markDirty(g, 1u << victim);
   }
   return victim;
@@ -616,8 +753,15 @@ void GroupBatch::packRange(Part& part, const uint32_t* groups, size_t n) {
     const uint32_t g = groups[i];
     Guard lk(*this, g);
     Hot& h = hot(g);
-    const uint32_t d = h.dirty;
+    uint32_t d = h.dirty;
     h.dirty = 0;
+    {  // slots the fast path acked in this generation or the next (stamp, then match)
+      const uint16_t* su = slotUseOf(g);
+      for (uint32_t s = 0; s < P_; ++s) {
+        const uint16_t u = ald(su[s]);
+        if (stampChangedIn(u, packGen_) || stampChangedIn(u, packGen_ + 1)) d |= 1u << s;
+      }
+    }
     const int64_t pi = h.pi, base = pi - 1;
     if (d & kDirtyHeader) {
       jrq_group_state& st = part.st.p[si++];
@@ -642,7 +786,7 @@ void GroupBatch::packRange(Part& part, const uint32_t* groups, size_t n) {
     const int64_t* m = matchOf(g);
     for (uint32_t b = d & 0xFFFFu; b; b &= b - 1) {
       const uint32_t s = static_cast<uint32_t>(__builtin_ctz(b));
-      const int64_t v = m[s] - base;
+      const int64_t v = ald(m[s]) - base;
       part.rec.p[ri++] = JRQ_REC(g, s, v > 0 ? v : 0);
     }
   }
@@ -700,11 +844,17 @@ uint32_t GroupBatch::flushLocked() {
       if (h.pi != 0 || h.lc != 0 || h.nruns != 0) bits |= kDirtyHeader;
       const int64_t* m = matchOf(g);
       for (uint32_t s = 0; s < P_; ++s)
-        if (m[s] != 0) bits |= 1u << s;
+        if (ald(m[s]) != 0) bits |= 1u << s;
       if (bits) markDirty(g, bits);
     }
   }
-  // swap out every thread's dirty list: callers go on marking groups for the next epoch
+  // end the generation and take its lists once its call regions have drained: callers go on
+  // listing groups (and the fast path stamping acks) in the next one
+  const uint32_t t = gen_.load(std::memory_order_acquire);
+  gen_.store(t + 1, std::memory_order_release);  // (orders the last swap of v[t & 1] before
+                                                 // its reuse in generation t + 2)
+  packGen_ = t;
+  waitRegions();
   size_t nl;
   {
     std::lock_guard<std::mutex> g(listsMu_);
@@ -713,10 +863,8 @@ uint32_t GroupBatch::flushLocked() {
     for (size_t i = 0; i < nl; ++i) {
       DirtyList& l = *lists_[i];
       work_[i].clear();
-      spinLock(l.mu);
-      std::swap(l.v, work_[i]);
-      l.n.store(0, std::memory_order_relaxed);
-      l.mu.store(0, std::memory_order_release);
+      std::swap(l.v[t & 1u], work_[i]);
+      l.n[t & 1u].store(0, std::memory_order_relaxed);
     }
   }
   std::vector<size_t> pre(nl + 1, 0);
@@ -855,7 +1003,7 @@ uint32_t GroupBatch::flushLocked() {
           ++nd0;
         }
       }
-      h.pi = c + 1;
+      ast(h.pi, c + 1);
       h.lc = c;
       dropDeadRuns(g);
       D.commits.push_back(Delivery::Commit{c, &waiter_[g]});
@@ -913,11 +1061,12 @@ void GroupBatch::startFlusher(const FlushPolicy& policy) {
         int64_t oldest = INT64_MAX;
         {
           std::lock_guard<std::mutex> g(listsMu_);
+          const uint32_t t = gen_.load(std::memory_order_acquire) & 1u;
           for (auto& l : lists_) {
-            const size_t k = l->n.load(std::memory_order_relaxed);
+            const size_t k = l->n[t].load(std::memory_order_relaxed);
             if (k) {
               pending += k;
-              oldest = std::min(oldest, l->firstNs.load(std::memory_order_relaxed));
+              oldest = std::min(oldest, l->firstNs[t].load(std::memory_order_relaxed));
             }
           }
         }
@@ -965,6 +1114,8 @@ bool BallotBox::init(const BallotBoxOptions& opts) {
 bool BallotBox::commitAt(int64_t first, int64_t last, const PeerId& peer) {
   GroupBatch& b = *batch_;
   const uint32_t id = peerId(peer);
+  const int r = b.ackFast(g_, first, last, id);
+  if (r >= 0) return r != 0;
   GroupBatch::Guard lk(b, g_);
   GroupBatch::Hot& h = b.hot(g_);
   const int64_t pi = h.pi;
@@ -976,14 +1127,15 @@ bool BallotBox::commitAt(int64_t first, int64_t last, const PeerId& peer) {
   // it, so Ballot.grant finds nothing (Ballot.java:100-127) and commitAt returns true
   if (s < 0) return true;
   int64_t& m = b.matchOf(g_)[s];
-  const int64_t lo = std::max(m + 1, pi);
+  const int64_t mv = ald(m);
+  const int64_t lo = std::max(mv + 1, pi);
   if (first > lo && b.gapCountsPeer(g_, s, lo, first - 1))
     throw std::logic_error("non-contiguous ack: the Replicator never skips entries");
-  if (last > m) {
-    m = last;
+  if (last > mv) {
+    ast(m, last);
     b.markDirty(g_, 1u << s);
+    ast(b.slotUseOf(g_)[s], stampOf(b.gen_.load(std::memory_order_acquire), false));
   }
-  b.slotUseOf(g_)[s] = static_cast<uint16_t>(b.flushes_.load(std::memory_order_relaxed));
   return true;
 }
 
@@ -999,18 +1151,25 @@ void BallotBox::clearPendingTasks() {
   {
     GroupBatch::Guard lk(b, g_);
     const GroupBatch::Hot& h = b.hot(g_);
-    decide = (h.dirty & 0xFFFFu) && h.pi != 0 && b.eng_;
+    // acks of the current generation (the locked path's dirty bits, the fast path's stamps)
+    bool acks = (h.dirty & 0xFFFFu) != 0;
+    const uint32_t t = b.gen_.load(std::memory_order_acquire);
+    for (uint32_t s = 0; s < b.P_; ++s) acks = acks || stampChangedIn(ald(b.slotUseOf(g_)[s]), t);
+    decide = acks && h.pi != 0 && b.eng_;
   }
   if (decide) b.flushLocked();
   std::unique_ptr<std::deque<std::pair<int64_t, std::function<void(bool)>>>> q;
   {
     GroupBatch::Guard lk(b, g_);
     GroupBatch::Hot& h = b.hot(g_);
+    // an ack of this leadership may still be on the fast path: it completes before pendingIndex
+    // drops to 0, and none starts after (resetPendingIndex relies on it)
+    if (h.pi != 0) b.quiesce(g_);
     q = std::move(b.closures_[g_]);
     h.nruns = 0;
     h.lastConf = 0;
-    h.pi = 0;
-    h.la = -1;
+    ast(h.pi, int64_t(0));
+    ast(h.la, int64_t(-1));
     b.markDirty(g_, GroupBatch::kDirtyHeader);
   }
   if (q)
@@ -1023,12 +1182,14 @@ bool BallotBox::resetPendingIndex(int64_t n) {
   GroupBatch::Hot& h = b.hot(g_);
   if (!(h.pi == 0 && h.la < h.pi)) return false;
   if (n <= h.lc) return false;
-  h.pi = n;
-  h.la = n - 1;
+  // (no fast-path ack can be in flight: pendingIndex is 0 -- never a leader, or stepped down
+  // through clearPendingTasks, which quiesced the group -- and the fast path writes nothing then)
+  ast(h.pi, n);
+  ast(h.la, n - 1);
   h.nruns = 0;
   h.lastConf = 0;
   // a new leader's replicators start over
-  std::fill(b.matchOf(g_), b.matchOf(g_) + b.P_, 0);
+  for (uint32_t s = 0; s < b.P_; ++s) ast(b.matchOf(g_)[s], int64_t(0));
   b.markDirty(g_, GroupBatch::kDirtyHeader | GroupBatch::kDirtyReset);
   return true;
 }
@@ -1095,7 +1256,7 @@ bool BallotBox::append(const Configuration& conf, const Configuration* oldConf, 
     b.dropDeadRuns(g_);
     b.markDirty(g_, GroupBatch::kDirtyHeader);
   }
-  h.la = idx + count - 1;
+  ast(h.la, idx + count - 1);
   b.markDirty(g_, GroupBatch::kDirtyLa);
   if (done) {  // ClosureQueue.appendPendingClosure (ClosureQueueImpl.java:98-105)
     auto& q = b.closures_[g_];

@@ -245,8 +245,17 @@ struct FlushPolicy {
 // setLastCommittedIndex): every BallotBox call may come from any thread, concurrently with
 // other calls and with flush().  Each group has its own lock (a one-byte spin lock: calls
 // are short), peers are interned in a lock-free-read process-wide table, and each calling
-// thread marks the groups it changes in its own dirty list, which flush() swaps out, so
-// callers keep recording acks for the next epoch while one is packed, decided and delivered.
+// thread lists the groups it changes in its own dirty list, which flush() takes, so callers
+// keep recording acks for the next epoch while one is packed, decided and delivered.
+// commitAt's common case -- a peer that has a slot acking entries contiguous with its last
+// ack -- takes no lock and no locked instruction: it raises the slot's match, stamps the slot
+// with the batch's generation and lists the group, inside a "call region" of its thread (a
+// counter of the thread's own); flush() starts a new generation and waits, behind one
+// membarrier(2), for every region of the old one to end, and the rare writers that move a
+// slot to another peer or reset a group's matches do the same under the group's lock.  Calls
+// for one (group, peer) must not overlap -- the Replicator makes them under its ThreadId lock
+// (Replicator.java:1155, 1391) -- overlapping ones could keep the lower of two acks (a later
+// commit, never a wrong one).
 // Flushes are serialised.  flush() packs and delivers on up to 16 threads; callbacks run
 // without the group's lock and may call commitAt / appendPendingTask* (on any group), but not
 // flush() or clearPendingTasks() of this batch (std::logic_error).
@@ -308,15 +317,20 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   // One group's record: what every API call and the flush touch, in one or two adjacent cache
   // lines (128 B at P = 5) instead of a word in each of nine arrays: the hot header, then
   // match[P] (int64, highest index acked per slot), slotPeer[P] (u32, interned PeerId of the
-  // slot), slotUse[P] (u16, flush count of the slot's last ack, mod 2^16: only orders the
-  // victims of a slot reassignment).  Its conf runs live apart (runs_: read when a conf changes
-  // or a run dies).
+  // slot), slotUse[P] (u16: the generation of the slot's last raising ack or assignment, mod
+  // 2^15, which orders the victims of a slot reassignment; bit 15 marks a fast-path ack that
+  // raised the match, which the pack of that generation or the next ships).  Its conf runs live apart (runs_: read when a conf changes or a run
+  // dies).  Fields the fast path reads or writes without the lock go through atomic accesses.
   struct Hot {
     std::atomic<uint8_t> lock;  // the group's one-byte spin lock
+    std::atomic<uint8_t> gate;  // set by a holder of the lock that moves slots or resets
+                                // matches: commitAt's fast path steps aside (quiesce)
     uint8_t nruns;              // conf runs of the pending queue
     uint8_t lastN, lastO;       // the last appended conf's peer counts (lastO 0xFF: no old
                                 // conf; lastN 0xFF: no cached conf)
-    uint32_t dirty;             // slots / lastAppended / header changed since the last pack
+    uint32_t dirty;             // lastAppended / header / slots changed under the lock since
+                                // the last pack (the fast path's acks are in the slot stamps)
+    uint32_t listed;            // the generation whose dirty list holds the group
     int64_t pi, lc, la;         // pendingIndex, lastCommittedIndex, lastAppended
     uint64_t lastConf;          // conf word of the last run (appends compare against it)
     uint64_t lastSlots;         // slot of the last conf's i-th peer, 4 bits each (<= 16 peers)
@@ -333,7 +347,11 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   }
 
   void lock(uint32_t g) const;
-  void unlock(uint32_t g) const { hot(g).lock.store(0, std::memory_order_release); }
+  void unlock(uint32_t g) const {
+    Hot& h = hot(g);
+    if (h.gate.load(std::memory_order_relaxed)) h.gate.store(0, std::memory_order_release);
+    h.lock.store(0, std::memory_order_release);
+  }
   struct Guard {  // the group's lock for a scope
     const GroupBatch& b;
     uint32_t g;
@@ -356,8 +374,18 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   bool gapCountsPeer(uint32_t g, int slot, int64_t lo, int64_t hi) const;
   void markDirty(uint32_t g, uint32_t bits);
   void dropDeadRuns(uint32_t g);
+  // commitAt's lock-free common case: 0 / 1 = its result, -1 = take the locked path
+  int ackFast(uint32_t g, int64_t first, int64_t last, uint32_t peer);
+  void listIn(DirtyList* l, Hot& h, uint32_t g, uint32_t t);
+  // under the group's lock, before moving a slot to another peer or resetting matches: no
+  // fast-path ack of the group is in flight or starts until the lock is released
+  void quiesce(uint32_t g);
+  // every call region that began before this returns has ended (flush: the old generation's
+  // lists and stamps are complete)
+  void waitRegions();
 
   DirtyList* myDirtyList();
+  DirtyList* myDirtyListSlow();  // a thread's first call in this batch, or a cache miss
   uint32_t flushLocked();
   void packRange(Part& part, const uint32_t* groups, size_t n);
   void relistAfterFailure();
@@ -381,9 +409,12 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   std::vector<std::vector<uint32_t>> work_;  // swapped-out dirty lists (buffers kept)
   std::vector<Part> parts_;
   std::vector<Delivery> deliveries_;
+  uint32_t packGen_ = 0;                  // the generation the running flush packs
   jrq_table* table_ = nullptr;
   PinnedBuf<uint64_t> changed_;
   std::atomic<uint64_t> flushes_{0};
+  // the dirty-list generation: flush() takes the lists of the generation it ends (1, 2, ...)
+  std::atomic<uint32_t> gen_{1};
   FlushStats stats_;
   std::unique_ptr<Pool> pool_;
   unsigned poolSize_ = 0;
@@ -391,5 +422,11 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   std::mutex errMu_;
   std::string flusherError_;              // what stopped the background flusher (rethrown once)
 };
+
+namespace testing {
+// Called inside commitAt's fast path between its reads and its writes when set (tests widen the
+// window a concurrent slot reassignment must not fall into).  Null in production.
+extern void (*fastPathHook)();
+}  // namespace testing
 
 }  // namespace jraft

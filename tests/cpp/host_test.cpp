@@ -9,6 +9,7 @@
 //   entity/LogEntryTest.java:95-125, util/CrcUtilTest.java:27-42
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <thread>
 #include <cstring>
@@ -782,6 +783,63 @@ static void testThrowingCallback(Engine& eng) {
     if (g != 3) CHECK(boxes[g].getLastCommittedIndex() == 5);
 }
 
+// commitAt's fast path against a step-down: peer 1's ack of entries 2..15 is held inside the
+// fast path (between its reads and its write, through the test hook) while another thread
+// steps the leader down.  clearPendingTasks must wait for it (quiesce): otherwise, as this
+// node becomes leader again with a shorter log (resetPendingIndex(10), entries 10..19 of the
+// new term), the held write lands on the new leadership's slot and counts as peer 1's ack of
+// entries it never received -- a commit of 10..19 with the leader's ack alone.
+namespace {
+std::atomic<int> g_hold{0};  // 1: the next fast-path ack parks (2 while parked) until 0
+}
+static void testFastPathStepDown(Engine& eng) {
+  auto batch = std::make_shared<GroupBatch>(&eng, 4, 3);
+  BallotBox box(batch, 2);
+  box.init({[](int64_t) {}});
+  Configuration c;
+  for (int p = 0; p < 3; ++p) c.peers.emplace_back("10.0.0.4", 6000 + p);
+  const PeerId p0("10.0.0.4", 6000), p1("10.0.0.4", 6001);
+  CHECK(box.resetPendingIndex(1));
+  CHECK(box.appendPendingTasks(c, nullptr, 100));
+  CHECK(box.commitAt(1, 1, p1));  // peer 1's slot exists: its next ack takes the fast path
+  batch->flush();
+  testing::fastPathHook = [] {
+    int one = 1;
+    if (g_hold.compare_exchange_strong(one, 2))
+      while (g_hold.load() == 2) std::this_thread::yield();
+  };
+  g_hold.store(1);
+  std::thread acker([&] { box.commitAt(2, 15, p1); });
+  while (g_hold.load() != 2) std::this_thread::yield();
+  std::atomic<bool> cleared{false};
+  std::thread stepDown([&] {
+    box.clearPendingTasks();
+    cleared.store(true);
+  });
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!cleared.load() && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200))
+    std::this_thread::yield();
+  const bool waited = !cleared.load();  // the step-down waited for the held ack
+  if (!waited) {  // (no quiesce) the new leadership starts while the old ack is still held
+    CHECK(box.resetPendingIndex(10));
+    CHECK(box.appendPendingTasks(c, nullptr, 10));
+    CHECK(box.commitAt(10, 19, p0));
+  }
+  g_hold.store(0);
+  acker.join();
+  stepDown.join();
+  testing::fastPathHook = nullptr;
+  if (waited) {
+    CHECK(box.resetPendingIndex(10));
+    CHECK(box.appendPendingTasks(c, nullptr, 10));
+    CHECK(box.commitAt(10, 19, p0));
+  }
+  batch->flush();
+  CHECK(waited);
+  CHECK(box.getLastCommittedIndex() == 0);  // 10..19 have the leader's ack only (a held ack
+                                            // landing late would commit 10..15)
+}
+
 // The append fast path reuses the group's last conf word only for the same peers in the same
 // split between conf and old conf: {a,b,c} then {a,b} + old {c} is a new run (Ballot.init with
 // oldQuorum 1), and entry 2 needs c's ack.
@@ -864,6 +922,7 @@ int main(int argc, char** argv) {
     tests.push_back({"testThrowingCallback", [&] { testThrowingCallback(e); }});
     tests.push_back({"testManyBatchesOneThread", [&] { testManyBatchesOneThread(e); }});
     tests.push_back({"testConfCacheSplit", [&] { testConfCacheSplit(e); }});
+    tests.push_back({"testFastPathStepDown", [&] { testFastPathStepDown(e); }});
   }
   for (auto& t : tests) {
     const int before = g_fail;

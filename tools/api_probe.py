@@ -21,13 +21,16 @@ OUT = os.path.join(ROOT, "tools", "_build")
 LIB = os.path.join(OUT, "libjraft_drive_fake.so")
 
 
-def build(flags="-O2", host_src=None):
+def build(flags="-O2 -fno-semantic-interposition", host_src=None):
     os.makedirs(OUT, exist_ok=True)
     srcs = [os.path.join(ROOT, p) for p in ("sofa-jraft_amd/host/jraft_drive.cpp",
                                             "sofa-jraft_amd/host/jraft_host.cpp",
                                             "tests/cpp/fake_jrq.cpp")]
-    if host_src:  # an A/B variant of the mirror (it includes "jraft_host.h" from its own dir)
-        srcs[1] = host_src
+    if host_src:  # an A/B variant of the mirror (it includes "jraft_host.h" from its own dir;
+        srcs[1] = host_src  # a jraft_drive.cpp beside it is built instead of the tree's)
+        drv = os.path.join(os.path.dirname(host_src), "jraft_drive.cpp")
+        if os.path.exists(drv):
+            srcs[0] = drv
     ora = os.path.join(OUT, "oracle_probe.o")
     subprocess.check_call(["gcc", "-O2", "-fPIC", "-std=c11", "-c",
                            os.path.join(ROOT, "oracle/jraft_oracle.c"), "-o", ora])
