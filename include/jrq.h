@@ -300,16 +300,20 @@ int jrq_table_check(jrq_table *t);
  * device-side snapshot / restore of the group table. */
 int jrq_table_copy(jrq_table *dst, const jrq_table *src);
 
-/* Device views of the table (e.g. last_committed as the rank's jrq_publish_committed_dev
- * send buffer, the node-wide getLastCommittedIndex snapshot). */
+/* Device views of the table.  The per-group fields live in tiles of tile_groups (256) groups:
+ * element g of a field is field[(g / tile_groups) * tile_stride + g % tile_groups] (each tile
+ * holds every field of its groups in one contiguous block: an epoch wave reads one block);
+ * match[p] starts at match + p * tile_groups. */
 typedef struct {
-    int64_t *match;          /* [num_peers][ld] */
+    int64_t *match;          /* match[p] row of tile 0 at match + p * tile_groups */
     int64_t *pending_index;  /* JRQ_PI_FOLLOWS_LC after a commit */
     int64_t *last_appended;
     int64_t *last_committed;
     uint64_t *conf;
-    uint64_t ld;
+    uint64_t ld;             /* row stride of the table's cold (per-run) fields */
     uint32_t G, num_peers;
+    uint32_t tile_groups;    /* 256 (JRQ_TABLE_SLICE) */
+    uint64_t tile_stride;    /* words from a tile to the next: 256 (num_peers + 4) */
 } jrq_table_view;
 int jrq_table_view_get(jrq_table *t, jrq_table_view *view_out);
 

@@ -1360,15 +1360,16 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   auto* t = new jrq_table();
   t->e = e;
   const uint64_t ld = (static_cast<uint64_t>(G) + 63) & ~63ull;  // pairs + 512-B rows
-  // rows (the state jrq_table_copy copies): match[P], pi, la, lc, conf, xstart[3], xconf[3],
-  // the flagged-entry slots flag_ent[waves][256][8] + flag_wcnt[waves] (u32); then the
-  // control word `invalid`
+  // the state jrq_table_copy copies: the hot tiles (256 groups each: match[P], pi, la, lc, conf
+  // as 256-word rows, JrqTableArgs), the cold rows xstart[3], xconf[3], the flagged-entry slots
+  // flag_ent[waves][256][8] + flag_wcnt[waves] (u32); then the control word `invalid`
   // (one 256-group range per epoch wave, rounded up to whole workgroups: every wave of the
   // grid reads its slots)
   const uint64_t ranges = (G + jrq::kTableSlice - 1) / jrq::kTableSlice;
   const uint64_t waves = (ranges + jrq::kTableBlockWaves - 1) / jrq::kTableBlockWaves * jrq::kTableBlockWaves;
   const uint64_t flag_words = waves * jrq::kFlagSlots * 8 + (waves + 1) / 2;
-  const uint64_t words = ld * (P + 4 + 2 * (jrq::kTableMaxRuns - 1)) + flag_words;
+  const uint64_t ts = static_cast<uint64_t>(P + 4) * jrq::kTableSlice;  // words per tile
+  const uint64_t words = waves * ts + ld * 2 * (jrq::kTableMaxRuns - 1) + flag_words;
   const size_t bytes = words * 8 + 64;
   t->slices = (G + JRQ_TABLE_SLICE - 1) / JRQ_TABLE_SLICE;
   if (hipMalloc(&t->mem, bytes) != hipSuccess || hipMemset(t->mem, 0, bytes) != hipSuccess ||
@@ -1382,11 +1383,12 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   int64_t* w = static_cast<int64_t*>(t->mem);
   JrqTableArgs& a = t->a;
   a.match = w;
-  a.pi = w + ld * P;
-  a.la = a.pi + ld;
-  a.lc = a.la + ld;
-  a.conf = reinterpret_cast<uint64_t*>(a.lc + ld);
-  a.xstart = reinterpret_cast<int64_t*>(a.conf + ld);
+  a.pi = w + jrq::kTableSlice * P;
+  a.la = a.pi + jrq::kTableSlice;
+  a.lc = a.la + jrq::kTableSlice;
+  a.conf = reinterpret_cast<uint64_t*>(a.lc + jrq::kTableSlice);
+  a.ts = ts;
+  a.xstart = w + waves * ts;
   a.xconf = reinterpret_cast<uint64_t*>(a.xstart + ld * (jrq::kTableMaxRuns - 1));
   a.flag_ent = reinterpret_cast<uint64_t*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
   a.flag_wcnt = reinterpret_cast<uint32_t*>(a.flag_ent + waves * jrq::kFlagSlots * 8);
@@ -1574,19 +1576,31 @@ int jrq_table_read(jrq_table* t, int64_t* pending_index, int64_t* last_appended,
   if (table_check(t)) return JRQ_E_INVALID;
   jrq_engine* e = t->e;
   DeviceGuard guard(e->device);
-  const size_t G = t->a.G, ld = t->a.ld, b = G * 8;
+  const size_t G = t->a.G;
   std::vector<int64_t> lc(G);
-  JRQ_HIP(e, hipMemcpyAsync(lc.data(), t->a.lc, b, hipMemcpyDeviceToHost, e->stream));
-  if (pending_index) JRQ_HIP(e, hipMemcpyAsync(pending_index, t->a.pi, b, hipMemcpyDeviceToHost, e->stream));
-  if (last_appended) JRQ_HIP(e, hipMemcpyAsync(last_appended, t->a.la, b, hipMemcpyDeviceToHost, e->stream));
+  // a tiled field back to G contiguous words: one 2-D copy of the whole tiles (256 words each,
+  // tile stride apart), one of the last partial tile
+  auto field = [&](int64_t* dst, const int64_t* row) -> hipError_t {
+    const size_t full = G / jrq::kTableSlice, rest = G % jrq::kTableSlice;
+    const size_t tb = jrq::kTableSlice * 8;
+    hipError_t r = hipSuccess;
+    if (full) r = hipMemcpy2DAsync(dst, tb, row, t->a.ts * 8, tb, full, hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess && rest)
+      r = hipMemcpyAsync(dst + full * jrq::kTableSlice, row + full * t->a.ts, rest * 8,
+                         hipMemcpyDeviceToHost, e->stream);
+    return r;
+  };
+  JRQ_HIP(e, field(lc.data(), t->a.lc));
+  if (pending_index) JRQ_HIP(e, field(pending_index, t->a.pi));
+  if (last_appended) JRQ_HIP(e, field(last_appended, t->a.la));
   if (match)
     for (uint32_t p = 0; p < t->a.P; ++p)
-      JRQ_HIP(e, hipMemcpyAsync(match + p * G, t->a.match + p * ld, b, hipMemcpyDeviceToHost, e->stream));
+      JRQ_HIP(e, field(match + p * G, t->a.match + p * jrq::kTableSlice));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   if (pending_index)
     for (size_t g = 0; g < G; ++g)
       if (pending_index[g] == JRQ_PI_FOLLOWS_LC) pending_index[g] = lc[g] + 1;
-  if (last_committed) std::memcpy(last_committed, lc.data(), b);
+  if (last_committed) std::memcpy(last_committed, lc.data(), G * 8);
   return JRQ_OK;
 }
 
@@ -1621,6 +1635,8 @@ int jrq_table_view_get(jrq_table* t, jrq_table_view* v) {
   v->last_committed = t->a.lc;
   v->conf = t->a.conf;
   v->ld = t->a.ld;
+  v->tile_groups = jrq::kTableSlice;
+  v->tile_stride = t->a.ts;
   v->G = t->a.G;
   v->num_peers = t->a.P;
   return JRQ_OK;

@@ -256,15 +256,22 @@ constexpr uint32_t kTableBlockWaves = 4;           // waves per epoch / flags wo
 constexpr int64_t kPiFollowsLc = INT64_MIN;        // JRQ_PI_FOLLOWS_LC
 constexpr uint32_t kFlagSlots = 256;               // flagged-entry slots per 256-group epoch wave
 }  // namespace jrq
+// The hot fields live in tiles of kTableSlice (256) groups, one tile per epoch wave: tile i
+// holds match[0..P-1], pendingIndex, lastAppended, lastCommitted, conf of groups [256 i,
+// 256 i + 256), each field as 256 consecutive words, so a wave's whole input is one contiguous
+// (8P + 32) * 256-B block (field-major rows over all groups ran 20 % slower:
+// tools/probes/streams_probe.hip).  The pointers below are the fields' rows in tile 0; element
+// g of a field is row[(g >> 8) * ts + (g & 255)] (tf()).
 struct JrqTableArgs {
-  int64_t* match;        // [P][ld]
-  int64_t* pi;           // [ld] pendingIndex, or kPiFollowsLc
-  int64_t* la;           // [ld]
-  int64_t* lc;           // [ld]
-  uint64_t* conf;        // [ld] run 0 conf word | JRQ_CONF_RUNS
+  int64_t* match;        // tile row of match[0]; match[p] at match + 256 p
+  int64_t* pi;           // pendingIndex, or kPiFollowsLc
+  int64_t* la;
+  int64_t* lc;
+  uint64_t* conf;        // run 0 conf word | JRQ_CONF_RUNS
+  uint64_t ts;           // words per tile: 256 (P + 4)
   int64_t* xstart;       // [jrq::kTableMaxRuns - 1][ld] extra run starts (INT64_MAX = unused)
   uint64_t* xconf;       // [kTableMaxRuns - 1][ld]
-  uint64_t ld;
+  uint64_t ld;           // row stride of xstart / xconf (cold fields: group-major rows)
   uint32_t G;            // groups (ld >= G rounded up to pairs; pad groups are not leaders)
   uint32_t P;
   uint32_t* invalid;     // records / headers skipped as invalid since the last jrq_table_check
@@ -275,6 +282,12 @@ struct JrqTableArgs {
                          // JRQ_CONF_RUNS as 64-B entries {group, run starts 1-3, conf words 0-3}
   uint32_t* flag_wcnt;   // [waves] how many
 };
+
+// Element g of a tiled hot field (its row in tile 0: t.pi, t.lc, t.match + 256 p, ...).
+template <class T>
+__host__ __device__ __forceinline__ T& tf(T* row, const JrqTableArgs& t, uint32_t g) {
+  return row[static_cast<size_t>(g >> 8) * t.ts + (g & 255u)];
+}
 
 // One group header as the ABI carries it (include/jrq.h jrq_group_state).
 struct JrqGroupState {

@@ -39,6 +39,17 @@ __device__ __forceinline__ i64x2 tld2o(const int64_t* base, uint32_t off) {
   return __builtin_nontemporal_load(reinterpret_cast<const gi64x2*>(b + off));
 }
 
+// Stores at byte offset `off` of a wave-uniform base, as tld2o loads (the base stays in SGPRs).
+typedef __attribute__((address_space(1))) i64x2 gi64x2w;
+typedef __attribute__((address_space(1))) int64_t gi64w;
+typedef __attribute__((address_space(1))) char gcharw;
+__device__ __forceinline__ void tst2o(int64_t* base, uint32_t off, i64x2 v);
+__device__ __forceinline__ void tst1o(int64_t* base, uint32_t off, int64_t v) {
+  gcharw* b = (gcharw*)base;
+  asm volatile("" : "+s"(b));
+  *reinterpret_cast<gi64w*>(b + off) = v;
+}
+
 // Cache policy of the epoch's stores (A/B knob, tools/ab_build.sh): nt -- plain stores measured
 // 2 % slower here (21.75 vs 22.14 us), while the pair kernel's are 1.5-7 % faster plain
 #ifndef JRQ_TABLE_NT_STORES
@@ -50,6 +61,15 @@ __device__ __forceinline__ void st_tab(T v, T* p) {
   __builtin_nontemporal_store(v, p);
 #else
   *p = v;
+#endif
+}
+__device__ __forceinline__ void tst2o(int64_t* base, uint32_t off, i64x2 v) {
+  gcharw* b = (gcharw*)base;
+  asm volatile("" : "+s"(b));
+#if JRQ_TABLE_NT_STORES
+  __builtin_nontemporal_store(v, reinterpret_cast<gi64x2w*>(b + off));
+#else
+  *reinterpret_cast<gi64x2w*>(b + off) = v;
 #endif
 }
 
@@ -66,8 +86,8 @@ __device__ __forceinline__ int64_t ent_field(const i64x2& v, uint32_t src, uint3
 // Writes of a committing group: lastCommitted, and pendingIndex -> JRQ_PI_FOLLOWS_LC once.
 __device__ __forceinline__ void table_commit_one(const JrqTableArgs& t, uint32_t g, int64_t pr,
                                                  int64_t out) {
-  t.lc[g] = out;
-  if (pr != kPiFollowsLc) t.pi[g] = kPiFollowsLc;
+  tf(t.lc, t, g) = out;
+  if (pr != kPiFollowsLc) tf(t.pi, t, g) = kPiFollowsLc;
 }
 
 // The epoch's changed list comes in fixed slices, one per 256-group wave range: wave w (groups
@@ -100,7 +120,7 @@ constexpr uint32_t kTableEpochBlock = 64 * kTableBlockWaves;
 // reloads the group.  No workgroup barrier, no atomics: each wave writes its own list slice and
 // count.
 template <int P>
-__global__ __launch_bounds__(kTableEpochBlock) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
+__global__ __launch_bounds__(kTableEpochBlock, 4) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
   constexpr uint32_t kWaves = kTableEpochBlock / 64;
   constexpr uint32_t kHand = 16;  // flagged groups per wave handed over through LDS
   constexpr uint32_t kEntLds = 4; // flagged-entry slots per wave copied to LDS up front
@@ -111,6 +131,7 @@ __global__ __launch_bounds__(kTableEpochBlock) JRQ_SGPRS_8WAVES void table_epoch
   const uint32_t wid = blockIdx.x * kWaves + w;
   const uint32_t gA = wid * kTableSlice + 2u * lane;  // pair A = (gA, gA + 1), B = A + 128
   uint64_t* const slice = t.changed + static_cast<size_t>(wid) * kTableSlice;
+  int64_t* const tile = t.match + static_cast<size_t>(__builtin_amdgcn_readfirstlane(wid)) * t.ts;
   // The wave's first four flagged-entry slots are loaded up front, beside the single-conf loads,
   // whatever the wave's count: 16 B per lane on lanes 0-15 (entry i = lanes 4i .. 4i + 3), read
   // by the walk through lane shuffles.  (The count is the wave's own ballot of its flagged
@@ -135,13 +156,14 @@ __global__ __launch_bounds__(kTableEpochBlock) JRQ_SGPRS_8WAVES void table_epoch
     for (int h = 0; h < 2; ++h) {
       const uint32_t g = gA + 128u * h;
       live[h] = g < t.G;
-      const uint32_t go = (live[h] ? g : 0u) * 8u;  // (g < 2^27)
-      pr[h] = tld2o(t.pi, go);
-      lc[h] = tld2o(t.lc, go);
-      la[h] = tld2o(t.la, go);
-      cw[h] = tld2o(reinterpret_cast<const int64_t*>(t.conf), go);
+      // the wave's tile (one contiguous block: its groups' every hot field), pair offset in it
+      const uint32_t go = (2u * lane + 128u * h) * 8u;
+      pr[h] = tld2o(tile + P * 256, go);
+      lc[h] = tld2o(tile + (P + 2) * 256, go);
+      la[h] = tld2o(tile + (P + 1) * 256, go);
+      cw[h] = tld2o(tile + (P + 3) * 256, go);
 #pragma unroll
-      for (int p = 0; p < P; ++p) mv[h][p] = tld2o(t.match + static_cast<size_t>(p) * t.ld, go);
+      for (int p = 0; p < P; ++p) mv[h][p] = tld2o(tile + p * 256, go);
     }
     uint32_t kbase = 0;  // hand-off ranks: A.x, A.y, B.x, B.y groups in the flags kernel's order
 #pragma unroll
@@ -191,17 +213,18 @@ __global__ __launch_bounds__(kTableEpochBlock) JRQ_SGPRS_8WAVES void table_epoch
   for (int h = 0; h < 2; ++h) {
     const uint32_t g = gA + 128u * h;
     const bool ca = c[2 * h], cb = c[2 * h + 1];
+    const uint32_t go = (2u * lane + 128u * h) * 8u;  // groups g, g + 1 in the wave's tile
     if (ca && cb) {
       i64x2 v;
       v.x = o[2 * h];
       v.y = o[2 * h + 1];
-      st_tab(v, reinterpret_cast<i64x2*>(t.lc + g));
+      tst2o(tile + (P + 2) * 256, go, v);
     } else {
-      if (ca) t.lc[g] = o[2 * h];
-      if (cb) t.lc[g + 1] = o[2 * h + 1];
+      if (ca) tst1o(tile + (P + 2) * 256, go, o[2 * h]);
+      if (cb) tst1o(tile + (P + 2) * 256, go + 8u, o[2 * h + 1]);
     }
-    if (ca && wpi[2 * h]) t.pi[g] = kPiFollowsLc;
-    if (cb && wpi[2 * h + 1]) t.pi[g + 1] = kPiFollowsLc;
+    if (ca && wpi[2 * h]) tst1o(tile + P * 256, go, kPiFollowsLc);
+    if (cb && wpi[2 * h + 1]) tst1o(tile + P * 256, go + 8u, kPiFollowsLc);
     const uint64_t ba = __ballot(ca), bb = __ballot(cb);
     if (ca) slice[cnt + __popcll(ba & below)] = (static_cast<uint64_t>(d[2 * h]) << 32) | g;
     if (cb) slice[cnt + __popcll(ba) + __popcll(bb & below)] = (static_cast<uint64_t>(d[2 * h + 1]) << 32) | (g + 1);
@@ -271,11 +294,11 @@ __global__ __launch_bounds__(kTableEpochBlock) JRQ_SGPRS_8WAVES void table_epoch
 #pragma unroll
         for (int p = 0; p < P; ++p) hm[p] = hs[3 + p];
       } else {  // more flagged groups than hand-off slots: reload (rare)
-        hpr = t.pi[h];
-        hlc = t.lc[h];
-        hla = t.la[h];
+        hpr = tf(t.pi, t, h);
+        hlc = tf(t.lc, t, h);
+        hla = tf(t.la, t, h);
 #pragma unroll
-        for (int p = 0; p < P; ++p) hm[p] = t.match[static_cast<size_t>(p) * t.ld + h];
+        for (int p = 0; p < P; ++p) hm[p] = tf(t.match + p * 256, t, h);
       }
       pi = hpr == kPiFollowsLc ? hlc + 1 : hpr;
       if (pi == 0) {
@@ -341,14 +364,14 @@ __global__ __launch_bounds__(kTableEpochBlock) JRQ_SGPRS_8WAVES void table_epoch
       int64_t out = 0, pr = 0, pi = 0, lc = 0;
       uint8_t st = 0;
       if (mine) {
-        pr = t.pi[h];
-        lc = t.lc[h];
-        const int64_t la = t.la[h];
+        pr = tf(t.pi, t, h);
+        lc = tf(t.lc, t, h);
+        const int64_t la = tf(t.la, t, h);
         int64_t m[P];
 #pragma unroll
-        for (int p = 0; p < P; ++p) m[p] = t.match[static_cast<size_t>(p) * t.ld + h];
+        for (int p = 0; p < P; ++p) m[p] = tf(t.match + p * 256, t, h);
         pi = pr == kPiFollowsLc ? lc + 1 : pr;
-        decide_single<P>(pi, la, lc, t.conf[h], m, out, st);
+        decide_single<P>(pi, la, lc, tf(t.conf, t, h), m, out, st);
         if (t.status) t.status[h] = st;
       }
       const bool commit = mine && out > lc;
@@ -423,7 +446,7 @@ __global__ __launch_bounds__(kFlagBlock) void table_flags_kernel(JrqTableArgs t)
     int64_t* e = ent + k * 8;
     e[0] = h;
     for (int r = 1; r < kTableMaxRuns; ++r) e[r] = t.xstart[static_cast<size_t>(r - 1) * t.ld + h];
-    e[4] = static_cast<int64_t>(t.conf[h] & ~kConfRuns);
+    e[4] = static_cast<int64_t>(tf(t.conf, t, h) & ~kConfRuns);
     for (int r = 1; r < kTableMaxRuns; ++r)
       e[4 + r] = static_cast<int64_t>(t.xconf[static_cast<size_t>(r - 1) * t.ld + h]);
   };
@@ -433,7 +456,7 @@ __global__ __launch_bounds__(kFlagBlock) void table_flags_kernel(JrqTableArgs t)
     const uint32_t g = gA + 128u * h;
     bool f0 = false, f1 = false;
     if (g < t.G) {
-      const i64x2 cw = tld2(reinterpret_cast<const int64_t*>(t.conf) + g);
+      const i64x2 cw = tld2(reinterpret_cast<const int64_t*>(&tf(t.conf, t, g)));
       f0 = static_cast<uint64_t>(cw.x) >> 63;
       f1 = (static_cast<uint64_t>(cw.y) >> 63) && g + 1 < t.G;
     }
@@ -461,11 +484,11 @@ __global__ __launch_bounds__(256) void table_states_kernel(JrqTableArgs t, const
     atomicAdd(t.invalid, 1u);
     return;
   }
-  t.pi[g] = st.pending_index;
-  t.la[g] = st.last_appended;
-  t.lc[g] = st.last_committed;
+  tf(t.pi, t, g) = st.pending_index;
+  tf(t.la, t, g) = st.last_appended;
+  tf(t.lc, t, g) = st.last_committed;
   const uint64_t c0 = nr ? (st.run_conf[0] & ~kConfRuns) : 0;
-  t.conf[g] = c0 | (nr > 1 ? kConfRuns : 0ull);  // (table_flags_kernel lists the flagged)
+  tf(t.conf, t, g) = c0 | (nr > 1 ? kConfRuns : 0ull);  // (table_flags_kernel lists the flagged)
 #pragma unroll
   for (int k = 1; k < kTableMaxRuns; ++k) {
     const size_t o = static_cast<size_t>(k - 1) * t.ld + g;
@@ -473,7 +496,7 @@ __global__ __launch_bounds__(256) void table_states_kernel(JrqTableArgs t, const
     t.xconf[o] = static_cast<uint32_t>(k) < nr ? (st.run_conf[k] & ~kConfRuns) : 0ull;
   }
   if (st.flags & 1u)  // JRQ_STATE_RESET_MATCH: a new leader's replicators start over
-    for (uint32_t p = 0; p < t.P; ++p) t.match[static_cast<size_t>(p) * t.ld + g] = pi - 1;
+    for (uint32_t p = 0; p < t.P; ++p) tf(t.match + p * 256, t, g) = pi - 1;
 }
 
 // 8-byte update records (include/jrq.h JRQ_REC): value relative to the group's pendingIndex.
@@ -489,19 +512,19 @@ __global__ __launch_bounds__(256) void table_recs_kernel(JrqTableArgs t, const u
     atomicAdd(t.invalid, 1u);
     return;
   }
-  const int64_t pr = t.pi[g], lc = t.lc[g];
+  const int64_t pr = tf(t.pi, t, g), lc = tf(t.lc, t, g);
   const int64_t pi = pr == kPiFollowsLc ? lc + 1 : pr;
   const int64_t val = pi - 1 + static_cast<int64_t>(v);
   if (f == 16u) {
     // entries pending on a group without a conf run (conf word 0: no header named one) could
     // never be decided as the reference decides them: refused and counted like any bad record
-    if (t.conf[g] == 0 && pi != 0 && val >= pi) {
+    if (tf(t.conf, t, g) == 0 && pi != 0 && val >= pi) {
       atomicAdd(t.invalid, 1u);
       return;
     }
-    t.la[g] = val;
+    tf(t.la, t, g) = val;
   } else {
-    t.match[static_cast<size_t>(f) * t.ld + g] = val;
+    tf(t.match + f * 256, t, g) = val;
   }
 }
 

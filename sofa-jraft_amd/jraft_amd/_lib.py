@@ -72,7 +72,7 @@ class TableView(C.Structure):
     _fields_ = [("match", C.c_void_p), ("pending_index", C.c_void_p),
                 ("last_appended", C.c_void_p), ("last_committed", C.c_void_p),
                 ("conf", C.c_void_p), ("ld", C.c_uint64), ("G", C.c_uint32),
-                ("num_peers", C.c_uint32)]
+                ("num_peers", C.c_uint32), ("tile_groups", C.c_uint32), ("tile_stride", C.c_uint64)]
 
 
 def rec(group, field, v):

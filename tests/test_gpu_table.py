@@ -194,6 +194,18 @@ def test_device_variant_and_view(engine, oracle):
     np.testing.assert_array_equal(got, ce)
     v = t.view()
     assert v.G == G and v.num_peers == P and v.ld >= G and v.last_committed
+    assert v.tile_groups == 256 and v.tile_stride == 256 * (P + 4)
+    # lastCommitted of group g through the view's tiled addressing
+    lcd = torch.empty(((G + 255) // 256) * v.tile_stride, dtype=torch.int64, device=dev)
+    src = torch.cuda.ByteStorage  # (the view is a raw device pointer: read it through a copy)
+    import ctypes
+    from jraft_amd import _lib as L
+    hip = ctypes.CDLL("libamdhip64.so")
+    assert hip.hipMemcpy(ctypes.c_void_p(lcd.data_ptr()), ctypes.c_void_p(v.match), lcd.numel() * 8, 3) == 0
+    words = lcd.cpu().numpy()
+    g = np.arange(G)
+    lc_view = words[(g // 256) * v.tile_stride + (P + 2) * 256 + g % 256]
+    np.testing.assert_array_equal(lc_view, ce)
     np.testing.assert_array_equal(t.read()["last_committed"], ce)
     t.close()
 
