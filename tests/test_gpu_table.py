@@ -197,9 +197,7 @@ def test_device_variant_and_view(engine, oracle):
     assert v.tile_groups == 256 and v.tile_stride == 256 * (P + 4)
     # lastCommitted of group g through the view's tiled addressing
     lcd = torch.empty(((G + 255) // 256) * v.tile_stride, dtype=torch.int64, device=dev)
-    src = torch.cuda.ByteStorage  # (the view is a raw device pointer: read it through a copy)
-    import ctypes
-    from jraft_amd import _lib as L
+    import ctypes  # (the view holds raw device pointers: read the tiles through hipMemcpy)
     hip = ctypes.CDLL("libamdhip64.so")
     assert hip.hipMemcpy(ctypes.c_void_p(lcd.data_ptr()), ctypes.c_void_p(v.match), lcd.numel() * 8, 3) == 0
     words = lcd.cpu().numpy()
