@@ -420,11 +420,14 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
     cfg = "C3" if world == 1 else "C4"
     P = W.CONFIGS[cfg]["peers"]
     Gtot = G * world
-    epochs = []
+    epochs, tiled = [], []
     for e in range(QUORUM_EPOCH_BUFFERS):
         b = W.quorum_batch(cfg, groups=G, group_offset=rank * G,
                            seed=(W.SEED_BASE ^ int(cfg[1])) + 7919 * e)
         epochs.append({k: to_dev(v, dev) for k, v in b.items()})
+        # the same epoch in the resident table's tile layout (jrq_quorum_epoch_tiles_dev)
+        tiled.append(to_dev(W.to_tiles(b["match"], b["pending_index"], b["last_appended"],
+                                       b["last_committed"], b["conf"]), dev))
     k = D.per_rank(Gtot, world)
     local = torch.empty(k, dtype=torch.int64, device=dev)
     status = torch.empty(G, dtype=torch.uint8, device=dev)
@@ -440,9 +443,12 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
 
     # one prepared launch per epoch buffer (arguments resolved once, as a C / JNI host keeps
     # its jrq_group_batch): the step loop then costs the GPU epoch, not Python marshalling
-    launchers = [eng.quorum_epoch_launcher(t["match"], t["pending_index"], t["last_appended"],
-                                           t["last_committed"], t["conf"], local, status)
-                 for t in epochs]
+    # The headline launches the epoch on tiled inputs (each wave reads one contiguous block:
+    # DESIGN.md §4.1); the same epochs from rows (jrq_quorum_epoch_dev) are timed beside it.
+    rows = [eng.quorum_epoch_launcher(t["match"], t["pending_index"], t["last_appended"],
+                                      t["last_committed"], t["conf"], local, status)
+            for t in epochs]
+    launchers = [eng.quorum_epoch_tiles_launcher(tt, P, G, local, status) for tt in tiled]
 
     def epoch_fn(i, out):
         if out is local:
@@ -458,6 +464,8 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
     se = D.ShardedEpochs(Gtot, world, rank, epoch_fn, allgather, local, snapshot,
                          publish_every=args.publish_every)
     # kernel only (HIP events on the engine's stream)
+    rows_ms, _ = ctx.timed(lambda i: rows[i % QUORUM_EPOCH_BUFFERS]())
+    rows_ms = max_over_ranks(rows_ms)
     k_ms, _ = ctx.timed(lambda i: epoch_fn(i, local))
     pub_ms = None
     k_ms_max = max_over_ranks(k_ms)
@@ -493,11 +501,15 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
                                          b["conf"][idx], chunk=1024)
         ok = bool(np.array_equal(local.cpu().numpy()[idx], ce))
     bpg = quorum_bytes_per_group(P)
-    rl = roofline(bpg * G, k_ms, kernel="quorum_epoch_pair_kernel<5, false>", bytes_per_group=bpg,
+    rl = roofline(bpg * G, k_ms, kernel="quorum_epoch_pair_kernel<5, false, true>", bytes_per_group=bpg,
                   survey_bytes_per_group=8 * P + 38,
                   frac_survey_bytes=(8 * P + 38) * G / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                   timing="one HIP event pair around --steps back-to-back launches / steps",
-                  **pmc_traffic("quorum", "quorum_epoch_pair_kernel<5, false>"))
+                  inputs="tiles (jrq_quorum_epoch_tiles_dev)",
+                  **pmc_traffic("quorum", "quorum_epoch_pair_kernel<5, false, true>"))
+    rl_rows = roofline(bpg * G, rows_ms, kernel="quorum_epoch_pair_kernel<5, false, false>",
+                       inputs="rows (jrq_quorum_epoch_dev)",
+                       **pmc_traffic("quorum", "quorum_epoch_pair_kernel<5, false, false>"))
     return {
         "value": value, "elapsed": elapsed, "cfg": cfg, "G": G, "P": P, "roofline": rl,
         "multi_gpu": {"rccl_nranks": nranks, "publish_every": args.publish_every,
@@ -506,6 +518,7 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
                       "kernel_only_decisions_per_s": Gtot / (k_ms_max * 1e-3),
                       "snapshot_bytes": 8 * k * world},
         "bit_exact_vs_oracle_4096_groups": ok,
+        "rows_entry_point": rl_rows,
     }
 
 
@@ -1498,6 +1511,10 @@ def compact_line(full: dict, detail_path: str | None = DETAIL_FILE) -> dict:
                              "frac": _r(full["roofline"].get("frac"), 3),
                              "traffic_ratio": (_roof_summary(full["roofline"]) or {}).get("traffic_ratio"),
                              "bit_exact": full.get("bit_exact_vs_oracle_4096_groups")}
+    qr = full.get("quorum_rows")
+    if qr:  # the same epochs from rows (jrq_quorum_epoch_dev)
+        legs["quorum_C3_rows"] = {"ms": _r(qr.get("kernel_ms"), 5), "frac": _r(qr.get("frac"), 3),
+                                  "traffic_ratio": (_roof_summary(qr) or {}).get("traffic_ratio")}
     t = full.get("resident_table")
     if t:
         legs["table"] = _leg_summary(t, "kernel_ms")
@@ -1651,6 +1668,7 @@ def main():
                 "groups_per_gpu": G, "peers": q["P"], "epoch_buffers": QUORUM_EPOCH_BUFFERS,
                 "parallelism": f"groupId shards x{world}"},
             "roofline": q["roofline"], "multi_gpu": q["multi_gpu"],
+            "quorum_rows": q["rows_entry_point"],
             "bit_exact_vs_oracle_4096_groups": q["bit_exact_vs_oracle_4096_groups"]})
     if "table" in legs:
         pair_ms = line.get("roofline", {}).get("kernel_ms")

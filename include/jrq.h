@@ -170,6 +170,24 @@ int jrq_quorum_epoch_dev(jrq_engine *e, const jrq_group_batch *in_dev, int64_t *
 int jrq_quorum_epoch(jrq_engine *e, const jrq_group_batch *in_host, int64_t *committed_out,
                      uint8_t *status_out, uint32_t G);
 
+/* The same epoch with the per-group inputs in tiles of 256 groups -- the resident table's
+ * layout (jrq_table_view): tile i holds match[0..num_peers-1], pending_index, last_appended,
+ * last_committed, conf of groups [256 i, 256 i + 256), each field as 256 consecutive int64
+ * words, so a tile is 256 (num_peers + 4) words and the tiles sit back to back from `tiles`
+ * (G rounded up to whole tiles).  A wave then reads one contiguous block instead of num_peers
+ * + 4 rows.  The conf runs and the outputs are as jrq_quorum_epoch_dev's.
+ * tiles and committed_out 16-B aligned, status_out 2-B aligned, G >= 2 (JRQ_E_INVALID
+ * otherwise). */
+typedef struct {
+    const int64_t *tiles;
+    uint32_t num_peers;
+    const uint32_t *run_off;    /* nullable: no group flagged JRQ_CONF_RUNS */
+    const int64_t *run_start;
+    const uint64_t *run_conf;
+} jrq_group_tiles;
+int jrq_quorum_epoch_tiles_dev(jrq_engine *e, const jrq_group_tiles *in_dev, int64_t *committed_out_dev,
+                               uint8_t *status_out_dev, uint32_t G);
+
 /* K successive epochs of the same G groups in one launch (the launch-bound small-G case,
  * e.g. C2's 10k groups; SURVEY.md §7 hard part 4).  Epoch k reads
  *   match + k*match_epoch_ld   (rows of in->match_ld, as jrq_quorum_epoch)

@@ -569,7 +569,7 @@ int jrq_quorum_epoch_dev(jrq_engine* e, const jrq_group_batch* in, int64_t* comm
       (in->run_off && (!in->run_start || !in->run_conf)) || in->match_ld < G)
     return fail(e, JRQ_E_INVALID, "missing array or match_ld < G");
   DeviceGuard guard(e->device);
-  JrqQuorumArgs a;
+  JrqQuorumArgs a{};
   a.match = in->match;
   a.pending_index = in->pending_index;
   a.last_appended = in->last_appended;
@@ -584,6 +584,38 @@ int jrq_quorum_epoch_dev(jrq_engine* e, const jrq_group_batch* in, int64_t* comm
   a.status = status_out;
   a.G = G;
   // enough 256-thread blocks for ~8 per CU, grid-stride beyond
+  JRQ_HIP(e, jrq_launch_quorum(&a, e->num_cus, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_quorum_epoch_tiles_dev(jrq_engine* e, const jrq_group_tiles* in, int64_t* committed_out,
+                               uint8_t* status_out, uint32_t G) {
+  if (!e || !in) return e ? fail(e, JRQ_E_INVALID, "null batch") : JRQ_E_INVALID;
+  if (G == 0) return JRQ_OK;
+  if (in->num_peers == 0 || in->num_peers > JRQ_MAX_PEERS)
+    return fail(e, JRQ_E_INVALID, "num_peers %u outside 1..%d", in->num_peers, JRQ_MAX_PEERS);
+  if (!in->tiles || !committed_out || !status_out || (in->run_off && (!in->run_start || !in->run_conf)))
+    return fail(e, JRQ_E_INVALID, "missing array");
+  if (G < 2 || (reinterpret_cast<uintptr_t>(in->tiles) & 15u) || (reinterpret_cast<uintptr_t>(committed_out) & 15u) ||
+      (reinterpret_cast<uintptr_t>(status_out) & 1u))
+    return fail(e, JRQ_E_INVALID, "tiles / committed_out not 16-B aligned, status_out odd or G < 2");
+  DeviceGuard guard(e->device);
+  const uint32_t P = in->num_peers;
+  JrqQuorumArgs a{};
+  a.match = in->tiles;
+  a.pending_index = in->tiles + 256u * P;
+  a.last_appended = a.pending_index + 256;
+  a.last_committed = a.last_appended + 256;
+  a.conf = reinterpret_cast<const uint64_t*>(a.last_committed + 256);
+  a.ts = 256ull * (P + 4);
+  a.run_off = in->run_off;
+  a.run_start = in->run_start;
+  a.run_conf = in->run_conf;
+  a.num_peers = P;
+  a.match_ld = 0;
+  a.committed = committed_out;
+  a.status = status_out;
+  a.G = G;
   JRQ_HIP(e, jrq_launch_quorum(&a, e->num_cus, e->stream));
   return JRQ_OK;
 }

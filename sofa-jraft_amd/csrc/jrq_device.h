@@ -246,6 +246,8 @@ struct JrqQuorumArgs {
   int64_t* committed;
   uint8_t* status;
   uint32_t G;
+  uint64_t ts;  // 0: the inputs are rows; else words per 256-group tile (the fields' rows in
+                // tile 0 above, match[p] at match + 256 p: jrq_quorum_epoch_tiles_dev)
 };
 
 // Resident group table (table.hip; include/jrq.h jrq_table).

@@ -137,8 +137,18 @@ constexpr uint32_t kPairBlock = 512;
 #define JRQ_PAIR_XCD_TILES 0
 #endif
 
-template <int P, bool kRuns>
+// kTiles: the inputs in the resident table's tiles (JrqQuorumArgs::ts != 0: 256-group tiles,
+// every field of a tile's groups in one contiguous block; jrq_quorum_epoch_tiles_dev), the
+// outputs as rows.  A wave's pairs sit in one half of one tile.
+template <int P, bool kRuns, bool kTiles>
 __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
+  // word of group g in a field's row (tiles: the field's row in tile 0)
+  auto at = [&](uint32_t g) -> size_t {
+    return kTiles ? static_cast<size_t>(g >> 8) * a.ts + (g & 255u) : static_cast<size_t>(g);
+  };
+  auto mrow = [&](int p) -> const int64_t* {
+    return a.match + (kTiles ? static_cast<size_t>(p) * 256u : static_cast<size_t>(p) * a.match_ld);
+  };
   constexpr uint32_t kWaves = kPairBlock / 64;
   constexpr uint32_t kHand = 16;
   __shared__ int64_t hand[kRuns ? kWaves : 1][kHand][P + 3];  // {pi, lc, la, match[P]}
@@ -160,13 +170,14 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
   bool slow = false;  // a group outside decide_single_rel's domain (never in a real batch)
   if (t < pairs) {
     const uint32_t g = t << 1;
-    const i64x2 pi = ld2nt(a.pending_index + g);
-    const i64x2 lc = ld2nt(a.last_committed + g);
-    const i64x2 la = ld2nt(a.last_appended + g);
-    const i64x2 cw = ld2nt(reinterpret_cast<const int64_t*>(a.conf) + g);
+    const size_t gi = at(g);
+    const i64x2 pi = ld2nt(a.pending_index + gi);
+    const i64x2 lc = ld2nt(a.last_committed + gi);
+    const i64x2 la = ld2nt(a.last_appended + gi);
+    const i64x2 cw = ld2nt(reinterpret_cast<const int64_t*>(a.conf) + gi);
     i64x2 m[P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) m[p] = ld2nt(a.match + static_cast<size_t>(p) * a.match_ld + g);
+    for (int p = 0; p < P; ++p) m[p] = ld2nt(mrow(p) + gi);
     f0 = kRuns && (static_cast<uint64_t>(cw.x) & kConfRuns);
     f1 = kRuns && (static_cast<uint64_t>(cw.y) & kConfRuns);
     int64_t m0[P], m1[P];
@@ -233,11 +244,11 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
 #pragma unroll
         for (int p = 0; p < P; ++p) hm[p] = hs[3 + p];
       } else if (act) {  // more flagged groups than hand-off slots: reload (rare)
-        hpi = a.pending_index[h];
-        hlc = a.last_committed[h];
-        hla = a.last_appended[h];
+        hpi = a.pending_index[at(h)];
+        hlc = a.last_committed[at(h)];
+        hla = a.last_appended[at(h)];
 #pragma unroll
-        for (int p = 0; p < P; ++p) hm[p] = a.match[static_cast<size_t>(p) * a.match_ld + h];
+        for (int p = 0; p < P; ++p) hm[p] = mrow(p)[at(h)];
       }
       int64_t cand = kI64Min;
       uint8_t st = 0;
@@ -270,14 +281,14 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
   if (__builtin_expect(__ballot(slow) != 0, 0) && slow) {
 #pragma unroll 1
     for (uint32_t g = t << 1; g < (t << 1) + 2; ++g) {
-      if (kRuns && (a.conf[g] & kConfRuns)) continue;  // (the walk decided it, exactly)
+      if (kRuns && (a.conf[at(g)] & kConfRuns)) continue;  // (the walk decided it, exactly)
       int64_t m[P];
 #pragma unroll
-      for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
+      for (int p = 0; p < P; ++p) m[p] = mrow(p)[at(g)];
       int64_t out;
       uint8_t st;
-      decide_single<P>(a.pending_index[g], a.last_appended[g], a.last_committed[g], a.conf[g], m,
-                       out, st);
+      decide_single<P>(a.pending_index[at(g)], a.last_appended[at(g)], a.last_committed[at(g)],
+                       a.conf[at(g)], m, out, st);
       a.committed[g] = out;
       a.status[g] = st;
     }
@@ -287,11 +298,11 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
     const uint32_t g = a.G - 1;
     int64_t m[P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) m[p] = a.match[static_cast<size_t>(p) * a.match_ld + g];
+    for (int p = 0; p < P; ++p) m[p] = mrow(p)[at(g)];
     int64_t out;
     uint8_t st;
-    decide<P>(a, g, a.pending_index[g], a.last_appended[g], a.last_committed[g], a.conf[g], m,
-              out, st);
+    decide<P>(a, g, a.pending_index[at(g)], a.last_appended[at(g)], a.last_committed[at(g)],
+              a.conf[at(g)], m, out, st);
     a.committed[g] = out;
     a.status[g] = st;
   }
@@ -524,6 +535,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
                     al16(a.last_appended) && al16(a.last_committed) && al16(a.conf) &&
                     al16(a.committed) && (reinterpret_cast<uintptr_t>(a.status) & 1u) == 0 &&
                     a.G >= 2;
+  if (a.ts && !pair) return hipErrorInvalidValue;  // (tiled inputs: the pair kernel only)
   // pair kernel: one lane per two groups, the whole grid at once; scalar kernel: one lane per
   // group, at most 8 workgroups per CU, grid-stride beyond
   const uint64_t lanes = pair ? (a.G >> 1) : a.G;
@@ -535,10 +547,14 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
   switch (args->num_peers) {
 #define JRQ_CASE(P)                                                                      \
   case P:                                                                                \
-    if (pair && a.run_off)                                                               \
-      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, true>), grid, blk, 0, stream, *args); \
+    if (pair && a.ts && a.run_off)                                                       \
+      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, true, true>), grid, blk, 0, stream, *args); \
+    else if (pair && a.ts)                                                               \
+      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, false, true>), grid, blk, 0, stream, *args); \
+    else if (pair && a.run_off)                                                          \
+      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, true, false>), grid, blk, 0, stream, *args); \
     else if (pair)                                                                       \
-      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, false>), grid, blk, 0, stream, *args); \
+      hipLaunchKernelGGL((jrq::quorum_epoch_pair_kernel<P, false, false>), grid, blk, 0, stream, *args); \
     else                                                                                 \
       hipLaunchKernelGGL(jrq::quorum_epoch_kernel<P>, grid, blk, 0, stream, *args);      \
     break;

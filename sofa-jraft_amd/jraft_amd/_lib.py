@@ -29,6 +29,12 @@ class JrqError(RuntimeError):
         self.code = code
 
 
+class GroupTiles(C.Structure):
+    """jrq_group_tiles (include/jrq.h)."""
+    _fields_ = [("tiles", C.c_void_p), ("num_peers", C.c_uint32), ("run_off", C.c_void_p),
+                ("run_start", C.c_void_p), ("run_conf", C.c_void_p)]
+
+
 class GroupBatch(C.Structure):
     """jrq_group_batch (include/jrq.h)."""
     _fields_ = [
@@ -100,6 +106,7 @@ SIGNATURES = [
     ("jrq_host_free", C.c_int, [_V]),
     ("jrq_debug_set", C.c_int, [_V, C.c_int, C.c_int64]),
     ("jrq_quorum_epoch_dev", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
+    ("jrq_quorum_epoch_tiles_dev", C.c_int, [_V, C.POINTER(GroupTiles), _V, _V, C.c_uint32]),
     ("jrq_quorum_epoch", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
     ("jrq_quorum_epochs_dev", C.c_int,
      [_V, C.POINTER(GroupBatch), C.c_uint32, C.c_uint64, C.c_uint64, _V, _V, C.c_uint32]),

@@ -129,6 +129,22 @@ class Engine:
         check(self._L.jrq_quorum_epoch_dev(self._h, C.byref(b), _dev_ptr(committed_out),
                                            _dev_ptr(status_out), G), self._h)
 
+    def quorum_epoch_tiles_launcher(self, tiles, P, G, committed_out, status_out, run_off=None,
+                                    run_start=None, run_conf=None):
+        """jrq_quorum_epoch_tiles_dev with its arguments resolved once: `tiles` a device tensor
+        in the table's tile layout (to_tiles); returns a zero-argument callable."""
+        b = _lib.GroupTiles(_dev_ptr(tiles), P, _dev_ptr(run_off), _dev_ptr(run_start), _dev_ptr(run_conf))
+        fn, h, ref = self._L.jrq_quorum_epoch_tiles_dev, self._h, C.byref(b)
+        co, so = _dev_ptr(committed_out), _dev_ptr(status_out)
+        keep = (b, tiles, committed_out, status_out, run_off, run_start, run_conf)
+
+        def launch():
+            rc = fn(h, ref, co, so, G)
+            if rc:
+                check(rc, h)
+        launch.keep = keep
+        return launch
+
     def quorum_epoch_launcher(self, match, pending_index, last_appended, last_committed, conf,
                               committed_out, status_out, run_off=None, run_start=None,
                               run_conf=None):

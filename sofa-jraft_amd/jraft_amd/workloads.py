@@ -100,6 +100,23 @@ def quorum_batch(cfg: str, groups: int | None = None, seed: int | None = None,
                 conf=conf.astype(np.uint64))
 
 
+def to_tiles(match, pending_index, last_appended, last_committed, conf) -> np.ndarray:
+    """A quorum batch in the resident table's tile layout (include/jrq.h jrq_group_tiles):
+    tiles of 256 groups, each holding match[0..P-1], pending_index, last_appended,
+    last_committed, conf as 256-word rows; int64 words, G rounded up to whole tiles (pad
+    groups: all zero, not leaders)."""
+    match = np.asarray(match)
+    P, G = match.shape[0], match.shape[1]
+    nt = (G + 255) // 256
+    rows = np.zeros((P + 4, nt * 256), np.int64)
+    rows[:P, :G] = match[:, :G]
+    rows[P, :G] = pending_index
+    rows[P + 1, :G] = last_appended
+    rows[P + 2, :G] = last_committed
+    rows[P + 3, :G] = np.asarray(conf).view(np.int64)
+    return np.ascontiguousarray(rows.reshape(P + 4, nt, 256).transpose(1, 0, 2)).reshape(-1)
+
+
 def entry_batch(n_entries: int, entry_bytes: int, seed: int, first_index: int = 1,
                 term: int = 1, corrupt_every: int = 0):
     """n DATA LogEntries of `entry_bytes` random bytes each (C1/C5 payload shape)."""

@@ -218,6 +218,52 @@ def test_dev_fast_path_with_flagged_runs(engine, oracle, P, run_prob, max_runs, 
     np.testing.assert_array_equal(st.cpu().numpy(), se)
 
 
+@pytest.mark.parametrize("P,run_prob,max_runs,G", [(5, 0.01, 4, 4096), (3, 0.3, 4, 4097),
+                                                   (5, 0.9, 9, 1030), (16, 0.5, 6, 515),
+                                                   (1, 0.2, 3, 2), (8, 0.0, 1, 300)])
+def test_tiles_entry_point_vs_replay(engine, oracle, P, run_prob, max_runs, G):
+    """jrq_quorum_epoch_tiles_dev: the same batches in the resident table's tile layout
+    (W.to_tiles: 256-group tiles, G not a multiple of 256, odd G, more flagged groups per wave
+    than hand-off slots) decide exactly as the replay through real BallotBoxes."""
+    import torch
+    from quorum_cases import flag_runs
+    b = random_batch(700 + P, G, P, run_prob=run_prob, max_runs=max_runs)
+    b["conf"] = flag_runs(b)
+    ce, se = _replay(oracle, b)
+    dev = torch.device("cuda:0")
+    tiles = torch.from_numpy(W.to_tiles(b["match"], b["pending_index"], b["last_appended"],
+                                        b["last_committed"], b["conf"])).to(dev)
+    t = _to_dev(b, ["run_off", "run_start", "run_conf"])
+    out = torch.empty(G, dtype=torch.int64, device=dev)
+    st = torch.empty(G, dtype=torch.uint8, device=dev)
+    engine.quorum_epoch_tiles_launcher(tiles, P, G, out, st, t["run_off"], t["run_start"],
+                                       t["run_conf"])()
+    engine.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), ce)
+    np.testing.assert_array_equal(st.cpu().numpy(), se)
+
+
+def test_tiles_entry_point_full_c3(engine):
+    """C3 at its full 1M groups through the tile layout: identical to the rows entry point
+    (itself checked against the oracle on C3 by test_full_c3_sampled_and_properties)."""
+    import torch
+    b = W.quorum_batch("C3")
+    P, G = b["match"].shape[0], b["match"].shape[1]
+    dev = torch.device("cuda:0")
+    t = _to_dev(b, ["match", "pending_index", "last_appended", "last_committed", "conf"])
+    o1 = torch.empty(G, dtype=torch.int64, device=dev)
+    s1 = torch.empty(G, dtype=torch.uint8, device=dev)
+    engine.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
+                            t["last_committed"], t["conf"], o1, s1)
+    tiles = torch.from_numpy(W.to_tiles(b["match"], b["pending_index"], b["last_appended"],
+                                        b["last_committed"], b["conf"])).to(dev)
+    o2 = torch.empty(G, dtype=torch.int64, device=dev)
+    s2 = torch.empty(G, dtype=torch.uint8, device=dev)
+    engine.quorum_epoch_tiles_launcher(tiles, P, G, o2, s2)()
+    engine.synchronize()
+    assert torch.equal(o1, o2) and torch.equal(s1, s2)
+
+
 @pytest.mark.parametrize("P,G,K", [(3, 1000, 9), (5, 777, 40), (2, 64, 1), (3, 130, 200)])
 def test_gpu_quorum_epochs_with_runs(engine, oracle, P, G, K):
     """K epochs in one launch with conf runs and flagged groups == K sequential replays."""
