@@ -531,6 +531,7 @@ GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
     for (uint32_t s = 0; s < P_; ++s) sp[s] = kNoPeer;
   }
   runs_.assign(static_cast<size_t>(G_) * JRQ_TABLE_MAX_RUNS, Run{0, 0});
+  packedIn_.reset(new uint64_t[G_]());
   waiter_.resize(G_);
   closures_.resize(G_);
 }
@@ -752,6 +753,11 @@ void GroupBatch::packRange(Part& part, const uint32_t* groups, size_t n) {
     if (i + kAhead < n) __builtin_prefetch(rec_ + static_cast<size_t>(groups[i + kAhead]) * stride_, 1);
     const uint32_t g = groups[i];
     Guard lk(*this, g);
+    // A group can sit on two threads' lists of one generation (two fast-path acks of different
+    // peers listing it at once): pack it once -- a second pass would ship the slots again, and
+    // the device applies an upload's records in parallel, so an older value could land last.
+    if (packedIn_[g] == packSerial_) continue;
+    packedIn_[g] = packSerial_;
     Hot& h = hot(g);
     uint32_t d = h.dirty;
     h.dirty = 0;
@@ -851,6 +857,7 @@ uint32_t GroupBatch::flushLocked() {
   // end the generation and take its lists once its call regions have drained: callers go on
   // listing groups (and the fast path stamping acks) in the next one
   const uint32_t t = gen_.load(std::memory_order_acquire);
+  ++packSerial_;
   gen_.store(t + 1, std::memory_order_release);  // (orders the last swap of v[t & 1] before
                                                  // its reuse in generation t + 2)
   packGen_ = t;

@@ -410,6 +410,8 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   std::vector<Part> parts_;
   std::vector<Delivery> deliveries_;
   uint32_t packGen_ = 0;                  // the generation the running flush packs
+  uint64_t packSerial_ = 0;               // flushes started (never wraps)
+  std::unique_ptr<uint64_t[]> packedIn_;  // [G] the flush that last packed the group
   jrq_table* table_ = nullptr;
   PinnedBuf<uint64_t> changed_;
   std::atomic<uint64_t> flushes_{0};

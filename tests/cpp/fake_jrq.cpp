@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <unordered_set>
 #include <string>
 #include <vector>
 
@@ -111,6 +112,11 @@ void jrq_table_destroy(jrq_table* t) { delete t; }
 // next `n` update calls fail as a lost device would, after applying nothing.
 static std::atomic<int> g_fail_updates{0};
 void fake_jrq_fail_updates(int n) { g_fail_updates.store(n); }
+// Records of one upload naming the same (group, field) twice: the device applies an upload's
+// records in parallel, so which of the two lands is not defined -- the host must never send
+// them (the double applies records last to first, so the older value wins, and counts them).
+static std::atomic<uint64_t> g_dup_records{0};
+uint64_t fake_jrq_dup_records() { return g_dup_records.load(); }
 
 int jrq_table_update_gather(jrq_table* t, uint32_t parts, const jrq_group_state* const* states,
                             const uint32_t* n_states, const uint64_t* const* recs,
@@ -142,8 +148,14 @@ int jrq_table_update_gather(jrq_table* t, uint32_t parts, const jrq_group_state*
       if (s.flags & JRQ_STATE_RESET_MATCH)
         for (uint32_t p = 0; p < t->P; ++p) t->match[static_cast<size_t>(g) * t->P + p] = pi - 1;
     }
-  for (uint32_t i = 0; i < parts; ++i)
-    for (uint32_t k = 0; k < n_recs[i]; ++k) {
+  {
+    std::unordered_set<uint64_t> seen;
+    for (uint32_t i = 0; i < parts; ++i)
+      for (uint32_t k = 0; k < n_recs[i]; ++k)
+        if (!seen.insert(recs[i][k] & 0xFFFFFFFFull).second) g_dup_records.fetch_add(1);
+  }
+  for (uint32_t i = parts; i-- > 0;)
+    for (uint32_t k = n_recs[i]; k-- > 0;) {
       const uint64_t r = recs[i][k];
       const uint32_t f = static_cast<uint32_t>(r & 31u), g = static_cast<uint32_t>(r >> 5) & ((1u << 27) - 1u);
       const int64_t v = static_cast<int64_t>(static_cast<uint32_t>(r >> 32));

@@ -28,6 +28,8 @@ using namespace jraft;
 // Failure injection, present only in the sanitizer builds' test double (tests/cpp/fake_jrq.cpp):
 // the next n jrq_table_update_gather calls fail.  Null against the real libjrq.so.
 extern "C" void fake_jrq_fail_updates(int n) __attribute__((weak));
+// Records of one upload that named the same (group, field) twice (the double counts them).
+extern "C" uint64_t fake_jrq_dup_records() __attribute__((weak));
 
 static int g_fail = 0, g_pass = 0;
 #define CHECK(c)                                                               \
@@ -593,6 +595,7 @@ static void testConcurrentCallers(Engine& eng, uint32_t G, int64_t kEntries) {
   batch->stopFlusher();
   batch->flush();
   CHECK(!failed);
+  if (fake_jrq_dup_records) CHECK(fake_jrq_dup_records() == 0);
   std::vector<jo_ballot_box*> ob(G);
   auto same = [&](uint32_t g) {
     const int64_t lc = jo_bb_last_committed_index(ob[g]);
