@@ -120,7 +120,7 @@ constexpr uint32_t kTableEpochBlock = 64 * kTableBlockWaves;
 // reloads the group.  No workgroup barrier, no atomics: each wave writes its own list slice and
 // count.
 template <int P>
-__global__ __launch_bounds__(kTableEpochBlock, 4) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
+__global__ __launch_bounds__(kTableEpochBlock, P <= 5 ? 4 : 2) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
   constexpr uint32_t kWaves = kTableEpochBlock / 64;
   constexpr uint32_t kHand = 16;  // flagged groups per wave handed over through LDS
   constexpr uint32_t kEntLds = 4; // flagged-entry slots per wave copied to LDS up front

@@ -1,0 +1,60 @@
+"""A/B (tools only): the resident table epoch at P peers (1M groups, every group committing),
+libjrq builds side by side in one process (tools/ab_inproc.py loading), alternating per round.
+
+  P=9 python tools/table_peers_ab.py old=ab/old/libjrq.so new=ab/new/libjrq.so"""
+import os, sys, json
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sofa-jraft_amd")); sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import torch
+import ctypes as C
+from ab_inproc import load_variant
+import jraft_amd._lib as L
+from jraft_amd import Table
+
+def main():
+    P = int(os.environ.get("P", "9")); G = 1 << 20; NB = 4
+    dev = torch.device("cuda:0"); s = torch.cuda.Stream(dev); torch.cuda.set_stream(s)
+    L.load()
+    rng = np.random.default_rng(1)
+    res = {}
+    variants = []
+    for sp in sys.argv[1:]:
+        name, _, path = sp.partition("=")
+        e = load_variant(path); e._L.jrq_set_stream(e._h, C.c_void_p(s.cuda_stream)); variants.append((name, e))
+    tabs = {}
+    for name, e in variants:
+        prist, work = [], []
+        for k in range(NB):
+            r = np.random.default_rng(100 + k)
+            st = Table.states(G)
+            st["group"] = np.arange(G); st["num_runs"] = 1; st["flags"] = L.STATE_RESET_MATCH
+            lc = r.integers(1 << 20, 1 << 30, G)
+            st["pending_index"] = L.PI_FOLLOWS_LC; st["last_committed"] = lc
+            st["last_appended"] = lc + 64
+            peers = np.arange(P, dtype=np.uint64)
+            conf = np.uint64(((1 << P) - 1) | ((P // 2 + 1) << 32))
+            st["run_conf"][:, 0] = conf
+            gs = np.arange(G)
+            recs = np.concatenate([L.rec(gs, p, r.integers(0, 65, G)) for p in range(P)])
+            t = Table(e, G, P); t.update(st, recs); prist.append(t); work.append(Table(e, G, P))
+        torch.cuda.synchronize()
+        tabs[name] = (prist, work, [w.list_buffers(dev) for w in work])
+    times = {n: [] for n, _ in variants}
+    for rep in range(12):
+        for name, _ in variants:
+            prist, work, lists = tabs[name]
+            for w, t in zip(work, prist): w.copy_from(t)
+            a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            for i in range(NB): work[i].epoch_dev(*lists[i])
+            z.record(s); z.synchronize()
+            if rep >= 2: times[name].append(a.elapsed_time(z) / NB * 1e3)
+    outs = {n: [w.gather_dev_list(*l) for w, l in zip(tabs[n][1], tabs[n][2])] for n, _ in variants}
+    names = [n for n, _ in variants]
+    same = all(np.array_equal(np.asarray(a), np.asarray(b)) for a, b in zip(outs[names[0]], outs[names[-1]]))
+    print(json.dumps({"P": P, "us": {n: float(np.median(t)) for n, t in times.items()},
+                      "changed": len(outs[names[0]][0]), "same": same}))
+
+if __name__ == "__main__":
+    main()
