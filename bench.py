@@ -39,7 +39,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 QUORUM_EPOCH_BUFFERS = 6
 LEGS = ("quorum", "table", "drive", "C2", "C2L", "C3K", "C5", "C1", "ae", "v2", "snapshot", "pinned",
-        "lease", "fanout", "peak", "cpu")
+        "lease", "readindex", "fanout", "peak", "cpu")
 
 
 def quorum_bytes_per_group(P: int) -> int:
@@ -1311,6 +1311,45 @@ def leg_lease(ctx, args, quorum_conf_dev, G, P):
             "roofline": roofline(lb, ms, **pmc_traffic("lease", f"lease_check_kernel<{P}>"))}
 
 
+def leg_readindex(ctx, args, quorum_conf_dev, quorum_conf, G, P):
+    """The ReadIndex heartbeat quorum (NodeImpl.java:1246-1396) over G leader
+    groups, one heartbeat round each: conf C3's, the leader in slot 0, a random subset of the
+    four followers answered in a random order, 55 % of the answers successful."""
+    import torch
+    eng, dev, rank = ctx.eng, ctx.dev, ctx.rank
+    rng = np.random.default_rng(rank ^ 0x4EAD)
+    self_np = np.zeros(G, np.uint8)
+    bufs = []
+    for _ in range(QUORUM_EPOCH_BUFFERS):  # rotating inputs, as the other legs
+        pos = np.argsort(rng.random((G, P - 1)), axis=1).astype(np.uint64) + np.uint64(1)
+        pos[rng.random((G, P - 1)) < 0.3] = 0  # not answered yet
+        order = (pos << (4 * np.arange(1, P, dtype=np.uint64))).sum(axis=1).astype(np.uint64)
+        okm = ((rng.random((G, P - 1)) < 0.55) << np.arange(1, P)).sum(axis=1).astype(np.uint16)
+        bufs.append((order, okm, to_dev(order, dev), to_dev(okm.view(np.int16), dev)))
+    self_slot = to_dev(self_np, dev)
+    res = torch.empty(G, dtype=torch.uint8, device=dev)
+
+    def step(i):
+        b = bufs[i % QUORUM_EPOCH_BUFFERS]
+        eng.readindex_quorum_dev(quorum_conf_dev, self_slot, b[2], b[3], P, res)
+    ms, _ = ctx.timed(step)
+    ok = None
+    counts = None
+    if ctx.oracle_checks:
+        import jraft_oracle as O
+        step(0)
+        ctx.sync()
+        exp = O.readindex_quorum(quorum_conf, self_np, bufs[0][0], bufs[0][1], P)
+        got = res.cpu().numpy()
+        ok = bool(np.array_equal(got, exp))
+        counts = {k: int((exp == v).sum()) for k, v in (("pending", 0), ("success", 1), ("failure", 2))}
+    rb = 20 * G  # conf 8 + order 8 + ok mask 2 + self slot 1 read, verdict 1 written
+    return {"workload": f"{G} leader groups x {P} peers, one ReadIndex heartbeat round each",
+            "rounds_per_s": G / (ms * 1e-3), "kernel_ms": ms, "bit_exact_vs_oracle": ok,
+            "verdicts": counts,
+            "roofline": roofline(rb, ms, **pmc_traffic("readindex", f"readindex_quorum_kernel<{P}>"))}
+
+
 def leg_fanout(ctx, args, G):
     """commit fan-out (FSMCaller.doCommitted / ClosureQueue.popClosureUntil) of C3 epochs: each
     epoch's committed[] feeds the fan-out of its groups; every launch starts from fresh closure
@@ -1711,10 +1750,13 @@ def main():
     if "C1" in legs:
         _LEG[0] = "C1"
         line["C1"] = leg_c1(ctx, args)
+    c3conf = W.quorum_batch("C3", groups=G)["conf"] if legs & {"lease", "readindex"} else None
     if "lease" in legs:
-        b = W.quorum_batch("C3", groups=G)
         _LEG[0] = "lease"
-        extras["lease_check"] = leg_lease(ctx, args, to_dev(b["conf"], dev), G, 5)
+        extras["lease_check"] = leg_lease(ctx, args, to_dev(c3conf, dev), G, 5)
+    if "readindex" in legs:
+        _LEG[0] = "readindex"
+        extras["readindex_quorum"] = leg_readindex(ctx, args, to_dev(c3conf, dev), c3conf, G, 5)
     if "fanout" in legs:
         _LEG[0] = "fanout"
         extras["commit_fanout"] = leg_fanout(ctx, args, G)

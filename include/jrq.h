@@ -445,6 +445,34 @@ int jrq_lease_check(jrq_engine *e, const int64_t *last_rpc_ts, uint64_t ld, uint
                     int64_t lease_timeout_ms, uint8_t *ok_out, int64_t *lease_start_inout,
                     uint16_t *dead_out);
 
+/* ------------------------------------------------ ReadIndex heartbeat quorum -- */
+
+/* The ReadOnlySafe round of NodeImpl.readLeader (JC/core/NodeImpl.java:1343-1396) for G leader
+ * groups, one heartbeat round per group (ReadOnlyServiceImpl batches a group's reads into one
+ * ReadIndexRequest), decided as ReadIndexHeartbeatResponseClosure.run does (:1246-1291).
+ * Per group g:
+ *   conf[g]       packed conf word (JRQ_CONF): its new-conf mask is the peer list (getQuorum,
+ *                 :1321-1327: quorum = peers.size()/2 + 1; <= 1 answers at once)
+ *   self_slot[g]  the leader's own slot (no heartbeat to it)
+ *   order[g]      4 bits per peer slot: the arrival position (1..15) of that slot's heartbeat
+ *                 response so far, 0 = none yet (equal positions: lower slot first)
+ *   ok_mask[g]    bit p = slot p's response was OK with success = true (else a failure)
+ * result_out[g] = JRQ_READINDEX_SUCCESS once ackSuccess + 1 >= quorum, JRQ_READINDEX_FAILURE
+ * once ackFailures >= failPeersThreshold (quorum - 1 for an even peer count, quorum for an
+ * odd one), whichever the arrival order reached first, else JRQ_READINDEX_PENDING.  Stateless:
+ * call again with the round's later responses added; a verdict never changes.  The host keeps
+ * readLeader's other checks (the term of lastCommittedIndex, the requester in the conf, the
+ * lease-based option). */
+#define JRQ_READINDEX_PENDING 0
+#define JRQ_READINDEX_SUCCESS 1
+#define JRQ_READINDEX_FAILURE 2
+int jrq_readindex_quorum_dev(jrq_engine *e, const uint64_t *conf_dev, const uint8_t *self_slot_dev,
+                             const uint64_t *order_dev, const uint16_t *ok_mask_dev,
+                             uint32_t num_peers, uint32_t G, uint8_t *result_out_dev);
+int jrq_readindex_quorum(jrq_engine *e, const uint64_t *conf, const uint8_t *self_slot,
+                         const uint64_t *order, const uint16_t *ok_mask, uint32_t num_peers,
+                         uint32_t G, uint8_t *result_out);
+
 /* ------------------------------------------------------- commit fan-out -- */
 
 /* What each group's FSMCaller does with the epoch's commit, for G groups:

@@ -195,6 +195,35 @@ void jo_lease_check(uint32_t G, uint32_t P, const int64_t *ts, const uint64_t *c
     free(t);
 }
 
+/* ReadIndex, ReadOnlySafe (JC/core/NodeImpl.java:1343-1396): getQuorum (:1321-1327), then
+ * ReadIndexHeartbeatResponseClosure (:1246-1291) run on each heartbeat response in arrival
+ * order -- position 1..15 from order's nibble per slot, equal positions in slot order --
+ * from the conf peers the leader sent a heartbeat to (every peer but itself). */
+uint8_t jo_readindex_round(uint32_t mask, uint32_t P, uint32_t self, uint64_t order, uint32_t ok_mask) {
+    int32_t ids[16];
+    const int32_t n = mask_to_ids(mask, ids); /* conf.getConf().getPeers() */
+    const int32_t quorum = n == 0 ? 0 : n / 2 + 1;
+    if (quorum <= 1) return 1; /* "Only one peer, fast path": success */
+    const int32_t failPeersThreshold = n % 2 == 0 ? (quorum - 1) : quorum;
+    int32_t ackSuccess = 0, ackFailures = 0;
+    for (uint32_t pos = 1; pos < 16; ++pos) {
+        for (int32_t i = 0; i < n; ++i) {
+            const uint32_t p = (uint32_t)ids[i];
+            if (p == self || p >= P || ((order >> (4 * p)) & 0xF) != pos) continue;
+            if ((ok_mask >> p) & 1u) ackSuccess++; else ackFailures++;
+            if (ackSuccess + 1 >= quorum) return 1;             /* respond success */
+            else if (ackFailures >= failPeersThreshold) return 2; /* respond !success */
+        }
+    }
+    return 0; /* not decided yet */
+}
+
+void jo_readindex_quorum(uint32_t G, uint32_t P, const uint64_t *conf, const uint8_t *self_slot,
+                         const uint64_t *order, const uint16_t *ok_mask, uint8_t *result) {
+    for (uint32_t g = 0; g < G; ++g)
+        result[g] = jo_readindex_round((uint32_t)(conf[g] & 0xFFFF), P, self_slot[g], order[g], ok_mask[g]);
+}
+
 /* ======================= Ballot (JC/entity/Ballot.java) ==================== */
 
 static void list_init(jo_peer_list *l, const int32_t *ids, int32_t n) {

@@ -79,6 +79,14 @@ void jo_lease_check(uint32_t G, uint32_t P, const int64_t *ts /* [P][G] */, cons
                     const uint8_t *self_slot, int64_t now_ms, int64_t lease_timeout_ms,
                     uint8_t *ok, int64_t *lease_start /* in/out */, uint16_t *dead);
 
+/* NodeImpl.readLeader's ReadOnlySafe heartbeat round (JC/core/NodeImpl.java:1246-1396) for
+ * one group: conf peers = the set bits of mask (slot order), heartbeat responses from slots
+ * < P other than self in arrival order (order: 4 bits per slot, position 1..15, 0 = none;
+ * ties by slot), ok_mask bit = success.  Returns 0 pending, 1 success, 2 failure. */
+uint8_t jo_readindex_round(uint32_t mask, uint32_t P, uint32_t self, uint64_t order, uint32_t ok_mask);
+void jo_readindex_quorum(uint32_t G, uint32_t P, const uint64_t *conf, const uint8_t *self_slot,
+                         const uint64_t *order, const uint16_t *ok_mask, uint8_t *result);
+
 /* ---------------- Ballot (JC/entity/Ballot.java) --------------------------- */
 
 #define JO_MAX_CONF 32 /* peers per Configuration list kept by the oracle */

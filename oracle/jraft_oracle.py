@@ -72,6 +72,10 @@ def lib():
         L.jo_lease_check.restype = None
         L.jo_lease_check.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.jo_readindex_round.restype = C.c_uint8
+        L.jo_readindex_round.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32]
+        L.jo_readindex_quorum.restype = None
+        L.jo_readindex_quorum.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 5
         L.jo_bb_new.restype = C.c_void_p
         L.jo_bb_free.argtypes = [C.c_void_p]
         for name in ("jo_bb_last_committed_index", "jo_bb_pending_index", "jo_bb_queue_size",
@@ -248,6 +252,22 @@ def lease_check(last_rpc_ts, conf, self_slot, now_ms, lease_timeout_ms, lease_st
     lib().jo_lease_check(G, P, _ptr(ts), _ptr(conf), _ptr(ss), now_ms, lease_timeout_ms,
                          _ptr(ok), _ptr(lead), _ptr(dead))
     return ok, lead, dead
+
+
+READINDEX_PENDING, READINDEX_SUCCESS, READINDEX_FAILURE = 0, 1, 2
+
+
+def readindex_quorum(conf, self_slot, order, ok_mask, P):
+    """NodeImpl.readLeader's ReadOnlySafe heartbeat round per group (NodeImpl.java:1246-1396):
+    the verdict of ReadIndexHeartbeatResponseClosure over the responses so far."""
+    conf = np.ascontiguousarray(conf, np.uint64)
+    ss = np.ascontiguousarray(self_slot, np.uint8)
+    order = np.ascontiguousarray(order, np.uint64)
+    okm = np.ascontiguousarray(ok_mask, np.uint16)
+    G = len(conf)
+    res = np.zeros(G, np.uint8)
+    lib().jo_readindex_quorum(G, P, _ptr(conf), _ptr(ss), _ptr(order), _ptr(okm), _ptr(res))
+    return res
 
 
 FAN_NONE, FAN_APPLY, FAN_SKIP, FAN_INVALID = 0, 1, 2, 3

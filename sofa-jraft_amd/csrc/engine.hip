@@ -29,6 +29,7 @@ extern "C" hipError_t jrq_launch_quorum_epochs(const JrqQuorumArgs* args, uint32
                                                int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_ae_meta(const JrqAeArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_lease(const JrqLeaseArgs* a, int num_cus, hipStream_t stream);
+extern "C" hipError_t jrq_launch_readindex(const JrqReadIndexArgs* a, int num_cus, hipStream_t stream);
 extern "C" hipError_t jrq_launch_fanout(const JrqFanoutArgs* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_v2_parse(const JrqV2Args* a, hipStream_t stream);
 extern "C" hipError_t jrq_launch_v2_finish(const JrqV2Args* a, const JrqCrcArgs* walk, int num_cus,
@@ -1006,6 +1007,61 @@ int jrq_lease_check(jrq_engine* e, const int64_t* ts, uint64_t ld, uint32_t num_
   JRQ_HIP(e, hipMemcpyAsync(ok_out, dok, G, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipMemcpyAsync(lease_start, dlead, static_cast<size_t>(G) * 8, hipMemcpyDeviceToHost, e->stream));
   if (dead_out) JRQ_HIP(e, hipMemcpyAsync(dead_out, ddead, static_cast<size_t>(G) * 2, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
+// ------------------------------------------------------------ ReadIndex -----
+
+static_assert(JRQ_READINDEX_PENDING == jrq::kRiPending && JRQ_READINDEX_SUCCESS == jrq::kRiSuccess &&
+                  JRQ_READINDEX_FAILURE == jrq::kRiFailure,
+              "ReadIndex verdicts");
+
+int jrq_readindex_quorum_dev(jrq_engine* e, const uint64_t* conf, const uint8_t* self_slot,
+                             const uint64_t* order, const uint16_t* ok_mask, uint32_t num_peers,
+                             uint32_t G, uint8_t* result_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (G == 0) return JRQ_OK;
+  if (!conf || !self_slot || !order || !ok_mask || !result_out || num_peers == 0 ||
+      num_peers > JRQ_MAX_PEERS)
+    return fail(e, JRQ_E_INVALID, "bad ReadIndex batch");
+  DeviceGuard guard(e->device);
+  JrqReadIndexArgs a{};
+  a.conf = conf;
+  a.self_slot = self_slot;
+  a.order = order;
+  a.ok_mask = ok_mask;
+  a.num_peers = num_peers;
+  a.G = G;
+  a.result = result_out;
+  JRQ_HIP(e, jrq_launch_readindex(&a, e->num_cus, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_readindex_quorum(jrq_engine* e, const uint64_t* conf, const uint8_t* self_slot,
+                         const uint64_t* order, const uint16_t* ok_mask, uint32_t num_peers,
+                         uint32_t G, uint8_t* result_out) {
+  if (!e) return JRQ_E_INVALID;
+  if (G == 0) return JRQ_OK;
+  if (!conf || !self_slot || !order || !ok_mask || !result_out || num_peers == 0 ||
+      num_peers > JRQ_MAX_PEERS)
+    return fail(e, JRQ_E_INVALID, "bad ReadIndex batch");
+  DeviceGuard guard(e->device);
+  int rc;
+  const uint64_t* dconf;
+  const uint8_t* dself;
+  const uint64_t* dord;
+  const uint16_t* dok;
+  if ((rc = stage_in(e, 0, conf, G, &dconf))) return rc;
+  if ((rc = stage_in(e, 1, self_slot, G, &dself))) return rc;
+  if ((rc = stage_in(e, 2, order, G, &dord))) return rc;
+  if ((rc = stage_in(e, 3, ok_mask, G, &dok))) return rc;
+  void* dres;
+  if ((rc = ensure_stage(e, 8, G, &dres))) return rc;
+  if ((rc = jrq_readindex_quorum_dev(e, dconf, dself, dord, dok, num_peers, G,
+                                     static_cast<uint8_t*>(dres))))
+    return rc;
+  JRQ_HIP(e, hipMemcpyAsync(result_out, dres, G, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }

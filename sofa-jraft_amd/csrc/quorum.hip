@@ -505,7 +505,77 @@ __global__ __launch_bounds__(256) void lease_check_kernel(JrqLeaseArgs a) {
   }
 }
 
+// --------------------------------------------------------------- ReadIndex ---
+// NodeImpl.readLeader's ReadOnlySafe round (jraft-core/.../core/NodeImpl.java:1343-1396) and
+// its ReadIndexHeartbeatResponseClosure (:1246-1291): quorum = peers.size()/2 + 1 (getQuorum,
+// :1321-1327; <= 1 answers at once), a heartbeat to every conf peer but the leader, and per
+// response, in arrival order: ackSuccess or ackFailures + 1, then success when ackSuccess + 1
+// >= quorum, else failure when ackFailures >= failPeersThreshold (quorum - 1 for an even
+// peer count, quorum for an odd one); the first verdict stands.  Restated without the loop:
+// the verdict is whichever threshold the arrival order crosses first -- the arrival key of
+// the (quorum-1)-th success against that of the threshold-th failure (key = position * 16 +
+// slot, so equal positions resolve by slot, as the oracle orders them).
+template <int P>
+__global__ __launch_bounds__(256) void readindex_quorum_kernel(JrqReadIndexArgs a) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G; g += stride) {
+    const uint64_t cw = __builtin_nontemporal_load(a.conf + g);
+    const uint64_t ord = __builtin_nontemporal_load(a.order + g);
+    const uint32_t okm = a.ok_mask[g];
+    const uint32_t self = a.self_slot[g];
+    const uint32_t mask = static_cast<uint32_t>(cw & 0xFFFFu) & ((1u << P) - 1u);
+    const uint32_t n = __builtin_popcount(static_cast<uint32_t>(cw & 0xFFFFu));  // peers.size()
+    const uint32_t q = n ? n / 2 + 1 : 0;
+    uint8_t res = kRiSuccess;  // quorum <= 1: the fast path answers at once
+    if (q > 1) {
+      const uint32_t need_ok = q - 1, need_fail = (n % 2 == 0) ? q - 1 : q;
+      // the crossing keys: the need-th smallest key among the successes / the failures
+      uint32_t t_ok = ~0u, t_fail = ~0u;
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        const uint32_t pos = static_cast<uint32_t>(ord >> (4 * p)) & 0xFu;
+        const bool resp = ((mask >> p) & 1u) && static_cast<uint32_t>(p) != self && pos != 0;
+        const bool ok = (okm >> p) & 1u;
+        const uint32_t key = pos * 16u + static_cast<uint32_t>(p);
+        uint32_t before = 0;  // responses of the same kind at or before this one
+#pragma unroll
+        for (int r = 0; r < P; ++r) {
+          const uint32_t pr = static_cast<uint32_t>(ord >> (4 * r)) & 0xFu;
+          const bool rr = ((mask >> r) & 1u) && static_cast<uint32_t>(r) != self && pr != 0;
+          const bool same = (((okm >> r) & 1u) != 0) == ok;
+          before += (rr && same && pr * 16u + static_cast<uint32_t>(r) <= key) ? 1u : 0u;
+        }
+        if (resp && ok && before == need_ok) t_ok = key;
+        if (resp && !ok && before == need_fail) t_fail = key;
+      }
+      res = t_ok < t_fail ? kRiSuccess
+                          : (t_fail != ~0u ? kRiFailure : kRiPending);
+    }
+    a.result[g] = res;
+  }
+}
+
 }  // namespace jrq
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_readindex(
+    const JrqReadIndexArgs* args, int num_cus, hipStream_t stream) {
+  const uint64_t need = (static_cast<uint64_t>(args->G) + 255) / 256;
+  const uint64_t cap = static_cast<uint64_t>(num_cus) * 8;
+  const dim3 grid(static_cast<unsigned>(need < cap ? (need ? need : 1) : cap)), blk(256);
+  switch (args->num_peers) {
+#define JRQ_CASE(P)                                                                        \
+  case P:                                                                                  \
+    hipLaunchKernelGGL(jrq::readindex_quorum_kernel<P>, grid, blk, 0, stream, *args); \
+    break;
+    JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
+    JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
+    JRQ_CASE(15) JRQ_CASE(16)
+#undef JRQ_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_lease(
     const JrqLeaseArgs* args, int num_cus, hipStream_t stream) {

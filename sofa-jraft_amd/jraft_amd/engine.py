@@ -313,6 +313,27 @@ class Engine:
                                           lease_timeout_ms, _dev_ptr(ok_out),
                                           _dev_ptr(lease_start_inout), _dev_ptr(dead_out)), self._h)
 
+    # -------------------------------------------------------- ReadIndex --
+    def readindex_quorum(self, conf, self_slot, order, ok_mask, num_peers):
+        """Host variant: the ReadIndex heartbeat round's verdict per group (uint8[G],
+        READINDEX_PENDING / _SUCCESS / _FAILURE; include/jrq.h jrq_readindex_quorum)."""
+        conf = _c(conf, np.uint64)
+        G = len(conf)
+        self_slot = _c(self_slot, np.uint8)
+        order = _c(order, np.uint64)
+        ok_mask = _c(ok_mask, np.uint16)
+        res = np.zeros(G, np.uint8)
+        check(self._L.jrq_readindex_quorum(self._h, _np_ptr(conf), _np_ptr(self_slot),
+                                           _np_ptr(order), _np_ptr(ok_mask), num_peers, G,
+                                           _np_ptr(res)), self._h)
+        return res
+
+    def readindex_quorum_dev(self, conf, self_slot, order, ok_mask, num_peers, result_out):
+        G = conf.shape[0]
+        check(self._L.jrq_readindex_quorum_dev(self._h, _dev_ptr(conf), _dev_ptr(self_slot),
+                                               _dev_ptr(order), _dev_ptr(ok_mask), num_peers, G,
+                                               _dev_ptr(result_out)), self._h)
+
     # ------------------------------------------------- AppendEntries verify --
     def append_entries_verify(self, req_off, prev_log_index, term, etype, data_len, checksum,
                               data, has_checksum=None, peer_xor=None):

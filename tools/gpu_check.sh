@@ -27,13 +27,13 @@ for s in $STEPS; do
     profd) run prof_drive 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/profd -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs table,drive ;;
     tbl)   run table_tests 600 python -m pytest tests/test_gpu_table.py -q -x -p no:cacheprovider --timeout 300 ;;
     pmc)   # one rocprofv3 --pmc pass per (leg, counter): every kernel name then carries one workload
-           for leg in ${PMC_LEGS:-quorum C2 C2L C3K C5 C1 table v2 snapshot lease fanout ae}; do
+           for leg in ${PMC_LEGS:-quorum C2 C2L C3K C5 C1 table v2 snapshot lease readindex fanout ae}; do
              for c in FETCH_SIZE WRITE_SIZE; do
                run pmc_${leg}_$c 180 rocprofv3 --kernel-trace --pmc $c -d gpurun_out/pmc_${leg}_$c -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs $leg
              done
            done ;;
     rdreq) # read-request sizes (exact read bytes = 32 n32 + 64 n64 + 128 n128), one pass per leg
-           for leg in ${PMC_LEGS:-quorum C2 C2L C3K C5 C1 table v2 snapshot lease fanout ae}; do
+           for leg in ${PMC_LEGS:-quorum C2 C2L C3K C5 C1 table v2 snapshot lease readindex fanout ae}; do
              run pmc_${leg}_RDREQ 180 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum -d gpurun_out/pmc_${leg}_RDREQ -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs $leg
            done ;;
     host)  run host_test 300 ./tests/_build/host_test gpu ;;
