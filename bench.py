@@ -1347,7 +1347,7 @@ def leg_readindex(ctx, args, quorum_conf_dev, quorum_conf, G, P):
     return {"workload": f"{G} leader groups x {P} peers, one ReadIndex heartbeat round each",
             "rounds_per_s": G / (ms * 1e-3), "kernel_ms": ms, "bit_exact_vs_oracle": ok,
             "verdicts": counts,
-            "roofline": roofline(rb, ms, **pmc_traffic("readindex", f"readindex_quorum_kernel<{P}>"))}
+            "roofline": roofline(rb, ms, **pmc_traffic("readindex", f"readindex_quorum_kernel<{P}, true>"))}
 
 
 def leg_fanout(ctx, args, G):

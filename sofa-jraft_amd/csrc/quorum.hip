@@ -516,56 +516,95 @@ __global__ __launch_bounds__(256) void lease_check_kernel(JrqLeaseArgs a) {
 // the (quorum-1)-th success against that of the threshold-th failure (key = position * 16 +
 // slot, so equal positions resolve by slot, as the oracle orders them).
 template <int P>
+__device__ __forceinline__ uint8_t readindex_verdict(uint64_t cw, uint64_t ord, uint32_t okm,
+                                                     uint32_t self) {
+  const uint32_t mask = static_cast<uint32_t>(cw & 0xFFFFu) & ((1u << P) - 1u);
+  const uint32_t n = __builtin_popcount(static_cast<uint32_t>(cw & 0xFFFFu));  // peers.size()
+  const uint32_t q = n ? n / 2 + 1 : 0;
+  if (q <= 1) return kRiSuccess;  // the fast path answers at once
+  const uint32_t need_ok = q - 1, need_fail = (n % 2 == 0) ? q - 1 : q;
+  // per responding slot a sort key: kind (failure = 1) above the arrival key position * 16 +
+  // slot, so that a success sorts before every failure; 0xFFFF = no response from that slot
+  uint32_t kk[P];
+  uint32_t n_ok = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const uint32_t pos = static_cast<uint32_t>(ord >> (4 * p)) & 0xFu;
+    const bool resp = ((mask >> p) & 1u) && static_cast<uint32_t>(p) != self && pos != 0;
+    const uint32_t fail = ((okm >> p) & 1u) ^ 1u;
+    kk[p] = resp ? (fail << 12) | (pos * 16u + static_cast<uint32_t>(p)) : 0xFFFFu;
+    n_ok += (resp && !fail) ? 1u : 0u;
+  }
+  // the crossing keys: the need-th smallest key among the successes / the failures (the rank
+  // of a failure counts every success below it: subtract them)
+  uint32_t t_ok = ~0u, t_fail = ~0u;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    uint32_t rank = 0;
+#pragma unroll
+    for (int r = 0; r < P; ++r) rank += kk[r] <= kk[p] ? 1u : 0u;
+    const bool fail = kk[p] >> 12 == 1u;
+    if (kk[p] != 0xFFFFu && !fail && rank == need_ok) t_ok = kk[p];
+    if (kk[p] != 0xFFFFu && fail && rank - n_ok == need_fail) t_fail = kk[p] & 0xFFFu;
+  }
+  return t_ok < t_fail ? kRiSuccess : (t_fail != ~0u ? kRiFailure : kRiPending);
+}
+
+// kQuad: four consecutive groups per lane -- two 16-B loads each of conf and order, 8 B of
+// ok masks, 4 of self slots, one 4-B verdict store (the one-group form moved 1-8 B per lane
+// per instruction); needs 16-B aligned conf / order, 8-B ok, 4-B self and result.
+template <int P, bool kQuad>
 __global__ __launch_bounds__(256) void readindex_quorum_kernel(JrqReadIndexArgs a) {
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G; g += stride) {
-    const uint64_t cw = __builtin_nontemporal_load(a.conf + g);
-    const uint64_t ord = __builtin_nontemporal_load(a.order + g);
-    const uint32_t okm = a.ok_mask[g];
-    const uint32_t self = a.self_slot[g];
-    const uint32_t mask = static_cast<uint32_t>(cw & 0xFFFFu) & ((1u << P) - 1u);
-    const uint32_t n = __builtin_popcount(static_cast<uint32_t>(cw & 0xFFFFu));  // peers.size()
-    const uint32_t q = n ? n / 2 + 1 : 0;
-    uint8_t res = kRiSuccess;  // quorum <= 1: the fast path answers at once
-    if (q > 1) {
-      const uint32_t need_ok = q - 1, need_fail = (n % 2 == 0) ? q - 1 : q;
-      // the crossing keys: the need-th smallest key among the successes / the failures
-      uint32_t t_ok = ~0u, t_fail = ~0u;
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        const uint32_t pos = static_cast<uint32_t>(ord >> (4 * p)) & 0xFu;
-        const bool resp = ((mask >> p) & 1u) && static_cast<uint32_t>(p) != self && pos != 0;
-        const bool ok = (okm >> p) & 1u;
-        const uint32_t key = pos * 16u + static_cast<uint32_t>(p);
-        uint32_t before = 0;  // responses of the same kind at or before this one
-#pragma unroll
-        for (int r = 0; r < P; ++r) {
-          const uint32_t pr = static_cast<uint32_t>(ord >> (4 * r)) & 0xFu;
-          const bool rr = ((mask >> r) & 1u) && static_cast<uint32_t>(r) != self && pr != 0;
-          const bool same = (((okm >> r) & 1u) != 0) == ok;
-          before += (rr && same && pr * 16u + static_cast<uint32_t>(r) <= key) ? 1u : 0u;
-        }
-        if (resp && ok && before == need_ok) t_ok = key;
-        if (resp && !ok && before == need_fail) t_fail = key;
-      }
-      res = t_ok < t_fail ? kRiSuccess
-                          : (t_fail != ~0u ? kRiFailure : kRiPending);
-    }
-    a.result[g] = res;
+  if (!kQuad) {
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G; g += stride)
+      a.result[g] = readindex_verdict<P>(__builtin_nontemporal_load(a.conf + g),
+                                         __builtin_nontemporal_load(a.order + g), a.ok_mask[g],
+                                         a.self_slot[g]);
+    return;
   }
+  const uint32_t quads = a.G / 4;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < quads; i += stride) {
+    using u64x2 = __attribute__((ext_vector_type(2))) uint64_t;
+    const u64x2 c0 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(a.conf) + 2 * i);
+    const u64x2 c1 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(a.conf) + 2 * i + 1);
+    const u64x2 o0 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(a.order) + 2 * i);
+    const u64x2 o1 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(a.order) + 2 * i + 1);
+    const uint64_t ok4 = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(a.ok_mask) + i);
+    const uint32_t s4 = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(a.self_slot) + i);
+    uint32_t r = readindex_verdict<P>(c0.x, o0.x, static_cast<uint32_t>(ok4 & 0xFFFFu), s4 & 0xFFu);
+    r |= static_cast<uint32_t>(readindex_verdict<P>(c0.y, o0.y, static_cast<uint32_t>((ok4 >> 16) & 0xFFFFu),
+                                                    (s4 >> 8) & 0xFFu)) << 8;
+    r |= static_cast<uint32_t>(readindex_verdict<P>(c1.x, o1.x, static_cast<uint32_t>((ok4 >> 32) & 0xFFFFu),
+                                                    (s4 >> 16) & 0xFFu)) << 16;
+    r |= static_cast<uint32_t>(readindex_verdict<P>(c1.y, o1.y, static_cast<uint32_t>(ok4 >> 48),
+                                                    s4 >> 24)) << 24;
+    reinterpret_cast<uint32_t*>(a.result)[i] = r;
+  }
+  // the last G % 4 groups, one per lane of the first wave
+  const uint32_t g = quads * 4 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x * blockDim.x + threadIdx.x < (a.G & 3u))
+    a.result[g] = readindex_verdict<P>(a.conf[g], a.order[g], a.ok_mask[g], a.self_slot[g]);
 }
 
 }  // namespace jrq
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_readindex(
     const JrqReadIndexArgs* args, int num_cus, hipStream_t stream) {
-  const uint64_t need = (static_cast<uint64_t>(args->G) + 255) / 256;
+  const bool quad = ((reinterpret_cast<uintptr_t>(args->conf) | reinterpret_cast<uintptr_t>(args->order)) & 15u) == 0 &&
+                    (reinterpret_cast<uintptr_t>(args->ok_mask) & 7u) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(args->self_slot) | reinterpret_cast<uintptr_t>(args->result)) & 3u) == 0;
+  const uint64_t lanes = quad ? (static_cast<uint64_t>(args->G) + 3) / 4 : args->G;
+  const uint64_t need = (lanes + 255) / 256;
   const uint64_t cap = static_cast<uint64_t>(num_cus) * 8;
   const dim3 grid(static_cast<unsigned>(need < cap ? (need ? need : 1) : cap)), blk(256);
   switch (args->num_peers) {
-#define JRQ_CASE(P)                                                                        \
-  case P:                                                                                  \
-    hipLaunchKernelGGL(jrq::readindex_quorum_kernel<P>, grid, blk, 0, stream, *args); \
+#define JRQ_CASE(P)                                                                                \
+  case P:                                                                                          \
+    if (quad)                                                                                      \
+      hipLaunchKernelGGL((jrq::readindex_quorum_kernel<P, true>), grid, blk, 0, stream, *args);  \
+    else                                                                                           \
+      hipLaunchKernelGGL((jrq::readindex_quorum_kernel<P, false>), grid, blk, 0, stream, *args); \
     break;
     JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
     JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
