@@ -63,7 +63,7 @@ def committed_from(changed, pi_before, lc_before):
 
 
 @pytest.mark.parametrize("P,G,runs", [(5, 4096, 0.4), (3, 3001, 0.4), (16, 777, 0.4), (1, 64, 0.4),
-                                      (5, 70001, 0.95)])
+                                      (5, 70001, 0.95), (9, 20001, 0.4), (16, 9000, 0.9)])
 def test_one_epoch_vs_replay(engine, oracle, P, G, runs):
     """One epoch vs the BallotBox replay.  The last case has 35 workgroups (several per list
     segment, a pad group) and nearly every group walking conf runs (many quad-walk passes
