@@ -926,16 +926,14 @@ def leg_pinned(ctx, args, c5state):
     PCIe transfers included; beside them the same calls from unregistered memory (the engine's
     pinned bounce chunks).  The reference copies a direct buffer into a new byte[] before
     checksumming it (CrcUtil.java:65-80)."""
-    import ctypes
-
     from jraft_amd import _lib
     from jraft_amd import workloads as W
     eng = ctx.eng
-    L = _lib.load()
     d, eb, expected, flip, out = c5state
     c1 = W.CONFIGS["C1"]
     e1 = W.entry_batch(c1["pending"], c1["entry_bytes"], seed=W.SEED_BASE ^ 1)
     res = {}
+    regs_before = _lib.host_registrations()
     for name, e, exp in (("C5", eb, expected ^ flip.astype(np.uint64)), ("C1", e1, None)):
         n = len(e["offsets"]) - 1
         arrs = {"payload": e["payload"], "etype": e["etype"], "index": e["index"], "term": e["term"],
@@ -944,16 +942,17 @@ def leg_pinned(ctx, args, c5state):
             arrs["expected"] = np.ascontiguousarray(exp)
         row = {}
         for pinned in (True, False):
-            regs = []
-            if pinned:
-                for a in arrs.values():
-                    if L.jrq_host_register(ctypes.c_void_p(a.ctypes.data), a.nbytes) == 0:
-                        regs.append(a)
-            try:
+            # registered: page-aligned copies that own their pages (a JNI host's DirectByteBuffers
+            # carved from an aligned slab), kept alive until after their unregistration, which
+            # must succeed (_lib.Registered raises otherwise).  Round 4 registered the arrays in
+            # place -- small ones share heap pages with their neighbours -- ignored the
+            # unregister codes and freed them; the next legs' copies faulted once.
+            src = {k: _lib.page_aligned_copy(a) for k, a in arrs.items()} if pinned else arrs
+            with _lib.Registered(src.values() if pinned else ()) as regs:
                 def call():
-                    return eng.logentry_checksum_batch(arrs["etype"], arrs["index"], arrs["term"],
-                                                       None, arrs["payload"], arrs["offsets"],
-                                                       expected=arrs.get("expected"))
+                    return eng.logentry_checksum_batch(src["etype"], src["index"], src["term"],
+                                                       None, src["payload"], src["offsets"],
+                                                       expected=src.get("expected"))
                 call()
                 walls = []
                 for _ in range(max(3, min(10, args.steps // 5))):
@@ -961,9 +960,8 @@ def leg_pinned(ctx, args, c5state):
                     r = call()
                     walls.append(time.perf_counter() - t0)
                 wall = float(np.median(walls))
-            finally:
-                for a in regs:
-                    L.jrq_host_unregister(ctypes.c_void_p(a.ctypes.data))
+                n_regs = len(regs.live)
+            del src
             got = r[0] if isinstance(r, tuple) else r
             ok = None
             if ctx.oracle_checks:
@@ -978,12 +976,18 @@ def leg_pinned(ctx, args, c5state):
             h2d = pay + sum(a.nbytes for k, a in arrs.items() if k != "payload")
             row["registered" if pinned else "unregistered"] = {
                 "ms_per_call": wall * 1e3, "GBps_payload_pcie_inclusive": pay / wall / 1e9,
-                "h2d_bytes": h2d, "registered_arrays": len(regs), "bit_exact_vs_oracle": ok}
+                "h2d_bytes": h2d, "registered_arrays": n_regs, "bit_exact_vs_oracle": ok}
         res[name] = {"entries": n, "payload_bytes": int(e["offsets"][-1]), **row}
+    regs_after = _lib.host_registrations()
+    if regs_after != regs_before:
+        raise RuntimeError(f"libjrq page-lock registry {regs_before} -> {regs_after} after the "
+                           f"pinned leg: a registration outlived its leg")
     return {"how": "jrq_logentry_checksum_batch (host variant: H2D of every input, the fixed-size "
                    "kernel, D2H of the results, synchronised) timed by wall clock per call; "
-                   "registered = every caller array jrq_host_register'ed first (DMA straight from "
-                   "it), unregistered = through the engine's 8 MiB pinned bounce chunks",
+                   "registered = every caller array copied to page-aligned memory and "
+                   "jrq_host_register'ed first (DMA straight from it), unregistered = through the "
+                   "engine's 8 MiB pinned bounce chunks",
+            "registry_after": {"ranges": regs_after[0], "bytes": regs_after[1]},
             **res}
 
 

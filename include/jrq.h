@@ -133,11 +133,21 @@ int jrq_synchronize(jrq_engine *e);
 /* Page-lock a host buffer (e.g. a DirectByteBuffer's address) for fast staging.  Host
  * variants (the functions without _dev) DMA registered input memory straight to the device;
  * other input memory goes through the engine's two pinned 8 MiB bounce chunks (a CPU copy
- * overlapped with the previous chunk's DMA). */
+ * overlapped with the previous chunk's DMA).
+ * The driver pins whole pages, so registrations are tracked by page: a range sharing a page
+ * with a live jrq_host_register / jrq_host_alloc range is refused with JRQ_E_STATE and nothing
+ * is pinned (its uploads still work, through the bounce chunks).  Page-aligned buffers of
+ * whole pages never collide (ByteBuffer.allocateDirect memory need not be: a JNI host that
+ * pins many small buffers should carve them from one aligned slab). */
 int jrq_host_register(void *ptr, size_t bytes);
 /* Call only after the last call that used the buffer has returned, and before the memory is
- * freed: a registration left over freed pages is a stale device mapping of that address. */
+ * freed: a registration left over freed pages is a stale device mapping of that address.
+ * ptr must be the start of a live jrq_host_register range (else JRQ_E_INVALID); on JRQ_E_HIP
+ * the range stays registered and known, and the caller must not free the memory. */
 int jrq_host_unregister(void *ptr);
+/* Leak check: the bytes of the live range starting at ptr (returns 1, or 0 if none), or with
+ * ptr == NULL the bytes of every live range (returns their count).  No reference counterpart. */
+int jrq_host_registered_bytes(const void *ptr, size_t *bytes);
 /* Page-locked host memory owned by the HIP driver (hipHostMalloc): staging for a host that has
  * no buffer of its own to register (the C++ mirror's pack buffers).  The pages never return to
  * the process heap while the device may map them.  *out = NULL on failure. */

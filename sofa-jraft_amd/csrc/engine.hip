@@ -228,10 +228,16 @@ int upload(jrq_engine* e, void* dst, const void* src, size_t bytes) {
 
 // Caller memory registered with HIP (jrq_host_register, hipHostMalloc) goes straight to the
 // DMA engine; anything else through the bounce chunks.
-// Page-locked ranges libjrq made itself (jrq_host_alloc / jrq_host_register), base -> bytes:
-// an upload from one of them needs no HIP pointer query (a flush stages ~30 parts).
+// Page-locked ranges libjrq made itself (jrq_host_alloc / jrq_host_register), base -> range:
+// an upload from one of them needs no HIP pointer query (a flush stages ~30 parts), and a
+// registration whose pages overlap a live one is refused (jrq_host_register).
+struct PinnedRange {
+  size_t bytes;
+  bool owned;  // jrq_host_alloc (freed with jrq_host_free), else a caller registration
+};
 std::mutex g_pinned_mu;
-std::map<uintptr_t, size_t> g_pinned;
+std::map<uintptr_t, PinnedRange> g_pinned;
+constexpr uintptr_t kPage = 4096;
 
 bool known_pinned(const void* p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -239,13 +245,40 @@ bool known_pinned(const void* p) {
   auto it = g_pinned.upper_bound(a);
   if (it == g_pinned.begin()) return false;
   --it;
-  return a < it->first + it->second;
+  return a < it->first + it->second.bytes;
 }
 
-void note_pinned(const void* p, size_t bytes) {
+// Does [p, p + bytes), widened to whole pages, share a page with a live range?  The driver pins
+// and maps whole pages, so two registrations sharing one would each hold a mapping of it.
+bool overlaps_live_pages(uintptr_t p, size_t bytes) {
+  const uintptr_t lo = p & ~(kPage - 1), hi = (p + bytes + kPage - 1) & ~(kPage - 1);
   std::lock_guard<std::mutex> lk(g_pinned_mu);
-  if (bytes) g_pinned[reinterpret_cast<uintptr_t>(p)] = bytes;
-  else g_pinned.erase(reinterpret_cast<uintptr_t>(p));
+  auto it = g_pinned.lower_bound(hi);  // first range starting at or past hi: no overlap
+  while (it != g_pinned.begin()) {
+    --it;
+    const uintptr_t rlo = it->first & ~(kPage - 1);
+    const uintptr_t rhi = (it->first + it->second.bytes + kPage - 1) & ~(kPage - 1);
+    if (rlo < hi && lo < rhi) return true;
+    if (rhi <= lo) break;  // ranges are disjoint in pages, so ordered by end as by start
+  }
+  return false;
+}
+
+void note_pinned(const void* p, size_t bytes, bool owned) {
+  std::lock_guard<std::mutex> lk(g_pinned_mu);
+  g_pinned[reinterpret_cast<uintptr_t>(p)] = PinnedRange{bytes, owned};
+}
+
+// The live range starting exactly at p: 1 caller registration, 2 jrq_host_alloc, 0 none.
+int pinned_kind(const void* p) {
+  std::lock_guard<std::mutex> lk(g_pinned_mu);
+  auto it = g_pinned.find(reinterpret_cast<uintptr_t>(p));
+  return it == g_pinned.end() ? 0 : (it->second.owned ? 2 : 1);
+}
+
+void forget_pinned(const void* p) {
+  std::lock_guard<std::mutex> lk(g_pinned_mu);
+  g_pinned.erase(reinterpret_cast<uintptr_t>(p));
 }
 
 bool host_pinned(const void* p) {
@@ -506,6 +539,17 @@ int jrq_debug_set(jrq_engine* e, int option, int64_t value) {
 // registered from one thread, or allocated with hipHostMalloc, the failing test passed
 // (DESIGN.md §4.10).  A JNI host may pin DirectByteBuffers from any thread, so the library
 // serialises the calls itself; they are rare (setup, buffer growth), never per epoch.
+//
+// Round 4 saw one more "illegal memory access" from a pageable device-to-host copy after a clean
+// synchronisation, in a bench run whose previous leg had registered numpy arrays that share
+// heap pages with their neighbours, ignored the unregister return codes and freed the arrays
+// (DESIGN.md §4.10).  The driver pins and maps whole pages: a page shared by two registrations
+// is mapped twice, and a registration that outlives its memory leaves HIP treating whatever the
+// allocator later puts at that address as registered -- a copy to or from it then DMAs through
+// a mapping of pages the process no longer has.  So the registry is kept at page granularity:
+// a registration whose pages touch a live one is refused (the buffer then travels through the
+// bounce chunks), an unregistration forgets its range only once HIP has dropped it, and only
+// ranges this library registered can be unregistered.
 namespace {
 std::mutex g_pin_mu;
 }  // namespace
@@ -513,23 +557,39 @@ std::mutex g_pin_mu;
 int jrq_host_register(void* ptr, size_t bytes) {
   if (!ptr || !bytes) return JRQ_E_INVALID;
   std::lock_guard<std::mutex> lk(g_pin_mu);
+  if (overlaps_live_pages(reinterpret_cast<uintptr_t>(ptr), bytes)) return JRQ_E_STATE;
   if (hipHostRegister(ptr, bytes, hipHostRegisterDefault) != hipSuccess) {
     (void)hipGetLastError();
     return JRQ_E_HIP;
   }
-  note_pinned(ptr, bytes);
+  note_pinned(ptr, bytes, false);
   return JRQ_OK;
 }
 
 int jrq_host_unregister(void* ptr) {
   if (!ptr) return JRQ_E_INVALID;
   std::lock_guard<std::mutex> lk(g_pin_mu);
-  note_pinned(ptr, 0);
+  if (pinned_kind(ptr) != 1) return JRQ_E_INVALID;  // not a live jrq_host_register range
   if (hipHostUnregister(ptr) != hipSuccess) {
     (void)hipGetLastError();
-    return JRQ_E_HIP;
+    return JRQ_E_HIP;  // still registered: still known, so no later registration overlaps it
   }
+  forget_pinned(ptr);
   return JRQ_OK;
+}
+
+int jrq_host_registered_bytes(const void* ptr, size_t* bytes) {
+  if (!bytes) return JRQ_E_INVALID;
+  std::lock_guard<std::mutex> lk(g_pinned_mu);
+  *bytes = 0;
+  if (!ptr) {  // NULL: the total over every live range (a leak check for hosts and tests)
+    for (auto& r : g_pinned) *bytes += r.second.bytes;
+    return static_cast<int>(g_pinned.size());
+  }
+  auto it = g_pinned.find(reinterpret_cast<uintptr_t>(ptr));
+  if (it == g_pinned.end()) return 0;
+  *bytes = it->second.bytes;
+  return 1;
 }
 
 int jrq_host_alloc(size_t bytes, void** out) {
@@ -542,18 +602,19 @@ int jrq_host_alloc(size_t bytes, void** out) {
     *out = nullptr;
     return JRQ_E_NOMEM;
   }
-  note_pinned(*out, bytes);
+  note_pinned(*out, bytes, true);
   return JRQ_OK;
 }
 
 int jrq_host_free(void* ptr) {
   if (!ptr) return JRQ_E_INVALID;
   std::lock_guard<std::mutex> lk(g_pin_mu);
-  note_pinned(ptr, 0);
+  if (pinned_kind(ptr) != 2) return JRQ_E_INVALID;  // not a live jrq_host_alloc block
   if (hipHostFree(ptr) != hipSuccess) {
     (void)hipGetLastError();
     return JRQ_E_HIP;
   }
+  forget_pinned(ptr);
   return JRQ_OK;
 }
 

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <condition_variable>
@@ -23,6 +24,7 @@ namespace jraft {
 
 namespace testing {
 void (*fastPathHook)() = nullptr;
+void (*slotAssignHook)() = nullptr;
 }  // namespace testing
 
 namespace {
@@ -291,9 +293,18 @@ bool registerMembarrier() {
 }
 const bool g_membarrier = registerMembarrier();
 
+// Callers that entered their regions with the cheap entry (g_membarrier) rely on this barrier
+// for the store->load order quiesce and flush need; a local fence cannot give it, so a failing
+// membarrier after a successful registration is fatal rather than a silent downgrade.
 void heavyBarrier() {
-  if (!g_membarrier || syscall(__NR_membarrier, MEMBARRIER_CMD_PRIVATE_EXPEDITED, 0, 0) != 0)
+  if (!g_membarrier) {
     std::atomic_thread_fence(std::memory_order_seq_cst);
+    return;
+  }
+  if (syscall(__NR_membarrier, MEMBARRIER_CMD_PRIVATE_EXPEDITED, 0, 0) != 0) {
+    std::fprintf(stderr, "jraft_host: membarrier(PRIVATE_EXPEDITED) failed after registration\n");
+    std::abort();
+  }
 }
 
 // a one-byte spin lock (calls hold it for a few hundred ns at most)
@@ -334,7 +345,10 @@ struct Region {
       seq.store(s + 1, std::memory_order_relaxed);
       std::atomic_signal_fence(std::memory_order_seq_cst);
     } else {
-      seq.store(s + 1, std::memory_order_seq_cst);
+      // without membarrier the entry itself must order this store before the region's loads
+      // (of the gate byte, the slot ids): a seq_cst store alone does not, in the C++ model
+      seq.store(s + 1, std::memory_order_relaxed);
+      std::atomic_thread_fence(std::memory_order_seq_cst);
     }
   }
   ~Region() { seq.store(s + 2, std::memory_order_release); }
@@ -610,7 +624,7 @@ int GroupBatch::ackFast(uint32_t g, int64_t first, int64_t last, uint32_t peer) 
   if (last > ald(h.la)) return -1;
   const uint32_t* sp = slotPeerOf(g);
   uint32_t s = 0;
-  while (s < P_ && ald(sp[s]) != peer) ++s;
+  while (s < P_ && __atomic_load_n(&sp[s], __ATOMIC_ACQUIRE) != peer) ++s;
   if (s == P_) return -1;
   int64_t* mp = matchOf(g) + s;
   const int64_t m = ald(*mp);
@@ -688,13 +702,18 @@ int GroupBatch::slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved
     if (victim < 0) return -1;
     quiesce(g);  // the slot's peer may be acking on the fast path
   }
-  ast(sp[victim], peer);
+  // The slot's stamp and match first, its peer last (a release store the fast path's acquire
+  // load of the slot ids pairs with): an ack of `peer` that finds the slot on the fast path --
+  // possible for a free slot, which is not quiesced -- then finds it fully set up, and nothing
+  // here overwrites what that ack writes (the reverse order could reset its match).
   ast(su[victim], stampOf(gen_.load(std::memory_order_acquire), false));
   int64_t* m = matchOf(g);
   if (ald(m[victim]) != 0) {
     ast(m[victim], int64_t(0));
     markDirty(g, 1u << victim);
   }
+  __atomic_store_n(&sp[victim], peer, __ATOMIC_RELEASE);
+  if (__builtin_expect(testing::slotAssignHook != nullptr, 0)) testing::slotAssignHook();
   return victim;
 }
 

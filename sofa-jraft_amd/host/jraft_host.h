@@ -429,6 +429,9 @@ namespace testing {
 // Called inside commitAt's fast path between its reads and its writes when set (tests widen the
 // window a concurrent slot reassignment must not fall into).  Null in production.
 extern void (*fastPathHook)();
+// Called under the group's lock right after a slot is given to a peer (its id published), when
+// set: a test acks from that peer on the fast path there.  Null in production.
+extern void (*slotAssignHook)();
 }  // namespace testing
 
 }  // namespace jraft

@@ -105,6 +105,7 @@ SIGNATURES = [
     ("jrq_host_unregister", C.c_int, [_V]),
     ("jrq_host_alloc", C.c_int, [C.c_size_t, C.POINTER(C.c_void_p)]),
     ("jrq_host_free", C.c_int, [_V]),
+    ("jrq_host_registered_bytes", C.c_int, [_V, C.POINTER(C.c_size_t)]),
     ("jrq_debug_set", C.c_int, [_V, C.c_int, C.c_int64]),
     ("jrq_quorum_epoch_dev", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
     ("jrq_quorum_epoch_tiles_dev", C.c_int, [_V, C.POINTER(GroupTiles), _V, _V, C.c_uint32]),
@@ -192,6 +193,64 @@ def check(rc: int, engine_handle=None) -> None:
     if rc != JRQ_OK:
         msg = load().jrq_last_error(engine_handle)
         raise JrqError(rc, msg.decode() if msg else "")
+
+
+PAGE = 4096
+_STILL_REGISTERED = []
+
+
+def page_aligned_copy(a):
+    """A copy of numpy array `a` that starts on a page and owns every page it touches (a
+    DirectByteBuffer carved from an aligned slab): jrq_host_register never refuses it for a
+    page shared with another registration, and freeing it frees no neighbour's page."""
+    import numpy as np
+    a = np.ascontiguousarray(a)
+    n = a.nbytes
+    buf = np.empty(((n + PAGE - 1) // PAGE) * PAGE + PAGE, np.uint8)
+    off = (-buf.ctypes.data) % PAGE
+    v = buf[off:off + n].view(a.dtype).reshape(a.shape)
+    v[...] = a
+    return v
+
+
+def host_registrations():
+    """(live ranges, their total bytes) in libjrq's page-lock registry."""
+    n = C.c_size_t()
+    k = load().jrq_host_registered_bytes(None, C.byref(n))
+    return int(k), int(n.value)
+
+
+class Registered:
+    """Context manager: jrq_host_register every array (page-aligned copies from
+    page_aligned_copy), unregister on exit and raise if any unregistration fails -- a
+    registration left over freed memory is a stale device mapping of that address."""
+
+    def __init__(self, arrays):
+        self.arrays = list(arrays)
+        self.live = []
+
+    def __enter__(self):
+        L = load()
+        for a in self.arrays:
+            rc = L.jrq_host_register(C.c_void_p(a.ctypes.data), a.nbytes)
+            if rc != JRQ_OK:
+                self.__exit__(None, None, None)
+                raise JrqError(rc, f"jrq_host_register({a.nbytes} B at {a.ctypes.data:#x})")
+            self.live.append(a)
+        return self
+
+    def __exit__(self, *exc):
+        L = load()
+        bad = []
+        while self.live:
+            a = self.live.pop()
+            rc = L.jrq_host_unregister(C.c_void_p(a.ctypes.data))
+            if rc != JRQ_OK:
+                bad.append((a.ctypes.data, a.nbytes, ERRORS.get(rc, rc)))
+                _STILL_REGISTERED.append(a)  # never freed while HIP may still map it
+        if bad and exc[0] is None:
+            raise JrqError(-3, f"jrq_host_unregister failed: {bad}")
+        return False
 
 
 def conf_word(new_mask: int, old_mask: int = 0, new_q: int | None = None,

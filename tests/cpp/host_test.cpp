@@ -534,7 +534,15 @@ static void testConcurrentCallers(Engine& eng, uint32_t G, int64_t kEntries) {
   // the NodeImpl disruptor: batches of appends per group, every 3rd entry with a closure
   th.emplace_back([&] {
     try {
-      for (int64_t k = 0; k < kEntries; k += 8)
+      for (int64_t k = 0; k < kEntries; k += 8) {
+        // halfway, hold the appends until the background flusher has flushed at least once:
+        // the flusher then provably ran concurrently with the callers, whatever the timing
+        if (k == (kEntries / 16) * 8) {
+          const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(60);
+          while (batch->flushCount() < 1 && std::chrono::steady_clock::now() < until)
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+          if (batch->flushCount() < 1) failed = true;
+        }
         for (uint32_t g = 0; g < G; ++g) {
           for (int64_t i = 0; i < 8; ++i) {
             const int64_t idx = pi0[g] + k + i;
@@ -551,6 +559,7 @@ static void testConcurrentCallers(Engine& eng, uint32_t G, int64_t kEntries) {
           }
           published[g].store(pi0[g] + k + 7, std::memory_order_release);
         }
+      }
     } catch (...) {
       failed = true;
     }
@@ -625,7 +634,8 @@ static void testConcurrentCallers(Engine& eng, uint32_t G, int64_t kEntries) {
     for (int64_t idx = pi0[g]; idx <= lc; ++idx) exp += idx % 3 == 0;
     CHECK(obs[g].closuresOk == exp && obs[g].closuresFailed == 0);
   }
-  CHECK(batch->flushCount() >= 3);
+  // >= 1 background flush (waited for mid-run above) + the explicit one after stopFlusher
+  CHECK(batch->flushCount() >= 2);
   // step-downs from several threads at once (groups g % 16 < 4), concurrent with acks of the
   // other groups by peer 4 up to the last entry
   std::vector<std::thread> th2;
@@ -843,6 +853,59 @@ static void testFastPathStepDown(Engine& eng) {
                                             // landing late would commit 10..15)
 }
 
+// a free slot is given to a peer (append names a new peer) while that peer's
+// replicator acks.  The ack can find the slot on the fast path as soon as the peer id is
+// published (a free slot is not quiesced), so slotOf must have written the slot's stamp and
+// match before publishing, and nothing after: here the ack runs, to completion, at the instant
+// the id is published (the test hook), and must survive -- c's next contiguous ack then takes
+// the fast path again (its match is 4, not reset to 0), and entry 5 ({a, c}) commits.
+namespace {
+std::atomic<int> g_assignArm{0};
+std::atomic<bool> g_assignAckDone{false};
+std::function<void()> g_assignAck;
+std::thread g_assignThread;
+std::atomic<int> g_fastCount{0};
+}  // namespace
+static void testFreeSlotAckDuringAssign(Engine& eng) {
+  auto batch = std::make_shared<GroupBatch>(&eng, 2, 3);
+  BallotBox box(batch, 1);
+  Waiter w;
+  CHECK(box.init({w.fn()}));
+  const PeerId a("10.0.0.5", 7000), b("10.0.0.5", 7001), c("10.0.0.5", 7002);
+  CHECK(box.resetPendingIndex(1));
+  CHECK(box.appendPendingTasks(conf("10.0.0.5:7000,10.0.0.5:7001"), nullptr, 4));
+  CHECK(box.commitAt(1, 4, a));
+  batch->flush();
+  CHECK(box.getLastCommittedIndex() == 0);
+  g_assignAck = [&] { box.commitAt(1, 4, c); };  // c catches up on 1..4 (no ballot counts it)
+  testing::slotAssignHook = [] {
+    int one = 1;
+    if (!g_assignArm.compare_exchange_strong(one, 0)) return;
+    g_assignThread = std::thread([] {
+      g_assignAck();
+      g_assignAckDone.store(true);
+    });
+    // the fast path takes no lock: it completes while this thread holds the group's lock
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!g_assignAckDone.load() && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5))
+      std::this_thread::yield();
+  };
+  g_assignArm.store(1);
+  CHECK(box.appendPendingTask(conf("10.0.0.5:7000,10.0.0.5:7002"), nullptr));  // entry 5: c's slot
+  testing::slotAssignHook = nullptr;
+  if (g_assignThread.joinable()) g_assignThread.join();
+  CHECK(g_assignAckDone.load());
+  testing::fastPathHook = [] { g_fastCount.fetch_add(1); };
+  CHECK(box.commitAt(5, 5, c));
+  testing::fastPathHook = nullptr;
+  CHECK(g_fastCount.load() == 1);  // contiguous with the kept ack of 1..4
+  CHECK(box.commitAt(5, 5, a));
+  CHECK(box.commitAt(1, 5, b));
+  batch->flush();
+  CHECK(box.getLastCommittedIndex() == 5);
+  CHECK(!w.calls.empty() && w.calls.back() == 5);
+}
+
 // The append fast path reuses the group's last conf word only for the same peers in the same
 // split between conf and old conf: {a,b,c} then {a,b} + old {c} is a new run (Ballot.init with
 // oldQuorum 1), and entry 2 needs c's ack.
@@ -926,6 +989,7 @@ int main(int argc, char** argv) {
     tests.push_back({"testManyBatchesOneThread", [&] { testManyBatchesOneThread(e); }});
     tests.push_back({"testConfCacheSplit", [&] { testConfCacheSplit(e); }});
     tests.push_back({"testFastPathStepDown", [&] { testFastPathStepDown(e); }});
+    tests.push_back({"testFreeSlotAckDuringAssign", [&] { testFreeSlotAckDuringAssign(e); }});
   }
   for (auto& t : tests) {
     const int before = g_fail;

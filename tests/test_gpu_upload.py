@@ -119,3 +119,98 @@ def test_concurrent_registrations_then_pageable_uploads(oracle):
     offs = np.arange(0, len(payload) + 1, 4096, dtype=np.uint64)
     with Engine(0) as e:
         np.testing.assert_array_equal(e.crc64_batch(payload, offs), oracle.crc64_batch(payload, offs))
+
+
+def test_registry_refuses_shared_pages_and_unknown_ranges(oracle):
+    """libjrq tracks registrations by page: a range sharing a page with a live one is refused
+    (JRQ_E_STATE, nothing pinned), so no page is mapped twice; unregistering a pointer that is
+    not the start of a live jrq_host_register range is refused (JRQ_E_INVALID) without calling
+    HIP; a refused buffer still uploads correctly, through the bounce chunks."""
+    import ctypes
+
+    from jraft_amd import Engine
+    L = _lib.load()
+    base = _lib.host_registrations()
+    buf = np.empty(6 * 4096, np.uint8)
+    a0 = (-buf.ctypes.data) % 4096
+    first = buf[a0:a0 + 4096 + 100]                  # pages 0 and 1
+    second = buf[a0 + 4096 + 200:a0 + 3 * 4096]       # pages 1 and 2: shares page 1
+    third = buf[a0 + 2 * 4096:a0 + 4 * 4096]         # pages 2 and 3: free of `first`
+    vp = lambda a: ctypes.c_void_p(a.ctypes.data)    # noqa: E731
+    assert L.jrq_host_register(vp(first), first.nbytes) == 0
+    try:
+        assert L.jrq_host_register(vp(second), second.nbytes) == -6   # JRQ_E_STATE
+        assert _lib.host_registrations() == (base[0] + 1, base[1] + first.nbytes)
+        assert L.jrq_host_unregister(vp(second)) == -1                # never registered
+        assert L.jrq_host_unregister(ctypes.c_void_p(first.ctypes.data + 8)) == -1  # interior
+        assert L.jrq_host_free(vp(first)) == -1                       # not a jrq_host_alloc block
+        assert L.jrq_host_register(vp(third), third.nbytes) == 0
+        assert L.jrq_host_unregister(vp(third)) == 0
+        # the refused range's upload takes the bounce chunks and is still right
+        second[:] = W.random_bytes(11, second.nbytes)
+        offs = np.array([0, 777, second.nbytes], np.uint64)
+        with Engine(0) as e:
+            np.testing.assert_array_equal(e.crc64_batch(second, offs), oracle.crc64_batch(second, offs))
+    finally:
+        assert L.jrq_host_unregister(vp(first)) == 0
+    assert L.jrq_host_unregister(vp(first)) == -1                     # already gone
+    assert _lib.host_registrations() == base
+    p = ctypes.c_void_p()
+    assert L.jrq_host_alloc(10000, ctypes.byref(p)) == 0
+    assert _lib.host_registrations()[0] == base[0] + 1
+    assert L.jrq_host_unregister(p) == -1                             # alloc'ed, not registered
+    assert L.jrq_host_free(p) == 0
+    assert _lib.host_registrations() == base
+
+
+def test_pinned_then_c1_then_lease_legs(engine):
+    """The bench sequence of round 4's one unexplained fault: the pinned leg
+    (every C5 / C1 input registered, used, unregistered), then C1, then the lease leg, whose
+    result copies faulted once.  The registry must be back at its size before the pinned leg,
+    HIP must know no registration over fresh arrays of the lease results' sizes, and both later
+    legs must be bit-exact against the oracle."""
+    import os
+    import sys
+    import types
+
+    import torch
+
+    from conftest import assert_unregistered, device_checkpoint
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, ROOT)
+    import bench
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.Stream(dev)
+    args = types.SimpleNamespace(steps=5, warmup=1, no_cpu=False)
+    base = _lib.host_registrations()
+    old = bench.WARM_MS
+    bench.WARM_MS = 5.0
+    try:
+        with torch.cuda.stream(stream):
+            engine.use_stream(stream.cuda_stream)
+            ctx = bench.Ctx(engine, stream, dev, 1, 0, args)
+            _, _, c5state = bench.leg_c5(ctx, args, lambda: None, lambda x: x, time_it=False)
+            pin = bench.leg_pinned(ctx, args, c5state)
+            del c5state
+            for name in ("C5", "C1"):
+                for how in ("registered", "unregistered"):
+                    assert pin[name][how]["bit_exact_vs_oracle"] is True, (name, how)
+            assert pin["C5"]["registered"]["registered_arrays"] == 6
+            assert _lib.host_registrations() == base
+            device_checkpoint("after the pinned leg")
+            c1 = bench.leg_c1(ctx, args)
+            assert c1["bit_exact_vs_oracle"] is True
+            G = 1 << 20
+            fresh = {"ok": np.empty(G, np.uint8), "lead": np.empty(G, np.int64),
+                     "dead": np.empty(G, np.int16), "ts": np.empty((5, G), np.int64)}
+            assert_unregistered(fresh, "before the lease leg")
+            del fresh
+            from jraft_amd import workloads as W
+            conf = W.quorum_batch("C3", groups=G)["conf"]
+            lease = bench.leg_lease(ctx, args, bench.to_dev(conf, dev), G, 5)
+            assert lease["bit_exact_vs_oracle"] is True
+            torch.cuda.synchronize()
+    finally:
+        bench.WARM_MS = old
+        engine.use_stream(None)
+    assert _lib.host_registrations() == base
