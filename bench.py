@@ -39,7 +39,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 QUORUM_EPOCH_BUFFERS = 6
 LEGS = ("quorum", "table", "drive", "C2", "C2L", "C3K", "C5", "C1", "ae", "v2", "snapshot", "pinned",
-        "lease", "readindex", "fanout", "peak", "cpu")
+        "lease", "readindex", "tick", "fanout", "peak", "cpu")
 
 
 def quorum_bytes_per_group(P: int) -> int:
@@ -385,6 +385,15 @@ class Ctx:
         self.eng, self.stream, self.dev = eng, stream, dev
         self.world, self.rank, self.args = world, rank, args
         self.oracle_checks = rank == 0 and not args.no_cpu
+        # the process group's backend: "nccl" (RCCL, the driver's scaling runs) or "gloo"
+        # (tests/test_gpu_bench_ranks.py: several ranks on one GPU, which RCCL refuses);
+        # gloo reduces host tensors
+        self.backend = getattr(args, "dist_backend", "nccl")
+
+    def coll_device(self):
+        """Where this process group's small collectives (max over ranks, gathers) run."""
+        import torch
+        return self.dev if self.backend == "nccl" else torch.device("cpu")
 
     def sync(self):
         import torch
@@ -396,7 +405,7 @@ class Ctx:
             return [x]
         import torch
         import torch.distributed as dist
-        t = torch.zeros(self.world, dtype=torch.float64, device=self.dev)
+        t = torch.zeros(self.world, dtype=torch.float64, device=self.coll_device())
         t[self.rank] = x
         dist.all_reduce(t)
         return [float(v) for v in t.cpu()]
@@ -434,12 +443,18 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
     # one GPU: the local committed[] already is the node-wide snapshot (nothing to gather)
     snapshot = torch.empty(k * world, dtype=torch.int64, device=dev) if world > 1 else local
     nranks = 1
-    if world > 1:
+    publish_via = "none (one GPU)"
+    if world > 1 and ctx.backend == "nccl":
         uid = [Engine.rccl_unique_id() if rank == 0 else None]
         import torch.distributed as dist
         dist.broadcast_object_list(uid, src=0)
         eng.rccl_init(world, rank, uid[0])
         nranks = eng.rccl_nranks()
+        publish_via = "RCCL all-gather (jrq_publish_committed_dev)"
+    elif world > 1:
+        import torch.distributed as dist
+        nranks = dist.get_world_size()
+        publish_via = "gloo all-gather of host copies (several ranks on one GPU: no RCCL)"
 
     # one prepared launch per epoch buffer (arguments resolved once, as a C / JNI host keeps
     # its jrq_group_batch): the step loop then costs the GPU epoch, not Python marshalling
@@ -459,8 +474,14 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
                              t["last_committed"], t["conf"], out, status)
 
     def allgather(send, recv):
-        if world > 1:
+        if world > 1 and ctx.backend == "nccl":
             eng.publish_committed_dev(send, recv)
+        elif world > 1:
+            import torch.distributed as dist
+            ctx.sync()
+            h = torch.empty(send.numel() * world, dtype=send.dtype)
+            dist.all_gather_into_tensor(h, send.cpu())
+            recv.copy_(h.to(recv.device))
     se = D.ShardedEpochs(Gtot, world, rank, epoch_fn, allgather, local, snapshot,
                          publish_every=args.publish_every)
     # kernel only (HIP events on the engine's stream)
@@ -512,7 +533,8 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
                        **pmc_traffic("quorum", "quorum_epoch_pair_kernel<5, false, false>"))
     return {
         "value": value, "elapsed": elapsed, "cfg": cfg, "G": G, "P": P, "roofline": rl,
-        "multi_gpu": {"rccl_nranks": nranks, "publish_every": args.publish_every,
+        "multi_gpu": {"rccl_nranks": nranks, "publish_via": publish_via,
+                      "publish_every": args.publish_every,
                       "kernel_only_ms": k_ms_max, "publish_ms": pub_ms,
                       "kernel_plus_publish_ms": elapsed * 1e3 / args.steps,
                       "kernel_only_decisions_per_s": Gtot / (k_ms_max * 1e-3),
@@ -1294,9 +1316,13 @@ def leg_lease(ctx, args, quorum_conf_dev, G, P):
     lok = torch.empty(G, dtype=torch.uint8, device=dev)
     ldead = torch.empty(G, dtype=torch.int16, device=dev)
 
+    # prepared launches (arguments resolved once, as a JNI host keeps its buffers): a Python
+    # call per launch costs about as much as the 13-us kernel and would starve the GPU
+    launchers = [eng.leader_tick_launcher(ts, quorum_conf_dev, self_slot, now_ms, lease_to, lok,
+                                          lead, ldead, None, None, None) for ts in ts_bufs]
+
     def step(i):
-        eng.lease_check_dev(ts_bufs[i % QUORUM_EPOCH_BUFFERS], quorum_conf_dev, self_slot, now_ms,
-                            lease_to, lok, lead, ldead)
+        launchers[i % QUORUM_EPOCH_BUFFERS]()
     ms, _ = ctx.timed(step)
     ok = None
     if ctx.oracle_checks:  # one launch on buffer 0 from fresh lease starts, every group
@@ -1312,7 +1338,8 @@ def leg_lease(ctx, args, quorum_conf_dev, G, P):
     lb = (8 * P + 28) * G
     return {"workload": f"{G} leader groups x {P} peers (conf + old conf), checkDeadNodes0",
             "decisions_per_s": G / (ms * 1e-3), "kernel_ms": ms, "bit_exact_vs_oracle": ok,
-            "roofline": roofline(lb, ms, **pmc_traffic("lease", f"lease_check_kernel<{P}>"))}
+            "roofline": roofline(lb, ms, kernel=f"leader_tick_pair_kernel<{P}, false>",
+                                 **pmc_traffic("lease", f"leader_tick_pair_kernel<{P}, false>"))}
 
 
 def leg_readindex(ctx, args, quorum_conf_dev, quorum_conf, G, P):
@@ -1333,9 +1360,10 @@ def leg_readindex(ctx, args, quorum_conf_dev, quorum_conf, G, P):
     self_slot = to_dev(self_np, dev)
     res = torch.empty(G, dtype=torch.uint8, device=dev)
 
+    launchers = [eng.readindex_launcher(quorum_conf_dev, self_slot, b[2], b[3], P, res) for b in bufs]
+
     def step(i):
-        b = bufs[i % QUORUM_EPOCH_BUFFERS]
-        eng.readindex_quorum_dev(quorum_conf_dev, self_slot, b[2], b[3], P, res)
+        launchers[i % QUORUM_EPOCH_BUFFERS]()
     ms, _ = ctx.timed(step)
     ok = None
     counts = None
@@ -1352,6 +1380,58 @@ def leg_readindex(ctx, args, quorum_conf_dev, quorum_conf, G, P):
             "rounds_per_s": G / (ms * 1e-3), "kernel_ms": ms, "bit_exact_vs_oracle": ok,
             "verdicts": counts,
             "roofline": roofline(rb, ms, **pmc_traffic("readindex", f"readindex_quorum_kernel<{P}, true>"))}
+
+
+def leg_tick(ctx, args, quorum_conf_dev, quorum_conf, G, P):
+    """The leader tick (jrq_leader_tick_dev): the lease check and the ReadIndex round of the
+    same G leader groups in one launch (the lease leg's timestamps and the ReadIndex leg's
+    responses, generated the same way), checked against both oracles on every group."""
+    import torch
+    eng, dev, rank = ctx.eng, ctx.dev, ctx.rank
+    rng = np.random.default_rng(rank ^ 0x71C4)
+    now_ms, lease_to = 1 << 40, 900
+    self_np = np.zeros(G, np.uint8)
+    bufs = []
+    for _ in range(QUORUM_EPOCH_BUFFERS):  # rotating inputs: no launch re-reads the last one's
+        ts = (now_ms - rng.integers(0, 2 * lease_to, (P, G))).astype(np.int64)
+        pos = np.argsort(rng.random((G, P - 1)), axis=1).astype(np.uint64) + np.uint64(1)
+        pos[rng.random((G, P - 1)) < 0.3] = 0
+        order = (pos << (4 * np.arange(1, P, dtype=np.uint64))).sum(axis=1).astype(np.uint64)
+        okm = ((rng.random((G, P - 1)) < 0.55) << np.arange(1, P)).sum(axis=1).astype(np.uint16)
+        bufs.append({"ts": ts, "order": order, "okm": okm, "d_ts": to_dev(ts, dev),
+                     "d_order": to_dev(order, dev), "d_okm": to_dev(okm.view(np.int16), dev)})
+    self_slot = to_dev(self_np, dev)
+    lead = torch.zeros(G, dtype=torch.int64, device=dev)
+    lok = torch.empty(G, dtype=torch.uint8, device=dev)
+    ldead = torch.empty(G, dtype=torch.int16, device=dev)
+    ri = torch.empty(G, dtype=torch.uint8, device=dev)
+    launchers = [eng.leader_tick_launcher(b["d_ts"], quorum_conf_dev, self_slot, now_ms, lease_to,
+                                          lok, lead, ldead, b["d_order"], b["d_okm"], ri)
+                 for b in bufs]
+    ms, _ = ctx.timed(lambda i: launchers[i % QUORUM_EPOCH_BUFFERS]())
+    ok = None
+    if ctx.oracle_checks:  # one launch on buffer 0 from fresh lease starts, every group
+        import jraft_oracle as O
+        lead.zero_()
+        launchers[0]()
+        ctx.sync()
+        b = bufs[0]
+        eok, elead, edead = O.lease_check(b["ts"], quorum_conf, self_np, now_ms, lease_to,
+                                          np.zeros(G, np.int64))
+        eri = O.readindex_quorum(quorum_conf, self_np, b["order"], b["okm"], P)
+        ok = bool(np.array_equal(lok.cpu().numpy(), eok)) and \
+            bool(np.array_equal(lead.cpu().numpy(), elead)) and \
+            bool(np.array_equal(ldead.cpu().numpy().view(np.uint16), edead)) and \
+            bool(np.array_equal(ri.cpu().numpy(), eri))
+    # per group: timestamps 8P + conf 8 + self 1 + lease start 8 read, 8 written + ok 1 + dead 2
+    # (the lease check, 8P + 28) + order 8 + ok mask 2 read, verdict 1 written (ReadIndex, 11)
+    tb = (8 * P + 39) * G
+    return {"workload": f"{G} leader groups x {P} peers: lease check + one ReadIndex heartbeat "
+                        f"round each, one launch (jrq_leader_tick_dev)",
+            "groups_per_s": G / (ms * 1e-3), "kernel_ms": ms, "bit_exact_vs_oracle": ok,
+            "roofline": roofline(tb, ms, kernel=f"leader_tick_pair_kernel<{P}, true>",
+                                 bytes_note="8P+39 B per group",
+                                 **pmc_traffic("tick", f"leader_tick_pair_kernel<{P}, true>"))}
 
 
 def leg_fanout(ctx, args, G):
@@ -1641,6 +1721,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--detail", default=os.path.join(ROOT, DETAIL_FILE),
                     help="file for the full per-leg result (the printed line is the summary)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 process group: nccl (RCCL, one GPU per rank) or gloo (tests: "
+                         "several ranks on one GPU, the snapshot all-gathered through host copies)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank on cuda:0 (tests of the N>1 orchestration on a 1-GPU box)")
     ap.add_argument("--legs", default="all",
                     help=f"comma list of {','.join(LEGS)} (the headline quorum leg always runs "
                          "unless the list omits it; PMC passes run one leg each)")
@@ -1665,10 +1750,14 @@ def main():
         legs = {"quorum", "C5"}
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if args.one_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 and args.dist_backend == "nccl":
         dist.init_process_group("nccl", device_id=dev)
+    elif world > 1:
+        dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
@@ -1677,7 +1766,8 @@ def main():
     def max_over_ranks(x: float) -> float:
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -1754,13 +1844,16 @@ def main():
     if "C1" in legs:
         _LEG[0] = "C1"
         line["C1"] = leg_c1(ctx, args)
-    c3conf = W.quorum_batch("C3", groups=G)["conf"] if legs & {"lease", "readindex"} else None
+    c3conf = W.quorum_batch("C3", groups=G)["conf"] if legs & {"lease", "readindex", "tick"} else None
     if "lease" in legs:
         _LEG[0] = "lease"
         extras["lease_check"] = leg_lease(ctx, args, to_dev(c3conf, dev), G, 5)
     if "readindex" in legs:
         _LEG[0] = "readindex"
         extras["readindex_quorum"] = leg_readindex(ctx, args, to_dev(c3conf, dev), c3conf, G, 5)
+    if "tick" in legs:
+        _LEG[0] = "tick"
+        extras["leader_tick"] = leg_tick(ctx, args, to_dev(c3conf, dev), c3conf, G, 5)
     if "fanout" in legs:
         _LEG[0] = "fanout"
         extras["commit_fanout"] = leg_fanout(ctx, args, G)

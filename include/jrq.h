@@ -469,19 +469,44 @@ int jrq_lease_check(jrq_engine *e, const int64_t *last_rpc_ts, uint64_t ld, uint
  *   ok_mask[g]    bit p = slot p's response was OK with success = true (else a failure)
  * result_out[g] = JRQ_READINDEX_SUCCESS once ackSuccess + 1 >= quorum, JRQ_READINDEX_FAILURE
  * once ackFailures >= failPeersThreshold (quorum - 1 for an even peer count, quorum for an
- * odd one), whichever the arrival order reached first, else JRQ_READINDEX_PENDING.  Stateless:
+ * odd one), whichever the arrival order reached first, else JRQ_READINDEX_PENDING;
+ * JRQ_READINDEX_INVALID when conf[g] names a slot >= num_peers (no response can come from it:
+ * the input is outside the contract, and the group would otherwise stay pending).  Stateless:
  * call again with the round's later responses added; a verdict never changes.  The host keeps
  * readLeader's other checks (the term of lastCommittedIndex, the requester in the conf, the
  * lease-based option). */
 #define JRQ_READINDEX_PENDING 0
 #define JRQ_READINDEX_SUCCESS 1
 #define JRQ_READINDEX_FAILURE 2
+#define JRQ_READINDEX_INVALID 3
 int jrq_readindex_quorum_dev(jrq_engine *e, const uint64_t *conf_dev, const uint8_t *self_slot_dev,
                              const uint64_t *order_dev, const uint16_t *ok_mask_dev,
                              uint32_t num_peers, uint32_t G, uint8_t *result_out_dev);
 int jrq_readindex_quorum(jrq_engine *e, const uint64_t *conf, const uint8_t *self_slot,
                          const uint64_t *order, const uint16_t *ok_mask, uint32_t num_peers,
                          uint32_t G, uint8_t *result_out);
+
+/* ---------------------------------------------------------------- leader tick -- */
+
+/* The leader's periodic pass over G leader groups in one launch: jrq_lease_check_dev's lease
+ * check (NodeImpl.handleStepDownTimeout -> checkDeadNodes, JC/core/NodeImpl.java:1970-2016)
+ * and jrq_readindex_quorum_dev's ReadIndex round (:1246-1396) of the same groups, which read
+ * the same conf word and self slot once.  The arguments and outputs are those two calls';
+ * order / ok_mask / ri_result_out may all be NULL (the lease check alone).  A JNI host calls it
+ * from the step-down timer (handleStepDownTimeout runs every electionTimeout / 2) with the
+ * heartbeat responses collected since the last tick.  No single reference counterpart: it
+ * batches two per-node timer / callback paths into one device pass. */
+int jrq_leader_tick_dev(jrq_engine *e, const int64_t *last_rpc_ts_dev, uint64_t ld,
+                        uint32_t num_peers, const uint64_t *conf_dev, const uint8_t *self_slot_dev,
+                        uint32_t G, int64_t now_ms, int64_t lease_timeout_ms, uint8_t *ok_out_dev,
+                        int64_t *lease_start_inout_dev, uint16_t *dead_out_dev,
+                        const uint64_t *order_dev, const uint16_t *ok_mask_dev,
+                        uint8_t *ri_result_out_dev);
+int jrq_leader_tick(jrq_engine *e, const int64_t *last_rpc_ts, uint64_t ld, uint32_t num_peers,
+                    const uint64_t *conf, const uint8_t *self_slot, uint32_t G, int64_t now_ms,
+                    int64_t lease_timeout_ms, uint8_t *ok_out, int64_t *lease_start_inout,
+                    uint16_t *dead_out, const uint64_t *order, const uint16_t *ok_mask,
+                    uint8_t *ri_result_out);
 
 /* ------------------------------------------------------- commit fan-out -- */
 

@@ -201,6 +201,8 @@ void jo_lease_check(uint32_t G, uint32_t P, const int64_t *ts, const uint64_t *c
  * from the conf peers the leader sent a heartbeat to (every peer but itself). */
 uint8_t jo_readindex_round(uint32_t mask, uint32_t P, uint32_t self, uint64_t order, uint32_t ok_mask) {
     int32_t ids[16];
+    /* a conf naming a slot >= P: outside the batch contract (include/jrq.h), reported INVALID */
+    if (P < 16 && (mask >> P) != 0) return 3;
     const int32_t n = mask_to_ids(mask, ids); /* conf.getConf().getPeers() */
     const int32_t quorum = n == 0 ? 0 : n / 2 + 1;
     if (quorum <= 1) return 1; /* "Only one peer, fast path": success */

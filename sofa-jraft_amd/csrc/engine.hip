@@ -1075,7 +1075,7 @@ int jrq_lease_check(jrq_engine* e, const int64_t* ts, uint64_t ld, uint32_t num_
 // ------------------------------------------------------------ ReadIndex -----
 
 static_assert(JRQ_READINDEX_PENDING == jrq::kRiPending && JRQ_READINDEX_SUCCESS == jrq::kRiSuccess &&
-                  JRQ_READINDEX_FAILURE == jrq::kRiFailure,
+                  JRQ_READINDEX_FAILURE == jrq::kRiFailure && JRQ_READINDEX_INVALID == jrq::kRiInvalid,
               "ReadIndex verdicts");
 
 int jrq_readindex_quorum_dev(jrq_engine* e, const uint64_t* conf, const uint8_t* self_slot,
@@ -1123,6 +1123,82 @@ int jrq_readindex_quorum(jrq_engine* e, const uint64_t* conf, const uint8_t* sel
                                      static_cast<uint8_t*>(dres))))
     return rc;
   JRQ_HIP(e, hipMemcpyAsync(result_out, dres, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
+// ------------------------------------------------------------ leader tick ---
+
+int jrq_leader_tick_dev(jrq_engine* e, const int64_t* ts, uint64_t ld, uint32_t num_peers,
+                        const uint64_t* conf, const uint8_t* self_slot, uint32_t G, int64_t now_ms,
+                        int64_t lease_timeout_ms, uint8_t* ok_out, int64_t* lease_start,
+                        uint16_t* dead_out, const uint64_t* order, const uint16_t* ok_mask,
+                        uint8_t* ri_result) {
+  if (!e) return JRQ_E_INVALID;
+  if (G == 0) return JRQ_OK;
+  if (!ts || !conf || !self_slot || !ok_out || !lease_start || ld < G || num_peers == 0 ||
+      num_peers > JRQ_MAX_PEERS)
+    return fail(e, JRQ_E_INVALID, "bad leader-tick batch");
+  if ((order != nullptr) != (ok_mask != nullptr) || (order != nullptr) != (ri_result != nullptr))
+    return fail(e, JRQ_E_INVALID, "order, ok_mask and ri_result: all three or none");
+  DeviceGuard guard(e->device);
+  JrqLeaseArgs a{};
+  a.last_rpc_ts = ts;
+  a.ld = ld;
+  a.conf = conf;
+  a.self_slot = self_slot;
+  a.now_ms = now_ms;
+  a.lease_timeout_ms = lease_timeout_ms;
+  a.num_peers = num_peers;
+  a.G = G;
+  a.ok = ok_out;
+  a.lease_start = lease_start;
+  a.dead = dead_out;
+  a.order = order;
+  a.ri_ok_mask = ok_mask;
+  a.ri_result = ri_result;
+  JRQ_HIP(e, jrq_launch_lease(&a, e->num_cus, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_leader_tick(jrq_engine* e, const int64_t* ts, uint64_t ld, uint32_t num_peers,
+                    const uint64_t* conf, const uint8_t* self_slot, uint32_t G, int64_t now_ms,
+                    int64_t lease_timeout_ms, uint8_t* ok_out, int64_t* lease_start,
+                    uint16_t* dead_out, const uint64_t* order, const uint16_t* ok_mask,
+                    uint8_t* ri_result) {
+  if (!e) return JRQ_E_INVALID;
+  if (G == 0) return JRQ_OK;
+  if (!ts || !conf || !self_slot || !ok_out || !lease_start || ld < G || num_peers == 0 ||
+      num_peers > JRQ_MAX_PEERS)
+    return fail(e, JRQ_E_INVALID, "bad leader-tick batch");
+  if ((order != nullptr) != (ok_mask != nullptr) || (order != nullptr) != (ri_result != nullptr))
+    return fail(e, JRQ_E_INVALID, "order, ok_mask and ri_result: all three or none");
+  DeviceGuard guard(e->device);
+  int rc;
+  const int64_t* dts;
+  const uint64_t *dconf, *dord = nullptr;
+  const uint8_t* dself;
+  const int64_t* dlead;
+  const uint16_t* dokm = nullptr;
+  if ((rc = stage_in(e, 0, ts, (num_peers - 1) * ld + G, &dts))) return rc;
+  if ((rc = stage_in(e, 1, conf, G, &dconf))) return rc;
+  if ((rc = stage_in(e, 2, self_slot, G, &dself))) return rc;
+  if ((rc = stage_in(e, 3, lease_start, G, &dlead))) return rc;
+  if (order && (rc = stage_in(e, 4, order, G, &dord))) return rc;
+  if (ok_mask && (rc = stage_in(e, 5, ok_mask, G, &dokm))) return rc;
+  void *dok, *ddead, *dres = nullptr;
+  if ((rc = ensure_stage(e, 8, G, &dok))) return rc;
+  if ((rc = ensure_stage(e, 9, static_cast<size_t>(G) * 2, &ddead))) return rc;
+  if (ri_result && (rc = ensure_stage(e, 10, G, &dres))) return rc;
+  if ((rc = jrq_leader_tick_dev(e, dts, ld, num_peers, dconf, dself, G, now_ms, lease_timeout_ms,
+                                static_cast<uint8_t*>(dok), const_cast<int64_t*>(dlead),
+                                static_cast<uint16_t*>(ddead), dord, dokm,
+                                static_cast<uint8_t*>(dres))))
+    return rc;
+  JRQ_HIP(e, hipMemcpyAsync(ok_out, dok, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(lease_start, dlead, static_cast<size_t>(G) * 8, hipMemcpyDeviceToHost, e->stream));
+  if (dead_out) JRQ_HIP(e, hipMemcpyAsync(dead_out, ddead, static_cast<size_t>(G) * 2, hipMemcpyDeviceToHost, e->stream));
+  if (ri_result) JRQ_HIP(e, hipMemcpyAsync(ri_result, dres, G, hipMemcpyDeviceToHost, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }

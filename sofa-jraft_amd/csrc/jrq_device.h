@@ -33,7 +33,7 @@ constexpr int kCrcRegsBlock = 768;   // the register boundary path's workgroup (
 // Status flags, identical to include/jrq.h jrq_group_status.
 constexpr uint8_t kStNotLeader = 1, kStOutOfRange = 2, kStEmptyConf = 4;
 // ReadIndex heartbeat round verdicts (include/jrq.h JRQ_READINDEX_*)
-constexpr uint8_t kRiPending = 0, kRiSuccess = 1, kRiFailure = 2;
+constexpr uint8_t kRiPending = 0, kRiSuccess = 1, kRiFailure = 2, kRiInvalid = 3;
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -160,6 +160,11 @@ struct JrqLeaseArgs {
   uint8_t* ok;                  // [G] bit0 conf quorum alive, bit1 old-conf quorum alive (or no old conf)
   int64_t* lease_start;         // [G] lastLeaderTimestamp after the checks (in/out)
   uint16_t* dead;               // [G] peer slots found dead (new | old conf), nullable
+  // the leader tick (jrq_leader_tick*): the ReadIndex round of the same groups, fused; null
+  // for the lease check alone
+  const uint64_t* order;        // [G] nibble p = arrival position of slot p's response, 0 = none
+  const uint16_t* ri_ok_mask;   // [G] bit p = slot p's response succeeded
+  uint8_t* ri_result;           // [G] kRiPending / kRiSuccess / kRiFailure / kRiInvalid
 };
 
 // ReadIndex heartbeat quorum (quorum.hip): one heartbeat round per group.
@@ -170,7 +175,7 @@ struct JrqReadIndexArgs {
   const uint16_t* ok_mask;      // [G] bit p = slot p's response succeeded
   uint32_t num_peers;
   uint32_t G;
-  uint8_t* result;              // [G] kRiPending / kRiSuccess / kRiFailure
+  uint8_t* result;              // [G] kRiPending / kRiSuccess / kRiFailure / kRiInvalid
 };
 
 // AppendEntries batch verify (append_entries.hip): inputs + engine scratch.

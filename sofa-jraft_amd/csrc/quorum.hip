@@ -518,8 +518,11 @@ __global__ __launch_bounds__(256) void lease_check_kernel(JrqLeaseArgs a) {
 template <int P>
 __device__ __forceinline__ uint8_t readindex_verdict(uint64_t cw, uint64_t ord, uint32_t okm,
                                                      uint32_t self) {
-  const uint32_t mask = static_cast<uint32_t>(cw & 0xFFFFu) & ((1u << P) - 1u);
-  const uint32_t n = __builtin_popcount(static_cast<uint32_t>(cw & 0xFFFFu));  // peers.size()
+  // a conf naming a slot >= num_peers has a peer no response can come from: not decidable
+  // from this batch's inputs (the reference has no slots), so it is reported, not left pending
+  if ((static_cast<uint32_t>(cw & 0xFFFFu) >> P) != 0) return kRiInvalid;
+  const uint32_t mask = static_cast<uint32_t>(cw & 0xFFFFu);
+  const uint32_t n = __builtin_popcount(mask);  // peers.size()
   const uint32_t q = n ? n / 2 + 1 : 0;
   if (q <= 1) return kRiSuccess;  // the fast path answers at once
   const uint32_t need_ok = q - 1, need_fail = (n % 2 == 0) ? q - 1 : q;
@@ -587,6 +590,107 @@ __global__ __launch_bounds__(256) void readindex_quorum_kernel(JrqReadIndexArgs 
     a.result[g] = readindex_verdict<P>(a.conf[g], a.order[g], a.ok_mask[g], a.self_slot[g]);
 }
 
+// ------------------------------------------------------------- leader tick ---
+// One group's lease check (NodeImpl.handleStepDownTimeout -> checkDeadNodes, :2003-2016):
+// the conf, then the old conf when not empty; each passing check moves the lease start.
+template <int P>
+__device__ __forceinline__ void lease_one(const int64_t (&ts)[P], uint64_t cw, uint32_t self,
+                                          int64_t now, int64_t timeout, int64_t& lead,
+                                          uint8_t& ok, uint16_t& dead) {
+  int64_t start;
+  ok = 0;
+  dead = 0;
+  if (alive_quorum<P>(ts, cw & 0xFFFFu, (cw >> 32) & 0xFFu, self, now, timeout, start, dead)) {
+    lead = start;
+    ok |= 1;
+  }
+  const uint32_t omask = (cw >> 16) & 0xFFFFu;
+  if (omask != 0) {
+    if (alive_quorum<P>(ts, omask, (cw >> 40) & 0xFFu, self, now, timeout, start, dead)) {
+      lead = start;
+      ok |= 2;
+    }
+  } else {
+    ok |= 2;
+  }
+}
+
+// The leader's periodic tick over G leader groups in one launch: the lease check and, when
+// kRI, the ReadIndex heartbeat round of the same groups (readindex_verdict), which read the
+// same conf word and self slot.  Two adjacent groups per lane, as the headline epoch kernel
+// (quorum_epoch_pair_kernel): every int64 stream (P timestamp rows, conf, lease start, order)
+// is read with 16-B nt loads, 1 KiB per wave instruction, the byte / u16 fields two at a time;
+// the whole grid at once.  Round 4 ran the two as separate launches of one group per lane
+// (lease 0.68 of HBM, ReadIndex 0.32: the 21-MB ReadIndex launch was latency-bound).
+// Needs 16-B aligned ts rows (even ld) / conf / lease_start / order, 4-B ok_mask and dead,
+// 2-B self_slot / ok / ri_result (jrq_launch_tick checks; else the one-group kernels run).
+// (JRQ_TICK_SGPR_CAP, an A/B knob: the 8-waves SGPR budget of the pair kernel -- a few SGPRs
+// spill to VGPR lanes at P = 5 -- against the compiler's own ~106 SGPRs, 6 waves per SIMD)
+#ifndef JRQ_TICK_SGPR_CAP
+#define JRQ_TICK_SGPR_CAP 1
+#endif
+#if JRQ_TICK_SGPR_CAP
+#define JRQ_TICK_ATTR JRQ_SGPRS_8WAVES
+#else
+#define JRQ_TICK_ATTR
+#endif
+template <int P, bool kRI>
+__global__ __launch_bounds__(512) JRQ_TICK_ATTR void leader_tick_pair_kernel(JrqLeaseArgs a) {
+  using u64x2 = __attribute__((ext_vector_type(2))) uint64_t;
+  using i64x2 = __attribute__((ext_vector_type(2))) int64_t;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t pairs = a.G >> 1;
+  if (i < pairs) {
+    const size_t g = 2 * static_cast<size_t>(i);
+    int64_t t0[P], t1[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const i64x2 v = __builtin_nontemporal_load(
+          reinterpret_cast<const i64x2*>(a.last_rpc_ts + static_cast<size_t>(p) * a.ld + g));
+      t0[p] = v.x;
+      t1[p] = v.y;
+    }
+    const u64x2 cw = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(a.conf + g));
+    const uint32_t s2 = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(a.self_slot + g));
+    i64x2 lead = __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(a.lease_start + g));
+    u64x2 ord = {0, 0};
+    uint32_t okm2 = 0;
+    if (kRI) {
+      ord = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(a.order + g));
+      okm2 = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(a.ri_ok_mask + g));
+    }
+    int64_t l0 = lead.x, l1 = lead.y;
+    uint8_t ok0, ok1;
+    uint16_t d0, d1;
+    lease_one<P>(t0, cw.x, s2 & 0xFFu, a.now_ms, a.lease_timeout_ms, l0, ok0, d0);
+    lease_one<P>(t1, cw.y, s2 >> 8, a.now_ms, a.lease_timeout_ms, l1, ok1, d1);
+    lead.x = l0;
+    lead.y = l1;
+    *reinterpret_cast<uint16_t*>(a.ok + g) = static_cast<uint16_t>(ok0 | (ok1 << 8));
+    *reinterpret_cast<i64x2*>(a.lease_start + g) = lead;
+    if (a.dead) *reinterpret_cast<uint32_t*>(a.dead + g) = static_cast<uint32_t>(d0) | (static_cast<uint32_t>(d1) << 16);
+    if (kRI) {
+      const uint32_t r0 = readindex_verdict<P>(cw.x, ord.x, okm2 & 0xFFFFu, s2 & 0xFFu);
+      const uint32_t r1 = readindex_verdict<P>(cw.y, ord.y, okm2 >> 16, s2 >> 8);
+      *reinterpret_cast<uint16_t*>(a.ri_result + g) = static_cast<uint16_t>(r0 | (r1 << 8));
+    }
+  } else if (i == pairs && (a.G & 1u)) {  // the odd last group, one lane
+    const size_t g = a.G - 1;
+    int64_t t[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) t[p] = a.last_rpc_ts[static_cast<size_t>(p) * a.ld + g];
+    const uint64_t cw = a.conf[g];
+    int64_t l = a.lease_start[g];
+    uint8_t ok;
+    uint16_t d;
+    lease_one<P>(t, cw, a.self_slot[g], a.now_ms, a.lease_timeout_ms, l, ok, d);
+    a.ok[g] = ok;
+    a.lease_start[g] = l;
+    if (a.dead) a.dead[g] = d;
+    if (kRI) a.ri_result[g] = readindex_verdict<P>(cw, a.order[g], a.ri_ok_mask[g], a.self_slot[g]);
+  }
+}
+
 }  // namespace jrq
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_readindex(
@@ -616,8 +720,48 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_readindex
   return hipGetLastError();
 }
 
+// The lease check, with the ReadIndex round fused when args->order is set (the leader tick):
+// the pair kernel when the arrays allow its wide accesses, else the one-group kernels.
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_lease(
     const JrqLeaseArgs* args, int num_cus, hipStream_t stream) {
+  auto al = [](const void* p, uintptr_t n) { return (reinterpret_cast<uintptr_t>(p) & (n - 1)) == 0; };
+  const JrqLeaseArgs& a = *args;
+  const bool ri = a.order != nullptr;
+  const bool pair = a.G >= 2 && (a.ld & 1u) == 0 && al(a.last_rpc_ts, 16) && al(a.conf, 16) &&
+                    al(a.lease_start, 16) && al(a.self_slot, 2) && al(a.ok, 2) && al(a.dead, 4) &&
+                    (!ri || (al(a.order, 16) && al(a.ri_ok_mask, 4) && al(a.ri_result, 2)));
+  if (pair) {
+    const uint64_t lanes = static_cast<uint64_t>(a.G) / 2 + 1;  // + the odd tail's lane
+    const dim3 grid(static_cast<unsigned>((lanes + 511) / 512)), blk(512);
+    switch (a.num_peers) {
+#define JRQ_CASE(P)                                                                             \
+  case P:                                                                                       \
+    if (ri)                                                                                     \
+      hipLaunchKernelGGL((jrq::leader_tick_pair_kernel<P, true>), grid, blk, 0, stream, a);   \
+    else                                                                                        \
+      hipLaunchKernelGGL((jrq::leader_tick_pair_kernel<P, false>), grid, blk, 0, stream, a);  \
+    break;
+      JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
+      JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
+      JRQ_CASE(15) JRQ_CASE(16)
+#undef JRQ_CASE
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if (ri) {  // unaligned leader tick: the ReadIndex kernel after the lease kernel below
+    JrqReadIndexArgs r{};
+    r.conf = a.conf;
+    r.self_slot = a.self_slot;
+    r.order = a.order;
+    r.ok_mask = a.ri_ok_mask;
+    r.num_peers = a.num_peers;
+    r.G = a.G;
+    r.result = a.ri_result;
+    const hipError_t s = jrq_launch_readindex(&r, num_cus, stream);
+    if (s != hipSuccess) return s;
+  }
   const uint64_t need = (static_cast<uint64_t>(args->G) + 255) / 256;
   const uint64_t cap = static_cast<uint64_t>(num_cus) * 8;
   const dim3 grid(static_cast<unsigned>(need < cap ? (need ? need : 1) : cap)), blk(256);

@@ -55,6 +55,17 @@ __device__ __forceinline__ void tst1o(int64_t* base, uint32_t off, int64_t v) {
 #ifndef JRQ_TABLE_NT_STORES
 #define JRQ_TABLE_NT_STORES 1
 #endif
+#ifndef JRQ_TABLE_AB_NODECIDE
+#define JRQ_TABLE_AB_NODECIDE 0
+#endif
+#ifndef JRQ_TABLE_AB_NOLIST
+#define JRQ_TABLE_AB_NOLIST 0
+#endif
+// (timing only: 1 = no lastCommitted stores; 2 = lastCommitted stored to a separate row -- the
+// first cold xstart row, which a table without conf runs never reads)
+#ifndef JRQ_TABLE_AB_LC
+#define JRQ_TABLE_AB_LC 0
+#endif
 template <class T>
 __device__ __forceinline__ void st_tab(T v, T* p) {
 #if JRQ_TABLE_NT_STORES
@@ -191,10 +202,15 @@ __global__ __launch_bounds__(kTableEpochBlock, P <= 5 ? 4 : 2) JRQ_SGPRS_8WAVES 
         for (int p = 0; p < P; ++p) hs[3 + p] = m[p];
       }
       const int64_t pi = prk == kPiFollowsLc ? lck + 1 : prk;
+#if JRQ_TABLE_AB_NODECIDE  // diagnosis only (tools/ab_build.sh): loads and stores, no decision
+      uint8_t s = static_cast<uint8_t>(cwk & 1u) | static_cast<uint8_t>(m[P - 1] & 2);
+      const uint32_t r = static_cast<uint32_t>(lak - pi + 1);
+#else
       RelGroup<P> rg;
       rel_map<P>(pi, lak, m, rg);
       uint8_t s;
       const uint32_t r = rel_cand<P>(cwk, rg, s);
+#endif
       s = pi == 0 ? kStNotLeader : s;
       x[k] = in && !f[k] && !rel_domain(pi, lak);
       o[k] = pi - 1 + static_cast<int64_t>(r);
@@ -214,20 +230,29 @@ __global__ __launch_bounds__(kTableEpochBlock, P <= 5 ? 4 : 2) JRQ_SGPRS_8WAVES 
     const uint32_t g = gA + 128u * h;
     const bool ca = c[2 * h], cb = c[2 * h + 1];
     const uint32_t go = (2u * lane + 128u * h) * 8u;  // groups g, g + 1 in the wave's tile
+#if JRQ_TABLE_AB_LC == 2
+    int64_t* const lcb = t.xstart + static_cast<size_t>(__builtin_amdgcn_readfirstlane(wid)) * 256;
+#else
+    int64_t* const lcb = tile + (P + 2) * 256;
+#endif
+#if JRQ_TABLE_AB_LC != 1
     if (ca && cb) {
       i64x2 v;
       v.x = o[2 * h];
       v.y = o[2 * h + 1];
-      tst2o(tile + (P + 2) * 256, go, v);
+      tst2o(lcb, go, v);
     } else {
-      if (ca) tst1o(tile + (P + 2) * 256, go, o[2 * h]);
-      if (cb) tst1o(tile + (P + 2) * 256, go + 8u, o[2 * h + 1]);
+      if (ca) tst1o(lcb, go, o[2 * h]);
+      if (cb) tst1o(lcb, go + 8u, o[2 * h + 1]);
     }
+#endif
     if (ca && wpi[2 * h]) tst1o(tile + P * 256, go, kPiFollowsLc);
     if (cb && wpi[2 * h + 1]) tst1o(tile + P * 256, go + 8u, kPiFollowsLc);
     const uint64_t ba = __ballot(ca), bb = __ballot(cb);
+#if !JRQ_TABLE_AB_NOLIST  // (diagnosis knob: no list entries)
     if (ca) slice[cnt + __popcll(ba & below)] = (static_cast<uint64_t>(d[2 * h]) << 32) | g;
     if (cb) slice[cnt + __popcll(ba) + __popcll(bb & below)] = (static_cast<uint64_t>(d[2 * h + 1]) << 32) | (g + 1);
+#endif
     cnt += __popcll(ba) + __popcll(bb);
     if (t.status && live[h]) {  // a flagged (or 64-bit) group's status is written by its own pass
       const uint32_t s2 = (st4 >> (16 * h)) & 0xFFFFu;

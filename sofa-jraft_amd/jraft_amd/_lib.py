@@ -58,7 +58,7 @@ PI_FOLLOWS_LC = -(1 << 63)             # JRQ_PI_FOLLOWS_LC
 REC_LAST_APPENDED = 16                 # JRQ_REC_LAST_APPENDED
 TABLE_SLICE = 256                      # JRQ_TABLE_SLICE
 STATE_RESET_MATCH = 1                  # JRQ_STATE_RESET_MATCH
-READINDEX_PENDING, READINDEX_SUCCESS, READINDEX_FAILURE = 0, 1, 2  # JRQ_READINDEX_*
+READINDEX_PENDING, READINDEX_SUCCESS, READINDEX_FAILURE, READINDEX_INVALID = 0, 1, 2, 3  # JRQ_READINDEX_*
 # jrq_debug_option (test / A-B hooks)
 DBG_CRC_SEG_BYTES, DBG_CRC_REGS, DBG_CRC_PRIO, DBG_CRC_SEG_MAP, DBG_UPLOAD_PAGEABLE = 1, 2, 3, 4, 5
 
@@ -133,6 +133,10 @@ SIGNATURES = [
      [_V, _V, C.c_uint64, C.c_uint32, _V, _V, C.c_uint32, C.c_int64, C.c_int64, _V, _V, _V]),
     ("jrq_readindex_quorum_dev", C.c_int, [_V, _V, _V, _V, _V, C.c_uint32, C.c_uint32, _V]),
     ("jrq_readindex_quorum", C.c_int, [_V, _V, _V, _V, _V, C.c_uint32, C.c_uint32, _V]),
+    ("jrq_leader_tick_dev", C.c_int,
+     [_V, _V, C.c_uint64, C.c_uint32, _V, _V, C.c_uint32, C.c_int64, C.c_int64, _V, _V, _V, _V, _V, _V]),
+    ("jrq_leader_tick", C.c_int,
+     [_V, _V, C.c_uint64, C.c_uint32, _V, _V, C.c_uint32, C.c_int64, C.c_int64, _V, _V, _V, _V, _V, _V]),
     ("jrq_commit_fanout_dev", C.c_int, [_V, C.c_uint32] + [_V] * 9),
     ("jrq_commit_fanout", C.c_int, [_V, C.c_uint32] + [_V] * 9),
     ("jrq_v2_decode_verify_dev", C.c_int, [_V, _V, _V, C.c_uint32] + [_V] * 11),

@@ -313,6 +313,59 @@ class Engine:
                                           lease_timeout_ms, _dev_ptr(ok_out),
                                           _dev_ptr(lease_start_inout), _dev_ptr(dead_out)), self._h)
 
+    # ------------------------------------------------------ leader tick --
+    def leader_tick(self, last_rpc_ts, conf, self_slot, now_ms, lease_timeout_ms, lease_start,
+                    order=None, ok_mask=None):
+        """Host variant of jrq_leader_tick: the lease check and (with order / ok_mask) the
+        ReadIndex round of the same groups in one launch.  Returns (ok, lease_start, dead,
+        ri_result or None)."""
+        ts = _c(last_rpc_ts, np.int64)
+        P, G = ts.shape
+        conf = _c(conf, np.uint64)
+        self_slot = _c(self_slot, np.uint8)
+        lead = np.array(lease_start, dtype=np.int64, copy=True)
+        ok = np.zeros(G, np.uint8)
+        dead = np.zeros(G, np.uint16)
+        order = _c(order, np.uint64)
+        ok_mask = _c(ok_mask, np.uint16)
+        res = np.zeros(G, np.uint8) if order is not None else None
+        check(self._L.jrq_leader_tick(self._h, _np_ptr(ts), G, P, _np_ptr(conf), _np_ptr(self_slot),
+                                      G, now_ms, lease_timeout_ms, _np_ptr(ok), _np_ptr(lead),
+                                      _np_ptr(dead), _np_ptr(order), _np_ptr(ok_mask),
+                                      _np_ptr(res)), self._h)
+        return ok, lead, dead, res
+
+    def leader_tick_dev(self, last_rpc_ts, conf, self_slot, now_ms, lease_timeout_ms, ok_out,
+                        lease_start_inout, dead_out=None, order=None, ok_mask=None,
+                        ri_result_out=None):
+        P = last_rpc_ts.shape[0]
+        G = conf.shape[0]
+        check(self._L.jrq_leader_tick_dev(self._h, _dev_ptr(last_rpc_ts), last_rpc_ts.stride(0), P,
+                                          _dev_ptr(conf), _dev_ptr(self_slot), G, now_ms,
+                                          lease_timeout_ms, _dev_ptr(ok_out),
+                                          _dev_ptr(lease_start_inout), _dev_ptr(dead_out),
+                                          _dev_ptr(order), _dev_ptr(ok_mask),
+                                          _dev_ptr(ri_result_out)), self._h)
+
+    def leader_tick_launcher(self, last_rpc_ts, conf, self_slot, now_ms, lease_timeout_ms, ok_out,
+                             lease_start_inout, dead_out, order, ok_mask, ri_result_out):
+        """The same call with its arguments resolved once (a host keeping its buffers): the
+        returned function launches one tick (the bench's step loop)."""
+        L, h = self._L, self._h
+        P = last_rpc_ts.shape[0]
+        G = conf.shape[0]
+        args = (h, _dev_ptr(last_rpc_ts), last_rpc_ts.stride(0), P, _dev_ptr(conf),
+                _dev_ptr(self_slot), G, now_ms, lease_timeout_ms, _dev_ptr(ok_out),
+                _dev_ptr(lease_start_inout), _dev_ptr(dead_out), _dev_ptr(order),
+                _dev_ptr(ok_mask), _dev_ptr(ri_result_out))
+        fn = L.jrq_leader_tick_dev
+
+        def launch():
+            rc = fn(*args)
+            if rc:
+                check(rc, h)
+        return launch
+
     # -------------------------------------------------------- ReadIndex --
     def readindex_quorum(self, conf, self_slot, order, ok_mask, num_peers):
         """Host variant: the ReadIndex heartbeat round's verdict per group (uint8[G],
@@ -327,6 +380,18 @@ class Engine:
                                            _np_ptr(order), _np_ptr(ok_mask), num_peers, G,
                                            _np_ptr(res)), self._h)
         return res
+
+    def readindex_launcher(self, conf, self_slot, order, ok_mask, num_peers, result_out):
+        """readindex_quorum_dev with its arguments resolved once (the bench's step loop)."""
+        h, fn = self._h, self._L.jrq_readindex_quorum_dev
+        args = (h, _dev_ptr(conf), _dev_ptr(self_slot), _dev_ptr(order), _dev_ptr(ok_mask),
+                num_peers, conf.shape[0], _dev_ptr(result_out))
+
+        def launch():
+            rc = fn(*args)
+            if rc:
+                check(rc, h)
+        return launch
 
     def readindex_quorum_dev(self, conf, self_slot, order, ok_mask, num_peers, result_out):
         G = conf.shape[0]

@@ -181,3 +181,32 @@ def test_gpu_dev_entry_point_and_rounds_in_steps(engine, oracle):
     np.testing.assert_array_equal(r2, oracle.readindex_quorum(conf, self_slot, order, okm, P))
     decided = r1 != PENDING
     np.testing.assert_array_equal(r2[decided], r1[decided])
+
+
+def _with_stray_slots(P, G, seed):
+    """random_rounds plus, for a third of the groups, conf bits at slots >= P (outside the
+    batch: ADVICE r04 -- no response can come from them)."""
+    conf, self_slot, order, okm, _ = random_rounds(seed, G, P)
+    rng = np.random.default_rng(seed + 1)
+    stray = rng.random(G) < 1 / 3
+    extra = rng.integers(P, 16, G) if P < 16 else np.zeros(G, np.int64)
+    conf = np.where(stray, conf | (np.uint64(1) << extra.astype(np.uint64)), conf).astype(np.uint64)
+    return conf, self_slot, order, okm, stray
+
+
+@pytest.mark.parametrize("P", [1, 3, 5, 15])
+def test_oracle_conf_beyond_num_peers_is_invalid(oracle, P):
+    conf, self_slot, order, okm, stray = _with_stray_slots(P, 2000, 50 + P)
+    got = oracle.readindex_quorum(conf, self_slot, order, okm, P)
+    assert (got[stray] == 3).all()
+    assert (got[~stray] != 3).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,G", [(3, 20001), (5, 20000), (15, 4099)])
+def test_gpu_conf_beyond_num_peers_is_invalid(engine, oracle, P, G):
+    conf, self_slot, order, okm, stray = _with_stray_slots(P, G, 60 + P)
+    e = oracle.readindex_quorum(conf, self_slot, order, okm, P)
+    g = engine.readindex_quorum(conf, self_slot, order, okm, P)
+    np.testing.assert_array_equal(g, e)
+    assert (g[stray] == 3).all()

@@ -144,6 +144,37 @@ def main():
                                    device=dev) for k, t in Engine.V2_FIELDS}
         legs["v2"] = (mk_v2, new_v2)
 
+    if "tick" in legs_env or "lease" in legs_env:  # leader tick over 1M groups x 5 peers
+        Gt, Pt = 1 << 20, 5
+        rng = np.random.default_rng(5)
+        conf_t = dev_t(W.quorum_batch("C3", groups=Gt)["conf"])
+        self_t = torch.zeros(Gt, dtype=torch.uint8, device=dev)
+        tb = []
+        for k in range(6):
+            ts = (1 << 40) - rng.integers(0, 1800, (Pt, Gt)).astype(np.int64)
+            order = rng.integers(0, 1 << 20, Gt).astype(np.int64)
+            okm = rng.integers(0, 1 << 5, Gt).astype(np.int16)
+            tb.append((dev_t(ts), dev_t(order), dev_t(okm)))
+
+        def mk_tick(ri):
+            def mk(e, o):
+                cnt = [0]
+                lead = torch.zeros(Gt, dtype=torch.int64, device=dev)
+                dead = torch.empty(Gt, dtype=torch.int16, device=dev)
+                res = torch.empty(Gt, dtype=torch.uint8, device=dev)
+
+                def f():
+                    ts, order, okm = tb[cnt[0] % 6]
+                    cnt[0] += 1
+                    e.leader_tick_dev(ts, conf_t, self_t, 1 << 40, 900, o, lead, dead,
+                                      order if ri else None, okm if ri else None,
+                                      res if ri else None)
+                return f
+            return mk
+        if "tick" in legs_env:
+            legs["tick"] = (mk_tick(True), lambda: torch.empty(Gt, dtype=torch.uint8, device=dev))
+        if "lease" in legs_env:
+            legs["lease"] = (mk_tick(False), lambda: torch.empty(Gt, dtype=torch.uint8, device=dev))
     pay64 = d5["payload"].view(torch.int64)
     acc = torch.empty((), dtype=torch.int64, device=dev)
     fns = {}

@@ -27,13 +27,13 @@ for s in $STEPS; do
     profd) run prof_drive 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/profd -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs table,drive ;;
     tbl)   run table_tests 600 python -m pytest tests/test_gpu_table.py -q -x -p no:cacheprovider --timeout 300 ;;
     pmc)   # one rocprofv3 --pmc pass per (leg, counter): every kernel name then carries one workload
-           for leg in ${PMC_LEGS:-quorum C2 C2L C3K C5 C1 table v2 snapshot lease readindex fanout ae}; do
+           for leg in ${PMC_LEGS:-quorum C2 C2L C3K C5 C1 table v2 snapshot lease readindex tick fanout ae}; do
              for c in FETCH_SIZE WRITE_SIZE; do
                run pmc_${leg}_$c 180 rocprofv3 --kernel-trace --pmc $c -d gpurun_out/pmc_${leg}_$c -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs $leg
              done
            done ;;
     rdreq) # read-request sizes (exact read bytes = 32 n32 + 64 n64 + 128 n128), one pass per leg
-           for leg in ${PMC_LEGS:-quorum C2 C2L C3K C5 C1 table v2 snapshot lease readindex fanout ae}; do
+           for leg in ${PMC_LEGS:-quorum C2 C2L C3K C5 C1 table v2 snapshot lease readindex tick fanout ae}; do
              run pmc_${leg}_RDREQ 180 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum -d gpurun_out/pmc_${leg}_RDREQ -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs $leg
            done ;;
     host)  run host_test 300 ./tests/_build/host_test gpu ;;
@@ -42,6 +42,10 @@ for s in $STEPS; do
              run bench_${TAG:-sel}_$v 600 env JRAFT_AMD_AB_LIB=ab/$v/libjrq.so python bench.py --steps 20 --warmup 5 --no-cpu --legs ${BENCH_LEGS:-table} --detail gpurun_out/bench_${TAG:-sel}_${v}_detail.json
            done ;;
     ab)    run ab_${TAG:-sel} 600 env AB_LEGS=${AB_LEGS:-C3,C5f,C1f,archive} python tools/ab_inproc.py ${AB_VARIANTS:-base=ab/base/libjrq.so} ;;
+    tpab)  # the resident table epoch, every group committing, libjrq variants side by side
+           for P in ${TP_PEERS:-5}; do
+             run tpab_${TAG:-sel}_P$P 300 env P=$P python tools/table_peers_ab.py ${TP_VARIANTS:-base=ab/base/libjrq.so}
+           done ;;
     fulltrace) # the default bench run under the tracer: the printed line, the full result and one
            # kernel trace of the same launches (tools/leg_traces.py --trace -> <tag>_leg_kernels.json)
            run fulltrace 900 rocprofv3 --kernel-trace --stats -d gpurun_out/full -o run --output-format csv -- python bench.py --detail gpurun_out/full_detail.json

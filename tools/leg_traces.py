@@ -52,7 +52,8 @@ LEG_KERNELS = {
             "v2_finish"]),
     "snapshot": (("next_rows", "snapshot_stream_crc64", "roofline"),
                  ["crc64_rounds_kernel<512u, false>", "crc64_finish_kernel<false>"]),
-    "lease": (("next_rows", "lease_check", "roofline"), ["lease_check_kernel<5>"]),
+    "lease": (("next_rows", "lease_check", "roofline"), ["leader_tick_pair_kernel<5, false>"]),
+    "tick": (("next_rows", "leader_tick", "roofline"), ["leader_tick_pair_kernel<5, true>"]),
     "readindex": (("next_rows", "readindex_quorum", "roofline"), ["readindex_quorum_kernel<5, true>"]),
     "fanout": (("next_rows", "commit_fanout", "roofline"), ["fanout_eval"]),
 }
