@@ -682,7 +682,10 @@ def leg_table(ctx, args, G, pair_ms):
                                          s["conf"][sub], np.concatenate([[0], np.cumsum(cnt)]),
                                          s["run_start"][idx], s["run_conf"][idx], chunk=1024)
         ok = ok and bool(np.array_equal(got[sub], ce))
-    alg = G * (8 * P + 32) + n_changed * 16
+    # per group: u32 match words 4P + pendingIndex, lastAppended, lastCommitted, conf 32 read;
+    # per committing group lastCommitted 8 + list delta 4 written; per 256-group slice its
+    # 32-B map and 4-B count (the flagged groups' run words, ~1 %, not counted)
+    alg = G * (4 * P + 32) + n_changed * 12 + ((G + 255) // 256) * 36
     for t in pristine + plain + work:
         t.close()
     return {"workload": f"C3 resident table: {G} groups x {P} peers, joint, 1% with a conf "
@@ -700,8 +703,9 @@ def leg_table(ctx, args, G, pair_ms):
                       f"pair; the pair kernel timed the same way on the same inputs",
             "bit_exact_vs_stateless_kernel_and_oracle": ok,
             "roofline": roofline(alg, t_ms, kernel="table_epoch_kernel<5>",
-                                 bytes_note="reads 8P+32 B per group, writes lastCommitted + list "
-                                            "entry 16 B per committing group",
+                                 bytes_note="reads 4P+32 B per group (u32 match words), writes "
+                                            "lastCommitted + list delta 12 B per committing group "
+                                            "+ 36 B per 256-group slice",
                                  **pmc_traffic("table", "table_epoch_kernel<5>"))}
 
 

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define JRQ_ABI_VERSION 2
+#define JRQ_ABI_VERSION 3
 #define JRQ_MAX_PEERS 16 /* peer slots per group (16-bit masks) */
 
 typedef struct jrq_engine jrq_engine;
@@ -180,8 +180,8 @@ int jrq_quorum_epoch_dev(jrq_engine *e, const jrq_group_batch *in_dev, int64_t *
 int jrq_quorum_epoch(jrq_engine *e, const jrq_group_batch *in_host, int64_t *committed_out,
                      uint8_t *status_out, uint32_t G);
 
-/* The same epoch with the per-group inputs in tiles of 256 groups -- the resident table's
- * layout (jrq_table_view): tile i holds match[0..num_peers-1], pending_index, last_appended,
+/* The same epoch with the per-group inputs in tiles of 256 groups (the resident table's tiling
+ * with int64 match words): tile i holds match[0..num_peers-1], pending_index, last_appended,
  * last_committed, conf of groups [256 i, 256 i + 256), each field as 256 consecutive int64
  * words, so a tile is 256 (num_peers + 4) words and the tiles sit back to back from `tiles`
  * (G rounded up to whole tiles).  A wave then reads one contiguous block instead of num_peers
@@ -223,11 +223,18 @@ int jrq_quorum_epochs_dev(jrq_engine *e, const jrq_group_batch *in_dev, uint32_t
  * instead of per entry, :197-215), and, per peer slot, the highest index the peer has
  * acknowledged through commitAt (Replicator acks are contiguous, Replicator.java:1387-1401).
  *
- * Device layout (SoA, 8-byte words, rows of ld >= G): match[P][ld], pending_index, last_appended,
- * last_committed, conf (run 0 + JRQ_CONF_RUNS), and JRQ_TABLE_MAX_RUNS - 1 inline extra runs
- * (run_start, run_conf) read only by flagged groups.  After its first commit a group's
+ * Device layout: tiles of 256 groups (jrq_table_view) holding match[P] as u32 words relative to
+ * the group's match base (below), pending_index, last_appended, last_committed, conf (run 0 +
+ * JRQ_CONF_RUNS) as int64 words, and JRQ_TABLE_MAX_RUNS - 1 inline extra runs (run_start,
+ * run_conf) in rows read only by flagged groups.  After its first commit a group's
  * pending_index word holds JRQ_PI_FOLLOWS_LC (pendingIndex = lastCommittedIndex + 1,
- * BallotBox.java:131-132), so a commit writes one word of state. */
+ * BallotBox.java:131-132), so a commit writes one word of state.
+ * Match base: pendingIndex - 1 rounded down to a multiple of 2^JRQ_TABLE_MATCH_PAGE (0 when not
+ * the leader); a slot's word is its match minus the base, 0 for a match below the base (it
+ * grants no pending entry either way).  Headers with a negative pendingIndex, one >= 2^62, or a
+ * pending queue longer than 2^31 - 1 entries (a Java ArrayList's bound) are refused as invalid,
+ * as are lastAppended records with v > 2^31 - 1. */
+#define JRQ_TABLE_MATCH_PAGE 30
 #define JRQ_TABLE_MAX_RUNS 4            /* conf runs per pending window (NodeImpl has <= 2) */
 #define JRQ_TABLE_MAX_GROUPS (1u << 27) /* groups per table (27-bit group ids in records) */
 #define JRQ_PI_FOLLOWS_LC INT64_MIN
@@ -306,9 +313,10 @@ int jrq_table_stage_apply(jrq_table *t);
  * Host variant: changed_out[0 .. *n_changed) (capacity G); synchronises and copies back only
  * the listed entries.
  * _dev: the list comes in jrq_table_slices(t) fixed slices, one per JRQ_TABLE_SLICE groups
- * (no reservation, no atomics: each slice is written by the one wave that decides its groups):
- * slice s lists n_changed_dev[s] of the groups [256 s, 256 s + 256) at changed_out_dev + 256 s
- * (capacity JRQ_TABLE_SLICE * jrq_table_slices(t) words). */
+ * (no reservation, no atomics: each slice is written by the one wave that decides its groups),
+ * slice s at changed_out_dev + 256 s (capacity JRQ_TABLE_SLICE * jrq_table_slices(t) words):
+ * words 0-3 a 256-bit map (bit i: group 256 s + i advanced), then from byte 32 the listed
+ * groups' (commit - pi + 1) as uint32, in group order; n_changed_dev[s] = the map's popcount. */
 int jrq_table_epoch_dev(jrq_table *t, uint64_t *changed_out_dev, uint32_t *n_changed_dev,
                         uint8_t *status_out_dev);
 int jrq_table_epoch(jrq_table *t, uint64_t *changed_out, uint32_t *n_changed,
@@ -329,11 +337,13 @@ int jrq_table_check(jrq_table *t);
 int jrq_table_copy(jrq_table *dst, const jrq_table *src);
 
 /* Device views of the table.  The per-group fields live in tiles of tile_groups (256) groups:
- * element g of a field is field[(g / tile_groups) * tile_stride + g % tile_groups] (each tile
- * holds every field of its groups in one contiguous block: an epoch wave reads one block);
- * match[p] starts at match + p * tile_groups. */
+ * element g of an int64 field is field[(g / tile_groups) * tile_stride + g % tile_groups] (each
+ * tile holds every field of its groups in one contiguous block: an epoch wave reads one block).
+ * The u32 match words of tile i start at match + 2 i tile_stride, slot p's 256 words at
+ * + 256 p, group k of the tile at position (k % 128) / 2 * 4 + (k / 128) * 2 + k % 2 (the
+ * epoch's lane order); match = match base + word (JRQ_TABLE_MATCH_PAGE). */
 typedef struct {
-    int64_t *match;          /* match[p] row of tile 0 at match + p * tile_groups */
+    uint32_t *match;         /* u32 words of tile 0 */
     int64_t *pending_index;  /* JRQ_PI_FOLLOWS_LC after a commit */
     int64_t *last_appended;
     int64_t *last_committed;
@@ -341,7 +351,7 @@ typedef struct {
     uint64_t ld;             /* row stride of the table's cold (per-run) fields */
     uint32_t G, num_peers;
     uint32_t tile_groups;    /* 256 (JRQ_TABLE_SLICE) */
-    uint64_t tile_stride;    /* words from a tile to the next: 256 (num_peers + 4) */
+    uint64_t tile_stride;    /* int64 words from a tile to the next: 128 num_peers + 1024 */
 } jrq_table_view;
 int jrq_table_view_get(jrq_table *t, jrq_table_view *view_out);
 

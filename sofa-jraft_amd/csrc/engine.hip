@@ -1585,15 +1585,15 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   auto* t = new jrq_table();
   t->e = e;
   const uint64_t ld = (static_cast<uint64_t>(G) + 63) & ~63ull;  // pairs + 512-B rows
-  // the state jrq_table_copy copies: the hot tiles (256 groups each: match[P], pi, la, lc, conf
-  // as 256-word rows, JrqTableArgs), the cold rows xstart[3], xconf[3], the flagged-entry slots
+  // the state jrq_table_copy copies: the hot tiles (256 groups each: match[P] as 256-u32 rows,
+  // pi, la, lc, conf as 256-word rows, JrqTableArgs), the cold rows xstart[3], xconf[3], the flagged-entry slots
   // flag_ent[waves][256][8] + flag_wcnt[waves] (u32); then the control word `invalid`
   // (one 256-group range per epoch wave, rounded up to whole workgroups: every wave of the
   // grid reads its slots)
   const uint64_t ranges = (G + jrq::kTableSlice - 1) / jrq::kTableSlice;
   const uint64_t waves = (ranges + jrq::kTableBlockWaves - 1) / jrq::kTableBlockWaves * jrq::kTableBlockWaves;
   const uint64_t flag_words = waves * jrq::kFlagSlots * 8 + (waves + 1) / 2;
-  const uint64_t ts = static_cast<uint64_t>(P + 4) * jrq::kTableSlice;  // words per tile
+  const uint64_t ts = static_cast<uint64_t>(P) * (jrq::kTableSlice / 2) + 4 * jrq::kTableSlice;  // words per tile
   const uint64_t words = waves * ts + ld * 2 * (jrq::kTableMaxRuns - 1) + flag_words;
   const size_t bytes = words * 8 + 64;
   t->slices = (G + JRQ_TABLE_SLICE - 1) / JRQ_TABLE_SLICE;
@@ -1607,8 +1607,8 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   }
   int64_t* w = static_cast<int64_t*>(t->mem);
   JrqTableArgs& a = t->a;
-  a.match = w;
-  a.pi = w + jrq::kTableSlice * P;
+  a.match = reinterpret_cast<uint32_t*>(w);
+  a.pi = w + (jrq::kTableSlice / 2) * P;
   a.la = a.pi + jrq::kTableSlice;
   a.lc = a.la + jrq::kTableSlice;
   a.conf = reinterpret_cast<uint64_t*>(a.lc + jrq::kTableSlice);
@@ -1815,16 +1815,30 @@ int jrq_table_read(jrq_table* t, int64_t* pending_index, int64_t* last_appended,
                          hipMemcpyDeviceToHost, e->stream);
     return r;
   };
+  std::vector<int64_t> pw(G);
   JRQ_HIP(e, field(lc.data(), t->a.lc));
-  if (pending_index) JRQ_HIP(e, field(pending_index, t->a.pi));
+  JRQ_HIP(e, field(pw.data(), t->a.pi));
   if (last_appended) JRQ_HIP(e, field(last_appended, t->a.la));
-  if (match)
-    for (uint32_t p = 0; p < t->a.P; ++p)
-      JRQ_HIP(e, field(match + p * G, t->a.match + p * jrq::kTableSlice));
+  // the u32 match words: every tile's P rows (P KiB at the tile's start) in one 2-D copy
+  const size_t tiles = (G + jrq::kTableSlice - 1) / jrq::kTableSlice;
+  std::vector<uint32_t> mw;
+  if (match) {
+    mw.resize(tiles * t->a.P * jrq::kTableSlice);
+    const size_t rb = static_cast<size_t>(t->a.P) * jrq::kTableSlice * 4;
+    JRQ_HIP(e, hipMemcpy2DAsync(mw.data(), rb, t->a.match, t->a.ts * 8, rb, tiles, hipMemcpyDeviceToHost,
+                                e->stream));
+  }
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
-  if (pending_index)
-    for (size_t g = 0; g < G; ++g)
-      if (pending_index[g] == JRQ_PI_FOLLOWS_LC) pending_index[g] = lc[g] + 1;
+  for (size_t g = 0; g < G; ++g)
+    if (pw[g] == JRQ_PI_FOLLOWS_LC) pw[g] = lc[g] + 1;
+  if (match)  // absolute: the group's match base + its word (mslot: the epoch's lane order)
+    for (size_t g = 0; g < G; ++g) {
+      const int64_t b = jrq::mbase(pw[g]);
+      const uint32_t* row = mw.data() + (g / jrq::kTableSlice) * t->a.P * jrq::kTableSlice;
+      for (uint32_t p = 0; p < t->a.P; ++p)
+        match[p * G + g] = b + static_cast<int64_t>(row[p * jrq::kTableSlice + jrq::mslot(g % jrq::kTableSlice)]);
+    }
+  if (pending_index) std::memcpy(pending_index, pw.data(), G * 8);
   if (last_committed) std::memcpy(last_committed, lc.data(), G * 8);
   return JRQ_OK;
 }

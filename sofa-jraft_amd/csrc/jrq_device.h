@@ -278,17 +278,21 @@ constexpr uint32_t kFlagSlots = 256;               // flagged-entry slots per 25
 }  // namespace jrq
 // The hot fields live in tiles of kTableSlice (256) groups, one tile per epoch wave: tile i
 // holds match[0..P-1], pendingIndex, lastAppended, lastCommitted, conf of groups [256 i,
-// 256 i + 256), each field as 256 consecutive words, so a wave's whole input is one contiguous
-// (8P + 32) * 256-B block (field-major rows over all groups ran 20 % slower:
-// tools/probes/streams_probe.hip).  The pointers below are the fields' rows in tile 0; element
-// g of a field is row[(g >> 8) * ts + (g & 255)] (tf()).
+// 256 i + 256), so a wave's whole input is one contiguous (4P + 32) * 256-B block (DESIGN.md
+// §4.9; field-major rows over all groups ran 20 % slower: tools/probes/streams_probe.hip).
+// pendingIndex, lastAppended, lastCommitted and conf are 256 consecutive int64 words each;
+// element g of such a field is row[(g >> 8) * ts + (g & 255)] (tf()).  The match of a slot is
+// a u32 relative to the group's match base (mbase(pendingIndex): pendingIndex - 1 rounded down
+// to a multiple of 2^30, fixed for a billion entries), saturated at 0 below it -- a match below
+// the pending window grants nothing whatever its value -- so a slot costs 4 B instead of 8
+// (r05); the 256 u32 of a slot's row sit in the epoch's lane order (mslot()).
 struct JrqTableArgs {
-  int64_t* match;        // tile row of match[0]; match[p] at match + 256 p
+  uint32_t* match;       // match[0] row of tile 0 (u32); match[p] at match + 256 p, tile stride 2 ts
   int64_t* pi;           // pendingIndex, or kPiFollowsLc
   int64_t* la;
   int64_t* lc;
   uint64_t* conf;        // run 0 conf word | JRQ_CONF_RUNS
-  uint64_t ts;           // words per tile: 256 (P + 4)
+  uint64_t ts;           // int64 words per tile: 128 P + 1024
   int64_t* xstart;       // [jrq::kTableMaxRuns - 1][ld] extra run starts (INT64_MAX = unused)
   uint64_t* xconf;       // [kTableMaxRuns - 1][ld]
   uint64_t ld;           // row stride of xstart / xconf (cold fields: group-major rows)
@@ -303,10 +307,29 @@ struct JrqTableArgs {
   uint32_t* flag_wcnt;   // [waves] how many
 };
 
-// Element g of a tiled hot field (its row in tile 0: t.pi, t.lc, t.match + 256 p, ...).
+// Element g of a tiled int64 field (its row in tile 0: t.pi, t.la, t.lc, t.conf).
 template <class T>
 __host__ __device__ __forceinline__ T& tf(T* row, const JrqTableArgs& t, uint32_t g) {
   return row[static_cast<size_t>(g >> 8) * t.ts + (g & 255u)];
+}
+
+namespace jrq {
+constexpr int kMatchPageBits = 30;  // match base granularity (JRQ_TABLE_MATCH_PAGE)
+// The match base of a group whose (resolved) pendingIndex is pi; 0 when not the leader.
+__host__ __device__ __forceinline__ int64_t mbase(int64_t pi) {
+  return pi > 0 ? ((pi - 1) & ~((int64_t{1} << kMatchPageBits) - 1)) : 0;
+}
+// Position of group k (0..255) of a tile in its u32 match rows: the epoch's lane l decides
+// groups {2l, 2l + 1} (pair A) and {128 + 2l, 129 + 2l} (pair B), and reads their four u32 of a
+// row as one 16-B load at byte 16 l.
+__host__ __device__ __forceinline__ uint32_t mslot(uint32_t k) {
+  return ((k & 127u) >> 1) * 4u + ((k >> 7) << 1) + (k & 1u);
+}
+}  // namespace jrq
+
+// The u32 match word of slot p of group g.
+__host__ __device__ __forceinline__ uint32_t& tm(const JrqTableArgs& t, uint32_t p, uint32_t g) {
+  return t.match[static_cast<size_t>(g >> 8) * (2 * t.ts) + p * 256u + jrq::mslot(g & 255u)];
 }
 
 // One group header as the ABI carries it (include/jrq.h jrq_group_state).

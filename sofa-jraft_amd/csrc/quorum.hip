@@ -443,6 +443,125 @@ __global__ __launch_bounds__(64 * W) void quorum_epochs_kernel(JrqQuorumArgs a, 
   }
 }
 
+// K epochs of a large batch (r05): with G/2 >= 2048 lanes per CU there is parallelism enough
+// over the groups alone, so one lane takes two adjacent groups through all K epochs in order,
+// carrying the prefix max in registers -- no chunk stitch, no LDS, no barrier -- and reads every
+// stream with 16-B loads (1 KiB per wave instruction; the chunk kernel's tiles of 32 groups
+// read 256-B row segments).  The same carried state as quorum_epochs_kernel.
+// One group's epoch candidate v_k (kI64Min: none) and its out-of-range flags.
+template <int P>
+__device__ __forceinline__ int64_t epoch_candidate(const JrqQuorumArgs& a, bool runs, uint32_t r0,
+                                                   uint32_t r1, int64_t pi0, int64_t la,
+                                                   uint64_t cw, int64_t (&m)[P], uint8_t& st) {
+  if (!runs && rel_domain(pi0, la) && pi0 != 0) {  // 32-bit, relative to pendingIndex_0
+    RelGroup<P> g;
+    rel_map<P>(pi0, la, m, g);
+    st = g.st;
+    uint8_t unused;
+    const uint32_t r = rel_cand<P>(cw, g, unused);
+    return r >= 1u ? pi0 - 1 + static_cast<int64_t>(r) : kI64Min;
+  }
+  st = mask_out_of_range<P>(m, la);
+  if (!runs) {
+    int64_t cand = run_bound<P>(m, cw);
+    cand = cand < la ? cand : la;
+    return cand >= pi0 ? cand : kI64Min;
+  }
+  uint8_t unused = 0;
+  return csr_runs_best<P>(a, r0, r1, pi0, la, kI64Min, m, unused);
+}
+
+// Status of epoch k beyond the out-of-range flags: not the leader, or an empty conf over an
+// entry still pending (pik = pendingIndex before epoch k).
+__device__ __forceinline__ uint8_t epoch_status(const JrqQuorumArgs& a, bool runs, uint32_t r0,
+                                                uint32_t r1, int64_t pi0, int64_t pik, int64_t la,
+                                                uint64_t cw, uint8_t st) {
+  if (pi0 == 0) return kStNotLeader;
+  if (!runs) return ((cw & 0xFFFFu) == 0 && la >= pik) ? static_cast<uint8_t>(st | kStEmptyConf) : st;
+  for (uint32_t r = r0; r < r1; ++r) {  // runs still pending at epoch k with an empty conf
+    const int64_t sr = (r == r0) ? pik : (a.run_start[r] > pik ? a.run_start[r] : pik);
+    const int64_t er = (r + 1 < r1) ? a.run_start[r + 1] - 1 : la;
+    if ((er < la ? er : la) >= sr && (a.run_conf[r] & 0xFFFFu) == 0) st |= kStEmptyConf;
+  }
+  return st;
+}
+
+template <int P>
+__global__ __launch_bounds__(512) void quorum_epochs_pair_kernel(JrqQuorumArgs a, uint32_t K,
+                                                                                 uint64_t match_eld,
+                                                                                 uint64_t la_eld) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t pairs = a.G >> 1;
+  const bool tail = i == pairs && (a.G & 1u);  // the odd last group, on one more lane
+  if (i >= pairs && !tail) return;
+  const uint32_t g = tail ? a.G - 1 : 2 * i;
+  const int n = tail ? 1 : 2;
+  int64_t pi0[2], lc0[2], vmax[2] = {kI64Min, kI64Min};
+  uint64_t cw[2];
+  bool runs[2];
+  uint32_t r0[2], r1[2];
+  if (!tail) {
+    const i64x2 p2 = ld2nt(a.pending_index + g), l2 = ld2nt(a.last_committed + g);
+    const i64x2 c2 = ld2nt(reinterpret_cast<const int64_t*>(a.conf) + g);
+    pi0[0] = p2.x; pi0[1] = p2.y;
+    lc0[0] = l2.x; lc0[1] = l2.y;
+    cw[0] = static_cast<uint64_t>(c2.x); cw[1] = static_cast<uint64_t>(c2.y);
+  } else {
+    pi0[0] = a.pending_index[g]; lc0[0] = a.last_committed[g]; cw[0] = a.conf[g];
+    pi0[1] = 0; lc0[1] = 0; cw[1] = 0;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    runs[h] = h < n && a.run_off != nullptr && (cw[h] & kConfRuns);
+    r0[h] = runs[h] ? a.run_off[g + h] : 0;
+    r1[h] = runs[h] ? a.run_off[g + h + 1] : 0;
+  }
+  for (uint32_t k = 0; k < K; ++k) {
+    int64_t la[2], m[2][P];
+    if (!tail) {
+      const i64x2 l2 = ld2nt(a.last_appended + k * la_eld + g);
+      la[0] = l2.x; la[1] = l2.y;
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        const i64x2 v = ld2nt(a.match + k * match_eld + static_cast<size_t>(p) * a.match_ld + g);
+        m[0][p] = v.x;
+        m[1][p] = v.y;
+      }
+    } else {
+      la[0] = a.last_appended[k * la_eld + g];
+      la[1] = 0;
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        m[0][p] = a.match[k * match_eld + static_cast<size_t>(p) * a.match_ld + g];
+        m[1][p] = 0;
+      }
+    }
+    int64_t out[2];
+    uint8_t s[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t prev = vmax[h];  // max v over the earlier epochs
+      uint8_t st = 0;
+      const int64_t v = epoch_candidate<P>(a, runs[h], r0[h], r1[h], pi0[h], la[h], cw[h], m[h], st);
+      vmax[h] = v > vmax[h] ? v : vmax[h];
+      out[h] = pi0[h] == 0 ? lc0[h] : (vmax[h] > lc0[h] ? vmax[h] : lc0[h]);
+      const int64_t pik = prev > lc0[h] ? prev + 1 : pi0[h];
+      s[h] = epoch_status(a, runs[h], r0[h], r1[h], pi0[h], pik, la[h], cw[h], st);
+    }
+    const size_t o = static_cast<size_t>(k) * a.G + g;
+    if (!tail) {
+      i64x2 c2;
+      c2.x = out[0];
+      c2.y = out[1];
+      st_pair(c2, reinterpret_cast<i64x2*>(a.committed + o));
+      st_pair(static_cast<uint16_t>(s[0] | (s[1] << 8)), reinterpret_cast<uint16_t*>(a.status + o));
+    } else {
+      a.committed[o] = out[0];
+      a.status[o] = s[0];
+    }
+  }
+}
+
 // ------------------------------------------------------------------ lease ---
 // NodeImpl.checkDeadNodes0 (jraft-core/.../core/NodeImpl.java:1970-2000) for one conf:
 // the leader itself is alive; another member is alive when now - lastRpcSendTimestamp <=
@@ -830,9 +949,33 @@ static inline uint32_t jrq_epochs_waves(uint32_t K, uint32_t C, uint32_t T, uint
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum_epochs(
     const JrqQuorumArgs* args, uint32_t K, uint64_t match_eld, uint64_t la_eld, int num_cus,
     hipStream_t stream) {
-  (void)num_cus;
-  // one workgroup per tile of groups; chunks of C epochs (two per wave), at most W waves,
-  // super-chunks beyond that
+  // a batch with 2048+ groups per CU (C3K: 1M groups): two groups per lane through every epoch
+  // in order (quorum_epochs_pair_kernel), when the arrays allow its 16-B accesses
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+  const JrqQuorumArgs& q = *args;
+  const bool pair = q.G % 2 == 0 && static_cast<uint64_t>(q.G) >= 2048ull * static_cast<uint64_t>(num_cus) &&
+                    (q.match_ld & 1u) == 0 && (match_eld & 1u) == 0 && (la_eld & 1u) == 0 &&
+                    al16(q.match) && al16(q.pending_index) && al16(q.last_appended) &&
+                    al16(q.last_committed) && al16(q.conf) && al16(q.committed) &&
+                    (reinterpret_cast<uintptr_t>(q.status) & 1u) == 0;
+  if (pair) {
+    const dim3 grid(static_cast<unsigned>((q.G / 2 + 511) / 512)), blk(512);
+    switch (q.num_peers) {
+#define JRQ_CASE(P)                                                                            \
+  case P:                                                                                      \
+    hipLaunchKernelGGL(jrq::quorum_epochs_pair_kernel<P>, grid, blk, 0, stream, q, K, match_eld, la_eld); \
+    break;
+      JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
+      JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
+      JRQ_CASE(15) JRQ_CASE(16)
+#undef JRQ_CASE
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  // otherwise one workgroup per tile of groups; chunks of C epochs (two per wave), at most W
+  // waves, super-chunks beyond that
   switch (args->num_peers) {
 #define JRQ_CASE(P)                                                                           \
   case P: {                                                                                   \

@@ -587,11 +587,10 @@ class Table:
                                           _dev_ptr(status_out)), self._eng.handle)
 
     def gather_dev_list(self, changed_out, n_changed_out) -> np.ndarray:
-        """Host copy of a device-variant list (slices back to back), as JRQ words."""
-        counts = n_changed_out.cpu().numpy().astype(np.int64)
-        words = changed_out.cpu().numpy().view(np.uint64).reshape(-1, _lib.TABLE_SLICE)
-        keep = np.arange(_lib.TABLE_SLICE)[None, :] < counts[:, None]
-        return words[keep]
+        """Host copy of a device-variant list as the host variant's words (delta << 32 | group),
+        slices in order: each slice is a 256-bit map of its listed groups, then their u32
+        deltas in group order (include/jrq.h jrq_table_epoch_dev)."""
+        return decode_slices(changed_out.cpu().numpy(), n_changed_out.cpu().numpy())
 
     def read(self) -> dict:
         G, P = self.G, self.P
@@ -614,6 +613,21 @@ class Table:
         v = TableView()
         check(self._L.jrq_table_view_get(self._h, C.byref(v)), self._eng.handle)
         return v
+
+
+def decode_slices(slices, counts) -> np.ndarray:
+    """jrq_table_epoch_dev's slices (int64 / uint64 words, JRQ_TABLE_SLICE per slice) and
+    per-slice counts -> the host list's words (delta << 32 | group), in group order."""
+    S = _lib.TABLE_SLICE
+    w = np.ascontiguousarray(slices).view(np.uint64).reshape(-1, S)
+    counts = np.asarray(counts).astype(np.int64)
+    bits = np.unpackbits(np.ascontiguousarray(w[:, :4]).view(np.uint8), axis=1, bitorder="little").astype(bool)
+    if not np.array_equal(bits.sum(axis=1), counts[:len(bits)]):
+        raise AssertionError("slice maps disagree with the per-slice counts")
+    deltas = np.ascontiguousarray(w[:, 4:]).view(np.uint32)  # [slices][504]
+    keep = np.arange(deltas.shape[1])[None, :] < counts[:, None]
+    groups = (np.nonzero(bits)[0] * S + np.nonzero(bits)[1]).astype(np.uint64)
+    return (deltas[keep].astype(np.uint64) << np.uint64(32)) | groups
 
 
 def decode_changed(words) -> tuple[np.ndarray, np.ndarray]:

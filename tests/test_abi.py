@@ -41,7 +41,7 @@ def test_ctypes_signatures_cover_header():
     names = {s[0] for s in _lib.SIGNATURES}
     assert names == set(declared_functions())
     L = _lib.load()
-    assert L.jrq_abi_version() == 2
+    assert L.jrq_abi_version() == 3
 
 
 def test_group_batch_layout_matches_header():

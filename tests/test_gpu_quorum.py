@@ -377,3 +377,51 @@ def test_pair_kernel_32bit_domain_edges(engine):
     engine.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy(), ce)
     np.testing.assert_array_equal(st.cpu().numpy(), se)
+
+
+def _tile_series(s, copies):
+    """`copies` back-to-back copies of a random_series batch (its run table's CSR re-based)."""
+    n, R = len(s["pending_index"]), len(s["run_start"])
+    out = {k: np.concatenate([s[k]] * copies, axis=-1) for k in
+           ("match", "last_appended", "pending_index", "last_committed", "conf", "run_start", "run_conf")}
+    ro = s["run_off"].astype(np.int64)
+    out["run_off"] = np.concatenate([ro[:-1] + c * R for c in range(copies)] + [[copies * R]]).astype(s["run_off"].dtype)
+    assert len(out["pending_index"]) == n * copies
+    return out
+
+
+@pytest.mark.parametrize("P,K", [(5, 8), (3, 5)])
+def test_gpu_quorum_epochs_large_batch(engine, oracle, P, K):
+    """K epochs of a batch large enough for the sequential pair kernel (G >= 2048 per CU, even:
+    two groups per lane through every epoch, quorum_epochs_pair_kernel) -- 147 copies of a
+    4096-group series with conf runs, flagged groups, non-leaders and out-of-range acks -- equal
+    the K sequential BallotBox replays on every copy; G - 1 groups of the same arrays (odd: the
+    chunk kernel) agree with it."""
+    import torch
+    from quorum_cases import flag_runs, random_series, series_replay
+    s = random_series(1300 + P, 4096, P, K)
+    s["conf"] = flag_runs(s)
+    ce, se = series_replay(oracle, s)
+    big = _tile_series(s, 147)
+    G = len(big["pending_index"])
+    assert G % 2 == 0 and G >= 2048 * 256
+    t = _to_dev(big, list(big.keys()))
+    c = torch.empty((K, G), dtype=torch.int64, device="cuda:0")
+    st = torch.empty((K, G), dtype=torch.uint8, device="cuda:0")
+    engine.quorum_epochs_dev(t["match"], t["pending_index"], t["last_appended"],
+                             t["last_committed"], t["conf"], c, st, run_off=t["run_off"],
+                             run_start=t["run_start"], run_conf=t["run_conf"])
+    engine.synchronize()
+    cg, sg = c.cpu().numpy(), st.cpu().numpy()
+    np.testing.assert_array_equal(cg, np.tile(ce, (1, 147)))
+    np.testing.assert_array_equal(sg, np.tile(se, (1, 147)))
+    # the chunk kernel on G - 1 groups of the same arrays (rows keep their strides)
+    G1 = G - 1
+    c1 = torch.empty((K, G1), dtype=torch.int64, device="cuda:0")
+    s1 = torch.empty((K, G1), dtype=torch.uint8, device="cuda:0")
+    engine.quorum_epochs_dev(t["match"][:, :, :G1], t["pending_index"][:G1], t["last_appended"][:, :G1],
+                             t["last_committed"][:G1], t["conf"][:G1], c1, s1, run_off=t["run_off"][:G1 + 1],
+                             run_start=t["run_start"], run_conf=t["run_conf"])
+    engine.synchronize()
+    np.testing.assert_array_equal(c1.cpu().numpy(), cg[:, :G1])
+    np.testing.assert_array_equal(s1.cpu().numpy(), sg[:, :G1])

@@ -194,17 +194,32 @@ def test_device_variant_and_view(engine, oracle):
     np.testing.assert_array_equal(got, ce)
     v = t.view()
     assert v.G == G and v.num_peers == P and v.ld >= G and v.last_committed
-    assert v.tile_groups == 256 and v.tile_stride == 256 * (P + 4)
-    # lastCommitted of group g through the view's tiled addressing
+    assert v.tile_groups == 256 and v.tile_stride == 128 * P + 1024
+    # lastCommitted of group g through the view's tiled addressing, and the u32 match words
     lcd = torch.empty(((G + 255) // 256) * v.tile_stride, dtype=torch.int64, device=dev)
     import ctypes  # (the view holds raw device pointers: read the tiles through hipMemcpy)
     hip = ctypes.CDLL("libamdhip64.so")
     assert hip.hipMemcpy(ctypes.c_void_p(lcd.data_ptr()), ctypes.c_void_p(v.match), lcd.numel() * 8, 3) == 0
     words = lcd.cpu().numpy()
     g = np.arange(G)
-    lc_view = words[(g // 256) * v.tile_stride + (P + 2) * 256 + g % 256]
+    assert v.last_committed == v.match + 8 * (128 * P + 512)
+    lc_view = words[(g // 256) * v.tile_stride + 128 * P + 512 + g % 256]
     np.testing.assert_array_equal(lc_view, ce)
-    np.testing.assert_array_equal(t.read()["last_committed"], ce)
+    rd = t.read()
+    np.testing.assert_array_equal(rd["last_committed"], ce)
+    k = g % 256
+    pos = (k % 128) // 2 * 4 + (k // 128) * 2 + k % 2  # the view's documented lane order
+    u32 = words.view(np.uint32)
+    pi = rd["pending_index"]
+    base = np.where(pi > 0, (pi - 1) & ~np.int64((1 << 30) - 1), 0)
+    for p in range(P):
+        w = u32[(g // 256) * 2 * v.tile_stride + 256 * p + pos].astype(np.int64)
+        np.testing.assert_array_equal(base + w, rd["match"][p])
+    # every leader's match at or above pendingIndex - 1 reads back exactly (below: raised to
+    # the base; match_recs sends none for non-leaders)
+    m = b["match"]
+    exact = (m >= (pi - 1)[None, :]) & (pi > 0)[None, :]
+    np.testing.assert_array_equal(rd["match"][exact], m[exact])
     t.close()
 
 
@@ -322,4 +337,28 @@ def test_flagged_groups_in_full_blocks(engine, G, joint):
         np.testing.assert_array_equal(got, exp_c)
         np.testing.assert_array_equal(stt, exp_s)
     t.check()
+    t.close()
+
+
+@pytest.mark.parametrize("G", [64, 300, 1000])
+def test_epoch_dev_writes_only_its_slices(engine, G):
+    """The epoch grid is whole workgroups (4 waves of 256 groups): a wave past the last slice
+    owns no slice and must write nothing -- the caller's list holds jrq_table_slices(t) slices
+    and its counts exactly that many words.  Sentinels after both buffers stay intact."""
+    import torch
+    P = 3
+    b = random_batch(77, G, P, run_prob=0.2)
+    t = Table(engine, G, P)
+    t.update(states_of(b), match_recs(b["match"], b["pending_index"]))
+    dev = torch.device("cuda:0")
+    S = t.slices()
+    pad = 4 * _lib.TABLE_SLICE
+    out = torch.full((S * _lib.TABLE_SLICE + pad,), -7, dtype=torch.int64, device=dev)
+    n = torch.full((S + 64,), -7, dtype=torch.int32, device=dev)
+    st = torch.full((G + 64,), 0xEE, dtype=torch.uint8, device=dev)
+    t.epoch_dev(out[:S * _lib.TABLE_SLICE], n[:S], st[:G])
+    engine.synchronize()
+    assert (out[S * _lib.TABLE_SLICE:] == -7).all().item()
+    assert (n[S:] == -7).all().item()
+    assert (st[G:] == 0xEE).all().item()
     t.close()
