@@ -197,6 +197,11 @@ typedef struct {
 } jrq_group_tiles;
 int jrq_quorum_epoch_tiles_dev(jrq_engine *e, const jrq_group_tiles *in_dev, int64_t *committed_out_dev,
                                uint8_t *status_out_dev, uint32_t G);
+/* Host variant (the JNI binding's stateless contract, INTEGRATION.md §2.5: one direct buffer
+ * of tiles per batch): the tiles and the run table are host memory, uploaded in one copy each;
+ * G >= 2.  Groups with several runs must carry JRQ_CONF_RUNS in their tile's conf word. */
+int jrq_quorum_epoch_tiles(jrq_engine *e, const jrq_group_tiles *in_host, int64_t *committed_out,
+                           uint8_t *status_out, uint32_t G);
 
 /* K successive epochs of the same G groups in one launch (the launch-bound small-G case,
  * e.g. C2's 10k groups; SURVEY.md §7 hard part 4).  Epoch k reads

@@ -682,6 +682,38 @@ int jrq_quorum_epoch_tiles_dev(jrq_engine* e, const jrq_group_tiles* in, int64_t
   return JRQ_OK;
 }
 
+int jrq_quorum_epoch_tiles(jrq_engine* e, const jrq_group_tiles* in, int64_t* committed_out,
+                           uint8_t* status_out, uint32_t G) {
+  if (!e || !in) return e ? fail(e, JRQ_E_INVALID, "null batch") : JRQ_E_INVALID;
+  if (G == 0) return JRQ_OK;
+  if (!committed_out || !status_out || !in->tiles || in->num_peers == 0 || in->num_peers > JRQ_MAX_PEERS ||
+      (in->run_off && (!in->run_start || !in->run_conf)))
+    return fail(e, JRQ_E_INVALID, "missing array or bad num_peers");
+  DeviceGuard guard(e->device);
+  jrq_group_tiles d = *in;
+  int rc;
+  const size_t words = (static_cast<size_t>(G) + 255) / 256 * 256 * (in->num_peers + 4);
+  if ((rc = stage_in(e, 0, in->tiles, words, &d.tiles))) return rc;
+  if (in->run_off) {  // host memory: the CSR is checked before a kernel indexes with it
+    const uint32_t* ro = in->run_off;
+    if (ro[0] != 0) return fail(e, JRQ_E_INVALID, "run_off must start at 0");
+    for (uint32_t g = 0; g < G; ++g)
+      if (ro[g + 1] < ro[g]) return fail(e, JRQ_E_INVALID, "run_off not monotone at group %u", g);
+    if ((rc = stage_in(e, 5, in->run_off, static_cast<size_t>(G) + 1, &d.run_off))) return rc;
+    if ((rc = stage_in(e, 6, in->run_start, ro[G], &d.run_start))) return rc;
+    if ((rc = stage_in(e, 7, in->run_conf, ro[G], &d.run_conf))) return rc;
+  }
+  void *dc = nullptr, *ds = nullptr;
+  if ((rc = ensure_stage(e, 8, static_cast<size_t>(G) * 8, &dc))) return rc;
+  if ((rc = ensure_stage(e, 9, G, &ds))) return rc;
+  if ((rc = jrq_quorum_epoch_tiles_dev(e, &d, static_cast<int64_t*>(dc), static_cast<uint8_t*>(ds), G)))
+    return rc;
+  JRQ_HIP(e, hipMemcpyAsync(committed_out, dc, static_cast<size_t>(G) * 8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipMemcpyAsync(status_out, ds, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
 int jrq_quorum_epoch(jrq_engine* e, const jrq_group_batch* in, int64_t* committed_out,
                      uint8_t* status_out, uint32_t G) {
   if (!e || !in) return e ? fail(e, JRQ_E_INVALID, "null batch") : JRQ_E_INVALID;

@@ -110,6 +110,7 @@ SIGNATURES = [
     ("jrq_quorum_epoch_dev", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
     ("jrq_quorum_epoch_tiles_dev", C.c_int, [_V, C.POINTER(GroupTiles), _V, _V, C.c_uint32]),
     ("jrq_quorum_epoch", C.c_int, [_V, C.POINTER(GroupBatch), _V, _V, C.c_uint32]),
+    ("jrq_quorum_epoch_tiles", C.c_int, [_V, C.POINTER(GroupTiles), _V, _V, C.c_uint32]),
     ("jrq_quorum_epochs_dev", C.c_int,
      [_V, C.POINTER(GroupBatch), C.c_uint32, C.c_uint64, C.c_uint64, _V, _V, C.c_uint32]),
     ("jrq_crc64_batch_dev", C.c_int, [_V, _V, _V, C.c_uint32, _V]),

@@ -145,6 +145,19 @@ class Engine:
         launch.keep = keep
         return launch
 
+    def quorum_epoch_tiles(self, tiles, P, G, run_off=None, run_start=None, run_conf=None):
+        """Host variant of the tiled epoch (jrq_quorum_epoch_tiles: the JNI binding's stateless
+        contract): `tiles` a numpy int64 array in the tile layout (W.to_tiles).  Returns
+        (committed int64[G], status uint8[G])."""
+        tiles = _c(tiles, np.int64)
+        ro, rs, rc_ = _c(run_off, np.uint32), _c(run_start, np.int64), _c(run_conf, np.uint64)
+        b = _lib.GroupTiles(_np_ptr(tiles), P, _np_ptr(ro), _np_ptr(rs), _np_ptr(rc_))
+        out = np.zeros(G, np.int64)
+        st = np.zeros(G, np.uint8)
+        check(self._L.jrq_quorum_epoch_tiles(self._h, C.byref(b), _np_ptr(out), _np_ptr(st), G),
+              self._h)
+        return out, st
+
     def quorum_epoch_launcher(self, match, pending_index, last_appended, last_committed, conf,
                               committed_out, status_out, run_off=None, run_start=None,
                               run_conf=None):

@@ -425,3 +425,23 @@ def test_gpu_quorum_epochs_large_batch(engine, oracle, P, K):
     engine.synchronize()
     np.testing.assert_array_equal(c1.cpu().numpy(), cg[:, :G1])
     np.testing.assert_array_equal(s1.cpu().numpy(), sg[:, :G1])
+
+
+@pytest.mark.parametrize("P,run_prob,G", [(5, 0.01, 4096), (3, 0.3, 3001), (16, 0.5, 515)])
+def test_tiles_host_variant_vs_replay(engine, oracle, P, run_prob, G):
+    """jrq_quorum_epoch_tiles (host memory: the JNI binding's one direct buffer of tiles per
+    batch) decides exactly as the replay through real BallotBoxes; a bad
+    run CSR is refused before any upload."""
+    from jraft_amd import JrqError
+    from quorum_cases import flag_runs
+    b = random_batch(1700 + P, G, P, run_prob=run_prob)
+    b["conf"] = flag_runs(b)
+    ce, se = _replay(oracle, b)
+    tiles = W.to_tiles(b["match"], b["pending_index"], b["last_appended"], b["last_committed"], b["conf"])
+    out, st = engine.quorum_epoch_tiles(tiles, P, G, b["run_off"], b["run_start"], b["run_conf"])
+    np.testing.assert_array_equal(out, ce)
+    np.testing.assert_array_equal(st, se)
+    bad = b["run_off"].copy()
+    bad[G // 2] = bad[G // 2 + 1] + 1  # not monotone
+    with pytest.raises(JrqError):
+        engine.quorum_epoch_tiles(tiles, P, G, bad, b["run_start"], b["run_conf"])

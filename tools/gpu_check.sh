@@ -44,7 +44,7 @@ for s in $STEPS; do
     ab)    run ab_${TAG:-sel} 600 env AB_LEGS=${AB_LEGS:-C3,C5f,C1f,archive} python tools/ab_inproc.py ${AB_VARIANTS:-base=ab/base/libjrq.so} ;;
     tpab)  # the resident table epoch, every group committing, libjrq variants side by side
            for P in ${TP_PEERS:-5}; do
-             run tpab_${TAG:-sel}_P$P 300 env P=$P python tools/table_peers_ab.py ${TP_VARIANTS:-base=ab/base/libjrq.so}
+             run tpab_${TAG:-sel}_P$P 300 env P=$P FLAG_FRAC=${FLAG_FRAC:-0} python tools/table_peers_ab.py ${TP_VARIANTS:-base=ab/base/libjrq.so}
            done ;;
     fulltrace) # the default bench run under the tracer: the printed line, the full result and one
            # kernel trace of the same launches (tools/leg_traces.py --trace -> <tag>_leg_kernels.json)

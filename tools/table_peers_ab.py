@@ -35,6 +35,13 @@ def main():
             peers = np.arange(P, dtype=np.uint64)
             conf = np.uint64(((1 << P) - 1) | ((P // 2 + 1) << 32))
             st["run_conf"][:, 0] = conf
+            ff = float(os.environ.get("FLAG_FRAC", "0"))  # groups with a conf change in the window
+            if ff > 0:
+                fl = r.random(G) < ff
+                st["num_runs"] = np.where(fl, 2, 1)
+                st["run_start"][:, 1] = np.where(fl, lc + 33, 0)
+                st["run_conf"][:, 1] = np.where(fl, np.uint64(((1 << P) - 1) | ((P // 2 + 1) << 32) |
+                                                              (0b111 << 16) | (2 << 40)), 0)
             gs = np.arange(G)
             recs = np.concatenate([L.rec(gs, p, r.integers(0, 65, G)) for p in range(P)])
             t = Table(e, G, P); t.update(st, recs); prist.append(t); work.append(Table(e, G, P))
@@ -59,7 +66,7 @@ def main():
     names = [n for n, _ in variants]
     same = {n: outs[n] is not None and all(np.array_equal(np.asarray(a), np.asarray(b))
                                          for a, b in zip(outs[names[0]], outs[n])) for n in names}
-    print(json.dumps({"P": P, "us": {n: float(np.median(t)) for n, t in times.items()},
+    print(json.dumps({"P": P, "flag_frac": os.environ.get("FLAG_FRAC", "0"), "us": {n: float(np.median(t)) for n, t in times.items()},
                       "changed": len(outs[names[0]][0]), "same_as_first": same}))
 
 if __name__ == "__main__":
