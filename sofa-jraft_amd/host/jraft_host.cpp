@@ -130,6 +130,23 @@ uint64_t Engine::peerXor(const LogEntry& e, std::map<std::string, uint64_t>& cac
   return x;
 }
 
+std::vector<uint64_t> Engine::peerChecksums(const std::vector<const LogEntry*>& entries) {
+  std::map<std::string, uint64_t> cache;
+  for (auto* e : entries)
+    for (auto* list : {&e->peers, &e->oldPeers, &e->learners, &e->oldLearners})
+      for (auto& p : *list) cache.emplace(p.toString(), 0);
+  if (!cache.empty()) {
+    std::vector<std::vector<uint8_t>> strs;
+    for (auto& kv : cache) strs.emplace_back(kv.first.begin(), kv.first.end());
+    auto crcs = crc64(strs);
+    size_t i = 0;
+    for (auto& kv : cache) kv.second = crcs[i++];
+  }
+  std::vector<uint64_t> px(entries.size());
+  for (size_t i = 0; i < entries.size(); ++i) px[i] = peerXor(*entries[i], cache);
+  return px;
+}
+
 std::vector<uint64_t> Engine::checksum(const std::vector<const LogEntry*>& entries) {
   // PeerId.checksum of every distinct peer string: one GPU CRC batch (PeerId.java:60-65)
   std::map<std::string, uint64_t> cache;
@@ -1345,6 +1362,228 @@ std::string BallotBox::describe() const {
     << "  pendingIndex: " << pi << "\n"
     << "  pendingMetaQueueSize: " << q << "\n";
   return o.str();
+}
+
+// -------------------------------------------------------- follower / reader
+
+std::vector<int32_t> FollowerVerifier::verify(const std::vector<const AppendEntriesRequest*>& reqs,
+                                              std::vector<uint64_t>* checksums) {
+  const uint32_t R = static_cast<uint32_t>(reqs.size());
+  std::vector<uint32_t> reqOff(R + 1, 0);
+  std::vector<int64_t> prev(R);
+  std::vector<const LogEntry*> metas;
+  for (uint32_t r = 0; r < R; ++r) {
+    const AppendEntriesRequest& q = *reqs[r];
+    if (q.dataLen.size() != q.entries.size()) throw std::invalid_argument("dataLen per entry");
+    prev[r] = q.prevLogIndex;
+    reqOff[r + 1] = reqOff[r] + static_cast<uint32_t>(q.entries.size());
+    for (auto& e : q.entries) metas.push_back(&e);
+  }
+  const uint32_t N = reqOff[R];
+  std::vector<int32_t> first(R, -1);
+  if (R == 0) return first;
+  // the PeerId checksums of configuration entries (one GPU CRC batch), then every request's
+  // entries in one launch sequence (scan -> CRC -> first corrupt)
+  const std::vector<uint64_t> px = eng_->peerChecksums(metas);
+  std::vector<int64_t> term(N), dlen(N);
+  std::vector<uint8_t> type(N), has(N);
+  std::vector<uint64_t> stored(N), out(N);
+  std::vector<uint8_t> corrupt(N);
+  std::vector<uint8_t> data;
+  uint32_t i = 0;
+  for (uint32_t r = 0; r < R; ++r) {
+    const AppendEntriesRequest& q = *reqs[r];
+    for (size_t k = 0; k < q.entries.size(); ++k, ++i) {
+      const LogEntry& e = q.entries[k];
+      term[i] = e.id.term;
+      type[i] = static_cast<uint8_t>(e.type);
+      dlen[i] = q.dataLen[k];
+      has[i] = e.hasChecksum();
+      stored[i] = e.getChecksum();
+    }
+    data.insert(data.end(), q.data.begin(), q.data.end());
+  }
+  if (data.empty()) data.push_back(0);
+  throwIfError(jrq_append_entries_verify(eng_->raw(), R, reqOff.data(), prev.data(), N, term.data(),
+                                         type.data(), dlen.data(), px.data(), stored.data(),
+                                         has.data(), data.data(), out.data(), corrupt.data(),
+                                         first.data()),
+               eng_->raw(), "jrq_append_entries_verify");
+  if (checksums) *checksums = std::move(out);
+  return first;
+}
+
+std::vector<DecodedEntry> LogReader::decode(const std::vector<std::vector<uint8_t>>& records) {
+  const uint32_t N = static_cast<uint32_t>(records.size());
+  std::vector<DecodedEntry> outv(N);
+  if (N == 0) return outv;
+  std::vector<uint64_t> off(N + 1, 0);
+  for (uint32_t i = 0; i < N; ++i) off[i + 1] = off[i] + records[i].size();
+  std::vector<uint8_t> buf(std::max<uint64_t>(off[N], 1));
+  for (uint32_t i = 0; i < N; ++i)
+    if (!records[i].empty()) std::memcpy(buf.data() + off[i], records[i].data(), records[i].size());
+  std::vector<uint8_t> status(N), type(N), has(N), corrupt(N);
+  std::vector<int64_t> index(N), term(N);
+  std::vector<uint64_t> stored(N), doff(N), dlen(N), sum(N);
+  std::vector<uint32_t> pc(N);
+  throwIfError(jrq_v2_decode_verify(eng_->raw(), buf.data(), off.data(), N, status.data(), type.data(),
+                                    index.data(), term.data(), stored.data(), has.data(), doff.data(),
+                                    dlen.data(), pc.data(), sum.data(), corrupt.data()),
+               eng_->raw(), "jrq_v2_decode_verify");
+  for (uint32_t i = 0; i < N; ++i) {
+    DecodedEntry& d = outv[i];
+    d.status = status[i];
+    if (d.status != JRQ_V2_OK) continue;
+    d.entry.type = static_cast<EntryType>(type[i]);
+    d.entry.id = LogId{index[i], term[i]};
+    if (has[i]) d.entry.setChecksum(stored[i]);
+    d.entry.data.assign(buf.begin() + static_cast<std::ptrdiff_t>(doff[i]),
+                        buf.begin() + static_cast<std::ptrdiff_t>(doff[i] + dlen[i]));
+    d.peerCount = pc[i];
+    d.corrupt = corrupt[i] != 0;
+  }
+  return outv;
+}
+
+// ------------------------------------------------------------- leader tick
+
+LeaderTicker::LeaderTicker(Engine& eng, uint32_t groups, uint32_t peers)
+    : eng_(&eng), G_(groups), P_(peers) {
+  if (peers == 0 || peers > JRQ_MAX_PEERS) throw std::invalid_argument("peers outside 1..16");
+  ts_.assign(static_cast<size_t>(P_) * G_, 0);
+  conf_.assign(G_, 0);
+  self_.assign(G_, 0);
+  lease_.assign(G_, 0);
+  order_.assign(G_, 0);
+  okMask_.assign(G_, 0);
+  arrivals_.assign(G_, 0);
+  peers_.resize(G_);
+  reads_.resize(G_);
+}
+
+int LeaderTicker::slot(uint32_t g, const PeerId& peer) const {
+  const uint32_t id = peerId(peer);
+  const auto& v = peers_[g];
+  for (size_t s = 0; s < v.size(); ++s)
+    if (v[s] == id) return static_cast<int>(s);
+  return -1;
+}
+
+void LeaderTicker::becomeLeader(uint32_t g, const Configuration& conf, const Configuration* oldConf,
+                                const PeerId& self, int64_t nowMs) {
+  if (g >= G_) throw std::out_of_range("group id");
+  std::vector<std::function<void(bool)>> failed;
+  {
+    std::lock_guard<std::mutex> l(mu_);
+    auto& v = peers_[g];
+    v.clear();
+    auto slotOf = [&](const PeerId& p) {
+      const uint32_t id = peerId(p);
+      for (size_t s = 0; s < v.size(); ++s)
+        if (v[s] == id) return static_cast<uint32_t>(s);
+      if (v.size() >= P_) throw std::length_error("more distinct peers than slots");
+      v.push_back(id);
+      return static_cast<uint32_t>(v.size() - 1);
+    };
+    uint32_t nm = 0, om = 0;
+    for (auto& p : conf.peers) nm |= 1u << slotOf(p);
+    if (oldConf)
+      for (auto& p : oldConf->peers) om |= 1u << slotOf(p);
+    self_[g] = static_cast<uint8_t>(slotOf(self));
+    // quorums as getQuorum / checkDeadNodes count them: peers.size() / 2 + 1 (distinct ids)
+    const uint32_t nn = static_cast<uint32_t>(__builtin_popcount(nm)), no = static_cast<uint32_t>(__builtin_popcount(om));
+    conf_[g] = JRQ_CONF(nm, om, nn / 2 + 1, no ? no / 2 + 1 : 0);
+    for (uint32_t s = 0; s < P_; ++s) ts_[static_cast<size_t>(s) * G_ + g] = nowMs;
+    lease_[g] = nowMs;
+    order_[g] = 0;
+    okMask_[g] = 0;
+    arrivals_[g] = 0;
+    failed.swap(reads_[g]);
+  }
+  for (auto& f : failed) f(false);
+}
+
+void LeaderTicker::stepDown(uint32_t g) {
+  std::vector<std::function<void(bool)>> failed;
+  {
+    std::lock_guard<std::mutex> l(mu_);
+    conf_[g] = 0;
+    failed.swap(reads_[g]);
+    order_[g] = 0;
+    okMask_[g] = 0;
+    arrivals_[g] = 0;
+  }
+  for (auto& f : failed) f(false);
+}
+
+void LeaderTicker::onRpcSent(uint32_t g, const PeerId& peer, int64_t nowMs) {
+  std::lock_guard<std::mutex> l(mu_);
+  const int s = slot(g, peer);
+  if (s >= 0) ts_[static_cast<size_t>(s) * G_ + g] = nowMs;
+}
+
+void LeaderTicker::readIndex(uint32_t g, std::function<void(bool)> done) {
+  bool fail = false;
+  {
+    std::lock_guard<std::mutex> l(mu_);
+    if (conf_[g] == 0) fail = true;  // not the leader: readLeader fails (EPERM)
+    else reads_[g].push_back(std::move(done));
+  }
+  if (fail) done(false);
+}
+
+void LeaderTicker::onHeartbeatResponse(uint32_t g, const PeerId& peer, bool success) {
+  std::lock_guard<std::mutex> l(mu_);
+  const int s = slot(g, peer);
+  if (s < 0 || reads_[g].empty() || ((order_[g] >> (4 * s)) & 0xFu) != 0) return;  // one response per peer
+  const uint32_t pos = arrivals_[g] < 15 ? ++arrivals_[g] : 15u;
+  order_[g] |= static_cast<uint64_t>(pos) << (4 * s);
+  if (success) okMask_[g] |= static_cast<uint16_t>(1u << s);
+}
+
+uint32_t LeaderTicker::tick(int64_t nowMs, int64_t leaseTimeoutMs, const StepDown& onStepDown) {
+  std::vector<uint8_t> ok(G_), ri(G_);
+  std::vector<uint16_t> dead(G_);
+  std::vector<std::pair<uint32_t, uint16_t>> downs;
+  std::vector<std::pair<std::function<void(bool)>, bool>> done;
+  {
+    std::lock_guard<std::mutex> l(mu_);
+    throwIfError(jrq_leader_tick(eng_->raw(), ts_.data(), G_, P_, conf_.data(), self_.data(), G_, nowMs,
+                                 leaseTimeoutMs, ok.data(), lease_.data(), dead.data(), order_.data(),
+                                 okMask_.data(), ri.data()),
+                 eng_->raw(), "jrq_leader_tick");
+    for (uint32_t g = 0; g < G_; ++g) {
+      if (conf_[g] == 0) continue;  // not a leader
+      if (!reads_[g].empty() && ri[g] != JRQ_READINDEX_PENDING) {
+        const bool good = ri[g] == JRQ_READINDEX_SUCCESS;
+        for (auto& f : reads_[g]) done.emplace_back(std::move(f), good);
+        reads_[g].clear();
+        order_[g] = 0;
+        okMask_[g] = 0;
+        arrivals_[g] = 0;
+      }
+      if (ok[g] != 3) {  // "Majority of the group dies": step down
+        downs.emplace_back(g, dead[g]);
+        conf_[g] = 0;
+        for (auto& f : reads_[g]) done.emplace_back(std::move(f), false);
+        reads_[g].clear();
+      }
+    }
+  }
+  for (auto& d : done) d.first(d.second);
+  if (onStepDown)
+    for (auto& d : downs) onStepDown(d.first, d.second);
+  return static_cast<uint32_t>(downs.size());
+}
+
+int64_t LeaderTicker::lastLeaderTimestamp(uint32_t g) const {
+  std::lock_guard<std::mutex> l(mu_);
+  return lease_[g];
+}
+
+bool LeaderTicker::isLeader(uint32_t g) const {
+  std::lock_guard<std::mutex> l(mu_);
+  return conf_[g] != 0;
 }
 
 }  // namespace jraft

@@ -126,6 +126,9 @@ class Engine {
   std::vector<uint64_t> checksum(const std::vector<const LogEntry*>& entries);
   // isCorrupted for a batch: hasChecksum && stored != checksum() (:156-158).
   std::vector<uint8_t> verify(const std::vector<const LogEntry*>& entries);
+  // Per entry, the XOR of the PeerId.checksum() of its peers, oldPeers, learners and
+  // oldLearners (LogEntry.java:101-108): one GPU CRC batch over the distinct peer strings.
+  std::vector<uint64_t> peerChecksums(const std::vector<const LogEntry*>& entries);
 
  private:
   uint64_t peerXor(const LogEntry& e, std::map<std::string, uint64_t>& cache);
@@ -161,6 +164,97 @@ class CRC64 {
   size_t flush_;
   uint64_t crc_ = 0;
   std::vector<uint8_t> buf_;
+};
+
+// -------------------------------------------------------- follower / reader
+
+// One AppendEntriesRequest as the follower receives it (rpc.proto AppendEntriesRequest /
+// raft.proto EntryMeta): the EntryMetas and the request's data, every entry's bytes back to
+// back (an ENTRY_TYPE_UNKNOWN meta consumes none, NodeImpl.java:1809-1823).
+struct AppendEntriesRequest {
+  int64_t prevLogIndex = 0;
+  std::vector<LogEntry> entries;  // meta fields; entries[i].data left empty (the bytes are in data)
+  std::vector<int64_t> dataLen;   // EntryMeta.data_len per entry
+  std::vector<uint8_t> data;
+};
+
+// NodeImpl.handleAppendEntriesRequest's per-entry isCorrupted loop (NodeImpl.java:1766-1792)
+// for a batch of requests at once (jrq_append_entries_verify): per request the position of its
+// first corrupt entry -- the one the reference answers with EINVAL -- or -1.
+class FollowerVerifier {
+ public:
+  explicit FollowerVerifier(Engine& eng) : eng_(&eng) {}
+  std::vector<int32_t> verify(const std::vector<const AppendEntriesRequest*>& reqs,
+                              std::vector<uint64_t>* checksums = nullptr);
+
+ private:
+  Engine* eng_;
+};
+
+// LogManagerImpl's read path (getEntry -> AutoDetectDecoder.decode -> isCorrupted,
+// LogManagerImpl.java:733-745) for a batch of stored V2 records (jrq_v2_decode_verify).
+struct DecodedEntry {
+  uint8_t status = 0;     // JRQ_V2_OK / _NULL (the reference's null) / _V1 / _HOST (decode on the host)
+  LogEntry entry;         // type, id, stored checksum, data (peers: decode on the host when needed)
+  uint32_t peerCount = 0; // peers + oldPeers + learners + oldLearners in the record
+  bool corrupt = false;   // isCorrupted(): LogEntryCorruptedException / RaftError.EIO
+};
+class LogReader {
+ public:
+  explicit LogReader(Engine& eng) : eng_(&eng) {}
+  std::vector<DecodedEntry> decode(const std::vector<std::vector<uint8_t>>& records);
+
+ private:
+  Engine* eng_;
+};
+
+// ------------------------------------------------------------- leader tick
+
+// The leader-side timers of many Raft groups, decided for all of them by one device pass
+// (jrq_leader_tick): NodeImpl.handleStepDownTimeout -> checkDeadNodes (NodeImpl.java:
+// 1970-2016: is a quorum of the conf -- and of the old conf -- alive, by each peer's
+// lastRpcSendTimestamp; the lease start moves to the oldest alive one) and the ReadOnlySafe
+// heartbeat round of readLeader (:1343-1396, ReadIndexHeartbeatResponseClosure :1246-1291).
+// Per group a slot per distinct peer of conf + old conf (<= peers), its timestamps and the open
+// ReadIndex round's responses in arrival order.  Calls lock the ticker (one mutex): the
+// per-RPC call is a few stores.
+class LeaderTicker {
+ public:
+  using StepDown = std::function<void(uint32_t group, uint16_t deadSlots)>;
+  LeaderTicker(Engine& eng, uint32_t groups, uint32_t peers);
+  // becomeLeader: the group's conf (and old conf while joint), the leader's own peer, the
+  // lease start (lastLeaderTimestamp); every peer's timestamp starts at nowMs
+  void becomeLeader(uint32_t g, const Configuration& conf, const Configuration* oldConf,
+                    const PeerId& self, int64_t nowMs);
+  void stepDown(uint32_t g);  // not checked any more; an open ReadIndex round fails
+  // Replicator: an RPC to `peer` left (its lastRpcSendTimestamp)
+  void onRpcSent(uint32_t g, const PeerId& peer, int64_t nowMs);
+  // readLeader, ReadOnlySafe: join the group's open heartbeat round (or start one); done runs
+  // once with the round's verdict (true: the read index may be served)
+  void readIndex(uint32_t g, std::function<void(bool)> done);
+  // a heartbeat response of the open round (success = response.getSuccess())
+  void onHeartbeatResponse(uint32_t g, const PeerId& peer, bool success);
+  // One pass over every leader group: groups without an alive quorum call stepDown (then
+  // stop being checked), decided ReadIndex rounds run their closures.  Returns the groups
+  // that failed the lease check.
+  uint32_t tick(int64_t nowMs, int64_t leaseTimeoutMs, const StepDown& onStepDown);
+  int64_t lastLeaderTimestamp(uint32_t g) const;
+  bool isLeader(uint32_t g) const;
+
+ private:
+  int slot(uint32_t g, const PeerId& peer) const;
+  Engine* eng_;
+  uint32_t G_, P_;
+  mutable std::mutex mu_;
+  std::vector<int64_t> ts_;          // [P][G] lastRpcSendTimestamp per slot
+  std::vector<uint64_t> conf_;       // [G] JRQ_CONF word of the slots (0: not a leader)
+  std::vector<uint8_t> self_;        // [G] the leader's slot
+  std::vector<int64_t> lease_;       // [G] lastLeaderTimestamp
+  std::vector<uint64_t> order_;      // [G] arrival positions of the open round's responses
+  std::vector<uint16_t> okMask_;     // [G]
+  std::vector<uint8_t> arrivals_;    // [G] responses in the open round so far
+  std::vector<std::vector<uint32_t>> peers_;  // [G] interned peer of each slot
+  std::vector<std::vector<std::function<void(bool)>>> reads_;  // [G] open round's closures
 };
 
 // --------------------------------------------------------------- ballot box

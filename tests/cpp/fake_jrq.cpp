@@ -259,4 +259,33 @@ int jrq_table_epoch(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, ui
   return JRQ_OK;
 }
 
+// the follower / reader / leader-tick paths of the host mirror, decided by the oracle
+int jrq_append_entries_verify(jrq_engine*, uint32_t R, const uint32_t* req_off, const int64_t* prev,
+                              uint32_t, const int64_t* term, const uint8_t* type,
+                              const int64_t* data_len, const uint64_t* peer_xor,
+                              const uint64_t* checksum, const uint8_t* has, const uint8_t* data,
+                              uint64_t* checksum_out, uint8_t* corrupt_out, int32_t* first_out) {
+  jo_append_entries_verify(R, req_off, prev, term, type, data_len, peer_xor, checksum, has, data,
+                           checksum_out, corrupt_out, first_out);
+  return JRQ_OK;
+}
+
+int jrq_v2_decode_verify(jrq_engine*, const uint8_t* rec, const uint64_t* off, uint32_t N,
+                         uint8_t* status, uint8_t* type, int64_t* index, int64_t* term,
+                         uint64_t* stored, uint8_t* has, uint64_t* doff, uint64_t* dlen,
+                         uint32_t* pc, uint64_t* sum, uint8_t* corrupt) {
+  jo_v2_decode_batch(rec, off, N, status, type, index, term, stored, has, doff, dlen, pc, sum, corrupt);
+  return JRQ_OK;
+}
+
+int jrq_leader_tick(jrq_engine*, const int64_t* ts, uint64_t ld, uint32_t P, const uint64_t* conf,
+                    const uint8_t* self, uint32_t G, int64_t now, int64_t timeout, uint8_t* ok,
+                    int64_t* lease, uint16_t* dead, const uint64_t* order, const uint16_t* okm,
+                    uint8_t* ri) {
+  if (ld != G) return JRQ_E_INVALID;  // (the mirror's rows are G apart)
+  jo_lease_check(G, P, ts, conf, self, now, timeout, ok, lease, dead);
+  if (order) jo_readindex_quorum(G, P, conf, self, order, okm, ri);
+  return JRQ_OK;
+}
+
 }  // extern "C"

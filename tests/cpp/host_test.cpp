@@ -948,6 +948,199 @@ static void testManyBatchesOneThread(Engine& eng) {
   for (auto& b : batches) CHECK(b->dirtyLists() == 1);
 }
 
+// ------------------------------------------------ follower / reader / leader tick
+
+// NodeImpl.handleAppendEntriesRequest's verify loop through FollowerVerifier (one GPU batch of
+// requests) against the oracle's loop: DATA entries of ragged sizes, UNKNOWN metas that consume
+// no data, a CONFIGURATION entry with peers, some stored checksums corrupted.
+static void testFollowerVerifierOnGpu(Engine& eng) {
+  std::mt19937_64 rng(41);
+  std::vector<AppendEntriesRequest> reqs(40);
+  const PeerId pa("10.1.1.1", 8081), pb("10.1.1.2", 8082, 1);
+  const uint64_t pxab = jo_peerid_checksum("10.1.1.1", 8081, 0) ^ jo_peerid_checksum("10.1.1.2", 8082, 1);
+  std::vector<uint32_t> reqOff(1, 0);
+  std::vector<int64_t> prev, term, dlen;
+  std::vector<uint8_t> type, has, data;
+  std::vector<uint64_t> px, stored;
+  for (size_t r = 0; r < reqs.size(); ++r) {
+    AppendEntriesRequest& q = reqs[r];
+    q.prevLogIndex = 1000 * static_cast<int64_t>(r);
+    const int n = static_cast<int>(rng() % 12);
+    for (int k = 0; k < n; ++k) {
+      LogEntry e;
+      const int kind = static_cast<int>(rng() % 10);
+      e.type = kind == 0 ? EntryType::UNKNOWN : kind == 1 ? EntryType::CONFIGURATION : EntryType::DATA;
+      e.id = LogId{q.prevLogIndex + 1 + k, 3};
+      const int64_t len = e.type == EntryType::UNKNOWN ? 0 : static_cast<int64_t>(rng() % 3000);
+      std::vector<uint8_t> bytes(static_cast<size_t>(len));
+      for (auto& b : bytes) b = static_cast<uint8_t>(rng());
+      uint64_t pxe = 0;
+      if (e.type == EntryType::CONFIGURATION) {
+        e.peers = {pa, pb};
+        pxe = pxab;
+      }
+      uint64_t c = jo_logentry_checksum(static_cast<int32_t>(e.type), e.id.index, e.id.term, pxe,
+                                        bytes.data(), bytes.size());
+      if (rng() % 7 == 0) c ^= 1;  // corrupted in transit
+      if (rng() % 9 != 0) e.setChecksum(c);  // some metas carry no checksum
+      q.entries.push_back(e);
+      q.dataLen.push_back(len);
+      q.data.insert(q.data.end(), bytes.begin(), bytes.end());
+      term.push_back(e.id.term);
+      type.push_back(static_cast<uint8_t>(e.type));
+      dlen.push_back(len);
+      px.push_back(pxe);
+      stored.push_back(e.getChecksum());
+      has.push_back(e.hasChecksum());
+    }
+    prev.push_back(q.prevLogIndex);
+    reqOff.push_back(reqOff.back() + static_cast<uint32_t>(n));
+    data.insert(data.end(), q.data.begin(), q.data.end());
+  }
+  std::vector<const AppendEntriesRequest*> rp;
+  for (auto& q : reqs) rp.push_back(&q);
+  FollowerVerifier fv(eng);
+  std::vector<uint64_t> sums;
+  const auto first = fv.verify(rp, &sums);
+  const uint32_t N = reqOff.back();
+  std::vector<uint64_t> esum(N);
+  std::vector<uint8_t> ecor(N);
+  std::vector<int32_t> efirst(reqs.size());
+  if (data.empty()) data.push_back(0);
+  jo_append_entries_verify(static_cast<uint32_t>(reqs.size()), reqOff.data(), prev.data(), term.data(),
+                           type.data(), dlen.data(), px.data(), stored.data(), has.data(), data.data(),
+                           esum.data(), ecor.data(), efirst.data());
+  CHECK(first == efirst);
+  CHECK(sums == esum);
+  int corrupt_requests = 0;
+  for (auto f : first) corrupt_requests += f >= 0;
+  CHECK(corrupt_requests > 3);
+}
+
+// LogManagerImpl's read path through LogReader: V2 records as V2Encoder writes them
+// (header, type 1, term 2, index 3, data 6, checksum 7), one corrupted, one truncated
+// (undecodable), one empty (the reference's null).
+static void testLogReaderOnGpu(Engine& eng) {
+  auto varint = [](std::vector<uint8_t>& o, uint64_t v) {
+    while (v >= 0x80) {
+      o.push_back(static_cast<uint8_t>(v | 0x80));
+      v >>= 7;
+    }
+    o.push_back(static_cast<uint8_t>(v));
+  };
+  std::mt19937_64 rng(43);
+  std::vector<std::vector<uint8_t>> recs;
+  std::vector<uint64_t> sums;
+  for (int i = 0; i < 300; ++i) {
+    std::vector<uint8_t> data(static_cast<size_t>(rng() % 5000));
+    for (auto& b : data) b = static_cast<uint8_t>(rng());
+    const int64_t index = 100 + i, term = 7;
+    uint64_t c = jo_logentry_checksum(2, index, term, 0, data.data(), data.size());
+    sums.push_back(c);
+    if (i == 17) c ^= 0x10;  // corrupted
+    std::vector<uint8_t> r = {0xBB, 0xD2, 0x01, 0, 0, 0};
+    r.push_back(0x08); varint(r, 2);
+    r.push_back(0x10); varint(r, static_cast<uint64_t>(term));
+    r.push_back(0x18); varint(r, static_cast<uint64_t>(index));
+    r.push_back(0x32); varint(r, data.size());
+    r.insert(r.end(), data.begin(), data.end());
+    r.push_back(0x38); varint(r, c);
+    if (i == 23) r.resize(r.size() - 3);  // truncated checksum varint
+    if (i == 29) r.clear();               // no bytes: the reference's null
+    recs.push_back(std::move(r));
+  }
+  LogReader rd(eng);
+  const auto out = rd.decode(recs);
+  CHECK(out.size() == recs.size());
+  for (int i = 0; i < 300; ++i) {
+    if (i == 23 || i == 29) {
+      CHECK(out[i].status != JRQ_V2_OK);
+      continue;
+    }
+    CHECK(out[i].status == JRQ_V2_OK);
+    CHECK(out[i].entry.type == EntryType::DATA && out[i].entry.id.index == 100 + i && out[i].entry.id.term == 7);
+    CHECK(out[i].corrupt == (i == 17));
+    CHECK(out[i].entry.hasChecksum() && (i == 17 || out[i].entry.getChecksum() == sums[i]));
+    CHECK(out[i].entry.checksum(eng) == sums[i]);  // the decoded bytes hash to the original
+  }
+}
+
+// Lease checks and ReadIndex rounds of many leader groups through LeaderTicker (one device
+// pass per tick) against the oracle's checkDeadNodes and closure replay on the same inputs.
+static void testLeaderTickerOnGpu(Engine& eng) {
+  const uint32_t G = 600, P = 5;
+  LeaderTicker lt(eng, G, P);
+  std::mt19937_64 rng(47);
+  std::vector<PeerId> ps;
+  for (uint32_t p = 0; p < 7; ++p) ps.emplace_back("10.2.0.1", static_cast<int32_t>(7000 + p));
+  const int64_t t0 = 1000000, lease = 900;
+  struct Exp { std::vector<int32_t> nids, oids; int32_t self; std::vector<int64_t> ts; std::vector<int> order; uint32_t okm = 0; };
+  std::vector<Exp> ex(G);
+  std::vector<int> verdict(G, -1);  // callback results: -1 none yet, 0 false, 1 true
+  for (uint32_t g = 0; g < G; ++g) {
+    Configuration c, o;
+    const uint32_t n = rng() % 2 ? 3 : 5;
+    for (uint32_t p = 0; p < n; ++p) c.peers.push_back(ps[p]);
+    const bool joint = g % 5 == 0;
+    if (joint) o.peers = {ps[0], ps[1], ps[2]};
+    lt.becomeLeader(g, c, joint ? &o : nullptr, ps[0], t0);
+    Exp& e = ex[g];
+    for (uint32_t p = 0; p < n; ++p) e.nids.push_back(static_cast<int32_t>(p));
+    if (joint) e.oids = {0, 1, 2};
+    e.self = 0;
+    e.ts.assign(P, t0);
+    for (uint32_t p = 1; p < n; ++p) {
+      const int64_t t = t0 + 2000 - static_cast<int64_t>(rng() % 2000);
+      lt.onRpcSent(g, ps[p], t);
+      e.ts[p] = t;
+    }
+    if (g % 3 == 0) {  // a ReadIndex round with some responses in a random order
+      lt.readIndex(g, [&verdict, g](bool ok) { verdict[g] = ok ? 1 : 0; });
+      std::vector<int> peers;
+      for (uint32_t p = 1; p < n; ++p) if (rng() % 4) peers.push_back(static_cast<int>(p));
+      std::shuffle(peers.begin(), peers.end(), rng);
+      for (int p : peers) {
+        const bool okr = rng() % 10 < 6;
+        lt.onHeartbeatResponse(g, ps[p], okr);
+        e.order.push_back(p);
+        if (okr) e.okm |= 1u << p;
+      }
+    }
+  }
+  std::vector<std::pair<uint32_t, uint16_t>> downs;
+  const int64_t now = t0 + 2000;
+  lt.tick(now, lease, [&](uint32_t g, uint16_t dead) { downs.emplace_back(g, dead); });
+  std::set<uint32_t> down;
+  for (auto& d : downs) down.insert(d.first);
+  for (uint32_t g = 0; g < G; ++g) {
+    const Exp& e = ex[g];
+    int64_t start = t0;
+    uint32_t dm = 0;
+    bool okn = jo_check_dead_nodes(e.nids.data(), static_cast<int32_t>(e.nids.size()), e.ts.data(), e.self, now, lease, &start, &dm);
+    bool oko = e.oids.empty() || jo_check_dead_nodes(e.oids.data(), static_cast<int32_t>(e.oids.size()), e.ts.data(), e.self, now, lease, &start, &dm);
+    const bool stepped = !(okn && oko);
+    CHECK(stepped == (down.count(g) != 0));
+    CHECK(lt.isLeader(g) == !stepped);
+    if (!stepped) CHECK(lt.lastLeaderTimestamp(g) == start);
+    if (g % 3 == 0) {
+      uint64_t order = 0;
+      for (size_t k = 0; k < e.order.size(); ++k) order |= static_cast<uint64_t>(k + 1) << (4 * e.order[k]);
+      uint32_t mask = 0;
+      for (int32_t p : e.nids) mask |= 1u << p;
+      const uint8_t r = jo_readindex_round(mask, P, 0, order, e.okm);
+      const int want = r == 1 ? 1 : r == 2 ? 0 : (stepped ? 0 : -1);
+      CHECK(verdict[g] == want);
+    } else {
+      CHECK(verdict[g] == -1);
+    }
+  }
+  CHECK(!downs.empty() && downs.size() < G);
+  // a second tick: the stepped-down groups are not checked again, the rest keep their lease
+  const size_t before = downs.size();
+  lt.tick(now, lease, [&](uint32_t g, uint16_t dead) { downs.emplace_back(g, dead); });
+  CHECK(downs.size() == before);
+}
+
 int main(int argc, char** argv) {
   // "gpu": with an engine (the real libjrq.so on the GPU box; the sanitizer builds link the
   // test double tests/cpp/fake_jrq.cpp instead and run the same list on the CPU)
@@ -990,6 +1183,9 @@ int main(int argc, char** argv) {
     tests.push_back({"testConfCacheSplit", [&] { testConfCacheSplit(e); }});
     tests.push_back({"testFastPathStepDown", [&] { testFastPathStepDown(e); }});
     tests.push_back({"testFreeSlotAckDuringAssign", [&] { testFreeSlotAckDuringAssign(e); }});
+    tests.push_back({"testFollowerVerifierOnGpu", [&] { testFollowerVerifierOnGpu(e); }});
+    tests.push_back({"testLogReaderOnGpu", [&] { testLogReaderOnGpu(e); }});
+    tests.push_back({"testLeaderTickerOnGpu", [&] { testLeaderTickerOnGpu(e); }});
   }
   for (auto& t : tests) {
     const int before = g_fail;
