@@ -1445,6 +1445,83 @@ std::vector<DecodedEntry> LogReader::decode(const std::vector<std::vector<uint8_
   return outv;
 }
 
+// --------------------------------------------------------------- FSM caller
+
+FSMCallerBatch::FSMCallerBatch(Engine& eng, uint32_t groups) : eng_(&eng), G_(groups) {
+  prev_.assign(G_, 0);
+  committed_.assign(G_, 0);
+  lastApplied_.assign(G_, 0);
+  cqFirst_.assign(G_, 0);
+  cqSize_.assign(G_, 0);
+  closures_.resize(G_);
+}
+
+void FSMCallerBatch::resetFirstIndex(uint32_t g, int64_t firstIndex) {
+  std::lock_guard<std::mutex> l(mu_);
+  if (!closures_[g].empty()) throw std::logic_error("resetFirstIndex on a non-empty ClosureQueue");  // :85-87
+  cqFirst_[g] = firstIndex;
+  cqSize_[g] = 0;
+}
+
+void FSMCallerBatch::appendPendingClosure(uint32_t g, std::function<void(bool)> done) {
+  std::lock_guard<std::mutex> l(mu_);
+  closures_[g].push_back(std::move(done));
+  cqSize_[g] = static_cast<int64_t>(closures_[g].size());
+}
+
+void FSMCallerBatch::setLastApplied(uint32_t g, int64_t lastApplied) {
+  std::lock_guard<std::mutex> l(mu_);
+  lastApplied_[g] = lastApplied;
+  prev_[g] = committed_[g] = std::max(committed_[g], lastApplied);
+}
+
+void FSMCallerBatch::onCommitted(uint32_t g, int64_t committedIndex) {
+  std::lock_guard<std::mutex> l(mu_);
+  if (committedIndex > committed_[g]) committed_[g] = committedIndex;
+}
+
+uint32_t FSMCallerBatch::doCommitted(const Apply& onApply, const std::function<void(uint32_t)>& onInvalid) {
+  struct Job {
+    uint32_t g;
+    int64_t first, last;
+    std::vector<std::function<void(bool)>> done;
+  };
+  std::vector<Job> jobs;
+  std::vector<uint32_t> invalid;
+  {
+    std::lock_guard<std::mutex> l(mu_);
+    std::vector<int64_t> first(G_), oldSize = cqSize_;
+    std::vector<uint8_t> status(G_);
+    std::vector<uint64_t> listed((G_ + 63) / 64);
+    uint32_t n = 0;
+    throwIfError(jrq_commit_fanout(eng_->raw(), G_, prev_.data(), committed_.data(), lastApplied_.data(),
+                                   cqFirst_.data(), cqSize_.data(), first.data(), status.data(),
+                                   listed.data(), &n),
+                 eng_->raw(), "jrq_commit_fanout");
+    for (size_t w = 0; w < listed.size(); ++w)
+      for (uint64_t b = listed[w]; b; b &= b - 1) {
+        const uint32_t g = static_cast<uint32_t>(w * 64 + static_cast<uint64_t>(__builtin_ctzll(b)));
+        if (status[g] == JRQ_FAN_INVALID) {
+          invalid.push_back(g);
+          continue;
+        }
+        Job j{g, lastApplied_[g] + 1, committed_[g], {}};
+        const int64_t popped = oldSize[g] - cqSize_[g];  // the kernel's pop, from the queue's front
+        for (int64_t k = 0; k < popped; ++k) {
+          j.done.push_back(std::move(closures_[g].front()));
+          closures_[g].pop_front();
+        }
+        lastApplied_[g] = committed_[g];
+        jobs.push_back(std::move(j));
+      }
+    prev_ = committed_;
+  }
+  for (auto& j : jobs) onApply(j.g, j.first, j.last, j.done);
+  if (onInvalid)
+    for (uint32_t g : invalid) onInvalid(g);
+  return static_cast<uint32_t>(jobs.size());
+}
+
 // ------------------------------------------------------------- leader tick
 
 LeaderTicker::LeaderTicker(Engine& eng, uint32_t groups, uint32_t peers)

@@ -208,6 +208,39 @@ class LogReader {
   Engine* eng_;
 };
 
+// --------------------------------------------------------------- FSM caller
+
+// The FSMCaller side of many groups (FSMCallerImpl.onCommitted / doCommitted, FSMCallerImpl.
+// java:239-244, 462-482, with each group's ClosureQueueImpl, ClosureQueueImpl.java:83-142): the
+// commits of an epoch are gated and their closures popped for every group by one device pass
+// (jrq_commit_fanout); the host then runs, per applying group, the popped closures and the
+// state machine over (lastApplied, committed].  A BallotBox's waiter feeds onCommitted.
+class FSMCallerBatch {
+ public:
+  // onApply(group, firstIndex, lastIndex, closures popped for [firstClosure, lastIndex])
+  using Apply = std::function<void(uint32_t group, int64_t first, int64_t last,
+                                   std::vector<std::function<void(bool)>>& closures)>;
+  FSMCallerBatch(Engine& eng, uint32_t groups);
+  // ClosureQueueImpl.resetFirstIndex (:83-92) when the node becomes leader; appendPendingClosure
+  // (:95-105) for each entry it appends (BallotBox.appendPendingTask)
+  void resetFirstIndex(uint32_t g, int64_t firstIndex);
+  void appendPendingClosure(uint32_t g, std::function<void(bool)> done);
+  void setLastApplied(uint32_t g, int64_t lastApplied);  // after loading a snapshot / at start
+  // FSMCallerImpl.onCommitted: the epoch's commit of the group (the largest one wins)
+  void onCommitted(uint32_t g, int64_t committedIndex);
+  // One doCommitted pass over every group with a new commit; returns the groups applied.
+  // onInvalid(g): popClosureUntil returned -1 ("Invalid firstClosureIndex").
+  uint32_t doCommitted(const Apply& onApply, const std::function<void(uint32_t)>& onInvalid = {});
+  int64_t lastApplied(uint32_t g) const { return lastApplied_[g]; }
+
+ private:
+  Engine* eng_;
+  uint32_t G_;
+  std::mutex mu_;
+  std::vector<int64_t> prev_, committed_, lastApplied_, cqFirst_, cqSize_;
+  std::vector<std::deque<std::function<void(bool)>>> closures_;
+};
+
 // ------------------------------------------------------------- leader tick
 
 // The leader-side timers of many Raft groups, decided for all of them by one device pass

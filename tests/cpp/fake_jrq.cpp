@@ -288,4 +288,26 @@ int jrq_leader_tick(jrq_engine*, const int64_t* ts, uint64_t ld, uint32_t P, con
   return JRQ_OK;
 }
 
+int jrq_commit_fanout(jrq_engine*, uint32_t G, const int64_t* prev, const int64_t* committed,
+                      const int64_t* last_applied, int64_t* cq_first, int64_t* cq_size,
+                      int64_t* first_out, uint8_t* status, uint64_t* listed, uint32_t* num_listed) {
+  std::vector<uint64_t> off(G + 1, 0);
+  std::vector<int64_t> seq;
+  for (uint32_t g = 0; g < G; ++g) {
+    if (committed[g] > prev[g]) seq.push_back(committed[g]);  // one onCommitted per moved group
+    off[g + 1] = seq.size();
+  }
+  std::vector<int64_t> la(last_applied, last_applied + G);
+  jo_commit_fanout_replay(G, off.data(), seq.data(), la.data(), cq_first, cq_size, first_out, status);
+  uint32_t n = 0;
+  for (uint32_t w = 0; w < (G + 63) / 64; ++w) listed[w] = 0;
+  for (uint32_t g = 0; g < G; ++g)
+    if (status[g] == JRQ_FAN_APPLY || status[g] == JRQ_FAN_INVALID) {
+      listed[g >> 6] |= 1ull << (g & 63);
+      ++n;
+    }
+  *num_listed = n;
+  return JRQ_OK;
+}
+
 }  // extern "C"

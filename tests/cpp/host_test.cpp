@@ -1141,6 +1141,68 @@ static void testLeaderTickerOnGpu(Engine& eng) {
   CHECK(downs.size() == before);
 }
 
+// FSMCallerImpl.doCommitted for many groups through FSMCallerBatch (one jrq_commit_fanout per
+// pass) against the oracle's call-by-call ClosureQueue / doCommitted replay: groups whose
+// commit did not move (or only a stale one arrived), commits below the queue's first index (no
+// closure popped), commits beyond the queue (INVALID), and ordinary pops.
+static void testFSMCallerBatchOnGpu(Engine& eng) {
+  const uint32_t G = 700;
+  FSMCallerBatch fc(eng, G);
+  std::mt19937_64 rng(53);
+  std::vector<int64_t> first(G), size(G), la(G), prev(G), com(G);
+  std::vector<std::vector<int>> ran(G);  // closure results per group, in run order
+  for (uint32_t g = 0; g < G; ++g) {
+    la[g] = 100 + static_cast<int64_t>(rng() % 50);
+    fc.setLastApplied(g, la[g]);
+    prev[g] = la[g];
+    first[g] = la[g] + 1 + static_cast<int64_t>(rng() % 3);
+    size[g] = static_cast<int64_t>(rng() % 20);
+    fc.resetFirstIndex(g, first[g]);
+    for (int64_t k = 0; k < size[g]; ++k)
+      fc.appendPendingClosure(g, [&ran, g, k](bool ok) { ran[g].push_back(ok ? static_cast<int>(k) : -1); });
+    const int kind = static_cast<int>(rng() % 6);
+    com[g] = kind == 0 ? prev[g]                                   // no commit
+             : kind == 1 ? la[g] - 1                              // stale: no onCommitted
+             : kind == 2 ? first[g] + size[g] + 5                 // beyond the queue: INVALID
+                         : first[g] + static_cast<int64_t>(rng() % (size[g] + 1));  // ordinary
+    if (com[g] > prev[g]) fc.onCommitted(g, com[g]);
+  }
+  std::vector<int> applied(G, 0), invalid(G, 0);
+  std::vector<std::pair<int64_t, int64_t>> range(G);
+  fc.doCommitted(
+      [&](uint32_t g, int64_t a, int64_t b, std::vector<std::function<void(bool)>>& done) {
+        applied[g] = 1;
+        range[g] = {a, b};
+        for (auto& d : done) d(true);
+      },
+      [&](uint32_t g) { invalid[g] = 1; });
+  // the oracle: one onCommitted per moved group, replayed call by call
+  std::vector<uint64_t> off(G + 1, 0);
+  std::vector<int64_t> seq;
+  for (uint32_t g = 0; g < G; ++g) {
+    if (com[g] > prev[g]) seq.push_back(com[g]);
+    off[g + 1] = seq.size();
+  }
+  std::vector<int64_t> ola = la, ofirst = first, osize = size, ofc(G);
+  std::vector<uint8_t> ost(G);
+  jo_commit_fanout_replay(G, off.data(), seq.data(), ola.data(), ofirst.data(), osize.data(), ofc.data(), ost.data());
+  int napply = 0, ninvalid = 0;
+  for (uint32_t g = 0; g < G; ++g) {
+    CHECK(applied[g] == (ost[g] == JRQ_FAN_APPLY));
+    CHECK(invalid[g] == (ost[g] == JRQ_FAN_INVALID));
+    napply += applied[g];
+    ninvalid += invalid[g];
+    const int64_t popped = size[g] - osize[g];
+    CHECK(static_cast<int64_t>(ran[g].size()) == popped);
+    for (int64_t k = 0; k < popped; ++k) CHECK(ran[g][static_cast<size_t>(k)] == static_cast<int>(k));
+    if (applied[g]) {
+      CHECK(range[g].first == la[g] + 1 && range[g].second == com[g]);
+      CHECK(fc.lastApplied(g) == ola[g]);
+    }
+  }
+  CHECK(napply > 100 && ninvalid > 20);
+}
+
 int main(int argc, char** argv) {
   // "gpu": with an engine (the real libjrq.so on the GPU box; the sanitizer builds link the
   // test double tests/cpp/fake_jrq.cpp instead and run the same list on the CPU)
@@ -1186,6 +1248,7 @@ int main(int argc, char** argv) {
     tests.push_back({"testFollowerVerifierOnGpu", [&] { testFollowerVerifierOnGpu(e); }});
     tests.push_back({"testLogReaderOnGpu", [&] { testLogReaderOnGpu(e); }});
     tests.push_back({"testLeaderTickerOnGpu", [&] { testLeaderTickerOnGpu(e); }});
+    tests.push_back({"testFSMCallerBatchOnGpu", [&] { testFSMCallerBatchOnGpu(e); }});
   }
   for (auto& t : tests) {
     const int before = g_fail;
