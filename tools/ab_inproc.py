@@ -106,6 +106,27 @@ def main():
                                    t["last_committed"], t["conf"], o, c3s)
             return f
         legs["C3"] = (mk_c3, lambda: torch.empty(1 << 20, dtype=torch.int64, device=dev))
+    if "C3K" in legs_env:  # 8 epochs of C3 per launch (jrq_quorum_epochs_dev)
+        sk = W.quorum_epoch_series("C3", 8)
+        dk = {kk: dev_t(np.ascontiguousarray(v)) for kk, v in sk.items()}
+        skst = torch.empty((8, 1 << 20), dtype=torch.uint8, device=dev)
+
+        def mk_c3k(e, o):
+            return lambda: e.quorum_epochs_dev(dk["match"], dk["pending_index"], dk["last_appended"],
+                                               dk["last_committed"], dk["conf"], o, skst)
+        legs["C3K"] = (mk_c3k, lambda: torch.empty((8, 1 << 20), dtype=torch.int64, device=dev))
+    for kk_, KE in (("C2K256", 256), ("C2K64", 64)):  # configs[1], KE epochs per launch
+        if kk_ not in legs_env:
+            continue
+        s2 = W.quorum_epoch_series("C2", KE)
+        d2 = {kk: dev_t(np.ascontiguousarray(v)) for kk, v in s2.items()}
+        G2 = d2["pending_index"].shape[0]
+        st2 = torch.empty((KE, G2), dtype=torch.uint8, device=dev)
+
+        def mk_c2k(e, o, d2=d2, st2=st2):
+            return lambda: e.quorum_epochs_dev(d2["match"], d2["pending_index"], d2["last_appended"],
+                                               d2["last_committed"], d2["conf"], o, st2)
+        legs[kk_] = (mk_c2k, lambda KE=KE, G2=G2: torch.empty((KE, G2), dtype=torch.int64, device=dev))
     if "C5f" in legs_env:  # the C5 entries (16 KiB each) through the fixed-size entry point
         def mk_c5f(e, o):
             cor = torch.empty(n5, dtype=torch.uint8, device=dev)
