@@ -323,23 +323,29 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
 // half-wave a chunk of C epochs of them -- and a scan over the chunk maxima in LDS stitches
 // the prefix.  Loads stay coalesced (32 consecutive groups = 256 B per row and epoch); small
 // tiles spread a 10k-group batch over all 256 CUs.
-// A chunk = C epochs of the tile's T groups on T lanes (T = 32: two chunks per wave), at most
-// W waves per workgroup, super-chunks beyond that.  Product shape (EpochChunk): C epochs per
-// half-wave (16 loads of P+1 words per lane at P = 3), 8 waves: a 10k-group batch is 313
-// workgroups, all resident at once (2 per CU) -- a 16-wave workgroup fits once per CU and left
-// a second, partial round of workgroups (13.5 vs 8.8 us).
-template <int P>
+// A chunk = C epochs of the tile's T groups on T lanes, at most W waves per workgroup,
+// super-chunks beyond that.  Product shape (EpochChunk, r05): tiles of T = 16 groups (a
+// quarter-wave chunk still loads whole 128-B lines: 16 groups x 8 B per row and epoch), at most
+// 4 waves, and 16 loads per lane (C = 4 epochs at P = 3) -- or 32 (C = 8) for a launch of 192+
+// epochs, whose workgroups then walk half as many super-chunks.  In-process A/B on the GPU
+// (tools/ab_inproc.py, profiles/r05e_ab_epochs_shapes.log), C2 at 256 / 64 epochs per launch:
+// round 4's T = 32, 8 waves, C = 4: 26.1 / 8.3 us; T = 16, 4 waves, C = 4: 24.5 / 7.4;
+// C = 8: 22.8 / 8.8 (so C = 8 only for long launches); 2 or 8 waves, T = 32 with 16 waves: all
+// slower.
+template <int P, bool kDeep>
 struct EpochChunk {
-  static constexpr int kC = (16 / (P + 1)) < 1 ? 1 : ((16 / (P + 1)) > 8 ? 8 : 16 / (P + 1));
-  static constexpr int kMaxWaves = 8;
-  static constexpr int kTile = 32;  // groups per workgroup
+  static constexpr int kLoads = kDeep ? 32 : 16;
+  static constexpr int kC = (kLoads / (P + 1)) < 1 ? 1 : ((kLoads / (P + 1)) > 8 ? 8 : kLoads / (P + 1));
+  static constexpr int kMaxWaves = 4;
+  static constexpr int kTile = 16;  // groups per workgroup
 };
+constexpr uint32_t kEpochsDeepK = 192;  // epochs per launch from which EpochChunk<P, true> runs
 
 template <int P, int C, int T, int W>
 __global__ __launch_bounds__(64 * W) void quorum_epochs_kernel(JrqQuorumArgs a, uint32_t K,
                                                                uint64_t match_eld,
                                                                uint64_t la_eld) {
-  static_assert(T == 32 || T == 64, "a chunk is a half or a whole wave");
+  static_assert(T == 16 || T == 32 || T == 64, "a chunk is a quarter, a half or a whole wave");
   constexpr uint32_t kPerWave = 64 / T;
   __shared__ int64_t chunk_max[kPerWave * W][T];
   const uint32_t lane = threadIdx.x & 63u;
@@ -974,23 +980,28 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum_ep
     }
     return hipGetLastError();
   }
-  // otherwise one workgroup per tile of groups; chunks of C epochs (two per wave), at most W
+  // otherwise one workgroup per tile of groups; chunks of C epochs (four per wave), at most W
   // waves, super-chunks beyond that
+  const bool deep = K >= jrq::kEpochsDeepK;
   switch (args->num_peers) {
-#define JRQ_CASE(P)                                                                           \
-  case P: {                                                                                   \
-    using E = jrq::EpochChunk<P>;                                                             \
+#define JRQ_LAUNCH(P, D)                                                                      \
+  {                                                                                           \
+    using E = jrq::EpochChunk<P, D>;                                                          \
     const dim3 grid(static_cast<unsigned>((static_cast<uint64_t>(args->G) + E::kTile - 1) /   \
                                           E::kTile));                                         \
     const uint32_t w = jrq_epochs_waves(K, E::kC, E::kTile, E::kMaxWaves);                    \
     hipLaunchKernelGGL((jrq::quorum_epochs_kernel<P, E::kC, E::kTile, E::kMaxWaves>), grid,   \
                        dim3(64u * w), 0, stream, *args, K, match_eld, la_eld);                \
-    break;                                                                                    \
   }
+#define JRQ_CASE(P)                                                                           \
+  case P:                                                                                     \
+    if (deep) JRQ_LAUNCH(P, true) else JRQ_LAUNCH(P, false)                                   \
+    break;
     JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
     JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
     JRQ_CASE(15) JRQ_CASE(16)
 #undef JRQ_CASE
+#undef JRQ_LAUNCH
     default:
       return hipErrorInvalidValue;
   }

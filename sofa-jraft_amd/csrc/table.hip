@@ -14,8 +14,9 @@
 //                        (pendingIndex becomes JRQ_PI_FOLLOWS_LC once), and the group is
 //                        listed in its wave's fixed slice of the changed list.
 //   table_list_*         host variant only: the slices gathered back to back.
-// HBM per group per epoch: reads match 8P + pendingIndex, lastAppended, lastCommitted, conf
-// 32 B; writes 8 B lastCommitted + 8 B list entry per committing group.
+// HBM per group per epoch: reads match 4P (u32 words against the group's match base) +
+// pendingIndex, lastAppended, lastCommitted, conf 32 B; writes 8 B lastCommitted + 4 B list
+// delta per committing group, 36 B of map + count per 256 groups.
 #include "quorum_core.h"
 
 namespace jrq {

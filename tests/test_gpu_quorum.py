@@ -162,7 +162,8 @@ def _series_oracle(s, K):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg,G,K", [("C2", 1000, 7), ("C3", 3000, 9), ("C2", 1, 1),
-                                     ("C2", 10_000, 64)])
+                                     ("C2", 10_000, 64), ("C2", 10_000, 256), ("C3", 3000, 300),
+                                     ("C2", 33, 129)])
 def test_gpu_quorum_epochs_series_vs_oracle(engine, cfg, G, K):
     """K epochs in one launch == K sequential BallotBox replays with carried state."""
     import torch
@@ -183,6 +184,44 @@ def test_gpu_quorum_epochs_series_vs_oracle(engine, cfg, G, K):
     assert np.array_equal(st.cpu().numpy(), se)
     if K > 1:
         assert (ce[-1] > ce[0]).any()  # commits actually move across epochs
+
+
+@pytest.mark.gpu
+def test_gpu_quorum_epochs_lookback_relaunch(engine):
+    """The look-back shape (quorum_epochs_lb_kernel: batches under 8 tiles per CU with more than
+    one segment of epochs) over a sequence of launches on one engine: growing and shrinking
+    grids (its workspace reallocated, generation stamps carried), a grid of ~15k workgroups --
+    far more than are resident at once, so segments wait on workgroups that finished long ago --
+    and repeated launches of one batch that must give identical results.  Groups are checked
+    against the oracle on a sample of columns (each group's epochs are independent of the
+    others')."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(11)
+    first = {}
+    for rep, (G, K) in enumerate([(10_000, 256), (60_000, 512), (500, 100), (10_000, 256),
+                                  (60_000, 512), (10_000, 256)]):
+        s = W.quorum_epoch_series("C2", K, groups=G)
+        s["pending_index"][::89] = 0
+        t = {k: torch.from_numpy(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v)).to(dev)
+             for k, v in s.items()}
+        c = torch.empty((K, G), dtype=torch.int64, device=dev)
+        st = torch.empty((K, G), dtype=torch.uint8, device=dev)
+        engine.quorum_epochs_dev(t["match"], t["pending_index"], t["last_appended"],
+                                 t["last_committed"], t["conf"], c, st)
+        engine.synchronize()
+        got_c, got_s = c.cpu().numpy(), st.cpu().numpy()
+        if (G, K) in first:
+            assert np.array_equal(got_c, first[(G, K)][0]) and np.array_equal(got_s, first[(G, K)][1])
+            continue
+        first[(G, K)] = (got_c, got_s)
+        sub = np.sort(rng.choice(G, min(G, 96), replace=False))
+        ss = {"match": s["match"][:, :, sub], "last_appended": s["last_appended"][:, sub],
+              "pending_index": s["pending_index"][sub], "last_committed": s["last_committed"][sub],
+              "conf": s["conf"][sub]}
+        ce, se = _series_oracle(ss, K)
+        assert np.array_equal(got_c[:, sub], ce), (G, K)
+        assert np.array_equal(got_s[:, sub], se), (G, K)
 
 
 def _to_dev(b, keys):
