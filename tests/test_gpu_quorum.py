@@ -187,14 +187,12 @@ def test_gpu_quorum_epochs_series_vs_oracle(engine, cfg, G, K):
 
 
 @pytest.mark.gpu
-def test_gpu_quorum_epochs_lookback_relaunch(engine):
-    """The look-back shape (quorum_epochs_lb_kernel: batches under 8 tiles per CU with more than
-    one segment of epochs) over a sequence of launches on one engine: growing and shrinking
-    grids (its workspace reallocated, generation stamps carried), a grid of ~15k workgroups --
-    far more than are resident at once, so segments wait on workgroups that finished long ago --
-    and repeated launches of one batch that must give identical results.  Groups are checked
-    against the oracle on a sample of columns (each group's epochs are independent of the
-    others')."""
+def test_gpu_quorum_epochs_relaunch_sequence(engine):
+    """jrq_quorum_epochs_dev over a sequence of launch shapes on one engine: both chunk depths
+    (C = 4 below 192 epochs per launch, C = 8 from there), batches of 313 to 3750 tiles of 16
+    groups (the larger ones with many super-chunks per workgroup), and repeated launches of one
+    batch that must give identical results.  Groups are checked against the oracle on a sample
+    of columns (each group's epochs are independent of the others')."""
     import torch
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(11)
