@@ -60,11 +60,25 @@ def crc_bytes(n_entries: int, payload_bytes: int, verify: bool = True, offsets: 
 
 
 def to_dev(arr, dev):
+    """A device copy of numpy `arr`, staged through page-locked host memory: the bench hands no
+    pageable memory to a HIP copy.  HIP locks the pages of a large pageable copy itself and may
+    keep them locked after the copy; an array freed afterwards and a later allocation at the
+    same address then meet a lock over pages that no longer exist -- rounds 4 and 5 each saw one
+    run end in "illegal memory access" at a result copy of the lease leg, after the C5 / C1 legs'
+    GiB-sized pageable transfers (profiles/faults/)."""
     import torch
     if arr is None:
         return None
     a = arr.view(np.int64) if arr.dtype == np.uint64 else arr
-    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(dev)
+
+
+def host_np(t):
+    """numpy copy of device tensor `t` through page-locked host memory (see to_dev)."""
+    import torch
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t)
+    return h.numpy()
 
 
 # ------------------------------------------------------------------ PMC citations --
@@ -520,7 +534,7 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
         ce, _, _ = O.quorum_epoch_replay(b["match"][:, idx], b["pending_index"][idx],
                                          b["last_appended"][idx], b["last_committed"][idx],
                                          b["conf"][idx], chunk=1024)
-        ok = bool(np.array_equal(local.cpu().numpy()[idx], ce))
+        ok = bool(np.array_equal(host_np(local)[idx], ce))
     bpg = quorum_bytes_per_group(P)
     rl = roofline(bpg * G, k_ms, kernel="quorum_epoch_pair_kernel<5, false, true>", bytes_per_group=bpg,
                   survey_bytes_per_group=8 * P + 38,
@@ -657,7 +671,7 @@ def leg_table(ctx, args, G, pair_ms):
         eng.quorum_epoch_dev(d["match"], d["pending_index"], d["last_appended"],
                              d["last_committed"], d["conf_a"], pcs[i], pst)
     p_ms = series_ms(pristine, pair)  # (the table copies run too: the same cache state)
-    pc_flagged = [x.cpu().numpy() for x in pcs]
+    pc_flagged = [host_np(x) for x in pcs]
     pp_ms = series_ms(pristine, pair_plain)
     ok = True
     for i in range(NB):  # table == stateless kernel, every group of every table
@@ -738,7 +752,7 @@ def leg_drive(ctx, args, G):
                                       d["last_committed"], d["conf"], c, cs, run_off=d["run_off"],
                                       run_start=d["run_start"], run_conf=d["run_conf"])
             ctx.sync()
-            ok = bool(np.array_equal(committed, c.cpu().numpy()))
+            ok = bool(np.array_equal(committed, host_np(c)))
             del d, c, cs
         sl = slice(1, K)
         f = float(np.mean(st["flush_ms"][sl]))
@@ -835,7 +849,7 @@ def leg_c2(ctx, args):
         sub = np.random.default_rng(2).choice(G2, 128, replace=False)
         pi = ser["pending_index"][sub].copy()
         lc = ser["last_committed"][sub].copy()
-        got = kc.cpu().numpy()
+        got = host_np(kc)
         ok = True
         for k in range(KE):
             ce, _, _ = O.quorum_epoch_replay(ser["match"][k][:, sub], pi,
@@ -852,7 +866,7 @@ def leg_c2(ctx, args):
             "entry_ballots_per_s": G2 * 1024 / (one_ms * 1e-3),
             "batched_epochs": {"epochs_per_launch": KE, "kernel_ms": k_ms,
                                "decisions_per_s": G2 * KE / (k_ms * 1e-3),
-                               "roofline": roofline(alg, k_ms, kernel="quorum_epochs_kernel<3>",
+                               "roofline": roofline(alg, k_ms, kernel="quorum_epochs_kernel<3, 8, 16, 4>",
                                                     **pmc_traffic("C2", "quorum_epochs_kernel<3,")),
                                "bit_exact_vs_oracle_128_groups": ok}}
 
@@ -882,7 +896,7 @@ def leg_c2l(ctx, args):
         sub = np.random.default_rng(3).choice(G2, 64, replace=False)
         pi = serl["pending_index"][sub].copy()
         lc = serl["last_committed"][sub].copy()
-        got = klc.cpu().numpy()
+        got = host_np(klc)
         ok_l = True
         for k in range(KL):
             ce, _, _ = O.quorum_epoch_replay(serl["match"][k][:, sub], pi,
@@ -895,7 +909,7 @@ def leg_c2l(ctx, args):
     del serl_d, klc, kls
     return {"epochs_per_launch": KL, "kernel_ms": kl_ms,
             "decisions_per_s": G2 * KL / (kl_ms * 1e-3),
-            "roofline": roofline(alg_l, kl_ms, kernel="quorum_epochs_kernel<3>",
+            "roofline": roofline(alg_l, kl_ms, kernel="quorum_epochs_kernel<3, 4, 16, 4>",
                                  **pmc_traffic("C2L", "quorum_epochs_kernel<3,")),
             "bit_exact_vs_oracle_64_groups": ok_l}
 
@@ -922,7 +936,7 @@ def leg_c3k(ctx, args, G):
         sub = np.random.default_rng(4).choice(G, 2048, replace=False)
         pi = ser["pending_index"][sub].copy()
         lc = ser["last_committed"][sub].copy()
-        got, gst = kc.cpu().numpy(), ks.cpu().numpy()
+        got, gst = host_np(kc), host_np(ks)
         ok = True
         for k in range(K):
             ce, se, _ = O.quorum_epoch_replay(ser["match"][k][:, sub], pi,
@@ -939,9 +953,9 @@ def leg_c3k(ctx, args, G):
     return {"workload": f"C3: {G} groups x {P} peers, joint, {K} successive epochs per launch",
             "epochs_per_launch": K, "kernel_ms": ms,
             "decisions_per_s": G * K / (ms * 1e-3),
-            "roofline": roofline(alg, ms, kernel="quorum_epochs_kernel<5>",
+            "roofline": roofline(alg, ms, kernel="quorum_epochs_pair_kernel<5>",
                                  bytes_note="8P+17 B per group-epoch + 24 B per group",
-                                 **pmc_traffic("C3K", "quorum_epochs_kernel<5,")),
+                                 **pmc_traffic("C3K", "quorum_epochs_pair_kernel<5>")),
             "bit_exact_vs_oracle_2048_groups": ok}
 
 
@@ -1072,8 +1086,8 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
     vo_ms, _ = ctx.timed(verify_offsets, steps, 2)
     ok_off = None
     if checks:
-        ok_off = bool(np.array_equal(out.cpu().numpy().view(np.uint64), expected)) and \
-            bool(np.array_equal(corrupt.cpu().numpy().astype(bool), flip))
+        ok_off = bool(np.array_equal(host_np(out).view(np.uint64), expected)) and \
+            bool(np.array_equal(host_np(corrupt).astype(bool), flip))
     v_ms, _ = ctx.timed(verify, steps, 2)
     c_ms, _ = ctx.timed(commit, steps, 2)
     s_ms, _ = ctx.timed(step, steps, 2)
@@ -1082,12 +1096,12 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
     pay = n * c5["entry_bytes"]
     ok = step_ok = None
     if checks:
-        ok = bool(np.array_equal(out.cpu().numpy().view(np.uint64), expected)) and \
-            bool(np.array_equal(corrupt.cpu().numpy().astype(bool), flip))
+        ok = bool(np.array_equal(host_np(out).view(np.uint64), expected)) and \
+            bool(np.array_equal(host_np(corrupt).astype(bool), flip))
         ce, se, _ = O.quorum_epoch_replay(qb["match"], qb["pending_index"], qb["last_appended"],
                                           qb["last_committed"], qb["conf"], chunk=1024)
-        step_ok = ok and bool(np.array_equal(qc.cpu().numpy(), ce)) and \
-            bool(np.array_equal(qs.cpu().numpy(), se))
+        step_ok = ok and bool(np.array_equal(host_np(qc), ce)) and \
+            bool(np.array_equal(host_np(qs), se))
     alg_v = crc_bytes(n, pay, verify=True, offsets=False)
     alg_c = quorum_bytes_per_group(3) * n
     per_rank_ms = ctx.gather(v_ms)
@@ -1143,8 +1157,8 @@ def leg_ae(ctx, args, c5state):
     ms, _ = ctx.timed(ae_step, max(10, args.steps), 2)
     ok = None
     if ctx.oracle_checks:
-        ok = bool(np.array_equal(ae_out.cpu().numpy().view(np.uint64), expected)) and \
-            bool((ae_first.cpu().numpy() == 0).all())  # entry 0 of each request is flipped
+        ok = bool(np.array_equal(host_np(ae_out).view(np.uint64), expected)) and \
+            bool((host_np(ae_first) == 0).all())  # entry 0 of each request is flipped
     pay = n * c5["entry_bytes"]
     # payload + per entry term 8, type 1, data_len 8, stored checksum 8, checksum out 8, corrupt
     # 1 + per request req_off 4, prevLogIndex 8, first corrupt 4 (scratch offsets / indices not
@@ -1171,7 +1185,7 @@ def leg_v2(ctx, args, c5state):
     ck = expected ^ flip.astype(np.uint64)
     rec_np, lens = W.v2_records(eb["etype"], eb["index"], eb["term"], eb["payload"],
                                 eb["offsets"], ck)
-    d_rec = torch.from_numpy(rec_np).to(dev)
+    d_rec = to_dev(rec_np, dev)
     d_roff = to_dev(lens, dev)
     v2_out = {k: torch.empty(n, dtype={np.uint8: torch.uint8, np.uint32: torch.int32}.get(t, torch.int64),
                              device=dev) for k, t in Engine.V2_FIELDS}
@@ -1179,17 +1193,17 @@ def leg_v2(ctx, args, c5state):
     def v2_step(i):
         eng.v2_decode_verify_dev(d_rec, d_roff, v2_out)
     ms, _ = ctx.timed(v2_step, max(10, args.steps), 2)
-    cor = v2_out["corrupt"].cpu().numpy().astype(bool)
+    cor = host_np(v2_out["corrupt"]).astype(bool)
     ok = None  # the stored checksums are the oracle's: nothing to compare without it
     if ctx.oracle_checks:
-        ok = bool((v2_out["status"].cpu().numpy() == 0).all()) and bool(np.array_equal(cor, flip))
-        ok = ok and bool(np.array_equal(v2_out["computed"].cpu().numpy().view(np.uint64), expected))
+        ok = bool((host_np(v2_out["status"]) == 0).all()) and bool(np.array_equal(cor, flip))
+        ok = ok and bool(np.array_equal(host_np(v2_out["computed"]).view(np.uint64), expected))
     sample_ok = None
     if ctx.oracle_checks:  # the oracle decoder on the first 512 records
         import jraft_oracle as O
         m = 512
         so = O.v2_decode_batch(rec_np[:int(lens[m])], lens[:m + 1])
-        sample_ok = bool(np.array_equal(so["computed"], v2_out["computed"].cpu().numpy()[:m].view(np.uint64)))
+        sample_ok = bool(np.array_equal(so["computed"], host_np(v2_out["computed"])[:m].view(np.uint64)))
     tot = int(lens[-1])
     alg = tot + 8 * (n + 1) + 56 * n
     return {"workload": f"{n} stored V2 records (C5 entries, 16 KiB data + header + checksum "
@@ -1225,17 +1239,17 @@ def leg_snapshot(ctx, args, c5state):
         import jraft_oracle as O
         reg1.zero_()
         eng.crc64_stream_update_dev(reg1, pay_u8, one_off)
-        whole = int(reg1.cpu().numpy().view(np.uint64)[0])
+        whole = int(host_np(reg1).view(np.uint64)[0])
         reg1.zero_()
         for a in range(0, tot_b, 64 << 20):
             eng.crc64_stream_update_dev(
                 reg1, pay_u8, torch.tensor([a, min(tot_b, a + (64 << 20))], dtype=torch.int64,
                                            device=dev))
-        chained = int(reg1.cpu().numpy().view(np.uint64)[0])
+        chained = int(host_np(reg1).view(np.uint64)[0])
         pre = 16 << 20
         reg1.zero_()
         eng.crc64_stream_update_dev(reg1, pay_u8, torch.tensor([0, pre], dtype=torch.int64, device=dev))
-        got_pre = int(reg1.cpu().numpy().view(np.uint64)[0])
+        got_pre = int(host_np(reg1).view(np.uint64)[0])
         ok = whole == chained and got_pre == O.crc64(eb["payload"][:pre].tobytes())
     return {"workload": f"C5 payload ({tot_b >> 20} MiB) as (a) one snapshot archive stream, "
                         f"(b) {n} region streams x 16 KiB chunks (CRC64.update on resident registers)",
@@ -1284,15 +1298,15 @@ def leg_c1(ctx, args):
         import jraft_oracle as O
         exp1 = O.logentry_checksum_batch(e1["etype"], e1["index"], e1["term"], None,
                                          e1["payload"], e1["offsets"])
-        ok_off = bool(np.array_equal(out1.cpu().numpy().view(np.uint64), exp1))
+        ok_off = bool(np.array_equal(host_np(out1).view(np.uint64), exp1))
     crc_ms, _ = ctx.timed(crc, max(10, args.steps), 2)
     ms, _ = ctx.timed(step, max(10, args.steps), 2)
     ok = None
     if ctx.oracle_checks:
         ce, se, _ = O.quorum_epoch_replay(q1["match"], q1["pending_index"], q1["last_appended"],
                                           q1["last_committed"], q1["conf"], chunk=1024)
-        ok = bool(np.array_equal(out1.cpu().numpy().view(np.uint64), exp1)) and \
-            bool(np.array_equal(c1c.cpu().numpy(), ce))
+        ok = bool(np.array_equal(host_np(out1).view(np.uint64), exp1)) and \
+            bool(np.array_equal(host_np(c1c), ce))
     alg = crc_bytes(n1, n1 * c1["entry_bytes"], verify=False, offsets=False)
     return {"workload": "C1: 1 group x 3 peers, 1M appended 256-B LogEntries: checksum + commitAt",
             "ms_per_step": ms, "entries_per_s": n1 / (ms * 1e-3),
@@ -1334,11 +1348,11 @@ def leg_lease(ctx, args, quorum_conf_dev, G, P):
         lead.zero_()
         step(0)
         ctx.sync()
-        eok, elead, edead = O.lease_check(ts_bufs[0].cpu().numpy(), quorum_conf_dev.cpu().numpy().view(np.uint64),
+        eok, elead, edead = O.lease_check(host_np(ts_bufs[0]), host_np(quorum_conf_dev).view(np.uint64),
                                           np.zeros(G, np.uint8), now_ms, lease_to, np.zeros(G, np.int64))
-        ok = bool(np.array_equal(lok.cpu().numpy(), eok)) and \
-            bool(np.array_equal(lead.cpu().numpy(), elead)) and \
-            bool(np.array_equal(ldead.cpu().numpy().view(np.uint16), edead))
+        ok = bool(np.array_equal(host_np(lok), eok)) and \
+            bool(np.array_equal(host_np(lead), elead)) and \
+            bool(np.array_equal(host_np(ldead).view(np.uint16), edead))
     lb = (8 * P + 28) * G
     return {"workload": f"{G} leader groups x {P} peers (conf + old conf), checkDeadNodes0",
             "decisions_per_s": G / (ms * 1e-3), "kernel_ms": ms, "bit_exact_vs_oracle": ok,
@@ -1376,7 +1390,7 @@ def leg_readindex(ctx, args, quorum_conf_dev, quorum_conf, G, P):
         step(0)
         ctx.sync()
         exp = O.readindex_quorum(quorum_conf, self_np, bufs[0][0], bufs[0][1], P)
-        got = res.cpu().numpy()
+        got = host_np(res)
         ok = bool(np.array_equal(got, exp))
         counts = {k: int((exp == v).sum()) for k, v in (("pending", 0), ("success", 1), ("failure", 2))}
     rb = 20 * G  # conf 8 + order 8 + ok mask 2 + self slot 1 read, verdict 1 written
@@ -1423,10 +1437,10 @@ def leg_tick(ctx, args, quorum_conf_dev, quorum_conf, G, P):
         eok, elead, edead = O.lease_check(b["ts"], quorum_conf, self_np, now_ms, lease_to,
                                           np.zeros(G, np.int64))
         eri = O.readindex_quorum(quorum_conf, self_np, b["order"], b["okm"], P)
-        ok = bool(np.array_equal(lok.cpu().numpy(), eok)) and \
-            bool(np.array_equal(lead.cpu().numpy(), elead)) and \
-            bool(np.array_equal(ldead.cpu().numpy().view(np.uint16), edead)) and \
-            bool(np.array_equal(ri.cpu().numpy(), eri))
+        ok = bool(np.array_equal(host_np(lok), eok)) and \
+            bool(np.array_equal(host_np(lead), elead)) and \
+            bool(np.array_equal(host_np(ldead).view(np.uint16), edead)) and \
+            bool(np.array_equal(host_np(ri), eri))
     # per group: timestamps 8P + conf 8 + self 1 + lease start 8 read, 8 written + ok 1 + dead 2
     # (the lease check, 8P + 28) + order 8 + ok mask 2 read, verdict 1 written (ReadIndex, 11)
     tb = (8 * P + 39) * G
@@ -1499,15 +1513,15 @@ def leg_fanout(ctx, args, G):
         launch(fan_sets[0])
         ctx.sync()
         f = fan_sets[0]
-        prev_c, c = f["prev"].cpu().numpy(), f["c"].cpu().numpy()
+        prev_c, c = host_np(f["prev"]), host_np(f["c"])
         adv = c > prev_c
         seq_off = np.zeros(G + 1, np.uint64)
         seq_off[1:] = np.cumsum(adv)
-        est, efc, _, ecf, ecs, _ = O.commit_fanout_replay(seq_off, c[adv], f["la"].cpu().numpy(),
-                                                          f["cf0"].cpu().numpy(), f["cs0"].cpu().numpy())
-        ok = bool(np.array_equal(fan_st.cpu().numpy(), est)) and \
-            bool(np.array_equal(fan_fc.cpu().numpy(), efc)) and \
-            bool(np.array_equal(f["cf"].cpu().numpy(), ecf)) and bool(np.array_equal(f["cs"].cpu().numpy(), ecs))
+        est, efc, _, ecf, ecs, _ = O.commit_fanout_replay(seq_off, c[adv], host_np(f["la"]),
+                                                          host_np(f["cf0"]), host_np(f["cs0"]))
+        ok = bool(np.array_equal(host_np(fan_st), est)) and \
+            bool(np.array_equal(host_np(fan_fc), efc)) and \
+            bool(np.array_equal(host_np(f["cf"]), ecf)) and bool(np.array_equal(host_np(f["cs"]), ecs))
     # reads prev/committed/lastApplied/cqFirst/cqSize 40 B, writes firstClosure 8 + status 1
     # + the listed bitmap 1/8; + 16 B queue write-back per popping group
     fb = 49 * G + G // 8 + 16 * n_pop

@@ -131,9 +131,10 @@ void *jrq_get_stream(jrq_engine *e);
 int jrq_set_stream(jrq_engine *e, void *hip_stream);
 int jrq_synchronize(jrq_engine *e);
 /* Page-lock a host buffer (e.g. a DirectByteBuffer's address) for fast staging.  Host
- * variants (the functions without _dev) DMA registered input memory straight to the device;
- * other input memory goes through the engine's two pinned 8 MiB bounce chunks (a CPU copy
- * overlapped with the previous chunk's DMA).
+ * variants (the functions without _dev) DMA registered memory straight to and from the device;
+ * other caller memory, inputs and outputs alike, goes through the engine's two pinned 8 MiB
+ * bounce chunks (a CPU copy overlapped with the other chunk's DMA): libjrq never hands pageable
+ * memory to a HIP copy.
  * The driver pins whole pages, so registrations are tracked by page: a range sharing a page
  * with a live jrq_host_register / jrq_host_alloc range is refused with JRQ_E_STATE and nothing
  * is pinned (its uploads still work, through the bounce chunks).  Page-aligned buffers of
@@ -163,7 +164,8 @@ typedef enum {
     JRQ_DBG_CRC_PRIO = 3,        /* progress-stepped wave priority steps, 0..3 (default 1) */
     JRQ_DBG_CRC_SEG_MAP = 4,     /* 1 contiguous chunks per workgroup (default), 0 interleaved */
     JRQ_DBG_UPLOAD_PAGEABLE = 5  /* 1: host variants hand unregistered caller memory to HIP's
-                                    pageable copy instead of the pinned bounce chunks */
+                                    pageable copies (uploads and result downloads) instead of the
+                                    pinned bounce chunks */
 } jrq_debug_option;
 int jrq_debug_set(jrq_engine *e, int option, int64_t value);
 

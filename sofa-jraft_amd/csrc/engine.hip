@@ -84,7 +84,7 @@ struct jrq_engine {
   bool upload_pageable = false;  // JRQ_DBG_UPLOAD_PAGEABLE: hand caller pages to HIP's own copy
   uint32_t max_groups = 0;
   uint8_t max_peers = 0;
-  DevBuf stage[27];  // 0-13 host-variant staging, 14 stream-update chunk CRCs, 15 fixed-size offsets, 16-19 AppendEntries scratch, 21-26 V2 decode scratch
+  DevBuf stage[27];  // 0-13 host-variant staging, 14 stream-update chunk CRCs, 15 fixed-size offsets, 16-19 AppendEntries scratch, 20 jrq_table_read de-tiling, 21-26 V2 decode scratch
   // pinned bounce buffers for the host variants' uploads (stage_in): two chunks, each
   // reusable once the copy recorded after it has run
   uint8_t* bounce[2] = {nullptr, nullptr};
@@ -207,12 +207,17 @@ int ensure_stage(jrq_engine* e, int slot, size_t bytes, void** out) {
 // pinning of caller pages at all.  JRQ_DBG_UPLOAD_PAGEABLE selects HIP's copy for A/B runs.)
 constexpr size_t kBounceChunk = size_t(8) << 20;
 
-int upload(jrq_engine* e, void* dst, const void* src, size_t bytes) {
+int ensure_bounce(jrq_engine* e) {
   for (int i = 0; i < 2; ++i)
     if (!e->bounce[i]) {
       JRQ_HIP(e, hipHostMalloc(reinterpret_cast<void**>(&e->bounce[i]), kBounceChunk, hipHostMallocDefault));
       JRQ_HIP(e, hipEventCreateWithFlags(&e->bounce_done[i], hipEventDisableTiming));
     }
+  return JRQ_OK;
+}
+
+int upload(jrq_engine* e, void* dst, const void* src, size_t bytes) {
+  if (int rc = ensure_bounce(e)) return rc;
   int i = 0;
   for (size_t off = 0; off < bytes; off += kBounceChunk, i ^= 1) {
     const size_t n = bytes - off < kBounceChunk ? bytes - off : kBounceChunk;
@@ -223,6 +228,41 @@ int upload(jrq_engine* e, void* dst, const void* src, size_t bytes) {
     JRQ_HIP(e, hipEventRecord(e->bounce_done[i], e->stream));
     e->bounce_busy[i] = true;
   }
+  return JRQ_OK;
+}
+
+// Device -> host into caller memory that is not page-locked: through the same bounce chunks
+// (the DMA into one chunk overlaps the CPU copy out of the other), so that no HIP copy ever
+// touches pageable memory.  HIP's pageable copies lock the caller's pages themselves and may
+// keep them locked after the copy returns; a buffer the caller frees and the allocator later
+// hands out again at the same address then meets a lock over pages that no longer exist.  Two
+// bench runs (rounds 4 and 5) ended in "illegal memory access" at a pageable result copy after
+// large pageable transfers of since-freed arrays.  Synchronous: the data is in
+// `dst` when it returns.
+int download(jrq_engine* e, void* dst, const void* src, size_t bytes) {
+  if (int rc = ensure_bounce(e)) return rc;
+  int prev = -1, i = 0;
+  size_t prev_off = 0, prev_n = 0;
+  auto drain = [&](int k, size_t off, size_t n) -> int {
+    JRQ_HIP(e, hipEventSynchronize(e->bounce_done[k]));
+    std::memcpy(static_cast<uint8_t*>(dst) + off, e->bounce[k], n);
+    e->bounce_busy[k] = false;
+    return JRQ_OK;
+  };
+  for (size_t off = 0; off < bytes; off += kBounceChunk, i ^= 1) {
+    const size_t n = bytes - off < kBounceChunk ? bytes - off : kBounceChunk;
+    if (e->bounce_busy[i]) JRQ_HIP(e, hipEventSynchronize(e->bounce_done[i]));  // an upload's DMA
+    JRQ_HIP(e, hipMemcpyAsync(e->bounce[i], static_cast<const uint8_t*>(src) + off, n,
+                              hipMemcpyDeviceToHost, e->stream));
+    JRQ_HIP(e, hipEventRecord(e->bounce_done[i], e->stream));
+    e->bounce_busy[i] = true;
+    if (prev >= 0)
+      if (int rc = drain(prev, prev_off, prev_n)) return rc;
+    prev = i;
+    prev_off = off;
+    prev_n = n;
+  }
+  if (prev >= 0) return drain(prev, prev_off, prev_n);
   return JRQ_OK;
 }
 
@@ -290,6 +330,20 @@ bool host_pinned(const void* p) {
   }
   return at.type == hipMemoryTypeHost;
 }
+
+int download_any(jrq_engine* e, void* dst, const void* src, size_t bytes) {
+  if (bytes == 0) return JRQ_OK;
+  if (e->upload_pageable || host_pinned(dst)) {
+    JRQ_HIP(e, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream));
+    return JRQ_OK;
+  }
+  return download(e, dst, src, bytes);
+}
+#define JRQ_DOWN(e, dst, src, bytes)                        \
+  do {                                                      \
+    const int _rc = download_any((e), (dst), (src), (bytes)); \
+    if (_rc) return _rc;                                    \
+  } while (0)
 
 int upload_any(jrq_engine* e, void* dst, const void* src, size_t bytes) {
   if (e->upload_pageable || host_pinned(src)) {
@@ -708,8 +762,8 @@ int jrq_quorum_epoch_tiles(jrq_engine* e, const jrq_group_tiles* in, int64_t* co
   if ((rc = ensure_stage(e, 9, G, &ds))) return rc;
   if ((rc = jrq_quorum_epoch_tiles_dev(e, &d, static_cast<int64_t*>(dc), static_cast<uint8_t*>(ds), G)))
     return rc;
-  JRQ_HIP(e, hipMemcpyAsync(committed_out, dc, static_cast<size_t>(G) * 8, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(status_out, ds, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, committed_out, dc, static_cast<size_t>(G) * 8);
+  JRQ_DOWN(e, status_out, ds, G);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
@@ -759,8 +813,8 @@ int jrq_quorum_epoch(jrq_engine* e, const jrq_group_batch* in, int64_t* committe
   if ((rc = ensure_stage(e, 9, G, &ds))) return rc;
   if ((rc = jrq_quorum_epoch_dev(e, &d, static_cast<int64_t*>(dc), static_cast<uint8_t*>(ds), G)))
     return rc;
-  JRQ_HIP(e, hipMemcpyAsync(committed_out, dc, static_cast<size_t>(G) * 8, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(status_out, ds, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, committed_out, dc, static_cast<size_t>(G) * 8);
+  JRQ_DOWN(e, status_out, ds, G);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
@@ -882,7 +936,7 @@ int jrq_crc64_batch(jrq_engine* e, const uint8_t* payload, const uint64_t* offse
     rc = crc_dispatch(e, a, 0);
   }
   if (rc) return rc;
-  JRQ_HIP(e, hipMemcpyAsync(crc_out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, crc_out, dout, static_cast<size_t>(N) * 8);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
@@ -927,7 +981,7 @@ int jrq_crc64_stream_update(jrq_engine* e, uint64_t* state, const uint8_t* paylo
   rc = jrq_crc64_stream_update_dev(e, ds, dp, doff, S);
   e->regs_hint = 0;
   if (rc) return rc;
-  JRQ_HIP(e, hipMemcpyAsync(state, ds, static_cast<size_t>(S) * 8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, state, ds, static_cast<size_t>(S) * 8);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
@@ -1037,8 +1091,8 @@ int jrq_logentry_checksum_batch(jrq_engine* e, const uint8_t* type, const int64_
     e->regs_hint = 0;
   }
   if (rc) return rc;
-  JRQ_HIP(e, hipMemcpyAsync(out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
-  if (corrupt_out) JRQ_HIP(e, hipMemcpyAsync(corrupt_out, dcor, N, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, out, dout, static_cast<size_t>(N) * 8);
+  if (corrupt_out) JRQ_DOWN(e, corrupt_out, dcor, N);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
@@ -1097,9 +1151,9 @@ int jrq_lease_check(jrq_engine* e, const int64_t* ts, uint64_t ld, uint32_t num_
                                 static_cast<uint8_t*>(dok), const_cast<int64_t*>(dlead),
                                 static_cast<uint16_t*>(ddead))))
     return rc;
-  JRQ_HIP(e, hipMemcpyAsync(ok_out, dok, G, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(lease_start, dlead, static_cast<size_t>(G) * 8, hipMemcpyDeviceToHost, e->stream));
-  if (dead_out) JRQ_HIP(e, hipMemcpyAsync(dead_out, ddead, static_cast<size_t>(G) * 2, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, ok_out, dok, G);
+  JRQ_DOWN(e, lease_start, dlead, static_cast<size_t>(G) * 8);
+  if (dead_out) JRQ_DOWN(e, dead_out, ddead, static_cast<size_t>(G) * 2);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
@@ -1154,7 +1208,7 @@ int jrq_readindex_quorum(jrq_engine* e, const uint64_t* conf, const uint8_t* sel
   if ((rc = jrq_readindex_quorum_dev(e, dconf, dself, dord, dok, num_peers, G,
                                      static_cast<uint8_t*>(dres))))
     return rc;
-  JRQ_HIP(e, hipMemcpyAsync(result_out, dres, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, result_out, dres, G);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
@@ -1227,10 +1281,10 @@ int jrq_leader_tick(jrq_engine* e, const int64_t* ts, uint64_t ld, uint32_t num_
                                 static_cast<uint16_t*>(ddead), dord, dokm,
                                 static_cast<uint8_t*>(dres))))
     return rc;
-  JRQ_HIP(e, hipMemcpyAsync(ok_out, dok, G, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(lease_start, dlead, static_cast<size_t>(G) * 8, hipMemcpyDeviceToHost, e->stream));
-  if (dead_out) JRQ_HIP(e, hipMemcpyAsync(dead_out, ddead, static_cast<size_t>(G) * 2, hipMemcpyDeviceToHost, e->stream));
-  if (ri_result) JRQ_HIP(e, hipMemcpyAsync(ri_result, dres, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, ok_out, dok, G);
+  JRQ_DOWN(e, lease_start, dlead, static_cast<size_t>(G) * 8);
+  if (dead_out) JRQ_DOWN(e, dead_out, ddead, static_cast<size_t>(G) * 2);
+  if (ri_result) JRQ_DOWN(e, ri_result, dres, G);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
@@ -1337,10 +1391,10 @@ int jrq_append_entries_verify(jrq_engine* e, uint32_t R, const uint32_t* req_off
                                           static_cast<uint8_t*>(dcor), static_cast<int32_t*>(dfirst))))
     return rc;
   if (N) {
-    JRQ_HIP(e, hipMemcpyAsync(checksum_out, dout, static_cast<size_t>(N) * 8, hipMemcpyDeviceToHost, e->stream));
-    JRQ_HIP(e, hipMemcpyAsync(corrupt_out, dcor, N, hipMemcpyDeviceToHost, e->stream));
+    JRQ_DOWN(e, checksum_out, dout, static_cast<size_t>(N) * 8);
+    JRQ_DOWN(e, corrupt_out, dcor, N);
   }
-  JRQ_HIP(e, hipMemcpyAsync(first_corrupt_out, dfirst, static_cast<size_t>(R) * 4, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, first_corrupt_out, dfirst, static_cast<size_t>(R) * 4);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
@@ -1411,12 +1465,12 @@ int jrq_commit_fanout(jrq_engine* e, uint32_t G, const int64_t* prev_committed,
                                   static_cast<uint32_t*>(dnum))))
     return rc;
   const size_t b8 = static_cast<size_t>(G) * 8;
-  JRQ_HIP(e, hipMemcpyAsync(cq_first, dcf, b8, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(cq_size, dcs, b8, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(first_closure_out, dfc, b8, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(status_out, dst, G, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(num_listed_out, dnum, 4, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(listed_out, dlist, words * 8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, cq_first, dcf, b8);
+  JRQ_DOWN(e, cq_size, dcs, b8);
+  JRQ_DOWN(e, first_closure_out, dfc, b8);
+  JRQ_DOWN(e, status_out, dst, G);
+  JRQ_DOWN(e, num_listed_out, dnum, 4);
+  JRQ_DOWN(e, listed_out, dlist, words * 8);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   return JRQ_OK;
 }
@@ -1546,18 +1600,18 @@ int jrq_v2_decode_verify(jrq_engine* e, const uint8_t* rec, const uint64_t* off,
            peer_counts ? static_cast<uint32_t*>(dpc) : nullptr, static_cast<uint64_t*>(dcmp),
            static_cast<uint8_t*>(dcor))))
     return rc;
-  JRQ_HIP(e, hipMemcpyAsync(status, dst, N, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(type, dty, N, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(index, didx, n8, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(term, dtm, n8, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(stored, dsto, n8, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(has_checksum, dhas, N, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(data_off, ddo, n8, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(data_len, ddl, n8, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, status, dst, N);
+  JRQ_DOWN(e, type, dty, N);
+  JRQ_DOWN(e, index, didx, n8);
+  JRQ_DOWN(e, term, dtm, n8);
+  JRQ_DOWN(e, stored, dsto, n8);
+  JRQ_DOWN(e, has_checksum, dhas, N);
+  JRQ_DOWN(e, data_off, ddo, n8);
+  JRQ_DOWN(e, data_len, ddl, n8);
   if (peer_counts)
-    JRQ_HIP(e, hipMemcpyAsync(peer_counts, dpc, static_cast<size_t>(N) * 4, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(computed, dcmp, n8, hipMemcpyDeviceToHost, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(corrupt, dcor, N, hipMemcpyDeviceToHost, e->stream));
+    JRQ_DOWN(e, peer_counts, dpc, static_cast<size_t>(N) * 4);
+  JRQ_DOWN(e, computed, dcmp, n8);
+  JRQ_DOWN(e, corrupt, dcor, N);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   for (uint32_t i = 0; i < N; ++i) data_off[i] += lo;  // back to the caller's base
   return JRQ_OK;
@@ -1813,13 +1867,13 @@ int jrq_table_epoch(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, ui
   uint32_t* off = t->n_dev + t->slices;
   uint32_t* total = off + t->slices;
   JRQ_HIP(e, jrq_launch_table_list_gather(slices, t->n_dev, t->slices, off, total, list, e->stream));
-  JRQ_HIP(e, hipMemcpyAsync(t->n_host, total, 4, hipMemcpyDeviceToHost, e->stream));
-  if (status_out) JRQ_HIP(e, hipMemcpyAsync(status_out, dst, G, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, t->n_host, total, 4);
+  if (status_out) JRQ_DOWN(e, status_out, dst, G);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   const uint32_t n = t->n_host[0];
   if (n > G) return fail(e, JRQ_E_STATE, "table list overflow (%u entries)", n);
   if (n) {
-    JRQ_HIP(e, hipMemcpyAsync(changed_out, list, static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, e->stream));
+    JRQ_DOWN(e, changed_out, list, static_cast<size_t>(n) * 8);
     JRQ_HIP(e, hipStreamSynchronize(e->stream));
   }
   *n_changed = n;
@@ -1834,33 +1888,40 @@ int jrq_table_read(jrq_table* t, int64_t* pending_index, int64_t* last_appended,
   jrq_engine* e = t->e;
   DeviceGuard guard(e->device);
   const size_t G = t->a.G;
-  std::vector<int64_t> lc(G);
-  // a tiled field back to G contiguous words: one 2-D copy of the whole tiles (256 words each,
-  // tile stride apart), one of the last partial tile
+  const size_t tiles = (G + jrq::kTableSlice - 1) / jrq::kTableSlice;
+  const size_t rb = static_cast<size_t>(t->a.P) * jrq::kTableSlice * 4;  // a tile's u32 match rows
+  // de-tiled on the device into staging (one 2-D copy per field: the whole tiles, 256 words
+  // each, tile stride apart; then the last partial tile), then one download of it all
+  void* stage = nullptr;
+  int rc;
+  if ((rc = ensure_stage(e, 20, 3 * G * 8 + (match ? tiles * rb : 0), &stage))) return rc;
+  int64_t* d_lc = static_cast<int64_t*>(stage);
+  int64_t* d_pi = d_lc + G;
+  int64_t* d_la = d_pi + G;
+  uint32_t* d_mw = reinterpret_cast<uint32_t*>(d_la + G);
   auto field = [&](int64_t* dst, const int64_t* row) -> hipError_t {
     const size_t full = G / jrq::kTableSlice, rest = G % jrq::kTableSlice;
     const size_t tb = jrq::kTableSlice * 8;
     hipError_t r = hipSuccess;
-    if (full) r = hipMemcpy2DAsync(dst, tb, row, t->a.ts * 8, tb, full, hipMemcpyDeviceToHost, e->stream);
+    if (full) r = hipMemcpy2DAsync(dst, tb, row, t->a.ts * 8, tb, full, hipMemcpyDeviceToDevice, e->stream);
     if (r == hipSuccess && rest)
       r = hipMemcpyAsync(dst + full * jrq::kTableSlice, row + full * t->a.ts, rest * 8,
-                         hipMemcpyDeviceToHost, e->stream);
+                         hipMemcpyDeviceToDevice, e->stream);
     return r;
   };
-  std::vector<int64_t> pw(G);
-  JRQ_HIP(e, field(lc.data(), t->a.lc));
-  JRQ_HIP(e, field(pw.data(), t->a.pi));
-  if (last_appended) JRQ_HIP(e, field(last_appended, t->a.la));
-  // the u32 match words: every tile's P rows (P KiB at the tile's start) in one 2-D copy
-  const size_t tiles = (G + jrq::kTableSlice - 1) / jrq::kTableSlice;
-  std::vector<uint32_t> mw;
-  if (match) {
-    mw.resize(tiles * t->a.P * jrq::kTableSlice);
-    const size_t rb = static_cast<size_t>(t->a.P) * jrq::kTableSlice * 4;
-    JRQ_HIP(e, hipMemcpy2DAsync(mw.data(), rb, t->a.match, t->a.ts * 8, rb, tiles, hipMemcpyDeviceToHost,
+  JRQ_HIP(e, field(d_lc, t->a.lc));
+  JRQ_HIP(e, field(d_pi, t->a.pi));
+  JRQ_HIP(e, field(d_la, t->a.la));
+  if (match)  // the u32 match words: every tile's P rows (P KiB at the tile's start)
+    JRQ_HIP(e, hipMemcpy2DAsync(d_mw, rb, t->a.match, t->a.ts * 8, rb, tiles, hipMemcpyDeviceToDevice,
                                 e->stream));
-  }
+  std::vector<int64_t> host(3 * G);
+  std::vector<uint32_t> mw(match ? tiles * rb / 4 : 0);
+  JRQ_DOWN(e, host.data(), stage, 3 * G * 8);
+  if (match) JRQ_DOWN(e, mw.data(), d_mw, tiles * rb);
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  const int64_t* lc = host.data();
+  int64_t* pw = host.data() + G;
   for (size_t g = 0; g < G; ++g)
     if (pw[g] == JRQ_PI_FOLLOWS_LC) pw[g] = lc[g] + 1;
   if (match)  // absolute: the group's match base + its word (mslot: the epoch's lane order)
@@ -1870,8 +1931,9 @@ int jrq_table_read(jrq_table* t, int64_t* pending_index, int64_t* last_appended,
       for (uint32_t p = 0; p < t->a.P; ++p)
         match[p * G + g] = b + static_cast<int64_t>(row[p * jrq::kTableSlice + jrq::mslot(g % jrq::kTableSlice)]);
     }
-  if (pending_index) std::memcpy(pending_index, pw.data(), G * 8);
-  if (last_committed) std::memcpy(last_committed, lc.data(), G * 8);
+  if (pending_index) std::memcpy(pending_index, pw, G * 8);
+  if (last_committed) std::memcpy(last_committed, lc, G * 8);
+  if (last_appended) std::memcpy(last_appended, host.data() + 2 * G, G * 8);
   return JRQ_OK;
 }
 
@@ -1879,7 +1941,7 @@ int jrq_table_check(jrq_table* t) {
   if (table_check(t)) return JRQ_E_INVALID;
   jrq_engine* e = t->e;
   DeviceGuard guard(e->device);
-  JRQ_HIP(e, hipMemcpyAsync(t->n_host + 1, t->a.invalid, 4, hipMemcpyDeviceToHost, e->stream));
+  JRQ_DOWN(e, t->n_host + 1, t->a.invalid, 4);
   JRQ_HIP(e, hipMemsetAsync(t->a.invalid, 0, 4, e->stream));
   JRQ_HIP(e, hipStreamSynchronize(e->stream));
   if (t->n_host[1])

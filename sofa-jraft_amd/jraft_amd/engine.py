@@ -15,6 +15,15 @@ from . import _lib
 from ._lib import GROUP_STATE, GroupBatch, TableView, check
 
 
+
+def _host_np(t):
+    """numpy copy of a device tensor through page-locked host memory: no pageable memory is
+    handed to a HIP copy (the round-4/5 faults)."""
+    import torch
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t)
+    return h.numpy()
+
 def _np_ptr(a):
     return None if a is None else C.c_void_p(a.ctypes.data)
 
@@ -603,7 +612,7 @@ class Table:
         """Host copy of a device-variant list as the host variant's words (delta << 32 | group),
         slices in order: each slice is a 256-bit map of its listed groups, then their u32
         deltas in group order (include/jrq.h jrq_table_epoch_dev)."""
-        return decode_slices(changed_out.cpu().numpy(), n_changed_out.cpu().numpy())
+        return decode_slices(_host_np(changed_out), _host_np(n_changed_out))
 
     def read(self) -> dict:
         G, P = self.G, self.P

@@ -214,3 +214,29 @@ def test_pinned_then_c1_then_lease_legs(engine):
         bench.WARM_MS = old
         engine.use_stream(None)
     assert _lib.host_registrations() == base
+
+
+def test_result_downloads_through_bounce_chunks(engine):
+    """Host-variant results land in caller memory that is not page-locked through the engine's
+    8 MiB bounce chunks (several chunks here: 1.5M groups = 12 MB of commits), never through a
+    HIP pageable copy; they equal the device entry point's results, copied out through
+    page-locked memory."""
+    import torch
+    b = W.quorum_batch("C2", groups=1_500_000)
+    c_host, s_host = engine.quorum_epoch(b["match"], b["pending_index"], b["last_appended"],
+                                         b["last_committed"], b["conf"])
+    dev = torch.device("cuda:0")
+    t = {k: torch.from_numpy(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v)).pin_memory().to(dev)
+         for k, v in b.items()}
+    G = b["pending_index"].shape[0]
+    out = torch.empty(G, dtype=torch.int64, device=dev)
+    st = torch.empty(G, dtype=torch.uint8, device=dev)
+    engine.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"], t["last_committed"],
+                            t["conf"], out, st)
+    engine.synchronize()
+    h = torch.empty(G, dtype=torch.int64, pin_memory=True)
+    h.copy_(out)
+    hs = torch.empty(G, dtype=torch.uint8, pin_memory=True)
+    hs.copy_(st)
+    assert np.array_equal(c_host, h.numpy()) and np.array_equal(s_host, hs.numpy())
+    assert (c_host >= b["last_committed"]).all()

@@ -22,7 +22,7 @@ for s in $STEPS; do
     quick) run bench_quick 600 python bench.py --steps 20 --warmup 3 --no-cpu ;;
     legs)  run bench_legs 600 python bench.py --steps 20 --warmup 3 --no-cpu --legs ${BENCH_LEGS:-quorum,table,drive,C2} ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
-    bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
+    bench) run bench 600 python bench.py --steps 20 --warmup 3 --detail gpurun_out/bench_detail.json ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu ;;
     profd) run prof_drive 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/profd -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs table,drive ;;
     tbl)   run table_tests 600 python -m pytest tests/test_gpu_table.py -q -x -p no:cacheprovider --timeout 300 ;;
