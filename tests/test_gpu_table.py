@@ -362,3 +362,65 @@ def test_epoch_dev_writes_only_its_slices(engine, G):
     assert (n[S:] == -7).all().item()
     assert (st[G:] == 0xEE).all().item()
     t.close()
+
+
+@pytest.mark.parametrize("P,joint", [(3, False), (5, True)])
+def test_match_base_rebase_across_2_30(engine, oracle, P, joint):
+    """The v3 layout keeps match as u32 words against mbase(pi) = (pi - 1) & ~(2^30 - 1).  Groups
+    whose commit carries pendingIndex across a 2^30 boundary (near 2^30 and near 2^31) have their
+    words rebased by the committing wave; the next epoch's acks (relative to the new
+    pendingIndex) must decide exactly as two carried BallotBox replays, and jrq_table_read must
+    return the absolute match of every slot at or above the new base."""
+    from jraft_amd import conf_word
+    G = 600
+    rng = np.random.default_rng(31 + P)
+    g = np.arange(G)
+    base0 = np.where(g % 2 == 0, 1 << 30, 1 << 31).astype(np.int64)
+    pi = base0 - 150 + (g % 200)                     # some cross the boundary, some do not
+    lc = pi - 1
+    la = pi + 500
+    cw = conf_word((1 << P) - 1, 0b111 if joint else 0)
+    conf = np.full(G, cw, np.uint64)
+    st = Table.states(G)
+    st["group"] = g
+    st["num_runs"] = 1
+    st["flags"] = _lib.STATE_RESET_MATCH
+    st["pending_index"] = pi
+    st["last_appended"] = la
+    st["last_committed"] = lc
+    st["run_conf"][:, 0] = cw
+    t = Table(engine, G, P)
+    t.update(st)
+    m1 = (pi - 1)[None, :] + rng.integers(0, 320, (P, G))
+    m1 = np.minimum(m1, la[None, :])
+    t.update(None, match_recs(m1, pi))
+    ce1, se1, _ = oracle.quorum_epoch_replay(m1, pi, la, lc, conf, chunk=64)
+    changed, st1 = t.epoch(status=True)
+    got1, listed = committed_from(changed, pi, lc)
+    np.testing.assert_array_equal(got1, ce1)
+    np.testing.assert_array_equal(st1, se1)
+    crossed = ((pi - 1) >> 30) != ((np.where(ce1 > lc, ce1 + 1, pi) - 1) >> 30)
+    assert crossed.sum() > 50 and (~crossed).sum() > 50  # both kinds present
+    pi1 = np.where(ce1 > lc, ce1 + 1, pi)
+    r = t.read()
+    np.testing.assert_array_equal(r["pending_index"], pi1)
+    nb = (pi1 - 1) & ~np.int64((1 << 30) - 1)
+    keep = m1 >= nb[None, :]
+    np.testing.assert_array_equal(r["match"][keep], m1[keep])
+    np.testing.assert_array_equal(r["match"][~keep], np.broadcast_to(nb, (P, G))[~keep])
+    # epoch 2: the queue grows and new acks arrive, relative to the new pendingIndex
+    la2 = pi1 + 400
+    m2 = np.maximum(m1, (pi1 - 1)[None, :] + rng.integers(0, 380, (P, G)))
+    m2 = np.minimum(m2, la2[None, :])
+    recs = [la_recs(la2, pi1, g)]
+    for p in range(P):
+        ch = np.nonzero(m2[p] != m1[p])[0]
+        recs.append(_lib.rec(ch, p, np.maximum(m2[p, ch] - (pi1[ch] - 1), 0)))
+    t.update(None, np.concatenate(recs))
+    ce2, se2, _ = oracle.quorum_epoch_replay(m2, pi1, la2, ce1, conf, chunk=64)
+    changed, st2 = t.epoch(status=True)
+    got2, _ = committed_from(changed, pi1, ce1)
+    np.testing.assert_array_equal(got2, ce2)
+    np.testing.assert_array_equal(st2, se2)
+    t.check()
+    t.close()
