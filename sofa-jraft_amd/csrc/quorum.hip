@@ -332,11 +332,17 @@ __global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair
 // round 4's T = 32, 8 waves, C = 4: 26.1 / 8.3 us; T = 16, 4 waves, C = 4: 24.5 / 7.4;
 // C = 8: 22.8 / 8.8 (so C = 8 only for long launches); 2 or 8 waves, T = 32 with 16 waves: all
 // slower.
+#ifndef JRQ_EPOCHS_DEEP_LOADS
+#define JRQ_EPOCHS_DEEP_LOADS 32
+#endif
+#ifndef JRQ_EPOCHS_WAVES
+#define JRQ_EPOCHS_WAVES 4
+#endif
 template <int P, bool kDeep>
 struct EpochChunk {
-  static constexpr int kLoads = kDeep ? 32 : 16;
+  static constexpr int kLoads = kDeep ? JRQ_EPOCHS_DEEP_LOADS : 16;
   static constexpr int kC = (kLoads / (P + 1)) < 1 ? 1 : ((kLoads / (P + 1)) > 8 ? 8 : kLoads / (P + 1));
-  static constexpr int kMaxWaves = 4;
+  static constexpr int kMaxWaves = JRQ_EPOCHS_WAVES;
   static constexpr int kTile = 16;  // groups per workgroup
 };
 constexpr uint32_t kEpochsDeepK = 192;  // epochs per launch from which EpochChunk<P, true> runs
