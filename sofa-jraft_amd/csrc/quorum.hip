@@ -498,7 +498,8 @@ __device__ __forceinline__ uint8_t epoch_status(const JrqQuorumArgs& a, bool run
   return st;
 }
 
-template <int P>
+// kRuns: the batch carries run tables (a.run_off); without them the walk is compiled out
+template <int P, bool kRuns>
 __global__ __launch_bounds__(512) void quorum_epochs_pair_kernel(JrqQuorumArgs a, uint32_t K,
                                                                                  uint64_t match_eld,
                                                                                  uint64_t la_eld) {
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(512) void quorum_epochs_pair_kernel(JrqQuorumArgs a
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    runs[h] = h < n && a.run_off != nullptr && (cw[h] & kConfRuns);
+    runs[h] = kRuns && h < n && (cw[h] & kConfRuns);
     r0[h] = runs[h] ? a.run_off[g + h] : 0;
     r1[h] = runs[h] ? a.run_off[g + h + 1] : 0;
   }
@@ -975,7 +976,10 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum_ep
     switch (q.num_peers) {
 #define JRQ_CASE(P)                                                                            \
   case P:                                                                                      \
-    hipLaunchKernelGGL(jrq::quorum_epochs_pair_kernel<P>, grid, blk, 0, stream, q, K, match_eld, la_eld); \
+    if (q.run_off)                                                                             \
+      hipLaunchKernelGGL((jrq::quorum_epochs_pair_kernel<P, true>), grid, blk, 0, stream, q, K, match_eld, la_eld); \
+    else                                                                                       \
+      hipLaunchKernelGGL((jrq::quorum_epochs_pair_kernel<P, false>), grid, blk, 0, stream, q, K, match_eld, la_eld); \
     break;
       JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
       JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)

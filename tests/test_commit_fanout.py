@@ -149,7 +149,7 @@ def test_closed_form_matches_call_by_call_replay(seed):
 # ------------------------------------------------------------------ GPU --
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G", [1, 4095, 4096, 4097, 50_000])
+@pytest.mark.parametrize("G", [1, 2, 66, 4095, 4096, 4097, 4098, 50_000])
 def test_gpu_fanout_vs_oracle(engine, G):
     ep = random_epoch(100 + G, G)
     st, fc, la, cf, cs, listed = oracle_epoch(ep)
@@ -222,10 +222,11 @@ def test_gpu_fanout_after_quorum_epoch_dev(engine):
 
 
 @pytest.mark.gpu
-def test_gpu_fanout_full_size_closed_form(engine):
+@pytest.mark.parametrize("G", [(1 << 20) + 37, (1 << 20) + 66])
+def test_gpu_fanout_full_size_closed_form(engine, G):
     """C3-sized batch (1M groups): the kernel against the numpy closed form (the form the
-    call-by-call replay pins above), including a non-multiple-of-64 tail."""
-    G = (1 << 20) + 37
+    call-by-call replay pins above), with a non-multiple-of-64 tail: odd G (one group per lane)
+    and even G (two per lane, fanout_pair; the last wave's second bitmap word partial)."""
     rng = np.random.default_rng(99)
     prev = rng.integers(0, 1 << 40, G).astype(np.int64)
     committed = prev + np.where(rng.random(G) < 0.8, rng.integers(1, 1024, G), 0)
