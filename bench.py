@@ -929,7 +929,15 @@ def leg_c3k(ctx, args, G):
     ks = torch.empty((K, G), dtype=torch.uint8, device=dev)
     launch = eng.quorum_epochs_launcher(d["match"], d["pending_index"], d["last_appended"],
                                         d["last_committed"], d["conf"], kc, ks)
-    ms, _ = ctx.timed(lambda i: launch())
+    rows_ms, _ = ctx.timed(lambda i: launch())
+    rows_c = host_np(kc)
+    # the same K epochs with every epoch's inputs in the tile layout (jrq_quorum_epochs_tiles_dev,
+    # the headline's layout): the leg's number; the rows entry point is timed beside it
+    tiles = to_dev(np.stack([W.to_tiles(ser["match"][k], ser["pending_index"], ser["last_appended"][k],
+                                        ser["last_committed"], ser["conf"]) for k in range(K)]), dev)
+    tlaunch = eng.quorum_epochs_tiles_launcher(tiles, 5, G, kc, ks)
+    ms, _ = ctx.timed(lambda i: tlaunch())
+    same_as_rows = bool(np.array_equal(host_np(kc), rows_c))
     ok = None
     if ctx.oracle_checks:  # the oracle on 2048 groups, all K epochs, state carried
         import jraft_oracle as O
@@ -949,13 +957,17 @@ def leg_c3k(ctx, args, G):
     # per group-epoch: match 8P + lastAppended 8 read, committed 8 + status 1 written; per
     # group pendingIndex / lastCommitted / conf once
     alg = G * K * (8 * P + 17) + G * 24
-    del d, kc, ks
-    return {"workload": f"C3: {G} groups x {P} peers, joint, {K} successive epochs per launch",
+    del d, kc, ks, tiles
+    return {"workload": f"C3: {G} groups x {P} peers, joint, {K} successive epochs per launch, "
+                        "inputs in tiles (jrq_quorum_epochs_tiles_dev)",
             "epochs_per_launch": K, "kernel_ms": ms,
             "decisions_per_s": G * K / (ms * 1e-3),
-            "roofline": roofline(alg, ms, kernel="quorum_epochs_pair_kernel<5>",
+            "roofline": roofline(alg, ms, kernel="quorum_epochs_pair_kernel<5, false, true>",
                                  bytes_note="8P+17 B per group-epoch + 24 B per group",
-                                 **pmc_traffic("C3K", "quorum_epochs_pair_kernel<5>")),
+                                 **pmc_traffic("C3K", "quorum_epochs_pair_kernel<5, false, true>")),
+            "rows_entry_point": {"kernel_ms": rows_ms, "frac": alg / (rows_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                                 "how": "jrq_quorum_epochs_dev (one array per field)",
+                                 "bit_exact_vs_tiles": same_as_rows},
             "bit_exact_vs_oracle_2048_groups": ok}
 
 

@@ -220,6 +220,17 @@ int jrq_quorum_epochs_dev(jrq_engine *e, const jrq_group_batch *in_dev, uint32_t
                           uint64_t match_epoch_ld, uint64_t la_epoch_ld,
                           int64_t *committed_out_dev, uint8_t *status_out_dev, uint32_t G);
 
+/* K epochs as jrq_quorum_epochs_dev, every epoch's inputs in the tile layout of
+ * jrq_quorum_epoch_tiles_dev: epoch k's tiles start epoch_ld int64 words after epoch 0's
+ * (epoch_ld even, >= the tiles' extent 256 (num_peers + 4) ceil(G / 256)); epoch k's match and
+ * last_appended words come from its own tiles, pending_index / last_committed / conf (the state
+ * before epoch 0) from epoch 0's.  Out as jrq_quorum_epochs_dev: committed_out[k*G + g],
+ * status_out[k*G + g].  tiles and committed_out 16-B aligned, status_out 2-B aligned, G >= 2,
+ * G even when K > 1 (JRQ_E_INVALID otherwise). */
+int jrq_quorum_epochs_tiles_dev(jrq_engine *e, const jrq_group_tiles *in_dev, uint32_t K,
+                                uint64_t epoch_ld, int64_t *committed_out_dev,
+                                uint8_t *status_out_dev, uint32_t G);
+
 /* -------------------------------------------------- resident group table -- */
 
 /* The drop-in path for a long-running multi-Raft host: the BallotBox state of G groups lives

@@ -853,6 +853,42 @@ int jrq_quorum_epochs_dev(jrq_engine* e, const jrq_group_batch* in, uint32_t K,
   return JRQ_OK;
 }
 
+int jrq_quorum_epochs_tiles_dev(jrq_engine* e, const jrq_group_tiles* in, uint32_t K,
+                                uint64_t epoch_ld, int64_t* committed_out, uint8_t* status_out,
+                                uint32_t G) {
+  if (!e || !in) return e ? fail(e, JRQ_E_INVALID, "null batch") : JRQ_E_INVALID;
+  if (G == 0 || K == 0) return JRQ_OK;
+  if (in->num_peers == 0 || in->num_peers > JRQ_MAX_PEERS)
+    return fail(e, JRQ_E_INVALID, "num_peers %u outside 1..%d", in->num_peers, JRQ_MAX_PEERS);
+  if (!in->tiles || !committed_out || !status_out || (in->run_off && (!in->run_start || !in->run_conf)))
+    return fail(e, JRQ_E_INVALID, "missing array");
+  const uint32_t P = in->num_peers;
+  const uint64_t extent = (static_cast<uint64_t>(G) + 255) / 256 * 256 * (P + 4);
+  if (K > 1 && epoch_ld < extent) return fail(e, JRQ_E_INVALID, "epoch_ld below the tiles' extent");
+  if (G < 2 || (epoch_ld & 1u) || (reinterpret_cast<uintptr_t>(in->tiles) & 15u) ||
+      (reinterpret_cast<uintptr_t>(committed_out) & 15u) || (G & 1u && K > 1) ||
+      (reinterpret_cast<uintptr_t>(status_out) & 1u))
+    return fail(e, JRQ_E_INVALID, "tiles / committed_out not 16-B aligned, epoch_ld odd, status_out odd, "
+                                  "G < 2, or G odd with K > 1");
+  DeviceGuard guard(e->device);
+  JrqQuorumArgs a{};
+  a.match = in->tiles;
+  a.pending_index = in->tiles + 256u * P;
+  a.last_appended = a.pending_index + 256;
+  a.last_committed = a.last_appended + 256;
+  a.conf = reinterpret_cast<const uint64_t*>(a.last_committed + 256);
+  a.ts = 256ull * (P + 4);
+  a.run_off = in->run_off;
+  a.run_start = in->run_start;
+  a.run_conf = in->run_conf;
+  a.num_peers = P;
+  a.committed = committed_out;
+  a.status = status_out;
+  a.G = G;
+  JRQ_HIP(e, jrq_launch_quorum_epochs(&a, K, epoch_ld, epoch_ld, e->num_cus, e->stream));
+  return JRQ_OK;
+}
+
 int jrq_crc64_batch_dev(jrq_engine* e, const uint8_t* payload, const uint64_t* offsets, uint32_t N,
                         uint64_t* crc_out) {
   if (!e) return JRQ_E_INVALID;

@@ -498,9 +498,18 @@ __device__ __forceinline__ uint8_t epoch_status(const JrqQuorumArgs& a, bool run
   return st;
 }
 
-// kRuns: the batch carries run tables (a.run_off); without them the walk is compiled out
-template <int P, bool kRuns>
-__global__ __launch_bounds__(512) void quorum_epochs_pair_kernel(JrqQuorumArgs a, uint32_t K,
+// kRuns: the batch carries run tables (a.run_off); without them the walk is compiled out.
+// kTiles: every epoch's inputs in the 256-group tiles of jrq_quorum_epoch_tiles_dev (a.ts =
+// the tile stride; epoch k's tiles match_eld words after epoch 0's), so a wave reads each
+// epoch's match and lastAppended fields as one contiguous block of its tile.
+#ifndef JRQ_EPOCHS_PAIR_BLOCK
+#define JRQ_EPOCHS_PAIR_BLOCK 512
+#endif
+#ifndef JRQ_EPOCHS_PAIR_UNROLL
+#define JRQ_EPOCHS_PAIR_UNROLL 1
+#endif
+template <int P, bool kRuns, bool kTiles>
+__global__ __launch_bounds__(JRQ_EPOCHS_PAIR_BLOCK) void quorum_epochs_pair_kernel(JrqQuorumArgs a, uint32_t K,
                                                                                  uint64_t match_eld,
                                                                                  uint64_t la_eld) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -509,18 +518,21 @@ __global__ __launch_bounds__(512) void quorum_epochs_pair_kernel(JrqQuorumArgs a
   if (i >= pairs && !tail) return;
   const uint32_t g = tail ? a.G - 1 : 2 * i;
   const int n = tail ? 1 : 2;
+  // word of group g in a field's row (tiles: in tile 0; a pair never straddles a tile)
+  const size_t at = kTiles ? static_cast<size_t>(g >> 8) * a.ts + (g & 255u) : static_cast<size_t>(g);
+  const size_t mstride = kTiles ? 256u : static_cast<size_t>(a.match_ld);
   int64_t pi0[2], lc0[2], vmax[2] = {kI64Min, kI64Min};
   uint64_t cw[2];
   bool runs[2];
   uint32_t r0[2], r1[2];
   if (!tail) {
-    const i64x2 p2 = ld2nt(a.pending_index + g), l2 = ld2nt(a.last_committed + g);
-    const i64x2 c2 = ld2nt(reinterpret_cast<const int64_t*>(a.conf) + g);
+    const i64x2 p2 = ld2nt(a.pending_index + at), l2 = ld2nt(a.last_committed + at);
+    const i64x2 c2 = ld2nt(reinterpret_cast<const int64_t*>(a.conf) + at);
     pi0[0] = p2.x; pi0[1] = p2.y;
     lc0[0] = l2.x; lc0[1] = l2.y;
     cw[0] = static_cast<uint64_t>(c2.x); cw[1] = static_cast<uint64_t>(c2.y);
   } else {
-    pi0[0] = a.pending_index[g]; lc0[0] = a.last_committed[g]; cw[0] = a.conf[g];
+    pi0[0] = a.pending_index[at]; lc0[0] = a.last_committed[at]; cw[0] = a.conf[at];
     pi0[1] = 0; lc0[1] = 0; cw[1] = 0;
   }
 #pragma unroll
@@ -529,23 +541,24 @@ __global__ __launch_bounds__(512) void quorum_epochs_pair_kernel(JrqQuorumArgs a
     r0[h] = runs[h] ? a.run_off[g + h] : 0;
     r1[h] = runs[h] ? a.run_off[g + h + 1] : 0;
   }
+#pragma unroll JRQ_EPOCHS_PAIR_UNROLL
   for (uint32_t k = 0; k < K; ++k) {
     int64_t la[2], m[2][P];
     if (!tail) {
-      const i64x2 l2 = ld2nt(a.last_appended + k * la_eld + g);
+      const i64x2 l2 = ld2nt(a.last_appended + k * la_eld + at);
       la[0] = l2.x; la[1] = l2.y;
 #pragma unroll
       for (int p = 0; p < P; ++p) {
-        const i64x2 v = ld2nt(a.match + k * match_eld + static_cast<size_t>(p) * a.match_ld + g);
+        const i64x2 v = ld2nt(a.match + k * match_eld + static_cast<size_t>(p) * mstride + at);
         m[0][p] = v.x;
         m[1][p] = v.y;
       }
     } else {
-      la[0] = a.last_appended[k * la_eld + g];
+      la[0] = a.last_appended[k * la_eld + at];
       la[1] = 0;
 #pragma unroll
       for (int p = 0; p < P; ++p) {
-        m[0][p] = a.match[k * match_eld + static_cast<size_t>(p) * a.match_ld + g];
+        m[0][p] = a.match[k * match_eld + static_cast<size_t>(p) * mstride + at];
         m[1][p] = 0;
       }
     }
@@ -971,20 +984,25 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum_ep
                     al16(q.match) && al16(q.pending_index) && al16(q.last_appended) &&
                     al16(q.last_committed) && al16(q.conf) && al16(q.committed) &&
                     (reinterpret_cast<uintptr_t>(q.status) & 1u) == 0;
-  if (pair) {
-    const dim3 grid(static_cast<unsigned>((q.G / 2 + 511) / 512)), blk(512);
+  if (pair || q.ts) {  // (tiled inputs: always the pair kernel, G >= 2 and aligned: the caller checks)
+    constexpr unsigned kB = JRQ_EPOCHS_PAIR_BLOCK;
+    const dim3 grid(static_cast<unsigned>((q.G / 2 + 1 + kB - 1) / kB)), blk(kB);  // + the odd tail's lane
     switch (q.num_peers) {
+#define JRQ_LAUNCH(P, R, T) \
+  hipLaunchKernelGGL((jrq::quorum_epochs_pair_kernel<P, R, T>), grid, blk, 0, stream, q, K, match_eld, la_eld)
 #define JRQ_CASE(P)                                                                            \
   case P:                                                                                      \
-    if (q.run_off)                                                                             \
-      hipLaunchKernelGGL((jrq::quorum_epochs_pair_kernel<P, true>), grid, blk, 0, stream, q, K, match_eld, la_eld); \
-    else                                                                                       \
-      hipLaunchKernelGGL((jrq::quorum_epochs_pair_kernel<P, false>), grid, blk, 0, stream, q, K, match_eld, la_eld); \
+    if (q.ts) {                                                                                \
+      if (q.run_off) JRQ_LAUNCH(P, true, true); else JRQ_LAUNCH(P, false, true);               \
+    } else {                                                                                   \
+      if (q.run_off) JRQ_LAUNCH(P, true, false); else JRQ_LAUNCH(P, false, false);             \
+    }                                                                                          \
     break;
       JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
       JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
       JRQ_CASE(15) JRQ_CASE(16)
 #undef JRQ_CASE
+#undef JRQ_LAUNCH
       default:
         return hipErrorInvalidValue;
     }

@@ -113,6 +113,8 @@ SIGNATURES = [
     ("jrq_quorum_epoch_tiles", C.c_int, [_V, C.POINTER(GroupTiles), _V, _V, C.c_uint32]),
     ("jrq_quorum_epochs_dev", C.c_int,
      [_V, C.POINTER(GroupBatch), C.c_uint32, C.c_uint64, C.c_uint64, _V, _V, C.c_uint32]),
+    ("jrq_quorum_epochs_tiles_dev", C.c_int,
+     [_V, C.POINTER(GroupTiles), C.c_uint32, C.c_uint64, _V, _V, C.c_uint32]),
     ("jrq_crc64_batch_dev", C.c_int, [_V, _V, _V, C.c_uint32, _V]),
     ("jrq_crc64_batch", C.c_int, [_V, _V, _V, C.c_uint32, _V]),
     ("jrq_crc64_fixed_dev", C.c_int, [_V, _V, C.c_uint64, C.c_uint32, _V]),

@@ -227,6 +227,25 @@ class Engine:
                                             last_appended.stride(0), _dev_ptr(committed_out),
                                             _dev_ptr(status_out), G), self._h)
 
+    def quorum_epochs_tiles_launcher(self, tiles, P, G, committed_out, status_out, run_off=None,
+                                     run_start=None, run_conf=None):
+        """jrq_quorum_epochs_tiles_dev with its arguments resolved once: `tiles` a device tensor
+        [K, words] (each row one epoch in the tile layout, W.to_tiles); committed_out /
+        status_out [K, G]."""
+        K = tiles.shape[0]
+        b = _lib.GroupTiles(_dev_ptr(tiles), P, _dev_ptr(run_off), _dev_ptr(run_start), _dev_ptr(run_conf))
+        fn, h, ref = self._L.jrq_quorum_epochs_tiles_dev, self._h, C.byref(b)
+        ld = tiles.stride(0)
+        co, so = _dev_ptr(committed_out), _dev_ptr(status_out)
+        keep = (b, tiles, committed_out, status_out, run_off, run_start, run_conf)
+
+        def launch():
+            rc = fn(h, ref, K, ld, co, so, G)
+            if rc:
+                check(rc, h)
+        launch.keep = keep
+        return launch
+
     # ------------------------------------------------------------ checksum --
     def crc64_batch(self, payload, offsets):
         payload = _c(payload, np.uint8)

@@ -301,6 +301,67 @@ def test_tiles_entry_point_full_c3(engine):
     assert torch.equal(o1, o2) and torch.equal(s1, s2)
 
 
+def _series_tiles(s, K):
+    """Every epoch of series `s` in the tile layout, one row per epoch (W.to_tiles)."""
+    return np.stack([W.to_tiles(s["match"][k], s["pending_index"], s["last_appended"][k],
+                                s["last_committed"], s["conf"]) for k in range(K)])
+
+
+@pytest.mark.parametrize("P,G,K,runs", [(3, 1000, 9, False), (5, 778, 12, True), (2, 64, 1, False),
+                                        (5, 777, 1, True), (3, 130, 40, True)])
+def test_gpu_quorum_epochs_tiles_vs_replay(engine, oracle, P, G, K, runs):
+    """jrq_quorum_epochs_tiles_dev: K epochs with each epoch's inputs in the tile layout ==
+    K sequential BallotBox replays with carried state (conf runs and flagged groups included,
+    G off the tile grid, odd G for one epoch)."""
+    import torch
+    from quorum_cases import flag_runs, random_series, series_replay
+    s = random_series(1900 + K, G, P, K)
+    if runs:
+        s["conf"] = flag_runs(s)
+    else:
+        s["conf"] = s["conf"] & ~np.uint64(1 << 63)
+        s["run_off"] = None
+    ce, se = series_replay(oracle, s) if runs else _series_oracle(
+        {k: v for k, v in s.items() if k != "run_off"}, K)
+    dev = torch.device("cuda:0")
+    tiles = torch.from_numpy(_series_tiles(s, K)).to(dev)
+    rt = _to_dev(s, ["run_off", "run_start", "run_conf"]) if runs else {}
+    c = torch.empty((K, G), dtype=torch.int64, device=dev)
+    st = torch.empty((K, G), dtype=torch.uint8, device=dev)
+    engine.quorum_epochs_tiles_launcher(tiles, P, G, c, st, rt.get("run_off"), rt.get("run_start"),
+                                        rt.get("run_conf"))()
+    engine.synchronize()
+    np.testing.assert_array_equal(c.cpu().numpy(), ce)
+    np.testing.assert_array_equal(st.cpu().numpy(), se)
+
+
+def test_gpu_quorum_epochs_tiles_full_c3(engine):
+    """C3 at its full 1M groups, 4 epochs per launch, tiles against the rows entry point (itself
+    checked against the oracle on large batches above); odd G with K > 1 is refused (its
+    committed rows would lose the 16-B alignment of the pair stores)."""
+    import torch
+    from jraft_amd import JrqError
+    K = 4
+    s = W.quorum_epoch_series("C3", K)
+    G = s["pending_index"].shape[0]
+    dev = torch.device("cuda:0")
+    d = {k: torch.from_numpy(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v)).to(dev)
+         for k, v in s.items()}
+    c1 = torch.empty((K, G), dtype=torch.int64, device=dev)
+    s1 = torch.empty((K, G), dtype=torch.uint8, device=dev)
+    engine.quorum_epochs_dev(d["match"], d["pending_index"], d["last_appended"], d["last_committed"],
+                             d["conf"], c1, s1)
+    tiles = torch.from_numpy(_series_tiles(s, K)).to(dev)
+    c2 = torch.empty((K, G), dtype=torch.int64, device=dev)
+    s2 = torch.empty((K, G), dtype=torch.uint8, device=dev)
+    engine.quorum_epochs_tiles_launcher(tiles, 5, G, c2, s2)()
+    engine.synchronize()
+    assert torch.equal(c1, c2) and torch.equal(s1, s2)
+    assert (c1[-1] > c1[0]).any()
+    with pytest.raises(JrqError):
+        engine.quorum_epochs_tiles_launcher(tiles, 5, G - 1, c2, s2)()
+
+
 @pytest.mark.parametrize("P,G,K", [(3, 1000, 9), (5, 777, 40), (2, 64, 1), (3, 130, 200)])
 def test_gpu_quorum_epochs_with_runs(engine, oracle, P, G, K):
     """K epochs in one launch with conf runs and flagged groups == K sequential replays."""

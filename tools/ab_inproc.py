@@ -115,6 +115,17 @@ def main():
             return lambda: e.quorum_epochs_dev(dk["match"], dk["pending_index"], dk["last_appended"],
                                                dk["last_committed"], dk["conf"], o, skst)
         legs["C3K"] = (mk_c3k, lambda: torch.empty((8, 1 << 20), dtype=torch.int64, device=dev))
+    if "C3KT" in legs_env:  # the same 8 epochs of C3 in the tile layout (jrq_quorum_epochs_tiles_dev)
+        skt = W.quorum_epoch_series("C3", 8)
+        Gt = skt["pending_index"].shape[0]
+        tl = torch.from_numpy(np.stack([W.to_tiles(skt["match"][k], skt["pending_index"],
+                                                   skt["last_appended"][k], skt["last_committed"],
+                                                   skt["conf"]) for k in range(8)])).to(dev)
+        sktst = torch.empty((8, Gt), dtype=torch.uint8, device=dev)
+
+        def mk_c3kt(e, o):
+            return e.quorum_epochs_tiles_launcher(tl, 5, Gt, o, sktst)
+        legs["C3KT"] = (mk_c3kt, lambda: torch.empty((8, Gt), dtype=torch.int64, device=dev))
     for kk_, KE in (("C2K256", 256), ("C2K64", 64)):  # configs[1], KE epochs per launch
         if kk_ not in legs_env:
             continue

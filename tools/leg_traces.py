@@ -41,7 +41,7 @@ LEG_KERNELS = {
     "table": (("resident_table", "roofline"), ["table_epoch_kernel<5>"]),
     "C2": (("C2", "batched_epochs", "roofline"), ["quorum_epochs_kernel<3,"]),
     "C2L": (("C2", "batched_epochs_64", "roofline"), ["quorum_epochs_kernel<3,"]),
-    "C3K": (("C3_k_epochs", "roofline"), ["quorum_epochs_pair_kernel<5>"]),
+    "C3K": (("C3_k_epochs", "roofline"), ["quorum_epochs_pair_kernel<5, false, true>"]),
     "C5": (("crc64", "roofline"), ["crc64_fixed_kernel<true, false>"]),
     "C1": (("C1", "roofline"), ["crc64_fixed_kernel<true, false>"]),
     "ae": (("next_rows", "append_entries_verify", "roofline"),
