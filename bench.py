@@ -1540,7 +1540,7 @@ def leg_fanout(ctx, args, G):
     return {"workload": f"{G} groups (C3 epoch output) -> doCommitted/popClosureUntil, "
                         f"{n_listed} listed, {n_pop} popping",
             "groups_per_s": G / (ms * 1e-3), "ms_per_launch": ms, "bit_exact_vs_oracle": ok,
-            "roofline": roofline(fb, ms, **pmc_traffic("fanout", "fanout_eval"))}
+            "roofline": roofline(fb, ms, kernel="fanout_pair", **pmc_traffic("fanout", "fanout_pair"))}
 
 
 def leg_peak(ctx):

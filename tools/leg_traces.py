@@ -55,7 +55,7 @@ LEG_KERNELS = {
     "lease": (("next_rows", "lease_check", "roofline"), ["leader_tick_pair_kernel<5, false>"]),
     "tick": (("next_rows", "leader_tick", "roofline"), ["leader_tick_pair_kernel<5, true>"]),
     "readindex": (("next_rows", "readindex_quorum", "roofline"), ["readindex_quorum_kernel<5, true>"]),
-    "fanout": (("next_rows", "commit_fanout", "roofline"), ["fanout_eval"]),
+    "fanout": (("next_rows", "commit_fanout", "roofline"), ["fanout_pair"]),
 }
 
 
