@@ -782,11 +782,23 @@ void GroupBatch::dropDeadRuns(uint32_t g) {
 
 // Append groups[0..n) to `part` (reserved for them): per group, under its lock, the dirty bits
 // are taken and the header or records written from the group's current state.
+#ifndef JRAFT_PACK_AHEAD
+#define JRAFT_PACK_AHEAD 4
+#endif
+#ifndef JRAFT_PREFETCH_LINES
+#define JRAFT_PREFETCH_LINES 1
+#endif
+// Prefetch (for writing) the first `JRAFT_PREFETCH_LINES` 64-B lines of group g's record.
+inline void prefetchRecord(const uint8_t* rec, size_t stride, uint32_t g) {
+  const uint8_t* r = rec + static_cast<size_t>(g) * stride;
+  for (size_t l = 0; l < JRAFT_PREFETCH_LINES && l * 64 < stride; ++l) __builtin_prefetch(r + 64 * l, 1);
+}
+
 void GroupBatch::packRange(Part& part, const uint32_t* groups, size_t n) {
   uint32_t si = part.ns, ri = part.nr;
-  constexpr size_t kAhead = 4;
+  constexpr size_t kAhead = JRAFT_PACK_AHEAD;
   for (size_t i = 0; i < n; ++i) {
-    if (i + kAhead < n) __builtin_prefetch(rec_ + static_cast<size_t>(groups[i + kAhead]) * stride_, 1);
+    if (i + kAhead < n) prefetchRecord(rec_, stride_, groups[i + kAhead]);
     const uint32_t g = groups[i];
     Guard lk(*this, g);
     // A group can sit on two threads' lists of one generation (two fast-path acks of different
@@ -1029,7 +1041,7 @@ uint32_t GroupBatch::flushLocked() {
     for (size_t i = i0; i < i1; ++i) {
       if (i + kAhead < i1) {
         const uint32_t a = static_cast<uint32_t>(changed_.p[i + kAhead]);
-        __builtin_prefetch(rec_ + static_cast<size_t>(a) * stride_, 1);
+        prefetchRecord(rec_, stride_, a);
         __builtin_prefetch(&closures_[a], 0);
         __builtin_prefetch(&waiter_[a], 0);
       }

@@ -10,8 +10,10 @@ import numpy as np
 
 from . import _lib
 
-DRIVE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
-                          "libjraft_drive.so")
+# (JRAFT_AMD_AB_DRIVE: a variant build's libjraft_drive.so, for tools/gpu_check.sh `dab` A/B
+# runs only -- the product path never sets it)
+DRIVE_PATH = os.environ.get("JRAFT_AMD_AB_DRIVE") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libjraft_drive.so")
 STATS = ("api_ms", "pack_ms", "device_ms", "deliver_ms", "flush_ms", "h2d_bytes", "d2h_bytes",
          "states", "records", "changed", "api_calls")
 _drv = None

@@ -41,6 +41,10 @@ for s in $STEPS; do
            for v in ${AB_LIBS:-base}; do
              run bench_${TAG:-sel}_$v 600 env JRAFT_AMD_AB_LIB=ab/$v/libjrq.so python bench.py --steps 20 --warmup 5 --no-cpu --legs ${BENCH_LEGS:-table} --detail gpurun_out/bench_${TAG:-sel}_${v}_detail.json
            done ;;
+    dab)   # the drive leg once per variant host build (ab/<v>/libjraft_drive.so + its libs), alternating
+           i=0; for v in ${AB_LIBS:-base}; do i=$((i+1))
+             run drive_${i}_$v 300 env JRAFT_AMD_AB_DRIVE=ab/$v/libjraft_drive.so python bench.py --steps 5 --warmup 2 --no-cpu --legs drive --detail gpurun_out/drive_${i}_${v}_detail.json
+           done ;;
     ab)    run ab_${TAG:-sel} 600 env AB_LEGS=${AB_LEGS:-C3,C5f,C1f,archive} python tools/ab_inproc.py ${AB_VARIANTS:-base=ab/base/libjrq.so} ;;
     tpab)  # the resident table epoch, every group committing, libjrq variants side by side
            for P in ${TP_PEERS:-5}; do
