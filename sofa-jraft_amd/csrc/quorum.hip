@@ -132,7 +132,16 @@ __device__ __forceinline__ void st_pair(T v, T* p) {
 // The single-conf decision runs in 32-bit arithmetic relative to pendingIndex
 // (decide_single_rel, quorum_core.h: C3 16.4 -> 15.6 us per epoch in round 3's tools/pair_probe.hip,
 // against 15.1 us for the loads and stores alone).
-constexpr uint32_t kPairBlock = 512;
+// Workgroup size of the pair kernel by input layout: in-process A/B (r05, 30 interleaved
+// rounds, profiles/r05e_ab_pair_block.log): rows 15.8 us at 512 threads, 15.2 at 1024, 16.6 at
+// 256; tiles 14.8 at 512 and at 256, 15.0 at 1024.
+#ifndef JRQ_PAIR_BLOCK_ROWS
+#define JRQ_PAIR_BLOCK_ROWS 1024
+#endif
+#ifndef JRQ_PAIR_BLOCK_TILES
+#define JRQ_PAIR_BLOCK_TILES 512
+#endif
+constexpr uint32_t pair_block(bool tiles) { return tiles ? JRQ_PAIR_BLOCK_TILES : JRQ_PAIR_BLOCK_ROWS; }
 #ifndef JRQ_PAIR_XCD_TILES
 #define JRQ_PAIR_XCD_TILES 0
 #endif
@@ -141,7 +150,8 @@ constexpr uint32_t kPairBlock = 512;
 // every field of a tile's groups in one contiguous block; jrq_quorum_epoch_tiles_dev), the
 // outputs as rows.  A wave's pairs sit in one half of one tile.
 template <int P, bool kRuns, bool kTiles>
-__global__ __launch_bounds__(kPairBlock) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
+__global__ __launch_bounds__(pair_block(kTiles)) JRQ_SGPRS_8WAVES void quorum_epoch_pair_kernel(JrqQuorumArgs a) {
+  constexpr uint32_t kPairBlock = pair_block(kTiles);
   // word of group g in a field's row (tiles: the field's row in tile 0)
   auto at = [&](uint32_t g) -> size_t {
     return kTiles ? static_cast<size_t>(g >> 8) * a.ts + (g & 255u) : static_cast<size_t>(g);
@@ -503,7 +513,7 @@ __device__ __forceinline__ uint8_t epoch_status(const JrqQuorumArgs& a, bool run
 // the tile stride; epoch k's tiles match_eld words after epoch 0's), so a wave reads each
 // epoch's match and lastAppended fields as one contiguous block of its tile.
 #ifndef JRQ_EPOCHS_PAIR_BLOCK
-#define JRQ_EPOCHS_PAIR_BLOCK 512
+#define JRQ_EPOCHS_PAIR_BLOCK 256
 #endif
 #ifndef JRQ_EPOCHS_PAIR_UNROLL
 #define JRQ_EPOCHS_PAIR_UNROLL 1
@@ -937,7 +947,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_quorum(
   // pair kernel: one lane per two groups, the whole grid at once; scalar kernel: one lane per
   // group, at most 8 workgroups per CU, grid-stride beyond
   const uint64_t lanes = pair ? (a.G >> 1) : a.G;
-  const uint32_t bs = pair ? jrq::kPairBlock : 256u;
+  const uint32_t bs = pair ? jrq::pair_block(a.ts != 0) : 256u;
   const dim3 blk(bs);
   const uint64_t need = (lanes + bs - 1) / bs;
   const uint64_t cap = pair ? need : static_cast<uint64_t>(num_cus) * 8;

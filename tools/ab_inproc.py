@@ -106,6 +106,23 @@ def main():
                                    t["last_committed"], t["conf"], o, c3s)
             return f
         legs["C3"] = (mk_c3, lambda: torch.empty(1 << 20, dtype=torch.int64, device=dev))
+    if "C3T" in legs_env:  # the headline: C3 epochs from tiles over 6 rotating inputs
+        c3t = []
+        for k in range(6):
+            b = W.quorum_batch("C3", seed=(W.SEED_BASE ^ 3) + 7919 * k)
+            c3t.append(torch.from_numpy(W.to_tiles(b["match"], b["pending_index"], b["last_appended"],
+                                                   b["last_committed"], b["conf"])).to(dev))
+        c3ts = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+
+        def mk_c3t(e, o):
+            ls = [e.quorum_epoch_tiles_launcher(t, 5, 1 << 20, o, c3ts) for t in c3t]
+            cnt = [0]
+
+            def f():
+                ls[cnt[0] % 6]()
+                cnt[0] += 1
+            return f
+        legs["C3T"] = (mk_c3t, lambda: torch.empty(1 << 20, dtype=torch.int64, device=dev))
     if "C3K" in legs_env:  # 8 epochs of C3 per launch (jrq_quorum_epochs_dev)
         sk = W.quorum_epoch_series("C3", 8)
         dk = {kk: dev_t(np.ascontiguousarray(v)) for kk, v in sk.items()}
