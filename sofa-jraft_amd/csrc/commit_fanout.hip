@@ -29,8 +29,14 @@
 
 namespace jrq {
 
-constexpr int kFanBlock = 1024;
-constexpr int kFanPerThread = 4;
+#ifndef JRQ_FAN_BLOCK
+#define JRQ_FAN_BLOCK 1024
+#endif
+#ifndef JRQ_FAN_PER_THREAD
+#define JRQ_FAN_PER_THREAD 4
+#endif
+constexpr int kFanBlock = JRQ_FAN_BLOCK;
+constexpr int kFanPerThread = JRQ_FAN_PER_THREAD;
 constexpr int kFanTile = kFanBlock * kFanPerThread;  // groups per tile
 
 // include/jrq.h jrq_fanout_status

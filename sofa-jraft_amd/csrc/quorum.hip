@@ -790,7 +790,10 @@ __device__ __forceinline__ void lease_one(const int64_t (&ts)[P], uint64_t cw, u
 #define JRQ_TICK_ATTR
 #endif
 template <int P, bool kRI>
-__global__ __launch_bounds__(512) JRQ_TICK_ATTR void leader_tick_pair_kernel(JrqLeaseArgs a) {
+#ifndef JRQ_TICK_BLOCK
+#define JRQ_TICK_BLOCK 512
+#endif
+__global__ __launch_bounds__(JRQ_TICK_BLOCK) JRQ_TICK_ATTR void leader_tick_pair_kernel(JrqLeaseArgs a) {
   using u64x2 = __attribute__((ext_vector_type(2))) uint64_t;
   using i64x2 = __attribute__((ext_vector_type(2))) int64_t;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -887,7 +890,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_lease(
                     (!ri || (al(a.order, 16) && al(a.ri_ok_mask, 4) && al(a.ri_result, 2)));
   if (pair) {
     const uint64_t lanes = static_cast<uint64_t>(a.G) / 2 + 1;  // + the odd tail's lane
-    const dim3 grid(static_cast<unsigned>((lanes + 511) / 512)), blk(512);
+    const dim3 grid(static_cast<unsigned>((lanes + JRQ_TICK_BLOCK - 1) / JRQ_TICK_BLOCK)), blk(JRQ_TICK_BLOCK);
     switch (a.num_peers) {
 #define JRQ_CASE(P)                                                                             \
   case P:                                                                                       \

@@ -193,6 +193,26 @@ def main():
                                    device=dev) for k, t in Engine.V2_FIELDS}
         legs["v2"] = (mk_v2, new_v2)
 
+    if "fanout" in legs_env:  # commit fan-out of a C3 epoch, 1M groups (steady state: after the
+        # first launch the queues hold nothing at or below the commit, so no group pops)
+        bq = W.quorum_batch("C3")
+        Gq = bq["pending_index"].shape[0]
+        fq = {k: dev_t(np.ascontiguousarray(v)) for k, v in bq.items()}
+        fc_c = torch.empty(Gq, dtype=torch.int64, device=dev)
+        fc_s = torch.empty(Gq, dtype=torch.uint8, device=dev)
+        variants[0][1].quorum_epoch_dev(fq["match"], fq["pending_index"], fq["last_appended"],
+                                        fq["last_committed"], fq["conf"], fc_c, fc_s)
+        torch.cuda.synchronize()
+
+        def mk_fan(e, o):
+            cf = fq["pending_index"].clone()
+            cs = (fq["last_appended"] - fq["pending_index"] + 1).clone()
+            la = fq["last_committed"].clone()
+            st = torch.empty(Gq, dtype=torch.uint8, device=dev)
+            lst = torch.empty((Gq + 63) // 64, dtype=torch.int64, device=dev)
+            num = torch.zeros(1, dtype=torch.int32, device=dev)
+            return lambda: e.commit_fanout_dev(fq["last_committed"], fc_c, la, cf, cs, o, st, lst, num)
+        legs["fanout"] = (mk_fan, lambda: torch.empty(Gq, dtype=torch.int64, device=dev))
     if "tick" in legs_env or "lease" in legs_env:  # leader tick over 1M groups x 5 peers
         Gt, Pt = 1 << 20, 5
         rng = np.random.default_rng(5)
