@@ -2,19 +2,26 @@
 import numpy as np
 
 
-def random_requests(seed, R, max_entries=64, max_len=3000, corrupt_frac=0.02, oracle=None):
+def random_requests(seed, R, max_entries=64, max_len=3000, corrupt_frac=0.02, oracle=None,
+                    uniform=None):
     """R requests; entries of random type (incl. UNKNOWN = 0, which consumes no data),
     random data_len, checksums as a leader would stamp them (from the oracle), a few
-    flipped so the follower must flag them, a few entries without a checksum."""
+    flipped so the follower must flag them, a few entries without a checksum.
+    uniform=L: every request holds max_entries entries of L bytes, none UNKNOWN (the batch the
+    fixed-size data path takes)."""
     rng = np.random.default_rng(seed)
-    n_per = rng.integers(0, max_entries + 1, R)
+    n_per = rng.integers(0, max_entries + 1, R) if uniform is None else np.full(R, max_entries)
     req_off = np.concatenate([[0], np.cumsum(n_per)]).astype(np.uint32)
     N = int(req_off[-1])
     prev = rng.integers(0, 1 << 40, R).astype(np.int64)
     term = rng.integers(1, 1 << 20, N).astype(np.int64)
-    etype = rng.choice([0, 1, 2, 2, 2, 3], N).astype(np.uint8)
-    data_len = rng.integers(0, max_len + 1, N).astype(np.int64)
-    data_len[rng.random(N) < 0.1] = 0
+    if uniform is None:
+        etype = rng.choice([0, 1, 2, 2, 2, 3], N).astype(np.uint8)
+        data_len = rng.integers(0, max_len + 1, N).astype(np.int64)
+        data_len[rng.random(N) < 0.1] = 0
+    else:
+        etype = rng.choice([1, 2, 2, 2, 3], N).astype(np.uint8)
+        data_len = np.full(N, uniform, np.int64)
     consumed = int(data_len[etype != 0].sum())
     data = rng.integers(0, 256, consumed, dtype=np.uint8)
     peer_xor = (rng.integers(0, 1 << 62, N).astype(np.uint64) * (etype == 3)).astype(np.uint64)

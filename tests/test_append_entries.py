@@ -57,3 +57,57 @@ def test_gpu_empty_requests(engine, oracle):
     req_off = np.array([0, 0, 0], np.uint32)
     out, cor, first = engine.append_entries_verify(req_off, [5, 6], [], [], [], [], None)
     assert list(first) == [-1, -1] and out.size == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,per,L,spoil", [(16, 256, 16384, None), (200, 1024, 256, None),
+                                          (16, 256, 16384, "length"), (16, 256, 16384, "unknown"),
+                                          (16, 256, 16384, "misaligned")])
+def test_gpu_uniform_entries(engine, oracle, R, per, L, spoil):
+    """Batches of one entry length, none UNKNOWN (a client's fixed-size commands: 16 KiB and
+    256-B entries), and the same batches spoiled: one entry one byte shorter, one entry UNKNOWN,
+    or (device entry point) a payload 8 bytes past a 16-B boundary.  All against the oracle,
+    corrupt flags included.  (A fixed-size data path for such batches was measured and dropped
+    in r05: its gate and the early-returning walk launches cost what the fixed kernel saved.)"""
+    import torch
+    b = random_requests(R + L, R, per, L, oracle=oracle, uniform=L)
+    if spoil in ("length", "unknown"):
+        i = len(b["data_len"]) // 3
+        if spoil == "length":
+            b["data_len"][i] -= 1
+            b["data"] = np.delete(b["data"], int(b["data_len"][:i].sum()))
+        else:
+            b["etype"][i] = 0
+            b["data"] = np.delete(b["data"], np.arange(int(b["data_len"][:i].sum()),
+                                                       int(b["data_len"][:i + 1].sum())))
+        good, _, _ = oracle.append_entries_verify(b["req_off"], b["prev_log_index"], b["term"],
+                                                  b["etype"], b["data_len"], b["checksum"],
+                                                  b["data"], has_checksum=np.zeros(len(b["term"]), np.uint8),
+                                                  peer_xor=b["peer_xor"])
+        b["checksum"] = good
+        b["checksum"][::97] ^= np.uint64(1)
+    args = (b["req_off"], b["prev_log_index"], b["term"], b["etype"], b["data_len"],
+            b["checksum"], b["data"])
+    kw = dict(has_checksum=b["has_checksum"], peer_xor=b["peer_xor"])
+    e_out, e_cor, e_first = oracle.append_entries_verify(*args, **kw)
+    assert e_cor.any()
+    if spoil != "misaligned":
+        g_out, g_cor, g_first = engine.append_entries_verify(*args, **kw)
+    else:  # the device entry point on a payload 8 bytes past a 16-B boundary
+        dev = torch.device("cuda:0")
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a.view(np.int64) if a.dtype == np.uint64 else a)).to(dev)
+        buf = torch.zeros(b["data"].size + 16, dtype=torch.uint8, device=dev)
+        buf[8:8 + b["data"].size] = torch.from_numpy(b["data"]).to(dev)
+        N, Rr = len(b["term"]), len(b["prev_log_index"])
+        out = torch.empty(N, dtype=torch.int64, device=dev)
+        cor = torch.empty(N, dtype=torch.uint8, device=dev)
+        first = torch.empty(Rr, dtype=torch.int32, device=dev)
+        engine.append_entries_verify_dev(t(b["req_off"].view(np.int32)), t(b["prev_log_index"]), t(b["term"]),
+                                         t(b["etype"]), t(b["data_len"]), t(b["checksum"]), buf[8:],
+                                         out, cor, first, has_checksum=t(b["has_checksum"]),
+                                         peer_xor=t(b["peer_xor"]))
+        engine.synchronize()
+        g_out, g_cor, g_first = out.cpu().numpy().view(np.uint64), cor.cpu().numpy(), first.cpu().numpy()
+    np.testing.assert_array_equal(g_out, e_out)
+    np.testing.assert_array_equal(g_cor, e_cor)
+    np.testing.assert_array_equal(g_first, e_first)
