@@ -362,7 +362,8 @@ def test_gpu_quorum_epochs_tiles_full_c3(engine):
         engine.quorum_epochs_tiles_launcher(tiles, 5, G - 1, c2, s2)()
 
 
-@pytest.mark.parametrize("P,G,K", [(3, 1000, 9), (5, 777, 40), (2, 64, 1), (3, 130, 200)])
+@pytest.mark.parametrize("P,G,K", [(3, 1000, 9), (5, 777, 40), (2, 64, 1), (3, 130, 200),
+                                   (16, 300, 70), (9, 500, 200), (1, 100, 300), (16, 40, 193)])
 def test_gpu_quorum_epochs_with_runs(engine, oracle, P, G, K):
     """K epochs in one launch with conf runs and flagged groups == K sequential replays."""
     import torch
