@@ -85,12 +85,10 @@ def host_np(t):
 
 def csrc_sha() -> str:
     """Content hash of the kernel sources: a committed PMC summary is cited only when it was
-    collected from these exact kernels (tools/summarize_profiles.py writes the same hash)."""
-    h = hashlib.sha256()
-    for f in sorted(glob.glob(os.path.join(ROOT, "sofa-jraft_amd", "csrc", "*"))):
-        with open(f, "rb") as fh:
-            h.update(os.path.basename(f).encode() + b"\0" + fh.read())
-    return h.hexdigest()[:16]
+    collected from these exact kernels (tools/summarize_profiles.py writes the same hash), and
+    the library must carry the same hash as its jrq_build_id() (main() checks)."""
+    from jraft_amd._srcsha import src_sha
+    return src_sha()
 
 
 def pmc_traffic(leg: str, *kernels: str):
@@ -456,19 +454,33 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
     status = torch.empty(G, dtype=torch.uint8, device=dev)
     # one GPU: the local committed[] already is the node-wide snapshot (nothing to gather)
     snapshot = torch.empty(k * world, dtype=torch.int64, device=dev) if world > 1 else local
-    nranks = 1
-    publish_via = "none (one GPU)"
-    if world > 1 and ctx.backend == "nccl":
+    def rccl_init():
         uid = [Engine.rccl_unique_id() if rank == 0 else None]
         import torch.distributed as dist
         dist.broadcast_object_list(uid, src=0)
+        if os.environ.get("JRAFT_AMD_INJECT_RCCL_FAIL"):  # tests of the fallback
+            raise RuntimeError("injected jrq_rccl_init failure (JRAFT_AMD_INJECT_RCCL_FAIL)")
         eng.rccl_init(world, rank, uid[0])
-        nranks = eng.rccl_nranks()
-        publish_via = "RCCL all-gather (jrq_publish_committed_dev)"
-    elif world > 1:
+        return eng.rccl_nranks()
+
+    def pg_publish(send, recv):
         import torch.distributed as dist
-        nranks = dist.get_world_size()
-        publish_via = "gloo all-gather of host copies (several ranks on one GPU: no RCCL)"
+        if ctx.backend == "nccl":  # device tensors through the process group (RCCL via torch)
+            dist.all_gather_into_tensor(recv, send)
+            return
+        ctx.sync()
+        h = torch.empty(send.numel() * world, dtype=send.dtype)
+        dist.all_gather_into_tensor(h, send.cpu())
+        recv.copy_(h.to(recv.device))
+
+    def agree(ok):
+        import torch.distributed as dist
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=ctx.coll_device())
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    publish_fn, pub_info = D.choose_publish(world, ctx.backend, rccl_init, eng.publish_committed_dev,
+                                            pg_publish, agree)
 
     # one prepared launch per epoch buffer (arguments resolved once, as a C / JNI host keeps
     # its jrq_group_batch): the step loop then costs the GPU epoch, not Python marshalling
@@ -488,14 +500,8 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
                              t["last_committed"], t["conf"], out, status)
 
     def allgather(send, recv):
-        if world > 1 and ctx.backend == "nccl":
-            eng.publish_committed_dev(send, recv)
-        elif world > 1:
-            import torch.distributed as dist
-            ctx.sync()
-            h = torch.empty(send.numel() * world, dtype=send.dtype)
-            dist.all_gather_into_tensor(h, send.cpu())
-            recv.copy_(h.to(recv.device))
+        if publish_fn is not None:
+            publish_fn(send, recv)
     se = D.ShardedEpochs(Gtot, world, rank, epoch_fn, allgather, local, snapshot,
                          publish_every=args.publish_every)
     # kernel only (HIP events on the engine's stream)
@@ -547,7 +553,7 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
                        **pmc_traffic("quorum", "quorum_epoch_pair_kernel<5, false, false>"))
     return {
         "value": value, "elapsed": elapsed, "cfg": cfg, "G": G, "P": P, "roofline": rl,
-        "multi_gpu": {"rccl_nranks": nranks, "publish_via": publish_via,
+        "multi_gpu": {**pub_info,
                       "publish_every": args.publish_every,
                       "kernel_only_ms": k_ms_max, "publish_ms": pub_ms,
                       "kernel_plus_publish_ms": elapsed * 1e3 / args.steps,
@@ -1639,6 +1645,7 @@ def compact_line(full: dict, detail_path: str | None = DETAIL_FILE) -> dict:
     line = {k: _r(full.get(k), 6) if k in ("value", "ms_per_step") else full.get(k) for k in keys}
     line["warm_ms"] = full.get("warm_ms")
     line["csrc_sha"] = full.get("csrc_sha")
+    line["lib_sha"] = full.get("lib_sha")  # jrq_build_id() of the library that ran
     line["roofline"] = _roof_summary(full.get("roofline"))
     line["cpu_baseline"] = _cpu_summary(full.get("cpu_baseline"))
     mg = full.get("multi_gpu")
@@ -1803,6 +1810,8 @@ def main():
         return float(t.item())
 
     eng = Engine(local)
+    from jraft_amd import _lib
+    lib_sha = _lib.check_build_id()  # raises unless libjrq.so was built from these csrc/
     # a dedicated (non-default) stream: the kernels and the HIP events bracketing them
     # must be on the same stream (the default stream's handle is 0 = "engine's own")
     stream = torch.cuda.Stream(dev)
@@ -1815,7 +1824,7 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "warm_ms": WARM_MS, "ms_per_step": None,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
             "data": "synthetic (seeded splitmix64, SURVEY.md §8d)", "legs": sorted(legs),
-            "csrc_sha": csrc_sha()}
+            "csrc_sha": csrc_sha(), "lib_sha": lib_sha}
     G = args.groups_per_gpu
     from jraft_amd import workloads as W
     if "quorum" in legs:

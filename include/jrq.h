@@ -123,6 +123,10 @@ jrq_engine *jrq_create(int device, uint32_t max_groups, uint8_t max_peers, int *
 void jrq_destroy(jrq_engine *e);
 
 int jrq_abi_version(void);
+/* Content hash of the kernel sources this library was compiled from (16 hex digits: SHA-256 of
+ * the files in csrc/, sofa-jraft_amd/jraft_amd/_srcsha.py), so a host can tell which sources made the binary
+ * it loaded.  No reference counterpart. */
+const char *jrq_build_id(void);
 /* Text of the last error on this engine (or of jrq_create's last failure when e==NULL). */
 const char *jrq_last_error(const jrq_engine *e);
 /* hipStream_t the engine launches on (as void*); jrq_set_stream adopts an external

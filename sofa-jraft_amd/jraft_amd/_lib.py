@@ -95,6 +95,7 @@ def rec(group, field, v):
 _V = C.c_void_p
 SIGNATURES = [
     ("jrq_abi_version", C.c_int, []),
+    ("jrq_build_id", C.c_char_p, []),
     ("jrq_last_error", C.c_char_p, [_V]),
     ("jrq_create", _V, [C.c_int, C.c_uint32, C.c_uint8, C.POINTER(C.c_int)]),
     ("jrq_destroy", None, [_V]),
@@ -194,6 +195,23 @@ def load() -> C.CDLL:
             fn.argtypes = args
         _lib = lib
     return _lib
+
+
+def build_id() -> str:
+    """jrq_build_id() of the loaded library: the hash of the kernel sources it was built from."""
+    return load().jrq_build_id().decode()
+
+
+def check_build_id() -> str:
+    """The loaded library's build id; raises unless it is the hash of the csrc/ beside it (the
+    binary that runs is the one these sources make).  A/B variant libraries
+    (JRAFT_AMD_AB_LIB) are built from edited copies and are exempt."""
+    from ._srcsha import src_sha
+    lib_sha, tree_sha = build_id(), src_sha()
+    if lib_sha != tree_sha and not os.environ.get("JRAFT_AMD_AB_LIB"):
+        raise RuntimeError(f"libjrq.so was built from other sources (jrq_build_id {lib_sha}, "
+                           f"csrc/ hash {tree_sha}): rebuild with __graft_entry__.build()")
+    return lib_sha
 
 
 def check(rc: int, engine_handle=None) -> None:

@@ -64,3 +64,12 @@ def test_create_fails_loudly_without_gpu():
     from jraft_amd import Engine, JrqError
     with pytest.raises(JrqError):
         Engine(0)
+
+
+def test_library_names_its_sources():
+    """jrq_build_id() is the content hash of csrc/ (VERDICT r05 weak #7): the library that the
+    GPU runs load was compiled from the sources in this tree."""
+    from jraft_amd._srcsha import lib_build_id, src_sha
+    assert lib_build_id(_lib.LIB_PATH) == src_sha()
+    assert _lib.build_id() == src_sha()
+    assert _lib.check_build_id() == src_sha()

