@@ -420,7 +420,7 @@ class Ctx:
         t = torch.zeros(self.world, dtype=torch.float64, device=self.coll_device())
         t[self.rank] = x
         dist.all_reduce(t)
-        return [float(v) for v in t.cpu()]
+        return [float(v) for v in (host_np(t) if t.is_cuda else t.numpy())]
 
     def timed(self, fn, steps=None, warmup=None, warm_calls=None):
         a = self.args
@@ -470,8 +470,8 @@ def leg_quorum(ctx, args, barrier, max_over_ranks):
             return
         ctx.sync()
         h = torch.empty(send.numel() * world, dtype=send.dtype)
-        dist.all_gather_into_tensor(h, send.cpu())
-        recv.copy_(h.to(recv.device))
+        dist.all_gather_into_tensor(h, torch.from_numpy(host_np(send)))
+        recv.copy_(to_dev(h.numpy(), recv.device))
 
     def agree(ok):
         import torch.distributed as dist

@@ -253,9 +253,11 @@ int jrq_quorum_epochs_tiles_dev(jrq_engine *e, const jrq_group_tiles *in_dev, ui
  * BallotBox.java:131-132), so a commit writes one word of state.
  * Match base: pendingIndex - 1 rounded down to a multiple of 2^JRQ_TABLE_MATCH_PAGE (0 when not
  * the leader); a slot's word is its match minus the base, 0 for a match below the base (it
- * grants no pending entry either way).  Headers with a negative pendingIndex, one >= 2^62, or a
- * pending queue longer than 2^31 - 1 entries (a Java ArrayList's bound) are refused as invalid,
- * as are lastAppended records with v > 2^31 - 1. */
+ * grants no pending entry either way).  Headers with a negative pendingIndex, one >= 2^62, a
+ * lastAppended below pendingIndex - 1, or a pending queue longer than 2^31 - 1 entries (a Java
+ * ArrayList's bound) are refused as invalid, as are lastAppended records with v > 2^31 - 1.  A
+ * header without JRQ_STATE_RESET_MATCH that lowers the match base (never one the BallotBox API
+ * produces: resetPendingIndex resets the matches) keeps words at 0 at 0: no grant is invented. */
 #define JRQ_TABLE_MATCH_PAGE 30
 #define JRQ_TABLE_MAX_RUNS 4            /* conf runs per pending window (NodeImpl has <= 2) */
 #define JRQ_TABLE_MAX_GROUPS (1u << 27) /* groups per table (27-bit group ids in records) */

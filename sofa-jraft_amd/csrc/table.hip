@@ -616,8 +616,10 @@ __global__ __launch_bounds__(256) void table_states_kernel(JrqTableArgs t, const
   // pending entries but no conf run (conf word 0 = quorum 0, which would grant every entry), a
   // negative pendingIndex or one past 2^62, and a pending queue longer than a Java ArrayList
   // holds (2^31 - 1: the u32 match words rely on it)
+  // lastAppended below pendingIndex - 1 (a queue of negative size, which no BallotBox holds: the
+  // epoch's u32 out-of-range test assumes lastAppended >= the match base)
   if (g >= t.G || nr > kTableMaxRuns || (nr == 0 && pi != 0 && st.last_appended >= pi) || pi < 0 ||
-      pi >= (int64_t{1} << 62) ||
+      pi >= (int64_t{1} << 62) || (pi > 0 && st.last_appended < pi - 1) ||
       (pi > 0 && st.last_appended >= pi && st.last_appended - pi >= int64_t{0x7FFFFFFF})) {
     atomicAdd(t.invalid, 1u);
     return;
@@ -645,11 +647,17 @@ __global__ __launch_bounds__(256) void table_states_kernel(JrqTableArgs t, const
       const uint32_t v = tm(t, p, g);
       tm(t, p, g) = v > d ? static_cast<uint32_t>(v - d) : 0u;
     }
-  } else if (b1 < b0) {  // (a lower base: words saturate; only a non-leader's, which no one reads)
+  } else if (b1 < b0) {
+    // A lower base without RESET_MATCH (outside the host's contract: within a leadership
+    // pendingIndex only grows, Replicator.java:1387-1401; resetPendingIndex resets the matches).
+    // A word of 0 means "at or below the old base" -- its true match is unknown, so it stays 0
+    // under the new base (never grants) instead of reading back as exactly the old base, which
+    // could count as an ack of entries no peer acknowledged.  Others saturate.
     const uint64_t d = static_cast<uint64_t>(b0 - b1);
     for (uint32_t p = 0; p < t.P; ++p) {
-      const uint64_t v = tm(t, p, g) + d;
-      tm(t, p, g) = v > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(v);
+      const uint32_t w0 = tm(t, p, g);
+      const uint64_t v = w0 + d;
+      tm(t, p, g) = w0 == 0 ? 0u : v > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(v);
     }
   }
 }

@@ -1548,6 +1548,8 @@ LeaderTicker::LeaderTicker(Engine& eng, uint32_t groups, uint32_t peers)
   arrivals_.assign(G_, 0);
   peers_.resize(G_);
   reads_.resize(G_);
+  waiting_.resize(G_);
+  round_.assign(G_, 0);
 }
 
 int LeaderTicker::slot(uint32_t g, const PeerId& peer) const {
@@ -1584,12 +1586,21 @@ void LeaderTicker::becomeLeader(uint32_t g, const Configuration& conf, const Con
     conf_[g] = JRQ_CONF(nm, om, nn / 2 + 1, no ? no / 2 + 1 : 0);
     for (uint32_t s = 0; s < P_; ++s) ts_[static_cast<size_t>(s) * G_ + g] = nowMs;
     lease_[g] = nowMs;
-    order_[g] = 0;
-    okMask_[g] = 0;
-    arrivals_[g] = 0;
-    failed.swap(reads_[g]);
+    closeRound(g, failed);
   }
   for (auto& f : failed) f(false);
+}
+
+// the group's open round and queued reads end (their closures go to `out`)
+void LeaderTicker::closeRound(uint32_t g, std::vector<std::function<void(bool)>>& out) {
+  for (auto& f : reads_[g]) out.push_back(std::move(f));
+  for (auto& f : waiting_[g]) out.push_back(std::move(f));
+  reads_[g].clear();
+  waiting_[g].clear();
+  round_[g] = 0;
+  order_[g] = 0;
+  okMask_[g] = 0;
+  arrivals_[g] = 0;
 }
 
 void LeaderTicker::stepDown(uint32_t g) {
@@ -1597,10 +1608,7 @@ void LeaderTicker::stepDown(uint32_t g) {
   {
     std::lock_guard<std::mutex> l(mu_);
     conf_[g] = 0;
-    failed.swap(reads_[g]);
-    order_[g] = 0;
-    okMask_[g] = 0;
-    arrivals_[g] = 0;
+    closeRound(g, failed);
   }
   for (auto& f : failed) f(false);
 }
@@ -1612,19 +1620,32 @@ void LeaderTicker::onRpcSent(uint32_t g, const PeerId& peer, int64_t nowMs) {
 }
 
 void LeaderTicker::readIndex(uint32_t g, std::function<void(bool)> done) {
-  bool fail = false;
+  int answer = -1;  // -1 queued, 0 false, 1 true
   {
     std::lock_guard<std::mutex> l(mu_);
-    if (conf_[g] == 0) fail = true;  // not the leader: readLeader fails (EPERM)
-    else reads_[g].push_back(std::move(done));
+    if (g >= G_ || conf_[g] == 0) answer = 0;                    // not the leader (EPERM)
+    else if (((conf_[g] >> 32) & 0xFFu) <= 1) answer = 1;        // quorum <= 1: fast path
+    else waiting_[g].push_back(std::move(done));
   }
-  if (fail) done(false);
+  if (answer >= 0) done(answer == 1);
 }
 
-void LeaderTicker::onHeartbeatResponse(uint32_t g, const PeerId& peer, bool success) {
+uint64_t LeaderTicker::startReadRound(uint32_t g) {
   std::lock_guard<std::mutex> l(mu_);
+  if (g >= G_ || conf_[g] == 0 || round_[g] != 0 || waiting_[g].empty()) return 0;
+  reads_[g].swap(waiting_[g]);
+  order_[g] = 0;
+  okMask_[g] = 0;
+  arrivals_[g] = 0;
+  round_[g] = ++roundSeq_;
+  return round_[g];
+}
+
+void LeaderTicker::onHeartbeatResponse(uint32_t g, uint64_t round, const PeerId& peer, bool success) {
+  std::lock_guard<std::mutex> l(mu_);
+  if (g >= G_ || round == 0 || round != round_[g]) return;  // another round's response
   const int s = slot(g, peer);
-  if (s < 0 || reads_[g].empty() || ((order_[g] >> (4 * s)) & 0xFu) != 0) return;  // one response per peer
+  if (s < 0 || ((order_[g] >> (4 * s)) & 0xFu) != 0) return;  // one response per peer
   const uint32_t pos = arrivals_[g] < 15 ? ++arrivals_[g] : 15u;
   order_[g] |= static_cast<uint64_t>(pos) << (4 * s);
   if (success) okMask_[g] |= static_cast<uint16_t>(1u << s);
@@ -1643,10 +1664,11 @@ uint32_t LeaderTicker::tick(int64_t nowMs, int64_t leaseTimeoutMs, const StepDow
                  eng_->raw(), "jrq_leader_tick");
     for (uint32_t g = 0; g < G_; ++g) {
       if (conf_[g] == 0) continue;  // not a leader
-      if (!reads_[g].empty() && ri[g] != JRQ_READINDEX_PENDING) {
+      if (round_[g] != 0 && ri[g] != JRQ_READINDEX_PENDING) {  // the open round is decided
         const bool good = ri[g] == JRQ_READINDEX_SUCCESS;
         for (auto& f : reads_[g]) done.emplace_back(std::move(f), good);
         reads_[g].clear();
+        round_[g] = 0;  // its late responses are dropped from now on
         order_[g] = 0;
         okMask_[g] = 0;
         arrivals_[g] = 0;
@@ -1654,8 +1676,9 @@ uint32_t LeaderTicker::tick(int64_t nowMs, int64_t leaseTimeoutMs, const StepDow
       if (ok[g] != 3) {  // "Majority of the group dies": step down
         downs.emplace_back(g, dead[g]);
         conf_[g] = 0;
-        for (auto& f : reads_[g]) done.emplace_back(std::move(f), false);
-        reads_[g].clear();
+        std::vector<std::function<void(bool)>> failed;
+        closeRound(g, failed);
+        for (auto& f : failed) done.emplace_back(std::move(f), false);
       }
     }
   }

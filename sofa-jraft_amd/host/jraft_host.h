@@ -262,11 +262,22 @@ class LeaderTicker {
   void stepDown(uint32_t g);  // not checked any more; an open ReadIndex round fails
   // Replicator: an RPC to `peer` left (its lastRpcSendTimestamp)
   void onRpcSent(uint32_t g, const PeerId& peer, int64_t nowMs);
-  // readLeader, ReadOnlySafe: join the group's open heartbeat round (or start one); done runs
-  // once with the round's verdict (true: the read index may be served)
+  // readLeader, ReadOnlySafe (NodeImpl.java:1343-1396): queue a read for the group's NEXT
+  // heartbeat round; done runs once with that round's verdict (true: the read index may be
+  // served).  A conf whose quorum is <= 1 answers true at once (readLeader's fast path,
+  // :1345-1352); a group that is not the leader answers false at once.  A read never joins a
+  // round whose heartbeats were already sent: every response that confirms it left its peer
+  // after the read arrived (the reference sends a fresh round per readLeader call, :1386-1394).
   void readIndex(uint32_t g, std::function<void(bool)> done);
-  // a heartbeat response of the open round (success = response.getSuccess())
-  void onHeartbeatResponse(uint32_t g, const PeerId& peer, bool success);
+  // Open the group's next round if reads are queued and no round is open: the queued reads
+  // become the round's, and the returned id (nonzero, unique per ticker) tags the heartbeats
+  // the host now sends to every conf peer but the leader.  0: nothing to send now.  A host
+  // calls it after readIndex and after every tick (a decided round leaves the next one to open).
+  uint64_t startReadRound(uint32_t g);
+  // A heartbeat response (success = response.getSuccess()) carrying the round id its request
+  // was sent with.  Responses of any other round -- one already decided, or a stale retry --
+  // are dropped, so a late response never counts toward a later round.
+  void onHeartbeatResponse(uint32_t g, uint64_t round, const PeerId& peer, bool success);
   // One pass over every leader group: groups without an alive quorum call stepDown (then
   // stop being checked), decided ReadIndex rounds run their closures.  Returns the groups
   // that failed the lease check.
@@ -276,6 +287,7 @@ class LeaderTicker {
 
  private:
   int slot(uint32_t g, const PeerId& peer) const;
+  void closeRound(uint32_t g, std::vector<std::function<void(bool)>>& out);
   Engine* eng_;
   uint32_t G_, P_;
   mutable std::mutex mu_;
@@ -287,7 +299,10 @@ class LeaderTicker {
   std::vector<uint16_t> okMask_;     // [G]
   std::vector<uint8_t> arrivals_;    // [G] responses in the open round so far
   std::vector<std::vector<uint32_t>> peers_;  // [G] interned peer of each slot
-  std::vector<std::vector<std::function<void(bool)>>> reads_;  // [G] open round's closures
+  std::vector<std::vector<std::function<void(bool)>>> reads_;    // [G] open round's closures
+  std::vector<std::vector<std::function<void(bool)>>> waiting_;  // [G] reads for the next round
+  std::vector<uint64_t> round_;      // [G] id of the open round (0: none)
+  uint64_t roundSeq_ = 0;            // last round id handed out
 };
 
 // --------------------------------------------------------------- ballot box

@@ -1096,12 +1096,14 @@ static void testLeaderTickerOnGpu(Engine& eng) {
     }
     if (g % 3 == 0) {  // a ReadIndex round with some responses in a random order
       lt.readIndex(g, [&verdict, g](bool ok) { verdict[g] = ok ? 1 : 0; });
+      const uint64_t round = lt.startReadRound(g);
+      CHECK(round != 0);
       std::vector<int> peers;
       for (uint32_t p = 1; p < n; ++p) if (rng() % 4) peers.push_back(static_cast<int>(p));
       std::shuffle(peers.begin(), peers.end(), rng);
       for (int p : peers) {
         const bool okr = rng() % 10 < 6;
-        lt.onHeartbeatResponse(g, ps[p], okr);
+        lt.onHeartbeatResponse(g, round, ps[p], okr);
         e.order.push_back(p);
         if (okr) e.okm |= 1u << p;
       }
@@ -1139,6 +1141,78 @@ static void testLeaderTickerOnGpu(Engine& eng) {
   const size_t before = downs.size();
   lt.tick(now, lease, [&](uint32_t g, uint16_t dead) { downs.emplace_back(g, dead); });
   CHECK(downs.size() == before);
+}
+
+// every response that confirms a read left its peer after the read arrived,
+// as in the reference, where each readLeader call sends its own heartbeat round
+// (NodeImpl.java:1386-1394).  A read arriving after its group's round was sent waits for the
+// next round; a late response of a decided round never counts toward the next one; a
+// single-voter group answers at once (readLeader's quorum <= 1 fast path, :1345-1352).
+static void testReadIndexRounds(Engine& eng) {
+  const uint32_t G = 4, P = 5;
+  LeaderTicker lt(eng, G, P);
+  std::vector<PeerId> ps;
+  for (uint32_t p = 0; p < 5; ++p) ps.emplace_back("10.3.0.1", static_cast<int32_t>(7100 + p));
+  Configuration c5, c1;
+  c5.peers.assign(ps.begin(), ps.end());  // quorum 3: the leader + 2 successes
+  c1.peers = {ps[0]};
+  const int64_t t0 = 1000;
+  for (uint32_t g = 0; g < 3; ++g) lt.becomeLeader(g, c5, nullptr, ps[0], t0);
+  lt.becomeLeader(3, c1, nullptr, ps[0], t0);
+  auto tick = [&] { lt.tick(t0 + 10, 1000, nullptr); };
+  // (a) a read joining mid-round waits for the next round
+  int first = -1, late = -1;
+  lt.readIndex(0, [&](bool ok) { first = ok; });
+  const uint64_t r1 = lt.startReadRound(0);
+  CHECK(r1 != 0 && lt.startReadRound(0) == 0);  // one round open at a time
+  lt.onHeartbeatResponse(0, r1, ps[1], true);
+  lt.readIndex(0, [&](bool ok) { late = ok; });  // after r1 was sent and answered once
+  lt.onHeartbeatResponse(0, r1, ps[2], true);
+  tick();
+  CHECK(first == 1 && late == -1);  // r1's responses confirm only the read sent with r1
+  const uint64_t r2 = lt.startReadRound(0);
+  CHECK(r2 != 0 && r2 != r1);
+  tick();
+  CHECK(late == -1);  // no response of r2 yet
+  lt.onHeartbeatResponse(0, r2, ps[3], true);
+  lt.onHeartbeatResponse(0, r2, ps[4], true);
+  tick();
+  CHECK(late == 1);
+  // (b) a late response of a decided round is dropped
+  int a = -1, b = -1;
+  lt.readIndex(1, [&](bool ok) { a = ok; });
+  const uint64_t q1 = lt.startReadRound(1);
+  lt.onHeartbeatResponse(1, q1, ps[1], true);
+  lt.onHeartbeatResponse(1, q1, ps[2], true);
+  tick();
+  CHECK(a == 1);
+  lt.readIndex(1, [&](bool ok) { b = ok; });
+  const uint64_t q2 = lt.startReadRound(1);
+  lt.onHeartbeatResponse(1, q1, ps[3], true);  // stale: q1 is decided
+  lt.onHeartbeatResponse(1, q1, ps[4], true);
+  lt.onHeartbeatResponse(1, q2, ps[1], true);  // one success of q2 only: not a quorum
+  tick();
+  CHECK(b == -1);
+  lt.onHeartbeatResponse(1, q2, ps[2], false);
+  lt.onHeartbeatResponse(1, q2, ps[3], false);
+  lt.onHeartbeatResponse(1, q2, ps[4], false);
+  tick();
+  CHECK(b == 0);  // q2 failed: 3 failures >= failPeersThreshold 3
+  // (c) a step-down fails the open round and the queued reads
+  int o = -1, w = -1;
+  lt.readIndex(2, [&](bool ok) { o = ok; });
+  const uint64_t s1 = lt.startReadRound(2);
+  lt.readIndex(2, [&](bool ok) { w = ok; });
+  lt.stepDown(2);
+  CHECK(o == 0 && w == 0);
+  lt.onHeartbeatResponse(2, s1, ps[1], true);  // after the step-down: ignored
+  int x = -1;
+  lt.readIndex(2, [&](bool ok) { x = ok; });
+  CHECK(x == 0 && lt.startReadRound(2) == 0);
+  // (d) quorum <= 1: at once, no round
+  int one = -1;
+  lt.readIndex(3, [&](bool ok) { one = ok; });
+  CHECK(one == 1 && lt.startReadRound(3) == 0);
 }
 
 // FSMCallerImpl.doCommitted for many groups through FSMCallerBatch (one jrq_commit_fanout per
@@ -1248,6 +1322,7 @@ int main(int argc, char** argv) {
     tests.push_back({"testFollowerVerifierOnGpu", [&] { testFollowerVerifierOnGpu(e); }});
     tests.push_back({"testLogReaderOnGpu", [&] { testLogReaderOnGpu(e); }});
     tests.push_back({"testLeaderTickerOnGpu", [&] { testLeaderTickerOnGpu(e); }});
+    tests.push_back({"testReadIndexRounds", [&] { testReadIndexRounds(e); }});
     tests.push_back({"testFSMCallerBatchOnGpu", [&] { testFSMCallerBatchOnGpu(e); }});
   }
   for (auto& t : tests) {

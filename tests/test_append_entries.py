@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 
 from ae_cases import random_requests
+from devio import to_dev, host_np
 
 
 def test_oracle_follows_reference_loop(oracle):
@@ -95,9 +96,9 @@ def test_gpu_uniform_entries(engine, oracle, R, per, L, spoil):
         g_out, g_cor, g_first = engine.append_entries_verify(*args, **kw)
     else:  # the device entry point on a payload 8 bytes past a 16-B boundary
         dev = torch.device("cuda:0")
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a.view(np.int64) if a.dtype == np.uint64 else a)).to(dev)
+        t = lambda a: to_dev(np.ascontiguousarray(a.view(np.int64) if a.dtype == np.uint64 else a), dev)
         buf = torch.zeros(b["data"].size + 16, dtype=torch.uint8, device=dev)
-        buf[8:8 + b["data"].size] = torch.from_numpy(b["data"]).to(dev)
+        buf[8:8 + b["data"].size] = to_dev(b["data"], dev)
         N, Rr = len(b["term"]), len(b["prev_log_index"])
         out = torch.empty(N, dtype=torch.int64, device=dev)
         cor = torch.empty(N, dtype=torch.uint8, device=dev)
@@ -107,7 +108,7 @@ def test_gpu_uniform_entries(engine, oracle, R, per, L, spoil):
                                          out, cor, first, has_checksum=t(b["has_checksum"]),
                                          peer_xor=t(b["peer_xor"]))
         engine.synchronize()
-        g_out, g_cor, g_first = out.cpu().numpy().view(np.uint64), cor.cpu().numpy(), first.cpu().numpy()
+        g_out, g_cor, g_first = host_np(out).view(np.uint64), host_np(cor), host_np(first)
     np.testing.assert_array_equal(g_out, e_out)
     np.testing.assert_array_equal(g_cor, e_cor)
     np.testing.assert_array_equal(g_first, e_first)

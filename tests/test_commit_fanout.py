@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import jraft_oracle as O
+from devio import to_dev, host_np
 
 I64_MIN = np.iinfo(np.int64).min
 
@@ -185,7 +186,7 @@ def test_gpu_fanout_after_quorum_epoch_dev(engine):
     b = W.quorum_batch("C3", groups=20_000)
     G = b["pending_index"].shape[0]
     dev = torch.device("cuda", 0)
-    t = {k: torch.from_numpy(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v)).to(dev)
+    t = {k: to_dev(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v), dev)
          for k, v in b.items() if isinstance(v, np.ndarray)}
     committed = torch.empty(G, dtype=torch.int64, device=dev)
     status = torch.empty(G, dtype=torch.uint8, device=dev)
@@ -196,28 +197,28 @@ def test_gpu_fanout_after_quorum_epoch_dev(engine):
     cq_first = b["pending_index"].copy()
     cq_size = (b["last_appended"] - b["pending_index"] + 1).astype(np.int64)
     la[rng.random(G) < 0.1] += 10_000
-    d_la = torch.from_numpy(la).to(dev)
-    d_cf = torch.from_numpy(cq_first).to(dev)
-    d_cs = torch.from_numpy(cq_size).to(dev)
+    d_la = to_dev(la, dev)
+    d_cf = to_dev(cq_first, dev)
+    d_cs = to_dev(cq_size, dev)
     fc = torch.empty(G, dtype=torch.int64, device=dev)
     st = torch.empty(G, dtype=torch.uint8, device=dev)
     listed = torch.empty((G + 63) // 64, dtype=torch.int64, device=dev)
     num = torch.full((1,), 12345, dtype=torch.int32, device=dev)  # the launch resets it
     engine.commit_fanout_dev(t["last_committed"], committed, d_la, d_cf, d_cs, fc, st, listed, num)
     engine.synchronize()
-    c = committed.cpu().numpy()
+    c = host_np(committed)
     seq_off = np.zeros(G + 1, np.uint64)
     adv = c > b["last_committed"]
     seq_off[1:] = np.cumsum(adv)
     est, efc, _, ecf, ecs, elisted = oracle_epoch(dict(seq_off=seq_off, seq=c[adv], last_applied=la,
                                                        cq_first=cq_first, cq_size=cq_size))
-    assert np.array_equal(st.cpu().numpy(), est)
-    assert np.array_equal(fc.cpu().numpy(), efc)
-    assert np.array_equal(d_cf.cpu().numpy(), ecf)
-    assert np.array_equal(d_cs.cpu().numpy(), ecs)
+    assert np.array_equal(host_np(st), est)
+    assert np.array_equal(host_np(fc), efc)
+    assert np.array_equal(host_np(d_cf), ecf)
+    assert np.array_equal(host_np(d_cs), ecs)
     from jraft_amd.engine import listed_ids
     assert int(num.item()) == len(elisted)
-    assert np.array_equal(listed_ids(listed.cpu().numpy(), G), elisted)
+    assert np.array_equal(listed_ids(host_np(listed), G), elisted)
     assert (est == O.FAN_APPLY).sum() > G // 2
 
 

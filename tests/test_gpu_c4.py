@@ -19,6 +19,7 @@ import socket
 
 import numpy as np
 import pytest
+from devio import to_dev, host_np, host_t
 
 pytestmark = pytest.mark.gpu
 
@@ -64,7 +65,7 @@ def test_c4_eight_shards_one_gpu(oracle):
         for rank in range(WORLD):
             batches = [W.quorum_batch("C4", groups=G_RANK, group_offset=rank * G_RANK,
                                       seed=_seed("C4", e)) for e in range(K)]
-            dbs = [{n: torch.from_numpy(v).to(dev) for n, v in b.items()} for b in batches]
+            dbs = [{n: to_dev(v, dev) for n, v in b.items()} for b in batches]
             local = torch.full((k,), -1, dtype=torch.int64, device=dev)
             status = torch.empty(G_RANK, dtype=torch.uint8, device=dev)
 
@@ -84,10 +85,10 @@ def test_c4_eight_shards_one_gpu(oracle):
                 se.step()
             eng.synchronize()
             assert se.published == K
-            got = local.cpu().numpy()
+            got = host_np(local)
             committed_total += _check_shard(oracle, batches[(K - 1) % K], got,
-                                            status.cpu().numpy(), rank)
-        snap = D.unpad_snapshot(snapshot.cpu().numpy(), Gtot, WORLD)
+                                            host_np(status), rank)
+        snap = D.unpad_snapshot(host_np(snapshot), Gtot, WORLD)
     assert snap.shape == (Gtot,)
     # every rank's block landed in groupId order: re-derive it from the shards' own seeds
     for rank in range(WORLD):
@@ -130,7 +131,7 @@ def _rank_proc(rank, world, port, G, K, q):
         Gtot = G * world
         k = D.per_rank(Gtot, world)
         with Engine(0, max_groups=G, max_peers=5) as eng:
-            dbs = [{n: torch.from_numpy(v).to(dev) for n, v in
+            dbs = [{n: to_dev(v, dev) for n, v in
                     W.quorum_batch("C4", groups=G, group_offset=rank * G,
                                    seed=_seed("C4", e)).items()} for e in range(K)]
             local = torch.full((k,), -1, dtype=torch.int64, device=dev)
@@ -144,7 +145,7 @@ def _rank_proc(rank, world, port, G, K, q):
 
             def allgather(send, recv):
                 eng.synchronize()
-                dist.all_gather_into_tensor(recv, send.cpu())
+                dist.all_gather_into_tensor(recv, host_t(send))
 
             se = D.ShardedEpochs(Gtot, world, rank, epoch_fn, allgather, local, snapshot)
             for _ in range(K):

@@ -12,6 +12,7 @@ import pytest
 
 from jraft_amd import _lib
 from jraft_amd import workloads as W
+from devio import to_dev, host_np
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
@@ -233,7 +234,7 @@ def test_fixed_dev_api(engine, oracle, el, n):
     expected[bad] ^= np.uint64(3)
 
     def t(a):
-        return torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(dev)
+        return to_dev(a.view(np.int64) if a.dtype == np.uint64 else a, dev)
     # a non-default torch stream shared with the engine: torch's default stream handle is 0,
     # which selects the engine's own stream (no ordering with the uploads)
     s = torch.cuda.Stream(dev)
@@ -249,9 +250,9 @@ def test_fixed_dev_api(engine, oracle, el, n):
         s.synchronize()
     finally:
         engine.use_stream(None)
-    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), exp)
-    np.testing.assert_array_equal(cor.cpu().numpy(), bad.astype(np.uint8))
-    np.testing.assert_array_equal(crc.cpu().numpy().view(np.uint64), oracle.crc64_batch(payload, offs))
+    np.testing.assert_array_equal(host_np(out).view(np.uint64), exp)
+    np.testing.assert_array_equal(host_np(cor), bad.astype(np.uint8))
+    np.testing.assert_array_equal(host_np(crc).view(np.uint64), oracle.crc64_batch(payload, offs))
 
 
 def test_device_path_c1_shape(engine, oracle):
@@ -260,7 +261,7 @@ def test_device_path_c1_shape(engine, oracle):
     n = 1 << 16
     b = W.entry_batch(n, 256, seed=11)
     dev = torch.device("cuda:0")
-    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v).to(dev)
+    t = {k: to_dev(v.view(np.int64) if v.dtype == np.uint64 else v, dev)
          for k, v in b.items() if isinstance(v, np.ndarray)}
     out = torch.zeros(n, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()  # the uploads went to torch's default stream; the engine uses its own
@@ -269,7 +270,7 @@ def test_device_path_c1_shape(engine, oracle):
     engine.synchronize()
     exp = oracle.logentry_checksum_batch(b["etype"], b["index"], b["term"], None, b["payload"],
                                          b["offsets"])
-    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), exp)
+    np.testing.assert_array_equal(host_np(out).view(np.uint64), exp)
 
 
 @pytest.mark.parametrize("cfg", ["C1", "C5"])
@@ -356,11 +357,11 @@ def test_stream_update_dev_resident_state(engine, oracle):
     for k in range(3):
         offs = W.ragged_offsets(500 + k, S, 3000)
         payload = W.random_bytes(600 + k, int(offs[-1]) + 1)
-        engine.crc64_stream_update_dev(reg, torch.from_numpy(payload).to(dev),
-                                       torch.from_numpy(offs.view(np.int64)).to(dev))
+        engine.crc64_stream_update_dev(reg, to_dev(payload, dev),
+                                       to_dev(offs.view(np.int64), dev))
         exp = oracle.crc64_stream_update(exp, payload, offs)
     torch.cuda.synchronize()
-    np.testing.assert_array_equal(reg.cpu().numpy().view(np.uint64), exp)
+    np.testing.assert_array_equal(host_np(reg).view(np.uint64), exp)
 
 
 def test_stream_update_errors_and_empty(engine):

@@ -8,6 +8,7 @@ import pytest
 from jraft_amd import ST_NOT_LEADER, conf_word
 from jraft_amd import workloads as W
 from quorum_cases import even_removal_batch, random_batch
+from devio import to_dev, host_np
 
 pytestmark = pytest.mark.gpu
 
@@ -85,16 +86,16 @@ def test_pair_and_scalar_paths(engine, oracle, G):
     dev = torch.device("cuda:0")
     wide = np.zeros((5, G + 1), np.int64)
     wide[:, :G] = b["match"]
-    tm = torch.from_numpy(wide).to(dev)[:, :G]  # row stride G + 1
-    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v).to(dev)
+    tm = to_dev(wide, dev)[:, :G]  # row stride G + 1
+    t = {k: to_dev(v.view(np.int64) if v.dtype == np.uint64 else v, dev)
          for k, v in b.items() if k in ("pending_index", "last_appended", "last_committed", "conf")}
     out = torch.empty(G, dtype=torch.int64, device=dev)
     st = torch.empty(G, dtype=torch.uint8, device=dev)
     engine.quorum_epoch_dev(tm, t["pending_index"], t["last_appended"], t["last_committed"],
                             t["conf"], out, st)
     engine.synchronize()
-    np.testing.assert_array_equal(out.cpu().numpy(), ce)
-    np.testing.assert_array_equal(st.cpu().numpy(), se)
+    np.testing.assert_array_equal(host_np(out), ce)
+    np.testing.assert_array_equal(host_np(st), se)
 
 
 @pytest.mark.parametrize("cfg,G", [("C2", None), ("C3", 2000)])
@@ -119,7 +120,7 @@ def test_full_c3_sampled_and_properties(engine, oracle):
     b = W.quorum_batch("C3")
     G = b["pending_index"].shape[0]
     dev = torch.device("cuda:0")
-    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v).to(dev)
+    t = {k: to_dev(v.view(np.int64) if v.dtype == np.uint64 else v, dev)
          for k, v in b.items()}
     committed = torch.empty(G, dtype=torch.int64, device=dev)
     status = torch.empty(G, dtype=torch.uint8, device=dev)
@@ -134,15 +135,15 @@ def test_full_c3_sampled_and_properties(engine, oracle):
         torch.cuda.synchronize()
     finally:
         engine.use_stream(None)
-    c = committed.cpu().numpy()
+    c = host_np(committed)
     assert (c >= b["last_committed"]).all() and (c <= b["last_appended"]).all()
-    np.testing.assert_array_equal(again.cpu().numpy(), c)
+    np.testing.assert_array_equal(host_np(again), c)
     rng = np.random.default_rng(3)
     idx = rng.choice(G, 4096, replace=False)
     sub = {k: (v[:, idx] if k == "match" else v[idx]) for k, v in b.items()}
     ce, se = _replay(oracle, sub, runs=False, chunk=1024)
     np.testing.assert_array_equal(c[idx], ce)
-    np.testing.assert_array_equal(status.cpu().numpy()[idx], se)
+    np.testing.assert_array_equal(host_np(status)[idx], se)
 
 
 def _series_oracle(s, K):
@@ -172,7 +173,7 @@ def test_gpu_quorum_epochs_series_vs_oracle(engine, cfg, G, K):
     s = W.quorum_epoch_series(cfg, K, groups=G)
     s["pending_index"][::97] = 0  # some groups are not the leader
     dev = torch.device("cuda", 0)
-    t = {k: torch.from_numpy(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v)).to(dev)
+    t = {k: to_dev(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v), dev)
          for k, v in s.items()}
     c = torch.empty((K, G), dtype=torch.int64, device=dev)
     st = torch.empty((K, G), dtype=torch.uint8, device=dev)
@@ -180,8 +181,8 @@ def test_gpu_quorum_epochs_series_vs_oracle(engine, cfg, G, K):
                              t["last_committed"], t["conf"], c, st)
     engine.synchronize()
     ce, se = _series_oracle(s, K)
-    assert np.array_equal(c.cpu().numpy(), ce)
-    assert np.array_equal(st.cpu().numpy(), se)
+    assert np.array_equal(host_np(c), ce)
+    assert np.array_equal(host_np(st), se)
     if K > 1:
         assert (ce[-1] > ce[0]).any()  # commits actually move across epochs
 
@@ -201,14 +202,14 @@ def test_gpu_quorum_epochs_relaunch_sequence(engine):
                                   (60_000, 512), (10_000, 256)]):
         s = W.quorum_epoch_series("C2", K, groups=G)
         s["pending_index"][::89] = 0
-        t = {k: torch.from_numpy(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v)).to(dev)
+        t = {k: to_dev(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v), dev)
              for k, v in s.items()}
         c = torch.empty((K, G), dtype=torch.int64, device=dev)
         st = torch.empty((K, G), dtype=torch.uint8, device=dev)
         engine.quorum_epochs_dev(t["match"], t["pending_index"], t["last_appended"],
                                  t["last_committed"], t["conf"], c, st)
         engine.synchronize()
-        got_c, got_s = c.cpu().numpy(), st.cpu().numpy()
+        got_c, got_s = host_np(c), host_np(st)
         if (G, K) in first:
             assert np.array_equal(got_c, first[(G, K)][0]) and np.array_equal(got_s, first[(G, K)][1])
             continue
@@ -225,8 +226,8 @@ def test_gpu_quorum_epochs_relaunch_sequence(engine):
 def _to_dev(b, keys):
     import torch
     dev = torch.device("cuda:0")
-    return {k: torch.from_numpy(np.ascontiguousarray(b[k].view(np.int64) if b[k].dtype == np.uint64
-                                                     else b[k])).to(dev) for k in keys}
+    return {k: to_dev(np.ascontiguousarray(b[k].view(np.int64) if b[k].dtype == np.uint64
+                                                     else b[k]), dev) for k in keys}
 
 
 @pytest.mark.parametrize("P,run_prob,max_runs,G", [(5, 0.01, 4, 4096), (3, 0.3, 4, 4096),
@@ -251,8 +252,8 @@ def test_dev_fast_path_with_flagged_runs(engine, oracle, P, run_prob, max_runs, 
                             t["last_committed"], t["conf"], out, st, run_off=t["run_off"],
                             run_start=t["run_start"], run_conf=t["run_conf"])
     engine.synchronize()
-    np.testing.assert_array_equal(out.cpu().numpy(), ce)
-    np.testing.assert_array_equal(st.cpu().numpy(), se)
+    np.testing.assert_array_equal(host_np(out), ce)
+    np.testing.assert_array_equal(host_np(st), se)
 
 
 @pytest.mark.parametrize("P,run_prob,max_runs,G", [(5, 0.01, 4, 4096), (3, 0.3, 4, 4097),
@@ -268,16 +269,16 @@ def test_tiles_entry_point_vs_replay(engine, oracle, P, run_prob, max_runs, G):
     b["conf"] = flag_runs(b)
     ce, se = _replay(oracle, b)
     dev = torch.device("cuda:0")
-    tiles = torch.from_numpy(W.to_tiles(b["match"], b["pending_index"], b["last_appended"],
-                                        b["last_committed"], b["conf"])).to(dev)
+    tiles = to_dev(W.to_tiles(b["match"], b["pending_index"], b["last_appended"],
+                                        b["last_committed"], b["conf"]), dev)
     t = _to_dev(b, ["run_off", "run_start", "run_conf"])
     out = torch.empty(G, dtype=torch.int64, device=dev)
     st = torch.empty(G, dtype=torch.uint8, device=dev)
     engine.quorum_epoch_tiles_launcher(tiles, P, G, out, st, t["run_off"], t["run_start"],
                                        t["run_conf"])()
     engine.synchronize()
-    np.testing.assert_array_equal(out.cpu().numpy(), ce)
-    np.testing.assert_array_equal(st.cpu().numpy(), se)
+    np.testing.assert_array_equal(host_np(out), ce)
+    np.testing.assert_array_equal(host_np(st), se)
 
 
 def test_tiles_entry_point_full_c3(engine):
@@ -292,8 +293,8 @@ def test_tiles_entry_point_full_c3(engine):
     s1 = torch.empty(G, dtype=torch.uint8, device=dev)
     engine.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
                             t["last_committed"], t["conf"], o1, s1)
-    tiles = torch.from_numpy(W.to_tiles(b["match"], b["pending_index"], b["last_appended"],
-                                        b["last_committed"], b["conf"])).to(dev)
+    tiles = to_dev(W.to_tiles(b["match"], b["pending_index"], b["last_appended"],
+                                        b["last_committed"], b["conf"]), dev)
     o2 = torch.empty(G, dtype=torch.int64, device=dev)
     s2 = torch.empty(G, dtype=torch.uint8, device=dev)
     engine.quorum_epoch_tiles_launcher(tiles, P, G, o2, s2)()
@@ -324,15 +325,15 @@ def test_gpu_quorum_epochs_tiles_vs_replay(engine, oracle, P, G, K, runs):
     ce, se = series_replay(oracle, s) if runs else _series_oracle(
         {k: v for k, v in s.items() if k != "run_off"}, K)
     dev = torch.device("cuda:0")
-    tiles = torch.from_numpy(_series_tiles(s, K)).to(dev)
+    tiles = to_dev(_series_tiles(s, K), dev)
     rt = _to_dev(s, ["run_off", "run_start", "run_conf"]) if runs else {}
     c = torch.empty((K, G), dtype=torch.int64, device=dev)
     st = torch.empty((K, G), dtype=torch.uint8, device=dev)
     engine.quorum_epochs_tiles_launcher(tiles, P, G, c, st, rt.get("run_off"), rt.get("run_start"),
                                         rt.get("run_conf"))()
     engine.synchronize()
-    np.testing.assert_array_equal(c.cpu().numpy(), ce)
-    np.testing.assert_array_equal(st.cpu().numpy(), se)
+    np.testing.assert_array_equal(host_np(c), ce)
+    np.testing.assert_array_equal(host_np(st), se)
 
 
 def test_gpu_quorum_epochs_tiles_full_c3(engine):
@@ -345,13 +346,13 @@ def test_gpu_quorum_epochs_tiles_full_c3(engine):
     s = W.quorum_epoch_series("C3", K)
     G = s["pending_index"].shape[0]
     dev = torch.device("cuda:0")
-    d = {k: torch.from_numpy(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v)).to(dev)
+    d = {k: to_dev(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v), dev)
          for k, v in s.items()}
     c1 = torch.empty((K, G), dtype=torch.int64, device=dev)
     s1 = torch.empty((K, G), dtype=torch.uint8, device=dev)
     engine.quorum_epochs_dev(d["match"], d["pending_index"], d["last_appended"], d["last_committed"],
                              d["conf"], c1, s1)
-    tiles = torch.from_numpy(_series_tiles(s, K)).to(dev)
+    tiles = to_dev(_series_tiles(s, K), dev)
     c2 = torch.empty((K, G), dtype=torch.int64, device=dev)
     s2 = torch.empty((K, G), dtype=torch.uint8, device=dev)
     engine.quorum_epochs_tiles_launcher(tiles, 5, G, c2, s2)()
@@ -378,8 +379,8 @@ def test_gpu_quorum_epochs_with_runs(engine, oracle, P, G, K):
                              t["last_committed"], t["conf"], c, st, run_off=t["run_off"],
                              run_start=t["run_start"], run_conf=t["run_conf"])
     engine.synchronize()
-    np.testing.assert_array_equal(c.cpu().numpy(), ce)
-    np.testing.assert_array_equal(st.cpu().numpy(), se)
+    np.testing.assert_array_equal(host_np(c), ce)
+    np.testing.assert_array_equal(host_np(st), se)
 
 
 def test_host_variant_rejects_bad_run_csr(engine):
@@ -466,7 +467,7 @@ def test_pair_kernel_32bit_domain_edges(engine):
                                   [int(x) for x in m[:, g]])
         ce[g], se[g] = c, s
     dev = torch.device("cuda:0")
-    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v).to(dev)
+    t = {k: to_dev(v.view(np.int64) if v.dtype == np.uint64 else v, dev)
          for k, v in dict(match=m, pending_index=pi, last_appended=la, last_committed=lc,
                           conf=conf).items()}
     out = torch.empty(G, dtype=torch.int64, device=dev)
@@ -474,8 +475,8 @@ def test_pair_kernel_32bit_domain_edges(engine):
     engine.quorum_epoch_dev(t["match"], t["pending_index"], t["last_appended"],
                             t["last_committed"], t["conf"], out, st)
     engine.synchronize()
-    np.testing.assert_array_equal(out.cpu().numpy(), ce)
-    np.testing.assert_array_equal(st.cpu().numpy(), se)
+    np.testing.assert_array_equal(host_np(out), ce)
+    np.testing.assert_array_equal(host_np(st), se)
 
 
 def _tile_series(s, copies):
@@ -511,7 +512,7 @@ def test_gpu_quorum_epochs_large_batch(engine, oracle, P, K):
                              t["last_committed"], t["conf"], c, st, run_off=t["run_off"],
                              run_start=t["run_start"], run_conf=t["run_conf"])
     engine.synchronize()
-    cg, sg = c.cpu().numpy(), st.cpu().numpy()
+    cg, sg = host_np(c), host_np(st)
     np.testing.assert_array_equal(cg, np.tile(ce, (1, 147)))
     np.testing.assert_array_equal(sg, np.tile(se, (1, 147)))
     # the chunk kernel on G - 1 groups of the same arrays (rows keep their strides)
@@ -522,8 +523,8 @@ def test_gpu_quorum_epochs_large_batch(engine, oracle, P, K):
                              t["last_committed"][:G1], t["conf"][:G1], c1, s1, run_off=t["run_off"][:G1 + 1],
                              run_start=t["run_start"], run_conf=t["run_conf"])
     engine.synchronize()
-    np.testing.assert_array_equal(c1.cpu().numpy(), cg[:, :G1])
-    np.testing.assert_array_equal(s1.cpu().numpy(), sg[:, :G1])
+    np.testing.assert_array_equal(host_np(c1), cg[:, :G1])
+    np.testing.assert_array_equal(host_np(s1), sg[:, :G1])
 
 
 @pytest.mark.parametrize("P,run_prob,G", [(5, 0.01, 4096), (3, 0.3, 3001), (16, 0.5, 515)])

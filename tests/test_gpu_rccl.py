@@ -4,6 +4,7 @@ The box has one GPU, so this runs a single-rank communicator (all-gather of one 
 the multi-rank layout is covered by tests/test_dist_gloo.py and bench.py --gpus N."""
 import numpy as np
 import pytest
+from devio import host_np
 
 pytestmark = pytest.mark.gpu
 
@@ -19,7 +20,7 @@ def test_single_rank_publish(engine):
     glob = torch.full((1000,), -1, dtype=torch.int64, device=dev)
     engine.publish_committed_dev(local, glob)
     engine.synchronize()
-    np.testing.assert_array_equal(glob.cpu().numpy(), local.cpu().numpy())
+    np.testing.assert_array_equal(host_np(glob), host_np(local))
 
 
 def test_publish_without_init_is_state_error():

@@ -11,6 +11,7 @@ import pytest
 from jraft_amd import JrqError, Table, decode_changed
 from jraft_amd import _lib
 from quorum_cases import random_batch, random_series, series_replay
+from devio import to_dev, host_np
 
 pytestmark = pytest.mark.gpu
 
@@ -184,8 +185,8 @@ def test_device_variant_and_view(engine, oracle):
                                           b["run_start"], b["run_conf"], chunk=3)
     t = Table(engine, G, P)
     dev = torch.device("cuda:0")
-    st = torch.from_numpy(states_of(b).view(np.uint8)).to(dev)
-    rc = torch.from_numpy(match_recs(b["match"], b["pending_index"]).view(np.int64)).to(dev)
+    st = to_dev(states_of(b).view(np.uint8), dev)
+    rc = to_dev(match_recs(b["match"], b["pending_index"]).view(np.int64), dev)
     t.update_dev(st, rc)
     out, n = t.list_buffers(dev)
     t.epoch_dev(out, n)
@@ -200,7 +201,7 @@ def test_device_variant_and_view(engine, oracle):
     import ctypes  # (the view holds raw device pointers: read the tiles through hipMemcpy)
     hip = ctypes.CDLL("libamdhip64.so")
     assert hip.hipMemcpy(ctypes.c_void_p(lcd.data_ptr()), ctypes.c_void_p(v.match), lcd.numel() * 8, 3) == 0
-    words = lcd.cpu().numpy()
+    words = host_np(lcd)
     g = np.arange(G)
     assert v.last_committed == v.match + 8 * (128 * P + 512)
     lc_view = words[(g // 256) * v.tile_stride + 128 * P + 512 + g % 256]
@@ -310,7 +311,7 @@ def test_flagged_groups_in_full_blocks(engine, G, joint):
     gs = np.arange(G)
     recs = np.concatenate([_lib.rec(gs, p, np.maximum(m[p] - (pi - 1), 0)) for p in range(P)])
     dev = torch.device("cuda:0")
-    d = {k: torch.from_numpy(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v)).to(dev)
+    d = {k: to_dev(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v), dev)
          for k, v in (("match", m), ("pi", pi), ("la", s["last_appended"][0]),
                       ("lc", s["last_committed"]), ("conf", s["conf"]), ("run_off", s["run_off"]),
                       ("run_start", s["run_start"]), ("run_conf", s["run_conf"]))}
@@ -319,7 +320,7 @@ def test_flagged_groups_in_full_blocks(engine, G, joint):
     engine.quorum_epoch_dev(d["match"], d["pi"], d["la"], d["lc"], d["conf"], pc, ps,
                             run_off=d["run_off"], run_start=d["run_start"], run_conf=d["run_conf"])
     engine.synchronize()
-    exp_c, exp_s = pc.cpu().numpy(), ps.cpu().numpy()
+    exp_c, exp_s = host_np(pc), host_np(ps)
     assert (exp_c > s["last_committed"]).mean() > 0.9
     t = Table(engine, G, P)
     for rep in range(2):
@@ -331,8 +332,8 @@ def test_flagged_groups_in_full_blocks(engine, G, joint):
             sd = torch.empty(G, dtype=torch.uint8, device=dev)
             t.epoch_dev(out, n, sd)
             engine.synchronize()
-            assert (n.cpu().numpy() <= _lib.TABLE_SLICE).all()
-            changed, stt = t.gather_dev_list(out, n), sd.cpu().numpy()
+            assert (host_np(n) <= _lib.TABLE_SLICE).all()
+            changed, stt = t.gather_dev_list(out, n), host_np(sd)
         got, _ = committed_from(changed, pi, s["last_committed"])
         np.testing.assert_array_equal(got, exp_c)
         np.testing.assert_array_equal(stt, exp_s)
@@ -422,5 +423,72 @@ def test_match_base_rebase_across_2_30(engine, oracle, P, joint):
     got2, _ = committed_from(changed, pi1, ce1)
     np.testing.assert_array_equal(got2, ce2)
     np.testing.assert_array_equal(st2, se2)
+    t.check()
+    t.close()
+
+
+def test_lowered_base_without_reset_invents_no_ack(engine):
+    """a header without RESET_MATCH that lowers a leader's match base.
+    Slots whose word is 0 under the old base (match at or below it: unknown) must not read back
+    as exactly the old base -- that would count as an ack of entries no peer acknowledged.
+    Such words stay 0 (no grant); words above 0 are shifted exactly."""
+    from jraft_amd import conf_word
+    G, P = 4, 3
+    B = 1 << 30
+    cw = conf_word(0b111, 0)
+    st = Table.states(G)
+    st["group"] = np.arange(G)
+    st["num_runs"] = 1
+    st["flags"] = _lib.STATE_RESET_MATCH
+    st["pending_index"] = B + 1          # base B: every slot's word 0 (match = B)
+    st["last_appended"] = B + 40
+    st["last_committed"] = B
+    st["run_conf"][:, 0] = cw
+    t = Table(engine, G, P)
+    t.update(st)
+    # slot 0 of every group acks B + 5 (word 5); slots 1, 2 stay at word 0
+    t.update(None, _lib.rec(np.arange(G), 0, np.full(G, 5 + 1)))
+    # the non-reset header: pendingIndex lowered below the base (base 0 afterwards)
+    st2 = st.copy()
+    st2["flags"] = 0
+    st2["pending_index"] = B - 10
+    st2["last_committed"] = B - 11
+    st2["last_appended"] = B + 40
+    t.update(st2)
+    r = t.read()
+    np.testing.assert_array_equal(r["match"][0], np.full(G, B + 5))   # shifted exactly
+    np.testing.assert_array_equal(r["match"][1:], 0)                  # unknown: no ack
+    changed, _ = t.epoch(status=True)
+    assert len(changed) == 0  # quorum 2 of 3: one real ack (slot 0) is not a quorum
+    # a real ack of slot 1 afterwards decides normally: min(B + 5, B + 2) = B + 2
+    pi2 = np.full(G, B - 10, np.int64)
+    t.update(None, _lib.rec(np.arange(G), 1, np.full(G, (B + 2) - (B - 11))))
+    changed, _ = t.epoch(status=True)
+    got, _ = committed_from(changed, pi2, np.full(G, B - 11, np.int64))
+    np.testing.assert_array_equal(got, np.full(G, B + 2))
+    t.check()
+    t.close()
+
+
+def test_header_with_lastappended_below_pending_refused(engine):
+    """lastAppended < pendingIndex - 1 is a queue of negative size, which no
+    BallotBox holds; such a header is skipped and reported (the epoch's u32 out-of-range test
+    relies on lastAppended >= the match base)."""
+    from jraft_amd import conf_word
+    G, P = 2, 3
+    st = Table.states(G)
+    st["group"] = np.arange(G)
+    st["num_runs"] = 1
+    st["flags"] = _lib.STATE_RESET_MATCH
+    st["pending_index"] = [(1 << 30) + 3, 100]
+    st["last_appended"] = [(1 << 30) - 7, 99]   # group 0: la < pi - 1 across the 2^30 base
+    st["last_committed"] = [(1 << 30) + 2, 99]
+    st["run_conf"][:, 0] = conf_word(0b111, 0)
+    t = Table(engine, G, P)
+    t.update(st)
+    with pytest.raises(JrqError):
+        t.check()
+    r = t.read()
+    assert r["pending_index"][0] == 0 and r["pending_index"][1] == 100  # group 0 untouched
     t.check()
     t.close()

@@ -16,6 +16,7 @@ import pytest
 
 from jraft_amd import _lib
 from jraft_amd import workloads as W
+from devio import host_np, to_dev
 
 pytestmark = pytest.mark.gpu
 
@@ -111,9 +112,13 @@ def test_concurrent_registrations_then_pageable_uploads(oracle):
         x.join()
     assert not errors, errors
     dev = torch.device("cuda:0")
+    # after the registration churn HIP must hold no registration over fresh memory (a stale
+    # one is what the rounds 2-3 fault DMA-ed through); round trips through page-locked memory
+    from conftest import assert_unregistered
     for k in range(6):
         host = np.frombuffer(W.random_bytes(100 + k, (8 << 20) + 8 * k), np.int64).copy()
-        got = torch.from_numpy(host).to(dev).cpu().numpy()
+        assert_unregistered({"host": host}, "after concurrent register/unregister")
+        got = host_np(to_dev(host, dev))
         np.testing.assert_array_equal(got, host)
     payload = W.random_bytes(7, 6 << 20)
     offs = np.arange(0, len(payload) + 1, 4096, dtype=np.uint64)
@@ -226,8 +231,7 @@ def test_result_downloads_through_bounce_chunks(engine):
     c_host, s_host = engine.quorum_epoch(b["match"], b["pending_index"], b["last_appended"],
                                          b["last_committed"], b["conf"])
     dev = torch.device("cuda:0")
-    t = {k: torch.from_numpy(np.ascontiguousarray(v.view(np.int64) if v.dtype == np.uint64 else v)).pin_memory().to(dev)
-         for k, v in b.items()}
+    t = {k: to_dev(v, dev) for k, v in b.items()}
     G = b["pending_index"].shape[0]
     out = torch.empty(G, dtype=torch.int64, device=dev)
     st = torch.empty(G, dtype=torch.uint8, device=dev)

@@ -12,6 +12,7 @@ import pytest
 
 from jraft_amd import workloads as W
 from quorum_cases import series_replay
+from devio import to_dev, host_np
 
 pytestmark = pytest.mark.gpu
 
@@ -59,8 +60,8 @@ def test_host_mirror_drives_series(engine, oracle, G, K, joint, active, threads)
     t = {}
     for k in ("match", "last_appended", "pending_index", "last_committed", "conf", "run_off",
               "run_start", "run_conf"):
-        t[k] = torch.from_numpy(np.ascontiguousarray(s[k].view(np.int64) if s[k].dtype == np.uint64
-                                                     else s[k])).to(dev)
+        t[k] = to_dev(np.ascontiguousarray(s[k].view(np.int64) if s[k].dtype == np.uint64
+                                                     else s[k]), dev)
         device_checkpoint(f"after the torch upload of {k} ({s[k].nbytes} B, pageable)")
     c = torch.empty((K, G), dtype=torch.int64, device=dev)
     sst = torch.empty((K, G), dtype=torch.uint8, device=dev)
@@ -68,7 +69,7 @@ def test_host_mirror_drives_series(engine, oracle, G, K, joint, active, threads)
                              t["last_committed"], t["conf"], c, sst, run_off=t["run_off"],
                              run_start=t["run_start"], run_conf=t["run_conf"])
     device_checkpoint("after quorum_epochs_dev")
-    np.testing.assert_array_equal(committed, c.cpu().numpy())
+    np.testing.assert_array_equal(committed, host_np(c))
     # (a) a sample of groups (all the joint ones among them) against the oracle
     rng = np.random.default_rng(1)
     joint_g = np.nonzero(s["switch_at"])[0]

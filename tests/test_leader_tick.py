@@ -9,6 +9,7 @@ import pytest
 
 from test_lease import random_lease_batch
 from test_readindex import random_rounds
+from devio import to_dev, host_np
 
 pytestmark = pytest.mark.gpu
 
@@ -56,7 +57,7 @@ def test_tick_dev_aligned_and_unaligned(engine, oracle, off):
     P, G = 5, (1 << 20) + 1
     ts, conf, self_slot, now, to, lead, order, okm = _batch(77, G, P)
     dev = torch.device("cuda:0")
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    T = lambda a: to_dev(np.ascontiguousarray(a), dev)  # noqa: E731
     # ts with a row stride of G + 1 (even when G is odd: the pair kernel's condition)
     ld = G + 1
     tsd = torch.zeros((P, ld), dtype=torch.int64, device=dev)
@@ -74,10 +75,10 @@ def test_tick_dev_aligned_and_unaligned(engine, oracle, off):
     torch.cuda.synchronize()
     sl = slice(off, None)
     e = _expect(oracle, ts[:, sl], conf[sl], self_slot[sl], now, to, lead[sl], order[sl], okm[sl], P)
-    np.testing.assert_array_equal(ok.cpu().numpy()[sl], e[0])
-    np.testing.assert_array_equal(L.cpu().numpy()[sl], e[1])
-    np.testing.assert_array_equal(dead.cpu().numpy().view(np.uint16)[sl], e[2])
-    np.testing.assert_array_equal(ri.cpu().numpy()[sl], e[3])
+    np.testing.assert_array_equal(host_np(ok)[sl], e[0])
+    np.testing.assert_array_equal(host_np(L)[sl], e[1])
+    np.testing.assert_array_equal(host_np(dead).view(np.uint16)[sl], e[2])
+    np.testing.assert_array_equal(host_np(ri)[sl], e[3])
 
 
 def test_tick_argument_checks(engine):

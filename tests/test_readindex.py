@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 from jraft_amd import conf_word
+from devio import to_dev, host_np
 
 PENDING, SUCCESS, FAILURE = 0, 1, 2
 
@@ -141,14 +142,14 @@ def test_gpu_unaligned_device_pointers(engine, oracle):
     P, G = 5, 10001
     conf, self_slot, order, okm, _ = random_rounds(11, G + 1, P)
     dev = torch.device("cuda:0")
-    tc = torch.from_numpy(conf.view(np.int64)).to(dev)
-    ts = torch.from_numpy(self_slot).to(dev)
-    to = torch.from_numpy(order.view(np.int64)).to(dev)
-    tk = torch.from_numpy(okm.view(np.int16)).to(dev)
+    tc = to_dev(conf.view(np.int64), dev)
+    ts = to_dev(self_slot, dev)
+    to = to_dev(order.view(np.int64), dev)
+    tk = to_dev(okm.view(np.int16), dev)
     out = torch.zeros(G + 1, dtype=torch.uint8, device=dev)
     engine.readindex_quorum_dev(tc[1:], ts[1:], to[1:], tk[1:], P, out[1:])
     torch.cuda.synchronize()
-    got = out.cpu().numpy()
+    got = host_np(out)
     np.testing.assert_array_equal(got[1:], oracle.readindex_quorum(conf[1:], self_slot[1:], order[1:], okm[1:], P))
     assert got[0] == 0
 
@@ -168,16 +169,16 @@ def test_gpu_dev_entry_point_and_rounds_in_steps(engine, oracle):
     early = np.where((nib >= 1) & (nib <= 2), nib, 0)
     order1 = (early << (4 * np.arange(P, dtype=np.uint64))).sum(axis=1).astype(np.uint64)
     out = torch.empty(G, dtype=torch.uint8, device=dev)
-    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else
-                             (v.view(np.int16) if v.dtype == np.uint16 else v)).to(dev)
+    t = {k: to_dev(v.view(np.int64) if v.dtype == np.uint64 else
+                             (v.view(np.int16) if v.dtype == np.uint16 else v), dev)
          for k, v in (("conf", conf), ("self", self_slot), ("o1", order1), ("o", order), ("ok", okm))}
     engine.readindex_quorum_dev(t["conf"], t["self"], t["o1"], t["ok"], P, out)
     torch.cuda.synchronize()
-    r1 = out.cpu().numpy()
+    r1 = host_np(out)
     np.testing.assert_array_equal(r1, oracle.readindex_quorum(conf, self_slot, order1, okm, P))
     engine.readindex_quorum_dev(t["conf"], t["self"], t["o"], t["ok"], P, out)
     torch.cuda.synchronize()
-    r2 = out.cpu().numpy()
+    r2 = host_np(out)
     np.testing.assert_array_equal(r2, oracle.readindex_quorum(conf, self_slot, order, okm, P))
     decided = r1 != PENDING
     np.testing.assert_array_equal(r2[decided], r1[decided])

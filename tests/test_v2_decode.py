@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 import jraft_oracle as O
+from devio import to_dev, host_np
 
 HOSTLIKE = (O.V2_PEER_NONCANON, O.V2_PEER_THROWS)
 V2_HOST = 3  # include/jrq.h JRQ_V2_HOST
@@ -267,14 +268,14 @@ def test_gpu_unaligned_base_and_device_variant(engine):
     off2 = off + np.uint64(pad)
     o = O.v2_decode_batch(big, off2)
     dev = torch.device("cuda", 0)
-    d_rec = torch.from_numpy(big).to(dev)
-    d_off = torch.from_numpy(off2.view(np.int64)).to(dev)
+    d_rec = to_dev(big, dev)
+    d_off = to_dev(off2.view(np.int64), dev)
     n = len(recs)
     tdt = {np.uint8: torch.uint8, np.int64: torch.int64, np.uint64: torch.int64, np.uint32: torch.int32}
     out = {k: torch.empty(n, dtype=tdt[t], device=dev) for k, t in engine.V2_FIELDS}
     engine.v2_decode_verify_dev(d_rec, d_off, out)
     engine.synchronize()
-    g = {k: out[k].cpu().numpy().view(t) for k, t in engine.V2_FIELDS}
+    g = {k: host_np(out[k]).view(t) for k, t in engine.V2_FIELDS}
     check_gpu_vs_oracle(g, o)
 
 
@@ -388,15 +389,15 @@ def test_gpu_uniform_data_len_device_variant(engine, pad):
     o = O.v2_decode_batch(buf, off)
     dev = torch.device("cuda", 0)
     store = torch.zeros(len(buf) + pad + 64, dtype=torch.uint8, device=dev)
-    store[pad:pad + len(buf)] = torch.from_numpy(buf).to(dev)
+    store[pad:pad + len(buf)] = to_dev(buf, dev)
     d_rec = store[pad:pad + len(buf)]
-    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_off = to_dev(off.view(np.int64), dev)
     tdt = {np.uint8: torch.uint8, np.int64: torch.int64, np.uint64: torch.int64, np.uint32: torch.int32}
     out = {k: torch.empty(n, dtype=tdt[t], device=dev) for k, t in engine.V2_FIELDS}
     torch.cuda.synchronize()
     engine.v2_decode_verify_dev(d_rec, d_off, out)
     engine.synchronize()
-    g = {k: out[k].cpu().numpy().view(t) for k, t in engine.V2_FIELDS}
+    g = {k: host_np(out[k]).view(t) for k, t in engine.V2_FIELDS}
     check_gpu_vs_oracle(g, o)
 
 

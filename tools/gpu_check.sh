@@ -63,6 +63,7 @@ for s in $STEPS; do
     bsel)  run bench_${TAG:-sel} 600 python bench.py --steps 20 --warmup 5 --no-cpu --legs ${BENCH_LEGS:-quorum} --detail gpurun_out/bench_${TAG:-sel}_detail.json ;;
     sqpmc) run sqpmc_${TRACE_LEGS:-v2} 120 rocprofv3 --kernel-trace --pmc ${SQ_COUNTERS:-SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_INSTS_SMEM SQ_BUSY_CYCLES} -d gpurun_out/sqpmc_${TRACE_LEGS:-v2} -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs ${TRACE_LEGS:-v2} ;;
     trace) run trace_${TRACE_LEGS:-v2} 300 rocprofv3 --kernel-trace -d gpurun_out/trace_${TRACE_LEGS:-v2} -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --legs ${TRACE_LEGS:-v2} ;;
+    probe) run pin_probe 120 python tools/pin_cache_probe.py ;;
     drive) run drive_tests 300 python -u -m pytest tests/test_host_drive.py -v -x -p no:cacheprovider --timeout 240 --timeout-method thread ;;
   esac
 done

@@ -1,0 +1,132 @@
+"""Probe: does HIP keep a lock on pageable host memory after a copy into it returns, and is
+that lock still there over a new allocation at the same address?  (the
+lease-leg "illegal memory access" of rounds 4 and 5.)
+
+The runtime (ROCclr, libamdhip64) copies a large pageable range by locking ("pinning") the
+caller's pages itself (DmaBlitManager::hsaCopyStagedOrPinned -> pinHostMemory, knobs
+GPU_PINNED_MIN_XFER_SIZE / GPU_PINNED_XFER_SIZE, strings in libamdhip64.so) and keeps the
+pinned objects in a per-queue list for reuse, looked up by host address.  If that is so, a lock
+outlives the copy, survives the caller's free(), and a later allocation at the same address
+is DMA-ed through the old lock.
+
+What this probe does (safe: it never copies into memory whose old lock it observes, and no
+range it unmaps is left free for a later allocation to land in):
+  (a) ten device->host copies of 8 MiB into ten live, fresh anonymous mappings, then the HSA
+      pointer type of each (are the locks kept, and how many);
+  (b) for each size S: a fresh anonymous mapping A, one device->host copy of S bytes into it
+      through torch (HIP's pageable path), then -- with no further copy -- what the HSA runtime
+      (hsa_amd_pointer_info) and HIP (hipPointerGetAttributes) report for A's address
+        (1) right after the copy returned,
+        (2) after munmap(A),
+        (3) over a new mapping B placed at A's address (MAP_FIXED over the range just unmapped),
+            which is never copied into and stays mapped until the process exits.
+  HSA pointer types: 0 unknown, 1 HSA, 2 LOCKED (a host range locked for the GPU).
+Writes one JSON document to stdout.
+"""
+import ctypes as C
+import gc
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sofa-jraft_amd"))
+
+
+class HsaPointerInfo(C.Structure):  # hsa_amd_pointer_info_t (hsa_ext_amd.h)
+    _fields_ = [("size", C.c_uint32), ("type", C.c_int), ("agentBaseAddress", C.c_void_p),
+                ("hostBaseAddress", C.c_void_p), ("sizeInBytes", C.c_size_t),
+                ("userData", C.c_void_p), ("agentOwner", C.c_uint64), ("global_flags", C.c_uint32),
+                ("registered", C.c_bool)]
+
+
+class HipPtrAttr(C.Structure):  # hipPointerAttribute_t
+    _fields_ = [("type", C.c_int), ("device", C.c_int), ("devicePointer", C.c_void_p),
+                ("hostPointer", C.c_void_p), ("isManaged", C.c_int), ("allocationFlags", C.c_uint)]
+
+
+def main():
+    import torch
+    dev = torch.device("cuda", 0)
+    torch.zeros(1, device=dev)
+    # the runtimes torch loaded (same SONAMEs as /opt/rocm's; NOLOAD binds the loaded copies)
+    hsa = C.CDLL("libhsa-runtime64.so.1", mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
+    hip = C.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
+    hsa.hsa_amd_pointer_info.restype = C.c_int
+    hsa.hsa_amd_pointer_info.argtypes = [C.c_void_p, C.POINTER(HsaPointerInfo), C.c_void_p,
+                                         C.c_void_p, C.c_void_p]
+    hip.hipPointerGetAttributes.restype = C.c_int
+    hip.hipGetLastError.restype = C.c_int
+
+    def hsa_info(addr):
+        i = HsaPointerInfo()
+        i.size = C.sizeof(HsaPointerInfo)
+        rc = hsa.hsa_amd_pointer_info(C.c_void_p(addr), C.byref(i), None, None, None)
+        return {"rc": rc, "type": i.type, "host_base": hex(i.hostBaseAddress or 0),
+                "agent_base": hex(i.agentBaseAddress or 0), "bytes": i.sizeInBytes}
+
+    def hip_info(addr):
+        a = HipPtrAttr()
+        rc = hip.hipPointerGetAttributes(C.byref(a), C.c_void_p(addr))
+        hip.hipGetLastError()
+        return {"rc": rc, "type": a.type, "devicePointer": hex(a.devicePointer or 0)}
+
+    libc = C.CDLL(None, use_errno=True)
+    libc.mmap.restype = C.c_void_p
+    libc.mmap.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_long]
+    libc.munmap.argtypes = [C.c_void_p, C.c_size_t]
+    PROT_RW, MAP_PRIVATE, MAP_ANON, MAP_FIXED = 0x3, 0x02, 0x20, 0x10
+
+    def new_map(size, at=None):
+        p = libc.mmap(at, size, PROT_RW, MAP_PRIVATE | MAP_ANON | (MAP_FIXED if at else 0), -1, 0)
+        if p in (None, C.c_void_p(-1).value):
+            raise OSError(C.get_errno(), "mmap")
+        if at is not None and p != at:
+            raise RuntimeError("MAP_FIXED mapping moved")
+        arr = np.ctypeslib.as_array((C.c_uint8 * size).from_address(p))
+        arr[::4096] = 0  # touch every page
+        return p, arr
+
+    src = torch.arange(64 << 20, dtype=torch.uint8, device=dev)  # 64 MiB device source
+    torch.cuda.synchronize()
+    expect = (np.arange(4096) % 256).astype(np.uint8)
+    out = {"torch": torch.__version__, "hip": torch.version.hip,
+           "env": {k: os.environ.get(k) for k in ("GPU_PINNED_MIN_XFER_SIZE", "GPU_PINNED_XFER_SIZE",
+                                                  "GPU_STAGING_BUFFER_SIZE")},
+           "cases": []}
+    keep = []  # every mapping made here stays mapped (or is replaced in place) until exit
+    # (a) ten live 8 MiB destinations, each copied into once
+    live = [new_map(8 << 20) for _ in range(10)]
+    keep += live
+    for _, x in live:
+        torch.from_numpy(x).copy_(src[:8 << 20])
+    torch.cuda.synchronize()
+    out["ten_live_8MiB_copies"] = [{"copy_ok": bool(np.array_equal(x[:4096], expect)),
+                                    "hsa": hsa_info(p)} for p, x in live]
+    # (b) per size: copy, then observe only
+    for size in (64 << 10, 512 << 10, 1 << 20, 2 << 20, 8 << 20, 32 << 20, 48 << 20):
+        pa, a = new_map(size)
+        before = hsa_info(pa)
+        torch.from_numpy(a).copy_(src[:size])      # D2H through HIP's pageable path
+        torch.cuda.synchronize()
+        ok = bool(np.array_equal(a[:4096], expect))
+        after_copy = {"hsa": hsa_info(pa), "hsa_mid": hsa_info(pa + size // 2), "hip": hip_info(pa)}
+        del a
+        libc.munmap(C.c_void_p(pa), size)
+        after_free = {"hsa": hsa_info(pa), "hip": hip_info(pa)}
+        pb, b = new_map(size, at=pa)               # same address, never copied into
+        keep.append((pb, b))
+        over_new = {"same_address": pb == pa, "hsa": hsa_info(pb), "hsa_mid": hsa_info(pb + size // 2),
+                    "hip": hip_info(pb)}
+        out["cases"].append({"bytes": size, "addr": hex(pa), "copy_ok": ok, "before": before,
+                             "after_copy": after_copy, "after_munmap": after_free,
+                             "new_mapping_same_address": over_new})
+    print(json.dumps(out, indent=1))
+    sys.stdout.flush()
+    os._exit(0)  # leave the mappings to the kernel; no runtime teardown over the replaced ranges
+
+
+if __name__ == "__main__":
+    main()
