@@ -262,7 +262,7 @@ int jrq_quorum_epochs_tiles_dev(jrq_engine *e, const jrq_group_tiles *in_dev, ui
 #define JRQ_TABLE_MAX_RUNS 4            /* conf runs per pending window (NodeImpl has <= 2) */
 #define JRQ_TABLE_MAX_GROUPS (1u << 27) /* groups per table (27-bit group ids in records) */
 #define JRQ_PI_FOLLOWS_LC INT64_MIN
-#define JRQ_TABLE_SLICE 256             /* groups per slice of an epoch's changed list (_dev) */
+#define JRQ_TABLE_SLICE 128             /* groups per slice of an epoch's changed list (_dev) */
 
 typedef struct jrq_table jrq_table;
 
@@ -338,8 +338,8 @@ int jrq_table_stage_apply(jrq_table *t);
  * the listed entries.
  * _dev: the list comes in jrq_table_slices(t) fixed slices, one per JRQ_TABLE_SLICE groups
  * (no reservation, no atomics: each slice is written by the one wave that decides its groups),
- * slice s at changed_out_dev + 256 s (capacity JRQ_TABLE_SLICE * jrq_table_slices(t) words):
- * words 0-3 a 256-bit map (bit i: group 256 s + i advanced), then from byte 32 the listed
+ * slice s at changed_out_dev + 128 s (capacity JRQ_TABLE_SLICE * jrq_table_slices(t) words):
+ * words 0-1 a 128-bit map (bit i: group 128 s + i advanced), then from byte 16 the listed
  * groups' (commit - pi + 1) as uint32, in group order; n_changed_dev[s] = the map's popcount. */
 int jrq_table_epoch_dev(jrq_table *t, uint64_t *changed_out_dev, uint32_t *n_changed_dev,
                         uint8_t *status_out_dev);
@@ -364,8 +364,8 @@ int jrq_table_copy(jrq_table *dst, const jrq_table *src);
  * element g of an int64 field is field[(g / tile_groups) * tile_stride + g % tile_groups] (each
  * tile holds every field of its groups in one contiguous block: an epoch wave reads one block).
  * The u32 match words of tile i start at match + 2 i tile_stride, slot p's 256 words at
- * + 256 p, group k of the tile at position (k % 128) / 2 * 4 + (k / 128) * 2 + k % 2 (the
- * epoch's lane order); match = match base + word (JRQ_TABLE_MATCH_PAGE). */
+ * + 256 p, group k of the tile at position k; match = match base + word
+ * (JRQ_TABLE_MATCH_PAGE). */
 typedef struct {
     uint32_t *match;         /* u32 words of tile 0 */
     int64_t *pending_index;  /* JRQ_PI_FOLLOWS_LC after a commit */
@@ -374,7 +374,7 @@ typedef struct {
     uint64_t *conf;
     uint64_t ld;             /* row stride of the table's cold (per-run) fields */
     uint32_t G, num_peers;
-    uint32_t tile_groups;    /* 256 (JRQ_TABLE_SLICE) */
+    uint32_t tile_groups;    /* 256 (2 JRQ_TABLE_SLICE) */
     uint64_t tile_stride;    /* int64 words from a tile to the next: 128 num_peers + 1024 */
 } jrq_table_view;
 int jrq_table_view_get(jrq_table *t, jrq_table_view *view_out);

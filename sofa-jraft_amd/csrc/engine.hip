@@ -45,7 +45,7 @@ extern "C" hipError_t jrq_launch_table_list_gather(const uint64_t* changed, cons
 
 static_assert(sizeof(jrq_group_state) == sizeof(JrqGroupState), "jrq_group_state layout");
 static_assert(JRQ_TABLE_MAX_RUNS == jrq::kTableMaxRuns, "table runs");
-static_assert(JRQ_TABLE_SLICE == jrq::kTableSlice, "table list slices");
+static_assert(JRQ_TABLE_SLICE == jrq::kListSlice, "table list slices");
 
 namespace {
 
@@ -1708,15 +1708,17 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   t->e = e;
   const uint64_t ld = (static_cast<uint64_t>(G) + 63) & ~63ull;  // pairs + 512-B rows
   // the state jrq_table_copy copies: the hot tiles (256 groups each: match[P] as 256-u32 rows,
-  // pi, la, lc, conf as 256-word rows, JrqTableArgs), the cold rows xstart[3], xconf[3], the flagged-entry slots
-  // flag_ent[waves][256][8] + flag_wcnt[waves] (u32); then the control word `invalid`
-  // (one 256-group range per epoch wave, rounded up to whole workgroups: every wave of the
-  // grid reads its slots)
-  const uint64_t ranges = (G + jrq::kTableSlice - 1) / jrq::kTableSlice;
-  const uint64_t waves = (ranges + jrq::kTableBlockWaves - 1) / jrq::kTableBlockWaves * jrq::kTableBlockWaves;
+  // pi, la, lc, conf as 256-word rows, JrqTableArgs), the cold rows xstart[3], xconf[3], the
+  // flagged-entry slots flag_ent[waves][128][8] + flag_wcnt[waves] (u32); then the control word
+  // `invalid`.  Epoch waves decide 128 groups (half a tile); the grid is whole workgroups of
+  // kTableBlockWaves waves, and every wave of it reads its tile and its slots: tiles and slots
+  // are allocated for the whole grid
+  const uint64_t waves = ((G + jrq::kListSlice - 1) / jrq::kListSlice + jrq::kTableBlockWaves - 1) /
+                         jrq::kTableBlockWaves * jrq::kTableBlockWaves;
+  const uint64_t tiles = (waves + 1) / 2;
   const uint64_t flag_words = waves * jrq::kFlagSlots * 8 + (waves + 1) / 2;
   const uint64_t ts = static_cast<uint64_t>(P) * (jrq::kTableSlice / 2) + 4 * jrq::kTableSlice;  // words per tile
-  const uint64_t words = waves * ts + ld * 2 * (jrq::kTableMaxRuns - 1) + flag_words;
+  const uint64_t words = tiles * ts + ld * 2 * (jrq::kTableMaxRuns - 1) + flag_words;
   const size_t bytes = words * 8 + 64;
   t->slices = (G + JRQ_TABLE_SLICE - 1) / JRQ_TABLE_SLICE;
   if (hipMalloc(&t->mem, bytes) != hipSuccess || hipMemset(t->mem, 0, bytes) != hipSuccess ||
@@ -1735,7 +1737,7 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   a.lc = a.la + jrq::kTableSlice;
   a.conf = reinterpret_cast<uint64_t*>(a.lc + jrq::kTableSlice);
   a.ts = ts;
-  a.xstart = w + waves * ts;
+  a.xstart = w + tiles * ts;
   a.xconf = reinterpret_cast<uint64_t*>(a.xstart + ld * (jrq::kTableMaxRuns - 1));
   a.flag_ent = reinterpret_cast<uint64_t*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
   a.flag_wcnt = reinterpret_cast<uint32_t*>(a.flag_ent + waves * jrq::kFlagSlots * 8);
@@ -1960,12 +1962,12 @@ int jrq_table_read(jrq_table* t, int64_t* pending_index, int64_t* last_appended,
   int64_t* pw = host.data() + G;
   for (size_t g = 0; g < G; ++g)
     if (pw[g] == JRQ_PI_FOLLOWS_LC) pw[g] = lc[g] + 1;
-  if (match)  // absolute: the group's match base + its word (mslot: the epoch's lane order)
+  if (match)  // absolute: the group's match base + its word (group order within the tile)
     for (size_t g = 0; g < G; ++g) {
       const int64_t b = jrq::mbase(pw[g]);
       const uint32_t* row = mw.data() + (g / jrq::kTableSlice) * t->a.P * jrq::kTableSlice;
       for (uint32_t p = 0; p < t->a.P; ++p)
-        match[p * G + g] = b + static_cast<int64_t>(row[p * jrq::kTableSlice + jrq::mslot(g % jrq::kTableSlice)]);
+        match[p * G + g] = b + static_cast<int64_t>(row[p * jrq::kTableSlice + g % jrq::kTableSlice]);
     }
   if (pending_index) std::memcpy(pending_index, pw, G * 8);
   if (last_committed) std::memcpy(last_committed, lc, G * 8);

@@ -271,21 +271,24 @@ struct JrqQuorumArgs {
 // Resident group table (table.hip; include/jrq.h jrq_table).
 namespace jrq {
 constexpr int kTableMaxRuns = 4;                   // JRQ_TABLE_MAX_RUNS
-constexpr uint32_t kTableSlice = 256;              // JRQ_TABLE_SLICE: groups per epoch wave
+constexpr uint32_t kTableSlice = 256;              // groups per tile (jrq_table_view.tile_groups)
+constexpr uint32_t kListSlice = 128;               // JRQ_TABLE_SLICE: groups per epoch wave and
+                                                   // per slice of its changed list (half a tile)
 constexpr uint32_t kTableBlockWaves = 4;           // waves per epoch / flags workgroup
 constexpr int64_t kPiFollowsLc = INT64_MIN;        // JRQ_PI_FOLLOWS_LC
-constexpr uint32_t kFlagSlots = 256;               // flagged-entry slots per 256-group epoch wave
+constexpr uint32_t kFlagSlots = kListSlice;        // flagged-entry slots per epoch wave
 }  // namespace jrq
-// The hot fields live in tiles of kTableSlice (256) groups, one tile per epoch wave: tile i
+// The hot fields live in tiles of kTableSlice (256) groups, two epoch waves per tile: tile i
 // holds match[0..P-1], pendingIndex, lastAppended, lastCommitted, conf of groups [256 i,
-// 256 i + 256), so a wave's whole input is one contiguous (4P + 32) * 256-B block (DESIGN.md
-// §4.9; field-major rows over all groups ran 20 % slower: tools/probes/streams_probe.hip).
-// pendingIndex, lastAppended, lastCommitted and conf are 256 consecutive int64 words each;
-// element g of such a field is row[(g >> 8) * ts + (g & 255)] (tf()).  The match of a slot is
-// a u32 relative to the group's match base (mbase(pendingIndex): pendingIndex - 1 rounded down
-// to a multiple of 2^30, fixed for a billion entries), saturated at 0 below it -- a match below
-// the pending window grants nothing whatever its value -- so a slot costs 4 B instead of 8
-// (r05); the 256 u32 of a slot's row sit in the epoch's lane order (mslot()).
+// 256 i + 256), so a tile is one contiguous (4P + 32) * 256-B block (field-major
+// rows over all groups ran 20 % slower: tools/probes/streams_probe.hip).  pendingIndex,
+// lastAppended, lastCommitted and conf are 256 consecutive int64 words each; element g of such
+// a field is row[(g >> 8) * ts + (g & 255)] (tf()).  The match of a slot is a u32 relative to
+// the group's match base (mbase(pendingIndex): pendingIndex - 1 rounded down to a multiple of
+// 2^30, fixed for a billion entries), saturated at 0 below it -- a match below the pending
+// window grants nothing whatever its value -- so a slot costs 4 B instead of 8 (r05); the 256
+// u32 of a slot's row sit in group order (r06: the epoch's lane l of half h reads groups
+// 128 h + 2 l, + 1 as one 8-B load).
 struct JrqTableArgs {
   uint32_t* match;       // match[0] row of tile 0 (u32); match[p] at match + 256 p, tile stride 2 ts
   int64_t* pi;           // pendingIndex, or kPiFollowsLc
@@ -299,10 +302,10 @@ struct JrqTableArgs {
   uint32_t G;            // groups (ld >= G rounded up to pairs; pad groups are not leaders)
   uint32_t P;
   uint32_t* invalid;     // records / headers skipped as invalid since the last jrq_table_check
-  uint64_t* changed;     // [slices][JRQ_TABLE_SLICE] out: wave w's entries at changed[128 w ..]
+  uint64_t* changed;     // [slices][JRQ_TABLE_SLICE] out: epoch wave w's slice at changed[128 w ..]
   uint32_t* n_changed;   // [slices] out
   uint8_t* status;       // [G] out, nullable
-  uint64_t* flag_ent;    // [waves][kFlagSlots][8] per 256-group epoch wave: its groups flagged
+  uint64_t* flag_ent;    // [waves][kFlagSlots][8] per 128-group epoch wave: its groups flagged
                          // JRQ_CONF_RUNS as 64-B entries {group, run starts 1-3, conf words 0-3}
   uint32_t* flag_wcnt;   // [waves] how many
 };
@@ -319,17 +322,11 @@ constexpr int kMatchPageBits = 30;  // match base granularity (JRQ_TABLE_MATCH_P
 __host__ __device__ __forceinline__ int64_t mbase(int64_t pi) {
   return pi > 0 ? ((pi - 1) & ~((int64_t{1} << kMatchPageBits) - 1)) : 0;
 }
-// Position of group k (0..255) of a tile in its u32 match rows: the epoch's lane l decides
-// groups {2l, 2l + 1} (pair A) and {128 + 2l, 129 + 2l} (pair B), and reads their four u32 of a
-// row as one 16-B load at byte 16 l.
-__host__ __device__ __forceinline__ uint32_t mslot(uint32_t k) {
-  return ((k & 127u) >> 1) * 4u + ((k >> 7) << 1) + (k & 1u);
-}
 }  // namespace jrq
 
 // The u32 match word of slot p of group g.
 __host__ __device__ __forceinline__ uint32_t& tm(const JrqTableArgs& t, uint32_t p, uint32_t g) {
-  return t.match[static_cast<size_t>(g >> 8) * (2 * t.ts) + p * 256u + jrq::mslot(g & 255u)];
+  return t.match[static_cast<size_t>(g >> 8) * (2 * t.ts) + p * 256u + (g & 255u)];
 }
 
 // One group header as the ABI carries it (include/jrq.h jrq_group_state).

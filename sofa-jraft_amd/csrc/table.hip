@@ -16,7 +16,7 @@
 //   table_list_*         host variant only: the slices gathered back to back.
 // HBM per group per epoch: reads match 4P (u32 words against the group's match base) +
 // pendingIndex, lastAppended, lastCommitted, conf 32 B; writes 8 B lastCommitted + 4 B list
-// delta per committing group, 36 B of map + count per 256 groups.
+// delta per committing group, 20 B of map + count per 128 groups.
 #include "quorum_core.h"
 
 namespace jrq {
@@ -104,9 +104,8 @@ __device__ __forceinline__ int64_t ent_field(const i64x2& v, uint32_t src, uint3
   return static_cast<int64_t>(comp ? y : x);
 }
 
-// Writes of a committing group: lastCommitted, pendingIndex -> JRQ_PI_FOLLOWS_LC once, and, when
-// the new pendingIndex moves the group's match base (once per 2^30 entries), its match words
-// re-expressed against the new base (m = base + word; words below it saturate at 0).
+// A committing group whose new pendingIndex moves its match base (once per 2^30 entries): its
+// match words re-expressed against the new base (m = base + word; words below it saturate at 0).
 template <int P>
 __device__ __forceinline__ void table_rebase(const JrqTableArgs& t, uint32_t g, int64_t b0, int64_t b1) {
   const uint64_t sh = static_cast<uint64_t>(b1 - b0);
@@ -116,27 +115,16 @@ __device__ __forceinline__ void table_rebase(const JrqTableArgs& t, uint32_t g, 
     tm(t, p, g) = s > sh ? static_cast<uint32_t>(s - sh) : 0u;
   }
 }
-template <int P>
-__device__ __forceinline__ void table_commit_one(const JrqTableArgs& t, uint32_t g, int64_t pr,
-                                                 int64_t pi, int64_t out) {
-  tf(t.lc, t, g) = out;
-  if (pr != kPiFollowsLc) tf(t.pi, t, g) = kPiFollowsLc;
-  const int64_t b0 = mbase(pi), b1 = mbase(out + 1);
-  if (b1 != b0) table_rebase<P>(t, g, b0, b1);
-}
-
 // Absolute match of a u32 word under base b.
 __device__ __forceinline__ int64_t mabs(int64_t b, uint32_t s) { return b + static_cast<int64_t>(s); }
 
-// The changed list of an epoch comes in fixed slices, one per 256-group wave range: slice s
-// (groups [256 s, 256 s + 256), decided by one wave) is 256 words at changed + 256 s: words
-// 0-3 a 256-bit map of the groups whose commit advanced (bit i = group 256 s + i), then from
-// byte 32 their deltas commit - pendingIndex + 1 as u32, in group order; n_changed[s] = how
-// many.  12 B per committing group + 4 B per 256 groups, where round 4's (delta << 32 | group)
-// words took 16 (the list's 8 B per group cost ~2 us of a 19-us C3 epoch:
-// tools/probes/table_shape_probe.hip, profiles/r05b_table_diag.json).  No reservation, no
-// atomics: round 3 reserved each workgroup's share with a 64-bit atomic, ~1.5 us per epoch.
-constexpr uint32_t kSliceMapWords = 4;
+// The changed list of an epoch comes in fixed slices, one per 128-group epoch wave: slice s
+// (groups [128 s, 128 s + 128), decided by one wave) is 128 words at changed + 128 s: words
+// 0-1 a 128-bit map of the groups whose commit advanced (bit i = group 128 s + i), then from
+// byte 16 their deltas commit - pendingIndex + 1 as u32, in group order; n_changed[s] = how
+// many.  12 B per committing group + 4 B per 128 groups.  No reservation, no atomics: each
+// slice is written by the one wave that decides its groups.
+constexpr uint32_t kSliceMapWords = 2;
 
 __device__ __forceinline__ uint64_t spread_bits(uint32_t x) {  // bit i -> bit 2i
   uint64_t v = x;
@@ -148,353 +136,271 @@ __device__ __forceinline__ uint64_t spread_bits(uint32_t x) {  // bit i -> bit 2
   return v;
 }
 
-// Shape: 256-thread workgroups, four groups per lane as two pairs -- pair A = groups (256 w +
-// 2 l, +1), pair B = pair A + 128: each int64 stream read with 16-B loads (1 KiB per wave
-// instruction), each u32 match row with one 16-B load per lane (its four groups: mslot()),
-// every load issued before the first decision: P + 8 load instructions per wave for 256
-// groups.  At <= 128 VGPRs 4 waves per SIMD fit, 4096 waves of 256 groups: a 1M-group epoch in
-// one round.  (Round 4 measured one pair per lane at 512 threads the same on the read side:
-// tools/probes/table_shape_probe.hip.)
+// Eight u32 words (one lane's pair of groups of a match row) at byte offset `off` of a
+// wave-uniform base.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const u32x2 gu32x2;
+__device__ __forceinline__ u32x2 tld2u(const int64_t* base, uint32_t off) {
+  gchar* b = (gchar*)base;
+  asm volatile("" : "+s"(b));
+  return __builtin_nontemporal_load(reinterpret_cast<const gu32x2*>(b + off));
+}
+
+// Shape (r06, "v4"): one wave per 128 groups (half a tile), two adjacent groups per lane -- the
+// pair kernel's shape.  Every int64 stream of the pair with one 16-B load (1 KiB per wave
+// instruction), every u32 match row with one 8-B load (512 B), all P + 4 loads issued before
+// the first decision.  <= 64 VGPRs at P <= 5: 8 waves per SIMD, a 1M-group epoch's 8192 waves
+// in one round, each with half of round 5's four-group chain (that kernel's single round of
+// 4096 waves at 4 per SIMD left every wave's loads, then decisions, then stores in the same
+// phase: 0.45 of spec).
 constexpr uint32_t kTableEpochBlock = 64 * kTableBlockWaves;
+#ifndef JRQ_TABLE_OCC  // waves per SIMD the epoch is compiled for at P <= 5 (A/B knob)
+#define JRQ_TABLE_OCC 7
+#endif
+
+// Runs of a flagged group from its flagged-entry slot {group, start1, start2, start3, conf0,
+// conf1, conf2, conf3} (unused runs: start INT64_MAX, conf 0).
+struct EntRuns {
+  int64_t e[8];
+  __device__ int64_t start(uint32_t r) const { return r == 0 ? kI64Min : e[r]; }
+  __device__ uint64_t conf(uint32_t r) const { return static_cast<uint64_t>(e[4 + r]); }
+};
+
+// The relative form of one group (rel_map from the u32 words): pi resolved, the window [pi, la]
+// in the words' terms -- a word u maps to r = u - o in [1, W] (o = pi - 1 - base < 2^30); an
+// ack past lastAppended is u > la - base (la >= pi - 1 >= base: headers with a smaller
+// lastAppended are refused).
+template <int P>
+__device__ __forceinline__ void map_words(int64_t pi, int64_t la, const uint32_t (&s)[P], RelGroup<P>& g) {
+  const int64_t b = mbase(pi);
+  const uint32_t o = static_cast<uint32_t>(pi - 1 - b), lab = static_cast<uint32_t>(la - b);
+  g.W = la >= pi ? static_cast<uint32_t>(la - pi) + 1u : 0u;
+  g.st = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const uint32_t dd = s[p] - o - 1u;
+    g.st |= s[p] > lab ? kStOutOfRange : 0;
+    g.r[p] = dd < g.W ? dd + 1u : 0u;
+  }
+}
 
 // One epoch over every group of the table, in place.  The single-conf decision runs in 32-bit
 // arithmetic relative to pendingIndex (rel_cand, the pair kernel's) straight from the u32 match
-// words: r = word - (pi - 1 - base) for a word inside the window; groups outside rel_domain
-// (never a real group) are decided again with 64-bit arithmetic in a wave-uniform pass.
-// A group with a conf change inside its pending window (JRQ_CONF_RUNS) is skipped by the
-// single-conf decision and walked by its own wave afterwards: its dynamic state (pendingIndex,
-// lastCommitted, lastAppended, absolute match) is what its owner lane loaded, left in the wave's
-// slice of LDS (the first 16 flagged groups of a wave; a wave-local hand-off, no barrier), and
-// its runs come from the wave's flagged-entry slots (table_flags_kernel writes them with every
-// header update: only headers change runs), eight lanes per group (one conf run per lane pair,
-// the pair splitting the run's new-conf and old-conf q-th largest).  The walk hands each
-// group's delta back to its owner lane through LDS, so the wave writes its list slice once, in
-// group order, after every decision.  No workgroup barrier, no atomics.
+// words.  A group with a conf change inside its pending window (JRQ_CONF_RUNS) is skipped by
+// that decision and decided afterwards by its own lane: its loaded state (pendingIndex word,
+// lastCommitted, lastAppended, match words) parked in the wave's slice of LDS during the
+// decisions (registers stay free for the single-conf path), its runs from the wave's
+// flagged-entry slots -- the first four loaded up front by lanes 0-15 beside the group loads
+// whatever the wave's count (a branch on the count would put a memory round trip in front of
+// every wave's loads), later ones by their owners.  Groups outside rel_domain (negative or huge
+// indexes; never a real group) are decided again with 64-bit arithmetic from reloaded words in
+// a wave-uniform branch.  No barrier beyond the wave's own, no atomics.
 template <int P>
-__global__ __launch_bounds__(kTableEpochBlock, P <= 5 ? 4 : 2) JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
+__global__ __launch_bounds__(kTableEpochBlock, P <= 5 ? JRQ_TABLE_OCC : (P <= 10 ? 4 : 2)) JRQ_SGPRS_8WAVES
+void table_epoch_kernel(JrqTableArgs t) {
   constexpr uint32_t kWaves = kTableEpochBlock / 64;
-  constexpr uint32_t kHand = 16;  // flagged groups per wave handed over through LDS
-  constexpr uint32_t kEntLds = 4; // flagged-entry slots per wave copied to lanes up front
-  __shared__ int64_t hand[kWaves][kHand][P + 3];   // {pendingIndex word, lc, la, match[P]}
-  __shared__ uint32_t walked[kWaves][kFlagSlots];  // the walk's delta per flagged rank (0: none)
+  constexpr uint32_t kEntLds = 4;  // flagged-entry slots per wave loaded up front
+  __shared__ int64_t entl[kWaves][kEntLds][8];
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
-  // wave wid holds groups [256 wid, 256 wid + 256): its flagged-entry slots, list slice, count
   const uint32_t wid = blockIdx.x * kWaves + w;
-  const uint32_t gA = wid * kTableSlice + 2u * lane;  // pair A = (gA, gA + 1), B = A + 128
-  uint64_t* const slice = t.changed + static_cast<size_t>(wid) * kTableSlice;
-  int64_t* const tile = reinterpret_cast<int64_t*>(t.match) + static_cast<size_t>(__builtin_amdgcn_readfirstlane(wid)) * t.ts;
+  const uint32_t half = wid & 1u;
+  const uint32_t g0 = wid * kListSlice + 2u * lane;  // this lane's pair (g0, g0 + 1)
+  int64_t* const tile = reinterpret_cast<int64_t*>(t.match) + static_cast<size_t>(__builtin_amdgcn_readfirstlane(wid >> 1)) * t.ts;
   const int64_t* const ent = reinterpret_cast<const int64_t*>(t.flag_ent) + static_cast<size_t>(wid) * kFlagSlots * 8;
-  // The wave's first four flagged-entry slots, loaded up front beside the single-conf loads
-  // whatever the wave's count: 16 B per lane on lanes 0-15 (entry i = lanes 4i .. 4i + 3), read
-  // by the walk through lane shuffles.  (Loading the count first and branching on it put a
-  // memory round trip in front of every wave's loads.)
-  i64x2 ev;
-  ev.x = 0;
-  ev.y = 0;
-  if (lane < 4 * kEntLds) ev = *reinterpret_cast<const i64x2*>(ent + lane * 2);
-  // per group k = 0..3 (A.x, A.y, B.x, B.y): live (inside the table), flagged, committing,
-  // outside rel_domain; commit delta, flagged rank, status
-  bool live[2], f[4], c[4], x[4], wpi[4], xb[4];
-  uint32_t d[4], rk[4], st4 = 0;
-  int64_t outv[4], bk[4];
-  {
-    i64x2 pr[2], lc[2], la[2], cw[2];
-    u32x4 mq[P];
-    const uint32_t go = 16u * lane;  // byte offset of pair A in a 2-KiB int64 row
+  // the first kEntLds slots (64 B each): one 8-B word per lane (lanes 32-63 read lanes 0-31's
+  // words again: no branch, no extra line), parked in LDS once it lands
+  const int64_t ev = __builtin_nontemporal_load(ent + (lane & (8 * kEntLds - 1)));
+  const uint32_t go = 16u * lane + 1024u * half;  // the pair's byte offset in a 2-KiB int64 row
+  const i64x2 pr = tld2o(tile + 128 * P, go);
+  const i64x2 la = tld2o(tile + 128 * P + 256, go);
+  const i64x2 lc = tld2o(tile + 128 * P + 512, go);
+  const i64x2 cw = tld2o(tile + 128 * P + 768, go);
+  u32x2 mq[P];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      live[h] = gA + 128u * h < t.G;
-      pr[h] = tld2o(tile + 128 * P, go + 1024u * h);
-      lc[h] = tld2o(tile + 128 * P + 512, go + 1024u * h);
-      la[h] = tld2o(tile + 128 * P + 256, go + 1024u * h);
-      cw[h] = tld2o(tile + 128 * P + 768, go + 1024u * h);
-    }
+  for (int p = 0; p < P; ++p) mq[p] = tld2u(tile + 128 * p, 8u * lane + 512u * half);
+  if (lane < 8 * kEntLds) entl[w][lane >> 3][lane & 7u] = ev;
+  bool f[2], c[2], x[2], wpi[2];
+  uint32_t d[2], st[2], rk[2];
+  int64_t outv[2], pir[2];
+  uint64_t bf[2];
 #pragma unroll
-    for (int p = 0; p < P; ++p) mq[p] = tld4o(tile + 128 * p, go);  // groups A.x, A.y, B.x, B.y
-    uint32_t kbase = 0;  // hand-off ranks: A.x, A.y, B.x, B.y groups in the flags kernel's order
+  for (int j = 0; j < 2; ++j) {
+    const uint32_t g = g0 + j;
+    const int64_t prk = j ? pr.y : pr.x, lck = j ? lc.y : lc.x, lak = j ? la.y : la.x;
+    const uint64_t cwk = static_cast<uint64_t>(j ? cw.y : cw.x);
+    const bool in = g < t.G;
+    f[j] = in && (cwk >> 63);
+    bf[j] = __ballot(f[j]);
+    rk[j] = (j ? __popcll(bf[0]) : 0u) + __popcll(bf[j] & below);
+    const int64_t pi = prk == kPiFollowsLc ? lck + 1 : prk;
+    uint32_t s[P];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int h = k >> 1;
-      const bool y = k & 1;
-      const uint32_t g = gA + 128u * h + (y ? 1u : 0u);
-      const int64_t prk = y ? pr[h].y : pr[h].x, lck = y ? lc[h].y : lc[h].x;
-      const int64_t lak = y ? la[h].y : la[h].x;
-      const uint64_t cwk = static_cast<uint64_t>(y ? cw[h].y : cw[h].x);
-      const bool in = live[h] && g < t.G;
-      f[k] = in && (cwk >> 63);
-      const uint64_t bf = __ballot(f[k]);
-      rk[k] = kbase + __popcll(bf & below);
-      kbase += __popcll(bf);
-      uint32_t s[P];
+    for (int p = 0; p < P; ++p) s[p] = j ? mq[p].y : mq[p].x;
+    RelGroup<P> rg;
+    map_words<P>(pi, lak, s, rg);
+    uint8_t s8;
+    const uint32_t r = rel_cand<P>(cwk, rg, s8);
+    st[j] = pi == 0 ? kStNotLeader : s8;
+    x[j] = in && !rel_domain(pi, lak);
+    c[j] = in && !f[j] && !x[j] && pi != 0 && r >= 1u && pi - 1 + static_cast<int64_t>(r) > lck;
+    d[j] = r;
+    outv[j] = pi - 1 + static_cast<int64_t>(r);
+    pir[j] = pi;
+    wpi[j] = prk != kPiFollowsLc;
+    // a flagged group (a conf change inside its window): its lane decides its runs right here,
+    // from the same relative words, the runs from its flagged-entry slot (LDS for the first
+    // kEntLds of the wave, memory beyond)
+    if (__builtin_expect(bf[j] != 0, 0)) {  // (wave-uniform)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (f[j] && !x[j]) {
+        uint32_t k = rk[j];
+        asm volatile("" : "+v"(k));
+        int64_t es[kTableMaxRuns];
+        uint64_t ec[kTableMaxRuns];
+        if (k < kEntLds) {
+          const int64_t* e = entl[w][k];
 #pragma unroll
-      for (int p = 0; p < P; ++p) s[p] = k == 0 ? mq[p].x : k == 1 ? mq[p].y : k == 2 ? mq[p].z : mq[p].w;
-      const int64_t pi = prk == kPiFollowsLc ? lck + 1 : prk;
-      const int64_t b = mbase(pi);
-      if (f[k] && rk[k] < kHand) {  // a flagged group's state -> the wave's hand-off slot
-        int64_t* hs = hand[w][rk[k]];
-        hs[0] = prk;
-        hs[1] = lck;
-        hs[2] = lak;
+          for (int q = 1; q < kTableMaxRuns; ++q) es[q] = e[q];
 #pragma unroll
-        for (int p = 0; p < P; ++p) hs[3 + p] = mabs(b, s[p]);
-      }
-#if JRQ_TABLE_AB_NODECIDE  // diagnosis only (tools/ab_build.sh): loads and stores, no decision
-      uint8_t st = static_cast<uint8_t>(cwk & 1u) | static_cast<uint8_t>(s[P - 1] & 2u);
-      const uint32_t r = static_cast<uint32_t>(lak - pi + 1);
-#else
-      // the window [pi, la] in the words' terms: a word u maps to r = u - o in [1, W] (o =
-      // pi - 1 - base < 2^30), an ack past lastAppended is u > la - base
-      RelGroup<P> rg;
-      const uint32_t o = static_cast<uint32_t>(pi - 1 - b), lab = static_cast<uint32_t>(lak - b);
-      rg.W = lak >= pi ? static_cast<uint32_t>(lak - pi) + 1u : 0u;
-      rg.st = 0;
+          for (int q = 1; q < kTableMaxRuns; ++q) ec[q] = static_cast<uint64_t>(e[4 + q]);
+        } else {
+          const int64_t* e = ent + static_cast<size_t>(k) * 8;
 #pragma unroll
-      for (int p = 0; p < P; ++p) {
-        const uint32_t dd = s[p] - o - 1u;
-        rg.st |= s[p] > lab ? kStOutOfRange : 0;
-        rg.r[p] = dd < rg.W ? dd + 1u : 0u;
-      }
-      uint8_t st;
-      const uint32_t r = rel_cand<P>(cwk, rg, st);
-#endif
-      st = pi == 0 ? kStNotLeader : st;
-      // (the u32 words need a window below 2^31, which header / record checks guarantee)
-      x[k] = in && !f[k] && !(pi == 0 || (pi > 0 && pi < (int64_t{1} << 62) &&
-                                            (lak < pi || lak - pi < int64_t{0x7FFFFFFF})));
-      // a flagged group is decided by the walk (its single-conf result here is discarded)
-      c[k] = in && !f[k] && !x[k] && pi != 0 && r >= 1u && pi - 1 + static_cast<int64_t>(r) > lck;
-      d[k] = r;
-      outv[k] = pi - 1 + static_cast<int64_t>(r);
-      bk[k] = b;
-      // pendingIndex = lastCommittedIndex + 1 from now on (BallotBox.java:131-132): one store
-      // per group and leadership, the steady state writes lastCommitted only; a commit that
-      // moves the match base (once per 2^30 entries) re-expresses the group's words
-      wpi[k] = prk != kPiFollowsLc;
-      xb[k] = c[k] && mbase(outv[k] + 1) != b;
-      st4 |= static_cast<uint32_t>(st) << (8 * k);
-    }
-    // the single-conf commits' lastCommitted, a pair at a time (the stores leave before the walk)
+          for (int q = 1; q < kTableMaxRuns; ++q) es[q] = e[q];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const bool ca = c[2 * h], cb = c[2 * h + 1];
-      const uint32_t off = go + 1024u * h;
-#if JRQ_TABLE_AB_LC != 1
-      int64_t* const lcb = tile + 128 * P + 512;
-      if (ca && cb) {
-        i64x2 v;
-        v.x = outv[2 * h];
-        v.y = outv[2 * h + 1];
-        tst2o(lcb, off, v);
-      } else {
-        if (ca) tst1o(lcb, off, outv[2 * h]);
-        if (cb) tst1o(lcb, off + 8u, outv[2 * h + 1]);
-      }
-#endif
-      if (ca && wpi[2 * h]) tst1o(tile + 128 * P, off, kPiFollowsLc);
-      if (cb && wpi[2 * h + 1]) tst1o(tile + 128 * P, off + 8u, kPiFollowsLc);
-    }
-    if (__builtin_expect(__ballot(xb[0] || xb[1] || xb[2] || xb[3]) != 0, 0)) {
-#pragma unroll 1
-      for (uint32_t k = 0; k < 4; ++k) {
-        const bool mine = k == 0 ? xb[0] : k == 1 ? xb[1] : k == 2 ? xb[2] : xb[3];
-        const int64_t b0 = k == 0 ? bk[0] : k == 1 ? bk[1] : k == 2 ? bk[2] : bk[3];
-        const int64_t o = k == 0 ? outv[0] : k == 1 ? outv[1] : k == 2 ? outv[2] : outv[3];
-        if (mine) table_rebase<P>(t, gA + 128u * (k >> 1) + (k & 1u), b0, mbase(o + 1));
-      }
-    }
-  }
-  if (t.status) {  // (a flagged or 64-bit group's status is written by its own pass)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t g = gA + 128u * h;
-      if (!live[h]) continue;
-      const uint32_t s2 = (st4 >> (16 * h)) & 0xFFFFu;
-      const bool ka = !f[2 * h] && !x[2 * h], kb = !f[2 * h + 1] && !x[2 * h + 1] && g + 1 < t.G;
-      if (ka && kb)
-        st_tab(static_cast<uint16_t>(s2), reinterpret_cast<uint16_t*>(t.status + g));
-      else {
-        if (ka) t.status[g] = static_cast<uint8_t>(s2);
-        if (kb) t.status[g + 1] = static_cast<uint8_t>(s2 >> 8);
-      }
-    }
-  }
-  // The walk.  Its reads are LDS (the hand-off slots and entries 0-3) except in waves with
-  // more than 4 / 16 flagged groups.
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the hand-off slots: this wave's)
-  __builtin_amdgcn_wave_barrier();
-  // eight lanes per flagged group: run r = (lane >> 1) & 3 of group slot lane >> 3, the lane
-  // pair splitting the run's two quorum checks (new conf, old conf: one q-th largest each,
-  // joined by one exchange)
-  const uint32_t q = lane >> 3, r = (lane >> 1) & 3u, mh = lane & 1u;
-  const uint32_t nflag = __popcll(__ballot(f[0])) + __popcll(__ballot(f[1])) +
-                         __popcll(__ballot(f[2])) + __popcll(__ballot(f[3]));
-  for (uint32_t base = 0; base < nflag; base += 8) {  // (wave-uniform)
-    const uint32_t i = base + q;
-    bool act = i < nflag;
-    // the entry {group, start1, start2, start3, conf0 .. conf3}: run r's start, the next run's
-    // start and run r's conf word (entries 0-3 from the lanes holding them, later ones from
-    // memory; values, not a pointer that could be either: a generic pointer makes flat loads,
-    // which wait for every outstanding memory operation)
-    int64_t eh = 0, ers = kI64Min, enx = kI64Max;
-    uint64_t rc = 0;
-    const uint32_t ie = i < kEntLds ? i : 0u;  // (every lane shuffles: the wave is converged)
-    const int64_t f0 = ent_field(ev, 4u * ie, 0u);
-    const int64_t fr = ent_field(ev, 4u * ie + (r >> 1), r & 1u);
-    const int64_t fn = ent_field(ev, 4u * ie + ((r + 1) >> 1), (r + 1) & 1u);
-    const int64_t fc = ent_field(ev, 4u * ie + ((4u + r) >> 1), (4u + r) & 1u);
-    if (act && i < kEntLds) {
-      eh = f0;
-      if (r != 0) ers = fr;
-      if (r != 3) enx = fn;
-      rc = static_cast<uint64_t>(fc);
-    } else if (act) {
-      const int64_t* e = ent + static_cast<size_t>(i) * 8;
-      eh = e[0];
-      if (r != 0) ers = e[r];
-      if (r != 3) enx = e[r + 1];
-      rc = static_cast<uint64_t>(e[4 + r]);
-    }
-    const uint32_t h = static_cast<uint32_t>(eh);
-    const int64_t rs = ers, nx = enx;
-    act = act && h < t.G;  // (the flags kernel writes only table groups: a guard, not a case)
-    int64_t cand64 = kI64Min, hpr = 0, hlc = 0, hla = 0, pi = 0;
-    uint8_t st = 0;
-    bool relp = false;
-    uint32_t kx = 0xFFFFFFFFu, sr = 0, er = 0;
-    if (act) {
-      int64_t hm[P];
-      if (i < kHand) {  // from the owner lane, through LDS
-        const int64_t* hs = hand[w][i];
-        hpr = hs[0];
-        hlc = hs[1];
-        hla = hs[2];
-#pragma unroll
-        for (int p = 0; p < P; ++p) hm[p] = hs[3 + p];
-      } else {  // more flagged groups than hand-off slots: reload (rare)
-        hpr = tf(t.pi, t, h);
-        hlc = tf(t.lc, t, h);
-        hla = tf(t.la, t, h);
-        const int64_t bb = mbase(hpr == kPiFollowsLc ? hlc + 1 : hpr);
-#pragma unroll
-        for (int p = 0; p < P; ++p) hm[p] = mabs(bb, tm(t, p, h));
-      }
-      pi = hpr == kPiFollowsLc ? hlc + 1 : hpr;
-      if (pi == 0) {
-        st = kStNotLeader;
-      } else {
-        const int64_t s = rs > pi ? rs : pi;
-        const int64_t e = nx == kI64Max ? hla : nx - 1;
-        const int64_t ee = e < hla ? e : hla;
-        // 32-bit arithmetic relative to pendingIndex for every real group, 64-bit outside
-        // rel_domain
-        if (rel_domain(pi, hla)) {
-          RelGroup<P> rg;
-          rel_map<P>(pi, hla, hm, rg);
-          st = rg.st;
-          if (ee >= s) {  // run_candidate_rel, this lane's half of it
-            if ((rc & 0xFFFFu) == 0) st |= kStEmptyConf;
-            relp = true;
-            sr = static_cast<uint32_t>(s - pi) + 1u;
-            er = static_cast<uint32_t>(ee - pi) + 1u;
-            const uint32_t msk = static_cast<uint32_t>((rc >> (mh ? 16 : 0)) & 0xFFFFu);
-            const uint32_t qq = static_cast<uint32_t>((rc >> (mh ? 40 : 32)) & 0xFFu);
-            kx = qq == 0 ? rg.W : kth_largest_rel<P>(rg.r, msk, qq);
-          }
-        } else {  // both lanes of the pair: the whole 64-bit run_candidate
-          st = mask_out_of_range<P>(hm, hla);
-          cand64 = run_candidate<P>(hm, rc, s, ee, st);
+          for (int q = 1; q < kTableMaxRuns; ++q) ec[q] = static_cast<uint64_t>(e[4 + q]);
         }
+        uint8_t sw = rg.st;
+        int64_t best = kI64Min;
+        if (pi != 0) {
+          {  // run 0, [pi, start1 - 1] under the group's conf word: its bound is r, the
+             // single-conf decision's (the same q-th largests), so no sort of its own
+            const int64_t e = es[1] == kI64Max ? lak : es[1] - 1;
+            const int64_t ee = e < lak ? e : lak;
+            if (ee >= pi) {
+              if ((cwk & 0xFFFFu) == 0) sw |= kStEmptyConf;
+              const uint32_t er = static_cast<uint32_t>(ee - pi) + 1u;
+              const uint32_t cc = r < er ? r : er;
+              if (cc >= 1u) best = pi - 1 + static_cast<int64_t>(cc);
+            }
+          }
+#pragma unroll
+          for (uint32_t q = 1; q < kTableMaxRuns; ++q) {
+            if (es[q] == kI64Max) break;  // unused runs (they come last)
+            const int64_t nx = q + 1 < kTableMaxRuns ? es[q + 1] : kI64Max;
+            const int64_t sr = es[q] > pi ? es[q] : pi;
+            const int64_t e = nx == kI64Max ? lak : nx - 1;
+            const int64_t ee = e < lak ? e : lak;
+            const int64_t cand = run_candidate_rel<P>(rg, ec[q], pi, sr, ee, sw);
+            best = cand > best ? cand : best;
+          }
+        }
+        st[j] = pi == 0 ? kStNotLeader : sw;
+        c[j] = pi != 0 && best > lck;
+        outv[j] = best;
+        d[j] = static_cast<uint32_t>(best - pi + 1);
       }
-    }
-    // the pair's two bounds (every lane exchanges: the wave stays converged)
-    const uint32_t kp = dpp32<kDppXor1>(kx);
-    int64_t cand = cand64;
-    if (relp) {
-      uint32_t cc = kx < kp ? kx : kp;
-      cc = cc < er ? cc : er;
-      cand = cc >= sr ? pi - 1 + static_cast<int64_t>(cc) : kI64Min;
-    }
-    // max over the group's 8 lanes, complete on its lead lane (the lane pairs agree already)
-    cand = max(cand, dpp64<kDppXor2>(cand));
-    cand = max(cand, dpp64<kDppHalfMirror>(cand));
-    uint32_t s32 = st;
-    s32 |= dpp32<kDppXor1>(s32);
-    s32 |= dpp32<kDppXor2>(s32);
-    s32 |= dpp32<kDppHalfMirror>(s32);
-    const bool lead = (lane & 7u) == 0;
-    const bool commit = act && lead && cand > hlc;  // pi == 0 (not the leader): kI64Min
-    if (act && lead) {
-      if (t.status) t.status[h] = static_cast<uint8_t>(s32);
-      if (commit) table_commit_one<P>(t, h, hpr, pi, cand);
-      walked[w][i] = commit ? static_cast<uint32_t>(cand - pi + 1) : 0u;
     }
   }
   // groups outside rel_domain (negative or huge indexes; never a real group): the 64-bit
-  // decision from reloaded words, in a wave-uniform branch kept out of the fast path's registers
-  if (__builtin_expect(__ballot(x[0] || x[1] || x[2] || x[3]) != 0, 0)) {
+  // decision from reloaded words, flagged or not, kept out of the fast path's registers
+  if (__builtin_expect(__ballot(x[0] || x[1]) != 0, 0)) {
 #pragma unroll 1
-    for (uint32_t k = 0; k < 4; ++k) {
-      const bool mine = k == 0 ? x[0] : k == 1 ? x[1] : k == 2 ? x[2] : x[3];
-      const uint32_t h = gA + 128u * (k >> 1) + (k & 1u);
+    for (uint32_t j = 0; j < 2; ++j) {
+      const bool mine = j ? x[1] : x[0];
       if (!mine) continue;
-      const int64_t pr = tf(t.pi, t, h), lc = tf(t.lc, t, h), la = tf(t.la, t, h);
-      const int64_t pi = pr == kPiFollowsLc ? lc + 1 : pr;
+      uint32_t h = g0 + j;
+      asm volatile("" : "+v"(h));
+      const int64_t prx = tf(t.pi, t, h), lcx = tf(t.lc, t, h), lax = tf(t.la, t, h);
+      const int64_t pi = prx == kPiFollowsLc ? lcx + 1 : prx;
       const int64_t bb = mbase(pi);
+      const uint64_t cwx = tf(t.conf, t, h);
       int64_t m[P];
 #pragma unroll
       for (int p = 0; p < P; ++p) m[p] = mabs(bb, tm(t, p, h));
-      int64_t out = 0;
-      uint8_t st = 0;
-      decide_single<P>(pi, la, lc, tf(t.conf, t, h), m, out, st);
-      if (t.status) t.status[h] = st;
-      const bool commit = out > lc;
-      if (commit) table_commit_one<P>(t, h, pr, pi, out);
-      const uint32_t dk = commit ? static_cast<uint32_t>(out - pi + 1) : 0u;
-      if (k == 0) { c[0] = commit; d[0] = dk; }
-      if (k == 1) { c[1] = commit; d[1] = dk; }
-      if (k == 2) { c[2] = commit; d[2] = dk; }
-      if (k == 3) { c[3] = commit; d[3] = dk; }
+      int64_t out = lcx;
+      uint8_t s8 = 0;
+      if (cwx >> 63) {  // its runs from the cold rows (run 0's conf in the conf word)
+        EntRuns R;
+        R.e[0] = h;
+        for (int r = 1; r < kTableMaxRuns; ++r) {
+          R.e[r] = t.xstart[static_cast<size_t>(r - 1) * t.ld + h];
+          R.e[4 + r] = static_cast<int64_t>(t.xconf[static_cast<size_t>(r - 1) * t.ld + h]);
+        }
+        R.e[4] = static_cast<int64_t>(cwx & ~kConfRuns);
+        uint32_t nr = 1;
+        while (nr < kTableMaxRuns && R.e[nr] != kI64Max) ++nr;
+        s8 = mask_out_of_range<P>(m, lax);
+        out = pi == 0 ? lcx : runs_best<P>(R, nr, pi, lax, lcx, m, s8);
+        s8 = pi == 0 ? kStNotLeader : s8;
+      } else {
+        decide_single<P>(pi, lax, lcx, cwx, m, out, s8);
+      }
+      const bool commit = out > lcx;
+      const uint32_t dj = static_cast<uint32_t>(out - pi + 1);
+      if (j == 0) { c[0] = commit; d[0] = dj; outv[0] = out; st[0] = s8; }
+      else        { c[1] = commit; d[1] = dj; outv[1] = out; st[1] = s8; }
     }
   }
-  // the walked groups' results back to their owner lanes
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (f[k]) {
-      const uint32_t dk = walked[w][rk[k]];
-      c[k] = dk != 0;
-      d[k] = dk;
+  // state writes of the committing groups: lastCommitted (a pair at a time), pendingIndex ->
+  // JRQ_PI_FOLLOWS_LC once (BallotBox.java:131-132: the steady state writes lastCommitted only),
+  // and, when the new pendingIndex moves the match base (once per 2^30 entries), the words
+  // re-expressed against it
+  {
+    int64_t* const lcb = tile + 128 * P + 512;
+    // the pair's row offset again, from the lane id (mbcnt) and the wave's half (an SGPR):
+    // recomputed, not kept live across the decisions (it was spilled and reloaded per store)
+    const uint32_t go = 16u * __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) +
+                        1024u * (__builtin_amdgcn_readfirstlane(wid) & 1u);
+#if JRQ_TABLE_AB_LC != 1
+    if (c[0] && c[1]) {
+      i64x2 v;
+      v.x = outv[0];
+      v.y = outv[1];
+      tst2o(lcb, go, v);
+    } else {
+      if (c[0]) tst1o(lcb, go, outv[0]);
+      if (c[1]) tst1o(lcb, go + 8u, outv[1]);
     }
-  // the list slice, in group order: the map (pair A's groups are bits 0-127 as 2 l, 2 l + 1,
-  // pair B's bits 128-255), then the deltas at their ranks (a lane's committing groups sit at
-  // consecutive ranks: one 8-B store per pair when both commit)
-  const uint64_t bA0 = __ballot(c[0]), bA1 = __ballot(c[1]), bB0 = __ballot(c[2]), bB1 = __ballot(c[3]);
-  const uint32_t nA = __popcll(bA0) + __popcll(bA1);
-  const uint32_t cnt = nA + __popcll(bB0) + __popcll(bB1);
+#endif
+    if (c[0] && wpi[0]) tst1o(tile + 128 * P, go, kPiFollowsLc);
+    if (c[1] && wpi[1]) tst1o(tile + 128 * P, go + 8u, kPiFollowsLc);
+    const bool xb0 = c[0] && mbase(outv[0] + 1) != mbase(pir[0]);
+    const bool xb1 = c[1] && mbase(outv[1] + 1) != mbase(pir[1]);
+    if (__builtin_expect(__ballot(xb0 || xb1) != 0, 0)) {
+      if (xb0) table_rebase<P>(t, g0, mbase(pir[0]), mbase(outv[0] + 1));
+      if (xb1) table_rebase<P>(t, g0 + 1, mbase(pir[1]), mbase(outv[1] + 1));
+    }
+  }
+  if (t.status && g0 < t.G) {
+    if (g0 + 1 < t.G)
+      st_tab(static_cast<uint16_t>(st[0] | (st[1] << 8)), reinterpret_cast<uint16_t*>(t.status + g0));
+    else
+      t.status[g0] = static_cast<uint8_t>(st[0]);
+  }
+  // the list slice, in group order: the map (lane l's pair = bits 2 l, 2 l + 1), then the deltas
+  // at their ranks (one 8-B store when both groups of the pair commit at an even rank)
+  const uint64_t b0 = __ballot(c[0]), b1 = __ballot(c[1]);
+  const uint32_t cnt = __popcll(b0) + __popcll(b1);
   // (a wave past the table's last slice -- the grid is whole workgroups -- owns no slice: the
   // caller's list has room for jrq_table_slices(t) slices only)
-  const bool owns = static_cast<uint64_t>(wid) * kTableSlice < t.G;
+  const bool owns = static_cast<uint64_t>(wid) * kListSlice < t.G;
+  uint64_t* const slice = t.changed + static_cast<size_t>(wid) * kListSlice;
 #if !JRQ_TABLE_AB_NOLIST  // (diagnosis knob: no list)
   if (lane < kSliceMapWords && owns) {
-    const uint64_t lo = lane < 2 ? bA0 : bB0, hi = lane < 2 ? bA1 : bB1;
-    const uint32_t sh = (lane & 1u) * 32u;
-    slice[lane] = spread_bits(static_cast<uint32_t>(lo >> sh)) | (spread_bits(static_cast<uint32_t>(hi >> sh)) << 1);
+    const uint32_t sh = lane * 32u;
+    slice[lane] = spread_bits(static_cast<uint32_t>(b0 >> sh)) | (spread_bits(static_cast<uint32_t>(b1 >> sh)) << 1);
   }
   uint32_t* const deltas = reinterpret_cast<uint32_t*>(slice + kSliceMapWords);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const uint64_t b0 = h ? bB0 : bA0, b1 = h ? bB1 : bA1;
-    const uint32_t at = (h ? nA : 0u) + __popcll(b0 & below) + __popcll(b1 & below);
-    const bool c0 = c[2 * h], c1 = c[2 * h + 1];
-    if (c0 && c1 && !(at & 1u)) {
-      *reinterpret_cast<uint64_t*>(deltas + at) = static_cast<uint64_t>(d[2 * h]) | (static_cast<uint64_t>(d[2 * h + 1]) << 32);
-    } else {
-      if (c0) deltas[at] = d[2 * h];
-      if (c1) deltas[at + (c0 ? 1u : 0u)] = d[2 * h + 1];
-    }
+  const uint32_t at = __popcll(b0 & below) + __popcll(b1 & below);
+  if (c[0] && c[1] && !(at & 1u)) {
+    *reinterpret_cast<uint64_t*>(deltas + at) = static_cast<uint64_t>(d[0]) | (static_cast<uint64_t>(d[1]) << 32);
+  } else {
+    if (c[0]) deltas[at] = d[0];
+    if (c[1]) deltas[at + (c[0] ? 1u : 0u)] = d[1];
   }
 #endif
   if (lane == 0 && owns) t.n_changed[wid] = cnt;
@@ -534,9 +440,9 @@ __global__ __launch_bounds__(kScanBlock) void table_list_scan_kernel(const uint3
   if (threadIdx.x == 0) total_out[0] = carry;
 }
 
-// One wave per slice: lane l takes the slice's groups 4 l .. 4 l + 3 (a nibble of its map),
-// their ranks from the map's popcounts, and writes each listed group as the host list's word
-// (delta << 32 | group).
+// One wave per slice: lane l takes the slice's groups 2 l, 2 l + 1 (two bits of its map), their
+// ranks from the map's popcounts, and writes each listed group as the host list's word (delta
+// << 32 | group).
 __global__ __launch_bounds__(512) void table_list_gather_kernel(const uint64_t* __restrict__ changed,
                                                                 const uint32_t* __restrict__ n,
                                                                 const uint32_t* __restrict__ off,
@@ -544,36 +450,31 @@ __global__ __launch_bounds__(512) void table_list_gather_kernel(const uint64_t* 
                                                                 uint64_t* __restrict__ out) {
   const uint32_t s = blockIdx.x * 8u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
   if (s >= slices || n[s] == 0) return;
-  const uint64_t* sl = changed + static_cast<size_t>(s) * kTableSlice;
+  const uint64_t* sl = changed + static_cast<size_t>(s) * kListSlice;
   const uint32_t* deltas = reinterpret_cast<const uint32_t*>(sl + kSliceMapWords);
-  const uint32_t wd = lane >> 4, sh = 4u * (lane & 15u);
+  const uint32_t wd = lane >> 5, sh = 2u * (lane & 31u);
   const uint64_t word = sl[wd];
-  uint32_t at = off[s] + __popcll(word & ((1ull << sh) - 1ull));
-  uint32_t rank = __popcll(word & ((1ull << sh) - 1ull));
-  for (uint32_t u = 0; u < wd; ++u) {
-    const uint32_t pc = __popcll(sl[u]);
-    at += pc;
-    rank += pc;
-  }
-  uint32_t nib = static_cast<uint32_t>(word >> sh) & 15u;
-  while (nib) {
-    const uint32_t b = __builtin_ctz(nib);
-    nib &= nib - 1u;
-    out[at++] = (static_cast<uint64_t>(deltas[rank++]) << 32) | (s * kTableSlice + 4u * lane + b);
+  uint32_t rank = __popcll(word & ((1ull << sh) - 1ull)) + (wd ? static_cast<uint32_t>(__popcll(sl[0])) : 0u);
+  uint32_t at = off[s] + rank;
+  uint32_t bits = static_cast<uint32_t>(word >> sh) & 3u;
+  while (bits) {
+    const uint32_t b = __builtin_ctz(bits);
+    bits &= bits - 1u;
+    out[at++] = (static_cast<uint64_t>(deltas[rank++]) << 32) | (s * kListSlice + 2u * lane + b);
   }
 }
 
-// The flagged-entry slots: per 256-group wave range of the epoch kernel, its groups flagged
-// JRQ_CONF_RUNS, each as a 64-B entry {group, start1 | start2, start3 | conf0, conf1 | conf2,
-// conf3} (run starts and conf words; unused runs: start INT64_MAX, conf 0), and their count.
-// Rebuilt after every update that carries group headers (only headers change runs and flags);
-// the waves map exactly as the epoch kernel's (lane l: pairs A = 256 w + 2 l and B = A + 128,
-// entries in the order A.x, A.y, B.x, B.y groups by ballot rank), no barrier, no atomics.
+// The flagged-entry slots: per 128-group epoch wave, its groups flagged JRQ_CONF_RUNS, each as
+// a 64-B entry {group, start1, start2, start3, conf0, conf1, conf2, conf3} (run starts and conf
+// words; unused runs: start INT64_MAX, conf 0), and their count.  Rebuilt after every update
+// that carries group headers (only headers change runs and flags); the waves map exactly as the
+// epoch kernel's (lane l: groups 128 w + 2 l, + 1; entries in the order of the even groups' ballot
+// ranks, then the odd groups'), no barrier, no atomics.
 constexpr uint32_t kFlagBlock = 64 * kTableBlockWaves;
 __global__ __launch_bounds__(kFlagBlock) void table_flags_kernel(JrqTableArgs t) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wid = blockIdx.x * (kFlagBlock / 64) + (threadIdx.x >> 6);
-  const uint32_t gA = wid * kTableSlice + 2u * lane;
+  const uint32_t g = wid * kListSlice + 2u * lane;
   const uint64_t below = (1ull << lane) - 1ull;
   int64_t* const ent = reinterpret_cast<int64_t*>(t.flag_ent) + static_cast<size_t>(wid) * kFlagSlots * 8;
   auto put = [&](uint32_t k, uint32_t h) {
@@ -584,22 +485,16 @@ __global__ __launch_bounds__(kFlagBlock) void table_flags_kernel(JrqTableArgs t)
     for (int r = 1; r < kTableMaxRuns; ++r)
       e[4 + r] = static_cast<int64_t>(t.xconf[static_cast<size_t>(r - 1) * t.ld + h]);
   };
-  uint32_t base = 0;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const uint32_t g = gA + 128u * h;
-    bool f0 = false, f1 = false;
-    if (g < t.G) {
-      const i64x2 cw = tld2(reinterpret_cast<const int64_t*>(&tf(t.conf, t, g)));
-      f0 = static_cast<uint64_t>(cw.x) >> 63;
-      f1 = (static_cast<uint64_t>(cw.y) >> 63) && g + 1 < t.G;
-    }
-    const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
-    if (f0) put(base + __popcll(b0 & below), g);
-    if (f1) put(base + __popcll(b0) + __popcll(b1 & below), g + 1);
-    base += __popcll(b0) + __popcll(b1);
+  bool f0 = false, f1 = false;
+  if (g < t.G) {
+    const i64x2 cw = tld2(reinterpret_cast<const int64_t*>(&tf(t.conf, t, g)));
+    f0 = static_cast<uint64_t>(cw.x) >> 63;
+    f1 = (static_cast<uint64_t>(cw.y) >> 63) && g + 1 < t.G;
   }
-  if (lane == 0) t.flag_wcnt[wid] = base;
+  const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
+  if (f0) put(__popcll(b0 & below), g);
+  if (f1) put(__popcll(b0) + __popcll(b1 & below), g + 1);
+  if (lane == 0) t.flag_wcnt[wid] = __popcll(b0) + __popcll(b1);
 }
 
 // Group headers: one lane per header (a group appears at most once per call).
@@ -701,7 +596,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_upd
   if (n_states) {
     hipLaunchKernelGGL(jrq::table_states_kernel, dim3((n_states + 255) / 256), dim3(256), 0,
                        stream, *a, states, n_states);
-    const uint32_t waves = (a->G + jrq::kTableSlice - 1) / jrq::kTableSlice;
+    const uint32_t waves = (a->G + jrq::kListSlice - 1) / jrq::kListSlice;
     hipLaunchKernelGGL(jrq::table_flags_kernel, dim3((waves + jrq::kFlagBlock / 64 - 1) / (jrq::kFlagBlock / 64)),
                        dim3(jrq::kFlagBlock), 0, stream, *a);
   }
@@ -723,7 +618,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_lis
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_epoch(
     const JrqTableArgs* a, hipStream_t stream) {
-  const uint32_t waves = (a->G + jrq::kTableSlice - 1) / jrq::kTableSlice;
+  const uint32_t waves = (a->G + jrq::kListSlice - 1) / jrq::kListSlice;
   const dim3 grid((waves + jrq::kTableEpochBlock / 64 - 1) / (jrq::kTableEpochBlock / 64)), blk(jrq::kTableEpochBlock);
   switch (a->P) {
 #define JRQ_CASE(P)                                                                   \

@@ -56,7 +56,7 @@ TABLE_MAX_RUNS = 4                     # JRQ_TABLE_MAX_RUNS
 TABLE_MAX_GROUPS = 1 << 27             # JRQ_TABLE_MAX_GROUPS
 PI_FOLLOWS_LC = -(1 << 63)             # JRQ_PI_FOLLOWS_LC
 REC_LAST_APPENDED = 16                 # JRQ_REC_LAST_APPENDED
-TABLE_SLICE = 256                      # JRQ_TABLE_SLICE
+TABLE_SLICE = 128                      # JRQ_TABLE_SLICE
 STATE_RESET_MATCH = 1                  # JRQ_STATE_RESET_MATCH
 READINDEX_PENDING, READINDEX_SUCCESS, READINDEX_FAILURE, READINDEX_INVALID = 0, 1, 2, 3  # JRQ_READINDEX_*
 # jrq_debug_option (test / A-B hooks)

@@ -622,14 +622,14 @@ class Table:
 
     def epoch_dev(self, changed_out, n_changed_out, status_out=None):
         """Device variant: changed_out capacity TABLE_SLICE * slices() words, n_changed_out
-        int32[slices()] per-slice counts (slice s lists groups [256 s, 256 s + 256) at
-        changed_out[256 s ..], see include/jrq.h)."""
+        int32[slices()] per-slice counts (slice s lists groups [128 s, 128 s + 128) at
+        changed_out[128 s ..], see include/jrq.h)."""
         check(self._L.jrq_table_epoch_dev(self._h, _dev_ptr(changed_out), _dev_ptr(n_changed_out),
                                           _dev_ptr(status_out)), self._eng.handle)
 
     def gather_dev_list(self, changed_out, n_changed_out) -> np.ndarray:
         """Host copy of a device-variant list as the host variant's words (delta << 32 | group),
-        slices in order: each slice is a 256-bit map of its listed groups, then their u32
+        slices in order: each slice is a 128-bit map of its listed groups, then their u32
         deltas in group order (include/jrq.h jrq_table_epoch_dev)."""
         return decode_slices(_host_np(changed_out), _host_np(n_changed_out))
 
@@ -656,16 +656,18 @@ class Table:
         return v
 
 
-def decode_slices(slices, counts) -> np.ndarray:
+def decode_slices(slices, counts, S: int | None = None) -> np.ndarray:
     """jrq_table_epoch_dev's slices (int64 / uint64 words, JRQ_TABLE_SLICE per slice) and
-    per-slice counts -> the host list's words (delta << 32 | group), in group order."""
-    S = _lib.TABLE_SLICE
+    per-slice counts -> the host list's words (delta << 32 | group), in group order.  (`S`:
+    another library build's slice size, for A/B tools.)"""
+    S = _lib.TABLE_SLICE if S is None else S
     w = np.ascontiguousarray(slices).view(np.uint64).reshape(-1, S)
     counts = np.asarray(counts).astype(np.int64)
-    bits = np.unpackbits(np.ascontiguousarray(w[:, :4]).view(np.uint8), axis=1, bitorder="little").astype(bool)
+    mw = S // 64  # map words per slice
+    bits = np.unpackbits(np.ascontiguousarray(w[:, :mw]).view(np.uint8), axis=1, bitorder="little").astype(bool)
     if not np.array_equal(bits.sum(axis=1), counts[:len(bits)]):
         raise AssertionError("slice maps disagree with the per-slice counts")
-    deltas = np.ascontiguousarray(w[:, 4:]).view(np.uint32)  # [slices][504]
+    deltas = np.ascontiguousarray(w[:, mw:]).view(np.uint32)  # [slices][2 (S - mw)]
     keep = np.arange(deltas.shape[1])[None, :] < counts[:, None]
     groups = (np.nonzero(bits)[0] * S + np.nonzero(bits)[1]).astype(np.uint64)
     return (deltas[keep].astype(np.uint64) << np.uint64(32)) | groups

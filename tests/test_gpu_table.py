@@ -209,7 +209,7 @@ def test_device_variant_and_view(engine, oracle):
     rd = t.read()
     np.testing.assert_array_equal(rd["last_committed"], ce)
     k = g % 256
-    pos = (k % 128) // 2 * 4 + (k // 128) * 2 + k % 2  # the view's documented lane order
+    pos = k  # the view's documented order: group order within the tile
     u32 = words.view(np.uint32)
     pi = rd["pending_index"]
     base = np.where(pi > 0, (pi - 1) & ~np.int64((1 << 30) - 1), 0)
@@ -447,7 +447,7 @@ def test_lowered_base_without_reset_invents_no_ack(engine):
     t = Table(engine, G, P)
     t.update(st)
     # slot 0 of every group acks B + 5 (word 5); slots 1, 2 stay at word 0
-    t.update(None, _lib.rec(np.arange(G), 0, np.full(G, 5 + 1)))
+    t.update(None, _lib.rec(np.arange(G), 0, np.full(G, 5)))  # match = pi - 1 + 5 = B + 5
     # the non-reset header: pendingIndex lowered below the base (base 0 afterwards)
     st2 = st.copy()
     st2["flags"] = 0

@@ -123,6 +123,58 @@ def main():
         out["cases"].append({"bytes": size, "addr": hex(pa), "copy_ok": ok, "before": before,
                              "after_copy": after_copy, "after_munmap": after_free,
                              "new_mapping_same_address": over_new})
+    # (c) host->device copies from fresh mappings (the other direction), observed the same way
+    out["h2d"] = []
+    for size in (1 << 20, 8 << 20, 48 << 20):
+        pa, a = new_map(size)
+        a[:] = 7
+        d = torch.empty(size, dtype=torch.uint8, device=dev)
+        d.copy_(torch.from_numpy(a))
+        torch.cuda.synchronize()
+        out["h2d"].append({"bytes": size, "copy_ok": bool((d[:4096] == 7).all().item()),
+                           "after_copy": hsa_info(pa), "after_copy_mid": hsa_info(pa + size // 2)})
+        keep.append((pa, a))
+        del d
+    # (d) during a copy: poll the destination's HSA record from another thread while a 48 MiB
+    # device->host copy runs (is the caller's range locked for the copy -- the pinned path --
+    # or staged?)
+    import threading
+    pd, dd = new_map(48 << 20)
+    keep.append((pd, dd))
+    seen, stop = [], [False]
+
+    def poll():
+        while not stop[0]:
+            t = hsa_info(pd + (24 << 20))["type"]
+            if t and t not in seen:
+                seen.append(t)
+    th = threading.Thread(target=poll)
+    th.start()
+    for _ in range(20):
+        torch.from_numpy(dd).copy_(src[:48 << 20])
+    torch.cuda.synchronize()
+    stop[0] = True
+    th.join()
+    out["during_48MiB_d2h_copies_types_seen"] = seen
+    out["after_48MiB_d2h_copies"] = hsa_info(pd)
+    # (e) the faulting call's own form: .cpu() of a device tensor into torch's CPU allocator,
+    # then the HSA record over the result while it is alive
+    t2 = torch.empty(1 << 20, dtype=torch.int16, device=dev).fill_(3)
+    h2 = t2.cpu()
+    out["torch_cpu_2MiB_int16"] = {"ok": bool((h2[:16] == 3).all()), "hsa": hsa_info(h2.data_ptr())}
+    # (f) an explicit registration and unregistration (what libjrq's jrq_host_register does):
+    # the record while registered and after hipHostUnregister
+    hip.hipHostRegister.restype = C.c_int
+    hip.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
+    hip.hipHostUnregister.restype = C.c_int
+    hip.hipHostUnregister.argtypes = [C.c_void_p]
+    pr, ar = new_map(4 << 20)
+    keep.append((pr, ar))
+    rr = hip.hipHostRegister(C.c_void_p(pr), 4 << 20, 0)
+    reg = hsa_info(pr)
+    ru = hip.hipHostUnregister(C.c_void_p(pr))
+    out["host_register_cycle"] = {"register_rc": rr, "registered": reg, "unregister_rc": ru,
+                                  "after_unregister": hsa_info(pr)}
     print(json.dumps(out, indent=1))
     sys.stdout.flush()
     os._exit(0)  # leave the mappings to the kernel; no runtime teardown over the replaced ranges

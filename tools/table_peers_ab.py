@@ -46,11 +46,16 @@ def main():
             recs = np.concatenate([L.rec(gs, p, r.integers(0, 65, G)) for p in range(P)])
             t = Table(e, G, P); t.update(st, recs); prist.append(t); work.append(Table(e, G, P))
         torch.cuda.synchronize()
-        tabs[name] = (prist, work, [w.list_buffers(dev) for w in work])
+        # this build's list slice size (256 before r06, 128 since): from its slice count
+        sl = work[0].slices()
+        S = 256 if sl == (G + 255) // 256 else 128
+        bufs = [(torch.empty(sl * S, dtype=torch.int64, device=dev), torch.zeros(sl, dtype=torch.int32, device=dev))
+                for _ in work]
+        tabs[name] = (prist, work, bufs, S)
     times = {n: [] for n, _ in variants}
     for rep in range(12):
         for name, _ in variants:
-            prist, work, lists = tabs[name]
+            prist, work, lists, _ = tabs[name]
             for w, t in zip(work, prist): w.copy_from(t)
             a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(s)
@@ -59,7 +64,8 @@ def main():
             if rep >= 2: times[name].append(a.elapsed_time(z) / NB * 1e3)
     def lists_of(n):  # (a diagnosis variant may write no list: None)
         try:
-            return [w.gather_dev_list(*l) for w, l in zip(tabs[n][1], tabs[n][2])]
+            from jraft_amd.engine import decode_slices, _host_np
+            return [decode_slices(_host_np(l[0]), _host_np(l[1]), tabs[n][3]) for l in tabs[n][2]]
         except AssertionError:
             return None
     outs = {n: lists_of(n) for n, _ in variants}
