@@ -280,7 +280,7 @@ typedef struct {
     uint64_t run_conf[JRQ_TABLE_MAX_RUNS];  /* JRQ_CONF words */
     int64_t run_start[JRQ_TABLE_MAX_RUNS];  /* run_start[0] is ignored (<= pendingIndex) */
 } jrq_group_state;           /* 96 bytes */
-#define JRQ_STATE_RESET_MATCH 1u
+#define JRQ_STATE_RESET_MATCH 1u  /* (JRQ_STATE_STAMP: see the order-free ack records below) */
 
 /* 8-byte update record: bits 0-4 field, bits 5-31 group, bits 32-63 v, a value relative to
  * the group's pendingIndex pi (after this call's group states are applied):
@@ -328,6 +328,34 @@ int jrq_table_stage_reserve(jrq_table *t, uint32_t max_states, uint32_t max_recs
 int jrq_table_stage(jrq_table *t, const jrq_group_state *states, uint32_t n_states,
                     const uint64_t *recs, uint32_t n_recs);
 int jrq_table_stage_apply(jrq_table *t);
+
+/* Order-free ack records (r06): what BallotBox.commitAt (the `last` of an ack) and
+ * appendPendingTask (the new lastAppended) record at call time, shipped as they were written --
+ * no pack pass over the groups' state at flush time (BallotBox.java:96-139, 197-215).
+ *   JRQ_ACK(group, field, index): bits 0-4 field (0..15 a peer slot, JRQ_REC_LAST_APPENDED),
+ *   bits 5-31 group, bits 32-63 the low 32 bits of the absolute log index.
+ * jrq_table_stage_apply applies them after the staged headers and JRQ_REC records, in any order
+ * (an order-free max): the device reconstructs the absolute index as the one within 2^31 of the
+ * group's pendingIndex - 1 (an ack lies in [pendingIndex - 1, pendingIndex + 2^31 - 1): the
+ * window of an ArrayList-bounded queue) and raises the slot's match, or lastAppended, to it.
+ * Records of a group that is not the leader (pendingIndex 0) are ignored.
+ * Stamps: records are staged in segments, each with a stamp S (a host-wide counter of resets,
+ * read when the segment was started).  A header with JRQ_STATE_STAMP sets the group's reset
+ * stamp R (from its run_start[0], which a header otherwise ignores); a record of that group
+ * from a segment with S < R is dropped -- it was recorded before the reset that header ships
+ * (an ack of an ended leadership, clearPendingTasks :147-156, or of a slot's previous peer).
+ * jrq_table_stage_reserve_acks sizes the staging for max_acks records in max_segments segments
+ * (it may synchronise, and drops acks staged but never applied); jrq_table_stage_acks queues
+ * one segment's H2D copy (asynchronous from page-locked memory, which must then stay unchanged
+ * until the next jrq_table_epoch or jrq_synchronize returns).  Invalid records (group >= G, a
+ * field past the slots, a lastAppended window >= 2^31 - 1) are skipped and counted
+ * (jrq_table_check). */
+#define JRQ_ACK(group, field, index)                                                           \
+    (((uint64_t)(uint32_t)(int64_t)(index) << 32) | ((uint64_t)(uint32_t)(group) << 5) |       \
+     (uint64_t)(field))
+#define JRQ_STATE_STAMP 2u
+int jrq_table_stage_reserve_acks(jrq_table *t, uint32_t max_acks, uint32_t max_segments);
+int jrq_table_stage_acks(jrq_table *t, uint64_t stamp, const uint64_t *acks, uint32_t n);
 
 /* One quorum epoch over every group of the table, state updated in place as BallotBox.commitAt
  * leaves it (BallotBox.java:96-139; commit -> lastCommittedIndex, pendingIndex = commit + 1).

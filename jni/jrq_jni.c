@@ -182,6 +182,21 @@ JNIEXPORT jint FN(tableStageApply)(JNIEnv *env, jclass cls, jlong table) {
     return jrq_jni_table_stage_apply(ENG(table));
 }
 
+/* order-free ack records (JRQ_ACK) recorded by the Java BallotBox at call time, one segment per
+ * reset stamp: what GpuGroupBatch.flush ships without a pack pass */
+JNIEXPORT jint FN(tableStageReserveAcks)(JNIEnv *env, jclass cls, jlong table, jint maxAcks,
+                                         jint maxSegments) {
+    (void)env;
+    (void)cls;
+    return jrq_jni_table_stage_reserve_acks(ENG(table), maxAcks, maxSegments);
+}
+
+JNIEXPORT jint FN(tableStageAcks)(JNIEnv *env, jclass cls, jlong table, jlong stamp, jobject acks,
+                                  jint n) {
+    (void)cls;
+    return jrq_jni_table_stage_acks(ENG(table), stamp, ADDR(acks), n);
+}
+
 /* returns the number of changed groups (>= 0) or a negative jrq_error */
 JNIEXPORT jint FN(tableEpoch)(JNIEnv *env, jclass cls, jlong table, jobject changed,
                               jobject statusOut) {

@@ -162,6 +162,20 @@ int32_t jrq_jni_table_stage_apply(jrq_addr table) {
     return jrq_table_stage_apply(A(jrq_table *, table));
 }
 
+int32_t jrq_jni_table_stage_reserve_acks(jrq_addr table, int32_t max_acks, int32_t max_segments) {
+    N(max_acks);
+    N(max_segments);
+    return jrq_table_stage_reserve_acks(A(jrq_table *, table), (uint32_t)max_acks,
+                                        (uint32_t)max_segments);
+}
+
+int32_t jrq_jni_table_stage_acks(jrq_addr table, int64_t stamp, jrq_addr acks, int32_t n) {
+    N(n);
+    if (stamp < 0) return JRQ_E_INVALID;
+    return jrq_table_stage_acks(A(jrq_table *, table), (uint64_t)stamp, A(const uint64_t *, acks),
+                                (uint32_t)n);
+}
+
 int32_t jrq_jni_table_epoch(jrq_addr table, jrq_addr changed, jrq_addr status_out) {
     uint32_t n = 0;
     int rc = jrq_table_epoch(A(jrq_table *, table), A(uint64_t *, changed), &n,

@@ -65,6 +65,8 @@ int32_t jrq_jni_table_stage_reserve(jrq_addr table, int32_t max_states, int32_t 
 int32_t jrq_jni_table_stage(jrq_addr table, jrq_addr states, int32_t n_states, jrq_addr recs,
                             int32_t n_recs);
 int32_t jrq_jni_table_stage_apply(jrq_addr table);
+int32_t jrq_jni_table_stage_reserve_acks(jrq_addr table, int32_t max_acks, int32_t max_segments);
+int32_t jrq_jni_table_stage_acks(jrq_addr table, int64_t stamp, jrq_addr acks, int32_t n);
 /* returns the number of changed groups written to `changed` (>= 0), or a jrq_error */
 int32_t jrq_jni_table_epoch(jrq_addr table, jrq_addr changed, jrq_addr status_out);
 int32_t jrq_jni_table_read(jrq_addr table, jrq_addr pending_index, jrq_addr last_appended,

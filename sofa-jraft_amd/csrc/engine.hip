@@ -39,6 +39,9 @@ extern "C" hipError_t jrq_launch_table_update(const JrqTableArgs* a, const JrqGr
                                               uint32_t n_states, const uint64_t* recs,
                                               uint32_t n_recs, hipStream_t stream);
 extern "C" hipError_t jrq_launch_table_epoch(const JrqTableArgs* a, hipStream_t stream);
+extern "C" hipError_t jrq_launch_table_acks(const JrqTableArgs* a, const uint64_t* acks, uint32_t n,
+                                            const uint32_t* seg_off, const uint64_t* seg_stamp,
+                                            uint32_t nseg, hipStream_t stream);
 extern "C" hipError_t jrq_launch_table_list_gather(const uint64_t* changed, const uint32_t* n,
                                                    uint32_t slices, uint32_t* off, uint32_t* total,
                                                    uint64_t* out, hipStream_t stream);
@@ -1665,6 +1668,11 @@ struct jrq_table {
   uint32_t slices = 0;        // JRQ_TABLE_SLICE-group slices of the changed list
   uint64_t stage_cap_s = 0, stage_cap_r = 0;  // jrq_table_stage: reserved capacity
   uint64_t staged_s = 0, staged_r = 0;        // headers / records staged since the last apply
+  DevBuf ack_stage, seg_stage;                // order-free ack records (jrq_table_stage_acks)
+  uint64_t stage_cap_a = 0, staged_a = 0;
+  uint32_t stage_cap_seg = 0;
+  std::vector<uint32_t> seg_off;              // staged segments: first record, stamp
+  std::vector<uint64_t> seg_stamp;
   size_t state_bytes = 0;     // the rows at the start of mem (jrq_table_copy)
 };
 
@@ -1718,7 +1726,7 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   const uint64_t tiles = (waves + 1) / 2;
   const uint64_t flag_words = waves * jrq::kFlagSlots * 8 + (waves + 1) / 2;
   const uint64_t ts = static_cast<uint64_t>(P) * (jrq::kTableSlice / 2) + 4 * jrq::kTableSlice;  // words per tile
-  const uint64_t words = tiles * ts + ld * 2 * (jrq::kTableMaxRuns - 1) + flag_words;
+  const uint64_t words = tiles * ts + ld * 2 * (jrq::kTableMaxRuns - 1) + flag_words + ld;  // + rstamp[ld]
   const size_t bytes = words * 8 + 64;
   t->slices = (G + JRQ_TABLE_SLICE - 1) / JRQ_TABLE_SLICE;
   if (hipMalloc(&t->mem, bytes) != hipSuccess || hipMemset(t->mem, 0, bytes) != hipSuccess ||
@@ -1741,6 +1749,7 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   a.xconf = reinterpret_cast<uint64_t*>(a.xstart + ld * (jrq::kTableMaxRuns - 1));
   a.flag_ent = reinterpret_cast<uint64_t*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
   a.flag_wcnt = reinterpret_cast<uint32_t*>(a.flag_ent + waves * jrq::kFlagSlots * 8);
+  a.rstamp = reinterpret_cast<uint64_t*>(a.flag_ent + waves * jrq::kFlagSlots * 8 + (waves + 1) / 2);
   a.invalid = reinterpret_cast<uint32_t*>(w + words);
   t->state_bytes = words * 8;
   a.ld = ld;
@@ -1755,7 +1764,7 @@ void jrq_table_destroy(jrq_table* t) {
   if (t->e) {
     DeviceGuard guard(t->e->device);
     (void)hipStreamSynchronize(t->e->stream);
-    for (DevBuf* b : {&t->st_stage, &t->rec_stage, &t->changed_stage})
+    for (DevBuf* b : {&t->st_stage, &t->rec_stage, &t->changed_stage, &t->ack_stage, &t->seg_stage})
       if (b->p) (void)hipFree(b->p);
     if (t->mem) (void)hipFree(t->mem);
     if (t->n_dev) (void)hipFree(t->n_dev);
@@ -1866,11 +1875,64 @@ int jrq_table_stage(jrq_table* t, const jrq_group_state* states, uint32_t n_stat
 
 int jrq_table_stage_apply(jrq_table* t) {
   if (table_check(t)) return JRQ_E_INVALID;
-  const uint64_t ns = t->staged_s, nr = t->staged_r;
-  t->staged_s = t->staged_r = 0;
-  if (!ns && !nr) return JRQ_OK;
-  return jrq_table_update_dev(t, static_cast<const jrq_group_state*>(t->st_stage.p), static_cast<uint32_t>(ns),
-                              static_cast<const uint64_t*>(t->rec_stage.p), static_cast<uint32_t>(nr));
+  const uint64_t ns = t->staged_s, nr = t->staged_r, na = t->staged_a;
+  t->staged_s = t->staged_r = t->staged_a = 0;
+  int rc;
+  if ((ns || nr) &&
+      (rc = jrq_table_update_dev(t, static_cast<const jrq_group_state*>(t->st_stage.p), static_cast<uint32_t>(ns),
+                                 static_cast<const uint64_t*>(t->rec_stage.p), static_cast<uint32_t>(nr))))
+    return rc;
+  if (na) {  // the ack segments' starts and stamps, then one launch over every record
+    jrq_engine* e = t->e;
+    DeviceGuard guard(e->device);
+    const uint32_t nseg = static_cast<uint32_t>(t->seg_off.size());
+    uint64_t* ds = static_cast<uint64_t*>(t->seg_stage.p);
+    uint32_t* doff = reinterpret_cast<uint32_t*>(ds + t->stage_cap_seg);
+    if ((rc = upload_any(e, ds, t->seg_stamp.data(), nseg * 8))) return rc;
+    if ((rc = upload_any(e, doff, t->seg_off.data(), nseg * 4))) return rc;
+    JRQ_HIP(e, jrq_launch_table_acks(&t->a, static_cast<const uint64_t*>(t->ack_stage.p), static_cast<uint32_t>(na),
+                                     doff, ds, nseg, e->stream));
+  }
+  t->seg_off.clear();
+  t->seg_stamp.clear();
+  return JRQ_OK;
+}
+
+int jrq_table_stage_reserve_acks(jrq_table* t, uint32_t max_acks, uint32_t max_segments) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  t->staged_a = 0;  // acks staged and never applied (a failed flush) are dropped
+  t->seg_off.clear();
+  t->seg_stamp.clear();
+  if (max_segments == 0) max_segments = 1;
+  DeviceGuard guard(e->device);
+  int rc;
+  void* p = nullptr;
+  if ((rc = stage_buf(e, t->ack_stage, static_cast<size_t>(max_acks) * 8, &p))) return rc;
+  if ((rc = stage_buf(e, t->seg_stage, static_cast<size_t>(max_segments) * 12, &p))) return rc;
+  t->stage_cap_a = t->ack_stage.cap / 8;
+  t->stage_cap_seg = static_cast<uint32_t>(t->seg_stage.cap / 12);
+  return JRQ_OK;
+}
+
+int jrq_table_stage_acks(jrq_table* t, uint64_t stamp, const uint64_t* acks, uint32_t n) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if (n && !acks) return fail(e, JRQ_E_INVALID, "null ack array");
+  if (n == 0) return JRQ_OK;
+  const bool merge = !t->seg_stamp.empty() && t->seg_stamp.back() == stamp;
+  if (t->staged_a + n > t->stage_cap_a || (!merge && t->seg_off.size() + 1 > t->stage_cap_seg))
+    return fail(e, JRQ_E_STATE, "table: ack staging beyond jrq_table_stage_reserve_acks");
+  DeviceGuard guard(e->device);
+  int rc;
+  if ((rc = upload_any(e, static_cast<uint64_t*>(t->ack_stage.p) + t->staged_a, acks, static_cast<size_t>(n) * 8)))
+    return rc;
+  if (!merge) {
+    t->seg_off.push_back(static_cast<uint32_t>(t->staged_a));
+    t->seg_stamp.push_back(stamp);
+  }
+  t->staged_a += n;
+  return JRQ_OK;
 }
 
 int jrq_table_epoch_dev(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, uint8_t* status_out) {

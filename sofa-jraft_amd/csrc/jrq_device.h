@@ -308,6 +308,8 @@ struct JrqTableArgs {
   uint64_t* flag_ent;    // [waves][kFlagSlots][8] per 128-group epoch wave: its groups flagged
                          // JRQ_CONF_RUNS as 64-B entries {group, run starts 1-3, conf words 0-3}
   uint32_t* flag_wcnt;   // [waves] how many
+  uint64_t* rstamp;      // [ld] reset stamp of each group (JRQ_STATE_STAMP headers): order-free
+                         // ack records from segments stamped earlier are dropped
 };
 
 // Element g of a tiled int64 field (its row in tile 0: t.pi, t.la, t.lc, t.conf).

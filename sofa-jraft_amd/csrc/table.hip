@@ -533,6 +533,7 @@ __global__ __launch_bounds__(256) void table_states_kernel(JrqTableArgs t, const
     t.xstart[o] = static_cast<uint32_t>(k) < nr ? st.run_start[k] : kI64Max;
     t.xconf[o] = static_cast<uint32_t>(k) < nr ? (st.run_conf[k] & ~kConfRuns) : 0ull;
   }
+  if (st.flags & 2u) t.rstamp[g] = static_cast<uint64_t>(st.run_start[0]);  // JRQ_STATE_STAMP
   if (st.flags & 1u) {  // JRQ_STATE_RESET_MATCH: a new leader's replicators start over
     const uint32_t w = pi > 0 ? static_cast<uint32_t>(pi - 1 - b1) : 0u;
     for (uint32_t p = 0; p < t.P; ++p) tm(t, p, g) = w;
@@ -588,7 +589,60 @@ __global__ __launch_bounds__(256) void table_recs_kernel(JrqTableArgs t, const u
   }
 }
 
+// Order-free ack records (include/jrq.h JRQ_ACK): one lane per record.  The record's segment
+// (a binary search over the few segment starts) gives its stamp; a record stamped before its
+// group's last reset is dropped.  The absolute index is the one within 2^31 of pendingIndex - 1
+// whose low 32 bits the record carries; a match raises its slot's u32 word (against the group's
+// match base, saturating: below the base it changes nothing), a lastAppended the group's queue
+// end -- both as atomic maxima, so records apply in any order.
+__global__ __launch_bounds__(256) void table_acks_kernel(JrqTableArgs t, const uint64_t* __restrict__ acks,
+                                                         uint32_t n, const uint32_t* __restrict__ seg_off,
+                                                         const uint64_t* __restrict__ seg_stamp, uint32_t nseg) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t r = acks[i];
+  const uint32_t f = static_cast<uint32_t>(r & 31u);
+  const uint32_t g = static_cast<uint32_t>(r >> 5) & ((1u << 27) - 1u);
+  const uint32_t low = static_cast<uint32_t>(r >> 32);
+  if (g >= t.G || f > 16u || (f < 16u && f >= t.P)) {
+    atomicAdd(t.invalid, 1u);
+    return;
+  }
+  uint32_t lo = 0, hi = nseg;  // the last segment starting at or before i
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (seg_off[mid] <= i) lo = mid;
+    else hi = mid;
+  }
+  if (seg_stamp[lo] < t.rstamp[g]) return;  // recorded before the group's last reset
+  const int64_t pr = tf(t.pi, t, g), lc = tf(t.lc, t, g);
+  const int64_t pi = pr == kPiFollowsLc ? lc + 1 : pr;
+  if (pi <= 0) return;  // not the leader: commitAt refuses (BallotBox.java:101-103)
+  const int64_t a = (pi - 1) + static_cast<int64_t>(static_cast<int32_t>(low - static_cast<uint32_t>(pi - 1)));
+  if (f == 16u) {
+    // a queue longer than an ArrayList, or entries pending without a conf run: refused, counted
+    if (a - pi >= int64_t{0x7FFFFFFF} || (tf(t.conf, t, g) == 0 && a >= pi)) {
+      atomicAdd(t.invalid, 1u);
+      return;
+    }
+    atomicMax(reinterpret_cast<long long*>(&tf(t.la, t, g)), static_cast<long long>(a));
+  } else {
+    const int64_t rel = a - mbase(pi);
+    if (rel <= 0) return;
+    atomicMax(&tm(t, f, g), rel > 0xFFFFFFFFll ? 0xFFFFFFFFu : static_cast<uint32_t>(rel));
+  }
+}
+
 }  // namespace jrq
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_acks(
+    const JrqTableArgs* a, const uint64_t* acks, uint32_t n, const uint32_t* seg_off,
+    const uint64_t* seg_stamp, uint32_t nseg, hipStream_t stream) {
+  if (n)
+    hipLaunchKernelGGL(jrq::table_acks_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, *a, acks, n,
+                       seg_off, seg_stamp, nseg);
+  return hipGetLastError();
+}
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_update(
     const JrqTableArgs* a, const JrqGroupState* states, uint32_t n_states, const uint64_t* recs,

@@ -141,8 +141,9 @@ extern "C" {
 
 const char* jraft_drive_last_error(void) { return g_err.c_str(); }
 
-// stats_out[k * 11 + i]: 0 api_ms, 1 pack_ms, 2 device_ms, 3 deliver_ms, 4 flush_ms,
-// 5 h2d_bytes, 6 d2h_bytes, 7 states, 8 records, 9 changed, 10 api_calls
+// stats_out[k * 12 + i]: 0 api_ms, 1 pack_ms, 2 device_ms, 3 deliver_ms, 4 flush_ms,
+// 5 h2d_bytes, 6 d2h_bytes, 7 states, 8 records (pack + call-time), 9 changed, 10 api_calls,
+// 11 acks (the call-time order-free records among them)
 int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t threads,
                        const int64_t* pi0, const int64_t* lc0, const uint64_t* conf_a,
                        const uint64_t* conf_b, const int64_t* switch_at, const int64_t* la,
@@ -230,7 +231,7 @@ int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t 
       for (uint32_t g = 0; g < G; ++g)
         committed_out[static_cast<size_t>(k) * G + g] = boxes[g].getLastCommittedIndex();
       const jraft::FlushStats& s = batch->lastFlush();
-      double* o = stats_out + static_cast<size_t>(k) * 11;
+      double* o = stats_out + static_cast<size_t>(k) * 12;
       o[0] = ms(t1 - t0);
       o[1] = s.pack_ms;
       o[2] = s.device_ms;
@@ -239,7 +240,8 @@ int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t 
       o[5] = static_cast<double>(s.h2d_bytes);
       o[6] = static_cast<double>(s.d2h_bytes);
       o[7] = s.states;
-      o[8] = s.records;
+      o[8] = static_cast<double>(s.records) + s.acks;
+      o[11] = s.acks;
       o[9] = s.changed;
       uint64_t nc = 0;
       for (uint64_t c : calls) nc += c;

@@ -348,6 +348,12 @@ struct alignas(128) GroupBatch::DirtyList {
   std::vector<uint32_t> v[2];
   std::atomic<size_t> n[2] = {};          // v[i].size(), for the flusher's policy
   std::atomic<int64_t> firstNs[2] = {};   // when v[i] got its first group
+  // the order-free records (JRQ_ACK) the thread wrote in generation t, in ack[t & 1]: page-locked
+  // (jrq_host_alloc, sized by the flushing thread between uses), DMA-ed as they are; nack[i]
+  // records, in segments (first record, reset stamp) of seg[i]
+  PinnedBuf<uint64_t> ack[2];
+  uint32_t nack[2] = {};
+  std::vector<std::pair<uint32_t, uint64_t>> seg[2];
 };
 
 namespace {
@@ -563,6 +569,7 @@ GroupBatch::GroupBatch(Engine* eng, uint32_t groups, uint32_t peers)
   }
   runs_.assign(static_cast<size_t>(G_) * JRQ_TABLE_MAX_RUNS, Run{0, 0});
   packedIn_.reset(new uint64_t[G_]());
+  rstamp_.reset(new uint64_t[G_]());
   waiter_.resize(G_);
   closures_.resize(G_);
 }
@@ -652,9 +659,31 @@ int GroupBatch::ackFast(uint32_t g, int64_t first, int64_t last, uint32_t peer) 
     ast(*mp, last);
     // after the match (the pack reads the stamp, then the match)
     ast(slotUseOf(g)[s], stampOf(t, true));
-    listIn(l, h, g, t);
+    // the ack itself goes up as an order-free record; the group is listed for the pack only
+    // when this thread's record buffer is full
+    if (!appendAck(l, t, JRQ_ACK(g, s, last))) listIn(l, h, g, t);
   }
   return 1;
+}
+
+bool GroupBatch::appendAck(DirtyList* l, uint32_t t, uint64_t rec) {
+  const uint32_t i = t & 1u;
+  const uint32_t n = l->nack[i];
+  // (acquire: the flushing thread publishes a first buffer of the generation in use, below)
+  if (n >= __atomic_load_n(&l->ack[i].cap, __ATOMIC_ACQUIRE)) return false;
+  // the counter of resets so far (a reset of this group happened-before this call saw its gate
+  // open, so the record is stamped at or after it)
+  const uint64_t R = resetSeq_.load(std::memory_order_acquire);
+  auto& sg = l->seg[i];
+  if (sg.empty() || sg.back().second != R) sg.emplace_back(n, R);
+  l->ack[i].p[n] = rec;
+  l->nack[i] = n + 1;
+  return true;
+}
+
+void GroupBatch::stampReset(uint32_t g) {
+  rstamp_[g] = resetSeq_.fetch_add(1, std::memory_order_acq_rel) + 1;
+  markDirty(g, kDirtyHeader);
 }
 
 // In a call region: g on this thread's list of generation t, unless it is on one already.
@@ -718,6 +747,10 @@ int GroupBatch::slotOf(uint32_t g, uint32_t peer, bool create, uint32_t reserved
         victim = static_cast<int>(s);
     if (victim < 0) return -1;
     quiesce(g);  // the slot's peer may be acking on the fast path
+    // its records (and every other record of the group written so far) are dropped by the
+    // reset stamp; the live slots' current matches go up again as pack records
+    stampReset(g);
+    markDirty(g, (1u << P_) - 1u);
   }
   // The slot's stamp and match first, its peer last (a release store the fast path's acquire
   // load of the slot ids pairs with): an ack of `peer` that finds the slot on the fast path --
@@ -833,6 +866,10 @@ void GroupBatch::packRange(Part& part, const uint32_t* groups, size_t n) {
         st.run_conf[r] = R[r].conf;
         st.run_start[r] = R[r].start;
       }
+      // the group's reset stamp rides in run_start[0] (which a header otherwise ignores):
+      // order-free records written before its last reset are dropped
+      st.flags |= JRQ_STATE_STAMP;
+      st.run_start[0] = static_cast<int64_t>(rstamp_[g]);
     } else if ((d & kDirtyLa) && pi != 0) {
       part.rec.p[ri++] = JRQ_REC(g, JRQ_REC_LAST_APPENDED, h.la - base);
     }
@@ -911,6 +948,7 @@ uint32_t GroupBatch::flushLocked() {
   packGen_ = t;
   waitRegions();
   size_t nl;
+  std::vector<DirtyList*> taken;  // the lists whose generation-t records this flush ships
   {
     std::lock_guard<std::mutex> g(listsMu_);
     nl = lists_.size();
@@ -920,8 +958,40 @@ uint32_t GroupBatch::flushLocked() {
       work_[i].clear();
       std::swap(l.v[t & 1u], work_[i]);
       l.n[t & 1u].store(0, std::memory_order_relaxed);
+      taken.push_back(&l);
     }
   }
+  const uint32_t ti = t & 1u;
+  size_t nacks = 0, nsegs = 0;
+  for (DirtyList* l : taken) {
+    nacks += l->nack[ti];
+    nsegs += l->seg[ti].size();
+  }
+  // the record buffers of generation t are consumed once the epoch has synchronised: emptied
+  // and sized for their next use (generation t + 2) from what this one held -- on this thread,
+  // as every page-locked allocation of the batch is
+  auto recycleAcks = [&] {
+    for (size_t i = 0; i < taken.size(); ++i) {
+      DirtyList* l = taken[i];
+      // what the thread wrote this generation: its records, or -- while it had no buffer --
+      // the groups it listed, each a queue size and P acks at most
+      const size_t used = std::max<size_t>(l->nack[ti], work_[i].size() * (P_ + 1));
+      l->nack[ti] = 0;
+      l->seg[ti].clear();
+      l->ack[ti].reserve(std::max<size_t>(used + used / 2, 1u << 14));
+      // a thread's first buffer of the generation now in use (t + 1): nothing writes a buffer
+      // of capacity 0, so it can be published now -- pointer first, capacity last (release)
+      PinnedBuf<uint64_t>& nx = l->ack[ti ^ 1u];
+      if (__atomic_load_n(&nx.cap, __ATOMIC_RELAXED) == 0) {
+        const size_t want = l->ack[ti].cap;
+        void* q = nullptr;
+        if (jrq_host_alloc(want * sizeof(uint64_t), &q) == JRQ_OK && q) {
+          nx.p = static_cast<uint64_t*>(q);
+          __atomic_store_n(&nx.cap, want, __ATOMIC_RELEASE);
+        }
+      }
+    }
+  };
   std::vector<size_t> pre(nl + 1, 0);
   for (size_t i = 0; i < nl; ++i) pre[i + 1] = pre[i] + work_[i].size();
   const size_t nd = pre[nl];
@@ -952,6 +1022,18 @@ uint32_t GroupBatch::flushLocked() {
     throwIfError(jrq_table_stage_reserve(table_, static_cast<uint32_t>(nd + 1),
                                          static_cast<uint32_t>(nd * (P_ + 1) + 1)),
                  eng_->raw(), "jrq_table_stage_reserve");
+    // the order-free records first: their DMA (page-locked, as written) overlaps the pack
+    throwIfError(jrq_table_stage_reserve_acks(table_, static_cast<uint32_t>(nacks), static_cast<uint32_t>(nsegs + 1)),
+                 eng_->raw(), "jrq_table_stage_reserve_acks");
+    for (DirtyList* l : taken) {
+      const auto& sg = l->seg[ti];
+      for (size_t k = 0; k < sg.size(); ++k) {
+        const uint32_t b = sg[k].first, e = k + 1 < sg.size() ? sg[k + 1].first : l->nack[ti];
+        throwIfError(jrq_table_stage_acks(table_, sg[k].second, l->ack[ti].p + b, e - b), eng_->raw(),
+                     "jrq_table_stage_acks");
+      }
+    }
+    stats.acks = static_cast<uint32_t>(nacks);
     auto packPart = [&](size_t k) {
       Part& P = parts_[k];
       const size_t b0 = nd * k / K, e0 = nd * (k + 1) / K;
@@ -1016,7 +1098,19 @@ uint32_t GroupBatch::flushLocked() {
     throwIfError(jrq_table_stage_apply(table_), eng_->raw(), "jrq_table_stage_apply");
     t1 = clk::now();
     throwIfError(jrq_table_epoch(table_, changed_.p, &n, nullptr), eng_->raw(), "jrq_table_epoch");
+    recycleAcks();
   } catch (...) {
+    // the groups of the generation's records go back on a list in full, like the listed ones
+    // (whatever part of this update reached the device, the next one re-syncs them)
+    (void)jrq_synchronize(eng_->raw());  // (no DMA may still read the buffers)
+    const uint32_t all = kDirtyHeader | kDirtyLa | ((1u << P_) - 1u);
+    for (DirtyList* l : taken)
+      for (uint32_t k = 0; k < l->nack[ti]; ++k) {
+        const uint32_t g = static_cast<uint32_t>(l->ack[ti].p[k] >> 5) & ((1u << 27) - 1u);
+        Guard lk(*this, g);
+        markDirty(g, all);
+      }
+    recycleAcks();
     relistAfterFailure();
     throw;
   }
@@ -1092,7 +1186,7 @@ uint32_t GroupBatch::flushLocked() {
   auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
   stats.changed = n;
   stats.h2d_bytes = static_cast<uint64_t>(stats.states) * sizeof(jrq_group_state) +
-                    static_cast<uint64_t>(stats.records) * 8;
+                    static_cast<uint64_t>(stats.records) * 8 + static_cast<uint64_t>(stats.acks) * 8;
   stats.d2h_bytes = 4 + static_cast<uint64_t>(n) * 8;
   stats.pack_ms = ms(t1 - t0);
   stats.device_ms = ms(t2 - t1);
@@ -1219,7 +1313,10 @@ void BallotBox::clearPendingTasks() {
     GroupBatch::Hot& h = b.hot(g_);
     // an ack of this leadership may still be on the fast path: it completes before pendingIndex
     // drops to 0, and none starts after (resetPendingIndex relies on it)
-    if (h.pi != 0) b.quiesce(g_);
+    if (h.pi != 0) {
+      b.quiesce(g_);
+      b.stampReset(g_);  // this leadership's records not yet applied are dropped
+    }
     q = std::move(b.closures_[g_]);
     h.nruns = 0;
     h.lastConf = 0;
@@ -1312,7 +1409,15 @@ bool BallotBox::append(const Configuration& conf, const Configuration* oldConf, 
     b.markDirty(g_, GroupBatch::kDirtyHeader);
   }
   ast(h.la, idx + count - 1);
-  b.markDirty(g_, GroupBatch::kDirtyLa);
+  {  // the new queue end as an order-free record (else the pack ships it)
+    GroupBatch::DirtyList* l = b.myDirtyList();
+    Region rg(l->seq);
+    const uint32_t t = b.gen_.load(std::memory_order_acquire);
+    if (!b.appendAck(l, t, JRQ_ACK(g_, JRQ_REC_LAST_APPENDED, h.la))) {
+      h.dirty |= GroupBatch::kDirtyLa;
+      b.listIn(l, h, g_, t);
+    }
+  }
   if (done) {  // ClosureQueue.appendPendingClosure (ClosureQueueImpl.java:98-105)
     auto& q = b.closures_[g_];
     if (!q) q.reset(new std::deque<std::pair<int64_t, std::function<void(bool)>>>());

@@ -361,6 +361,7 @@ class BallotBox {
 struct FlushStats {
   uint32_t states = 0;       // group headers uploaded (96 B each)
   uint32_t records = 0;      // 8-B update records uploaded (changed acks / queue sizes)
+  uint32_t acks = 0;         // 8-B order-free records written at call time (JRQ_ACK)
   uint32_t changed = 0;      // groups whose commit advanced (8-B entries downloaded)
   uint64_t h2d_bytes = 0, d2h_bytes = 0;
   double pack_ms = 0, device_ms = 0, deliver_ms = 0;
@@ -518,6 +519,14 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   void dropDeadRuns(uint32_t g);
   // commitAt's lock-free common case: 0 / 1 = its result, -1 = take the locked path
   int ackFast(uint32_t g, int64_t first, int64_t last, uint32_t peer);
+  // In a call region of generation t: the order-free record `rec` (JRQ_ACK) on this thread's
+  // buffer of t, in the segment of the current reset stamp; false when the buffer is full (the
+  // caller then lists the group for the pack, as before)
+  bool appendAck(DirtyList* l, uint32_t t, uint64_t rec);
+  // Under the group's lock, after quiesce(g): records of g written so far are stale (an ended
+  // leadership, a slot given to another peer): the group's next header carries a new reset
+  // stamp, which drops them on the device
+  void stampReset(uint32_t g);
   void listIn(DirtyList* l, Hot& h, uint32_t g, uint32_t t);
   // under the group's lock, before moving a slot to another peer or resetting matches: no
   // fast-path ack of the group is in flight or starts until the lock is released
@@ -554,6 +563,10 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   uint32_t packGen_ = 0;                  // the generation the running flush packs
   uint64_t packSerial_ = 0;               // flushes started (never wraps)
   std::unique_ptr<uint64_t[]> packedIn_;  // [G] the flush that last packed the group
+  // Resets (stampReset) so far; a record is written in a segment stamped with this counter, and
+  // a group's headers carry the counter of its last reset (JRQ_STATE_STAMP)
+  std::atomic<uint64_t> resetSeq_{0};
+  std::unique_ptr<uint64_t[]> rstamp_;    // [G] the group's last reset (under its lock)
   jrq_table* table_ = nullptr;
   PinnedBuf<uint64_t> changed_;
   std::atomic<uint64_t> flushes_{0};

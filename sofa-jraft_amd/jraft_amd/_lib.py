@@ -58,6 +58,7 @@ PI_FOLLOWS_LC = -(1 << 63)             # JRQ_PI_FOLLOWS_LC
 REC_LAST_APPENDED = 16                 # JRQ_REC_LAST_APPENDED
 TABLE_SLICE = 128                      # JRQ_TABLE_SLICE
 STATE_RESET_MATCH = 1                  # JRQ_STATE_RESET_MATCH
+STATE_STAMP = 2                        # JRQ_STATE_STAMP
 READINDEX_PENDING, READINDEX_SUCCESS, READINDEX_FAILURE, READINDEX_INVALID = 0, 1, 2, 3  # JRQ_READINDEX_*
 # jrq_debug_option (test / A-B hooks)
 DBG_CRC_SEG_BYTES, DBG_CRC_REGS, DBG_CRC_PRIO, DBG_CRC_SEG_MAP, DBG_UPLOAD_PAGEABLE = 1, 2, 3, 4, 5
@@ -80,6 +81,15 @@ class TableView(C.Structure):
                 ("last_appended", C.c_void_p), ("last_committed", C.c_void_p),
                 ("conf", C.c_void_p), ("ld", C.c_uint64), ("G", C.c_uint32),
                 ("num_peers", C.c_uint32), ("tile_groups", C.c_uint32), ("tile_stride", C.c_uint64)]
+
+
+def ack(group, field, index):
+    """JRQ_ACK(group, field, index) -- vectorised: the low 32 bits of the absolute index."""
+    import numpy as np
+    g = np.asarray(group, dtype=np.uint64)
+    f = np.asarray(field, dtype=np.uint64)
+    lo = np.asarray(index, dtype=np.int64).astype(np.uint64) & np.uint64(0xFFFFFFFF)
+    return (lo << np.uint64(32)) | (g << np.uint64(5)) | f
 
 
 def rec(group, field, v):
@@ -156,6 +166,8 @@ SIGNATURES = [
     ("jrq_table_epoch_dev", C.c_int, [_V, _V, _V, _V]),
     ("jrq_table_epoch", C.c_int, [_V, _V, _V, _V]),
     ("jrq_table_slices", C.c_uint32, [_V]),
+    ("jrq_table_stage_reserve_acks", C.c_int, [_V, C.c_uint32, C.c_uint32]),
+    ("jrq_table_stage_acks", C.c_int, [_V, C.c_uint64, _V, C.c_uint32]),
     ("jrq_table_read", C.c_int, [_V, _V, _V, _V, _V]),
     ("jrq_table_check", C.c_int, [_V]),
     ("jrq_table_copy", C.c_int, [_V, _V]),

@@ -14,8 +14,10 @@ from . import _lib
 # runs only -- the product path never sets it)
 DRIVE_PATH = os.environ.get("JRAFT_AMD_AB_DRIVE") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libjraft_drive.so")
+# records: every 8-B update record uploaded (pack records + acks); acks: those written at call
+# time as order-free JRQ_ACK records (include/jrq.h), without a pack pass
 STATS = ("api_ms", "pack_ms", "device_ms", "deliver_ms", "flush_ms", "h2d_bytes", "d2h_bytes",
-         "states", "records", "changed", "api_calls")
+         "states", "records", "changed", "api_calls", "acks")
 _drv = None
 
 

@@ -599,6 +599,30 @@ class Table:
         check(self._L.jrq_table_update_dev(self._h, _dev_ptr(states), ns, _dev_ptr(recs), nr),
               self._eng.handle)
 
+    def stage_reserve(self, max_states: int, max_recs: int, max_acks: int = 0, max_segments: int = 1):
+        """jrq_table_stage_reserve (+ jrq_table_stage_reserve_acks): staging for the streamed
+        update (headers, JRQ_REC records, order-free JRQ_ACK segments)."""
+        check(self._L.jrq_table_stage_reserve(self._h, max_states, max_recs), self._eng.handle)
+        check(self._L.jrq_table_stage_reserve_acks(self._h, max_acks, max_segments), self._eng.handle)
+        self._staged = []
+
+    def stage(self, states=None, recs=None):
+        st = None if states is None else np.ascontiguousarray(states, dtype=GROUP_STATE)
+        rc = None if recs is None else np.ascontiguousarray(recs, dtype=np.uint64)
+        check(self._L.jrq_table_stage(self._h, _np_ptr(st), 0 if st is None else len(st),
+                                      _np_ptr(rc), 0 if rc is None else len(rc)), self._eng.handle)
+        self._staged.append((st, rc))
+
+    def stage_acks(self, stamp: int, acks):
+        """One segment of order-free JRQ_ACK records recorded under reset stamp `stamp`."""
+        a = np.ascontiguousarray(acks, dtype=np.uint64)
+        check(self._L.jrq_table_stage_acks(self._h, stamp, _np_ptr(a), len(a)), self._eng.handle)
+        self._staged.append(a)
+
+    def stage_apply(self):
+        check(self._L.jrq_table_stage_apply(self._h), self._eng.handle)
+        self._keep = self._staged
+
     def epoch(self, status: bool = False):
         """Host variant: returns (changed uint64[n] as JRQ words, status uint8[G] or None)."""
         out = np.zeros(max(self.G, 1), np.uint64)

@@ -41,6 +41,9 @@ struct jrq_table {
   std::mutex mu;  // the real table orders calls on the engine stream
   std::vector<jrq_group_state> staged_s;  // jrq_table_stage: copied at once (the real one DMAs)
   std::vector<uint64_t> staged_r;
+  std::vector<uint64_t> rstamp;           // JRQ_STATE_STAMP per group
+  std::vector<uint64_t> staged_a;         // jrq_table_stage_acks: records, segments
+  std::vector<std::pair<size_t, uint64_t>> segs;
 };
 
 extern "C" {
@@ -51,6 +54,7 @@ jrq_engine* jrq_create(int, uint32_t, uint8_t, int* err) {
 }
 void jrq_destroy(jrq_engine* e) { delete e; }
 const char* jrq_last_error(const jrq_engine* e) { return e ? e->err.c_str() : g_err.c_str(); }
+int jrq_synchronize(jrq_engine* e) { return e ? JRQ_OK : JRQ_E_INVALID; }  // (calls complete at once)
 int jrq_host_register(void* p, size_t n) { return p && n ? JRQ_OK : JRQ_E_INVALID; }
 int jrq_host_unregister(void* p) { return p ? JRQ_OK : JRQ_E_INVALID; }
 int jrq_host_alloc(size_t n, void** out) {
@@ -103,6 +107,7 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   t->nr.assign(G, 0);
   t->start.assign(static_cast<size_t>(G) * JRQ_TABLE_MAX_RUNS, 0);
   t->conf.assign(static_cast<size_t>(G) * JRQ_TABLE_MAX_RUNS, 0);
+  t->rstamp.assign(G, 0);
   if (err) *err = JRQ_OK;
   return t;
 }
@@ -144,6 +149,10 @@ int jrq_table_update_gather(jrq_table* t, uint32_t parts, const jrq_group_state*
       for (uint32_t r = 0; r < JRQ_TABLE_MAX_RUNS; ++r) {
         t->start[g * JRQ_TABLE_MAX_RUNS + r] = s.run_start[r];
         t->conf[g * JRQ_TABLE_MAX_RUNS + r] = s.run_conf[r] & ~JRQ_CONF_RUNS;
+      }
+      if (s.flags & JRQ_STATE_STAMP) {  // run_start[0] carries the reset stamp (run 0 has none)
+        t->rstamp[g] = static_cast<uint64_t>(s.run_start[0]);
+        t->start[g * JRQ_TABLE_MAX_RUNS] = 0;
       }
       if (s.flags & JRQ_STATE_RESET_MATCH)
         for (uint32_t p = 0; p < t->P; ++p) t->match[static_cast<size_t>(g) * t->P + p] = pi - 1;
@@ -192,18 +201,65 @@ int jrq_table_stage(jrq_table* t, const jrq_group_state* states, uint32_t n_stat
   return JRQ_OK;
 }
 
+int jrq_table_stage_reserve_acks(jrq_table* t, uint32_t, uint32_t) {
+  std::lock_guard<std::mutex> l(t->mu);
+  t->staged_a.clear();
+  t->segs.clear();
+  return JRQ_OK;
+}
+
+int jrq_table_stage_acks(jrq_table* t, uint64_t stamp, const uint64_t* acks, uint32_t n) {
+  std::lock_guard<std::mutex> l(t->mu);
+  if (!n) return JRQ_OK;
+  t->segs.emplace_back(t->staged_a.size(), stamp);
+  t->staged_a.insert(t->staged_a.end(), acks, acks + n);
+  return JRQ_OK;
+}
+
 int jrq_table_stage_apply(jrq_table* t) {
   std::vector<jrq_group_state> s;
-  std::vector<uint64_t> r;
+  std::vector<uint64_t> r, a;
+  std::vector<std::pair<size_t, uint64_t>> segs;
   {
     std::lock_guard<std::mutex> l(t->mu);
     std::swap(s, t->staged_s);
     std::swap(r, t->staged_r);
+    std::swap(a, t->staged_a);
+    std::swap(segs, t->segs);
   }
   const jrq_group_state* sp = s.data();  // (update_gather carries the failure injection)
   const uint64_t* rp = r.data();
   const uint32_t ns = static_cast<uint32_t>(s.size()), nr = static_cast<uint32_t>(r.size());
-  return jrq_table_update_gather(t, 1, &sp, &ns, &rp, &nr);
+  const int rc = jrq_table_update_gather(t, 1, &sp, &ns, &rp, &nr);
+  if (rc) return rc;
+  // the order-free ack records (include/jrq.h JRQ_ACK): after the headers and records, a max,
+  // records stamped before their group's last reset dropped
+  std::lock_guard<std::mutex> l(t->mu);
+  for (size_t k = 0; k < segs.size(); ++k) {
+    const size_t e = k + 1 < segs.size() ? segs[k + 1].first : a.size();
+    for (size_t i = segs[k].first; i < e; ++i) {
+      const uint64_t w = a[i];
+      const uint32_t f = static_cast<uint32_t>(w & 31u), g = static_cast<uint32_t>(w >> 5) & ((1u << 27) - 1u);
+      if (g >= t->G || f > 16u || (f < 16u && f >= t->P)) {
+        ++t->invalid;
+        continue;
+      }
+      if (segs[k].second < t->rstamp[g] || t->pi[g] <= 0) continue;
+      const int64_t b = t->pi[g] - 1;
+      const int64_t v = b + static_cast<int32_t>(static_cast<uint32_t>(w >> 32) - static_cast<uint32_t>(b));
+      if (f == 16u) {
+        if (v - t->pi[g] >= 0x7FFFFFFF || (t->nr[g] == 0 && v >= t->pi[g])) {
+          ++t->invalid;
+          continue;
+        }
+        t->la[g] = std::max(t->la[g], v);
+      } else {
+        int64_t& m = t->match[static_cast<size_t>(g) * t->P + f];
+        m = std::max(m, v);
+      }
+    }
+  }
+  return JRQ_OK;
 }
 
 #ifdef FAKE_JRQ_CLOSED_FORM

@@ -374,6 +374,37 @@ static void testAddPeerCatchUpOnGpu(Engine& eng) {
   CHECK(t.same() && t.box.getLastCommittedIndex() == 111);
 }
 
+// The order-free records (JRQ_ACK, r06): acks and queue growth written at call time, applied on
+// the device as a max.  A slot given to another peer resets the group's stamp, which drops every
+// record of the group written before it -- the live peers' acks among them -- so the pack must
+// ship their current matches again: the commit below needs them (3 slots: peers 1, 2 in the
+// conf, 3 a catch-up peer; peer 4 then takes peer 3's slot in the same epoch).
+static void testResetStampKeepsLiveAcks(Engine& eng) {
+  auto batch = std::make_shared<GroupBatch>(&eng, 2, 3);
+  Twin t(batch, 1);
+  CHECK(t.box.resetPendingIndex(1) && jo_bb_reset_pending_index(t.bb, 1) == JO_TRUE);
+  const std::vector<int32_t> c12 = {1, 2}, c124 = {1, 2, 4};
+  CHECK(t.append(c12, nullptr, 10));  // 1..10
+  t.ack(1, 2, 3);                     // peer 3 takes the free third slot
+  batch->flush();                     // (sizes this thread's record buffers)
+  CHECK(t.same() && batch->lastFlush().acks == 0);
+  t.ack(1, 10, 1);                    // records (JRQ_ACK), not pack records
+  t.ack(1, 6, 2);
+  CHECK(t.append(c124, &c12, 1));     // 11: peer 4 needs a slot: peer 3's (no live conf names it)
+  batch->flush();
+  CHECK(batch->lastFlush().acks >= 3);
+  CHECK(t.same() && t.box.getLastCommittedIndex() == 6);  // peers 1, 2 acked 1..6
+  t.ack(7, 11, 2);
+  t.ack(1, 11, 4);
+  batch->flush();  // 11 is joint: {1, 2, 4} has 2 and 4, but {1, 2} only 2
+  CHECK(t.same());
+  CHECK(t.box.getLastCommittedIndex() == 10);
+  t.ack(11, 11, 1);
+  batch->flush();
+  CHECK(t.same());
+  CHECK(t.box.getLastCommittedIndex() == 11);
+}
+
 // Random call sequences (appends under stable and joint confs, conf changes that replace
 // peers, contiguous acks from members and catch-up peers, step-downs and new terms) through
 // the mirror and the oracle; the state must agree after every flush.  More distinct peers
@@ -1323,6 +1354,7 @@ int main(int argc, char** argv) {
     tests.push_back({"testLogReaderOnGpu", [&] { testLogReaderOnGpu(e); }});
     tests.push_back({"testLeaderTickerOnGpu", [&] { testLeaderTickerOnGpu(e); }});
     tests.push_back({"testReadIndexRounds", [&] { testReadIndexRounds(e); }});
+    tests.push_back({"testResetStampKeepsLiveAcks", [&] { testResetStampKeepsLiveAcks(e); }});
     tests.push_back({"testFSMCallerBatchOnGpu", [&] { testFSMCallerBatchOnGpu(e); }});
   }
   for (auto& t : tests) {

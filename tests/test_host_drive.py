@@ -90,6 +90,9 @@ def test_host_mirror_drives_series(engine, oracle, G, K, joint, active, threads)
     # flush); download = the changed commits
     recs, changed = _expected_counts(s, committed)
     np.testing.assert_array_equal(st["records"], recs)
+    # after the first flush (which sizes the threads' record buffers) the acks and queue sizes
+    # go up as the order-free records written at call time, not as pack records
+    assert (st["acks"][1:] == st["records"][1:]).all() and st["acks"][0] == 0
     np.testing.assert_array_equal(st["changed"], changed)
     assert st["states"][0] == G and (st["states"][1:] == 0).all()
     np.testing.assert_array_equal(st["h2d_bytes"], st["states"] * 96 + st["records"] * 8)

@@ -171,10 +171,17 @@ def main():
     pr, ar = new_map(4 << 20)
     keep.append((pr, ar))
     rr = hip.hipHostRegister(C.c_void_p(pr), 4 << 20, 0)
-    reg = hsa_info(pr)
+    reg = {"hsa": hsa_info(pr), "hip": hip_info(pr)}
     ru = hip.hipHostUnregister(C.c_void_p(pr))
     out["host_register_cycle"] = {"register_rc": rr, "registered": reg, "unregister_rc": ru,
-                                  "after_unregister": hsa_info(pr)}
+                                  "after_unregister": {"hsa": hsa_info(pr), "hip": hip_info(pr)}}
+    # the instruments themselves: a hipHostMalloc'ed range (what each reports for memory HIP
+    # certainly holds page-locked)
+    hip.hipHostMalloc.restype = C.c_int
+    hip.hipHostMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+    hp = C.c_void_p()
+    rh = hip.hipHostMalloc(C.byref(hp), 1 << 20, 0)
+    out["host_malloc_instrument_check"] = {"rc": rh, "hsa": hsa_info(hp.value), "hip": hip_info(hp.value)}
     print(json.dumps(out, indent=1))
     sys.stdout.flush()
     os._exit(0)  # leave the mappings to the kernel; no runtime teardown over the replaced ranges
