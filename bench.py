@@ -744,9 +744,9 @@ def leg_drive(ctx, args, G):
     from jraft_amd import workloads as W
     K = 6
     out = {}
-    for active, threads in ((1.0, 1), (1.0, 16), (0.1, 16)):
+    for active, threads, shards in ((1.0, 1, 1), (1.0, 16, 1), (0.1, 16, 1), (1.0, 16, 2)):
         s = W.host_series("C3", K, groups=G, joint_frac=0.01, active=active)
-        committed, st = drive.drive_epochs(ctx.dev.index, s, threads=threads)
+        committed, st = drive.drive_epochs(ctx.dev.index, s, threads=threads, shards=shards)
         ok = None
         if active == 1.0:  # every group against the stateless K-epoch kernel
             d = {k: to_dev(s[k], ctx.dev) for k in ("match", "last_appended", "pending_index",
@@ -764,8 +764,9 @@ def leg_drive(ctx, args, G):
         f = float(np.mean(st["flush_ms"][sl]))
         api = float(np.mean(st["api_ms"][sl]))
         pcie = float(np.mean(st["h2d_bytes"][sl] + st["d2h_bytes"][sl]))
-        out[f"active_{int(active * 100)}pct_{threads}_threads"] = {
-            "api_threads": threads,
+        key = f"active_{int(active * 100)}pct_{threads}_threads"
+        out[key + (f"_{shards}_engines" if shards > 1 else "")] = {
+            "api_threads": threads, "engines": shards,
             "flush_ms": f, "pack_ms": float(np.mean(st["pack_ms"][sl])),
             "device_ms": float(np.mean(st["device_ms"][sl])),
             "deliver_ms": float(np.mean(st["deliver_ms"][sl])),
@@ -807,7 +808,11 @@ def leg_drive(ctx, args, G):
                         f"1% with a conf change in the pending window, {K} epochs",
             "how": "flush = pack changed records + H2D (pinned) + apply + epoch kernels + D2H of "
                    "the changed commits + closures / onCommitted; api = the appendPendingTask / "
-                   "commitAt calls of the epoch (made before the flush, from `api_threads` threads)",
+                   "commitAt calls of the epoch (made before the flush, from `api_threads` threads); "
+                   "engines = 2: the groups in two contiguous blocks over two engines on this GPU "
+                   "(ShardedGroupBatch), both shards' epochs concurrent, then the node-wide "
+                   "committed snapshot published to both engines inside flush_ms (device copies: RCCL "
+                   "needs one device per rank), then read back against every BallotBox",
             **out, "ack_to_onCommitted_latency": lats}
 
 

@@ -658,6 +658,40 @@ int jrq_rccl_nranks(jrq_engine *e);
 int jrq_publish_committed_dev(jrq_engine *e, const int64_t *local_dev, int64_t *global_dev,
                               uint64_t count_per_rank);
 
+/* Single-process form (r06): one host process -- a JVM holding every region of its node, as
+ * RheaKV's StoreEngine does (RK/StoreEngine.java:93) -- drives n engines, one per GPU, each with
+ * a resident table over a contiguous block of the node's groups (jraft::ShardedGroupBatch).
+ * jrq_rccl_init_all creates one communicator per engine in one call (ncclCommInitAll over the
+ * engines' devices, rank i = engines[i]); JRQ_E_RCCL if RCCL refuses (e.g. two engines on one
+ * device), and the engines then have none. */
+int jrq_rccl_init_all(jrq_engine *const *engines, int n);
+/* The node-wide snapshot of n engines' committed[count_per_engine] arrays: global_dev[i] (on
+ * engine i's device, n * count_per_engine words) receives every local_dev[j] at j *
+ * count_per_engine.  One grouped RCCL all-gather when every engine has a communicator from
+ * jrq_rccl_init_all; else device-to-device copies (hipMemcpyPeerAsync, each destination stream
+ * waiting for the source engine's stream).  Asynchronous on each engine's stream. */
+int jrq_publish_committed_all_dev(jrq_engine *const *engines, int n, const int64_t *const *local_dev,
+                                  int64_t *const *global_dev, uint64_t count_per_engine);
+/* lastCommittedIndex of every group of the table, contiguous: out_dev[g] for g < G (the tiled
+ * lc row de-tiled on the device), asynchronous on the engine's stream -- the local part of a
+ * snapshot. */
+int jrq_table_committed_dev(jrq_table *t, int64_t *out_dev);
+
+/* A node-wide snapshot object for a single-process host: n tables (one per engine, in group
+ * order: table i holds groups [i k, i k + G_i), k = the first table's G; every table but the last
+ * has exactly k groups) and, per engine, device buffers of k local and n k gathered words
+ * (rank-major, the last block padded with -1).  jrq_snapshot_publish de-tiles every table's
+ * committed[] (jrq_table_committed_dev) and gathers them (jrq_publish_committed_all_dev) on the
+ * engines' streams; jrq_snapshot_read synchronises engine i and copies its gathered snapshot to
+ * host_out[0 .. sum G_i), unpadded (what getLastCommittedIndex readers on any GPU see,
+ * BallotBox.java:67-79).  jrq_snapshot_via: 1 = RCCL (jrq_rccl_init_all succeeded), 0 = copies. */
+typedef struct jrq_snapshot jrq_snapshot;
+jrq_snapshot *jrq_snapshot_create(jrq_table *const *tables, int n, int *err);
+void jrq_snapshot_destroy(jrq_snapshot *s);
+int jrq_snapshot_publish(jrq_snapshot *s);
+int jrq_snapshot_read(jrq_snapshot *s, int i, int64_t *host_out);
+int jrq_snapshot_via(const jrq_snapshot *s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -217,6 +217,41 @@ JNIEXPORT jint FN(tableCheck)(JNIEnv *env, jclass cls, jlong table) {
     return jrq_jni_table_check(ENG(table));
 }
 
+/* engines / tables: a direct buffer of n longs (native handles) */
+JNIEXPORT jint FN(rcclInitAll)(JNIEnv *env, jclass cls, jobject engines, jint n) {
+    (void)cls;
+    return jrq_jni_rccl_init_all(ADDR(engines), n);
+}
+
+JNIEXPORT jlong FN(snapshotCreate)(JNIEnv *env, jclass cls, jobject tables, jint n,
+                                   jobject errOut) {
+    (void)cls;
+    return (jlong)jrq_jni_snapshot_create(ADDR(tables), n, ADDR(errOut));
+}
+
+JNIEXPORT void FN(snapshotDestroy)(JNIEnv *env, jclass cls, jlong snap) {
+    (void)env;
+    (void)cls;
+    jrq_jni_snapshot_destroy(ENG(snap));
+}
+
+JNIEXPORT jint FN(snapshotPublish)(JNIEnv *env, jclass cls, jlong snap) {
+    (void)env;
+    (void)cls;
+    return jrq_jni_snapshot_publish(ENG(snap));
+}
+
+JNIEXPORT jint FN(snapshotRead)(JNIEnv *env, jclass cls, jlong snap, jint i, jobject out) {
+    (void)cls;
+    return jrq_jni_snapshot_read(ENG(snap), i, ADDR(out));
+}
+
+JNIEXPORT jint FN(snapshotVia)(JNIEnv *env, jclass cls, jlong snap) {
+    (void)env;
+    (void)cls;
+    return jrq_jni_snapshot_via(ENG(snap));
+}
+
 JNIEXPORT jint FN(crc64Batch)(JNIEnv *env, jclass cls, jlong eng, jobject payload,
                               jobject offsets, jint n, jobject out) {
     (void)cls;

@@ -193,6 +193,41 @@ int32_t jrq_jni_table_read(jrq_addr table, jrq_addr pending_index, jrq_addr last
 
 int32_t jrq_jni_table_check(jrq_addr table) { return jrq_table_check(A(jrq_table *, table)); }
 
+/* jrq_addr words are handles; on an LP64 host they are pointer-sized, checked below */
+typedef char jrq_jni_addr_is_a_pointer[sizeof(jrq_addr) == sizeof(void *) ? 1 : -1];
+
+int32_t jrq_jni_rccl_init_all(jrq_addr engines, int32_t n) {
+    if (n <= 0 || !engines) return JRQ_E_INVALID;
+    return jrq_rccl_init_all(A(jrq_engine *const *, engines), n);
+}
+
+jrq_addr jrq_jni_snapshot_create(jrq_addr tables, int32_t n, jrq_addr err_out) {
+    int err = 0;
+    jrq_snapshot *s = NULL;
+    if (n <= 0 || !tables) {
+        err = JRQ_E_INVALID;
+    } else {
+        s = jrq_snapshot_create(A(jrq_table *const *, tables), n, &err);
+    }
+    if (err_out) *A(int32_t *, err_out) = (int32_t)err;
+    return (jrq_addr)(intptr_t)s;
+}
+
+void jrq_jni_snapshot_destroy(jrq_addr snap) { jrq_snapshot_destroy(A(jrq_snapshot *, snap)); }
+
+int32_t jrq_jni_snapshot_publish(jrq_addr snap) {
+    return jrq_snapshot_publish(A(jrq_snapshot *, snap));
+}
+
+int32_t jrq_jni_snapshot_read(jrq_addr snap, int32_t i, jrq_addr host_out) {
+    N(i);
+    return jrq_snapshot_read(A(jrq_snapshot *, snap), i, A(int64_t *, host_out));
+}
+
+int32_t jrq_jni_snapshot_via(jrq_addr snap) {
+    return jrq_snapshot_via(A(const jrq_snapshot *, snap));
+}
+
 int32_t jrq_jni_crc64_batch(jrq_addr eng, jrq_addr payload, jrq_addr offsets, int32_t n,
                             jrq_addr crc_out) {
     N(n);

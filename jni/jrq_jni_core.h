@@ -73,6 +73,15 @@ int32_t jrq_jni_table_read(jrq_addr table, jrq_addr pending_index, jrq_addr last
                            jrq_addr last_committed, jrq_addr match);
 int32_t jrq_jni_table_check(jrq_addr table);
 
+/* one JVM, N engines (ShardedGroupBatch): `engines` / `tables` is the
+ * address of n jrq_addr words */
+int32_t jrq_jni_rccl_init_all(jrq_addr engines, int32_t n);
+jrq_addr jrq_jni_snapshot_create(jrq_addr tables, int32_t n, jrq_addr err_out);
+void jrq_jni_snapshot_destroy(jrq_addr snap);
+int32_t jrq_jni_snapshot_publish(jrq_addr snap);
+int32_t jrq_jni_snapshot_read(jrq_addr snap, int32_t i, jrq_addr host_out);
+int32_t jrq_jni_snapshot_via(jrq_addr snap);
+
 /* checksums (CrcUtil.java:36-80, CRC64.java:100-126, LogEntry.java:88-108,156-158) */
 int32_t jrq_jni_crc64_batch(jrq_addr eng, jrq_addr payload, jrq_addr offsets, int32_t n,
                             jrq_addr crc_out);

@@ -1982,6 +1982,22 @@ int jrq_table_epoch(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, ui
 
 uint32_t jrq_table_slices(const jrq_table* t) { return t ? t->slices : 0; }
 
+int jrq_table_committed_dev(jrq_table* t, int64_t* out_dev) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if (!out_dev) return fail(e, JRQ_E_INVALID, "null committed output");
+  DeviceGuard guard(e->device);
+  const size_t G = t->a.G, full = G / jrq::kTableSlice, rest = G % jrq::kTableSlice;
+  const size_t tb = jrq::kTableSlice * 8;  // the lc rows, tile by tile (lastCommitted is never
+                                            // encoded: only pendingIndex follows it)
+  if (full)
+    JRQ_HIP(e, hipMemcpy2DAsync(out_dev, tb, t->a.lc, t->a.ts * 8, tb, full, hipMemcpyDeviceToDevice, e->stream));
+  if (rest)
+    JRQ_HIP(e, hipMemcpyAsync(out_dev + full * jrq::kTableSlice, t->a.lc + full * t->a.ts, rest * 8,
+                              hipMemcpyDeviceToDevice, e->stream));
+  return JRQ_OK;
+}
+
 int jrq_table_read(jrq_table* t, int64_t* pending_index, int64_t* last_appended,
                    int64_t* last_committed, int64_t* match) {
   if (table_check(t)) return JRQ_E_INVALID;
@@ -2119,6 +2135,180 @@ int jrq_publish_committed_dev(jrq_engine* e, const int64_t* local, int64_t* glob
   ncclResult_t r = ncclAllGather(local, global, count_per_rank, ncclInt64, e->comm, e->stream);
   if (r != ncclSuccess) return fail(e, JRQ_E_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
   return JRQ_OK;
+}
+
+}  // extern "C"
+
+struct jrq_snapshot {
+  std::vector<jrq_table*> t;
+  std::vector<jrq_engine*> e;
+  std::vector<int64_t*> local, global;
+  std::vector<uint32_t> G;
+  uint64_t k = 0;
+  int via = 0;
+};
+
+extern "C" {
+
+jrq_snapshot* jrq_snapshot_create(jrq_table* const* tables, int n, int* err) {
+  auto set = [&](int c) {
+    if (err) *err = c;
+  };
+  if (!tables || n <= 0) {
+    set(JRQ_E_INVALID);
+    return nullptr;
+  }
+  auto* s = new jrq_snapshot();
+  for (int i = 0; i < n; ++i) {
+    if (!tables[i] || !tables[i]->e) {
+      delete s;
+      set(JRQ_E_INVALID);
+      return nullptr;
+    }
+    s->t.push_back(tables[i]);
+    s->e.push_back(tables[i]->e);
+    s->G.push_back(tables[i]->a.G);
+  }
+  s->k = s->G[0];
+  for (int i = 0; i + 1 < n; ++i)
+    if (s->G[i] != s->k || s->G[n - 1] > s->k) {
+      fail(s->e[0], JRQ_E_INVALID, "snapshot: tables must hold k groups each (the last at most k)");
+      delete s;
+      set(JRQ_E_INVALID);
+      return nullptr;
+    }
+  if (n == 1 && s->G[0] > s->k) s->k = s->G[0];
+  s->local.assign(n, nullptr);
+  s->global.assign(n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    DeviceGuard guard(s->e[i]->device);
+    if (hipMalloc(&s->local[i], s->k * 8) != hipSuccess ||
+        hipMalloc(&s->global[i], s->k * 8 * n) != hipSuccess ||
+        hipMemset(s->local[i], 0xFF, s->k * 8) != hipSuccess) {
+      fail(s->e[i], JRQ_E_NOMEM, "snapshot: device buffers");
+      jrq_snapshot_destroy(s);
+      set(JRQ_E_NOMEM);
+      return nullptr;
+    }
+  }
+  bool all = true;
+  for (int i = 0; i < n; ++i) all = all && s->e[i]->comm && s->e[i]->nranks == n && s->e[i]->rank == i;
+  s->via = all ? 1 : 0;
+  set(JRQ_OK);
+  return s;
+}
+
+void jrq_snapshot_destroy(jrq_snapshot* s) {
+  if (!s) return;
+  for (size_t i = 0; i < s->e.size(); ++i) {
+    DeviceGuard guard(s->e[i]->device);
+    (void)hipStreamSynchronize(s->e[i]->stream);
+    if (s->local[i]) (void)hipFree(s->local[i]);
+    if (s->global[i]) (void)hipFree(s->global[i]);
+  }
+  delete s;
+}
+
+int jrq_snapshot_publish(jrq_snapshot* s) {
+  if (!s) return JRQ_E_INVALID;
+  const int n = static_cast<int>(s->t.size());
+  for (int i = 0; i < n; ++i) {
+    const int rc = jrq_table_committed_dev(s->t[i], s->local[i]);
+    if (rc) return rc;
+  }
+  std::vector<const int64_t*> loc(s->local.begin(), s->local.end());
+  return jrq_publish_committed_all_dev(s->e.data(), n, loc.data(), s->global.data(), s->k);
+}
+
+int jrq_snapshot_read(jrq_snapshot* s, int i, int64_t* host_out) {
+  if (!s || i < 0 || i >= static_cast<int>(s->e.size()) || !host_out) return JRQ_E_INVALID;
+  jrq_engine* e = s->e[i];
+  DeviceGuard guard(e->device);
+  const int n = static_cast<int>(s->t.size());
+  std::vector<int64_t> all(s->k * n);
+  JRQ_DOWN(e, all.data(), s->global[i], all.size() * 8);
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  uint64_t at = 0;
+  for (int j = 0; j < n; ++j) {
+    std::memcpy(host_out + at, all.data() + s->k * j, static_cast<size_t>(s->G[j]) * 8);
+    at += s->G[j];
+  }
+  return JRQ_OK;
+}
+
+int jrq_snapshot_via(const jrq_snapshot* s) { return s ? s->via : JRQ_E_INVALID; }
+
+int jrq_rccl_init_all(jrq_engine* const* engines, int n) {
+  if (!engines || n <= 0) return JRQ_E_INVALID;
+  std::vector<int> devs(n);
+  for (int i = 0; i < n; ++i) {
+    if (!engines[i]) return JRQ_E_INVALID;
+    devs[i] = engines[i]->device;
+  }
+  for (int i = 0; i < n; ++i)
+    if (engines[i]->comm) {
+      (void)ncclCommDestroy(engines[i]->comm);
+      engines[i]->comm = nullptr;
+    }
+  std::vector<ncclComm_t> comms(n, nullptr);
+  const ncclResult_t r = ncclCommInitAll(comms.data(), n, devs.data());
+  if (r != ncclSuccess) {
+    for (auto c : comms)
+      if (c) (void)ncclCommDestroy(c);
+    return fail(engines[0], JRQ_E_RCCL, "ncclCommInitAll: %s", ncclGetErrorString(r));
+  }
+  for (int i = 0; i < n; ++i) {
+    engines[i]->comm = comms[i];
+    engines[i]->nranks = n;
+    engines[i]->rank = i;
+  }
+  return JRQ_OK;
+}
+
+int jrq_publish_committed_all_dev(jrq_engine* const* engines, int n, const int64_t* const* local,
+                                  int64_t* const* global, uint64_t count) {
+  if (!engines || n <= 0 || !local || !global) return JRQ_E_INVALID;
+  bool rccl = true;
+  for (int i = 0; i < n; ++i) {
+    if (!engines[i] || !local[i] || !global[i]) return JRQ_E_INVALID;
+    rccl = rccl && engines[i]->comm && engines[i]->nranks == n && engines[i]->rank == i;
+  }
+  if (rccl) {  // one grouped all-gather over the n communicators
+    ncclResult_t r = ncclGroupStart();
+    for (int i = 0; i < n && r == ncclSuccess; ++i) {
+      DeviceGuard guard(engines[i]->device);
+      r = ncclAllGather(local[i], global[i], count, ncclInt64, engines[i]->comm, engines[i]->stream);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      return fail(engines[0], JRQ_E_RCCL, "grouped ncclAllGather: %s",
+                  ncclGetErrorString(r != ncclSuccess ? r : r2));
+    return JRQ_OK;
+  }
+  // device-to-device copies: destination i's stream waits for source j's stream, then copies
+  std::vector<hipEvent_t> ev(n, nullptr);
+  int rc = JRQ_OK;
+  for (int j = 0; j < n && rc == JRQ_OK; ++j) {
+    DeviceGuard guard(engines[j]->device);
+    if (hipEventCreateWithFlags(&ev[j], hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(ev[j], engines[j]->stream) != hipSuccess)
+      rc = fail(engines[j], JRQ_E_HIP, "publish: event on engine %d", j);
+  }
+  for (int i = 0; i < n && rc == JRQ_OK; ++i) {
+    DeviceGuard guard(engines[i]->device);
+    for (int j = 0; j < n && rc == JRQ_OK; ++j) {
+      if (hipStreamWaitEvent(engines[i]->stream, ev[j], 0) != hipSuccess ||
+          hipMemcpyPeerAsync(global[i] + static_cast<size_t>(j) * count, engines[i]->device, local[j],
+                             engines[j]->device, count * 8, engines[i]->stream) != hipSuccess)
+        rc = fail(engines[i], JRQ_E_HIP, "publish: copy %d -> %d", j, i);
+    }
+  }
+  for (int j = 0; j < n; ++j)
+    if (ev[j]) {
+      DeviceGuard guard(engines[j]->device);
+      (void)hipEventDestroy(ev[j]);  // (released once the waits it is part of complete)
+    }
+  return rc;
 }
 
 }  // extern "C"

@@ -29,6 +29,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <exception>
@@ -144,19 +145,42 @@ const char* jraft_drive_last_error(void) { return g_err.c_str(); }
 // stats_out[k * 12 + i]: 0 api_ms, 1 pack_ms, 2 device_ms, 3 deliver_ms, 4 flush_ms,
 // 5 h2d_bytes, 6 d2h_bytes, 7 states, 8 records (pack + call-time), 9 changed, 10 api_calls,
 // 11 acks (the call-time order-free records among them)
-int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t threads,
-                       const int64_t* pi0, const int64_t* lc0, const uint64_t* conf_a,
-                       const uint64_t* conf_b, const int64_t* switch_at, const int64_t* la,
-                       const int64_t* match, int64_t* committed_out, double* stats_out) {
+//
+// jraft_drive_epochs_sharded -- the same over `shards` engines on `device` in one process
+// (ShardedGroupBatch: contiguous group blocks, the shards' epochs concurrent on their streams);
+// after each flush the node-wide snapshot is published, and committed_out is read from engine
+// k % shards's copy of it, checked against every group's getLastCommittedIndex.  stats: pack,
+// device and deliver ms are the slowest shard's; bytes, states, records and changed the sums.
+int jraft_drive_epochs_sharded(int device, uint32_t shards, uint32_t G, uint32_t P, uint32_t K,
+                               uint32_t threads, const int64_t* pi0, const int64_t* lc0,
+                               const uint64_t* conf_a, const uint64_t* conf_b,
+                               const int64_t* switch_at, const int64_t* la, const int64_t* match,
+                               int64_t* committed_out, double* stats_out) {
   using clk = std::chrono::steady_clock;
   auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
   try {
     const unsigned T = std::max(1u, std::min(threads, G));
-    jraft::Engine eng(device, G, static_cast<uint8_t>(P));
-    auto batch = std::make_shared<jraft::GroupBatch>(&eng, G, P);
+    const uint32_t S = std::max(1u, std::min(shards, G));
+    const uint32_t per = (G + S - 1) / S;
+    std::vector<std::unique_ptr<jraft::Engine>> engs;
+    std::vector<jraft::Engine*> ep;
+    for (uint32_t i = 0; i < S; ++i) {
+      engs.emplace_back(new jraft::Engine(device, S == 1 ? G : per, static_cast<uint8_t>(P)));
+      ep.push_back(engs.back().get());
+    }
+    std::shared_ptr<jraft::GroupBatch> batch;
+    std::unique_ptr<jraft::ShardedGroupBatch> sharded;
     std::vector<jraft::BallotBox> boxes;
     boxes.reserve(G);
-    for (uint32_t g = 0; g < G; ++g) boxes.emplace_back(batch, g);
+    if (S == 1) {
+      batch = std::make_shared<jraft::GroupBatch>(ep[0], G, P);
+      for (uint32_t g = 0; g < G; ++g) boxes.emplace_back(batch, g);
+    } else {
+      sharded.reset(new jraft::ShardedGroupBatch(ep, G, P));
+      sharded->rcclInitAll();  // one device: refused, copies
+      for (uint32_t g = 0; g < G; ++g) boxes.push_back(sharded->box(g));
+    }
+    std::vector<int64_t> snap(sharded ? G : 0);
     std::vector<jraft::PeerId> peers;
     for (uint32_t p = 0; p < P; ++p) peers.emplace_back("127.0.0.1", 8001 + static_cast<int>(p));
     // every distinct conf word's Configurations, built before the threads start (read-only)
@@ -226,23 +250,38 @@ int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t 
         calls[t] = n;
       });
       const auto t1 = clk::now();
-      batch->flush();
+      if (sharded) {
+        sharded->flush();
+        sharded->publish();
+      } else {
+        batch->flush();
+      }
       const auto t2 = clk::now();
-      for (uint32_t g = 0; g < G; ++g)
-        committed_out[static_cast<size_t>(k) * G + g] = boxes[g].getLastCommittedIndex();
-      const jraft::FlushStats& s = batch->lastFlush();
+      int64_t* ck = committed_out + static_cast<size_t>(k) * G;
+      for (uint32_t g = 0; g < G; ++g) ck[g] = boxes[g].getLastCommittedIndex();
+      if (sharded) {
+        sharded->readSnapshot(k % S, snap.data());
+        for (uint32_t g = 0; g < G; ++g)
+          if (snap[g] != ck[g])
+            throw std::runtime_error("published snapshot of group " + std::to_string(g) + " on engine " +
+                                     std::to_string(k % S) + " differs from its getLastCommittedIndex");
+      }
       double* o = stats_out + static_cast<size_t>(k) * 12;
+      std::fill(o, o + 12, 0.0);
+      for (uint32_t i = 0; i < S; ++i) {
+        const jraft::FlushStats& s = sharded ? sharded->lastFlush(i) : batch->lastFlush();
+        o[1] = std::max(o[1], s.pack_ms);
+        o[2] = std::max(o[2], s.device_ms);
+        o[3] = std::max(o[3], s.deliver_ms);
+        o[5] += static_cast<double>(s.h2d_bytes);
+        o[6] += static_cast<double>(s.d2h_bytes);
+        o[7] += s.states;
+        o[8] += static_cast<double>(s.records) + s.acks;
+        o[11] += s.acks;
+        o[9] += s.changed;
+      }
       o[0] = ms(t1 - t0);
-      o[1] = s.pack_ms;
-      o[2] = s.device_ms;
-      o[3] = s.deliver_ms;
       o[4] = ms(t2 - t1);
-      o[5] = static_cast<double>(s.h2d_bytes);
-      o[6] = static_cast<double>(s.d2h_bytes);
-      o[7] = s.states;
-      o[8] = static_cast<double>(s.records) + s.acks;
-      o[11] = s.acks;
-      o[9] = s.changed;
       uint64_t nc = 0;
       for (uint64_t c : calls) nc += c;
       o[10] = static_cast<double>(nc);
@@ -252,6 +291,14 @@ int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t 
     g_err = ex.what();
     return -1;
   }
+}
+
+int jraft_drive_epochs(int device, uint32_t G, uint32_t P, uint32_t K, uint32_t threads,
+                       const int64_t* pi0, const int64_t* lc0, const uint64_t* conf_a,
+                       const uint64_t* conf_b, const int64_t* switch_at, const int64_t* la,
+                       const int64_t* match, int64_t* committed_out, double* stats_out) {
+  return jraft_drive_epochs_sharded(device, 1, G, P, K, threads, pi0, lc0, conf_a, conf_b, switch_at,
+                                    la, match, committed_out, stats_out);
 }
 
 // out[0] commits (onCommitted calls), 1 entries appended, 2 commitAt calls, 3 seconds,

@@ -1639,6 +1639,101 @@ uint32_t FSMCallerBatch::doCommitted(const Apply& onApply, const std::function<v
   return static_cast<uint32_t>(jobs.size());
 }
 
+// ---------------------------------------------------------- sharded batch
+
+ShardedGroupBatch::ShardedGroupBatch(const std::vector<Engine*>& engines, uint32_t groups, uint32_t peers)
+    : eng_(engines), G_(groups) {
+  if (engines.empty()) throw std::invalid_argument("ShardedGroupBatch needs at least one engine");
+  for (Engine* e : engines)
+    if (!e) throw std::invalid_argument("ShardedGroupBatch: null engine");
+  const uint32_t n = static_cast<uint32_t>(engines.size());
+  if (groups < n) throw std::invalid_argument("ShardedGroupBatch: fewer groups than engines");
+  k_ = static_cast<uint32_t>((static_cast<uint64_t>(groups) + n - 1) / n);
+  if (static_cast<uint64_t>(k_) * (n - 1) >= groups)
+    throw std::invalid_argument("ShardedGroupBatch: the last engine would hold no group");
+  const unsigned per = std::max(1u, std::min(16u, usableCpus()) / n);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t lo = i * k_, hi = std::min(groups, lo + k_);
+    shard_.push_back(std::make_shared<GroupBatch>(engines[i], hi - lo, peers));
+    shard_.back()->setFlushThreads(per);
+  }
+}
+
+ShardedGroupBatch::~ShardedGroupBatch() {
+  if (snap_) jrq_snapshot_destroy(snap_);
+}
+
+const std::shared_ptr<GroupBatch>& ShardedGroupBatch::shardOf(uint32_t g, uint32_t* local) const {
+  if (g >= G_) throw std::out_of_range("group id");
+  const uint32_t s = g / k_;
+  if (local) *local = g - s * k_;
+  return shard_[s];
+}
+
+BallotBox ShardedGroupBatch::box(uint32_t g) const {
+  uint32_t l = 0;
+  const auto& b = shardOf(g, &l);
+  return BallotBox(b, l);
+}
+
+void ShardedGroupBatch::setFlushThreads(unsigned n) {
+  for (auto& b : shard_) b->setFlushThreads(n);
+}
+
+uint32_t ShardedGroupBatch::flush() {
+  const size_t n = shard_.size();
+  std::vector<uint32_t> changed(n, 0);
+  std::vector<std::exception_ptr> err(n);
+  auto one = [&](size_t i) {
+    try {
+      changed[i] = shard_[i]->flush();
+    } catch (...) {
+      err[i] = std::current_exception();
+    }
+  };
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < n; ++i) th.emplace_back(one, i);
+  one(0);
+  for (auto& t : th) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+  uint32_t total = 0;
+  for (uint32_t c : changed) total += c;
+  return total;
+}
+
+bool ShardedGroupBatch::rcclInitAll() {
+  std::vector<jrq_engine*> raw;
+  for (Engine* e : eng_) raw.push_back(e->raw());
+  rccl_ = jrq_rccl_init_all(raw.data(), static_cast<int>(raw.size())) == JRQ_OK;
+  if (snap_) {  // (the snapshot object records how it publishes when it is made)
+    jrq_snapshot_destroy(snap_);
+    snap_ = nullptr;
+  }
+  return rccl_;
+}
+
+void ShardedGroupBatch::publish() {
+  if (!snap_) {
+    std::vector<jrq_table*> tabs;
+    for (auto& b : shard_) {
+      if (!b->table_) throw std::logic_error("ShardedGroupBatch::publish before the first flush");
+      tabs.push_back(b->table_);
+    }
+    int err = 0;
+    snap_ = jrq_snapshot_create(tabs.data(), static_cast<int>(tabs.size()), &err);
+    if (!snap_) throwIfError(err ? err : JRQ_E_NOMEM, eng_[0]->raw(), "jrq_snapshot_create");
+  }
+  throwIfError(jrq_snapshot_publish(snap_), eng_[0]->raw(), "jrq_snapshot_publish");
+}
+
+void ShardedGroupBatch::readSnapshot(uint32_t i, int64_t* out) {
+  if (!snap_) throw std::logic_error("ShardedGroupBatch::readSnapshot before publish");
+  throwIfError(jrq_snapshot_read(snap_, static_cast<int>(i), out), eng_[i]->raw(), "jrq_snapshot_read");
+}
+
+bool ShardedGroupBatch::publishedOverRccl() const { return snap_ && jrq_snapshot_via(snap_) == 1; }
+
 // ------------------------------------------------------------- leader tick
 
 LeaderTicker::LeaderTicker(Engine& eng, uint32_t groups, uint32_t peers)

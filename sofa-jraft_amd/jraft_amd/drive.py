@@ -32,6 +32,9 @@ def load():
         d.jraft_drive_epochs.restype = C.c_int
         d.jraft_drive_epochs.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.c_uint32] + [C.c_void_p] * 9
+        d.jraft_drive_epochs_sharded.restype = C.c_int
+        d.jraft_drive_epochs_sharded.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32,
+                                                 C.c_uint32, C.c_uint32] + [C.c_void_p] * 9
         d.jraft_drive_latency.restype = C.c_int
         d.jraft_drive_latency.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                           C.c_double, C.c_uint32, C.c_uint32, C.c_uint32,
@@ -40,10 +43,12 @@ def load():
     return _drv
 
 
-def drive_epochs(device: int, s: dict, threads: int = 1):
+def drive_epochs(device: int, s: dict, threads: int = 1, shards: int = 1):
     """Replay series `s` (workloads.host_series) through BallotBox, each epoch's calls made by
     `threads` threads (contiguous group slices); returns (committed [K][G] after each flush,
-    stats dict of per-epoch arrays named by STATS)."""
+    stats dict of per-epoch arrays named by STATS).  shards > 1: the groups over that many
+    engines on `device` (ShardedGroupBatch), committed read from the published node-wide
+    snapshot (checked against every BallotBox inside the driver)."""
     d = load()
     K, P, G = s["match"].shape
     arrs = {k: np.ascontiguousarray(s[k]) for k in ("pending_index", "last_committed", "conf_a",
@@ -52,9 +57,10 @@ def drive_epochs(device: int, s: dict, threads: int = 1):
     out = np.zeros((K, G), np.int64)
     stats = np.zeros((K, len(STATS)), np.float64)
     ptr = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
-    rc = d.jraft_drive_epochs(device, G, P, K, threads, ptr(arrs["pending_index"]), ptr(arrs["last_committed"]),
-                              ptr(arrs["conf_a"]), ptr(arrs["conf_b"]), ptr(arrs["switch_at"]),
-                              ptr(arrs["last_appended"]), ptr(arrs["match"]), ptr(out), ptr(stats))
+    rc = d.jraft_drive_epochs_sharded(device, shards, G, P, K, threads, ptr(arrs["pending_index"]),
+                                      ptr(arrs["last_committed"]), ptr(arrs["conf_a"]), ptr(arrs["conf_b"]),
+                                      ptr(arrs["switch_at"]), ptr(arrs["last_appended"]), ptr(arrs["match"]),
+                                      ptr(out), ptr(stats))
     if rc != 0:
         raise RuntimeError("jraft_drive_epochs: " + (d.jraft_drive_last_error() or b"").decode())
     return out, {k: stats[:, i] for i, k in enumerate(STATS)}

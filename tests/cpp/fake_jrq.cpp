@@ -262,6 +262,60 @@ int jrq_table_stage_apply(jrq_table* t) {
   return JRQ_OK;
 }
 
+// The single-process snapshot (include/jrq.h jrq_snapshot): "device" memory is host memory
+// here; RCCL is never available, so it publishes by copies, as two engines on one GPU do.
+int jrq_rccl_init_all(jrq_engine* const* engines, int n) {
+  if (!engines || n <= 0) return JRQ_E_INVALID;
+  engines[0]->err = "ncclCommInitAll: not in the test double";
+  return JRQ_E_RCCL;
+}
+int jrq_table_committed_dev(jrq_table* t, int64_t* out) {
+  std::lock_guard<std::mutex> l(t->mu);
+  std::copy(t->lc.begin(), t->lc.end(), out);
+  return JRQ_OK;
+}
+int jrq_publish_committed_all_dev(jrq_engine* const*, int n, const int64_t* const* local,
+                                  int64_t* const* global, uint64_t count) {
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) std::copy(local[j], local[j] + count, global[i] + static_cast<size_t>(j) * count);
+  return JRQ_OK;
+}
+struct jrq_snapshot {
+  std::vector<jrq_table*> t;
+  uint64_t k = 0;
+  std::vector<std::vector<int64_t>> local, global;
+};
+jrq_snapshot* jrq_snapshot_create(jrq_table* const* tables, int n, int* err) {
+  auto* s = new jrq_snapshot();
+  s->t.assign(tables, tables + n);
+  s->k = tables[0]->G;
+  s->local.assign(n, std::vector<int64_t>(s->k, -1));
+  s->global.assign(n, std::vector<int64_t>(s->k * n, -1));
+  if (err) *err = JRQ_OK;
+  return s;
+}
+void jrq_snapshot_destroy(jrq_snapshot* s) { delete s; }
+int jrq_snapshot_publish(jrq_snapshot* s) {
+  const int n = static_cast<int>(s->t.size());
+  std::vector<const int64_t*> loc;
+  std::vector<int64_t*> glob;
+  for (int i = 0; i < n; ++i) {
+    jrq_table_committed_dev(s->t[i], s->local[i].data());
+    loc.push_back(s->local[i].data());
+    glob.push_back(s->global[i].data());
+  }
+  return jrq_publish_committed_all_dev(nullptr, n, loc.data(), glob.data(), s->k);
+}
+int jrq_snapshot_read(jrq_snapshot* s, int i, int64_t* out) {
+  uint64_t at = 0;
+  for (size_t j = 0; j < s->t.size(); ++j) {
+    std::copy(s->global[i].begin() + s->k * j, s->global[i].begin() + s->k * j + s->t[j]->G, out + at);
+    at += s->t[j]->G;
+  }
+  return JRQ_OK;
+}
+int jrq_snapshot_via(const jrq_snapshot*) { return 0; }
+
 #ifdef FAKE_JRQ_CLOSED_FORM
 // The host-API cost probe (tools/api_probe.py) needs 1M-group epochs in milliseconds, not the
 // replay's seconds: the closed form of DESIGN.md §1 (a run [s, e] commits min(e, k_new, k_old)

@@ -8,6 +8,7 @@
 //   core/BallotBoxTest.java:62-154, entity/BallotTest.java:37-50,
 //   entity/LogEntryTest.java:95-125, util/CrcUtilTest.java:27-42
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -403,6 +404,54 @@ static void testResetStampKeepsLiveAcks(Engine& eng) {
   batch->flush();
   CHECK(t.same());
   CHECK(t.box.getLastCommittedIndex() == 11);
+}
+
+// The node's groups over three engines in one process (ShardedGroupBatch, r06): every group's
+// commits against its oracle BallotBox after each concurrent flush of the shards, and the
+// published node-wide snapshot (device copies: RCCL refuses three engines on one GPU) equal to
+// every group's getLastCommittedIndex.
+static void testShardedBatchOnGpu(Engine& eng) {
+  Engine e1(0, 1u << 12, 16), e2(0, 1u << 12, 16);
+  const uint32_t G = 1001, P = 5;
+  ShardedGroupBatch sb({&eng, &e1, &e2}, G, P);
+  CHECK(sb.shards() == 3 && sb.groupsPerShard() == 334);
+  CHECK(!sb.rcclInitAll());  // one GPU (or the test double): copies
+  std::vector<Twin> tw;
+  tw.reserve(G);
+  for (uint32_t g = 0; g < G; ++g) {
+    uint32_t l = 0;
+    tw.emplace_back(sb.shardOf(g, &l), l);
+  }
+  std::mt19937_64 rng(91);
+  const std::vector<int32_t> c5 = {1, 2, 3, 4, 5};
+  for (uint32_t g = 0; g < G; ++g) {
+    const int64_t pi = 1 + static_cast<int64_t>(rng() % 1000);
+    CHECK(tw[g].box.resetPendingIndex(pi) && jo_bb_reset_pending_index(tw[g].bb, pi) == JO_TRUE);
+  }
+  std::vector<std::array<int64_t, 5>> m(G);
+  for (uint32_t g = 0; g < G; ++g) m[g].fill(tw[g].box.getPendingIndex() - 1);
+  std::vector<int64_t> snap(G);
+  for (int epoch = 0; epoch < 4; ++epoch) {
+    for (uint32_t g = 0; g < G; ++g) {
+      CHECK(tw[g].append(c5, nullptr, 1 + static_cast<int64_t>(rng() % 20)));
+      const int64_t la = tw[g].box.getPendingIndex() + tw[g].box.getPendingMetaQueueSize() - 1;
+      for (int p = 0; p < 5; ++p) {
+        const int64_t to = std::min(la, m[g][p] + static_cast<int64_t>(rng() % 25));
+        if (to > m[g][p]) {
+          tw[g].ack(m[g][p] + 1, to, p + 1);
+          m[g][p] = to;
+        }
+      }
+    }
+    sb.flush();
+    sb.publish();
+    for (uint32_t g = 0; g < G; ++g) CHECK(tw[g].same());
+    for (uint32_t i = 0; i < sb.shards(); ++i) {
+      sb.readSnapshot(i, snap.data());
+      for (uint32_t g = 0; g < G; ++g) CHECK(snap[g] == tw[g].box.getLastCommittedIndex());
+    }
+  }
+  CHECK(!sb.publishedOverRccl());
 }
 
 // Random call sequences (appends under stable and joint confs, conf changes that replace
@@ -1355,6 +1404,7 @@ int main(int argc, char** argv) {
     tests.push_back({"testLeaderTickerOnGpu", [&] { testLeaderTickerOnGpu(e); }});
     tests.push_back({"testReadIndexRounds", [&] { testReadIndexRounds(e); }});
     tests.push_back({"testResetStampKeepsLiveAcks", [&] { testResetStampKeepsLiveAcks(e); }});
+    tests.push_back({"testShardedBatchOnGpu", [&] { testShardedBatchOnGpu(e); }});
     tests.push_back({"testFSMCallerBatchOnGpu", [&] { testFSMCallerBatchOnGpu(e); }});
   }
   for (auto& t : tests) {

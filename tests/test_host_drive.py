@@ -39,19 +39,23 @@ def _expected_counts(s, committed):
     return recs, changed
 
 
-@pytest.mark.parametrize("G,K,joint,active,threads", [(20000, 5, 0.05, 0.5, 1),
-                                                      (4096, 4, 0.3, 1.0, 1),
-                                                      (50000, 4, 0.1, 0.8, 16)])
-def test_host_mirror_drives_series(engine, oracle, G, K, joint, active, threads):
+@pytest.mark.parametrize("G,K,joint,active,threads,shards", [(20000, 5, 0.05, 0.5, 1, 1),
+                                                             (4096, 4, 0.3, 1.0, 1, 1),
+                                                             (50000, 4, 0.1, 0.8, 16, 1),
+                                                             (50000, 4, 0.1, 0.8, 16, 2),
+                                                             (4099, 4, 0.3, 1.0, 3, 3)])
+def test_host_mirror_drives_series(engine, oracle, G, K, joint, active, threads, shards):
     """threads = 16: each epoch's calls come from 16 threads at once (group slices); the
-    flush packs and delivers on its own worker threads (> 8192 changed groups)."""
+    flush packs and delivers on its own worker threads (> 8192 changed groups).  shards > 1:
+    the groups over that many engines in this process (ShardedGroupBatch, the last block
+    ragged), committed read back from the published node-wide snapshot."""
     import torch
     from conftest import assert_unregistered, device_checkpoint
 
     from jraft_amd import drive
     s = W.host_series("C3", K, groups=G, joint_frac=joint, active=active)
     assert_unregistered(s, "before drive_epochs")
-    committed, st = drive.drive_epochs(0, s, threads=threads)
+    committed, st = drive.drive_epochs(0, s, threads=threads, shards=shards)
     # (round 3 saw one "illegal memory access" in this test: the checkpoints name the step)
     device_checkpoint("after drive_epochs (the mirror's flushes, its engine destroyed)")
     assert_unregistered(s, "after drive_epochs")
@@ -96,7 +100,8 @@ def test_host_mirror_drives_series(engine, oracle, G, K, joint, active, threads)
     np.testing.assert_array_equal(st["changed"], changed)
     assert st["states"][0] == G and (st["states"][1:] == 0).all()
     np.testing.assert_array_equal(st["h2d_bytes"], st["states"] * 96 + st["records"] * 8)
-    np.testing.assert_array_equal(st["d2h_bytes"], 4 + st["changed"] * 8)  # the list's total + entries
+    # each shard's list total + the entries
+    np.testing.assert_array_equal(st["d2h_bytes"], 4 * shards + st["changed"] * 8)
 
 
 def test_flusher_latency_small():
