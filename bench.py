@@ -703,9 +703,9 @@ def leg_table(ctx, args, G, pair_ms):
                                          s["run_start"][idx], s["run_conf"][idx], chunk=1024)
         ok = ok and bool(np.array_equal(got[sub], ce))
     # per group: u32 match words 4P + pendingIndex, lastAppended, lastCommitted, conf 32 read;
-    # per committing group lastCommitted 8 + list delta 4 written; per 256-group slice its
-    # 32-B map and 4-B count (the flagged groups' run words, ~1 %, not counted)
-    alg = G * (4 * P + 32) + n_changed * 12 + ((G + 255) // 256) * 36
+    # per committing group lastCommitted 8 + list delta 4 written; per 128-group slice its
+    # 16-B map and 4-B count (the flagged groups' run words, ~1 %, not counted)
+    alg = G * (4 * P + 32) + n_changed * 12 + ((G + 127) // 128) * 20
     for t in pristine + plain + work:
         t.close()
     return {"workload": f"C3 resident table: {G} groups x {P} peers, joint, 1% with a conf "
@@ -725,7 +725,7 @@ def leg_table(ctx, args, G, pair_ms):
             "roofline": roofline(alg, t_ms, kernel="table_epoch_kernel<5>",
                                  bytes_note="reads 4P+32 B per group (u32 match words), writes "
                                             "lastCommitted + list delta 12 B per committing group "
-                                            "+ 36 B per 256-group slice",
+                                            "+ 20 B per 128-group slice",
                                  **pmc_traffic("table", "table_epoch_kernel<5>"))}
 
 
