@@ -1721,8 +1721,10 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   // `invalid`.  Epoch waves decide 128 groups (half a tile); the grid is whole workgroups of
   // kTableBlockWaves waves, and every wave of it reads its tile and its slots: tiles and slots
   // are allocated for the whole grid
-  const uint64_t waves = ((G + jrq::kListSlice - 1) / jrq::kListSlice + jrq::kTableBlockWaves - 1) /
-                         jrq::kTableBlockWaves * jrq::kTableBlockWaves;
+  // (units of 128 groups, allocated for whole workgroups of two units per wave, which covers
+  // the one-unit grid too)
+  const uint64_t kUnitAlign = 2 * jrq::kTableBlockWaves;
+  const uint64_t waves = ((G + jrq::kListSlice - 1) / jrq::kListSlice + kUnitAlign - 1) / kUnitAlign * kUnitAlign;
   const uint64_t tiles = (waves + 1) / 2;
   const uint64_t flag_words = waves * jrq::kFlagSlots * 8 + (waves + 1) / 2;
   const uint64_t ts = static_cast<uint64_t>(P) * (jrq::kTableSlice / 2) + 4 * jrq::kTableSlice;  // words per tile

@@ -195,31 +195,49 @@ __device__ __forceinline__ void map_words(int64_t pi, int64_t la, const uint32_t
 // every wave's loads), later ones by their owners.  Groups outside rel_domain (negative or huge
 // indexes; never a real group) are decided again with 64-bit arithmetic from reloaded words in
 // a wave-uniform branch.  No barrier beyond the wave's own, no atomics.
+#ifndef JRQ_TABLE_LAZY_ENT  // (r06 A/B knob) flagged-entry words read where the walk uses them
+#define JRQ_TABLE_LAZY_ENT 0
+#endif
+#ifndef JRQ_TABLE_ENT_LDS  // flagged-entry slots per unit loaded up front (4: lanes 32-63 repeat)
+#define JRQ_TABLE_ENT_LDS 4
+#endif
+constexpr uint32_t kEntLds = JRQ_TABLE_ENT_LDS;
+
+// One unit's loads (128 groups, half a tile; the unit's list slice and flagged-entry slots are
+// its own): every int64 stream of the lane's pair with one 16-B load (1 KiB per wave
+// instruction), every u32 match row with one 8-B load (512 B), and the lane's word of the unit's
+// first kEntLds flagged-entry slots (64 B each; lanes 32-63 read lanes 0-31's words again: no
+// branch, no extra line).  `u` is wave-uniform.
 template <int P>
-__global__ __launch_bounds__(kTableEpochBlock, P <= 5 ? JRQ_TABLE_OCC : (P <= 10 ? 4 : 2)) JRQ_SGPRS_8WAVES
-void table_epoch_kernel(JrqTableArgs t) {
-  constexpr uint32_t kWaves = kTableEpochBlock / 64;
-  constexpr uint32_t kEntLds = 4;  // flagged-entry slots per wave loaded up front
-  __shared__ int64_t entl[kWaves][kEntLds][8];
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  const uint64_t below = (1ull << lane) - 1ull;
-  const uint32_t wid = blockIdx.x * kWaves + w;
-  const uint32_t half = wid & 1u;
-  const uint32_t g0 = wid * kListSlice + 2u * lane;  // this lane's pair (g0, g0 + 1)
-  int64_t* const tile = reinterpret_cast<int64_t*>(t.match) + static_cast<size_t>(__builtin_amdgcn_readfirstlane(wid >> 1)) * t.ts;
-  const int64_t* const ent = reinterpret_cast<const int64_t*>(t.flag_ent) + static_cast<size_t>(wid) * kFlagSlots * 8;
-  // the first kEntLds slots (64 B each): one 8-B word per lane (lanes 32-63 read lanes 0-31's
-  // words again: no branch, no extra line), parked in LDS once it lands
-  const int64_t ev = __builtin_nontemporal_load(ent + (lane & (8 * kEntLds - 1)));
-  const uint32_t go = 16u * lane + 1024u * half;  // the pair's byte offset in a 2-KiB int64 row
-  const i64x2 pr = tld2o(tile + 128 * P, go);
-  const i64x2 la = tld2o(tile + 128 * P + 256, go);
-  const i64x2 lc = tld2o(tile + 128 * P + 512, go);
-  const i64x2 cw = tld2o(tile + 128 * P + 768, go);
+struct UnitIn {
+  int64_t ev;
+  i64x2 pr, la, lc, cw;
   u32x2 mq[P];
+};
+
+template <int P>
+__device__ __forceinline__ void unit_load(const JrqTableArgs& t, uint32_t u, uint32_t lane, UnitIn<P>& in) {
+  const int64_t* const tile = reinterpret_cast<const int64_t*>(t.match) + static_cast<size_t>(u >> 1) * t.ts;
+  const int64_t* const ent = reinterpret_cast<const int64_t*>(t.flag_ent) + static_cast<size_t>(u) * kFlagSlots * 8;
+  in.ev = __builtin_nontemporal_load(ent + (lane & (8 * kEntLds - 1)));
+  const uint32_t go = 16u * lane + 1024u * (u & 1u);  // the pair's byte offset in a 2-KiB int64 row
+  in.pr = tld2o(tile + 128 * P, go);
+  in.la = tld2o(tile + 128 * P + 256, go);
+  in.lc = tld2o(tile + 128 * P + 512, go);
+  in.cw = tld2o(tile + 128 * P + 768, go);
 #pragma unroll
-  for (int p = 0; p < P; ++p) mq[p] = tld2u(tile + 128 * p, 8u * lane + 512u * half);
-  if (lane < 8 * kEntLds) entl[w][lane >> 3][lane & 7u] = ev;
+  for (int p = 0; p < P; ++p) in.mq[p] = tld2u(tile + 128 * p, 8u * lane + 512u * (u & 1u));
+}
+
+// The unit's decisions and writes, from its loads.
+template <int P>
+__device__ __forceinline__ void unit_decide(const JrqTableArgs& t, uint32_t u, uint32_t lane,
+                                            int64_t (&entw)[kEntLds][8], const UnitIn<P>& ui) {
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint32_t g0 = u * kListSlice + 2u * lane;  // this lane's pair (g0, g0 + 1)
+  int64_t* const tile = reinterpret_cast<int64_t*>(t.match) + static_cast<size_t>(u >> 1) * t.ts;
+  const int64_t* const ent = reinterpret_cast<const int64_t*>(t.flag_ent) + static_cast<size_t>(u) * kFlagSlots * 8;
+  if (lane < 8 * kEntLds) entw[lane >> 3][lane & 7u] = ui.ev;
   bool f[2], c[2], x[2], wpi[2];
   uint32_t d[2], st[2], rk[2];
   int64_t outv[2], pir[2];
@@ -227,8 +245,8 @@ void table_epoch_kernel(JrqTableArgs t) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const uint32_t g = g0 + j;
-    const int64_t prk = j ? pr.y : pr.x, lck = j ? lc.y : lc.x, lak = j ? la.y : la.x;
-    const uint64_t cwk = static_cast<uint64_t>(j ? cw.y : cw.x);
+    const int64_t prk = j ? ui.pr.y : ui.pr.x, lck = j ? ui.lc.y : ui.lc.x, lak = j ? ui.la.y : ui.la.x;
+    const uint64_t cwk = static_cast<uint64_t>(j ? ui.cw.y : ui.cw.x);
     const bool in = g < t.G;
     f[j] = in && (cwk >> 63);
     bf[j] = __ballot(f[j]);
@@ -236,7 +254,7 @@ void table_epoch_kernel(JrqTableArgs t) {
     const int64_t pi = prk == kPiFollowsLc ? lck + 1 : prk;
     uint32_t s[P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) s[p] = j ? mq[p].y : mq[p].x;
+    for (int p = 0; p < P; ++p) s[p] = j ? ui.mq[p].y : ui.mq[p].x;
     RelGroup<P> rg;
     map_words<P>(pi, lak, s, rg);
     uint8_t s8;
@@ -252,16 +270,26 @@ void table_epoch_kernel(JrqTableArgs t) {
     // from the same relative words, the runs from its flagged-entry slot (LDS for the first
     // kEntLds of the wave, memory beyond)
     if (__builtin_expect(bf[j] != 0, 0)) {  // (wave-uniform)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the parked entries are read by other lanes: LDS operations of one wave complete in
+      // issue order, so only the compiler's order is needed (a fence here made the waitcnt
+      // pass drain every load in flight, the next unit's among them, at the join below)
+      asm volatile("" ::: "memory");
       if (f[j] && !x[j]) {
         uint32_t k = rk[j];
         asm volatile("" : "+v"(k));
+#if JRQ_TABLE_LAZY_ENT
+        // the slot's words read where they are used (LDS for the first kEntLds slots, memory
+        // beyond): no array of them live across the walk (register pressure sets occupancy)
+        const int64_t* const eg = ent + static_cast<size_t>(k) * 8;
+        const bool inl = k < kEntLds;
+        const uint32_t kl = inl ? k : 0u;
+        auto est = [&](uint32_t q) -> int64_t { return inl ? entw[kl][q] : eg[q]; };
+        auto ecf = [&](uint32_t q) -> uint64_t { return static_cast<uint64_t>(inl ? entw[kl][4 + q] : eg[4 + q]); };
+#else
         int64_t es[kTableMaxRuns];
         uint64_t ec[kTableMaxRuns];
         if (k < kEntLds) {
-          const int64_t* e = entl[w][k];
+          const int64_t* e = entw[k];
 #pragma unroll
           for (int q = 1; q < kTableMaxRuns; ++q) es[q] = e[q];
 #pragma unroll
@@ -272,13 +300,20 @@ void table_epoch_kernel(JrqTableArgs t) {
           for (int q = 1; q < kTableMaxRuns; ++q) es[q] = e[q];
 #pragma unroll
           for (int q = 1; q < kTableMaxRuns; ++q) ec[q] = static_cast<uint64_t>(e[4 + q]);
+          // settled here (a rare branch): a load still pending where it joins the common path
+          // made the waitcnt pass drain every load in flight there -- the next unit's too
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         }
+        auto est = [&](uint32_t q) -> int64_t { return es[q]; };
+        auto ecf = [&](uint32_t q) -> uint64_t { return ec[q]; };
+#endif
         uint8_t sw = rg.st;
         int64_t best = kI64Min;
         if (pi != 0) {
           {  // run 0, [pi, start1 - 1] under the group's conf word: its bound is r, the
              // single-conf decision's (the same q-th largests), so no sort of its own
-            const int64_t e = es[1] == kI64Max ? lak : es[1] - 1;
+            const int64_t s1 = est(1);
+            const int64_t e = s1 == kI64Max ? lak : s1 - 1;
             const int64_t ee = e < lak ? e : lak;
             if (ee >= pi) {
               if ((cwk & 0xFFFFu) == 0) sw |= kStEmptyConf;
@@ -289,12 +324,13 @@ void table_epoch_kernel(JrqTableArgs t) {
           }
 #pragma unroll
           for (uint32_t q = 1; q < kTableMaxRuns; ++q) {
-            if (es[q] == kI64Max) break;  // unused runs (they come last)
-            const int64_t nx = q + 1 < kTableMaxRuns ? es[q + 1] : kI64Max;
-            const int64_t sr = es[q] > pi ? es[q] : pi;
+            const int64_t sq = est(q);
+            if (sq == kI64Max) break;  // unused runs (they come last)
+            const int64_t nx = q + 1 < kTableMaxRuns ? est(q + 1) : kI64Max;
+            const int64_t sr = sq > pi ? sq : pi;
             const int64_t e = nx == kI64Max ? lak : nx - 1;
             const int64_t ee = e < lak ? e : lak;
-            const int64_t cand = run_candidate_rel<P>(rg, ec[q], pi, sr, ee, sw);
+            const int64_t cand = run_candidate_rel<P>(rg, ecf(q), pi, sr, ee, sw);
             best = cand > best ? cand : best;
           }
         }
@@ -354,7 +390,7 @@ void table_epoch_kernel(JrqTableArgs t) {
     // the pair's row offset again, from the lane id (mbcnt) and the wave's half (an SGPR):
     // recomputed, not kept live across the decisions (it was spilled and reloaded per store)
     const uint32_t go = 16u * __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) +
-                        1024u * (__builtin_amdgcn_readfirstlane(wid) & 1u);
+                        1024u * (u & 1u);
 #if JRQ_TABLE_AB_LC != 1
     if (c[0] && c[1]) {
       i64x2 v;
@@ -387,8 +423,8 @@ void table_epoch_kernel(JrqTableArgs t) {
   const uint32_t cnt = __popcll(b0) + __popcll(b1);
   // (a wave past the table's last slice -- the grid is whole workgroups -- owns no slice: the
   // caller's list has room for jrq_table_slices(t) slices only)
-  const bool owns = static_cast<uint64_t>(wid) * kListSlice < t.G;
-  uint64_t* const slice = t.changed + static_cast<size_t>(wid) * kListSlice;
+  const bool owns = static_cast<uint64_t>(u) * kListSlice < t.G;
+  uint64_t* const slice = t.changed + static_cast<size_t>(u) * kListSlice;
 #if !JRQ_TABLE_AB_NOLIST  // (diagnosis knob: no list)
   if (lane < kSliceMapWords && owns) {
     const uint32_t sh = lane * 32u;
@@ -403,7 +439,35 @@ void table_epoch_kernel(JrqTableArgs t) {
     if (c[1]) deltas[at + (c[0] ? 1u : 0u)] = d[1];
   }
 #endif
-  if (lane == 0 && owns) t.n_changed[wid] = cnt;
+  if (lane == 0 && owns) t.n_changed[u] = cnt;
+}
+
+
+// JRQ_TABLE_UNITS (r06 A/B knob): units per wave.  1: one wave per unit (8192 waves for 1M
+// groups, JRQ_TABLE_OCC per SIMD).  2: one wave per tile, both halves' loads issued before the
+// first half's decisions, so a wave decides one unit while the other's loads are in flight.
+#ifndef JRQ_TABLE_UNITS
+#define JRQ_TABLE_UNITS 1
+#endif
+template <int P>
+__global__ __launch_bounds__(kTableEpochBlock, JRQ_TABLE_UNITS == 2 ? 4 : (P <= 5 ? JRQ_TABLE_OCC : (P <= 10 ? 4 : 2)))
+JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
+  constexpr uint32_t kWaves = kTableEpochBlock / 64;
+  __shared__ int64_t entl[kWaves][kEntLds][8];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + w);
+#if JRQ_TABLE_UNITS == 2
+  UnitIn<P> a, b;
+  unit_load<P>(t, 2u * wid, lane, a);
+  unit_load<P>(t, 2u * wid + 1u, lane, b);
+  unit_decide<P>(t, 2u * wid, lane, entl[w], a);
+  asm volatile("" ::: "memory");  // (the first unit's LDS reads before the second's parking)
+  unit_decide<P>(t, 2u * wid + 1u, lane, entl[w], b);
+#else
+  UnitIn<P> a;
+  unit_load<P>(t, wid, lane, a);
+  unit_decide<P>(t, wid, lane, entl[w], a);
+#endif
 }
 
 // Host variant of the epoch: the slices' counts scanned into offsets (one workgroup; a
@@ -672,7 +736,8 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_lis
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_epoch(
     const JrqTableArgs* a, hipStream_t stream) {
-  const uint32_t waves = (a->G + jrq::kListSlice - 1) / jrq::kListSlice;
+  const uint32_t units = (a->G + jrq::kListSlice - 1) / jrq::kListSlice;
+  const uint32_t waves = (units + JRQ_TABLE_UNITS - 1) / JRQ_TABLE_UNITS;
   const dim3 grid((waves + jrq::kTableEpochBlock / 64 - 1) / (jrq::kTableEpochBlock / 64)), blk(jrq::kTableEpochBlock);
   switch (a->P) {
 #define JRQ_CASE(P)                                                                   \

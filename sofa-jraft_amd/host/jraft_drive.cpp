@@ -28,6 +28,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -172,11 +173,17 @@ int jraft_drive_epochs_sharded(int device, uint32_t shards, uint32_t G, uint32_t
     std::unique_ptr<jraft::ShardedGroupBatch> sharded;
     std::vector<jraft::BallotBox> boxes;
     boxes.reserve(G);
+    // (JRAFT_DRIVE_FLUSH_THREADS: the flush pool's size, for tools/drive_ab.py; unset: the
+    // batch's default)
+    const char* ft = std::getenv("JRAFT_DRIVE_FLUSH_THREADS");
+    const unsigned fthreads = ft ? static_cast<unsigned>(std::atoi(ft)) : 0u;
     if (S == 1) {
       batch = std::make_shared<jraft::GroupBatch>(ep[0], G, P);
+      if (fthreads) batch->setFlushThreads(fthreads);
       for (uint32_t g = 0; g < G; ++g) boxes.emplace_back(batch, g);
     } else {
       sharded.reset(new jraft::ShardedGroupBatch(ep, G, P));
+      if (fthreads) sharded->setFlushThreads(fthreads);
       sharded->rcclInitAll();  // one device: refused, copies
       for (uint32_t g = 0; g < G; ++g) boxes.push_back(sharded->box(g));
     }
@@ -192,6 +199,13 @@ int jraft_drive_epochs_sharded(int device, uint32_t shards, uint32_t G, uint32_t
     // the callers' own state, group-major (a Replicator keeps its peer's matchIndex; here one
     // row per group of the P peers' acks per epoch and of their previous acks), laid out before
     // the timed calls so that the timing is the API's, not a strided walk of the input series
+    // (each group's Configurations resolved once: a NodeImpl holds its conf, it does not look it
+    // up per task)
+    std::vector<const Confs*> ca(G), cb(G, nullptr);
+    for (uint32_t g = 0; g < G; ++g) {
+      ca[g] = &confs.at(conf_a[g]);
+      if (switch_at && switch_at[g] > 0) cb[g] = &confs.at(conf_b[g]);
+    }
     std::vector<int64_t> prev(static_cast<size_t>(P) * G, 0);
     std::vector<int64_t> acks(static_cast<size_t>(K) * G * P);
     for (uint32_t k = 0; k < K; ++k)
@@ -201,18 +215,18 @@ int jraft_drive_epochs_sharded(int device, uint32_t shards, uint32_t G, uint32_t
     auto append = [&](uint32_t g, int64_t from, int64_t to) -> uint64_t {  // entries [from, to]
       uint64_t calls = 0;
       const int64_t sw = switch_at ? switch_at[g] : 0;
-      auto run = [&](uint64_t cw, int64_t a, int64_t b) {
+      auto run = [&](const Confs* cp, int64_t a, int64_t b) {
         if (b < a) return;
-        const Confs& c = confs.at(cw);
+        const Confs& c = *cp;
         if (!boxes[g].appendPendingTasks(c.cur, c.hasOld ? &c.old : nullptr, b - a + 1))
           throw std::runtime_error("appendPendingTasks refused");
         ++calls;
       };
       if (sw > 0) {
-        run(conf_a[g], from, std::min(to, sw - 1));
-        run(conf_b[g], std::max(from, sw), to);
+        run(ca[g], from, std::min(to, sw - 1));
+        run(cb[g], std::max(from, sw), to);
       } else {
-        run(conf_a[g], from, to);
+        run(ca[g], from, to);
       }
       return calls;
     };

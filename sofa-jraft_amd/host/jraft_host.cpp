@@ -818,6 +818,9 @@ void GroupBatch::dropDeadRuns(uint32_t g) {
 #ifndef JRAFT_PACK_AHEAD
 #define JRAFT_PACK_AHEAD 4
 #endif
+#ifndef JRAFT_DELIVER_AHEAD
+#define JRAFT_DELIVER_AHEAD 8
+#endif
 #ifndef JRAFT_PREFETCH_LINES
 #define JRAFT_PREFETCH_LINES 1
 #endif
@@ -1131,7 +1134,7 @@ uint32_t GroupBatch::flushLocked() {
     D.commits.clear();
     D.done.clear();
     D.ndone.clear();
-    constexpr size_t kAhead = 8;
+    constexpr size_t kAhead = JRAFT_DELIVER_AHEAD;
     for (size_t i = i0; i < i1; ++i) {
       if (i + kAhead < i1) {
         const uint32_t a = static_cast<uint32_t>(changed_.p[i + kAhead]);

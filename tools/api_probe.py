@@ -58,11 +58,10 @@ def main():
     K, P, G = s["match"].shape
     arrs = {k: np.ascontiguousarray(s[k]) for k in ("pending_index", "last_committed", "conf_a",
                                                     "conf_b", "switch_at", "last_appended", "match")}
-    names = ("api_ms", "pack_ms", "device_ms", "deliver_ms", "flush_ms", "h2d", "d2h", "states",
-             "records", "changed", "calls")
+    from jraft_amd.drive import STATS as names
     for T in [int(x) for x in a.threads.split(",")]:
         out = np.zeros((K, G), np.int64)
-        st = np.zeros((K, 11), np.float64)
+        st = np.zeros((K, len(names)), np.float64)
         p = lambda x: C.c_void_p(x.ctypes.data)  # noqa: E731
         rc = d.jraft_drive_epochs(0, G, P, K, T, p(arrs["pending_index"]), p(arrs["last_committed"]),
                                   p(arrs["conf_a"]), p(arrs["conf_b"]), p(arrs["switch_at"]),
@@ -71,8 +70,8 @@ def main():
             raise SystemExit(d.jraft_drive_last_error().decode())
         m = st[1:].mean(axis=0)
         r = dict(zip(names, m))
-        print(f"threads {T}: api {r['api_ms']:.2f} ms ({r['calls'] / 1e6:.2f}M calls, "
-              f"{r['api_ms'] * 1e6 * T / r['calls']:.1f} ns/call/thread), pack {r['pack_ms']:.2f} ms, "
+        print(f"threads {T}: api {r['api_ms']:.2f} ms ({r['api_calls'] / 1e6:.2f}M calls, "
+              f"{r['api_ms'] * 1e6 * T / r['api_calls']:.1f} ns/call/thread), pack {r['pack_ms']:.2f} ms, "
               f"fake device {r['device_ms']:.2f} ms, deliver {r['deliver_ms']:.2f} ms, "
               f"changed {r['changed']:.0f}; first epoch api {st[0, 0]:.1f} ms flush {st[0, 4]:.1f} ms",
               flush=True)

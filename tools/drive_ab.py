@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Alternating A/B of host-mirror builds on the GPU box: the C3 drive series (bench.py leg
+`drive`) through each variant's libjraft_drive.so (tools/host_ab_build.sh), round-robin in one
+process, `--rounds` times; per variant the median over every steady epoch of api / pack / device /
+deliver / flush ms, and whether the commits equal the first variant's.  Not part of any product path.
+
+    python tools/drive_ab.py NAME=ab/NAME/libjraft_drive.so ... [--rounds 5] [--epochs 10]
+        [--flush-threads 16,8]   (each variant once per flush-pool size: NAME@16, NAME@8)
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sofa-jraft_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--epochs", type=int, default=10)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--groups", type=int, default=1 << 20)
+    ap.add_argument("--active", type=float, default=1.0)
+    ap.add_argument("--flush-threads", default="", help="comma list of flush-pool sizes to alternate")
+    a = ap.parse_args()
+    from jraft_amd import _lib, drive
+    from jraft_amd import workloads as W
+    _lib.load()
+    libs = {}
+    for v in a.variants:
+        name, path = v.split("=", 1)
+        d = C.CDLL(os.path.abspath(path))
+        d.jraft_drive_last_error.restype = C.c_char_p
+        d.jraft_drive_epochs.restype = C.c_int
+        d.jraft_drive_epochs.argtypes = [C.c_int] + [C.c_uint32] * 4 + [C.c_void_p] * 9
+        for ft in (a.flush_threads.split(",") if a.flush_threads else [""]):
+            libs[f"{name}@{ft}" if ft else name] = (d, ft)
+    s = W.host_series("C3", a.epochs, groups=a.groups, joint_frac=0.01, active=a.active)
+    K, P, G = s["match"].shape
+    arrs = {k: np.ascontiguousarray(s[k]) for k in ("pending_index", "last_committed", "conf_a",
+                                                    "conf_b", "switch_at", "last_appended", "match")}
+    p = lambda x: C.c_void_p(x.ctypes.data)  # noqa: E731
+    per = {n: [] for n in libs}
+    ref, same = None, {n: True for n in libs}
+    for r in range(a.rounds):
+        for n, (d, ft) in libs.items():
+            if ft:
+                os.environ["JRAFT_DRIVE_FLUSH_THREADS"] = ft
+            else:
+                os.environ.pop("JRAFT_DRIVE_FLUSH_THREADS", None)
+            out = np.zeros((K, G), np.int64)
+            st = np.zeros((K, len(drive.STATS)), np.float64)
+            rc = d.jraft_drive_epochs(0, G, P, K, a.threads, p(arrs["pending_index"]), p(arrs["last_committed"]),
+                                      p(arrs["conf_a"]), p(arrs["conf_b"]), p(arrs["switch_at"]),
+                                      p(arrs["last_appended"]), p(arrs["match"]), p(out), p(st))
+            if rc:
+                raise SystemExit(f"{n}: " + d.jraft_drive_last_error().decode())
+            if ref is None:
+                ref = out
+            same[n] = same[n] and bool(np.array_equal(out, ref))
+            per[n].append(st[1:])
+            print(f"round {r} {n}: flush {np.median(st[1:, 4]):.2f} deliver {np.median(st[1:, 3]):.2f} "
+                  f"api {np.median(st[1:, 0]):.2f}", flush=True)
+    res = {}
+    for n, L in per.items():
+        m = np.concatenate(L)
+        res[n] = {k: round(float(np.median(m[:, i])), 3) for i, k in enumerate(drive.STATS)
+                  if k in ("api_ms", "pack_ms", "device_ms", "deliver_ms", "flush_ms")}
+        res[n]["same_commits"] = same[n]
+    print(json.dumps({"threads": a.threads, "groups": G, "epochs": K, "rounds": a.rounds,
+                      "active": a.active, "median_ms": res}))
+
+
+if __name__ == "__main__":
+    main()
