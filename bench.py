@@ -589,6 +589,77 @@ def table_load(table, s):
     return st, recs
 
 
+def leg_table_fanout(ctx, series, pristine, work, lists, series_ms, G, NB, t_ms, alg):
+    """The commit fan-out fused into the table epoch (jrq_table_epoch_fanout_dev: FSMCallerImpl
+    .doCommitted / ClosureQueueImpl.popClosureUntil of every committing group, FSMCallerImpl.java:
+    462-482, ClosureQueueImpl.java:113-142) against the same epoch followed by the separate
+    fan-out over dense arrays (jrq_table_committed_dev + jrq_commit_fanout_dev), same timing.
+    Each group's FSMCaller is caught up (lastAppliedIndex = lastCommittedIndex) with one closure
+    per pending entry (NodeImpl.executeApplyingTasks appends one per task), so every committing
+    group pops."""
+    import torch
+
+    from jraft_amd import decode_changed
+    eng, dev = ctx.eng, ctx.dev
+    fsm = []
+    for i, t in enumerate(pristine):
+        s = series[i]
+        lc0 = s["last_committed"].astype(np.int64)
+        la0 = s["last_appended"][0].astype(np.int64)
+        fsm.append((lc0.copy(), lc0 + 1, np.maximum(la0 - lc0, 0)))
+        t.fsm_update(np.arange(G, dtype=np.uint32), *fsm[-1])
+    fans = [w.fan_buffers(dev) for w in work]
+
+    def fused(i):
+        work[i].epoch_fanout_dev(*lists[i], *fans[i])
+    f_ms = series_ms(pristine, fused)
+    fw = [work[i].gather_dev_list(*lists[i]) for i in range(NB)]
+    fn = [host_np(lists[i][1]) for i in range(NB)]
+    ff = [host_np(fans[i][0]) for i in range(NB)]
+    fs = [host_np(fans[i][1]) for i in range(NB)]
+    fq = [work[i].fsm_read() for i in range(NB)]
+    prev = [to_dev(series[i]["last_committed"].astype(np.int64), dev) for i in range(NB)]
+    appl = [to_dev(fsm[i][0], dev) for i in range(NB)]
+    cq0 = [(to_dev(fsm[i][1], dev), to_dev(fsm[i][2], dev)) for i in range(NB)]
+    cq = [(torch.empty_like(a), torch.empty_like(b)) for a, b in cq0]
+    com = [torch.empty(G, dtype=torch.int64, device=dev) for _ in range(NB)]
+    ufc = [torch.empty(G, dtype=torch.int64, device=dev) for _ in range(NB)]
+    ust = [torch.empty(G, dtype=torch.uint8, device=dev) for _ in range(NB)]
+    ubm = torch.empty((G + 63) // 64, dtype=torch.int64, device=dev)
+    unum = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def restore():
+        for (a, b), (a0, b0) in zip(cq, cq0):
+            a.copy_(a0)
+            b.copy_(b0)
+
+    def unfused(i):
+        work[i].epoch_dev(*lists[i])
+        work[i].committed_dev(com[i])
+        eng.commit_fanout_dev(prev[i], com[i], appl[i], cq[i][0], cq[i][1], ufc[i], ust[i], ubm, unum)
+    u_ms = series_ms(pristine, unfused, restore)
+    ok = True
+    for i in range(NB):  # fused == epoch + separate fan-out, every group of every table
+        g, _ = decode_changed(fw[i])
+        ffl = np.concatenate([ff[i][k * 128: k * 128 + fn[i][k]] for k in range(len(fn[i]))])
+        fsl = np.concatenate([fs[i][k * 128: k * 128 + fn[i][k]] for k in range(len(fn[i]))])
+        st_u, fc_u = host_np(ust[i]), host_np(ufc[i])
+        ok = ok and bool(np.array_equal(fsl, st_u[g]) and np.array_equal(ffl, fc_u[g]))
+        ok = ok and bool(np.count_nonzero(st_u) == len(g))
+        ok = ok and bool(np.array_equal(fq[i][1], host_np(cq[i][0])) and np.array_equal(fq[i][2], host_np(cq[i][1])))
+    n_changed = len(fw[-1])
+    # the fused epoch reads the FSMCaller rows (24 B per group) and writes per committing group
+    # its fan result (9 B) and the popped queue (16 B)
+    falg = alg + G * 24 + n_changed * 25
+    return {"kernel_ms": f_ms, "epoch_then_fanout_ms": u_ms, "epoch_alone_ms": t_ms,
+            "fused_over_epoch_alone": f_ms / t_ms, "fused_over_unfused": f_ms / u_ms,
+            "bit_exact_vs_epoch_then_fanout": ok,
+            "roofline": roofline(falg, f_ms, kernel="table_epoch_kernel<5, true>",
+                                 bytes_note="the epoch's bytes + 24 B of FSMCaller state read per "
+                                            "group + 25 B per committing group (fan result, "
+                                            "popped queue)")}
+
+
 def leg_table(ctx, args, G, pair_ms):
     """The drop-in path's device cost: one epoch of the resident group table (csrc/table.hip)
     over C3 (1M groups x 5 peers, joint) with 1% of the groups holding a conf change inside
@@ -622,20 +693,26 @@ def leg_table(ctx, args, G, pair_ms):
     lists = [w.list_buffers(dev) for w in work]
     reps = max(3, args.steps // 4)
 
-    def series_ms(src, launch):
+    def series_ms(src, launch, restore=None):
         """median over reps of (event pair around NB back-to-back launches) / NB"""
         for w, t in zip(work, src):
             w.copy_from(t)
+        if restore:
+            restore()
         def warm(i):  # untimed series, each from fresh tables too
             if i % NB == 0:
                 for w, t in zip(work, src):
                     w.copy_from(t)
+                if restore:
+                    restore()
             launch(i % NB)
         warm_until(warm, ctx.stream, ctx.sync, warm_ms=WARM_MS / 4)
         out = []
         for _ in range(reps):
             for w, t in zip(work, src):
                 w.copy_from(t)
+            if restore:
+                restore()
             a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             mark(ctx.stream)
             a.record(ctx.stream)
@@ -706,6 +783,7 @@ def leg_table(ctx, args, G, pair_ms):
     # per committing group lastCommitted 8 + list delta 4 written; per 128-group slice its
     # 16-B map and 4-B count (the flagged groups' run words, ~1 %, not counted)
     alg = G * (4 * P + 32) + n_changed * 12 + ((G + 127) // 128) * 20
+    fan = leg_table_fanout(ctx, series, pristine, work, lists, series_ms, G, NB, t_ms, alg)
     for t in pristine + plain + work:
         t.close()
     return {"workload": f"C3 resident table: {G} groups x {P} peers, joint, 1% with a conf "
@@ -722,6 +800,7 @@ def leg_table(ctx, args, G, pair_ms):
                       f"launches on {NB} distinct fresh tables) / {NB}; the restores run before the "
                       f"pair; the pair kernel timed the same way on the same inputs",
             "bit_exact_vs_stateless_kernel_and_oracle": ok,
+            "fused_fanout": fan,
             "roofline": roofline(alg, t_ms, kernel="table_epoch_kernel<5>",
                                  bytes_note="reads 4P+32 B per group (u32 match words), writes "
                                             "lastCommitted + list delta 12 B per committing group "
@@ -1688,6 +1767,12 @@ def compact_line(full: dict, detail_path: str | None = DETAIL_FILE) -> dict:
         legs["table"]["over_pair"] = _r(t.get("table_over_pair"), 3)
         legs["table"]["no_conf_over_pair"] = _r(t.get("no_conf_table_over_pair"), 3)
         legs["table"]["no_conf_ms"] = _r(t.get("kernel_ms_no_conf_change"), 5)
+        fz = t.get("fused_fanout")
+        if fz:  # the epoch with the commit fan-out fused in, and the two-launch path it replaces
+            legs["table_fanout"] = {"ms": _r(fz.get("kernel_ms"), 5),
+                                    "frac": _r(fz["roofline"].get("frac"), 3),
+                                    "epoch_then_fanout_ms": _r(fz.get("epoch_then_fanout_ms"), 5),
+                                    "bit_exact": fz.get("bit_exact_vs_epoch_then_fanout")}
     c2 = full.get("C2") or {}
     if "kernel_ms" in c2:
         legs["C2_one_epoch"] = {"ms": _r(c2["kernel_ms"], 5), "bit_exact": None}

@@ -672,6 +672,29 @@ int jrq_rccl_init_all(jrq_engine *const *engines, int n);
  * waiting for the source engine's stream).  Asynchronous on each engine's stream. */
 int jrq_publish_committed_all_dev(jrq_engine *const *engines, int n, const int64_t *const *local_dev,
                                   int64_t *const *global_dev, uint64_t count_per_engine);
+/* FSMCaller state beside the table (r06): per group lastAppliedIndex (FSMCallerImpl, JC/core/
+ * FSMCallerImpl.java:462-470) and its ClosureQueue's (firstIndex, size) (JC/closure/
+ * ClosureQueueImpl.java:83-142), all 0 at creation.  jrq_table_fsm_update sets n groups' values
+ * (each group at most once per call; a group >= G is skipped and counted, jrq_table_check);
+ * jrq_table_fsm_read returns every group's (G words each, nullable outputs).
+ * jrq_table_epoch_fanout[_dev] is jrq_table_epoch with jrq_commit_fanout fused in: for every
+ * group whose commit moved, FSMCallerImpl.doCommitted's gate and popClosureUntil on its new
+ * lastCommittedIndex (jrq_commit_fanout's closed form), the queue updated in place.  Host
+ * variant: changed_out as jrq_table_epoch's; fan_first_out[i] / fan_status_out[i] for list
+ * entry i (popClosureUntil's result -- the first popped closure's index, committed + 1 when none
+ * pops, -1 for INVALID -- and the jrq_fanout_status; NONE is never listed).  Device variant:
+ * slices as jrq_table_epoch_dev; fan_first_out[s * JRQ_TABLE_SLICE + r] / fan_status_out[...]
+ * for the slice's r-th committing group (r < n_changed_out[s]), jrq_table_slices(t) slices each. */
+int jrq_table_fsm_update(jrq_table *t, const uint32_t *groups, const int64_t *last_applied,
+                         const int64_t *cq_first, const int64_t *cq_size, uint32_t n);
+int jrq_table_fsm_update_dev(jrq_table *t, const uint32_t *groups_dev, const int64_t *last_applied_dev,
+                             const int64_t *cq_first_dev, const int64_t *cq_size_dev, uint32_t n);
+int jrq_table_fsm_read(jrq_table *t, int64_t *last_applied, int64_t *cq_first, int64_t *cq_size);
+int jrq_table_epoch_fanout(jrq_table *t, uint64_t *changed_out, uint32_t *n_changed,
+                           int64_t *fan_first_out, uint8_t *fan_status_out);
+int jrq_table_epoch_fanout_dev(jrq_table *t, uint64_t *slices_out, uint32_t *n_changed_out,
+                               int64_t *fan_first_out, uint8_t *fan_status_out);
+
 /* lastCommittedIndex of every group of the table, contiguous: out_dev[g] for g < G (the tiled
  * lc row de-tiled on the device), asynchronous on the engine's stream -- the local part of a
  * snapshot. */

@@ -252,6 +252,26 @@ JNIEXPORT jint FN(snapshotVia)(JNIEnv *env, jclass cls, jlong snap) {
     return jrq_jni_snapshot_via(ENG(snap));
 }
 
+JNIEXPORT jint FN(tableFsmUpdate)(JNIEnv *env, jclass cls, jlong table, jobject groups,
+                                  jobject lastApplied, jobject cqFirst, jobject cqSize, jint n) {
+    (void)cls;
+    return jrq_jni_table_fsm_update(ENG(table), ADDR(groups), ADDR(lastApplied), ADDR(cqFirst),
+                                    ADDR(cqSize), n);
+}
+
+JNIEXPORT jint FN(tableFsmRead)(JNIEnv *env, jclass cls, jlong table, jobject lastApplied,
+                                jobject cqFirst, jobject cqSize) {
+    (void)cls;
+    return jrq_jni_table_fsm_read(ENG(table), ADDR(lastApplied), ADDR(cqFirst), ADDR(cqSize));
+}
+
+/* returns the number of changed groups (>= 0) or a negative jrq_error */
+JNIEXPORT jint FN(tableEpochFanout)(JNIEnv *env, jclass cls, jlong table, jobject changed,
+                                    jobject fanFirst, jobject fanStatus) {
+    (void)cls;
+    return jrq_jni_table_epoch_fanout(ENG(table), ADDR(changed), ADDR(fanFirst), ADDR(fanStatus));
+}
+
 JNIEXPORT jint FN(crc64Batch)(JNIEnv *env, jclass cls, jlong eng, jobject payload,
                               jobject offsets, jint n, jobject out) {
     (void)cls;

@@ -193,6 +193,29 @@ int32_t jrq_jni_table_read(jrq_addr table, jrq_addr pending_index, jrq_addr last
 
 int32_t jrq_jni_table_check(jrq_addr table) { return jrq_table_check(A(jrq_table *, table)); }
 
+int32_t jrq_jni_table_fsm_update(jrq_addr table, jrq_addr groups, jrq_addr last_applied,
+                                 jrq_addr cq_first, jrq_addr cq_size, int32_t n) {
+    N(n);
+    return jrq_table_fsm_update(A(jrq_table *, table), A(const uint32_t *, groups),
+                                A(const int64_t *, last_applied), A(const int64_t *, cq_first),
+                                A(const int64_t *, cq_size), (uint32_t)n);
+}
+
+int32_t jrq_jni_table_fsm_read(jrq_addr table, jrq_addr last_applied, jrq_addr cq_first,
+                               jrq_addr cq_size) {
+    return jrq_table_fsm_read(A(jrq_table *, table), A(int64_t *, last_applied),
+                              A(int64_t *, cq_first), A(int64_t *, cq_size));
+}
+
+int32_t jrq_jni_table_epoch_fanout(jrq_addr table, jrq_addr changed, jrq_addr fan_first,
+                                   jrq_addr fan_status) {
+    uint32_t n = 0;
+    int rc = jrq_table_epoch_fanout(A(jrq_table *, table), A(uint64_t *, changed), &n,
+                                    A(int64_t *, fan_first), A(uint8_t *, fan_status));
+    if (rc != JRQ_OK) return rc;
+    return (int32_t)n;
+}
+
 /* jrq_addr words are handles; on an LP64 host they are pointer-sized, checked below */
 typedef char jrq_jni_addr_is_a_pointer[sizeof(jrq_addr) == sizeof(void *) ? 1 : -1];
 

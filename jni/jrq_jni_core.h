@@ -72,6 +72,15 @@ int32_t jrq_jni_table_epoch(jrq_addr table, jrq_addr changed, jrq_addr status_ou
 int32_t jrq_jni_table_read(jrq_addr table, jrq_addr pending_index, jrq_addr last_appended,
                            jrq_addr last_committed, jrq_addr match);
 int32_t jrq_jni_table_check(jrq_addr table);
+/* FSMCaller state and the fused fan-out epoch (FSMCallerImpl.java:462-482,
+ * ClosureQueueImpl.java:113-142) */
+int32_t jrq_jni_table_fsm_update(jrq_addr table, jrq_addr groups, jrq_addr last_applied,
+                                 jrq_addr cq_first, jrq_addr cq_size, int32_t n);
+int32_t jrq_jni_table_fsm_read(jrq_addr table, jrq_addr last_applied, jrq_addr cq_first,
+                               jrq_addr cq_size);
+/* returns the number of changed groups (>= 0), or a jrq_error */
+int32_t jrq_jni_table_epoch_fanout(jrq_addr table, jrq_addr changed, jrq_addr fan_first,
+                                   jrq_addr fan_status);
 
 /* one JVM, N engines (ShardedGroupBatch): `engines` / `tables` is the
  * address of n jrq_addr words */

@@ -39,9 +39,6 @@ constexpr int kFanBlock = JRQ_FAN_BLOCK;
 constexpr int kFanPerThread = JRQ_FAN_PER_THREAD;
 constexpr int kFanTile = kFanBlock * kFanPerThread;  // groups per tile
 
-// include/jrq.h jrq_fanout_status
-constexpr uint8_t kFanNone = 0, kFanApply = 1, kFanSkip = 2, kFanInvalid = 3;
-
 __device__ __forceinline__ bool listed(uint8_t st) { return st == kFanApply || st == kFanInvalid; }
 
 // Tile slot k of thread t is group base + k*kFanBlock + t: every load is a coalesced stream,
@@ -103,26 +100,7 @@ __global__ __launch_bounds__(kFanBlock) void fanout_eval(JrqFanoutArgs a) {
   }
 }
 
-// One group's doCommitted gate and popClosureUntil (the closed form above): status, the
-// first popped closure index, and the queue after the pops (f, n unchanged unless it pops).
-__device__ __forceinline__ uint8_t fan_one(int64_t prev, int64_t c, int64_t applied, int64_t& f,
-                                           int64_t& n, int64_t& first_closure) {
-  first_closure = 0;
-  if (c <= prev) return kFanNone;  // onCommitted was not called for this group
-  if (applied >= c) return kFanSkip;
-  if (n == 0 || c < f) {
-    first_closure = c + 1;
-    return kFanApply;
-  }
-  if (c > f + n - 1) {
-    first_closure = -1;
-    return kFanInvalid;
-  }
-  first_closure = f;
-  n -= c - f + 1;
-  f = c + 1;
-  return kFanApply;
-}
+// (fan_one: the per-group closed form above, jrq_device.h, shared with the table's fused epoch)
 
 // Bits 0..31 of x to the even bits, of y to the odd bits (a pair lane's two groups are
 // adjacent in the bitmap).

@@ -39,6 +39,12 @@ extern "C" hipError_t jrq_launch_table_update(const JrqTableArgs* a, const JrqGr
                                               uint32_t n_states, const uint64_t* recs,
                                               uint32_t n_recs, hipStream_t stream);
 extern "C" hipError_t jrq_launch_table_epoch(const JrqTableArgs* a, hipStream_t stream);
+extern "C" hipError_t jrq_launch_table_fsm(const JrqTableArgs* a, const uint32_t* groups, const int64_t* applied,
+                                           const int64_t* first, const int64_t* size, uint32_t n,
+                                           hipStream_t stream);
+extern "C" hipError_t jrq_launch_table_fan_gather(const int64_t* ff, const uint8_t* fs, const uint32_t* n,
+                                                  const uint32_t* off, uint32_t slices, int64_t* out_first,
+                                                  uint8_t* out_status, hipStream_t stream);
 extern "C" hipError_t jrq_launch_table_acks(const JrqTableArgs* a, const uint64_t* acks, uint32_t n,
                                             const uint32_t* seg_off, const uint64_t* seg_stamp,
                                             uint32_t nseg, hipStream_t stream);
@@ -1669,6 +1675,7 @@ struct jrq_table {
   uint64_t stage_cap_s = 0, stage_cap_r = 0;  // jrq_table_stage: reserved capacity
   uint64_t staged_s = 0, staged_r = 0;        // headers / records staged since the last apply
   DevBuf ack_stage, seg_stage;                // order-free ack records (jrq_table_stage_acks)
+  DevBuf fsm_stage;                           // jrq_table_fsm_update (host variant)
   uint64_t stage_cap_a = 0, staged_a = 0;
   uint32_t stage_cap_seg = 0;
   std::vector<uint32_t> seg_off;              // staged segments: first record, stamp
@@ -1728,7 +1735,8 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   const uint64_t tiles = (waves + 1) / 2;
   const uint64_t flag_words = waves * jrq::kFlagSlots * 8 + (waves + 1) / 2;
   const uint64_t ts = static_cast<uint64_t>(P) * (jrq::kTableSlice / 2) + 4 * jrq::kTableSlice;  // words per tile
-  const uint64_t words = tiles * ts + ld * 2 * (jrq::kTableMaxRuns - 1) + flag_words + ld;  // + rstamp[ld]
+  // + rstamp[ld], + fsm[3][ld] (lastAppliedIndex, ClosureQueue firstIndex and size)
+  const uint64_t words = tiles * ts + ld * 2 * (jrq::kTableMaxRuns - 1) + flag_words + ld + 3 * ld;
   const size_t bytes = words * 8 + 64;
   t->slices = (G + JRQ_TABLE_SLICE - 1) / JRQ_TABLE_SLICE;
   if (hipMalloc(&t->mem, bytes) != hipSuccess || hipMemset(t->mem, 0, bytes) != hipSuccess ||
@@ -1752,6 +1760,7 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   a.flag_ent = reinterpret_cast<uint64_t*>(a.xconf + ld * (jrq::kTableMaxRuns - 1));
   a.flag_wcnt = reinterpret_cast<uint32_t*>(a.flag_ent + waves * jrq::kFlagSlots * 8);
   a.rstamp = reinterpret_cast<uint64_t*>(a.flag_ent + waves * jrq::kFlagSlots * 8 + (waves + 1) / 2);
+  a.fsm = reinterpret_cast<int64_t*>(a.rstamp + ld);
   a.invalid = reinterpret_cast<uint32_t*>(w + words);
   t->state_bytes = words * 8;
   a.ld = ld;
@@ -1766,7 +1775,7 @@ void jrq_table_destroy(jrq_table* t) {
   if (t->e) {
     DeviceGuard guard(t->e->device);
     (void)hipStreamSynchronize(t->e->stream);
-    for (DevBuf* b : {&t->st_stage, &t->rec_stage, &t->changed_stage, &t->ack_stage, &t->seg_stage})
+    for (DevBuf* b : {&t->st_stage, &t->rec_stage, &t->changed_stage, &t->ack_stage, &t->seg_stage, &t->fsm_stage})
       if (b->p) (void)hipFree(b->p);
     if (t->mem) (void)hipFree(t->mem);
     if (t->n_dev) (void)hipFree(t->n_dev);
@@ -1976,6 +1985,106 @@ int jrq_table_epoch(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, ui
   if (n > G) return fail(e, JRQ_E_STATE, "table list overflow (%u entries)", n);
   if (n) {
     JRQ_DOWN(e, changed_out, list, static_cast<size_t>(n) * 8);
+    JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  }
+  *n_changed = n;
+  return JRQ_OK;
+}
+
+int jrq_table_fsm_update_dev(jrq_table* t, const uint32_t* groups_dev, const int64_t* last_applied_dev,
+                             const int64_t* cq_first_dev, const int64_t* cq_size_dev, uint32_t n) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if (n && (!groups_dev || !last_applied_dev || !cq_first_dev || !cq_size_dev))
+    return fail(e, JRQ_E_INVALID, "null fsm update array");
+  DeviceGuard guard(e->device);
+  JRQ_HIP(e, jrq_launch_table_fsm(&t->a, groups_dev, last_applied_dev, cq_first_dev, cq_size_dev, n, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_table_fsm_update(jrq_table* t, const uint32_t* groups, const int64_t* last_applied,
+                         const int64_t* cq_first, const int64_t* cq_size, uint32_t n) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if (n && (!groups || !last_applied || !cq_first || !cq_size)) return fail(e, JRQ_E_INVALID, "null fsm update array");
+  if (n == 0) return JRQ_OK;
+  DeviceGuard guard(e->device);
+  // one staging block: the three int64 arrays, then the group ids
+  void* d = nullptr;
+  int rc;
+  if ((rc = stage_buf(e, t->fsm_stage, static_cast<size_t>(n) * 28, &d))) return rc;
+  int64_t* da = static_cast<int64_t*>(d);
+  uint32_t* dg = reinterpret_cast<uint32_t*>(da + 3ull * n);
+  if ((rc = upload_any(e, da, last_applied, static_cast<size_t>(n) * 8)) ||
+      (rc = upload_any(e, da + n, cq_first, static_cast<size_t>(n) * 8)) ||
+      (rc = upload_any(e, da + 2ull * n, cq_size, static_cast<size_t>(n) * 8)) ||
+      (rc = upload_any(e, dg, groups, static_cast<size_t>(n) * 4)))
+    return rc;
+  return jrq_table_fsm_update_dev(t, dg, da, da + n, da + 2ull * n, n);
+}
+
+int jrq_table_fsm_read(jrq_table* t, int64_t* last_applied, int64_t* cq_first, int64_t* cq_size) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  DeviceGuard guard(e->device);
+  const size_t G = t->a.G;
+  if (last_applied) JRQ_DOWN(e, last_applied, t->a.fsm, G * 8);
+  if (cq_first) JRQ_DOWN(e, cq_first, t->a.fsm + t->a.ld, G * 8);
+  if (cq_size) JRQ_DOWN(e, cq_size, t->a.fsm + 2 * t->a.ld, G * 8);
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  return JRQ_OK;
+}
+
+int jrq_table_epoch_fanout_dev(jrq_table* t, uint64_t* slices_out, uint32_t* n_changed_out,
+                               int64_t* fan_first_out, uint8_t* fan_status_out) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if (!slices_out || !n_changed_out || !fan_first_out || !fan_status_out)
+    return fail(e, JRQ_E_INVALID, "null fan-out epoch output");
+  DeviceGuard guard(e->device);
+  JrqTableArgs a = t->a;
+  a.changed = slices_out;
+  a.n_changed = n_changed_out;
+  a.status = nullptr;
+  a.fan_first = fan_first_out;
+  a.fan_status = fan_status_out;
+  JRQ_HIP(e, jrq_launch_table_epoch(&a, e->stream));
+  return JRQ_OK;
+}
+
+int jrq_table_epoch_fanout(jrq_table* t, uint64_t* changed_out, uint32_t* n_changed, int64_t* fan_first_out,
+                           uint8_t* fan_status_out) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  jrq_engine* e = t->e;
+  if (!changed_out || !n_changed || !fan_first_out || !fan_status_out)
+    return fail(e, JRQ_E_INVALID, "null fan-out epoch output");
+  DeviceGuard guard(e->device);
+  const uint32_t S = t->slices;
+  const size_t cap = static_cast<size_t>(S) * JRQ_TABLE_SLICE;
+  int rc;
+  void* dch = nullptr;
+  // staging: the slices and their gathered list, the slice-shaped fan results and their gathered
+  // copies (first closures, then statuses)
+  if ((rc = stage_buf(e, t->changed_stage, 2 * cap * 8 + 2 * cap * 8 + 2 * cap, &dch))) return rc;
+  uint64_t* slices = static_cast<uint64_t*>(dch);
+  uint64_t* list = slices + cap;
+  int64_t* ff = reinterpret_cast<int64_t*>(list + cap);
+  int64_t* lf = ff + cap;
+  uint8_t* fs = reinterpret_cast<uint8_t*>(lf + cap);
+  uint8_t* ls = fs + cap;
+  if ((rc = jrq_table_epoch_fanout_dev(t, slices, t->n_dev, ff, fs))) return rc;
+  uint32_t* off = t->n_dev + S;
+  uint32_t* total = off + S;
+  JRQ_HIP(e, jrq_launch_table_list_gather(slices, t->n_dev, S, off, total, list, e->stream));
+  JRQ_HIP(e, jrq_launch_table_fan_gather(ff, fs, t->n_dev, off, S, lf, ls, e->stream));
+  JRQ_DOWN(e, t->n_host, total, 4);
+  JRQ_HIP(e, hipStreamSynchronize(e->stream));
+  const uint32_t n = t->n_host[0];
+  if (n > t->a.G) return fail(e, JRQ_E_STATE, "table list overflow (%u entries)", n);
+  if (n) {
+    JRQ_DOWN(e, changed_out, list, static_cast<size_t>(n) * 8);
+    JRQ_DOWN(e, fan_first_out, lf, static_cast<size_t>(n) * 8);
+    JRQ_DOWN(e, fan_status_out, ls, n);
     JRQ_HIP(e, hipStreamSynchronize(e->stream));
   }
   *n_changed = n;

@@ -310,6 +310,11 @@ struct JrqTableArgs {
   uint32_t* flag_wcnt;   // [waves] how many
   uint64_t* rstamp;      // [ld] reset stamp of each group (JRQ_STATE_STAMP headers): order-free
                          // ack records from segments stamped earlier are dropped
+  int64_t* fsm;          // [3][ld] FSMCaller state of each group (r06): lastAppliedIndex, then the
+                         // ClosureQueue's firstIndex and size (jrq_table_fsm_update)
+  int64_t* fan_first;    // [slices][JRQ_TABLE_SLICE] out, fused fan-out epochs only: popClosureUntil's
+                         // result of the slice's committing groups, at their delta ranks
+  uint8_t* fan_status;   // [slices][JRQ_TABLE_SLICE] out: their jrq_fanout_status
 };
 
 // Element g of a tiled int64 field (its row in tile 0: t.pi, t.la, t.lc, t.conf).
@@ -319,6 +324,32 @@ __host__ __device__ __forceinline__ T& tf(T* row, const JrqTableArgs& t, uint32_
 }
 
 namespace jrq {
+// include/jrq.h jrq_fanout_status
+constexpr uint8_t kFanNone = 0, kFanApply = 1, kFanSkip = 2, kFanInvalid = 3;
+
+// One group's FSMCallerImpl.doCommitted gate and ClosureQueueImpl.popClosureUntil for the epoch's
+// last committed index c (FSMCallerImpl.java:462-482, ClosureQueueImpl.java:113-142; the closed
+// form of commit_fanout.hip): the status, the first popped closure's index (c + 1 when none is
+// popped, -1 for INVALID) and the queue (f, n) after the pops.
+__device__ __forceinline__ uint8_t fan_one(int64_t prev, int64_t c, int64_t applied, int64_t& f,
+                                           int64_t& n, int64_t& first_closure) {
+  first_closure = 0;
+  if (c <= prev) return kFanNone;  // onCommitted was not called for this group
+  if (applied >= c) return kFanSkip;
+  if (n == 0 || c < f) {
+    first_closure = c + 1;
+    return kFanApply;
+  }
+  if (c > f + n - 1) {
+    first_closure = -1;
+    return kFanInvalid;
+  }
+  first_closure = f;
+  n -= c - f + 1;
+  f = c + 1;
+  return kFanApply;
+}
+
 constexpr int kMatchPageBits = 30;  // match base granularity (JRQ_TABLE_MATCH_PAGE)
 // The match base of a group whose (resolved) pendingIndex is pi; 0 when not the leader.
 __host__ __device__ __forceinline__ int64_t mbase(int64_t pi) {

@@ -213,9 +213,10 @@ struct UnitIn {
   int64_t ev;
   i64x2 pr, la, lc, cw;
   u32x2 mq[P];
+  i64x2 ap, cf, cs;  // the fused fan-out's FSMCaller rows (kFan only)
 };
 
-template <int P>
+template <int P, bool kFan>
 __device__ __forceinline__ void unit_load(const JrqTableArgs& t, uint32_t u, uint32_t lane, UnitIn<P>& in) {
   const int64_t* const tile = reinterpret_cast<const int64_t*>(t.match) + static_cast<size_t>(u >> 1) * t.ts;
   const int64_t* const ent = reinterpret_cast<const int64_t*>(t.flag_ent) + static_cast<size_t>(u) * kFlagSlots * 8;
@@ -227,10 +228,17 @@ __device__ __forceinline__ void unit_load(const JrqTableArgs& t, uint32_t u, uin
   in.cw = tld2o(tile + 128 * P + 768, go);
 #pragma unroll
   for (int p = 0; p < P; ++p) in.mq[p] = tld2u(tile + 128 * p, 8u * lane + 512u * (u & 1u));
+  if (kFan) {  // the pair's lastAppliedIndex, ClosureQueue firstIndex and size (pad lanes: group 0's)
+    const uint32_t g0 = u * kListSlice + 2u * lane;
+    const size_t gp = g0 < t.G ? g0 : 0u;
+    in.ap = __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(t.fsm + gp));
+    in.cf = __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(t.fsm + t.ld + gp));
+    in.cs = __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(t.fsm + 2 * t.ld + gp));
+  }
 }
 
 // The unit's decisions and writes, from its loads.
-template <int P>
+template <int P, bool kFan>
 __device__ __forceinline__ void unit_decide(const JrqTableArgs& t, uint32_t u, uint32_t lane,
                                             int64_t (&entw)[kEntLds][8], const UnitIn<P>& ui) {
   const uint64_t below = (1ull << lane) - 1ull;
@@ -440,6 +448,35 @@ __device__ __forceinline__ void unit_decide(const JrqTableArgs& t, uint32_t u, u
   }
 #endif
   if (lane == 0 && owns) t.n_changed[u] = cnt;
+  // the fused fan-out (jrq_table_epoch_fanout): each committing group's doCommitted /
+  // popClosureUntil on its new lastCommittedIndex (fan_one), the queue written back where it
+  // popped, the result at the group's delta rank in the slice's fan arrays
+  if (kFan) {
+    int64_t f0 = ui.cf.x, n0 = ui.cs.x, f1 = ui.cf.y, n1 = ui.cs.y, fc0 = 0, fc1 = 0;
+    const uint8_t s0 = c[0] ? fan_one(ui.lc.x, outv[0], ui.ap.x, f0, n0, fc0) : kFanNone;
+    const uint8_t s1 = c[1] ? fan_one(ui.lc.y, outv[1], ui.ap.y, f1, n1, fc1) : kFanNone;
+    if (f0 != ui.cf.x || f1 != ui.cf.y) {  // a pop moved firstIndex
+      i64x2 nf, nn;
+      nf.x = f0;
+      nf.y = f1;
+      nn.x = n0;
+      nn.y = n1;
+      *reinterpret_cast<i64x2*>(t.fsm + t.ld + g0) = nf;
+      *reinterpret_cast<i64x2*>(t.fsm + 2 * t.ld + g0) = nn;
+    }
+    const uint32_t r0 = __popcll(b0 & below) + __popcll(b1 & below);
+    int64_t* const ff = t.fan_first + static_cast<size_t>(u) * kListSlice;
+    uint8_t* const fs = t.fan_status + static_cast<size_t>(u) * kListSlice;
+    if (c[0]) {
+      ff[r0] = fc0;
+      fs[r0] = s0;
+    }
+    if (c[1]) {
+      const uint32_t r1 = r0 + (c[0] ? 1u : 0u);
+      ff[r1] = fc1;
+      fs[r1] = s1;
+    }
+  }
 }
 
 
@@ -449,8 +486,8 @@ __device__ __forceinline__ void unit_decide(const JrqTableArgs& t, uint32_t u, u
 #ifndef JRQ_TABLE_UNITS
 #define JRQ_TABLE_UNITS 1
 #endif
-template <int P>
-__global__ __launch_bounds__(kTableEpochBlock, JRQ_TABLE_UNITS == 2 ? 4 : (P <= 5 ? JRQ_TABLE_OCC : (P <= 10 ? 4 : 2)))
+template <int P, bool kFan>
+__global__ __launch_bounds__(kTableEpochBlock, JRQ_TABLE_UNITS == 2 ? 4 : (P <= 5 ? (kFan ? 6 : JRQ_TABLE_OCC) : (P <= 10 ? 4 : 2)))
 JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
   constexpr uint32_t kWaves = kTableEpochBlock / 64;
   __shared__ int64_t entl[kWaves][kEntLds][8];
@@ -458,16 +495,51 @@ JRQ_SGPRS_8WAVES void table_epoch_kernel(JrqTableArgs t) {
   const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + w);
 #if JRQ_TABLE_UNITS == 2
   UnitIn<P> a, b;
-  unit_load<P>(t, 2u * wid, lane, a);
-  unit_load<P>(t, 2u * wid + 1u, lane, b);
-  unit_decide<P>(t, 2u * wid, lane, entl[w], a);
+  unit_load<P, kFan>(t, 2u * wid, lane, a);
+  unit_load<P, kFan>(t, 2u * wid + 1u, lane, b);
+  unit_decide<P, kFan>(t, 2u * wid, lane, entl[w], a);
   asm volatile("" ::: "memory");  // (the first unit's LDS reads before the second's parking)
-  unit_decide<P>(t, 2u * wid + 1u, lane, entl[w], b);
+  unit_decide<P, kFan>(t, 2u * wid + 1u, lane, entl[w], b);
 #else
   UnitIn<P> a;
-  unit_load<P>(t, wid, lane, a);
-  unit_decide<P>(t, wid, lane, entl[w], a);
+  unit_load<P, kFan>(t, wid, lane, a);
+  unit_decide<P, kFan>(t, wid, lane, entl[w], a);
 #endif
+}
+
+// jrq_table_fsm_update: n groups' FSMCaller state (lastAppliedIndex, ClosureQueue firstIndex and
+// size), one group per lane; a group past the table is skipped and counted.
+__global__ __launch_bounds__(256) void table_fsm_kernel(JrqTableArgs t, const uint32_t* __restrict__ groups,
+                                                        const int64_t* __restrict__ applied,
+                                                        const int64_t* __restrict__ first,
+                                                        const int64_t* __restrict__ size, uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t g = groups[i];
+    if (g >= t.G) {
+      atomicAdd(t.invalid, 1u);
+      continue;
+    }
+    t.fsm[g] = applied[i];
+    t.fsm[t.ld + g] = first[i];
+    t.fsm[2 * t.ld + g] = size[i];
+  }
+}
+
+// Host variant of the fused fan-out: each slice's fan results (ranks 0 .. n[s) of its fan arrays)
+// gathered behind the slices before it, in the host list's order (one wave per slice).
+__global__ __launch_bounds__(512) void table_fan_gather_kernel(const int64_t* __restrict__ ff,
+                                                               const uint8_t* __restrict__ fs,
+                                                               const uint32_t* __restrict__ n,
+                                                               const uint32_t* __restrict__ off,
+                                                               uint32_t slices, int64_t* __restrict__ out_first,
+                                                               uint8_t* __restrict__ out_status) {
+  const uint32_t s = blockIdx.x * 8u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (s >= slices) return;
+  const uint32_t cnt = n[s], o = off[s];
+  for (uint32_t r = lane; r < cnt; r += 64u) {
+    out_first[o + r] = ff[static_cast<size_t>(s) * kListSlice + r];
+    out_status[o + r] = fs[static_cast<size_t>(s) * kListSlice + r];
+  }
 }
 
 // Host variant of the epoch: the slices' counts scanned into offsets (one workgroup; a
@@ -742,7 +814,10 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_epo
   switch (a->P) {
 #define JRQ_CASE(P)                                                                   \
   case P:                                                                             \
-    hipLaunchKernelGGL(jrq::table_epoch_kernel<P>, grid, blk, 0, stream, *a);         \
+    if (a->fan_first)                                                                 \
+      hipLaunchKernelGGL((jrq::table_epoch_kernel<P, true>), grid, blk, 0, stream, *a); \
+    else                                                                              \
+      hipLaunchKernelGGL((jrq::table_epoch_kernel<P, false>), grid, blk, 0, stream, *a); \
     break;
     JRQ_CASE(1) JRQ_CASE(2) JRQ_CASE(3) JRQ_CASE(4) JRQ_CASE(5) JRQ_CASE(6) JRQ_CASE(7)
     JRQ_CASE(8) JRQ_CASE(9) JRQ_CASE(10) JRQ_CASE(11) JRQ_CASE(12) JRQ_CASE(13) JRQ_CASE(14)
@@ -751,5 +826,24 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_epo
     default:
       return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_fsm(
+    const JrqTableArgs* a, const uint32_t* groups, const int64_t* applied, const int64_t* first,
+    const int64_t* size, uint32_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint32_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(jrq::table_fsm_kernel, dim3(blocks < 4096 ? blocks : 4096), dim3(256), 0, stream, *a,
+                     groups, applied, first, size, n);
+  return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_fan_gather(
+    const int64_t* ff, const uint8_t* fs, const uint32_t* n, const uint32_t* off, uint32_t slices,
+    int64_t* out_first, uint8_t* out_status, hipStream_t stream) {
+  if (slices == 0) return hipSuccess;
+  hipLaunchKernelGGL(jrq::table_fan_gather_kernel, dim3((slices + 7) / 8), dim3(512), 0, stream, ff, fs, n,
+                     off, slices, out_first, out_status);
   return hipGetLastError();
 }

@@ -168,6 +168,11 @@ SIGNATURES = [
     ("jrq_table_slices", C.c_uint32, [_V]),
     ("jrq_table_stage_reserve_acks", C.c_int, [_V, C.c_uint32, C.c_uint32]),
     ("jrq_table_committed_dev", C.c_int, [_V, _V]),
+    ("jrq_table_fsm_update", C.c_int, [_V, _V, _V, _V, _V, C.c_uint32]),
+    ("jrq_table_fsm_update_dev", C.c_int, [_V, _V, _V, _V, _V, C.c_uint32]),
+    ("jrq_table_fsm_read", C.c_int, [_V, _V, _V, _V]),
+    ("jrq_table_epoch_fanout", C.c_int, [_V, _V, _V, _V, _V]),
+    ("jrq_table_epoch_fanout_dev", C.c_int, [_V, _V, _V, _V, _V]),
     ("jrq_rccl_init_all", C.c_int, [_V, C.c_int]),
     ("jrq_publish_committed_all_dev", C.c_int, [_V, C.c_int, _V, _V, C.c_uint64]),
     ("jrq_snapshot_create", _V, [_V, C.c_int, C.POINTER(C.c_int)]),

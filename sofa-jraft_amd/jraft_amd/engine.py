@@ -657,6 +657,57 @@ class Table:
         deltas in group order (include/jrq.h jrq_table_epoch_dev)."""
         return decode_slices(_host_np(changed_out), _host_np(n_changed_out))
 
+    # ------------------------------------- FSMCaller state + fused fan-out (r06) --
+    def fsm_update(self, groups, last_applied, cq_first, cq_size):
+        """Host variant of jrq_table_fsm_update: n groups' lastAppliedIndex and ClosureQueue
+        (firstIndex, size)."""
+        g = _c(groups, np.uint32)
+        a, f, z = (_c(x, np.int64) for x in (last_applied, cq_first, cq_size))
+        check(self._L.jrq_table_fsm_update(self._h, _np_ptr(g), _np_ptr(a), _np_ptr(f), _np_ptr(z), len(g)),
+              self._eng.handle)
+
+    def fsm_update_dev(self, groups, last_applied, cq_first, cq_size, n=None):
+        n = groups.shape[0] if n is None else n
+        check(self._L.jrq_table_fsm_update_dev(self._h, _dev_ptr(groups), _dev_ptr(last_applied),
+                                               _dev_ptr(cq_first), _dev_ptr(cq_size), n), self._eng.handle)
+
+    def fsm_read(self):
+        """(last_applied, cq_first, cq_size), G int64 each."""
+        o = [np.zeros(self.G, np.int64) for _ in range(3)]
+        check(self._L.jrq_table_fsm_read(self._h, *[_np_ptr(x) for x in o]), self._eng.handle)
+        return tuple(o)
+
+    def epoch_fanout(self):
+        """Host variant of jrq_table_epoch_fanout: (changed uint64[n] as JRQ words, fan_first
+        int64[n], fan_status uint8[n]) -- the epoch and each listed group's doCommitted /
+        popClosureUntil in list order."""
+        n0 = max(self.G, 1)
+        out = np.zeros(n0, np.uint64)
+        ff = np.zeros(n0, np.int64)
+        fs = np.zeros(n0, np.uint8)
+        n = C.c_uint32(0)
+        check(self._L.jrq_table_epoch_fanout(self._h, _np_ptr(out), C.byref(n), _np_ptr(ff), _np_ptr(fs)),
+              self._eng.handle)
+        self._keep = None
+        k = n.value
+        return out[:k].copy(), ff[:k].copy(), fs[:k].copy()
+
+    def committed_dev(self, out):
+        """Every group's lastCommittedIndex into the device tensor `out` (G int64, group order)."""
+        check(self._L.jrq_table_committed_dev(self._h, _dev_ptr(out)), self._eng.handle)
+
+    def fan_buffers(self, device):
+        """(fan_first_out, fan_status_out) device tensors sized for epoch_fanout_dev."""
+        import torch
+        s = self.slices()
+        return (torch.empty(s * _lib.TABLE_SLICE, dtype=torch.int64, device=device),
+                torch.empty(s * _lib.TABLE_SLICE, dtype=torch.uint8, device=device))
+
+    def epoch_fanout_dev(self, changed_out, n_changed_out, fan_first_out, fan_status_out):
+        check(self._L.jrq_table_epoch_fanout_dev(self._h, _dev_ptr(changed_out), _dev_ptr(n_changed_out),
+                                                 _dev_ptr(fan_first_out), _dev_ptr(fan_status_out)),
+              self._eng.handle)
+
     def read(self) -> dict:
         G, P = self.G, self.P
         o = dict(pending_index=np.zeros(G, np.int64), last_appended=np.zeros(G, np.int64),
