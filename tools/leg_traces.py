@@ -38,7 +38,8 @@ PEAK = 8000.0  # GB/s, MI355X HBM3E (MI355X_MICROARCH.md)
 # leg -> (path of its roofline object in the bench detail, kernels of one timed launch)
 LEG_KERNELS = {
     "quorum": (("roofline",), ["quorum_epoch_pair_kernel<5, false, true>"]),
-    "table": (("resident_table", "roofline"), ["table_epoch_kernel<5>"]),
+    "table": (("resident_table", "roofline"), ["table_epoch_kernel<5, false>"]),
+    "table_fanout": (("resident_table", "fused_fanout", "roofline"), ["table_epoch_kernel<5, true>"]),
     "C2": (("C2", "batched_epochs", "roofline"), ["quorum_epochs_kernel<3,"]),
     "C2L": (("C2", "batched_epochs_64", "roofline"), ["quorum_epochs_kernel<3,"]),
     "C3K": (("C3_k_epochs", "roofline"), ["quorum_epochs_pair_kernel<5, false, true>"]),
