@@ -1648,8 +1648,8 @@ def leg_peak(ctx):
     h = words.numel() // 2
     rd_ms, _ = ctx.timed(lambda i: torch.bitwise_xor(words[:h], words[h:],
                                                      out=dst.view(torch.int64)[:h]), 5, 2)
-    acc = torch.empty(1, dtype=torch.int64, device=ctx.dev)
-    sm_ms, _ = ctx.timed(lambda i: torch.sum(words, out=acc[0]), 5, 2)
+    acc = torch.empty((), dtype=torch.int64, device=ctx.dev)
+    sm_ms, _ = ctx.timed(lambda i: torch.sum(words, dim=0, out=acc), 5, 2)
     return {"copy_GBps": 2 * src.numel() / (cp_ms * 1e-3) / 1e9,
             "xor_GBps": 1.5 * src.numel() / (rd_ms * 1e-3) / 1e9,
             "read_GBps": src.numel() / (sm_ms * 1e-3) / 1e9,
