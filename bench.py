@@ -852,6 +852,8 @@ def leg_drive(ctx, args, G):
             "flush_ms": f, "pack_ms": float(np.mean(st["pack_ms"][sl])),
             "device_ms": float(np.mean(st["device_ms"][sl])),
             "deliver_ms": float(np.mean(st["deliver_ms"][sl])),
+            "deliver_apply_ms": float(np.mean(st["deliver_apply_ms"][sl])),
+            "deliver_callbacks_ms": float(np.mean(st["deliver_callbacks_ms"][sl])),
             "api_ms_per_epoch": api,
             "api_calls_per_epoch": float(np.mean(st["api_calls"][sl])),
             "end_to_end_ms_per_epoch": api + f,

@@ -143,9 +143,10 @@ extern "C" {
 
 const char* jraft_drive_last_error(void) { return g_err.c_str(); }
 
-// stats_out[k * 12 + i]: 0 api_ms, 1 pack_ms, 2 device_ms, 3 deliver_ms, 4 flush_ms,
+// stats_out[k * 14 + i]: 0 api_ms, 1 pack_ms, 2 device_ms, 3 deliver_ms, 4 flush_ms,
 // 5 h2d_bytes, 6 d2h_bytes, 7 states, 8 records (pack + call-time), 9 changed, 10 api_calls,
-// 11 acks (the call-time order-free records among them)
+// 11 acks (the call-time order-free records among them), 12 deliver_apply_ms, 13
+// deliver_callbacks_ms (the slowest deliver worker's two passes)
 //
 // jraft_drive_epochs_sharded -- the same over `shards` engines on `device` in one process
 // (ShardedGroupBatch: contiguous group blocks, the shards' epochs concurrent on their streams);
@@ -280,8 +281,8 @@ int jraft_drive_epochs_sharded(int device, uint32_t shards, uint32_t G, uint32_t
             throw std::runtime_error("published snapshot of group " + std::to_string(g) + " on engine " +
                                      std::to_string(k % S) + " differs from its getLastCommittedIndex");
       }
-      double* o = stats_out + static_cast<size_t>(k) * 12;
-      std::fill(o, o + 12, 0.0);
+      double* o = stats_out + static_cast<size_t>(k) * 14;
+      std::fill(o, o + 14, 0.0);
       for (uint32_t i = 0; i < S; ++i) {
         const jraft::FlushStats& s = sharded ? sharded->lastFlush(i) : batch->lastFlush();
         o[1] = std::max(o[1], s.pack_ms);
@@ -293,6 +294,8 @@ int jraft_drive_epochs_sharded(int device, uint32_t shards, uint32_t G, uint32_t
         o[8] += static_cast<double>(s.records) + s.acks;
         o[11] += s.acks;
         o[9] += s.changed;
+        o[12] = std::max(o[12], s.deliver_apply_ms);
+        o[13] = std::max(o[13], s.deliver_callbacks_ms);
       }
       o[0] = ms(t1 - t0);
       o[4] = ms(t2 - t1);

@@ -1129,7 +1129,9 @@ uint32_t GroupBatch::flushLocked() {
   const size_t dparts = partsFor(n, 1u << 12);
   if (deliveries_.size() < dparts) deliveries_.resize(dparts);
   std::vector<std::exception_ptr> errs(dparts);
+  std::vector<double> apply_ms(dparts, 0.0), cb_ms(dparts, 0.0);
   parallelFor(n, 1u << 12, [&](unsigned part, size_t i0, size_t i1) {
+    const auto d0 = clk::now();
     Delivery& D = deliveries_[part];
     D.commits.clear();
     D.done.clear();
@@ -1161,6 +1163,7 @@ uint32_t GroupBatch::flushLocked() {
       D.commits.push_back(Delivery::Commit{c, &waiter_[g]});
       D.ndone.push_back(nd0);
     }
+    const auto d1 = clk::now();
     struct Scope {
       const GroupBatch* prev;
       explicit Scope(const GroupBatch* b) : prev(tl_delivering) { tl_delivering = b; }
@@ -1183,6 +1186,8 @@ uint32_t GroupBatch::flushLocked() {
     }
     D.commits.clear();
     D.done.clear();
+    apply_ms[part] = std::chrono::duration<double, std::milli>(d1 - d0).count();
+    cb_ms[part] = std::chrono::duration<double, std::milli>(clk::now() - d1).count();
   });
   flushes_.fetch_add(1, std::memory_order_relaxed);
   const auto t3 = clk::now();
@@ -1194,6 +1199,10 @@ uint32_t GroupBatch::flushLocked() {
   stats.pack_ms = ms(t1 - t0);
   stats.device_ms = ms(t2 - t1);
   stats.deliver_ms = ms(t3 - t2);
+  for (size_t i = 0; i < dparts; ++i) {
+    stats.deliver_apply_ms = std::max(stats.deliver_apply_ms, apply_ms[i]);
+    stats.deliver_callbacks_ms = std::max(stats.deliver_callbacks_ms, cb_ms[i]);
+  }
   stats_ = stats;
   for (auto& e : errs)
     if (e) std::rethrow_exception(e);

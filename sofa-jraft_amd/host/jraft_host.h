@@ -365,6 +365,9 @@ struct FlushStats {
   uint32_t changed = 0;      // groups whose commit advanced (8-B entries downloaded)
   uint64_t h2d_bytes = 0, d2h_bytes = 0;
   double pack_ms = 0, device_ms = 0, deliver_ms = 0;
+  // the slowest deliver worker's two passes: commits applied under the groups' locks, then the
+  // closures and onCommitted callbacks
+  double deliver_apply_ms = 0, deliver_callbacks_ms = 0;
 };
 
 // When the background flusher (GroupBatch::startFlusher) runs an epoch: as soon as the oldest

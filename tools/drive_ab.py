@@ -71,7 +71,7 @@ def main():
     for n, L in per.items():
         m = np.concatenate(L)
         res[n] = {k: round(float(np.median(m[:, i])), 3) for i, k in enumerate(drive.STATS)
-                  if k in ("api_ms", "pack_ms", "device_ms", "deliver_ms", "flush_ms")}
+                  if k in ("api_ms", "pack_ms", "device_ms", "deliver_ms", "flush_ms", "deliver_apply_ms", "deliver_callbacks_ms")}
         res[n]["same_commits"] = same[n]
     print(json.dumps({"threads": a.threads, "groups": G, "epochs": K, "rounds": a.rounds,
                       "active": a.active, "median_ms": res}))
