@@ -669,7 +669,9 @@ int jrq_rccl_init_all(jrq_engine *const *engines, int n);
  * engine i's device, n * count_per_engine words) receives every local_dev[j] at j *
  * count_per_engine.  One grouped RCCL all-gather when every engine has a communicator from
  * jrq_rccl_init_all; else device-to-device copies (hipMemcpyPeerAsync, each destination stream
- * waiting for the source engine's stream).  Asynchronous on each engine's stream. */
+ * waiting for the source engine's stream, and each source stream then waiting for the copies
+ * that read its buffer, so a later write of local_dev[j] on engine j's stream follows them).
+ * Asynchronous on each engine's stream. */
 int jrq_publish_committed_all_dev(jrq_engine *const *engines, int n, const int64_t *const *local_dev,
                                   int64_t *const *global_dev, uint64_t count_per_engine);
 /* FSMCaller state beside the table (r06): per group lastAppliedIndex (FSMCallerImpl, JC/core/

@@ -2414,11 +2414,26 @@ int jrq_publish_committed_all_dev(jrq_engine* const* engines, int n, const int64
         rc = fail(engines[i], JRQ_E_HIP, "publish: copy %d -> %d", j, i);
     }
   }
-  for (int j = 0; j < n; ++j)
-    if (ev[j]) {
-      DeviceGuard guard(engines[j]->device);
-      (void)hipEventDestroy(ev[j]);  // (released once the waits it is part of complete)
-    }
+  // and every source stream waits for the copies that read its buffer: its next write of
+  // local[j] (the next publish's de-tiled lastCommitted) cannot overtake them
+  std::vector<hipEvent_t> done(n, nullptr);
+  for (int i = 0; i < n && rc == JRQ_OK; ++i) {
+    DeviceGuard guard(engines[i]->device);
+    if (hipEventCreateWithFlags(&done[i], hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(done[i], engines[i]->stream) != hipSuccess)
+      rc = fail(engines[i], JRQ_E_HIP, "publish: completion event on engine %d", i);
+  }
+  for (int j = 0; j < n && rc == JRQ_OK; ++j) {
+    DeviceGuard guard(engines[j]->device);
+    for (int i = 0; i < n && rc == JRQ_OK; ++i)
+      if (i != j && hipStreamWaitEvent(engines[j]->stream, done[i], 0) != hipSuccess)
+        rc = fail(engines[j], JRQ_E_HIP, "publish: engine %d waiting for engine %d's copies", j, i);
+  }
+  for (int j = 0; j < n; ++j) {
+    DeviceGuard guard(engines[j]->device);
+    if (ev[j]) (void)hipEventDestroy(ev[j]);  // (released once the waits it is part of complete)
+    if (done[j]) (void)hipEventDestroy(done[j]);
+  }
   return rc;
 }
 
