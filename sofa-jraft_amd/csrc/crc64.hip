@@ -895,19 +895,19 @@ __global__ __launch_bounds__(256) void crc64_finish_kernel(JrqCrcArgs a) {
 // segment walk takes the batch instead.  With kLogEntry the record's partial checksum (type ^
 // crc(LogId) ^ peers, from v2_parse) arrives in peer_xor: out = partial ^ crc(data) and the
 // verify compare, as v2_finish does on the segment-walk path.
-template <bool kLogEntry, bool kStarts>
-__global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
+template <bool kLogEntry, bool kStarts, int kBlock>
+__global__ __launch_bounds__(kBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t lds_tab[kCrcLdsBytes / 8];
   if (kStarts && a.gate[0] == 0) return;
   const char* lds = reinterpret_cast<const char*>(lds_tab);
-  constexpr uint32_t kTabPer = kCrcLdsBytes / 8 / kCrcBlock;
+  constexpr uint32_t kTabPer = kCrcLdsBytes / 8 / kBlock;
   uint64_t tab_v[kTabPer];  // this thread's share of the table image (written after the first loads)
 #pragma unroll
   for (uint32_t i = 0; i < kTabPer; ++i)
-    tab_v[i] = a.slice[CrcTab::src_index(threadIdx.x + i * kCrcBlock)];
+    tab_v[i] = a.slice[CrcTab::src_index(threadIdx.x + i * kBlock)];
   auto build_tables = [&]() {
 #pragma unroll
-    for (uint32_t i = 0; i < kTabPer; ++i) lds_tab[threadIdx.x + i * kCrcBlock] = tab_v[i];
+    for (uint32_t i = 0; i < kTabPer; ++i) lds_tab[threadIdx.x + i * kBlock] = tab_v[i];
     __syncthreads();
   };
   const CrcTab tb(threadIdx.x & 63u);
@@ -922,8 +922,8 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
   const uint32_t EPR = 64u >> kl;                              // entries per row
   const uint32_t rows = (n + EPR - 1) / EPR;
   // contiguous rows per wave (a wave streams 64 * EL * rows bytes in order)
-  const uint32_t W = gridDim.x * (kCrcBlock / 64);
-  const uint32_t w = blockIdx.x * (kCrcBlock / 64) + (L0 >> 6);
+  const uint32_t W = gridDim.x * (kBlock / 64);
+  const uint32_t w = blockIdx.x * (kBlock / 64) + (L0 >> 6);
   const uint32_t per = rows / W, extra = rows % W;
   const uint32_t r0 = __builtin_amdgcn_readfirstlane(w * per + (w < extra ? w : extra));
   const uint32_t r1 = __builtin_amdgcn_readfirstlane(r0 + per + (w < extra ? 1u : 0u));
@@ -1122,18 +1122,27 @@ __global__ __launch_bounds__(kCrcBlock) void crc64_fixed_kernel(JrqCrcArgs a) {
 // < 2^32, (entry_bytes / fixed_k) % 256 == 0.
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_crc64_fixed(
     JrqCrcArgs* args, int log_entry, int grid, hipStream_t stream) {
+  // one lane per entry (C1-like batches, several rows per wave): 1024-thread workgroups (118
+  // VGPRs, 4 waves per SIMD); pieces of larger entries: 512 (r06 A/B, profiles/r06_experiments.json)
+  const bool wide = args->starts == nullptr && args->fixed_k == 1;
   if (args->starts != nullptr && log_entry)  // V2 decode: partial ^ crc(data), gated on the device
-    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<true, true>), dim3(grid), dim3(jrq::kCrcBlock), 0,
-                       stream, *args);
+    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<true, true, jrq::kCrcFixedBlock>), dim3(grid),
+                       dim3(jrq::kCrcFixedBlock), 0, stream, *args);
   else if (args->starts != nullptr)  // plain CRCs at given starts, gated on the device
-    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<false, true>), dim3(grid), dim3(jrq::kCrcBlock), 0,
-                       stream, *args);
+    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<false, true, jrq::kCrcFixedBlock>), dim3(grid),
+                       dim3(jrq::kCrcFixedBlock), 0, stream, *args);
+  else if (log_entry && wide)
+    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<true, false, jrq::kCrcFixedWideBlock>), dim3(grid),
+                       dim3(jrq::kCrcFixedWideBlock), 0, stream, *args);
   else if (log_entry)
-    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<true, false>), dim3(grid), dim3(jrq::kCrcBlock), 0,
-                       stream, *args);
+    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<true, false, jrq::kCrcFixedBlock>), dim3(grid),
+                       dim3(jrq::kCrcFixedBlock), 0, stream, *args);
+  else if (wide)
+    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<false, false, jrq::kCrcFixedWideBlock>), dim3(grid),
+                       dim3(jrq::kCrcFixedWideBlock), 0, stream, *args);
   else
-    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<false, false>), dim3(grid), dim3(jrq::kCrcBlock), 0,
-                       stream, *args);
+    hipLaunchKernelGGL((jrq::crc64_fixed_kernel<false, false, jrq::kCrcFixedBlock>), dim3(grid),
+                       dim3(jrq::kCrcFixedBlock), 0, stream, *args);
   return hipGetLastError();
 }
 

@@ -400,7 +400,7 @@ __global__ void iota_offsets_kernel(uint64_t* off, uint32_t n, uint64_t entry_by
 uint32_t crc_fixed_k(const jrq_engine* e, const void* payload, uint64_t entry_bytes, uint32_t N) {
   if (entry_bytes < 256 || entry_bytes % 256 != 0 || (reinterpret_cast<uintptr_t>(payload) & 15u))
     return 0;
-  const uint64_t lanes = static_cast<uint64_t>(e->crc_grid) * jrq::kCrcBlock;
+  const uint64_t lanes = static_cast<uint64_t>(e->crc_grid) * jrq::kCrcFixedBlock;
   uint32_t k = 1;
   while (static_cast<uint64_t>(N) * k < lanes && k < 64 && (entry_bytes / (2 * k)) % 256 == 0) k *= 2;
   if (static_cast<uint64_t>(N) * k < lanes || entry_bytes / k >= (1ull << 26)) return 0;
@@ -1567,7 +1567,7 @@ int jrq_v2_decode_verify_dev(jrq_engine* e, const uint8_t* rec, const uint64_t* 
   v.blk = static_cast<uint64_t*>(blk);
   // (the fixed-size path hashes from the 128-B line of each data start: records 128-B aligned)
   v.lanes = (reinterpret_cast<uintptr_t>(rec) & 127u) ? ~0ull
-                                                     : static_cast<uint64_t>(e->crc_grid) * jrq::kCrcBlock;
+                                                     : static_cast<uint64_t>(e->crc_grid) * jrq::kCrcFixedBlock;
   JRQ_HIP(e, jrq_launch_v2_parse(&v, e->stream));  // (its last block writes the gate)
   // every record with the same data length (the common case: fixed-size commands): the data
   // ranges alone, k lanes per record (crc64_fixed_kernel at the data starts), finished in place

@@ -29,6 +29,16 @@ constexpr int kSliceTables = 8;
 constexpr int kCrcLdsBytes = 8 * 256 * 8 * 8;
 constexpr int kCrcBlock = 512;       // threads per workgroup (8 waves, 1 workgroup / CU)
 constexpr int kCrcRegsBlock = 768;   // the register boundary path's workgroup (crc64.hip)
+#ifndef JRQ_CRC_FIXED_BLOCK          // (A/B knob) the fixed-size kernel's workgroup
+#define JRQ_CRC_FIXED_BLOCK 512
+#endif
+constexpr int kCrcFixedBlock = JRQ_CRC_FIXED_BLOCK;
+#ifndef JRQ_CRC_FIXED_WIDE_BLOCK     // (A/B knob) its workgroup when one lane takes a whole entry
+#define JRQ_CRC_FIXED_WIDE_BLOCK 1024
+#endif
+constexpr int kCrcFixedWideBlock = JRQ_CRC_FIXED_WIDE_BLOCK;
+static_assert(kCrcLdsBytes / 8 % kCrcFixedBlock == 0 && kCrcLdsBytes / 8 % kCrcFixedWideBlock == 0,
+              "the table image splits evenly over the fixed kernel's threads");
 
 // Status flags, identical to include/jrq.h jrq_group_status.
 constexpr uint8_t kStNotLeader = 1, kStOutOfRange = 2, kStEmptyConf = 4;

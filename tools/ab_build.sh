@@ -14,5 +14,9 @@ for s in $crc $srcs; do
   objs="$objs $o"
 done
 wait
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/libjrq.so $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+# jrq_build_id(): the variant's own sources' hash (as the Makefile does for the product library)
+sha=$(python3 sofa-jraft_amd/jraft_amd/_srcsha.py $src)
+printf 'static const char id[] = "JRQ_BUILD_ID=%s";\nconst char *jrq_build_id(void) { return id + 13; }\n' $sha > $out/build_id.c
+gcc -O2 -fPIC -c $out/build_id.c -o $out/build_id.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/libjrq.so $objs $out/build_id.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "built $out/libjrq.so"
