@@ -1225,8 +1225,8 @@ def leg_c5(ctx, args, barrier, max_over_ranks, time_it=True):
            "offsets_path": {"ms_per_launch": vo_ms, "bit_exact_vs_oracle": ok_off,
                             "GBps_payload": pay / (vo_ms * 1e-3) / 1e9,
                             "how": "jrq_logentry_checksum_batch_dev (segment walk + finish kernel)"},
-           "roofline": roofline(alg_v, v_ms, kernel="crc64_fixed_kernel<true, false>",
-                                **pmc_traffic("C5", "crc64_fixed_kernel<true, false>"))}
+           "roofline": roofline(alg_v, v_ms, kernel="crc64_fixed_kernel<true, false, 512>",
+                                **pmc_traffic("C5", "crc64_fixed_kernel<true, false, 512>"))}
     per_rank_step_ok = ctx.gather(-1.0 if step_ok is None else float(step_ok))
     c5_step = {"workload": f"C5 as BASELINE states it: 64k regions x 3 replicas x 16 KiB entries "
                            f"per GPU ({n * world} regions over {world} GPU(s), region shards by "
@@ -1317,9 +1317,9 @@ def leg_v2(ctx, args, c5state):
                         f"field), decode + isCorrupted",
             "GBps_records": tot / (ms * 1e-3) / 1e9, "ms_per_batch": ms,
             "bit_exact_vs_oracle": ok, "oracle_decoder_sample_ok": sample_ok,
-            "roofline": roofline(alg, ms, kernel="v2_parse + crc64_fixed_kernel<true, true> (+ the "
+            "roofline": roofline(alg, ms, kernel="v2_parse + crc64_fixed_kernel<true, true, 512> (+ the "
                                                  "segment walk's two launches, which return at once)",
-                                 **pmc_traffic("v2", "v2_parse", "crc64_fixed_kernel<true, true>",
+                                 **pmc_traffic("v2", "v2_parse", "crc64_fixed_kernel<true, true, 512>",
                                                "crc64_rounds_kernel<768u, true>", "v2_finish"))}
 
 
@@ -1423,9 +1423,9 @@ def leg_c1(ctx, args):
                              "how": "jrq_logentry_checksum_batch_dev (segment walk + finish kernel)",
                              "frac": crc_bytes(n1, n1 * c1["entry_bytes"], verify=False) /
                              (off_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS},
-            "roofline": roofline(alg, crc_ms, kernel="crc64_fixed_kernel<true, false> (1M x 256 B LogEntries, "
+            "roofline": roofline(alg, crc_ms, kernel="crc64_fixed_kernel<true, false, 1024> (1M x 256 B LogEntries, "
                                                     "jrq_logentry_checksum_fixed_dev)",
-                                 **pmc_traffic("C1", "crc64_fixed_kernel<true, false>"))}
+                                 **pmc_traffic("C1", "crc64_fixed_kernel<true, false, 1024>"))}
 
 
 def leg_lease(ctx, args, quorum_conf_dev, G, P):

@@ -43,13 +43,13 @@ LEG_KERNELS = {
     "C2": (("C2", "batched_epochs", "roofline"), ["quorum_epochs_kernel<3,"]),
     "C2L": (("C2", "batched_epochs_64", "roofline"), ["quorum_epochs_kernel<3,"]),
     "C3K": (("C3_k_epochs", "roofline"), ["quorum_epochs_pair_kernel<5, false, true>"]),
-    "C5": (("crc64", "roofline"), ["crc64_fixed_kernel<true, false>"]),
-    "C1": (("C1", "roofline"), ["crc64_fixed_kernel<true, false>"]),
+    "C5": (("crc64", "roofline"), ["crc64_fixed_kernel<true, false, 512>"]),
+    "C1": (("C1", "roofline"), ["crc64_fixed_kernel<true, false, 1024>"]),
     "ae": (("next_rows", "append_entries_verify", "roofline"),
            ["ae_block_sums", "ae_scan_sums", "ae_meta", "crc64_rounds_kernel<512u, false>",
             "crc64_finish_kernel<true>", "ae_first_corrupt"]),
     "v2": (("next_rows", "v2_decode_verify", "roofline"),
-           ["v2_parse", "crc64_fixed_kernel<true, true>", "crc64_rounds_kernel<768u, true>",
+           ["v2_parse", "crc64_fixed_kernel<true, true, 512>", "crc64_rounds_kernel<768u, true>",
             "v2_finish"]),
     "snapshot": (("next_rows", "snapshot_stream_crc64", "roofline"),
                  ["crc64_rounds_kernel<512u, false>", "crc64_finish_kernel<false>"]),
