@@ -356,6 +356,19 @@ int jrq_table_stage_apply(jrq_table *t);
 #define JRQ_STATE_STAMP 2u
 int jrq_table_stage_reserve_acks(jrq_table *t, uint32_t max_acks, uint32_t max_segments);
 int jrq_table_stage_acks(jrq_table *t, uint64_t stamp, const uint64_t *acks, uint32_t n);
+/* Records streamed to the device while they are written (r06): a caller keeps device regions of
+ * the table (jrq_table_ack_region: `capacity` records, freed with the table or by
+ * jrq_table_ack_region_free, which synchronises), queues copies of page-locked records into them
+ * as they fill (jrq_table_ack_push: from any thread, concurrently with the table's other calls --
+ * it only queues an H2D copy on the engine's stream and reports failure by code alone; pageable
+ * memory is refused with JRQ_E_INVALID), and at the flush registers each segment where it lies
+ * (jrq_table_stage_acks_dev: `n` records at a device address, after jrq_table_stage_reserve_acks,
+ * whose max_acks then counts only the records copied by jrq_table_stage_acks).  The copies queued
+ * before jrq_table_stage_apply are on the stream ahead of the apply. */
+int jrq_table_ack_region(jrq_table *t, uint64_t capacity, uint64_t **region_out);
+int jrq_table_ack_region_free(jrq_table *t, uint64_t *region);
+int jrq_table_ack_push(jrq_table *t, uint64_t *region_dst, const uint64_t *host_src, uint32_t n);
+int jrq_table_stage_acks_dev(jrq_table *t, uint64_t stamp, const uint64_t *acks_dev, uint32_t n);
 
 /* One quorum epoch over every group of the table, state updated in place as BallotBox.commitAt
  * leaves it (BallotBox.java:96-139; commit -> lastCommittedIndex, pendingIndex = commit + 1).

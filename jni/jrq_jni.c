@@ -197,6 +197,26 @@ JNIEXPORT jint FN(tableStageAcks)(JNIEnv *env, jclass cls, jlong table, jlong st
     return jrq_jni_table_stage_acks(ENG(table), stamp, ADDR(acks), n);
 }
 
+/* regionOut: a direct buffer of one long receiving the region's device address */
+JNIEXPORT jint FN(tableAckRegion)(JNIEnv *env, jclass cls, jlong table, jlong capacity,
+                                  jobject regionOut) {
+    (void)cls;
+    return jrq_jni_table_ack_region(ENG(table), capacity, ADDR(regionOut));
+}
+
+JNIEXPORT jint FN(tableAckRegionFree)(JNIEnv *env, jclass cls, jlong table, jlong region) {
+    (void)env;
+    (void)cls;
+    return jrq_jni_table_ack_region_free(ENG(table), ENG(region));
+}
+
+/* from any thread: the calling thread's page-locked record buffer, from element `from` */
+JNIEXPORT jint FN(tableAckPush)(JNIEnv *env, jclass cls, jlong table, jlong regionDst, jobject records,
+                                jint from, jint n) {
+    (void)cls;
+    return jrq_jni_table_ack_push(ENG(table), ENG(regionDst), ADDR(records), from, n);
+}
+
 /* returns the number of changed groups (>= 0) or a negative jrq_error */
 JNIEXPORT jint FN(tableEpoch)(JNIEnv *env, jclass cls, jlong table, jobject changed,
                               jobject statusOut) {

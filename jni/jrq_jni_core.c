@@ -176,6 +176,28 @@ int32_t jrq_jni_table_stage_acks(jrq_addr table, int64_t stamp, jrq_addr acks, i
                                 (uint32_t)n);
 }
 
+int32_t jrq_jni_table_ack_region(jrq_addr table, int64_t capacity, jrq_addr region_out) {
+    uint64_t *r = NULL;
+    int rc;
+    if (capacity <= 0 || !region_out) return JRQ_E_INVALID;
+    rc = jrq_table_ack_region(A(jrq_table *, table), (uint64_t)capacity, &r);
+    if (rc == JRQ_OK) *A(jrq_addr *, region_out) = (jrq_addr)(intptr_t)r;
+    return rc;
+}
+
+int32_t jrq_jni_table_ack_region_free(jrq_addr table, jrq_addr region) {
+    return jrq_table_ack_region_free(A(jrq_table *, table), A(uint64_t *, region));
+}
+
+int32_t jrq_jni_table_ack_push(jrq_addr table, jrq_addr region_dst, jrq_addr host_src, int32_t from,
+                               int32_t n) {
+    N(from);
+    N(n);
+    if (!region_dst || !host_src) return JRQ_E_INVALID;
+    return jrq_table_ack_push(A(jrq_table *, table), A(uint64_t *, region_dst) + from,
+                              A(const uint64_t *, host_src) + from, (uint32_t)n);
+}
+
 int32_t jrq_jni_table_epoch(jrq_addr table, jrq_addr changed, jrq_addr status_out) {
     uint32_t n = 0;
     int rc = jrq_table_epoch(A(jrq_table *, table), A(uint64_t *, changed), &n,

@@ -67,6 +67,14 @@ int32_t jrq_jni_table_stage(jrq_addr table, jrq_addr states, int32_t n_states, j
 int32_t jrq_jni_table_stage_apply(jrq_addr table);
 int32_t jrq_jni_table_stage_reserve_acks(jrq_addr table, int32_t max_acks, int32_t max_segments);
 int32_t jrq_jni_table_stage_acks(jrq_addr table, int64_t stamp, jrq_addr acks, int32_t n);
+/* records streamed while they are written: region_out is the address of
+ * one jrq_addr word receiving the region's device address; ack_push may be called from any
+ * thread (host_src: a page-locked direct buffer's address) */
+int32_t jrq_jni_table_ack_region(jrq_addr table, int64_t capacity, jrq_addr region_out);
+int32_t jrq_jni_table_ack_region_free(jrq_addr table, jrq_addr region);
+/* records [from, from + n) of the buffer at host_src to the same positions of the region */
+int32_t jrq_jni_table_ack_push(jrq_addr table, jrq_addr region_dst, jrq_addr host_src, int32_t from,
+                               int32_t n);
 /* returns the number of changed groups written to `changed` (>= 0), or a jrq_error */
 int32_t jrq_jni_table_epoch(jrq_addr table, jrq_addr changed, jrq_addr status_out);
 int32_t jrq_jni_table_read(jrq_addr table, jrq_addr pending_index, jrq_addr last_appended,

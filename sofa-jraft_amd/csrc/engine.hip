@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -45,7 +46,7 @@ extern "C" hipError_t jrq_launch_table_fsm(const JrqTableArgs* a, const uint32_t
 extern "C" hipError_t jrq_launch_table_fan_gather(const int64_t* ff, const uint8_t* fs, const uint32_t* n,
                                                   const uint32_t* off, uint32_t slices, int64_t* out_first,
                                                   uint8_t* out_status, hipStream_t stream);
-extern "C" hipError_t jrq_launch_table_acks(const JrqTableArgs* a, const uint64_t* acks, uint32_t n,
+extern "C" hipError_t jrq_launch_table_acks(const JrqTableArgs* a, const uint64_t* const* seg_ptr, uint32_t n,
                                             const uint32_t* seg_off, const uint64_t* seg_stamp,
                                             uint32_t nseg, hipStream_t stream);
 extern "C" hipError_t jrq_launch_table_list_gather(const uint64_t* changed, const uint32_t* n,
@@ -1676,10 +1677,15 @@ struct jrq_table {
   uint64_t staged_s = 0, staged_r = 0;        // headers / records staged since the last apply
   DevBuf ack_stage, seg_stage;                // order-free ack records (jrq_table_stage_acks)
   DevBuf fsm_stage;                           // jrq_table_fsm_update (host variant)
-  uint64_t stage_cap_a = 0, staged_a = 0;
+  uint64_t stage_cap_a = 0, staged_a = 0;    // records copied into ack_stage
+  uint64_t ack_total = 0;                     // records of every staged segment
   uint32_t stage_cap_seg = 0;
-  std::vector<uint32_t> seg_off;              // staged segments: first record, stamp
-  std::vector<uint64_t> seg_stamp;
+  std::vector<uint32_t> seg_off;              // staged segments: first record (over all), stamp,
+  std::vector<uint64_t> seg_stamp;            // where its records are (ack_stage or a region)
+  std::vector<uint64_t> seg_ptr;
+  uint64_t seg_last_n = 0;                    // the last segment's record count (merging)
+  std::vector<void*> regions;                 // jrq_table_ack_region allocations
+  std::mutex regions_mu;
   size_t state_bytes = 0;     // the rows at the start of mem (jrq_table_copy)
 };
 
@@ -1777,6 +1783,7 @@ void jrq_table_destroy(jrq_table* t) {
     (void)hipStreamSynchronize(t->e->stream);
     for (DevBuf* b : {&t->st_stage, &t->rec_stage, &t->changed_stage, &t->ack_stage, &t->seg_stage, &t->fsm_stage})
       if (b->p) (void)hipFree(b->p);
+    for (void* r : t->regions) (void)hipFree(r);
     if (t->mem) (void)hipFree(t->mem);
     if (t->n_dev) (void)hipFree(t->n_dev);
     if (t->n_host) (void)hipHostFree(t->n_host);
@@ -1886,43 +1893,68 @@ int jrq_table_stage(jrq_table* t, const jrq_group_state* states, uint32_t n_stat
 
 int jrq_table_stage_apply(jrq_table* t) {
   if (table_check(t)) return JRQ_E_INVALID;
-  const uint64_t ns = t->staged_s, nr = t->staged_r, na = t->staged_a;
-  t->staged_s = t->staged_r = t->staged_a = 0;
+  const uint64_t ns = t->staged_s, nr = t->staged_r, na = t->ack_total;
+  t->staged_s = t->staged_r = t->staged_a = t->ack_total = 0;
   int rc;
   if ((ns || nr) &&
       (rc = jrq_table_update_dev(t, static_cast<const jrq_group_state*>(t->st_stage.p), static_cast<uint32_t>(ns),
                                  static_cast<const uint64_t*>(t->rec_stage.p), static_cast<uint32_t>(nr))))
     return rc;
-  if (na) {  // the ack segments' starts and stamps, then one launch over every record
+  if (na) {  // the ack segments' stamps, places and starts, then one launch over every record
     jrq_engine* e = t->e;
     DeviceGuard guard(e->device);
     const uint32_t nseg = static_cast<uint32_t>(t->seg_off.size());
     uint64_t* ds = static_cast<uint64_t*>(t->seg_stage.p);
-    uint32_t* doff = reinterpret_cast<uint32_t*>(ds + t->stage_cap_seg);
+    uint64_t* dp = ds + t->stage_cap_seg;
+    uint32_t* doff = reinterpret_cast<uint32_t*>(dp + t->stage_cap_seg);
     if ((rc = upload_any(e, ds, t->seg_stamp.data(), nseg * 8))) return rc;
+    if ((rc = upload_any(e, dp, t->seg_ptr.data(), nseg * 8))) return rc;
     if ((rc = upload_any(e, doff, t->seg_off.data(), nseg * 4))) return rc;
-    JRQ_HIP(e, jrq_launch_table_acks(&t->a, static_cast<const uint64_t*>(t->ack_stage.p), static_cast<uint32_t>(na),
+    JRQ_HIP(e, jrq_launch_table_acks(&t->a, reinterpret_cast<const uint64_t* const*>(dp), static_cast<uint32_t>(na),
                                      doff, ds, nseg, e->stream));
   }
   t->seg_off.clear();
   t->seg_stamp.clear();
+  t->seg_ptr.clear();
   return JRQ_OK;
 }
+
+namespace {
+// One staged segment of order-free records at device address p: merged into the last one when it
+// has the same stamp and continues it in memory.
+int add_ack_segment(jrq_table* t, uint64_t stamp, const uint64_t* p, uint32_t n) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  if (!t->seg_stamp.empty() && t->seg_stamp.back() == stamp && t->seg_ptr.back() + 8 * t->seg_last_n == a) {
+    t->seg_last_n += n;
+  } else {
+    if (t->seg_off.size() + 1 > t->stage_cap_seg)
+      return fail(t->e, JRQ_E_STATE, "table: ack segments beyond jrq_table_stage_reserve_acks");
+    if (t->ack_total + n > 0xFFFFFFFFull) return fail(t->e, JRQ_E_STATE, "table: more than 2^32 ack records");
+    t->seg_off.push_back(static_cast<uint32_t>(t->ack_total));
+    t->seg_stamp.push_back(stamp);
+    t->seg_ptr.push_back(a);
+    t->seg_last_n = n;
+  }
+  t->ack_total += n;
+  return JRQ_OK;
+}
+}  // namespace
 
 int jrq_table_stage_reserve_acks(jrq_table* t, uint32_t max_acks, uint32_t max_segments) {
   if (table_check(t)) return JRQ_E_INVALID;
   jrq_engine* e = t->e;
-  t->staged_a = 0;  // acks staged and never applied (a failed flush) are dropped
+  t->staged_a = t->ack_total = 0;  // acks staged and never applied (a failed flush) are dropped
   t->seg_off.clear();
   t->seg_stamp.clear();
+  t->seg_ptr.clear();
   if (max_segments == 0) max_segments = 1;
   DeviceGuard guard(e->device);
   int rc;
   void* p = nullptr;
   if ((rc = stage_buf(e, t->ack_stage, static_cast<size_t>(max_acks) * 8, &p))) return rc;
-  if ((rc = stage_buf(e, t->seg_stage, static_cast<size_t>(max_segments) * 12, &p))) return rc;
+  if ((rc = stage_buf(e, t->seg_stage, static_cast<size_t>(max_segments) * 20, &p))) return rc;
   t->stage_cap_a = t->ack_stage.cap / 8;
-  t->stage_cap_seg = static_cast<uint32_t>(t->seg_stage.cap / 12);
+  t->stage_cap_seg = static_cast<uint32_t>(t->seg_stage.cap / 20);
   return JRQ_OK;
 }
 
@@ -1931,18 +1963,67 @@ int jrq_table_stage_acks(jrq_table* t, uint64_t stamp, const uint64_t* acks, uin
   jrq_engine* e = t->e;
   if (n && !acks) return fail(e, JRQ_E_INVALID, "null ack array");
   if (n == 0) return JRQ_OK;
-  const bool merge = !t->seg_stamp.empty() && t->seg_stamp.back() == stamp;
-  if (t->staged_a + n > t->stage_cap_a || (!merge && t->seg_off.size() + 1 > t->stage_cap_seg))
+  if (t->staged_a + n > t->stage_cap_a)
     return fail(e, JRQ_E_STATE, "table: ack staging beyond jrq_table_stage_reserve_acks");
   DeviceGuard guard(e->device);
   int rc;
-  if ((rc = upload_any(e, static_cast<uint64_t*>(t->ack_stage.p) + t->staged_a, acks, static_cast<size_t>(n) * 8)))
-    return rc;
-  if (!merge) {
-    t->seg_off.push_back(static_cast<uint32_t>(t->staged_a));
-    t->seg_stamp.push_back(stamp);
-  }
+  uint64_t* dst = static_cast<uint64_t*>(t->ack_stage.p) + t->staged_a;
+  if ((rc = add_ack_segment(t, stamp, dst, n))) return rc;
+  if ((rc = upload_any(e, dst, acks, static_cast<size_t>(n) * 8))) return rc;
   t->staged_a += n;
+  return JRQ_OK;
+}
+
+int jrq_table_stage_acks_dev(jrq_table* t, uint64_t stamp, const uint64_t* acks_dev, uint32_t n) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  if (n && !acks_dev) return fail(t->e, JRQ_E_INVALID, "null ack array");
+  if (n == 0) return JRQ_OK;
+  return add_ack_segment(t, stamp, acks_dev, n);
+}
+
+int jrq_table_ack_region(jrq_table* t, uint64_t capacity, uint64_t** region_out) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  if (!region_out || capacity == 0) return fail(t->e, JRQ_E_INVALID, "ack region: null output or zero capacity");
+  DeviceGuard guard(t->e->device);
+  void* p = nullptr;
+  if (hipMalloc(&p, capacity * 8) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(t->e, JRQ_E_NOMEM, "ack region of %llu records", static_cast<unsigned long long>(capacity));
+  }
+  {
+    std::lock_guard<std::mutex> l(t->regions_mu);
+    t->regions.push_back(p);
+  }
+  *region_out = static_cast<uint64_t*>(p);
+  return JRQ_OK;
+}
+
+int jrq_table_ack_region_free(jrq_table* t, uint64_t* region) {
+  if (table_check(t)) return JRQ_E_INVALID;
+  {
+    std::lock_guard<std::mutex> l(t->regions_mu);
+    auto it = std::find(t->regions.begin(), t->regions.end(), static_cast<void*>(region));
+    if (it == t->regions.end()) return fail(t->e, JRQ_E_INVALID, "not an ack region of this table");
+    t->regions.erase(it);
+  }
+  DeviceGuard guard(t->e->device);
+  JRQ_HIP(t->e, hipStreamSynchronize(t->e->stream));  // (copies into it or reads of it may be queued)
+  JRQ_HIP(t->e, hipFree(region));
+  return JRQ_OK;
+}
+
+int jrq_table_ack_push(jrq_table* t, uint64_t* region_dst, const uint64_t* host_src, uint32_t n) {
+  // callable from any thread, concurrently with the table's other calls: it only queues a copy
+  // on the engine's stream, and reports errors by code alone (no shared error text)
+  if (!t || !t->e || (n && (!region_dst || !host_src))) return JRQ_E_INVALID;
+  if (n == 0) return JRQ_OK;
+  if (!t->e->upload_pageable && !host_pinned(host_src)) return JRQ_E_INVALID;
+  DeviceGuard guard(t->e->device);
+  if (hipMemcpyAsync(region_dst, host_src, static_cast<size_t>(n) * 8, hipMemcpyHostToDevice, t->e->stream) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    return JRQ_E_HIP;
+  }
   return JRQ_OK;
 }
 

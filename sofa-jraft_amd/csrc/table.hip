@@ -731,24 +731,27 @@ __global__ __launch_bounds__(256) void table_recs_kernel(JrqTableArgs t, const u
 // whose low 32 bits the record carries; a match raises its slot's u32 word (against the group's
 // match base, saturating: below the base it changes nothing), a lastAppended the group's queue
 // end -- both as atomic maxima, so records apply in any order.
-__global__ __launch_bounds__(256) void table_acks_kernel(JrqTableArgs t, const uint64_t* __restrict__ acks,
+// Record i of the update: in segment s (the last whose first record seg_off[s] is <= i), at
+// seg_ptr[s][i - seg_off[s]] -- a segment's records are contiguous wherever they are (the staging
+// buffer, or a caller's device region filled by jrq_table_ack_push).
+__global__ __launch_bounds__(256) void table_acks_kernel(JrqTableArgs t, const uint64_t* const* __restrict__ seg_ptr,
                                                          uint32_t n, const uint32_t* __restrict__ seg_off,
                                                          const uint64_t* __restrict__ seg_stamp, uint32_t nseg) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
-  const uint64_t r = acks[i];
+  uint32_t lo = 0, hi = nseg;  // the last segment starting at or before i
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (seg_off[mid] <= i) lo = mid;
+    else hi = mid;
+  }
+  const uint64_t r = seg_ptr[lo][i - seg_off[lo]];
   const uint32_t f = static_cast<uint32_t>(r & 31u);
   const uint32_t g = static_cast<uint32_t>(r >> 5) & ((1u << 27) - 1u);
   const uint32_t low = static_cast<uint32_t>(r >> 32);
   if (g >= t.G || f > 16u || (f < 16u && f >= t.P)) {
     atomicAdd(t.invalid, 1u);
     return;
-  }
-  uint32_t lo = 0, hi = nseg;  // the last segment starting at or before i
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (seg_off[mid] <= i) lo = mid;
-    else hi = mid;
   }
   if (seg_stamp[lo] < t.rstamp[g]) return;  // recorded before the group's last reset
   const int64_t pr = tf(t.pi, t, g), lc = tf(t.lc, t, g);
@@ -772,10 +775,10 @@ __global__ __launch_bounds__(256) void table_acks_kernel(JrqTableArgs t, const u
 }  // namespace jrq
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t jrq_launch_table_acks(
-    const JrqTableArgs* a, const uint64_t* acks, uint32_t n, const uint32_t* seg_off,
+    const JrqTableArgs* a, const uint64_t* const* seg_ptr, uint32_t n, const uint32_t* seg_off,
     const uint64_t* seg_stamp, uint32_t nseg, hipStream_t stream) {
   if (n)
-    hipLaunchKernelGGL(jrq::table_acks_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, *a, acks, n,
+    hipLaunchKernelGGL(jrq::table_acks_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, *a, seg_ptr, n,
                        seg_off, seg_stamp, nseg);
   return hipGetLastError();
 }

@@ -143,10 +143,11 @@ extern "C" {
 
 const char* jraft_drive_last_error(void) { return g_err.c_str(); }
 
-// stats_out[k * 14 + i]: 0 api_ms, 1 pack_ms, 2 device_ms, 3 deliver_ms, 4 flush_ms,
+// stats_out[k * 17 + i]: 0 api_ms, 1 pack_ms, 2 device_ms, 3 deliver_ms, 4 flush_ms,
 // 5 h2d_bytes, 6 d2h_bytes, 7 states, 8 records (pack + call-time), 9 changed, 10 api_calls,
 // 11 acks (the call-time order-free records among them), 12 deliver_apply_ms, 13
-// deliver_callbacks_ms (the slowest deliver worker's two passes)
+// deliver_callbacks_ms (the slowest deliver worker's two passes), 14 pack_wait_ms, 15
+// pack_apply_ms, 16 acks_streamed
 //
 // jraft_drive_epochs_sharded -- the same over `shards` engines on `device` in one process
 // (ShardedGroupBatch: contiguous group blocks, the shards' epochs concurrent on their streams);
@@ -176,6 +177,10 @@ int jraft_drive_epochs_sharded(int device, uint32_t shards, uint32_t G, uint32_t
     boxes.reserve(G);
     // (JRAFT_DRIVE_FLUSH_THREADS: the flush pool's size, for tools/drive_ab.py; unset: the
     // batch's default)
+    // (JRAFT_DRIVE_ACK_CHUNK: records a calling thread streams to the device at once, 0 = never
+    // during the calls -- every record then goes up at the flush; tools/drive_ab.py A/B only)
+    if (const char* ac = std::getenv("JRAFT_DRIVE_ACK_CHUNK"))
+      jraft::testing::ackChunkRecords.store(std::atoi(ac) > 0 ? static_cast<uint32_t>(std::atoi(ac)) : 0xFFFFFFFFu);
     const char* ft = std::getenv("JRAFT_DRIVE_FLUSH_THREADS");
     const unsigned fthreads = ft ? static_cast<unsigned>(std::atoi(ft)) : 0u;
     if (S == 1) {
@@ -281,8 +286,8 @@ int jraft_drive_epochs_sharded(int device, uint32_t shards, uint32_t G, uint32_t
             throw std::runtime_error("published snapshot of group " + std::to_string(g) + " on engine " +
                                      std::to_string(k % S) + " differs from its getLastCommittedIndex");
       }
-      double* o = stats_out + static_cast<size_t>(k) * 14;
-      std::fill(o, o + 14, 0.0);
+      double* o = stats_out + static_cast<size_t>(k) * 17;
+      std::fill(o, o + 17, 0.0);
       for (uint32_t i = 0; i < S; ++i) {
         const jraft::FlushStats& s = sharded ? sharded->lastFlush(i) : batch->lastFlush();
         o[1] = std::max(o[1], s.pack_ms);
@@ -296,6 +301,9 @@ int jraft_drive_epochs_sharded(int device, uint32_t shards, uint32_t G, uint32_t
         o[9] += s.changed;
         o[12] = std::max(o[12], s.deliver_apply_ms);
         o[13] = std::max(o[13], s.deliver_callbacks_ms);
+        o[14] = std::max(o[14], s.pack_wait_ms);
+        o[15] = std::max(o[15], s.pack_apply_ms);
+        o[16] += s.acks_streamed;
       }
       o[0] = ms(t1 - t0);
       o[4] = ms(t2 - t1);

@@ -25,6 +25,7 @@ namespace jraft {
 namespace testing {
 void (*fastPathHook)() = nullptr;
 void (*slotAssignHook)() = nullptr;
+std::atomic<uint32_t> ackChunkRecords{GroupBatch::kAckChunk};
 }  // namespace testing
 
 namespace {
@@ -353,6 +354,12 @@ struct alignas(128) GroupBatch::DirtyList {
   // records, in segments (first record, reset stamp) of seg[i]
   PinnedBuf<uint64_t> ack[2];
   uint32_t nack[2] = {};
+  // ack[i]'s device region (jrq_table_ack_region, as many records as ack[i].cap; set before the
+  // capacity is published) and how many of its records the thread has pushed there so far: full
+  // chunks go up while the thread writes (jrq_table_ack_push), the flush pushes the rest
+  uint64_t* dack[2] = {};
+  size_t dcap[2] = {};
+  uint32_t shipped[2] = {};
   std::vector<std::pair<uint32_t, uint64_t>> seg[2];
 };
 
@@ -678,7 +685,29 @@ bool GroupBatch::appendAck(DirtyList* l, uint32_t t, uint64_t rec) {
   if (sg.empty() || sg.back().second != R) sg.emplace_back(n, R);
   l->ack[i].p[n] = rec;
   l->nack[i] = n + 1;
+  // a full chunk goes up now, on the engine's stream, while the thread goes on writing: the
+  // flush then has only the last partial chunk to copy (a failed push leaves it to the flush)
+  if (l->dack[i] && n + 1 - l->shipped[i] >= testing::ackChunkRecords.load(std::memory_order_relaxed) &&
+      jrq_table_ack_push(table_, l->dack[i] + l->shipped[i], l->ack[i].p + l->shipped[i],
+                         n + 1 - l->shipped[i]) == JRQ_OK)
+    l->shipped[i] = n + 1;
   return true;
+}
+
+// The device region behind a thread's record buffer of parity i, as large as the buffer (on the
+// flushing thread, between the buffer's uses).
+void GroupBatch::ensureRegion(DirtyList& l, uint32_t i, size_t cap) {
+  if (!table_ || cap == 0 || l.dcap[i] >= cap) return;
+  if (l.dack[i]) {
+    (void)jrq_table_ack_region_free(table_, l.dack[i]);
+    l.dack[i] = nullptr;
+    l.dcap[i] = 0;
+  }
+  uint64_t* r = nullptr;
+  if (jrq_table_ack_region(table_, cap, &r) == JRQ_OK && r) {  // else the staging copy path
+    l.dack[i] = r;
+    l.dcap[i] = cap;
+  }
 }
 
 void GroupBatch::stampReset(uint32_t g) {
@@ -950,6 +979,7 @@ uint32_t GroupBatch::flushLocked() {
                                                  // its reuse in generation t + 2)
   packGen_ = t;
   waitRegions();
+  const auto tw = clk::now();
   size_t nl;
   std::vector<DirtyList*> taken;  // the lists whose generation-t records this flush ships
   {
@@ -980,8 +1010,10 @@ uint32_t GroupBatch::flushLocked() {
       // the groups it listed, each a queue size and P acks at most
       const size_t used = std::max<size_t>(l->nack[ti], work_[i].size() * (P_ + 1));
       l->nack[ti] = 0;
+      l->shipped[ti] = 0;
       l->seg[ti].clear();
       l->ack[ti].reserve(std::max<size_t>(used + used / 2, 1u << 14));
+      ensureRegion(*l, ti, l->ack[ti].cap);
       // a thread's first buffer of the generation now in use (t + 1): nothing writes a buffer
       // of capacity 0, so it can be published now -- pointer first, capacity last (release)
       PinnedBuf<uint64_t>& nx = l->ack[ti ^ 1u];
@@ -990,6 +1022,7 @@ uint32_t GroupBatch::flushLocked() {
         void* q = nullptr;
         if (jrq_host_alloc(want * sizeof(uint64_t), &q) == JRQ_OK && q) {
           nx.p = static_cast<uint64_t*>(q);
+          ensureRegion(*l, ti ^ 1u, want);  // (before the capacity is published)
           __atomic_store_n(&nx.cap, want, __ATOMIC_RELEASE);
         }
       }
@@ -1025,15 +1058,33 @@ uint32_t GroupBatch::flushLocked() {
     throwIfError(jrq_table_stage_reserve(table_, static_cast<uint32_t>(nd + 1),
                                          static_cast<uint32_t>(nd * (P_ + 1) + 1)),
                  eng_->raw(), "jrq_table_stage_reserve");
-    // the order-free records first: their DMA (page-locked, as written) overlaps the pack
-    throwIfError(jrq_table_stage_reserve_acks(table_, static_cast<uint32_t>(nacks), static_cast<uint32_t>(nsegs + 1)),
+    // the order-free records first: the threads streamed their full chunks to their device
+    // regions while writing them (on the engine's stream, ahead of everything below); the rest
+    // goes up now, and every segment is registered where it lies.  A thread without a region
+    // (its first generation) has its records copied through the staging buffer.
+    size_t ncopy = 0;
+    for (DirtyList* l : taken)
+      if (!l->dack[ti]) ncopy += l->nack[ti];
+    throwIfError(jrq_table_stage_reserve_acks(table_, static_cast<uint32_t>(ncopy), static_cast<uint32_t>(nsegs + 1)),
                  eng_->raw(), "jrq_table_stage_reserve_acks");
     for (DirtyList* l : taken) {
+      const uint32_t na = l->nack[ti];
+      uint64_t* const dr = l->dack[ti];
+      stats.acks_streamed += dr ? l->shipped[ti] : 0u;
+      if (dr && na > l->shipped[ti]) {
+        throwIfError(jrq_table_ack_push(table_, dr + l->shipped[ti], l->ack[ti].p + l->shipped[ti], na - l->shipped[ti]),
+                     eng_->raw(), "jrq_table_ack_push");
+        l->shipped[ti] = na;
+      }
       const auto& sg = l->seg[ti];
       for (size_t k = 0; k < sg.size(); ++k) {
-        const uint32_t b = sg[k].first, e = k + 1 < sg.size() ? sg[k + 1].first : l->nack[ti];
-        throwIfError(jrq_table_stage_acks(table_, sg[k].second, l->ack[ti].p + b, e - b), eng_->raw(),
-                     "jrq_table_stage_acks");
+        const uint32_t b = sg[k].first, e = k + 1 < sg.size() ? sg[k + 1].first : na;
+        if (dr)
+          throwIfError(jrq_table_stage_acks_dev(table_, sg[k].second, dr + b, e - b), eng_->raw(),
+                       "jrq_table_stage_acks_dev");
+        else
+          throwIfError(jrq_table_stage_acks(table_, sg[k].second, l->ack[ti].p + b, e - b), eng_->raw(),
+                       "jrq_table_stage_acks");
       }
     }
     stats.acks = static_cast<uint32_t>(nacks);
@@ -1098,7 +1149,10 @@ uint32_t GroupBatch::flushLocked() {
         }
       });
     }
+    const auto ta0 = clk::now();
     throwIfError(jrq_table_stage_apply(table_), eng_->raw(), "jrq_table_stage_apply");
+    stats.pack_wait_ms = std::chrono::duration<double, std::milli>(tw - t0).count();
+    stats.pack_apply_ms = std::chrono::duration<double, std::milli>(clk::now() - ta0).count();
     t1 = clk::now();
     throwIfError(jrq_table_epoch(table_, changed_.p, &n, nullptr), eng_->raw(), "jrq_table_epoch");
     recycleAcks();

@@ -362,12 +362,16 @@ struct FlushStats {
   uint32_t states = 0;       // group headers uploaded (96 B each)
   uint32_t records = 0;      // 8-B update records uploaded (changed acks / queue sizes)
   uint32_t acks = 0;         // 8-B order-free records written at call time (JRQ_ACK)
+  uint32_t acks_streamed = 0;  // of them, pushed to the device by the calling threads themselves
   uint32_t changed = 0;      // groups whose commit advanced (8-B entries downloaded)
   uint64_t h2d_bytes = 0, d2h_bytes = 0;
   double pack_ms = 0, device_ms = 0, deliver_ms = 0;
   // the slowest deliver worker's two passes: commits applied under the groups' locks, then the
   // closures and onCommitted callbacks
   double deliver_apply_ms = 0, deliver_callbacks_ms = 0;
+  // inside pack_ms: ending the generation (its call regions drained), and the apply call (which
+  // waits for the records' copies ahead of it on the stream)
+  double pack_wait_ms = 0, pack_apply_ms = 0;
 };
 
 // When the background flusher (GroupBatch::startFlusher) runs an epoch: as soon as the oldest
@@ -407,6 +411,7 @@ struct FlushPolicy {
 // flush() or clearPendingTasks() of this batch (std::logic_error).
 class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
  public:
+  static constexpr uint32_t kAckChunk = 1u << 15;  // records a thread pushes to the device at once
   // eng may be null until the first flush() (host-only state checks need no GPU)
   GroupBatch(Engine* eng, uint32_t groups, uint32_t peers);
   ~GroupBatch();
@@ -459,6 +464,7 @@ class GroupBatch : public std::enable_shared_from_this<GroupBatch> {
   struct Part;       // one pack worker's share of a flush
   struct Delivery;   // one deliver worker's commits and callbacks
   static constexpr uint32_t kNoPeer = 0xFFFFFFFFu;
+  void ensureRegion(DirtyList& l, uint32_t i, size_t cap);
   static constexpr uint32_t kDirtyLa = 1u << 16, kDirtyHeader = 1u << 17, kDirtyReset = 1u << 18;
 
   // One group's record: what every API call and the flush touch, in one or two adjacent cache
@@ -635,6 +641,9 @@ extern void (*fastPathHook)();
 // Called under the group's lock right after a slot is given to a peer (its id published), when
 // set: a test acks from that peer on the fast path there.  Null in production.
 extern void (*slotAssignHook)();
+// Records a calling thread pushes to the device at once (GroupBatch::kAckChunk); tests make it
+// small so that the pushes interleave with everything else.
+extern std::atomic<uint32_t> ackChunkRecords;
 }  // namespace testing
 
 }  // namespace jraft

@@ -168,6 +168,10 @@ SIGNATURES = [
     ("jrq_table_slices", C.c_uint32, [_V]),
     ("jrq_table_stage_reserve_acks", C.c_int, [_V, C.c_uint32, C.c_uint32]),
     ("jrq_table_committed_dev", C.c_int, [_V, _V]),
+    ("jrq_table_ack_region", C.c_int, [_V, C.c_uint64, _V]),
+    ("jrq_table_ack_region_free", C.c_int, [_V, _V]),
+    ("jrq_table_ack_push", C.c_int, [_V, _V, _V, C.c_uint32]),
+    ("jrq_table_stage_acks_dev", C.c_int, [_V, C.c_uint64, _V, C.c_uint32]),
     ("jrq_table_fsm_update", C.c_int, [_V, _V, _V, _V, _V, C.c_uint32]),
     ("jrq_table_fsm_update_dev", C.c_int, [_V, _V, _V, _V, _V, C.c_uint32]),
     ("jrq_table_fsm_read", C.c_int, [_V, _V, _V, _V]),

@@ -18,7 +18,8 @@ DRIVE_PATH = os.environ.get("JRAFT_AMD_AB_DRIVE") or os.path.join(
 # time as order-free JRQ_ACK records (include/jrq.h), without a pack pass
 STATS = ("api_ms", "pack_ms", "device_ms", "deliver_ms", "flush_ms", "h2d_bytes", "d2h_bytes",
          "states", "records", "changed", "api_calls", "acks", "deliver_apply_ms",
-         "deliver_callbacks_ms")
+         "deliver_callbacks_ms", "pack_wait_ms", "pack_apply_ms",
+         "acks_streamed")
 _drv = None
 
 

@@ -43,6 +43,7 @@ struct jrq_table {
   std::vector<uint64_t> staged_r;
   std::vector<uint64_t> rstamp;           // JRQ_STATE_STAMP per group
   std::vector<uint64_t> staged_a;         // jrq_table_stage_acks: records, segments
+  std::vector<uint64_t*> regions;         // jrq_table_ack_region (freed with the table)
   std::vector<std::pair<size_t, uint64_t>> segs;
 };
 
@@ -111,7 +112,11 @@ jrq_table* jrq_table_create(jrq_engine* e, uint32_t G, uint32_t P, int* err) {
   if (err) *err = JRQ_OK;
   return t;
 }
-void jrq_table_destroy(jrq_table* t) { delete t; }
+void jrq_table_destroy(jrq_table* t) {
+  if (!t) return;
+  for (uint64_t* r : t->regions) delete[] r;
+  delete t;
+}
 
 // Failure injection for the host tests (tests/cpp/host_test.cpp testFlushFailureRelists): the
 // next `n` update calls fail as a lost device would, after applying nothing.
@@ -214,6 +219,30 @@ int jrq_table_stage_acks(jrq_table* t, uint64_t stamp, const uint64_t* acks, uin
   t->segs.emplace_back(t->staged_a.size(), stamp);
   t->staged_a.insert(t->staged_a.end(), acks, acks + n);
   return JRQ_OK;
+}
+
+// Streamed records (jrq_table_ack_region / _push / jrq_table_stage_acks_dev): regions are host
+// memory here and a push copies at once (it touches no table state: callable from any thread).
+int jrq_table_ack_region(jrq_table* t, uint64_t capacity, uint64_t** region_out) {
+  std::lock_guard<std::mutex> l(t->mu);
+  *region_out = new uint64_t[capacity];
+  t->regions.push_back(*region_out);
+  return JRQ_OK;
+}
+int jrq_table_ack_region_free(jrq_table* t, uint64_t* region) {
+  std::lock_guard<std::mutex> l(t->mu);
+  auto it = std::find(t->regions.begin(), t->regions.end(), region);
+  if (it == t->regions.end()) return JRQ_E_INVALID;
+  t->regions.erase(it);
+  delete[] region;
+  return JRQ_OK;
+}
+int jrq_table_ack_push(jrq_table*, uint64_t* dst, const uint64_t* src, uint32_t n) {
+  std::memcpy(dst, src, static_cast<size_t>(n) * 8);
+  return JRQ_OK;
+}
+int jrq_table_stage_acks_dev(jrq_table* t, uint64_t stamp, const uint64_t* acks, uint32_t n) {
+  return jrq_table_stage_acks(t, stamp, acks, n);
 }
 
 int jrq_table_stage_apply(jrq_table* t) {

@@ -1392,6 +1392,18 @@ int main(int argc, char** argv) {
     tests.push_back({"testConcurrentCallers", [&] { testConcurrentCallers(e, 384, 400); }});
     // > 8192 changed groups per epoch: flush() packs and delivers on several threads
     tests.push_back({"testConcurrentCallersWide", [&] { testConcurrentCallers(e, 20000, 48); }});
+    // the same with the record chunks streamed every 37 records (jrq_table_ack_push from the
+    // calling threads while others call, flush and push tails)
+    tests.push_back({"testConcurrentCallersStreamed", [&] {
+                       testing::ackChunkRecords.store(37);
+                       try {
+                         testConcurrentCallers(e, 2000, 120);
+                       } catch (...) {
+                         testing::ackChunkRecords.store(GroupBatch::kAckChunk);
+                         throw;
+                       }
+                       testing::ackChunkRecords.store(GroupBatch::kAckChunk);
+                     }});
     tests.push_back({"testReentrantFlushRefused", [&] { testReentrantFlushRefused(e); }});
     tests.push_back({"testFlushFailureRelists", [&] { testFlushFailureRelists(e); }});
     tests.push_back({"testThrowingCallback", [&] { testThrowingCallback(e); }});

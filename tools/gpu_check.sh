@@ -45,8 +45,9 @@ for s in $STEPS; do
            i=0; for v in ${AB_LIBS:-base}; do i=$((i+1))
              run drive_${i}_$v 300 env JRAFT_AMD_AB_DRIVE=ab/$v/libjraft_drive.so python bench.py --steps 5 --warmup 2 --no-cpu --legs drive --detail gpurun_out/drive_${i}_${v}_detail.json
            done ;;
-    hab)   # host-mirror builds round-robin in one process (tools/drive_ab.py), medians per variant
-           run hab_${TAG:-sel} 600 python tools/drive_ab.py $(for v in ${AB_LIBS:-hA}; do echo $v=ab/$v/libjraft_drive.so; done) --flush-threads "${FLUSH_THREADS:-}" --rounds ${ROUNDS:-5} --epochs ${EPOCHS:-10} --threads ${THREADS:-16} --active ${ACTIVE:-1.0} ;;
+    hab)   # host-mirror builds round-robin, one process per run (tools/drive_ab.py), medians per
+           # variant; AB_SPECS: the variant list itself (NAME=path[:VAR=VALUE] ...)
+           run hab_${TAG:-sel} 900 python tools/drive_ab.py ${AB_SPECS:-$(for v in ${AB_LIBS:-hA}; do echo $v=ab/$v/libjraft_drive.so; done)} --flush-threads "${FLUSH_THREADS:-}" --rounds ${ROUNDS:-5} --epochs ${EPOCHS:-10} --threads ${THREADS:-16} --active ${ACTIVE:-1.0} ;;
     ab)    run ab_${TAG:-sel} 600 env AB_LEGS=${AB_LEGS:-C3,C5f,C1f,archive} python tools/ab_inproc.py ${AB_VARIANTS:-base=ab/base/libjrq.so} ;;
     tpab)  # the resident table epoch, every group committing, libjrq variants side by side
            for P in ${TP_PEERS:-5}; do
