@@ -1,6 +1,6 @@
 """tools/leg_traces.py on a synthetic whole-run trace: timed series are matched to their legs by
 the run's `timed_series_legs`, and each leg's fraction is recomputed from its own launches only
-(two legs here share a kernel name, as C5 and C1 do)."""
+(two legs here run the same kernel template, as C5 and C1 do)."""
 import csv
 import json
 import os
@@ -20,7 +20,8 @@ def _write_trace(d, rows):
 
 
 def test_whole_run_trace_split_by_labels(tmp_path):
-    fixed = "void jrq::crc64_fixed_kernel<true, false>(JrqCrcArgs)"
+    fixed = "void jrq::crc64_fixed_kernel<true, false, 512>(JrqCrcArgs)"
+    wide = "void jrq::crc64_fixed_kernel<true, false, 1024>(JrqCrcArgs)"
     rows, t = [], 0
 
     def series(name, dur_ns, n):
@@ -35,7 +36,7 @@ def test_whole_run_trace_split_by_labels(tmp_path):
 
     series(fixed, 175_000, 4)   # C5: 1 GB per launch
     series("other_kernel", 10_000, 3)  # an unlabelled leg's series
-    series(fixed, 60_000, 4)    # C1: same kernel name, 0.3 GB per launch
+    series(wide, 60_000, 4)     # C1: the same kernel's one-lane-per-entry form, 0.3 GB per launch
     trace = tmp_path / "full"
     _write_trace(str(trace), rows)
     detail = {"timed_series_legs": ["C5", "drive", "C1"],
