@@ -816,7 +816,8 @@ def leg_drive(ctx, args, G):
     mirror's BallotBox API (appendPendingTask / commitAt) over the resident table, one
     GroupBatch::flush() per epoch (libjraft_drive.so): changed records from page-locked
     buffers -> H2D -> apply + epoch kernels -> D2H of the changed commits -> closures /
-    onCommitted.  Reported per steady epoch (epochs 1..K-1; epoch 0 loads every group), with
+    onCommitted.  Reported per steady epoch (epochs 3..K-1: epoch 0 loads every group, epochs 1-2
+    size the calling threads' record buffers and their device regions), with
     the epoch's API calls made by 1 and by 16 threads (contiguous group slices), and the
     end-to-end rate including those calls.  Then the ack -> onCommitted latency under the
     background flusher's policy, with 16 producer threads."""
@@ -824,7 +825,7 @@ def leg_drive(ctx, args, G):
 
     from jraft_amd import drive
     from jraft_amd import workloads as W
-    K = 6
+    K = 10
     out = {}
     for active, threads, shards in ((1.0, 1, 1), (1.0, 16, 1), (0.1, 16, 1), (1.0, 16, 2)):
         s = W.host_series("C3", K, groups=G, joint_frac=0.01, active=active)
@@ -842,7 +843,7 @@ def leg_drive(ctx, args, G):
             ctx.sync()
             ok = bool(np.array_equal(committed, host_np(c)))
             del d, c, cs
-        sl = slice(1, K)
+        sl = slice(3, K)
         f = float(np.mean(st["flush_ms"][sl]))
         api = float(np.mean(st["api_ms"][sl]))
         pcie = float(np.mean(st["h2d_bytes"][sl] + st["d2h_bytes"][sl]))
@@ -864,6 +865,7 @@ def leg_drive(ctx, args, G):
             "changed_per_epoch": float(np.mean(st["changed"][sl])),
             "pcie_bytes_per_epoch": pcie, "pcie_GBps": pcie / (f * 1e-3) / 1e9,
             "first_epoch_flush_ms": float(st["flush_ms"][0]),
+            "sizing_epochs_flush_ms": [float(x) for x in st["flush_ms"][1:3]],
             "bit_exact_vs_stateless_kernel": ok}
     lats = {}
     # (1M groups at one entry per group per second -- 1M entries/s, 5M acks/s -- and at ten:
