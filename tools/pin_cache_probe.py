@@ -182,6 +182,59 @@ def main():
     hp = C.c_void_p()
     rh = hip.hipHostMalloc(C.byref(hp), 1 << 20, 0)
     out["host_malloc_instrument_check"] = {"rc": rh, "hsa": hsa_info(hp.value), "hip": hip_info(hp.value)}
+    # (g) r06 follow-up: sizes at and above ROCclr's pinned-transfer threshold (GPU_PINNED_MIN_XFER_SIZE,
+    # 128 MiB by default as far as we know -- cases (a)-(f) all stayed below it, so they never
+    # exercised the pin-in-place path the r05 bench's GiB-sized pageable uploads took).  Per size:
+    # a host->device copy from a fresh mapping with a second thread polling the source's record
+    # during the copy, the record after the copy, after munmap, and over a new mapping at the
+    # same address (observed only, never copied into); then the same for a device->host copy.
+    big_src = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    big_src[:4096] = torch.from_numpy(expect).to(dev)
+    torch.cuda.synchronize()
+    out["pinned_threshold_cases"] = []
+
+    def observe(addr, size, run):
+        seen_h, seen_p, stop2 = [], [], [False]
+
+        def poll2():
+            while not stop2[0]:
+                hi = hsa_info(addr + size // 2)
+                if hi["type"] and hi["type"] not in seen_h:
+                    seen_h.append(hi["type"])
+                hp_ = hip_info(addr + size // 2)
+                if hp_["type"] and hp_["type"] not in seen_p:
+                    seen_p.append(hp_["type"])
+        th2 = threading.Thread(target=poll2)
+        th2.start()
+        run()
+        torch.cuda.synchronize()
+        stop2[0] = True
+        th2.join()
+        return {"hsa_types_seen_during": seen_h, "hip_types_seen_during": seen_p}
+
+    for size in (128 << 20, 256 << 20, 1 << 30):
+        for direction in ("h2d", "d2h"):
+            pa, a = new_map(size)
+            if direction == "h2d":
+                a[:4096] = expect
+                dd2 = torch.empty(size, dtype=torch.uint8, device=dev)
+                during = observe(pa, size, lambda: dd2.copy_(torch.from_numpy(a)))
+                ok = bool(np.array_equal(dd2[:4096].cpu().numpy(), expect))
+                del dd2
+            else:
+                during = observe(pa, size, lambda: torch.from_numpy(a).copy_(big_src[:size]))
+                ok = bool(np.array_equal(a[:4096], expect))
+            rec = {"bytes": size, "direction": direction, "copy_ok": ok, "during": during,
+                   "after_copy": {"hsa": hsa_info(pa), "hsa_mid": hsa_info(pa + size // 2), "hip": hip_info(pa),
+                                  "hip_mid": hip_info(pa + size // 2)}}
+            del a
+            libc.munmap(C.c_void_p(pa), size)
+            rec["after_munmap"] = {"hsa": hsa_info(pa), "hip": hip_info(pa), "hip_mid": hip_info(pa + size // 2)}
+            pb, b = new_map(size, at=pa)
+            keep.append((pb, b))
+            rec["new_mapping_same_address"] = {"same_address": pb == pa, "hsa": hsa_info(pb),
+                                               "hip": hip_info(pb), "hip_mid": hip_info(pb + size // 2)}
+            out["pinned_threshold_cases"].append(rec)
     print(json.dumps(out, indent=1))
     sys.stdout.flush()
     os._exit(0)  # leave the mappings to the kernel; no runtime teardown over the replaced ranges
