@@ -1179,18 +1179,29 @@ uint32_t GroupBatch::flushLocked() {
   // group in order.  A callback that throws cannot leave a group half-applied: the host state
   // then stays what the device table already holds (its pendingIndex follows lastCommitted),
   // and the first exception is rethrown after every callback ran.  A commit touches one group
-  // record at a random place: prefetch a few groups ahead.
+  // record at a random place: prefetch a few groups ahead.  The workers claim the list in
+  // kDeliverChunks chunks each, in order, rather than one fixed range each: a worker the OS
+  // deschedules then holds up one chunk, not a sixteenth of the flush (r06 A/B, one process
+  // per run: deliver 1.93 -> 1.58 ms median at 16 API threads).  A worker's
+  // groups still come in list order, so its callbacks run group by group in order.
   const size_t dparts = partsFor(n, 1u << 12);
   if (deliveries_.size() < dparts) deliveries_.resize(dparts);
   std::vector<std::exception_ptr> errs(dparts);
   std::vector<double> apply_ms(dparts, 0.0), cb_ms(dparts, 0.0);
-  parallelFor(n, 1u << 12, [&](unsigned part, size_t i0, size_t i1) {
+  constexpr size_t kDeliverChunks = 4;
+  const size_t chunk = (n + dparts * kDeliverChunks - 1) / (dparts * kDeliverChunks);
+  std::atomic<size_t> nextChunk{0};
+  auto deliverPart = [&](unsigned part) {
     const auto d0 = clk::now();
     Delivery& D = deliveries_[part];
     D.commits.clear();
     D.done.clear();
     D.ndone.clear();
     constexpr size_t kAhead = JRAFT_DELIVER_AHEAD;
+    for (;;) {
+    const size_t i0 = nextChunk.fetch_add(1, std::memory_order_relaxed) * chunk;
+    if (i0 >= n) break;
+    const size_t i1 = std::min<size_t>(n, i0 + chunk);
     for (size_t i = i0; i < i1; ++i) {
       if (i + kAhead < i1) {
         const uint32_t a = static_cast<uint32_t>(changed_.p[i + kAhead]);
@@ -1217,6 +1228,7 @@ uint32_t GroupBatch::flushLocked() {
       D.commits.push_back(Delivery::Commit{c, &waiter_[g]});
       D.ndone.push_back(nd0);
     }
+    }
     const auto d1 = clk::now();
     struct Scope {
       const GroupBatch* prev;
@@ -1242,7 +1254,14 @@ uint32_t GroupBatch::flushLocked() {
     D.done.clear();
     apply_ms[part] = std::chrono::duration<double, std::milli>(d1 - d0).count();
     cb_ms[part] = std::chrono::duration<double, std::milli>(clk::now() - d1).count();
-  });
+  };
+  if (dparts == 1) {
+    deliverPart(0u);
+  } else {
+    pool_->run([&](unsigned i, unsigned) {
+      if (i < dparts) deliverPart(i);
+    });
+  }
   flushes_.fetch_add(1, std::memory_order_relaxed);
   const auto t3 = clk::now();
   auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
